@@ -1,0 +1,196 @@
+"""Packed op-log format (include/mt_oplog.h) and builders.
+
+A *document log* is one replica's arrival-ordered event stream: sequenced messages
+(``Client.applyMsg``, reference ``packages/dds/merge-tree/src/client.ts:797-819``) interleaved
+with the replica's own local edits (``insertSegmentLocal`` / ``removeRangeLocal`` /
+``annotateRangeLocal``, client.ts:202/189/164). A *batch* is many document logs concatenated
+with per-document offsets; it is what the HIP replay engine (``libmtreplay.so``) consumes.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+
+OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 4
+OPF_LOCAL = 0x80
+SEG_TEXT, SEG_MARKER = 0, 1
+COMBINE_NONE, COMBINE_REWRITE = 0, 1
+VALUE_FALSY = 0x8000
+
+OP_DTYPE = np.dtype(
+    [
+        ("kind", "u1"),
+        ("seg_kind", "u1"),
+        ("client", "<u2"),
+        ("seq", "<i4"),
+        ("ref_seq", "<i4"),
+        ("min_seq", "<i4"),
+        ("pos1", "<i4"),
+        ("pos2", "<i4"),
+        ("text_off", "<u4"),
+        ("text_len", "<u2"),
+        ("props", "<u2"),
+    ]
+)
+assert OP_DTYPE.itemsize == 32
+PROPS_DTYPE = np.dtype([("kv_off", "<u4"), ("nkv", "<u2"), ("combining", "u1"), ("_pad", "u1")])
+KV_DTYPE = np.dtype([("key", "<u2"), ("value", "<u2")])
+
+
+def canonical_json(v: Any) -> str:
+    """Canonical JSON of a property value: structural equality == string equality, which is
+    what ``matchProperties`` (properties.ts:61-92) tests for JSON-shaped values."""
+    return json.dumps(v, sort_keys=True, separators=(",", ":"), ensure_ascii=False)
+
+
+def _falsy(v: Any) -> bool:
+    return v is not None and not v and not isinstance(v, (dict, list))
+
+
+class Interner:
+    """Batch-global key / value string tables. Value id 0 is JSON null (= delete)."""
+
+    def __init__(self) -> None:
+        self.keys: List[str] = [""]
+        self.key_ids: Dict[str, int] = {}
+        self.values: List[str] = ["null"]
+        self.value_ids: Dict[str, int] = {}
+
+    def key(self, k: str) -> int:
+        i = self.key_ids.get(k)
+        if i is None:
+            i = len(self.keys)
+            if i >= 0xFFFF:
+                raise ValueError("too many distinct property keys")
+            self.keys.append(k)
+            self.key_ids[k] = i
+        return i
+
+    def value(self, v: Any) -> int:
+        if v is None:
+            return 0
+        s = canonical_json(v)
+        i = self.value_ids.get(s)
+        if i is None:
+            i = len(self.values)
+            if i >= VALUE_FALSY:
+                raise ValueError("too many distinct property values")
+            self.values.append(s)
+            self.value_ids[s] = i
+        return i | (VALUE_FALSY if _falsy(v) else 0)
+
+    def key_str(self, i: int) -> str:
+        return self.keys[i]
+
+    def value_obj(self, i: int) -> Any:
+        return json.loads(self.values[i & ~VALUE_FALSY])
+
+
+@dataclass
+class DocLog:
+    """One replica's event stream plus its text / props pools."""
+
+    interner: Interner
+    local_long_id: int = 0
+    ops: List[tuple] = field(default_factory=list)
+    text: List[int] = field(default_factory=list)
+    props: List[tuple] = field(default_factory=list)
+    kv: List[tuple] = field(default_factory=list)
+
+    def _props(self, props: Optional[Dict[str, Any]], combining: int = COMBINE_NONE) -> int:
+        if props is None:
+            return 0
+        off = len(self.kv)
+        for k, v in props.items():
+            self.kv.append((self.interner.key(k), self.interner.value(v)))
+        self.props.append((off, len(props), combining, 0))
+        return len(self.props)
+
+    def _text(self, text: str) -> tuple:
+        units = text.encode("utf-16-le")
+        arr = np.frombuffer(units, dtype="<u2")
+        off = len(self.text)
+        self.text.extend(arr.tolist())
+        return off, len(arr)
+
+    def add(self, kind: int, *, client: int = 0, seq: int = 0, ref_seq: int = 0, min_seq: int = 0,
+            pos1: int = 0, pos2: int = 0, text: Optional[str] = None, marker: Optional[int] = None,
+            props: Optional[Dict[str, Any]] = None, combining: int = COMBINE_NONE) -> None:
+        seg_kind = SEG_TEXT
+        toff = tlen = 0
+        if kind & 7 == OP_INSERT:
+            if marker is not None:
+                seg_kind = SEG_MARKER
+                pos2 = marker
+            else:
+                toff, tlen = self._text(text or "")
+        pidx = self._props(props, combining)
+        self.ops.append((kind, seg_kind, client, seq, ref_seq, min_seq, pos1, pos2, toff, tlen, pidx))
+
+    def arrays(self):
+        ops = np.array(self.ops, dtype=OP_DTYPE) if self.ops else np.zeros(0, OP_DTYPE)
+        text = np.array(self.text, dtype="<u2") if self.text else np.zeros(1, "<u2")
+        props = np.array(self.props, dtype=PROPS_DTYPE) if self.props else np.zeros(1, PROPS_DTYPE)
+        kv = np.array(self.kv, dtype=KV_DTYPE) if self.kv else np.zeros(1, KV_DTYPE)
+        return ops, text, props, kv
+
+
+@dataclass
+class Batch:
+    """Many document logs, concatenated; offsets are per-document (length ndocs+1)."""
+
+    ops: np.ndarray
+    op_off: np.ndarray
+    text: np.ndarray
+    text_off: np.ndarray
+    props: np.ndarray
+    props_off: np.ndarray
+    kv: np.ndarray
+    kv_off: np.ndarray
+    local_long_id: np.ndarray
+
+    @property
+    def ndocs(self) -> int:
+        return len(self.op_off) - 1
+
+    @property
+    def nops(self) -> int:
+        return int(self.op_off[-1])
+
+    def doc(self, d: int):
+        return (
+            self.ops[self.op_off[d]: self.op_off[d + 1]],
+            self.text[self.text_off[d]: max(self.text_off[d + 1], self.text_off[d] + 1)],
+            self.props[self.props_off[d]: max(self.props_off[d + 1], self.props_off[d] + 1)],
+            self.kv[self.kv_off[d]: max(self.kv_off[d + 1], self.kv_off[d] + 1)],
+        )
+
+    def subset(self, docs: Sequence[int]) -> "Batch":
+        return Batch.from_arrays([self.doc(d) for d in docs], [int(self.local_long_id[d]) for d in docs])
+
+    @staticmethod
+    def from_arrays(per_doc, local_ids) -> "Batch":
+        def cat(idx, dt):
+            parts = [p[idx] for p in per_doc]
+            off = np.zeros(len(parts) + 1, np.int64)
+            off[1:] = np.cumsum([len(x) for x in parts])
+            arr = np.concatenate(parts) if parts else np.zeros(0, dt)
+            if len(arr) == 0:
+                arr = np.zeros(1, dt)
+            return np.ascontiguousarray(arr), off
+
+        ops, op_off = cat(0, OP_DTYPE)
+        if op_off[-1] == 0:
+            ops = np.zeros(0, OP_DTYPE)
+        text, text_off = cat(1, np.dtype("<u2"))
+        props, props_off = cat(2, PROPS_DTYPE)
+        kv, kv_off = cat(3, KV_DTYPE)
+        return Batch(ops, op_off, text, text_off, props, props_off, kv, kv_off,
+                     np.asarray(local_ids, np.int32))
+
+    @staticmethod
+    def from_logs(logs: Sequence[DocLog]) -> "Batch":
+        return Batch.from_arrays([lg.arrays() for lg in logs], [lg.local_long_id for lg in logs])

@@ -1,0 +1,112 @@
+/*
+ * mt_oplog.h — packed op-log and canonical-dump formats shared by the HIP replay
+ * engine (libmtreplay.so), the host facades and the test oracle.
+ *
+ * One record = one event in ONE replica's arrival-ordered stream, i.e. exactly what
+ * the reference `Client` sees:
+ *   - a sequenced message  -> Client.applyMsg      (packages/dds/merge-tree/src/client.ts:797-819)
+ *       * from another client      -> applyRemoteOp  (client.ts:768-795)
+ *       * from this replica itself -> ackPendingSegment (client.ts:589-626, mergeTree.ts:1926-1953)
+ *       * a non-op message (NOOP)  -> only updateSeqNumbers (client.ts:818-828)
+ *   - a local edit (MT_OPF_LOCAL) -> insertSegmentLocal / removeRangeLocal / annotateRangeLocal
+ *                                    (client.ts:202, 189, 164)
+ *
+ * Wire-level mapping (reference ops.ts:29-102, protocol.ts:132-172):
+ *   kind       <- IMergeTreeOp.type (INSERT=0, REMOVE=1, ANNOTATE=2), NOOP = non-op message
+ *   client     <- msg.clientId, as an index into the document's long-client-id table
+ *   seq/ref/min<- sequenceNumber / referenceSequenceNumber / minimumSequenceNumber
+ *   pos1/pos2  <- op.pos1 / op.pos2           (positions in UTF-16 code units)
+ *   text       <- op.seg (string or {text, props}) as UTF-16 code units in the doc text pool
+ *   props      <- op.props / op.seg.props     (1-based index into the doc props table)
+ *
+ * All integers little-endian; records are 32 bytes, naturally aligned.
+ */
+#ifndef MT_OPLOG_H
+#define MT_OPLOG_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* op kinds (low 3 bits of mt_op_rec.kind); values follow MergeTreeDeltaType (ops.ts:29-34) */
+enum {
+    MT_OP_INSERT = 0,
+    MT_OP_REMOVE = 1,
+    MT_OP_ANNOTATE = 2,
+    MT_OP_NOOP = 4, /* sequenced message that is not a merge-tree op: advances currentSeq/MSN only */
+};
+#define MT_OP_KIND_MASK 0x07
+#define MT_OPF_LOCAL 0x80 /* unsequenced local edit made by this replica */
+
+/* segment kinds */
+enum {
+    MT_SEG_TEXT = 0,   /* TextSegment   (textSegment.ts:16-112)            */
+    MT_SEG_MARKER = 1, /* Marker, length 1 (mergeTree.ts:668-832)          */
+};
+
+/* combining ops for annotate (ops.ts ICombiningOp); only none and "rewrite" are supported */
+enum {
+    MT_COMBINE_NONE = 0,
+    MT_COMBINE_REWRITE = 1,
+};
+
+typedef struct mt_op_rec {
+    uint8_t kind;      /* MT_OP_* | MT_OPF_LOCAL                                          */
+    uint8_t seg_kind;  /* insert: MT_SEG_*                                                  */
+    uint16_t client;   /* long-client index (doc-local); ignored for local edits            */
+    int32_t seq;       /* sequence number; ignored for local edits                           */
+    int32_t ref_seq;   /* reference sequence number; ignored for local edits                 */
+    int32_t min_seq;   /* minimum sequence number carried by the message                     */
+    int32_t pos1;      /* insert position / range start                                      */
+    int32_t pos2;      /* range end (exclusive); insert of a marker: its refType             */
+    uint32_t text_off; /* insert text: offset in UTF-16 units into the doc text pool         */
+    uint16_t text_len; /* insert text: length in UTF-16 units                                */
+    uint16_t props;    /* 0 = none, else 1-based index into the doc props table              */
+} mt_op_rec;
+
+/* One property set carried by an op: nkv (key,value) pairs starting at kv_off in the doc kv
+ * pool. value 0 == JSON null (delete the key, segmentPropertiesManager.ts:102-106).
+ * Key and value ids index the batch-global string tables (value strings are canonical JSON). */
+typedef struct mt_props_rec {
+    uint32_t kv_off;
+    uint16_t nkv;
+    uint8_t combining; /* MT_COMBINE_* */
+    uint8_t _pad;
+} mt_props_rec;
+
+/* value ids carrying this bit are falsy JSON values (0, "", false); relevant to `rewrite`
+ * (segmentPropertiesManager.ts:72: `!newProps[key]`) */
+#define MT_VALUE_FALSY 0x8000
+
+typedef struct mt_kv {
+    uint16_t key;
+    uint16_t value;
+} mt_kv;
+
+/* ---- canonical segment dump (binary) ------------------------------------------------------
+ * Header, then one variable-length record per segment in walkAllSegments order
+ * (mergeTree.ts:3002-3016). The per-document digest is FNV-1a-64 over these bytes.
+ *
+ * header: int32 currentSeq, minSeq, localSeq, localLength, nsegs, nleaf
+ * record: uint8 kind; uint8 flags; uint8 noverlap; uint8 ngroups;
+ *         int32 len, seq, client, removedSeq, removedClient, localSeq, localRemovedSeq, leaf;
+ *         int32 overlap[noverlap];
+ *         uint16 nprops; uint16 refType; (key,value) x nprops sorted by key id;
+ *         text: len x uint16 (text segments only)
+ * client fields are LONG client indices; -1 = the reference's "original" (LocalClientId).
+ */
+enum {
+    MT_DF_HAS_PROPS = 1,
+    MT_DF_REMOVED = 2,
+    MT_DF_LSEQ = 4,
+    MT_DF_LRSEQ = 8,
+};
+
+#define MT_FNV_OFFSET 0xcbf29ce484222325ULL
+#define MT_FNV_PRIME 0x100000001b3ULL
+
+#ifdef __cplusplus
+}
+#endif
+#endif
