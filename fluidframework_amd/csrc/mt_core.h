@@ -1,0 +1,1336 @@
+/*
+ * mt_core.h — the merge-tree replay core, single source for the HIP kernel (one wavefront per
+ * document) and for the host build that the generator and the CPU spec tests use.
+ *
+ * Representation ("leaf slabs"). The reference keeps a B-tree of MergeBlocks with at most
+ * MaxNodesInBlock-1 = 7 children (mergeTree.ts:329-382). Segment boundaries depend on the exact
+ * leaf-block partition (zamboni merges only inside a leaf, mergeTree.ts:1322-1398; inserts tie
+ * at leaf ends, 2464-2478), so the block skeleton is kept, but flattened for a wavefront:
+ *   - every block is a node; a LEAF node owns a slab of 8 row slots (7 children + the transient
+ *     8th the reference uses before splitting, mergeTree.ts:2487-2503);
+ *   - rows are stored structure-of-arrays by slot (slot = node * 8 + child index);
+ *   - `lorder` lists leaf nodes in document order, so document order = (lorder[k], j);
+ *   - interior nodes keep parent / child lists only for split propagation and pack.
+ * Position resolution replaces the root-to-leaf walk with a wavefront prefix scan of
+ * perspective-visible lengths over all slots in document order (nodeLength, 1692-1732); the
+ * PartialSequenceLengths summaries are not needed because the scan sums leaves directly.
+ *
+ * Wave abstraction: W::N lanes execute every function; control flow and all "scalar" values are
+ * uniform across lanes. Cross-lane work goes through W (exclusive scan, ballot, broadcast). The
+ * host build uses W::N = 1 so the same code runs serially.
+ */
+#pragma once
+#include <stdint.h>
+
+#include "../../include/mt_oplog.h"
+
+#ifdef __HIPCC__
+#define MT_HD __host__ __device__
+#define MT_DEV __device__
+#else
+#define MT_HD
+#define MT_DEV
+#endif
+
+namespace mt {
+
+enum : int32_t {
+    UNIVERSAL_SEQ = 0,
+    UNASSIGNED_SEQ = -1,
+    NOREM = INT32_MIN, /* rseq when not removed */
+    NONE = INT32_MIN,
+    MAXN = 8,          /* MaxNodesInBlock (mergeTree.ts:333) */
+    GRANULARITY = 256, /* TextSegmentGranularity (mergeTree.ts:1093) */
+    NKEYS = 8,         /* property key slots per document */
+    NGRP = 4,          /* segment-group FIFO depth per row */
+    NOVL = 8,          /* removedClientOverlap entries per row */
+};
+enum : uint8_t { LOCAL_CLIENT = 0xFF }; /* short id of LocalClientId (-1) */
+
+/* error codes (mt_engine.h MT_E_*) */
+enum : int32_t {
+    E_OK = 0,
+    E_INSERT_FAILED = 1, /* mergeTree.ts:2243-2249 */
+    E_ASSERT = 2,
+    E_INVALID_RANGE = 3, /* client.ts:486-548 (local op rejected) */
+    E_UNSUPPORTED = 4,
+    E_CAPACITY = 5,
+};
+
+/* row flag bits */
+enum : uint8_t {
+    RF_MARKER = 1,
+    RF_PROPS = 2, /* properties !== undefined (and propertyManager exists) */
+    RF_LSEQ = 4,
+    RF_LRSEQ = 8,
+};
+
+struct Caps {
+    int32_t ncap; /* nodes per doc (slots = ncap * 8) */
+    int32_t hcap; /* zamboni heap entries */
+    int32_t acap; /* text arena half-size (UTF-16 units); arena holds 2 halves */
+    int32_t mcap; /* segment-group membership log entries */
+    int32_t gcap; /* pending segment groups (local ops in flight) */
+    int32_t ccap; /* clients per doc */
+};
+
+/* per-document scalar header */
+struct DocHdr {
+    int32_t root, nleaf, freeHead, nfree;
+    int32_t currentSeq, minSeq, localSeq, collaborating;
+    int32_t localShort, localLong, nclients, nextSid;
+    int32_t heapN, memN, gqHead, gqN;
+    int32_t arenaTop, arenaSide, err, errOp;
+    int32_t nkeys, opsDone, hwSlots, hwHeap;
+    uint16_t keys[NKEYS];
+};
+
+/* batch-wide column base pointers (per-doc stride = capacity) */
+struct Cols {
+    /* rows: ncap*8 per doc */
+    int32_t *len, *seq, *rseq, *lseq, *lrseq;
+    uint32_t *sid, *toff;
+    uint8_t *cli, *rcli, *flags, *ng, *prw;
+    uint64_t* ovl;
+    uint16_t* pv; /* NKEYS per row */
+    uint8_t* pk;  /* NKEYS per row: pendingKeyUpdateCount */
+    int32_t* grp; /* NGRP per row: segmentGroups FIFO (group ids) */
+    /* nodes: ncap per doc */
+    int16_t *nparent, *kids, *lorder, *lpos;
+    int8_t *nchild, *nlevel, *nscour;
+    /* heap: hcap per doc */
+    uint32_t* hsid;
+    int32_t* hseq;
+    /* membership log: mcap per doc */
+    int32_t* mgid;
+    uint32_t* msid;
+    /* pending group FIFO: gcap per doc (ring) */
+    int32_t* gq;
+    /* text arena: 2*acap per doc */
+    uint16_t* arena;
+    /* clients: ccap per doc, short -> long */
+    uint16_t* s2l;
+    DocHdr* hdr;
+};
+
+/* A view of one document: column pointers already offset to this doc. */
+struct Doc {
+    int32_t *len, *seq, *rseq, *lseq, *lrseq;
+    uint32_t *sid, *toff;
+    uint8_t *cli, *rcli, *flags, *ng, *prw;
+    uint64_t* ovl;
+    uint16_t* pv;
+    uint8_t* pk;
+    int32_t* grp;
+    int16_t *nparent, *kids, *lorder, *lpos;
+    int8_t *nchild, *nlevel, *nscour;
+    uint32_t* hsid;
+    int32_t* hseq;
+    int32_t* mgid;
+    uint32_t* msid;
+    int32_t* gq;
+    uint16_t* arena;
+    uint16_t* s2l;
+    DocHdr* h;
+    Caps caps;
+};
+
+MT_HD inline Doc doc_view(const Cols& c, const Caps& k, int64_t d) {
+    Doc v;
+    int64_t rs = (int64_t)k.ncap * MAXN, ns = k.ncap;
+    v.len = c.len + d * rs;
+    v.seq = c.seq + d * rs;
+    v.rseq = c.rseq + d * rs;
+    v.lseq = c.lseq + d * rs;
+    v.lrseq = c.lrseq + d * rs;
+    v.sid = c.sid + d * rs;
+    v.toff = c.toff + d * rs;
+    v.cli = c.cli + d * rs;
+    v.rcli = c.rcli + d * rs;
+    v.flags = c.flags + d * rs;
+    v.ng = c.ng + d * rs;
+    v.prw = c.prw + d * rs;
+    v.ovl = c.ovl + d * rs;
+    v.pv = c.pv + d * rs * NKEYS;
+    v.pk = c.pk + d * rs * NKEYS;
+    v.grp = c.grp + d * rs * NGRP;
+    v.nparent = c.nparent + d * ns;
+    v.kids = c.kids + d * ns * MAXN;
+    v.lorder = c.lorder + d * ns;
+    v.lpos = c.lpos + d * ns;
+    v.nchild = c.nchild + d * ns;
+    v.nlevel = c.nlevel + d * ns;
+    v.nscour = c.nscour + d * ns;
+    v.hsid = c.hsid + d * k.hcap;
+    v.hseq = c.hseq + d * k.hcap;
+    v.mgid = c.mgid + d * k.mcap;
+    v.msid = c.msid + d * k.mcap;
+    v.gq = c.gq + d * k.gcap;
+    v.arena = c.arena + d * (int64_t)k.acap * 2;
+    v.s2l = c.s2l + d * k.ccap;
+    v.h = c.hdr + d;
+    v.caps = k;
+    return v;
+}
+
+/* Op pools of one document. */
+struct Pools {
+    const mt_op_rec* ops;
+    int64_t nops;
+    const uint16_t* text;
+    const mt_props_rec* props;
+    const mt_kv* kv;
+};
+
+/* ------------------------------------------------------------------------------------------
+ * Replica: all operations of one document replica, executed by one wave.
+ * ---------------------------------------------------------------------------------------- */
+template <class W>
+struct Replica {
+    Doc d;
+    W w;
+
+    MT_HD Replica(const Doc& doc, const W& wave) : d(doc), w(wave) {}
+
+    MT_HD void fail(int32_t e) {
+        if (d.h->err == E_OK) {
+            d.h->err = e;
+            d.h->errOp = d.h->opsDone;
+        }
+    }
+
+    /* ---- node allocation ------------------------------------------------------------- */
+    MT_HD int32_t alloc_node(int8_t level) {
+        int32_t n = d.h->freeHead;
+        if (n < 0) {
+            fail(E_CAPACITY);
+            return -1;
+        }
+        d.h->freeHead = d.nparent[n];
+        d.h->nfree--;
+        d.nparent[n] = -1;
+        d.nchild[n] = 0;
+        d.nlevel[n] = level;
+        d.nscour[n] = -1; /* needsScour undefined */
+        return n;
+    }
+    MT_HD void free_node(int32_t n) {
+        d.nparent[n] = (int16_t)d.h->freeHead;
+        d.nchild[n] = 0;
+        d.h->freeHead = n;
+        d.h->nfree++;
+    }
+
+    /* ---- init -------------------------------------------------------------------------- */
+    MT_HD void init() {
+        /* node 0 = empty root leaf (initialNode, mergeTree.ts:1159-1163) */
+        int32_t ncap = d.caps.ncap;
+        for (int32_t b = 0; b < ncap; b += W::N) {
+            int32_t n = b + w.lane();
+            if (n < ncap) {
+                d.nparent[n] = (int16_t)(n + 1 < ncap ? n + 1 : -1);
+                d.nchild[n] = 0;
+                d.nlevel[n] = 0;
+                d.nscour[n] = -1;
+            }
+        }
+        w.sync();
+        DocHdr* h = d.h;
+        h->freeHead = 1;
+        h->nfree = ncap - 1;
+        h->root = 0;
+        d.nparent[0] = -1;
+        d.lorder[0] = 0;
+        d.lpos[0] = 0;
+        h->nleaf = 1;
+        h->currentSeq = 0;
+        h->minSeq = 0;
+        h->localSeq = 0;
+        h->collaborating = 0;
+        h->localShort = -1; /* collabWindow.clientId = LocalClientId */
+        h->localLong = -1;
+        h->nclients = 0;
+        h->nextSid = 1;
+        h->heapN = 0;
+        h->memN = 0;
+        h->gqHead = 0;
+        h->gqN = 0;
+        h->arenaTop = 0;
+        h->arenaSide = 0;
+        h->err = 0;
+        h->errOp = -1;
+        h->nkeys = 0;
+        h->opsDone = 0;
+        h->hwSlots = 0;
+        h->hwHeap = 0;
+        w.sync();
+    }
+
+    /* ---- clients (client.ts:637-661) --------------------------------------------------- */
+    MT_HD int32_t short_of(int32_t longId) {
+        for (int32_t i = 0; i < d.h->nclients; i++)
+            if (d.s2l[i] == longId) return i;
+        return -1;
+    }
+    MT_HD int32_t get_or_add_short(int32_t longId) {
+        int32_t s = short_of(longId);
+        if (s >= 0) return s;
+        int32_t n = d.h->nclients;
+        if (n >= d.caps.ccap || n >= 0xFE) {
+            fail(E_CAPACITY);
+            return 0;
+        }
+        d.s2l[n] = (uint16_t)longId;
+        d.h->nclients = n + 1;
+        return n;
+    }
+    /* startOrUpdateCollaboration (client.ts:1053-1073) + startCollaboration (mergeTree.ts:1287) */
+    MT_HD void start_collab(int32_t longId, int32_t minSeq, int32_t curSeq) {
+        if (d.h->localLong >= 0) return;
+        d.h->localLong = longId;
+        d.h->localShort = get_or_add_short(longId);
+        d.h->minSeq = minSeq;
+        d.h->currentSeq = curSeq;
+        d.h->collaborating = 1;
+    }
+
+    /* ---- row helpers ------------------------------------------------------------------- */
+    MT_HD static bool removed(const Doc& d, int32_t s) { return d.rseq[s] != NOREM; }
+    MT_HD bool is_local(int32_t client) const {
+        return !d.h->collaborating || client == d.h->localShort;
+    }
+    /* nodeLength of a leaf (mergeTree.ts:1692-1732); local perspective -> localNetLength */
+    MT_HD int32_t vis(int32_t s, int32_t refSeq, int32_t client) const {
+        int32_t L = d.len[s];
+        if (is_local(client)) return d.rseq[s] == NOREM ? L : 0;
+        int32_t c = d.cli[s] == LOCAL_CLIENT ? -1 : d.cli[s];
+        int32_t sq = d.seq[s];
+        if (!(c == client || (sq != UNASSIGNED_SEQ && sq <= refSeq))) return 0;
+        int32_t rs = d.rseq[s];
+        if (rs != NOREM) {
+            int32_t rc = d.rcli[s] == LOCAL_CLIENT ? -1 : d.rcli[s];
+            if (rc == client) return 0;
+            uint64_t ov = d.ovl[s];
+            for (int k = 0; k < NOVL; k++) {
+                uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
+                if (e == 0) break;
+                if ((int32_t)e - 1 == client) return 0;
+            }
+            if (rs != UNASSIGNED_SEQ && rs <= refSeq) return 0;
+        }
+        return L;
+    }
+    /* localNetLength (mergeTree.ts:1195-1206) */
+    MT_HD int32_t local_len(int32_t s) const { return d.rseq[s] == NOREM ? d.len[s] : 0; }
+
+    MT_HD int32_t slot_at(int32_t t) const { /* t = k*8+j over lorder; -1 if not a row */
+        int32_t k = t >> 3, j = t & 7;
+        if (k >= d.h->nleaf) return -1;
+        int32_t n = d.lorder[k];
+        return j < d.nchild[n] ? n * MAXN + j : -1;
+    }
+
+    /* copy every column of row a to row b (same doc) */
+    MT_HD void copy_row(int32_t b, int32_t a) {
+        d.len[b] = d.len[a];
+        d.seq[b] = d.seq[a];
+        d.rseq[b] = d.rseq[a];
+        d.lseq[b] = d.lseq[a];
+        d.lrseq[b] = d.lrseq[a];
+        d.sid[b] = d.sid[a];
+        d.toff[b] = d.toff[a];
+        d.cli[b] = d.cli[a];
+        d.rcli[b] = d.rcli[a];
+        d.flags[b] = d.flags[a];
+        d.ng[b] = d.ng[a];
+        d.prw[b] = d.prw[a];
+        d.ovl[b] = d.ovl[a];
+        for (int k = 0; k < NKEYS; k++) {
+            d.pv[b * NKEYS + k] = d.pv[a * NKEYS + k];
+            d.pk[b * NKEYS + k] = d.pk[a * NKEYS + k];
+        }
+        for (int k = 0; k < NGRP; k++) d.grp[b * NGRP + k] = d.grp[a * NGRP + k];
+    }
+
+    /* ---- perspective scans ------------------------------------------------------------- */
+    /* Total length under a perspective (getLength, mergeTree.ts:1610). */
+    MT_HD int32_t length(int32_t refSeq, int32_t client) {
+        int32_t total = 0;
+        int32_t T = d.h->nleaf * MAXN;
+        for (int32_t b = 0; b < T; b += W::N) {
+            int32_t s = slot_at(b + w.lane());
+            int32_t v = s >= 0 ? vis(s, refSeq, client) : 0;
+            total += w.sum(v);
+        }
+        return total;
+    }
+    /* First row (document order) with P < pos <= P + vis; returns t (lorder coordinate) or -1,
+     * and P of that row. */
+    MT_HD int32_t find_reach(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+        int32_t run = 0;
+        int32_t T = d.h->nleaf * MAXN;
+        for (int32_t b = 0; b < T; b += W::N) {
+            int32_t t = b + w.lane();
+            int32_t s = slot_at(t);
+            int32_t v = s >= 0 ? vis(s, refSeq, client) : 0;
+            int32_t tot;
+            int32_t P = run + w.excl_scan(v, &tot);
+            bool hit = s >= 0 && P < pos && pos <= P + v;
+            uint64_t m = w.ballot(hit);
+            if (m) {
+                int32_t l = W::ffs(m);
+                *Pout = w.bcast(P, l);
+                return b + l;
+            }
+            run += tot;
+            if (run >= pos && pos > 0) break;
+        }
+        return -1;
+    }
+
+    /* ---- structure: inserting a row into a leaf slab --------------------------------- */
+    /* Insert an empty row slot at child index j of leaf n (shift right). Returns the slot of
+     * the new row, or -1. May split the leaf (and ancestors) afterwards; the returned slot is
+     * remapped by `place_after_split` — callers use the returned final slot. */
+    MT_HD void node_insert_child(int32_t p, int32_t idx, int32_t child) {
+        /* interior node p: insert `child` at idx (insertChildNode, mergeTree.ts:2162-2172) */
+        int32_t n = d.nchild[p];
+        for (int32_t i = n; i > idx; i--) d.kids[p * MAXN + i] = d.kids[p * MAXN + i - 1];
+        d.kids[p * MAXN + idx] = (int16_t)child;
+        d.nchild[p] = (int8_t)(n + 1);
+        d.nparent[child] = (int16_t)p;
+    }
+    MT_HD int32_t child_index(int32_t p, int32_t child) const {
+        for (int32_t i = 0; i < d.nchild[p]; i++)
+            if (d.kids[p * MAXN + i] == child) return i;
+        return -1;
+    }
+    /* insert leaf `nl` into lorder right after leaf `after` */
+    MT_HD void lorder_insert_after(int32_t after, int32_t nl) {
+        int32_t k = d.lpos[after] + 1;
+        int32_t n = d.h->nleaf;
+        /* shift lorder[k..n-1] right by one (uniform loop; small) */
+        for (int32_t i = n; i > k; i--) {
+            int32_t x = d.lorder[i - 1];
+            d.lorder[i] = (int16_t)x;
+            d.lpos[x] = (int16_t)i;
+        }
+        d.lorder[k] = (int16_t)nl;
+        d.lpos[nl] = (int16_t)k;
+        d.h->nleaf = n + 1;
+    }
+    /* split (mergeTree.ts:2509-2522) of a full node (8 children) into 4 + 4; the new node is
+     * inserted after it in its parent, recursively; root split -> updateRoot (1909-1920).
+     * Returns the new node. */
+    MT_HD int32_t split_node(int32_t n) {
+        int8_t lvl = d.nlevel[n];
+        int32_t nn = alloc_node(lvl);
+        if (nn < 0) return -1;
+        d.nscour[nn] = -1;
+        if (lvl == 0) {
+            for (int32_t i = 0; i < 4; i++) copy_row(nn * MAXN + i, n * MAXN + 4 + i);
+        } else {
+            for (int32_t i = 0; i < 4; i++) {
+                int32_t c = d.kids[n * MAXN + 4 + i];
+                d.kids[nn * MAXN + i] = (int16_t)c;
+                d.nparent[c] = (int16_t)nn;
+            }
+        }
+        d.nchild[n] = 4;
+        d.nchild[nn] = 4;
+        if (lvl == 0) lorder_insert_after(n, nn);
+        int32_t p = d.nparent[n];
+        if (p < 0) {
+            int32_t r = alloc_node((int8_t)(lvl + 1));
+            if (r < 0) return -1;
+            d.kids[r * MAXN + 0] = (int16_t)n;
+            d.kids[r * MAXN + 1] = (int16_t)nn;
+            d.nchild[r] = 2;
+            d.nparent[n] = (int16_t)r;
+            d.nparent[nn] = (int16_t)r;
+            d.h->root = r;
+        } else {
+            node_insert_child(p, child_index(p, n) + 1, nn);
+            if (d.nchild[p] >= MAXN) split_node(p);
+        }
+        return nn;
+    }
+    /* Make room at child index j of leaf n; returns slot for the new row (after any split). */
+    MT_HD int32_t leaf_insert_slot(int32_t n, int32_t j) {
+        int32_t c = d.nchild[n];
+        for (int32_t i = c; i > j; i--) copy_row(n * MAXN + i, n * MAXN + i - 1);
+        d.nchild[n] = (int8_t)(c + 1);
+        if (c + 1 >= MAXN) {
+            int32_t nn = split_node(n);
+            if (nn < 0) return -1;
+            if (j >= 4) return nn * MAXN + (j - 4);
+        }
+        return n * MAXN + j;
+    }
+
+    /* ---- text arena -------------------------------------------------------------------- */
+    MT_HD uint16_t* arena_base(int32_t side) { return d.arena + (int64_t)side * d.caps.acap; }
+    /* reserve n units at the arena top; compacts into the other half when full */
+    MT_HD int32_t arena_alloc(int32_t n) {
+        if (d.h->arenaTop + n > d.caps.acap) {
+            arena_gc();
+            if (d.h->arenaTop + n > d.caps.acap) {
+                fail(E_CAPACITY);
+                return -1;
+            }
+        }
+        int32_t off = d.h->arenaTop;
+        d.h->arenaTop = off + n;
+        return off;
+    }
+    MT_HD void arena_copy(uint16_t* dst, const uint16_t* src, int32_t n) {
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            uint16_t v = i < n ? src[i] : 0;
+            w.sync();
+            if (i < n) dst[i] = v;
+        }
+        w.sync();
+    }
+    /* copy all live text rows into the other half, in document order */
+    MT_HD void arena_gc() {
+        int32_t from = d.h->arenaSide, to = from ^ 1;
+        uint16_t* src = arena_base(from);
+        uint16_t* dst = arena_base(to);
+        int32_t top = 0;
+        int32_t T = d.h->nleaf * MAXN;
+        for (int32_t t = 0; t < T; t++) {
+            int32_t s = slot_at(t);
+            if (s < 0 || (d.flags[s] & RF_MARKER)) continue;
+            int32_t L = d.len[s];
+            arena_copy(dst + top, src + d.toff[s], L);
+            d.toff[s] = (uint32_t)top;
+            top += L;
+        }
+        d.h->arenaSide = to;
+        d.h->arenaTop = top;
+        w.sync();
+    }
+
+    /* ---- splitAt (mergeTree.ts:523-567, textSegment.ts:103-111) ------------------------ */
+    /* Split the row at lorder coordinate t at offset off (0 < off < len). Returns the slot of
+     * the LEFT part afterwards (the right part is the next row in document order). */
+    MT_HD int32_t split_row(int32_t t, int32_t off) {
+        int32_t n = d.lorder[t >> 3], j = t & 7;
+        int32_t s0 = n * MAXN + j;
+        if (d.flags[s0] & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
+        bool willSplit = d.nchild[n] + 1 >= MAXN;
+        int32_t rs = leaf_insert_slot(n, j + 1);
+        if (rs < 0) return -1;
+        /* the left part stays at n*8+j unless the leaf split moved children 4..7 */
+        int32_t ls = n * MAXN + j;
+        if (willSplit && j >= 4) ls = d.lorder[d.lpos[n] + 1] * MAXN + (j - 4);
+        copy_row(rs, ls);
+        d.len[rs] = d.len[ls] - off;
+        d.toff[rs] = d.toff[ls] + (uint32_t)off;
+        d.len[ls] = off;
+        d.sid[rs] = (uint32_t)d.h->nextSid++;
+        /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
+         * same groups, appended at the end of each group's segment list */
+        int32_t ng = d.ng[ls];
+        for (int32_t g = 0; g < ng; g++) mem_append(d.grp[ls * NGRP + g], d.sid[rs]);
+        return ls;
+    }
+
+    /* ---- segment groups ---------------------------------------------------------------- */
+    MT_HD void mem_append(int32_t gid, uint32_t sid) {
+        int32_t m = d.h->memN;
+        if (m >= d.caps.mcap) {
+            mem_compact();
+            m = d.h->memN;
+            if (m >= d.caps.mcap) {
+                fail(E_CAPACITY);
+                return;
+            }
+        }
+        d.mgid[m] = gid;
+        d.msid[m] = sid;
+        d.h->memN = m + 1;
+    }
+    MT_HD void mem_compact() {
+        /* drop entries of groups already acked (gid < head gid) */
+        int32_t head = d.h->gqN ? d.gq[d.h->gqHead % d.caps.gcap] : 0x7fffffff;
+        int32_t wpos = 0;
+        for (int32_t i = 0; i < d.h->memN; i++) {
+            if (d.mgid[i] >= head) {
+                d.mgid[wpos] = d.mgid[i];
+                d.msid[wpos] = d.msid[i];
+                wpos++;
+            }
+        }
+        d.h->memN = wpos;
+    }
+    /* SegmentGroupCollection.enqueue (segmentGroupCollection.ts:28-31) */
+    MT_HD void row_enqueue_group(int32_t s, int32_t gid) {
+        int32_t ng = d.ng[s];
+        if (ng >= NGRP) {
+            fail(E_CAPACITY);
+            return;
+        }
+        d.grp[s * NGRP + ng] = gid;
+        d.ng[s] = (uint8_t)(ng + 1);
+        mem_append(gid, d.sid[s]);
+    }
+    /* addToPendingList (mergeTree.ts:1955-1962); the group id is the op's localSeq */
+    MT_HD void pending_add(int32_t s, int32_t gid, bool* created) {
+        if (!*created) {
+            if (d.h->gqN >= d.caps.gcap) {
+                fail(E_CAPACITY);
+                return;
+            }
+            d.gq[(d.h->gqHead + d.h->gqN) % d.caps.gcap] = gid;
+            d.h->gqN++;
+            *created = true;
+        }
+        row_enqueue_group(s, gid);
+    }
+
+    /* ---- zamboni heap (collections.ts:212-264, LRUSegmentComparer mergeTree.ts:957-960) ---- */
+    MT_HD void heap_add(uint32_t sid, int32_t seq) {
+        int32_t n = d.h->heapN;
+        if (n >= d.caps.hcap) {
+            fail(E_CAPACITY);
+            return;
+        }
+        /* L[k] (1-based) lives at index k-1 */
+        int32_t k = n + 1;
+        d.hsid[k - 1] = sid;
+        d.hseq[k - 1] = seq;
+        d.h->heapN = n + 1;
+        if (n + 1 > d.h->hwHeap) d.h->hwHeap = n + 1;
+        while (k > 1 && d.hseq[(k >> 1) - 1] - d.hseq[k - 1] > 0) {
+            uint32_t ts = d.hsid[(k >> 1) - 1];
+            int32_t tq = d.hseq[(k >> 1) - 1];
+            d.hsid[(k >> 1) - 1] = d.hsid[k - 1];
+            d.hseq[(k >> 1) - 1] = d.hseq[k - 1];
+            d.hsid[k - 1] = ts;
+            d.hseq[k - 1] = tq;
+            k >>= 1;
+        }
+    }
+    MT_HD void heap_pop(uint32_t* sid, int32_t* seq) {
+        int32_t cnt = d.h->heapN;
+        *sid = d.hsid[0];
+        *seq = d.hseq[0];
+        d.hsid[0] = d.hsid[cnt - 1];
+        d.hseq[0] = d.hseq[cnt - 1];
+        cnt--;
+        d.h->heapN = cnt;
+        int32_t k = 1;
+        while ((k << 1) <= cnt) {
+            int32_t j = k << 1;
+            if (j < cnt && d.hseq[j - 1] - d.hseq[j] > 0) j++;
+            if (d.hseq[k - 1] - d.hseq[j - 1] <= 0) break;
+            uint32_t ts = d.hsid[k - 1];
+            int32_t tq = d.hseq[k - 1];
+            d.hsid[k - 1] = d.hsid[j - 1];
+            d.hseq[k - 1] = d.hseq[j - 1];
+            d.hsid[j - 1] = ts;
+            d.hseq[j - 1] = tq;
+            k = j;
+        }
+    }
+    /* addToLRUSet (mergeTree.ts:1306-1316) */
+    MT_HD void add_lru(int32_t s, int32_t seq) {
+        int32_t n = s / MAXN;
+        if (d.nscour[n] != 1 && seq > d.h->currentSeq) {
+            d.nscour[n] = 1;
+            heap_add(d.sid[s], seq);
+        }
+    }
+    /* locate a row by stable id; -1 if unlinked */
+    MT_HD int32_t find_sid(uint32_t sid) {
+        int32_t T = d.h->nleaf * MAXN;
+        for (int32_t b = 0; b < T; b += W::N) {
+            int32_t s = slot_at(b + w.lane());
+            uint64_t m = w.ballot(s >= 0 && d.sid[s] == sid);
+            if (m) return w.bcast(s, W::ffs(m));
+        }
+        return -1;
+    }
+
+    /* ---- properties (segmentPropertiesManager.ts:35-111) ---------------------------- */
+    MT_HD int32_t key_slot(uint16_t key) {
+        for (int32_t i = 0; i < d.h->nkeys; i++)
+            if (d.h->keys[i] == key) return i;
+        if (d.h->nkeys >= NKEYS) {
+            fail(E_UNSUPPORTED);
+            return -1;
+        }
+        d.h->keys[d.h->nkeys] = key;
+        return d.h->nkeys++;
+    }
+    MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
+        if (!(d.flags[s] & RF_PROPS)) {
+            d.prw[s] = 0;
+            d.flags[s] |= RF_PROPS;
+            for (int k = 0; k < NKEYS; k++) {
+                d.pv[s * NKEYS + k] = 0;
+                d.pk[s * NKEYS + k] = 0;
+            }
+        }
+        if (d.prw[s] > 0 && seq != UNASSIGNED_SEQ && collaborating) return;
+        if (rewrite) {
+            if (collaborating && seq == UNASSIGNED_SEQ) d.prw[s]++;
+            for (int32_t k = 0; k < d.h->nkeys; k++) {
+                if (d.pv[s * NKEYS + k] == 0) continue;
+                bool inNew = false;
+                for (int32_t j = 0; j < nkv; j++)
+                    if (kv[j].key == d.h->keys[k] && kv[j].value != 0 && !(kv[j].value & MT_VALUE_FALSY)) inNew = true;
+                bool modify = seq == UNASSIGNED_SEQ || d.pk[s * NKEYS + k] == 0;
+                if (!inNew && modify) d.pv[s * NKEYS + k] = 0;
+            }
+        }
+        for (int32_t j = 0; j < nkv; j++) {
+            int32_t k = key_slot(kv[j].key);
+            if (k < 0) return;
+            if (collaborating) {
+                if (seq == UNASSIGNED_SEQ) {
+                    if (d.pk[s * NKEYS + k] == 0xFF) {
+                        fail(E_CAPACITY);
+                        return;
+                    }
+                    d.pk[s * NKEYS + k]++;
+                } else if (!(d.pk[s * NKEYS + k] == 0)) {
+                    continue;
+                }
+            }
+            d.pv[s * NKEYS + k] = kv[j].value;
+        }
+    }
+    /* ackPendingProperties (segmentPropertiesManager.ts:19-33) */
+    MT_HD void ack_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite) {
+        if (rewrite) d.prw[s]--;
+        for (int32_t j = 0; j < nkv; j++) {
+            int32_t k = key_slot(kv[j].key);
+            if (k < 0) return;
+            if (d.pk[s * NKEYS + k]) d.pk[s * NKEYS + k]--;
+        }
+    }
+    MT_HD bool match_props(int32_t a, int32_t b) const { /* matchProperties (properties.ts:61-92) */
+        bool pa = d.flags[a] & RF_PROPS, pb = d.flags[b] & RF_PROPS;
+        if (pa != pb) return false;
+        if (!pa) return true;
+        for (int k = 0; k < NKEYS; k++)
+            if (d.pv[a * NKEYS + k] != d.pv[b * NKEYS + k]) return false;
+        return true;
+    }
+
+    /* ---- zamboni: scourNode / pack / zamboniSegments (mergeTree.ts:1322-1511) ---------- */
+    /* canAppend (textSegment.ts:63-68) */
+    MT_HD bool can_append(int32_t a, int32_t b) {
+        if (d.flags[a] & RF_MARKER) return false;
+        int32_t L = d.len[a];
+        if (L > 0 && arena_base(d.h->arenaSide)[d.toff[a] + L - 1] == '\n') return false;
+        if (d.flags[b] & RF_MARKER) return false;
+        return d.len[a] <= GRANULARITY || d.len[b] <= GRANULARITY;
+    }
+    /* TextSegment.append (textSegment.ts:74-85): the merged text is rebuilt at the arena top */
+    MT_HD void append_text(int32_t a, int32_t b) {
+        int32_t La = d.len[a], Lb = d.len[b];
+        uint16_t* base = arena_base(d.h->arenaSide);
+        if ((int32_t)d.toff[a] + La == d.h->arenaTop && d.h->arenaTop + Lb <= d.caps.acap) {
+            int32_t off = arena_alloc(Lb);
+            arena_copy(base + off, base + d.toff[b], Lb);
+        } else if ((int32_t)d.toff[a] + La == (int32_t)d.toff[b]) {
+            /* already contiguous */
+        } else {
+            int32_t off = arena_alloc(La + Lb);
+            if (off < 0) return;
+            base = arena_base(d.h->arenaSide); /* a GC may have switched halves */
+            arena_copy(base + off, base + d.toff[a], La);
+            arena_copy(base + off + La, base + d.toff[b], Lb);
+            d.toff[a] = (uint32_t)off;
+        }
+        d.len[a] = La + Lb;
+    }
+    /* scourNode on leaf n: compacts the slab in place; returns the new child count. Rows are
+     * merged into their predecessor or unlinked exactly as the reference decides. */
+    MT_HD int32_t scour_leaf(int32_t n) {
+        int32_t c = d.nchild[n];
+        int32_t wpos = 0;
+        int32_t prev = -1; /* slot of prevSegment in the compacted slab */
+        int32_t minSeq = d.h->minSeq;
+        for (int32_t k = 0; k < c; k++) {
+            int32_t s = n * MAXN + k;
+            if (d.ng[s] == 0) {
+                if (d.rseq[s] != NOREM) {
+                    if (d.rseq[s] > minSeq) {
+                        if (wpos != k) copy_row(n * MAXN + wpos, s);
+                        wpos++;
+                    }
+                    /* else: unlinked */
+                    prev = -1;
+                } else {
+                    if (d.seq[s] <= minSeq) {
+                        bool ok = prev >= 0 && can_append(prev, s) && match_props(prev, s) && local_len(s) > 0;
+                        if (ok) {
+                            append_text(prev, s);
+                        } else {
+                            int32_t dst = n * MAXN + wpos;
+                            if (wpos != k) copy_row(dst, s);
+                            wpos++;
+                            prev = local_len(dst) > 0 ? dst : -1;
+                        }
+                    } else {
+                        if (wpos != k) copy_row(n * MAXN + wpos, s);
+                        wpos++;
+                        prev = -1;
+                    }
+                }
+            } else {
+                if (wpos != k) copy_row(n * MAXN + wpos, s);
+                wpos++;
+                prev = -1;
+            }
+        }
+        d.nchild[n] = (int8_t)wpos;
+        return wpos;
+    }
+    /* pack (mergeTree.ts:1401-1453) of `block`'s parent */
+    MT_HD void pack(int32_t block) {
+        int32_t parent = d.nparent[block];
+        int32_t pc = d.nchild[parent];
+        int8_t lvl = d.nlevel[block];
+        if (lvl == 0) {
+            /* scour every sibling leaf, then redistribute their rows over new leaves */
+            int32_t total = 0;
+            for (int32_t i = 0; i < pc; i++) total += scour_leaf(d.kids[parent * MAXN + i]);
+            int32_t cc = total / (MAXN / 2);
+            if (cc > MAXN - 1) cc = MAXN - 1;
+            if (cc < 1) cc = 1;
+            int32_t base = total / cc, extra = total % cc;
+            /* new leaves; rows move from the old slabs (old leaves are read in order) */
+            int32_t oldk[MAXN];
+            for (int32_t i = 0; i < pc; i++) oldk[i] = d.kids[parent * MAXN + i];
+            int32_t firstPos = d.lpos[oldk[0]];
+            int32_t newk[MAXN];
+            int32_t ri = 0, rj = 0; /* read cursor: old leaf index, child index */
+            for (int32_t ni = 0; ni < cc; ni++) {
+                int32_t cnt = base + (extra > 0 ? 1 : 0);
+                if (extra > 0) extra--;
+                int32_t nb = alloc_node(0);
+                if (nb < 0) return;
+                newk[ni] = nb;
+                for (int32_t q = 0; q < cnt; q++) {
+                    while (rj >= d.nchild[oldk[ri]]) {
+                        ri++;
+                        rj = 0;
+                    }
+                    copy_row(nb * MAXN + q, oldk[ri] * MAXN + rj);
+                    rj++;
+                }
+                d.nchild[nb] = (int8_t)cnt;
+                d.nparent[nb] = (int16_t)parent;
+            }
+            for (int32_t i = 0; i < pc; i++) free_node(oldk[i]);
+            /* lorder: replace [firstPos, firstPos+pc) with the new leaves */
+            int32_t nl = d.h->nleaf;
+            int32_t delta = cc - pc;
+            if (delta < 0) {
+                for (int32_t i = firstPos + pc; i < nl; i++) {
+                    int32_t x = d.lorder[i];
+                    d.lorder[i + delta] = (int16_t)x;
+                    d.lpos[x] = (int16_t)(i + delta);
+                }
+            } else if (delta > 0) {
+                for (int32_t i = nl - 1; i >= firstPos + pc; i--) {
+                    int32_t x = d.lorder[i];
+                    d.lorder[i + delta] = (int16_t)x;
+                    d.lpos[x] = (int16_t)(i + delta);
+                }
+            }
+            for (int32_t i = 0; i < cc; i++) {
+                d.lorder[firstPos + i] = (int16_t)newk[i];
+                d.lpos[newk[i]] = (int16_t)(firstPos + i);
+            }
+            d.h->nleaf = nl + delta;
+            for (int32_t i = 0; i < cc; i++) d.kids[parent * MAXN + i] = (int16_t)newk[i];
+            d.nchild[parent] = (int8_t)cc;
+        } else {
+            /* interior: collect grandchildren in order, regroup into new interior nodes */
+            int16_t hold[MAXN * MAXN];
+            int32_t total = 0;
+            int32_t oldk[MAXN];
+            for (int32_t i = 0; i < pc; i++) {
+                int32_t cb = d.kids[parent * MAXN + i];
+                oldk[i] = cb;
+                for (int32_t q = 0; q < d.nchild[cb]; q++) hold[total++] = d.kids[cb * MAXN + q];
+            }
+            int32_t cc = total / (MAXN / 2);
+            if (cc > MAXN - 1) cc = MAXN - 1;
+            if (cc < 1) cc = 1;
+            int32_t base = total / cc, extra = total % cc;
+            for (int32_t i = 0; i < pc; i++) free_node(oldk[i]);
+            int32_t read = 0;
+            for (int32_t ni = 0; ni < cc; ni++) {
+                int32_t cnt = base + (extra > 0 ? 1 : 0);
+                if (extra > 0) extra--;
+                int32_t nb = alloc_node(lvl);
+                if (nb < 0) return;
+                for (int32_t q = 0; q < cnt; q++) {
+                    int32_t ch = hold[read++];
+                    d.kids[nb * MAXN + q] = (int16_t)ch;
+                    d.nparent[ch] = (int16_t)nb;
+                }
+                d.nchild[nb] = (int8_t)cnt;
+                d.nparent[nb] = (int16_t)parent;
+                d.kids[parent * MAXN + ni] = (int16_t)nb;
+            }
+            d.nchild[parent] = (int8_t)cc;
+        }
+        if (d.nchild[parent] < MAXN / 2 && d.nparent[parent] >= 0) pack(parent);
+    }
+    /* zamboniSegments (mergeTree.ts:1455-1511) */
+    MT_HD void zamboni() {
+        if (!d.h->collaborating) return;
+        for (int i = 0; i < 2; i++) {
+            if (d.h->heapN < 1) break;
+            if (d.hseq[0] > d.h->minSeq) break;
+            uint32_t sid;
+            int32_t mseq;
+            heap_pop(&sid, &mseq);
+            int32_t s = find_sid(sid);
+            if (s < 0) continue;
+            int32_t n = s / MAXN;
+            if (d.nscour[n] == 0) continue;
+            int32_t before = d.nchild[n];
+            int32_t after = scour_leaf(n);
+            d.nscour[n] = 0;
+            if (after < before) {
+                if (after < MAXN / 2 && d.nparent[n] >= 0) pack(n);
+            }
+        }
+    }
+    /* setMinSeq (mergeTree.ts:1751-1769) */
+    MT_HD void set_min_seq(int32_t minSeq) {
+        if (!(minSeq <= d.h->currentSeq)) fail(E_ASSERT);
+        if (!(d.h->minSeq <= minSeq)) fail(E_ASSERT);
+        if (minSeq > d.h->minSeq) {
+            d.h->minSeq = minSeq;
+            zamboni();
+        }
+    }
+
+    /* ---- insert (insertSegments 2001-2031, blockInsert 2174-2257) -------------------- */
+    /* breakTie for a zero-length row (2281-2310) */
+    MT_HD bool break_tie(int32_t s, int32_t refSeq, int32_t client) const {
+        int32_t rs = d.rseq[s];
+        if (rs != NOREM && rs != 0 && rs <= refSeq && rs != UNASSIGNED_SEQ) return false;
+        if (client == d.h->localShort) return true;
+        return d.seq[s] != UNASSIGNED_SEQ;
+    }
+    /* continueFrom (2187-2194): first row after leaf lorder[k] with localNetLength > 0 is a
+     * local-pending insert */
+    MT_HD bool continue_from(int32_t k) {
+        int32_t T = d.h->nleaf * MAXN;
+        for (int32_t b = (k + 1) * MAXN; b < T; b += W::N) {
+            int32_t s = slot_at(b + w.lane());
+            uint64_t m = w.ballot(s >= 0 && local_len(s) > 0);
+            if (m) {
+                int32_t f = w.bcast(s, W::ffs(m));
+                return d.seq[f] == UNASSIGNED_SEQ;
+            }
+        }
+        return false;
+    }
+    /* ensureIntervalBoundary (2274-2278): split the row strictly containing pos */
+    MT_HD void ensure_boundary(int32_t pos, int32_t refSeq, int32_t client) {
+        int32_t P;
+        int32_t t = find_reach(pos, refSeq, client, &P);
+        if (t < 0) return;
+        int32_t s = slot_at(t);
+        int32_t v = vis(s, refSeq, client);
+        if (P + v > pos) split_row(t, pos - P);
+    }
+    /* returns the slot of the inserted row or -1 */
+    MT_HD int32_t insert_row(int32_t pos, int32_t refSeq, int32_t client, int32_t seq) {
+        int32_t k, j;
+        if (pos == 0) {
+            k = 0;
+            j = 0;
+        } else {
+            int32_t P;
+            int32_t t = find_reach(pos, refSeq, client, &P);
+            if (t < 0) return -1;
+            int32_t s = slot_at(t);
+            int32_t v = vis(s, refSeq, client);
+            k = t >> 3;
+            j = t & 7;
+            if (P + v > pos) {
+                /* pos strictly inside (only possible for an unsplittable segment): insert before */
+            } else {
+                j++;
+            }
+        }
+        for (;;) {
+            int32_t n = d.lorder[k];
+            int32_t c = d.nchild[n];
+            for (; j < c; j++) {
+                int32_t s = n * MAXN + j;
+                if (vis(s, refSeq, client) > 0 || break_tie(s, refSeq, client)) return leaf_insert_slot(n, j);
+            }
+            if (seq != UNASSIGNED_SEQ && k + 1 < d.h->nleaf && continue_from(k)) {
+                k++;
+                j = 0;
+                continue;
+            }
+            return leaf_insert_slot(n, c);
+        }
+    }
+    MT_HD void insert_segments(const mt_op_rec& op, const Pools& p, int32_t refSeq, int32_t client, int32_t seq) {
+        int32_t pos = op.pos1;
+        ensure_boundary(pos, refSeq, client);
+        bool hasL = seq == UNASSIGNED_SEQ;
+        int32_t localSeq = hasL ? ++d.h->localSeq : 0;
+        bool marker = op.seg_kind == MT_SEG_MARKER;
+        int32_t L = marker ? 1 : op.text_len;
+        if (L > 0) {
+            int32_t off = 0;
+            if (!marker) {
+                off = arena_alloc(L);
+                if (off < 0) return;
+            }
+            int32_t s = insert_row(pos, refSeq, client, seq);
+            if (s < 0) {
+                fail(E_INSERT_FAILED);
+                return;
+            }
+            d.len[s] = L;
+            d.seq[s] = seq;
+            d.rseq[s] = NOREM;
+            d.lseq[s] = localSeq;
+            d.lrseq[s] = 0;
+            d.cli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
+            d.rcli[s] = 0;
+            d.flags[s] = (uint8_t)((marker ? RF_MARKER : 0) | (hasL ? RF_LSEQ : 0));
+            d.ng[s] = 0;
+            d.prw[s] = 0;
+            d.ovl[s] = 0;
+            d.sid[s] = (uint32_t)d.h->nextSid++;
+            if (marker) {
+                d.toff[s] = (uint32_t)op.pos2;
+            } else {
+                d.toff[s] = (uint32_t)off;
+                arena_copy(arena_base(d.h->arenaSide) + off, p.text + op.text_off, L);
+            }
+            for (int k = 0; k < NKEYS; k++) {
+                d.pv[s * NKEYS + k] = 0;
+                d.pk[s * NKEYS + k] = 0;
+            }
+            if (op.props) { /* TextSegment.make(text, props): addProperties without collab */
+                const mt_props_rec& pr = p.props[op.props - 1];
+                add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE, 0, false);
+            }
+            if (d.h->collaborating) { /* saveIfLocal (2197-2212) */
+                if (seq == UNASSIGNED_SEQ && client == d.h->localShort) {
+                    bool created = false;
+                    pending_add(s, localSeq, &created);
+                } else if (seq > d.h->minSeq) {
+                    add_lru(s, seq);
+                }
+            }
+        }
+        if (d.h->collaborating && seq != UNASSIGNED_SEQ) zamboni();
+    }
+
+    /* ---- range ops: markRangeRemoved (2640-2752) / annotateRange (2598-2638) ----------- */
+    template <class F>
+    MT_HD void map_range(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
+        int32_t run = 0;
+        int32_t T = d.h->nleaf * MAXN;
+        for (int32_t b = 0; b < T; b += W::N) {
+            int32_t t = b + w.lane();
+            int32_t s = slot_at(t);
+            int32_t v = s >= 0 ? vis(s, refSeq, client) : 0;
+            int32_t tot;
+            int32_t P = run + w.excl_scan(v, &tot);
+            bool hit = s >= 0 && v > 0 && P < end && P + v > start;
+            uint64_t m = w.ballot(hit);
+            while (m) {
+                int32_t l = W::ffs(m);
+                m &= m - 1;
+                leaf(w.bcast(s, l));
+            }
+            run += tot;
+            if (run >= end) break;
+        }
+    }
+    MT_HD void mark_range_removed(int32_t start, int32_t end, int32_t refSeq, int32_t client, int32_t seq) {
+        ensure_boundary(start, refSeq, client);
+        ensure_boundary(end, refSeq, client);
+        bool hasL = seq == UNASSIGNED_SEQ;
+        int32_t localSeq = hasL ? ++d.h->localSeq : 0;
+        bool created = false;
+        map_range(start, end, refSeq, client, [&](int32_t s) {
+            if (d.rseq[s] != NOREM) {
+                if (d.rseq[s] == UNASSIGNED_SEQ) {
+                    d.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
+                    d.rseq[s] = seq;
+                    d.flags[s] &= (uint8_t)~RF_LRSEQ;
+                } else {
+                    uint64_t ov = d.ovl[s];
+                    int k = 0;
+                    while (k < NOVL && ((ov >> (8 * k)) & 0xFF)) k++;
+                    if (k >= NOVL) {
+                        fail(E_UNSUPPORTED);
+                    } else {
+                        d.ovl[s] = ov | ((uint64_t)(client + 1) << (8 * k));
+                    }
+                }
+            } else {
+                d.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
+                d.rseq[s] = seq;
+                d.lrseq[s] = localSeq;
+                if (hasL)
+                    d.flags[s] |= RF_LRSEQ;
+                else
+                    d.flags[s] &= (uint8_t)~RF_LRSEQ;
+            }
+            if (d.h->collaborating) {
+                if (d.rseq[s] == UNASSIGNED_SEQ && client == d.h->localShort)
+                    pending_add(s, localSeq, &created);
+                else
+                    add_lru(s, seq);
+            }
+        });
+        if (d.h->collaborating && seq != UNASSIGNED_SEQ) zamboni();
+    }
+    MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t refSeq,
+                              int32_t client, int32_t seq) {
+        ensure_boundary(start, refSeq, client);
+        ensure_boundary(end, refSeq, client);
+        int32_t localSeq = seq == UNASSIGNED_SEQ ? ++d.h->localSeq : 0;
+        bool created = false;
+        bool collab = d.h->collaborating;
+        map_range(start, end, refSeq, client, [&](int32_t s) {
+            add_props(s, kv, nkv, rewrite, seq, collab);
+            if (collab) {
+                if (seq == UNASSIGNED_SEQ)
+                    pending_add(s, localSeq, &created);
+                else
+                    add_lru(s, seq);
+            }
+        });
+        if (d.h->collaborating && seq != UNASSIGNED_SEQ) zamboni();
+    }
+
+    /* ---- ack (mergeTree.ts:1926-1953, BaseSegment.ack 486-521) ------------------------ */
+    MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
+        if (d.h->gqN > 0) {
+            int32_t gid = d.gq[d.h->gqHead % d.caps.gcap];
+            d.h->gqHead = (d.h->gqHead + 1) % d.caps.gcap;
+            d.h->gqN--;
+            for (int32_t i = 0; i < d.h->memN; i++) {
+                if (d.mgid[i] != gid) continue;
+                int32_t s = find_sid(d.msid[i]);
+                if (s < 0) {
+                    fail(E_ASSERT);
+                    continue;
+                }
+                /* dequeue the row's head group; must be this group */
+                int32_t ng = d.ng[s];
+                if (ng < 1 || d.grp[s * NGRP] != gid) fail(E_ASSERT);
+                for (int32_t g = 1; g < ng; g++) d.grp[s * NGRP + g - 1] = d.grp[s * NGRP + g];
+                if (ng > 0) d.ng[s] = (uint8_t)(ng - 1);
+                if (kind == MT_OP_ANNOTATE) {
+                    if (!(d.flags[s] & RF_PROPS)) fail(E_ASSERT);
+                    ack_props(s, kv, nkv, rewrite);
+                } else if (kind == MT_OP_INSERT) {
+                    if (d.seq[s] != UNASSIGNED_SEQ) fail(E_ASSERT);
+                    d.seq[s] = seq;
+                    d.flags[s] &= (uint8_t)~RF_LSEQ;
+                } else if (kind == MT_OP_REMOVE) {
+                    if (d.rseq[s] == NOREM || d.rseq[s] == 0) fail(E_ASSERT);
+                    d.flags[s] &= (uint8_t)~RF_LRSEQ;
+                    if (d.rseq[s] == UNASSIGNED_SEQ) d.rseq[s] = seq;
+                } else {
+                    fail(E_ASSERT);
+                }
+                add_lru(s, seq);
+            }
+            /* drop this group's membership entries when it heads the log */
+            if (d.h->memN > 0 && d.h->memN >= d.caps.mcap / 2) mem_compact();
+        }
+        zamboni();
+    }
+
+    /* ---- Client.applyMsg (client.ts:797-819) / local edits ---------------------------- */
+    MT_HD void apply(const mt_op_rec& op, const Pools& p) {
+        if (d.h->err) return;
+        int32_t kind = op.kind & MT_OP_KIND_MASK;
+        const mt_kv* kv = 0;
+        int32_t nkv = 0;
+        bool rw = false;
+        if (op.props && kind == MT_OP_ANNOTATE) {
+            const mt_props_rec& pr = p.props[op.props - 1];
+            kv = p.kv + pr.kv_off;
+            nkv = pr.nkv;
+            rw = pr.combining == MT_COMBINE_REWRITE;
+        }
+        if (op.kind & MT_OPF_LOCAL) {
+            int32_t client = d.h->collaborating ? d.h->localShort : -1;
+            int32_t refSeq = d.h->currentSeq;
+            int32_t seq = d.h->collaborating ? UNASSIGNED_SEQ : UNIVERSAL_SEQ;
+            /* getValidOpRange (client.ts:486-548) */
+            int32_t length = length_local();
+            int32_t start = op.pos1, end = op.pos2;
+            bool bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
+            if (kind != MT_OP_INSERT && end <= start) bad = true;
+            if (bad) {
+                fail(E_INVALID_RANGE);
+                return;
+            }
+            if (kind == MT_OP_INSERT) {
+                if (op.seg_kind != MT_SEG_MARKER && op.text_len == 0) return;
+                insert_segments(op, p, refSeq, client, seq);
+            } else if (kind == MT_OP_REMOVE) {
+                mark_range_removed(start, end, refSeq, client, seq);
+            } else if (kind == MT_OP_ANNOTATE) {
+                annotate_range(start, end, kv, nkv, rw, refSeq, client, seq);
+            }
+            d.h->opsDone++;
+            return;
+        }
+        get_or_add_short(op.client);
+        if (kind != MT_OP_NOOP) {
+            if ((int32_t)op.client == d.h->localLong) {
+                ack(kind, kv, nkv, rw, op.seq);
+            } else {
+                int32_t client = get_or_add_short(op.client);
+                if (kind == MT_OP_INSERT)
+                    insert_segments(op, p, op.ref_seq, client, op.seq);
+                else if (kind == MT_OP_REMOVE)
+                    mark_range_removed(op.pos1, op.pos2, op.ref_seq, client, op.seq);
+                else if (kind == MT_OP_ANNOTATE)
+                    annotate_range(op.pos1, op.pos2, kv, nkv, rw, op.ref_seq, client, op.seq);
+                if (!(d.h->currentSeq < op.seq)) fail(E_ASSERT);
+                if (!(d.h->minSeq <= op.min_seq)) fail(E_ASSERT);
+            }
+        }
+        /* updateSeqNumbers (client.ts:821-828) */
+        if (!(d.h->currentSeq <= op.seq)) fail(E_ASSERT);
+        d.h->currentSeq = op.seq;
+        if (!(op.min_seq <= op.seq)) fail(E_ASSERT);
+        set_min_seq(op.min_seq);
+        d.h->opsDone++;
+        int32_t slots = d.h->nleaf * MAXN;
+        if (slots > d.h->hwSlots) d.h->hwSlots = slots;
+    }
+    MT_HD int32_t length_local() { return length(d.h->currentSeq, d.h->localShort); }
+
+    /* ---- reads: text (MergeTreeTextHelper.getText, textSegment.ts:154-275) ------------ */
+    /* Writes at most cap units; returns the text length under the perspective. */
+    MT_HD int64_t get_text(int32_t refSeq, int32_t client, uint16_t* out, int64_t cap) {
+        int64_t n = 0;
+        int32_t T = d.h->nleaf * MAXN;
+        const uint16_t* base = arena_base(d.h->arenaSide);
+        for (int32_t t = 0; t < T; t++) {
+            int32_t s = slot_at(t);
+            if (s < 0 || (d.flags[s] & RF_MARKER)) continue;
+            int32_t v = vis(s, refSeq, client);
+            if (v <= 0) continue;
+            if (out) {
+                int32_t m = v;
+                if (n + m > cap) m = (int32_t)(cap - n > 0 ? cap - n : 0);
+                arena_copy(out + n, base + d.toff[s], m);
+            }
+            n += v;
+        }
+        return n;
+    }
+
+    /* ---- canonical dump (include/mt_oplog.h) ------------------------------------------- */
+    MT_HD static void put_bytes(uint8_t* out, int64_t cap, int64_t* n, const void* src, int64_t k) {
+        if (out && *n + k <= cap) {
+            const uint8_t* p = (const uint8_t*)src;
+            for (int64_t i = 0; i < k; i++) out[*n + i] = p[i];
+        }
+        *n += k;
+    }
+    MT_HD int32_t long_of(uint8_t sh) const { return sh == LOCAL_CLIENT ? -1 : (int32_t)d.s2l[sh]; }
+    /* Single-lane (lane 0 writes) serial dump; returns the byte count. */
+    MT_HD int64_t dump(uint8_t* out, int64_t cap) {
+        int64_t n = 0;
+        bool wr = w.lane() == 0;
+        uint8_t* o = wr ? out : 0;
+        int32_t nsegs = 0;
+        int32_t T = d.h->nleaf * MAXN;
+        for (int32_t t = 0; t < T; t++)
+            if (slot_at(t) >= 0) nsegs++;
+        int32_t hdr[6] = {d.h->currentSeq, d.h->minSeq, d.h->localSeq, length_local(), nsegs, d.h->nleaf};
+        put_bytes(o, cap, &n, hdr, sizeof(hdr));
+        const uint16_t* base = arena_base(d.h->arenaSide);
+        for (int32_t t = 0; t < T; t++) {
+            int32_t s = slot_at(t);
+            if (s < 0) continue;
+            uint8_t fl = d.flags[s];
+            bool rem = d.rseq[s] != NOREM;
+            int nov = 0;
+            while (nov < NOVL && ((d.ovl[s] >> (8 * nov)) & 0xFF)) nov++;
+            int np = 0;
+            if (fl & RF_PROPS)
+                for (int k = 0; k < NKEYS; k++)
+                    if (d.pv[s * NKEYS + k]) np++;
+            uint8_t b4[4] = {(uint8_t)((fl & RF_MARKER) ? MT_SEG_MARKER : MT_SEG_TEXT),
+                             (uint8_t)(((fl & RF_PROPS) ? MT_DF_HAS_PROPS : 0) | (rem ? MT_DF_REMOVED : 0) |
+                                       ((fl & RF_LSEQ) ? MT_DF_LSEQ : 0) | ((fl & RF_LRSEQ) ? MT_DF_LRSEQ : 0)),
+                             (uint8_t)nov, d.ng[s]};
+            put_bytes(o, cap, &n, b4, 4);
+            int32_t f[8] = {d.len[s],
+                            d.seq[s],
+                            long_of(d.cli[s]),
+                            rem ? d.rseq[s] : 0,
+                            rem ? long_of(d.rcli[s]) : 0,
+                            (fl & RF_LSEQ) ? d.lseq[s] : 0,
+                            (fl & RF_LRSEQ) ? d.lrseq[s] : 0,
+                            t >> 3};
+            put_bytes(o, cap, &n, f, sizeof(f));
+            for (int k = 0; k < nov; k++) {
+                int32_t lo = long_of((uint8_t)(((d.ovl[s] >> (8 * k)) & 0xFF) - 1));
+                put_bytes(o, cap, &n, &lo, 4);
+            }
+            uint16_t h2[2] = {(uint16_t)np, (uint16_t)((fl & RF_MARKER) ? d.toff[s] : 0)};
+            put_bytes(o, cap, &n, h2, 4);
+            /* props sorted by global key id */
+            int32_t last = -1;
+            for (int q = 0; q < np; q++) {
+                int32_t best = -1, bk = 0x7fffffff;
+                for (int k = 0; k < NKEYS; k++) {
+                    int32_t key = d.h->keys[k];
+                    if (d.pv[s * NKEYS + k] && key > last && key < bk) {
+                        bk = key;
+                        best = k;
+                    }
+                }
+                uint16_t kv2[2] = {(uint16_t)bk, d.pv[s * NKEYS + best]};
+                put_bytes(o, cap, &n, kv2, 4);
+                last = bk;
+            }
+            if (!(fl & RF_MARKER)) put_bytes(o, cap, &n, base + d.toff[s], 2 * (int64_t)d.len[s]);
+        }
+        return n;
+    }
+    MT_HD static uint64_t fnv(const uint8_t* p, int64_t n) {
+        uint64_t h = MT_FNV_OFFSET;
+        for (int64_t i = 0; i < n; i++) {
+            h ^= p[i];
+            h *= MT_FNV_PRIME;
+        }
+        return h;
+    }
+
+    MT_HD void replay(const Pools& p) {
+        for (int64_t i = 0; i < p.nops; i++) {
+            apply(p.ops[i], p);
+            if (d.h->err) break;
+        }
+    }
+};
+
+} /* namespace mt */

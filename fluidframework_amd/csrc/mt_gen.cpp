@@ -1,0 +1,345 @@
+/*
+ * mt_gen.cpp — deterministic synthetic op-log generator (BASELINE.md "Synthetic inputs").
+ *
+ * Produces, per document, ONE replica's arrival-ordered event stream in the packed format of
+ * include/mt_oplog.h. Positions must be valid in the perspective (refSeq, clientId) of the
+ * client that issues each op, so the generator drives a model replica — the serial host build
+ * of the engine's own replay core (mt_core.h) — through exactly the events it emits, and draws
+ * every position from that replica's length under the issuing perspective (getLength,
+ * mergeTree.ts:1610). Per-doc PRNG: xoshiro256** seeded with splitmix64(seed_base + doc).
+ *
+ * Workloads (configs in BASELINE.json):
+ *   MTG_OBSERVER  (config 2): clients 1..n-1 edit, the replica (long id 0) only observes;
+ *                  refSeq = MSN = seq - 1.
+ *   MTG_LAGGED    (config 3): replica = long id 1 with local edits acked up to ack_lag later;
+ *                  remote refSeq lag U{0..max_lag}; MSN = min over clients' last refSeq.
+ * Both take an op mix, insert/remove length ranges and optional coalescing defeaters
+ * (distinct insert props, trailing newlines) used by the large-doc config.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/mt_oplog.h"
+#include "mt_core.h"
+#include "mt_gen.h"
+#include "mt_store.h"
+#include "mt_wave.h"
+
+using namespace mt;
+
+/* ---- PRNG ------------------------------------------------------------------------------- */
+static uint64_t splitmix64(uint64_t* x) {
+    uint64_t z = (*x += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+typedef struct {
+    uint64_t s[4];
+} rng_t;
+static inline uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+static uint64_t next64(rng_t* r) { /* xoshiro256** */
+    uint64_t res = rotl(r->s[1] * 5, 7) * 9;
+    uint64_t t = r->s[1] << 17;
+    r->s[2] ^= r->s[0];
+    r->s[3] ^= r->s[1];
+    r->s[1] ^= r->s[2];
+    r->s[0] ^= r->s[3];
+    r->s[2] ^= t;
+    r->s[3] = rotl(r->s[3], 45);
+    return res;
+}
+static void seed(rng_t* r, uint64_t s) {
+    uint64_t x = s;
+    for (int i = 0; i < 4; i++) r->s[i] = splitmix64(&x);
+}
+/* uniform integer in [lo, hi] */
+static int32_t uni(rng_t* r, int32_t lo, int32_t hi) {
+    if (hi <= lo) return lo;
+    uint64_t span = (uint64_t)(hi - lo) + 1;
+    return lo + (int32_t)(next64(r) % span);
+}
+
+/* ---- model replica ---------------------------------------------------------------------- */
+struct Model {
+    Cols c;
+    Caps k;
+    uint8_t* mem;
+    Replica<WaveHost>* r;
+    const mt_props_rec* props;
+    const mt_kv* kv;
+    const uint16_t* text;
+    bool ok;
+};
+static void model_init(Model* m, const mtg_params* P, int32_t local_long) {
+    m->k = Caps{P->model_ncap > 0 ? P->model_ncap : 2048, 0, 0, 0, 0, 64};
+    m->k.hcap = m->k.ncap * 2;
+    m->k.acap = P->model_acap > 0 ? P->model_acap : (1 << 17);
+    m->k.mcap = 1 << 14;
+    m->k.gcap = 4096;
+    size_t bytes = layout(m->c, m->k, 1, nullptr);
+    m->mem = (uint8_t*)calloc(1, bytes);
+    m->ok = m->mem != nullptr;
+    if (!m->ok) return;
+    layout(m->c, m->k, 1, m->mem);
+    m->r = new Replica<WaveHost>(doc_view(m->c, m->k, 0), WaveHost());
+    m->r->init();
+    m->r->start_collab(local_long, 0, 0);
+}
+static void model_free(Model* m) {
+    delete m->r;
+    free(m->mem);
+}
+/* length under the perspective of long client `cl` at refSeq (lp: the replica's local view) */
+static int32_t m_length(Model* m, int32_t refSeq, int32_t cl, int lp) {
+    if (lp) return m->r->length_local();
+    int32_t sh = m->r->short_of(cl);
+    if (sh < 0) sh = 0x7fff;
+    return m->r->length(refSeq, sh);
+}
+static void m_apply(Model* m, const mt_op_rec* e) {
+    Pools p = {e, 1, m->text, m->props, m->kv};
+    m->r->apply(*e, p);
+}
+
+/* ---- event emission ---------------------------------------------------------------------- */
+typedef struct {
+    mt_op_rec* ops;
+    int64_t nops, cap;
+    uint16_t* text;
+    int64_t ntext, tcap;
+    int overflow;
+} Out;
+
+static mt_op_rec* emit(Out* o) {
+    if (o->nops >= o->cap) {
+        o->overflow = 1;
+        return NULL;
+    }
+    mt_op_rec* r = &o->ops[o->nops++];
+    memset(r, 0, sizeof(*r));
+    return r;
+}
+static const char ALNUM[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789";
+
+/* fixed props table: annotate {key in b,i,u,c : value in 0,1,2,3,null} -> records 1..20;
+ * insert props {s: v} for v in 0..4095 -> records 21..4116 (see mtg_props_table). */
+#define ANN_RECORDS 20
+static int ann_props(rng_t* r) { return 1 + uni(r, 0, ANN_RECORDS - 1); }
+
+/* Draw an op valid for perspective (refSeq, client); kind forced to insert on an empty view. */
+static void gen_op(const mtg_params* P, rng_t* r, Model* m, int32_t refSeq, int32_t client, int lp, Out* o,
+                   mt_op_rec* e, int insert_index) {
+    int32_t len = m_length(m, refSeq, client, lp);
+    int roll = uni(r, 0, 99);
+    int kind;
+    if (len == 0 || roll < P->pct_insert)
+        kind = MT_OP_INSERT;
+    else if (roll < P->pct_insert + P->pct_remove)
+        kind = MT_OP_REMOVE;
+    else
+        kind = MT_OP_ANNOTATE;
+    e->kind = (uint8_t)kind;
+    if (kind == MT_OP_INSERT) {
+        e->pos1 = uni(r, 0, len);
+        int tl = uni(r, 1, P->max_ins_len);
+        if (o->ntext + tl > o->tcap) {
+            o->overflow = 1;
+            tl = 0;
+        }
+        e->text_off = (uint32_t)o->ntext;
+        for (int i = 0; i < tl; i++) o->text[o->ntext++] = (uint16_t)ALNUM[uni(r, 0, 61)];
+        if (tl && P->newline_pct && uni(r, 0, 99) < P->newline_pct) o->text[o->ntext - 1] = '\n';
+        e->text_len = (uint16_t)tl;
+        if (P->distinct_props) e->props = (uint16_t)(1 + ANN_RECORDS + (insert_index % 4096));
+    } else {
+        e->pos1 = uni(r, 0, len - 1);
+        int span = uni(r, 1, P->max_rem_len);
+        e->pos2 = e->pos1 + span > len ? len : e->pos1 + span;
+        if (kind == MT_OP_ANNOTATE) e->props = (uint16_t)ann_props(r);
+    }
+}
+
+typedef struct {
+    mt_op_rec op;
+    int32_t target;
+} Pending;
+
+static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {
+    rng_t r;
+    seed(&r, P->seed_base + (uint64_t)doc);
+    int nclients = P->nclients < 2 ? 2 : P->nclients;
+    if (nclients > 32) nclients = 32;
+    int me = P->mode == MTG_OBSERVER ? 0 : 1;
+    Model m;
+    model_init(&m, P, me);
+    if (!m.ok) {
+        o->overflow = 1;
+        return;
+    }
+    m.props = props;
+    m.kv = kv;
+    m.text = o->text;
+    int32_t lastRef[32] = {0};
+    int insert_index = 0;
+    int32_t seq = 0;
+    if (P->mode == MTG_OBSERVER) {
+        while (seq < P->ops_per_doc && !o->overflow && !m.r->d.h->err) {
+            int client = uni(&r, 1, nclients - 1);
+            int32_t ref = seq; /* refSeq = seq - 1 for the op sequenced now */
+            mt_op_rec* e = emit(o);
+            if (!e) break;
+            gen_op(P, &r, &m, ref, client, 0, o, e, insert_index);
+            seq++;
+            e->client = (uint16_t)client;
+            e->seq = seq;
+            e->ref_seq = ref;
+            e->min_seq = seq - 1;
+            if (e->kind == MT_OP_INSERT) insert_index++;
+            m_apply(&m, e);
+        }
+    } else { /* MTG_LAGGED */
+        Pending* q = (Pending*)malloc(sizeof(Pending) * (P->ops_per_doc + 16));
+        int qh = 0, qn = 0;
+        int32_t lastTarget = 0, msn = 0;
+        while (seq < P->ops_per_doc && !o->overflow && !m.r->d.h->err) {
+            int32_t cur = m.r->d.h->currentSeq;
+            /* 1. a local edit, made against the local view (client.ts:164-211) */
+            if (P->local_pct && uni(&r, 0, 99) < P->local_pct && qn < 4000) {
+                mt_op_rec* e = emit(o);
+                if (!e) break;
+                gen_op(P, &r, &m, cur, me, 1, o, e, insert_index);
+                if (e->kind == MT_OP_INSERT && e->text_len == 0) {
+                    o->nops--;
+                    continue;
+                }
+                e->kind |= MT_OPF_LOCAL;
+                e->client = (uint16_t)me;
+                e->seq = -1;
+                e->ref_seq = cur;
+                if ((e->kind & MT_OP_KIND_MASK) == MT_OP_INSERT) insert_index++;
+                m_apply(&m, e);
+                int32_t target = cur + uni(&r, 1, P->ack_lag > 0 ? P->ack_lag : 1);
+                if (target <= lastTarget) target = lastTarget + 1;
+                lastTarget = target;
+                Pending pe;
+                pe.op = *e;
+                pe.op.kind &= (uint8_t)~MT_OPF_LOCAL;
+                pe.op.ref_seq = cur;
+                pe.target = target;
+                q[qh + qn++] = pe;
+                continue;
+            }
+            /* 2. the next sequenced message: our own op (ack) when due, else a remote op */
+            seq++;
+            mt_op_rec* e = emit(o);
+            if (!e) break;
+            if (qn > 0 && q[qh].target <= seq) {
+                Pending pe = q[qh++];
+                qn--;
+                if (pe.op.ref_seq > lastRef[me]) lastRef[me] = pe.op.ref_seq;
+                int32_t mn = INT32_MAX;
+                for (int k = 0; k < nclients; k++)
+                    if (lastRef[k] < mn) mn = lastRef[k];
+                if (mn > msn) msn = mn;
+                *e = pe.op;
+                e->seq = seq;
+                e->min_seq = msn;
+            } else {
+                int client = uni(&r, 0, nclients - 2);
+                if (client >= me) client++;
+                int32_t ref = cur - uni(&r, 0, P->max_lag);
+                if (ref < lastRef[client]) ref = lastRef[client];
+                if (ref < msn) ref = msn;
+                lastRef[client] = ref;
+                int32_t mn = INT32_MAX;
+                for (int k = 0; k < nclients; k++)
+                    if (lastRef[k] < mn) mn = lastRef[k];
+                if (mn > msn) msn = mn;
+                gen_op(P, &r, &m, ref, client, 0, o, e, insert_index);
+                e->client = (uint16_t)client;
+                e->seq = seq;
+                e->ref_seq = ref;
+                e->min_seq = msn;
+                if (e->kind == MT_OP_INSERT) insert_index++;
+            }
+            m_apply(&m, e);
+        }
+        free(q);
+    }
+    if (m.r->d.h->err) o->overflow = 2;
+    model_free(&m);
+}
+
+/* ---- batch API --------------------------------------------------------------------------- */
+typedef struct {
+    const mtg_params* P;
+    int64_t doc_base, ndocs, op_stride, text_stride;
+    int tid, threads;
+    mt_op_rec* ops;
+    int64_t* nops;
+    uint16_t* text;
+    int64_t* ntext;
+    int* status;
+    const mt_props_rec* props;
+    const mt_kv* kv;
+} Job;
+static void* worker(void* p) {
+    Job* j = (Job*)p;
+    for (int64_t d = j->tid; d < j->ndocs; d += j->threads) {
+        Out o = {j->ops + d * j->op_stride, 0, j->op_stride, j->text + d * j->text_stride, 0, j->text_stride, 0};
+        gen_doc(j->P, j->doc_base + d, &o, j->props, j->kv);
+        j->nops[d] = o.nops;
+        j->ntext[d] = o.ntext;
+        if (o.overflow) *j->status = o.overflow == 2 ? -2 : -1;
+    }
+    return NULL;
+}
+extern "C" int mtg_generate(const mtg_params* P, int64_t doc_base, int64_t ndocs, int64_t op_stride,
+                            int64_t text_stride, mt_op_rec* ops, int64_t* nops, uint16_t* text, int64_t* ntext,
+                            int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    static mt_props_rec props[20 + 4096];
+    static mt_kv kv[20 + 4096];
+    mtg_props_table(props, kv);
+    pthread_t th[256];
+    Job jobs[256];
+    int status = 0;
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = Job{P, doc_base, ndocs, op_stride, text_stride, t, threads, ops, nops, text, ntext, &status,
+                      props, kv};
+        pthread_create(&th[t], NULL, worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    return status;
+}
+
+/* The fixed props table every generated doc shares: records 1..20 annotate one key of
+ * {b,i,u,c} (key ids 1..4) with value ids for JSON 0,1,2,3 (value id = v + 1; "0" is falsy)
+ * or null; records 21..4116 are insert props {s: v}, key id 5, v in 0..4095. */
+extern "C" int mtg_props_table(mt_props_rec* props, mt_kv* kv) {
+    int n = 0;
+    for (int k = 0; k < 4; k++)
+        for (int v = 0; v < 5; v++) {
+            props[n].kv_off = (uint32_t)n;
+            props[n].nkv = 1;
+            props[n].combining = MT_COMBINE_NONE;
+            props[n]._pad = 0;
+            kv[n].key = (uint16_t)(k + 1);
+            kv[n].value = v == 4 ? 0 : (uint16_t)((v + 1) | (v == 0 ? MT_VALUE_FALSY : 0));
+            n++;
+        }
+    for (int v = 0; v < 4096; v++) {
+        props[n].kv_off = (uint32_t)n;
+        props[n].nkv = 1;
+        props[n].combining = MT_COMBINE_NONE;
+        props[n]._pad = 0;
+        kv[n].key = 5;
+        kv[n].value = (uint16_t)((v + 1) | (v == 0 ? MT_VALUE_FALSY : 0));
+        n++;
+    }
+    return n;
+}

@@ -1,0 +1,125 @@
+"""Synthetic workloads for BASELINE.json's configs (native generator ``csrc/mt_gen.c``)."""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import native
+from . import oplog as ol
+
+MTG_OBSERVER, MTG_LAGGED = 2, 3
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "mode", "ops_per_doc", "nclients", "max_lag", "local_pct", "ack_lag", "pct_insert",
+        "pct_remove", "max_ins_len", "max_rem_len", "distinct_props", "newline_pct", "model_ncap",
+        "model_acap")] + [
+        ("seed_base", ctypes.c_uint64)]
+
+
+@dataclass
+class Workload:
+    mode: int
+    ops_per_doc: int
+    nclients: int = 8
+    max_lag: int = 0
+    local_pct: int = 0
+    ack_lag: int = 64
+    pct_insert: int = 60
+    pct_remove: int = 30
+    max_ins_len: int = 8
+    max_rem_len: int = 16
+    distinct_props: int = 0
+    newline_pct: int = 0
+    model_ncap: int = 0
+    model_acap: int = 0
+    seed_base: int = 0x5EED0000
+
+
+# BASELINE.json configs (BASELINE.md "CPU-baseline plan" table)
+def config2(ops_per_doc: int = 10_000) -> Workload:
+    """4,096 docs x 10k ops, observer replica, refSeq = MSN = seq - 1, 60/30/10."""
+    return Workload(MTG_OBSERVER, ops_per_doc)
+
+
+def config3(ops_per_doc: int = 4_096) -> Workload:
+    """65,536 docs, 8 clients, lag <= 64, local-pending replica (~1/8 local edits)."""
+    return Workload(MTG_LAGGED, ops_per_doc, max_lag=64, local_pct=12, ack_lag=64)
+
+
+def config4(ops_per_doc: int = 1_000_000) -> Workload:
+    """256 large docs, lag 64, 70/25/5, coalescing defeated by distinct props + newlines."""
+    return Workload(MTG_LAGGED, ops_per_doc, max_lag=64, local_pct=0, pct_insert=70, pct_remove=25,
+                    distinct_props=1, newline_pct=25, model_ncap=32000, model_acap=1 << 22)
+
+
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        L = ctypes.CDLL(native.build_gen())
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        L.mtg_generate.argtypes = [ctypes.POINTER(_Params), i64, i64, i64, i64, vp, vp, vp, vp, ctypes.c_int]
+        L.mtg_props_table.argtypes = [vp, vp]
+        _LIB = L
+    return _LIB
+
+
+def generator_interner() -> ol.Interner:
+    """The key/value ids mtg_props_table uses: keys b,i,u,c,s = 1..5; value id v+1 = JSON v."""
+    it = ol.Interner()
+    for k in ("b", "i", "u", "c", "s"):
+        it.key(k)
+    for v in range(4096):
+        it.value(v)
+    return it
+
+
+def props_table():
+    props = np.zeros(20 + 4096, ol.PROPS_DTYPE)
+    kv = np.zeros(20 + 4096, ol.KV_DTYPE)
+    n = _lib().mtg_props_table(props.ctypes.data, kv.ctypes.data)
+    assert n == len(props)
+    return props, kv
+
+
+def generate(w: Workload, ndocs: int, doc_base: int = 0, threads: int = 0) -> ol.Batch:
+    """Generate `ndocs` document logs (docs doc_base .. doc_base+ndocs-1) as one Batch."""
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    p = _Params(**{k: int(getattr(w, k)) for k, _ in _Params._fields_})
+    op_stride = int(w.ops_per_doc * (1 + w.local_pct / 50.0)) + 16
+    text_stride = op_stride * w.max_ins_len
+    ops = np.zeros(ndocs * op_stride, ol.OP_DTYPE)
+    text = np.zeros(ndocs * text_stride, "<u2")
+    nops = np.zeros(ndocs, np.int64)
+    ntext = np.zeros(ndocs, np.int64)
+    rc = _lib().mtg_generate(ctypes.byref(p), doc_base, ndocs, op_stride, text_stride, ops.ctypes.data,
+                             nops.ctypes.data, text.ctypes.data, ntext.ctypes.data, threads)
+    if rc == -1:
+        raise RuntimeError("generator buffer overflow")
+    if rc == -2:
+        raise RuntimeError("generator model replica reported an error (capacity)")
+    # compact the fixed-stride buffers
+    op_off = np.zeros(ndocs + 1, np.int64)
+    op_off[1:] = np.cumsum(nops)
+    text_off = np.zeros(ndocs + 1, np.int64)
+    text_off[1:] = np.cumsum(ntext)
+    opi = (np.arange(ndocs, dtype=np.int64)[:, None] * op_stride + np.arange(op_stride)[None, :])
+    mask = np.arange(op_stride)[None, :] < nops[:, None]
+    ops_c = ops[opi[mask]]
+    ti = (np.arange(ndocs, dtype=np.int64)[:, None] * text_stride + np.arange(text_stride)[None, :])
+    tmask = np.arange(text_stride)[None, :] < ntext[:, None]
+    text_c = text[ti[tmask]]
+    if len(text_c) == 0:
+        text_c = np.zeros(1, "<u2")
+    props, kv = props_table()
+    zeros = np.zeros(ndocs + 1, np.int64)
+    local = np.full(ndocs, 0 if w.mode == MTG_OBSERVER else 1, np.int32)
+    return ol.Batch(ops_c, op_off, text_c, text_off, props, zeros, kv, zeros.copy(), local)

@@ -1,0 +1,47 @@
+"""Locating and (re)building the package's native libraries in-tree.
+
+Built artefacts live in ``fluidframework_amd/build/`` (git-ignored, shipped to the GPU box with
+the repo snapshot). Nothing here falls back to Python: a missing library raises.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+BUILD = os.path.join(PKG, "build")
+CSRC = os.path.join(PKG, "csrc")
+
+
+def lib_path(name: str) -> str:
+    return os.path.join(BUILD, name)
+
+
+def _stale(out, srcs):
+    return not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(s) for s in srcs)
+
+
+CORE_HDRS = ("mt_core.h", "mt_wave.h", "mt_store.h")
+
+
+def build_gen() -> str:
+    """Synthetic workload generator (host code; its model replica is the host core build)."""
+    out = lib_path("libmtgen.so")
+    srcs = [os.path.join(CSRC, f) for f in ("mt_gen.cpp", "mt_gen.h") + CORE_HDRS]
+    if _stale(out, srcs):
+        os.makedirs(BUILD, exist_ok=True)
+        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", out, srcs[0], "-lpthread"],
+                       check=True)
+    return out
+
+
+def build_core_host() -> str:
+    """Serial host build of the replay core (generator model + CPU spec tests; not the
+    product compute path, which is the HIP kernel in libmtreplay.so)."""
+    out = lib_path("libmtcore_host.so")
+    srcs = [os.path.join(CSRC, f) for f in ("mt_core_host.cpp", "mt_core.h", "mt_wave.h", "mt_store.h")]
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(s) for s in srcs):
+        os.makedirs(BUILD, exist_ok=True)
+        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", out, srcs[0]], check=True)
+    return out

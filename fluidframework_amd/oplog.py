@@ -161,11 +161,13 @@ class Batch:
         return int(self.op_off[-1])
 
     def doc(self, d: int):
+        """(ops, text, props, kv) of document d. Pools are returned as suffixes starting at the
+        document's offset: documents may share one pool (offsets need not increase)."""
         return (
             self.ops[self.op_off[d]: self.op_off[d + 1]],
-            self.text[self.text_off[d]: max(self.text_off[d + 1], self.text_off[d] + 1)],
-            self.props[self.props_off[d]: max(self.props_off[d + 1], self.props_off[d] + 1)],
-            self.kv[self.kv_off[d]: max(self.kv_off[d + 1], self.kv_off[d] + 1)],
+            self.text[self.text_off[d]:],
+            self.props[self.props_off[d]:],
+            self.kv[self.kv_off[d]:],
         )
 
     def subset(self, docs: Sequence[int]) -> "Batch":

@@ -1,0 +1,108 @@
+"""ctypes wrapper of the serial host build of the replay core (libmtcore_host.so) — used by the
+CPU spec tests to compare the engine's algorithm with the oracle without a GPU."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from fluidframework_amd import native
+from fluidframework_amd import oplog as ol
+
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        path = native.build_core_host()
+        L = ctypes.CDLL(path)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.mth_create.restype = vp
+        L.mth_create.argtypes = [i64, vp]
+        L.mth_destroy.argtypes = [vp]
+        L.mth_start_collab.argtypes = [vp, i64, i32, i32, i32]
+        L.mth_apply.argtypes = [vp, i64, vp, vp, vp, vp]
+        L.mth_replay.argtypes = [vp, i64, vp, i64, vp, vp, vp]
+        L.mth_error.argtypes = [vp, i64]
+        L.mth_error_op.argtypes = [vp, i64]
+        L.mth_length.argtypes = [vp, i64, i32, i32]
+        L.mth_length_local.argtypes = [vp, i64]
+        L.mth_text.argtypes = [vp, i64, i32, i32, vp, i64]
+        L.mth_text.restype = i64
+        L.mth_dump.argtypes = [vp, i64, vp, i64]
+        L.mth_dump.restype = i64
+        L.mth_digest.argtypes = [vp, i64]
+        L.mth_digest.restype = ctypes.c_uint64
+        L.mth_stats.argtypes = [vp, i64, vp]
+        _L = L
+    return _L
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+DEFAULT_CAPS = (512, 1024, 1 << 16, 4096, 1024, 64)
+
+
+class HostStore:
+    def __init__(self, ndocs: int, caps=DEFAULT_CAPS):
+        self.L = lib()
+        self.caps = np.asarray(caps, np.int32)
+        self.h = self.L.mth_create(ndocs, _p(self.caps))
+        if not self.h:
+            raise RuntimeError("mth_create failed")
+        self.ndocs = ndocs
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.mth_destroy(self.h)
+            self.h = None
+
+    def start_collab(self, doc, long_id, min_seq=0, cur_seq=0):
+        self.L.mth_start_collab(self.h, doc, long_id, min_seq, cur_seq)
+
+    def replay(self, doc, ops, text, props, kv):
+        ops = np.ascontiguousarray(ops)
+        if len(ops) == 0:
+            return self.error(doc)
+        return self.L.mth_replay(self.h, doc, _p(ops), len(ops), _p(text), _p(props), _p(kv))
+
+    def error(self, doc):
+        return self.L.mth_error(self.h, doc)
+
+    def dump(self, doc) -> bytes:
+        n = self.L.mth_dump(self.h, doc, None, 0)
+        buf = np.zeros(n, np.uint8)
+        self.L.mth_dump(self.h, doc, _p(buf), n)
+        return buf.tobytes()
+
+    def digest(self, doc) -> int:
+        return int(self.L.mth_digest(self.h, doc))
+
+    def text(self, doc, ref_seq=0, long_client=-1) -> str:
+        n = self.L.mth_text(self.h, doc, ref_seq, long_client, None, 0)
+        buf = np.zeros(max(n, 1), "<u2")
+        self.L.mth_text(self.h, doc, ref_seq, long_client, _p(buf), n)
+        return buf[:n].tobytes().decode("utf-16-le")
+
+    def stats(self, doc):
+        out = np.zeros(8, np.int32)
+        self.L.mth_stats(self.h, doc, _p(out))
+        return dict(zip(("nleaf", "hw_slots", "hw_heap", "heap", "mem", "arena_top", "nodes", "ops"), out.tolist()))
+
+
+def replay_batch(batch: ol.Batch, caps=DEFAULT_CAPS):
+    """Replay every document of a batch on the host core; returns (digests, errors, store)."""
+    st = HostStore(batch.ndocs, caps)
+    dig = np.zeros(batch.ndocs, np.uint64)
+    err = np.zeros(batch.ndocs, np.int32)
+    for d in range(batch.ndocs):
+        st.start_collab(d, int(batch.local_long_id[d]))
+        ops, text, props, kv = batch.doc(d)
+        err[d] = st.replay(d, ops, text, props, kv)
+        dig[d] = st.digest(d)
+    return dig, err, st
