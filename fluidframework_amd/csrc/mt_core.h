@@ -42,7 +42,6 @@ enum : int32_t {
     MAXN = 8,          /* MaxNodesInBlock (mergeTree.ts:333) */
     GRANULARITY = 256, /* TextSegmentGranularity (mergeTree.ts:1093) */
     NKEYS = 8,         /* property key slots per document */
-    NGRP = 4,          /* segment-group FIFO depth per row */
     NOVL = 8,          /* removedClientOverlap entries per row */
 };
 enum : uint8_t { LOCAL_CLIENT = 0xFF }; /* short id of LocalClientId (-1) */
@@ -82,6 +81,9 @@ struct DocHdr {
     int32_t heapN, memN, gqHead, gqN;
     int32_t arenaTop, arenaSide, err, errOp;
     int32_t nkeys, opsDone, hwSlots, hwHeap;
+    int32_t nrows, seqOps;      /* rows in the table (tombstones included); sequenced msgs applied */
+    int64_t sumR, sumW;         /* roofline counters: sum over sequenced msgs of rows before the op,
+                                   rows written by the op (BASELINE.md A(op) = 16 R + 32 W) */
     uint16_t keys[NKEYS];
 };
 
@@ -94,7 +96,6 @@ struct Cols {
     uint64_t* ovl;
     uint16_t* pv; /* NKEYS per row */
     uint8_t* pk;  /* NKEYS per row: pendingKeyUpdateCount */
-    int32_t* grp; /* NGRP per row: segmentGroups FIFO (group ids) */
     /* nodes: ncap per doc */
     int16_t *nparent, *kids, *lorder, *lpos;
     int8_t *nchild, *nlevel, *nscour;
@@ -121,7 +122,6 @@ struct Doc {
     uint64_t* ovl;
     uint16_t* pv;
     uint8_t* pk;
-    int32_t* grp;
     int16_t *nparent, *kids, *lorder, *lpos;
     int8_t *nchild, *nlevel, *nscour;
     uint32_t* hsid;
@@ -153,7 +153,6 @@ MT_HD inline Doc doc_view(const Cols& c, const Caps& k, int64_t d) {
     v.ovl = c.ovl + d * rs;
     v.pv = c.pv + d * rs * NKEYS;
     v.pk = c.pk + d * rs * NKEYS;
-    v.grp = c.grp + d * rs * NGRP;
     v.nparent = c.nparent + d * ns;
     v.kids = c.kids + d * ns * MAXN;
     v.lorder = c.lorder + d * ns;
@@ -263,6 +262,10 @@ struct Replica {
         h->opsDone = 0;
         h->hwSlots = 0;
         h->hwHeap = 0;
+        h->nrows = 0;
+        h->seqOps = 0;
+        h->sumR = 0;
+        h->sumW = 0;
         w.sync();
     }
 
@@ -349,7 +352,6 @@ struct Replica {
             d.pv[b * NKEYS + k] = d.pv[a * NKEYS + k];
             d.pk[b * NKEYS + k] = d.pk[a * NKEYS + k];
         }
-        for (int k = 0; k < NGRP; k++) d.grp[b * NGRP + k] = d.grp[a * NGRP + k];
     }
 
     /* ---- perspective scans ------------------------------------------------------------- */
@@ -422,38 +424,42 @@ struct Replica {
     /* split (mergeTree.ts:2509-2522) of a full node (8 children) into 4 + 4; the new node is
      * inserted after it in its parent, recursively; root split -> updateRoot (1909-1920).
      * Returns the new node. */
-    MT_HD int32_t split_node(int32_t n) {
-        int8_t lvl = d.nlevel[n];
-        int32_t nn = alloc_node(lvl);
-        if (nn < 0) return -1;
-        d.nscour[nn] = -1;
-        if (lvl == 0) {
-            for (int32_t i = 0; i < 4; i++) copy_row(nn * MAXN + i, n * MAXN + 4 + i);
-        } else {
-            for (int32_t i = 0; i < 4; i++) {
-                int32_t c = d.kids[n * MAXN + 4 + i];
-                d.kids[nn * MAXN + i] = (int16_t)c;
-                d.nparent[c] = (int16_t)nn;
+    MT_HD int32_t split_node(int32_t n0) {
+        int32_t first = -1;
+        int32_t n = n0;
+        for (;;) { /* iterative: a split may overflow the parent, up to the root */
+            int8_t lvl = d.nlevel[n];
+            int32_t nn = alloc_node(lvl);
+            if (nn < 0) return -1;
+            if (first < 0) first = nn;
+            if (lvl == 0) {
+                for (int32_t i = 0; i < 4; i++) copy_row(nn * MAXN + i, n * MAXN + 4 + i);
+            } else {
+                for (int32_t i = 0; i < 4; i++) {
+                    int32_t c = d.kids[n * MAXN + 4 + i];
+                    d.kids[nn * MAXN + i] = (int16_t)c;
+                    d.nparent[c] = (int16_t)nn;
+                }
             }
-        }
-        d.nchild[n] = 4;
-        d.nchild[nn] = 4;
-        if (lvl == 0) lorder_insert_after(n, nn);
-        int32_t p = d.nparent[n];
-        if (p < 0) {
-            int32_t r = alloc_node((int8_t)(lvl + 1));
-            if (r < 0) return -1;
-            d.kids[r * MAXN + 0] = (int16_t)n;
-            d.kids[r * MAXN + 1] = (int16_t)nn;
-            d.nchild[r] = 2;
-            d.nparent[n] = (int16_t)r;
-            d.nparent[nn] = (int16_t)r;
-            d.h->root = r;
-        } else {
+            d.nchild[n] = 4;
+            d.nchild[nn] = 4;
+            if (lvl == 0) lorder_insert_after(n, nn);
+            int32_t p = d.nparent[n];
+            if (p < 0) {
+                int32_t r = alloc_node((int8_t)(lvl + 1));
+                if (r < 0) return -1;
+                d.kids[r * MAXN + 0] = (int16_t)n;
+                d.kids[r * MAXN + 1] = (int16_t)nn;
+                d.nchild[r] = 2;
+                d.nparent[n] = (int16_t)r;
+                d.nparent[nn] = (int16_t)r;
+                d.h->root = r;
+                return first;
+            }
             node_insert_child(p, child_index(p, n) + 1, nn);
-            if (d.nchild[p] >= MAXN) split_node(p);
+            if (d.nchild[p] < MAXN) return first;
+            n = p;
         }
-        return nn;
     }
     /* Make room at child index j of leaf n; returns slot for the new row (after any split). */
     MT_HD int32_t leaf_insert_slot(int32_t n, int32_t j) {
@@ -530,10 +536,18 @@ struct Replica {
         d.toff[rs] = d.toff[ls] + (uint32_t)off;
         d.len[ls] = off;
         d.sid[rs] = (uint32_t)d.h->nextSid++;
+        d.h->nrows++;
+        d.h->sumW += 2;
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
-         * same groups, appended at the end of each group's segment list */
-        int32_t ng = d.ng[ls];
-        for (int32_t g = 0; g < ng; g++) mem_append(d.grp[ls * NGRP + g], d.sid[rs]);
+         * same pending groups (in the row's FIFO order = log order), appended at the end of each
+         * group's segment list */
+        if (d.ng[ls]) {
+            int32_t head = d.h->gqN ? d.gq[d.h->gqHead % d.caps.gcap] : 0x7fffffff;
+            uint32_t lsid = d.sid[ls];
+            int32_t m0 = d.h->memN;
+            for (int32_t i = 0; i < m0; i++)
+                if (d.msid[i] == lsid && d.mgid[i] >= head) mem_append(d.mgid[i], d.sid[rs]);
+        }
         return ls;
     }
 
@@ -568,11 +582,10 @@ struct Replica {
     /* SegmentGroupCollection.enqueue (segmentGroupCollection.ts:28-31) */
     MT_HD void row_enqueue_group(int32_t s, int32_t gid) {
         int32_t ng = d.ng[s];
-        if (ng >= NGRP) {
+        if (ng >= 255) {
             fail(E_CAPACITY);
             return;
         }
-        d.grp[s * NGRP + ng] = gid;
         d.ng[s] = (uint8_t)(ng + 1);
         mem_append(gid, d.sid[s]);
     }
@@ -789,11 +802,14 @@ struct Replica {
                 prev = -1;
             }
         }
+        d.h->nrows -= c - wpos;
         d.nchild[n] = (int8_t)wpos;
         return wpos;
     }
     /* pack (mergeTree.ts:1401-1453) of `block`'s parent */
-    MT_HD void pack(int32_t block) {
+    MT_HD void pack(int32_t block0) {
+      int32_t block = block0;
+      for (;;) { /* iterative: pack recurses upward while the parent underflows (1447-1452) */
         int32_t parent = d.nparent[block];
         int32_t pc = d.nchild[parent];
         int8_t lvl = d.nlevel[block];
@@ -884,7 +900,9 @@ struct Replica {
             }
             d.nchild[parent] = (int8_t)cc;
         }
-        if (d.nchild[parent] < MAXN / 2 && d.nparent[parent] >= 0) pack(parent);
+        if (!(d.nchild[parent] < MAXN / 2 && d.nparent[parent] >= 0)) return;
+        block = parent;
+      }
     }
     /* zamboniSegments (mergeTree.ts:1455-1511) */
     MT_HD void zamboni() {
@@ -1013,6 +1031,8 @@ struct Replica {
             d.prw[s] = 0;
             d.ovl[s] = 0;
             d.sid[s] = (uint32_t)d.h->nextSid++;
+            d.h->nrows++;
+            d.h->sumW++;
             if (marker) {
                 d.toff[s] = (uint32_t)op.pos2;
             } else {
@@ -1068,6 +1088,7 @@ struct Replica {
         int32_t localSeq = hasL ? ++d.h->localSeq : 0;
         bool created = false;
         map_range(start, end, refSeq, client, [&](int32_t s) {
+            d.h->sumW++;
             if (d.rseq[s] != NOREM) {
                 if (d.rseq[s] == UNASSIGNED_SEQ) {
                     d.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
@@ -1109,6 +1130,7 @@ struct Replica {
         bool created = false;
         bool collab = d.h->collaborating;
         map_range(start, end, refSeq, client, [&](int32_t s) {
+            d.h->sumW++;
             add_props(s, kv, nkv, rewrite, seq, collab);
             if (collab) {
                 if (seq == UNASSIGNED_SEQ)
@@ -1133,10 +1155,9 @@ struct Replica {
                     fail(E_ASSERT);
                     continue;
                 }
-                /* dequeue the row's head group; must be this group */
+                /* dequeue the row's head group (groups are acked in FIFO order, so it is this one) */
                 int32_t ng = d.ng[s];
-                if (ng < 1 || d.grp[s * NGRP] != gid) fail(E_ASSERT);
-                for (int32_t g = 1; g < ng; g++) d.grp[s * NGRP + g - 1] = d.grp[s * NGRP + g];
+                if (ng < 1) fail(E_ASSERT);
                 if (ng > 0) d.ng[s] = (uint8_t)(ng - 1);
                 if (kind == MT_OP_ANNOTATE) {
                     if (!(d.flags[s] & RF_PROPS)) fail(E_ASSERT);
@@ -1198,6 +1219,8 @@ struct Replica {
             return;
         }
         get_or_add_short(op.client);
+        d.h->seqOps++;
+        d.h->sumR += d.h->nrows;
         if (kind != MT_OP_NOOP) {
             if ((int32_t)op.client == d.h->localLong) {
                 ack(kind, kv, nkv, rw, op.seq);
@@ -1246,25 +1269,43 @@ struct Replica {
     }
 
     /* ---- canonical dump (include/mt_oplog.h) ------------------------------------------- */
-    MT_HD static void put_bytes(uint8_t* out, int64_t cap, int64_t* n, const void* src, int64_t k) {
-        if (out && *n + k <= cap) {
-            const uint8_t* p = (const uint8_t*)src;
-            for (int64_t i = 0; i < k; i++) out[*n + i] = p[i];
-        }
-        *n += k;
+    /* byte sink: writes into a buffer (if any) and/or folds FNV-1a-64 */
+    struct Sink {
+        uint8_t* out;
+        int64_t cap, n;
+        uint64_t h;
+        bool hash;
+    };
+    MT_HD static void put_bytes(Sink* k, const void* src, int64_t len) {
+        const uint8_t* p = (const uint8_t*)src;
+        if (k->out && k->n + len <= k->cap)
+            for (int64_t i = 0; i < len; i++) k->out[k->n + i] = p[i];
+        if (k->hash)
+            for (int64_t i = 0; i < len; i++) {
+                k->h ^= p[i];
+                k->h *= MT_FNV_PRIME;
+            }
+        k->n += len;
     }
     MT_HD int32_t long_of(uint8_t sh) const { return sh == LOCAL_CLIENT ? -1 : (int32_t)d.s2l[sh]; }
-    /* Single-lane (lane 0 writes) serial dump; returns the byte count. */
+    /* Serial dump (only lane 0 writes the buffer); returns the byte count. */
     MT_HD int64_t dump(uint8_t* out, int64_t cap) {
-        int64_t n = 0;
-        bool wr = w.lane() == 0;
-        uint8_t* o = wr ? out : 0;
+        Sink k = {w.lane() == 0 ? out : 0, cap, 0, MT_FNV_OFFSET, false};
+        dump_to(&k);
+        return k.n;
+    }
+    MT_HD uint64_t digest() {
+        Sink k = {0, 0, 0, MT_FNV_OFFSET, true};
+        dump_to(&k);
+        return k.h;
+    }
+    MT_HD void dump_to(Sink* o) {
         int32_t nsegs = 0;
         int32_t T = d.h->nleaf * MAXN;
         for (int32_t t = 0; t < T; t++)
             if (slot_at(t) >= 0) nsegs++;
         int32_t hdr[6] = {d.h->currentSeq, d.h->minSeq, d.h->localSeq, length_local(), nsegs, d.h->nleaf};
-        put_bytes(o, cap, &n, hdr, sizeof(hdr));
+        put_bytes(o, hdr, sizeof(hdr));
         const uint16_t* base = arena_base(d.h->arenaSide);
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
@@ -1281,7 +1322,7 @@ struct Replica {
                              (uint8_t)(((fl & RF_PROPS) ? MT_DF_HAS_PROPS : 0) | (rem ? MT_DF_REMOVED : 0) |
                                        ((fl & RF_LSEQ) ? MT_DF_LSEQ : 0) | ((fl & RF_LRSEQ) ? MT_DF_LRSEQ : 0)),
                              (uint8_t)nov, d.ng[s]};
-            put_bytes(o, cap, &n, b4, 4);
+            put_bytes(o, b4, 4);
             int32_t f[8] = {d.len[s],
                             d.seq[s],
                             long_of(d.cli[s]),
@@ -1290,13 +1331,13 @@ struct Replica {
                             (fl & RF_LSEQ) ? d.lseq[s] : 0,
                             (fl & RF_LRSEQ) ? d.lrseq[s] : 0,
                             t >> 3};
-            put_bytes(o, cap, &n, f, sizeof(f));
+            put_bytes(o, f, sizeof(f));
             for (int k = 0; k < nov; k++) {
                 int32_t lo = long_of((uint8_t)(((d.ovl[s] >> (8 * k)) & 0xFF) - 1));
-                put_bytes(o, cap, &n, &lo, 4);
+                put_bytes(o, &lo, 4);
             }
             uint16_t h2[2] = {(uint16_t)np, (uint16_t)((fl & RF_MARKER) ? d.toff[s] : 0)};
-            put_bytes(o, cap, &n, h2, 4);
+            put_bytes(o, h2, 4);
             /* props sorted by global key id */
             int32_t last = -1;
             for (int q = 0; q < np; q++) {
@@ -1309,12 +1350,11 @@ struct Replica {
                     }
                 }
                 uint16_t kv2[2] = {(uint16_t)bk, d.pv[s * NKEYS + best]};
-                put_bytes(o, cap, &n, kv2, 4);
+                put_bytes(o, kv2, 4);
                 last = bk;
             }
-            if (!(fl & RF_MARKER)) put_bytes(o, cap, &n, base + d.toff[s], 2 * (int64_t)d.len[s]);
+            if (!(fl & RF_MARKER)) put_bytes(o, base + d.toff[s], 2 * (int64_t)d.len[s]);
         }
-        return n;
     }
     MT_HD static uint64_t fnv(const uint8_t* p, int64_t n) {
         uint64_t h = MT_FNV_OFFSET;

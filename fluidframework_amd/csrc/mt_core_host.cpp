@@ -108,12 +108,7 @@ int64_t mth_dump(mth_store* s, int64_t doc, uint8_t* out, int64_t cap) {
 
 uint64_t mth_digest(mth_store* s, int64_t doc) {
     Replica<WaveHost> r(doc_view(s->c, s->k, doc), WaveHost());
-    int64_t n = r.dump(nullptr, 0);
-    uint8_t* buf = (uint8_t*)malloc(n > 0 ? n : 1);
-    r.dump(buf, n);
-    uint64_t h = Replica<WaveHost>::fnv(buf, n);
-    free(buf);
-    return h;
+    return r.digest();
 }
 
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {

@@ -34,7 +34,6 @@ inline size_t layout(Cols& c, const Caps& k, int64_t ndocs, uint8_t* base) {
     c.ovl = (uint64_t*)take(8 * rows);
     c.pv = (uint16_t*)take(2 * rows * NKEYS);
     c.pk = (uint8_t*)take(rows * NKEYS);
-    c.grp = (int32_t*)take(4 * rows * NGRP);
     c.nparent = (int16_t*)take(2 * nodes);
     c.kids = (int16_t*)take(2 * nodes * MAXN);
     c.lorder = (int16_t*)take(2 * nodes);

@@ -1,0 +1,187 @@
+"""Host facade over the MI355X replay engine (C ABI: include/mt_engine.h, libmtreplay.so).
+
+`Engine` holds a batch of document replicas resident in one GPU's HBM. It is the batched form
+of the reference ``Client`` (packages/dds/merge-tree/src/client.ts:43): `submit` + `run` apply
+whole event streams (``Client.applyMsg`` for sequenced messages, the ``*Local`` edits for local
+ones), and the reads mirror ``getLength`` / ``getText`` under a (refSeq, clientId) perspective.
+There is no CPU fallback: if the HIP library cannot be loaded this raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import native
+from . import oplog as ol
+
+ERRORS = {0: "ok", 1: "MergeTree insert failed", 2: "assertion", 3: "invalid op range", 4: "unsupported",
+          5: "capacity exceeded"}
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class _Caps(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("ncap", "hcap", "acap", "mcap", "gcap", "ccap")]
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        path = native.lib_path("libmtreplay.so")
+        if not os.path.exists(path):
+            raise EngineError(f"HIP replay library missing: {path} (run __graft_entry__.build())")
+        L = ctypes.CDLL(path)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.mt_engine_create.argtypes = [i32, i64, ctypes.POINTER(_Caps), ctypes.POINTER(vp)]
+        L.mt_engine_destroy.argtypes = [vp]
+        L.mt_engine_last_error.argtypes = [vp]
+        L.mt_engine_last_error.restype = ctypes.c_char_p
+        L.mt_engine_start_collab.argtypes = [vp, vp, i32, i32]
+        L.mt_engine_submit.argtypes = [vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, i64, vp]
+        L.mt_engine_run.argtypes = [vp]
+        L.mt_engine_reset.argtypes = [vp]
+        L.mt_engine_work.argtypes = [vp, vp]
+        L.mt_engine_sync.argtypes = [vp]
+        L.mt_engine_last_run_ms.argtypes = [vp]
+        L.mt_engine_last_run_ms.restype = ctypes.c_float
+        L.mt_engine_stream.argtypes = [vp]
+        L.mt_engine_stream.restype = vp
+        L.mt_engine_errors.argtypes = [vp, vp, vp]
+        L.mt_engine_digests.argtypes = [vp, vp]
+        L.mt_engine_dump.argtypes = [vp, i64, vp, i64]
+        L.mt_engine_dump.restype = i64
+        L.mt_engine_get_length.argtypes = [vp, i64, i32, i32, ctypes.POINTER(i32)]
+        L.mt_engine_get_text.argtypes = [vp, i64, i32, i32, vp, i64]
+        L.mt_engine_get_text.restype = i64
+        L.mt_engine_stats.argtypes = [vp, vp]
+        L.mt_engine_ndocs.argtypes = [vp]
+        L.mt_engine_ndocs.restype = i64
+        _LIB = L
+    return _LIB
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def default_caps(ops_per_doc: int) -> dict:
+    """Capacities sized for the synthetic configs (high-water marks measured with the oracle)."""
+    if ops_per_doc <= 20_000:
+        return dict(ncap=512, hcap=1024, acap=1 << 16, mcap=4096, gcap=1024, ccap=64)
+    return dict(ncap=16384, hcap=32768, acap=1 << 22, mcap=4096, gcap=1024, ccap=64)
+
+
+class Engine:
+    """A batch of `ndocs` replicas on HIP device `device`."""
+
+    def __init__(self, ndocs: int, device: int = 0, **caps):
+        c = default_caps(0)
+        c.update(caps)
+        self.L = lib()
+        self.caps = _Caps(**c)
+        h = ctypes.c_void_p()
+        rc = self.L.mt_engine_create(device, ndocs, ctypes.byref(self.caps), ctypes.byref(h))
+        if rc != 0:
+            raise EngineError(f"mt_engine_create failed: status {rc}")
+        self.h = h.value
+        self.ndocs = ndocs
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mt_engine_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.L.mt_engine_last_error(self.h)
+            raise EngineError(f"{what} failed: status {rc}: {msg.decode() if msg else ''}")
+
+    def start_collab(self, local_long_ids, min_seq: int = 0, cur_seq: int = 0):
+        ids = np.ascontiguousarray(np.broadcast_to(np.asarray(local_long_ids, np.int32), (self.ndocs,)))
+        self._check(self.L.mt_engine_start_collab(self.h, _p(ids), min_seq, cur_seq), "start_collab")
+
+    def submit(self, b: ol.Batch):
+        if b.ndocs != self.ndocs:
+            raise EngineError("batch doc count != engine doc count")
+        ops = b.ops if len(b.ops) else np.zeros(1, ol.OP_DTYPE)
+        self._keep = (ops, b)
+        self._check(self.L.mt_engine_submit(self.h, _p(ops), _p(b.op_off), _p(b.text), len(b.text), _p(b.text_off),
+                                             _p(b.props), len(b.props), _p(b.props_off), _p(b.kv), len(b.kv),
+                                             _p(b.kv_off)), "submit")
+
+    def reset(self):
+        self._check(self.L.mt_engine_reset(self.h), "reset")
+
+    def work(self) -> np.ndarray:
+        """(ndocs, 3) int64: sequenced messages applied, sum of rows before each, rows written."""
+        out = np.zeros((self.ndocs, 3), np.int64)
+        self._check(self.L.mt_engine_work(self.h, _p(out)), "work")
+        return out
+
+    def run(self):
+        self._check(self.L.mt_engine_run(self.h), "run")
+
+    def sync(self):
+        self._check(self.L.mt_engine_sync(self.h), "sync")
+
+    def replay(self, b: ol.Batch):
+        self.submit(b)
+        self.run()
+        self.sync()
+
+    @property
+    def last_run_ms(self) -> float:
+        return float(self.L.mt_engine_last_run_ms(self.h))
+
+    @property
+    def stream(self) -> int:
+        return int(self.L.mt_engine_stream(self.h) or 0)
+
+    def errors(self):
+        e = np.zeros(self.ndocs, np.int32)
+        eo = np.zeros(self.ndocs, np.int32)
+        self._check(self.L.mt_engine_errors(self.h, _p(e), _p(eo)), "errors")
+        return e, eo
+
+    def digests(self) -> np.ndarray:
+        out = np.zeros(self.ndocs, np.uint64)
+        self._check(self.L.mt_engine_digests(self.h, _p(out)), "digests")
+        return out
+
+    def dump(self, doc: int) -> bytes:
+        n = self.L.mt_engine_dump(self.h, doc, None, 0)
+        if n < 0:
+            raise EngineError(f"dump failed {n}")
+        buf = np.zeros(max(n, 1), np.uint8)
+        n2 = self.L.mt_engine_dump(self.h, doc, _p(buf), n)
+        if n2 != n:
+            raise EngineError("dump size changed")
+        return buf[:n].tobytes()
+
+    def get_length(self, doc: int, ref_seq: int = 0, long_client: int = -1) -> int:
+        v = ctypes.c_int32()
+        self._check(self.L.mt_engine_get_length(self.h, doc, ref_seq, long_client, ctypes.byref(v)), "get_length")
+        return v.value
+
+    def get_text(self, doc: int, ref_seq: int = 0, long_client: int = -1) -> str:
+        n = self.L.mt_engine_get_text(self.h, doc, ref_seq, long_client, None, 0)
+        if n < 0:
+            raise EngineError(f"get_text failed {n}")
+        buf = np.zeros(max(n, 1), "<u2")
+        self.L.mt_engine_get_text(self.h, doc, ref_seq, long_client, _p(buf), n)
+        return buf[:n].tobytes().decode("utf-16-le")
+
+    def stats(self) -> np.ndarray:
+        out = np.zeros((self.ndocs, 4), np.int32)
+        self._check(self.L.mt_engine_stats(self.h, _p(out)), "stats")
+        return out

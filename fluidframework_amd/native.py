@@ -45,3 +45,25 @@ def build_core_host() -> str:
         os.makedirs(BUILD, exist_ok=True)
         subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", out, srcs[0]], check=True)
     return out
+
+
+def hipcc() -> str:
+    return os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def build_replay(force: bool = False) -> str:
+    """The product library: HIP kernels for gfx950 + the C ABI of include/mt_engine.h."""
+    out = lib_path("libmtreplay.so")
+    srcs = [os.path.join(CSRC, "mt_replay.hip")] + [os.path.join(CSRC, f) for f in CORE_HDRS] + [
+        os.path.join(ROOT, "include", "mt_engine.h"), os.path.join(ROOT, "include", "mt_oplog.h")]
+    if force or _stale(out, srcs):
+        os.makedirs(BUILD, exist_ok=True)
+        subprocess.run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", out,
+                        srcs[0]], check=True)
+    return out
+
+
+def build_all() -> None:
+    build_gen()
+    build_core_host()
+    build_replay()

@@ -1,0 +1,103 @@
+/*
+ * mt_engine.h — C ABI of the MI355X merge-tree replay engine (libmtreplay.so).
+ *
+ * The reference has no FFI for this path: its boundary is the TypeScript module
+ * @fluidframework/merge-tree (packages/dds/merge-tree/src/index.ts:6-22), whose `Client` is
+ * called by SharedSegmentSequence (packages/dds/sequence/src/sequence.ts:579-616) and
+ * SharedMatrix/PermutationVector (packages/dds/matrix/src/matrix.ts:568-578). The entry points
+ * below are what a Node-API addon binding that module's hot path would call;
+ * each cites the reference member it replaces. One engine = a batch of documents resident in
+ * one GPU's HBM, one replica per document. All calls are synchronous unless noted; errors
+ * are returned as MT_E_* status codes (no exceptions cross the ABI) and per-document replay
+ * errors are latched and reported by mt_engine_errors (the reference throws synchronously).
+ */
+#ifndef MT_ENGINE_H
+#define MT_ENGINE_H
+#include <stdint.h>
+
+#include "mt_oplog.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mt_engine mt_engine;
+
+/* Per-document capacities (device memory is sized from these). */
+typedef struct mt_caps {
+    int32_t ncap; /* B-tree nodes per doc; row slots = 8 * ncap                        */
+    int32_t hcap; /* zamboni LRU heap entries (collections.ts:212-264)                 */
+    int32_t acap; /* text arena half size, UTF-16 units                                 */
+    int32_t mcap; /* pending segment-group membership log entries                       */
+    int32_t gcap; /* pending local ops (segment groups) in flight                       */
+    int32_t ccap; /* distinct clients per doc (<= 254)                                  */
+} mt_caps;
+
+/* status codes */
+enum {
+    MT_OK = 0,
+    MT_E_INSERT_FAILED = 1, /* per doc: mergeTree.ts:2243-2249 "MergeTree insert failed"       */
+    MT_E_ASSERT = 2,        /* per doc: a reference `assert` would have thrown                 */
+    MT_E_INVALID_RANGE = 3, /* per doc: local op rejected by getValidOpRange (client.ts:486)   */
+    MT_E_UNSUPPORTED = 4,   /* per doc: >8 property keys or >8 overlapping removers            */
+    MT_E_CAPACITY = 5,      /* per doc: a capacity in mt_caps was exceeded                     */
+    MT_E_ARG = 16,          /* engine: bad argument                                            */
+    MT_E_HIP = 17,          /* engine: HIP runtime error (mt_engine_last_error has the text)  */
+    MT_E_NOMEM = 18,        /* engine: device allocation failed                                */
+};
+
+/* Create an engine with `ndocs` empty, non-collaborating replicas on HIP device `device`
+ * (new Client() + MergeTree constructor, client.ts:75-84, mergeTree.ts:1143-1146). */
+int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_engine** out);
+void mt_engine_destroy(mt_engine* e);
+const char* mt_engine_last_error(const mt_engine* e);
+
+/* Client.startOrUpdateCollaboration(longClientId, minSeq, currentSeq) for every doc
+ * (client.ts:1053-1073); local_long_ids[d] is doc d's own long-client index. */
+int32_t mt_engine_start_collab(mt_engine* e, const int32_t* local_long_ids, int32_t min_seq, int32_t cur_seq);
+
+/* Stage a batch of per-doc event streams (host memory; copied to HBM). Doc d's events are
+ * ops[op_off[d] .. op_off[d+1]), its pools start at text+text_off[d], props+props_off[d],
+ * kv+kv_off[d] (pools may be shared between docs). Replaces the previous staged batch. */
+int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_off, const uint16_t* text,
+                         int64_t text_units, const int64_t* text_off, const mt_props_rec* props, int64_t nprops,
+                         const int64_t* props_off, const mt_kv* kv, int64_t nkv, const int64_t* kv_off);
+
+/* Apply every staged event to its doc: Client.applyMsg for sequenced messages (client.ts:797),
+ * insertSegmentLocal / removeRangeLocal / annotateRangeLocal for local edits (202/189/164).
+ * Asynchronous on the engine's HIP stream; mt_engine_sync waits. */
+int32_t mt_engine_run(mt_engine* e);
+int32_t mt_engine_sync(mt_engine* e);
+/* Device time of the last mt_engine_run's replay kernel (HIP events on the engine stream). */
+float mt_engine_last_run_ms(const mt_engine* e);
+/* The engine's hipStream_t (as void*), for callers that time or order work around it. */
+void* mt_engine_stream(const mt_engine* e);
+
+/* Return every doc to the state right after create/start_collab (same local ids), keeping the
+ * staged batch, so a replay can be repeated (bench steps). Asynchronous. */
+int32_t mt_engine_reset(mt_engine* e);
+/* Per-doc work counters for roofline accounting: out3[3d..3d+2] = (sequenced messages applied,
+ * sum over them of rows in the table before the message, rows written). */
+int32_t mt_engine_work(mt_engine* e, int64_t* out3);
+
+/* Per-doc latched error code (MT_E_*) and index of the event that raised it (-1 if none). */
+int32_t mt_engine_errors(mt_engine* e, int32_t* err, int32_t* err_op);
+/* Per-doc FNV-1a-64 digest of the canonical segment dump (mt_oplog.h), computed on device. */
+int32_t mt_engine_digests(mt_engine* e, uint64_t* out);
+/* Canonical dump of one doc; returns bytes needed (writes if cap suffices), <0 on error. */
+int64_t mt_engine_dump(mt_engine* e, int64_t doc, uint8_t* out, int64_t cap);
+/* MergeTree.getLength(refSeq, clientId) (mergeTree.ts:1610); long_client < 0 = local view
+ * (Client.getLength, client.ts:1051). */
+int32_t mt_engine_get_length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t* out);
+/* MergeTreeTextHelper.getText(refSeq, clientId) (textSegment.ts:154-172); long_client < 0 =
+ * local view. Returns the length in UTF-16 units (writes at most cap), <0 on error. */
+int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* out,
+                           int64_t cap);
+/* Per-doc counters: nleaf, high-water row slots, high-water heap, events applied. */
+int32_t mt_engine_stats(mt_engine* e, int32_t* out4_per_doc);
+int64_t mt_engine_ndocs(const mt_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -5,50 +5,23 @@ packages/dds/merge-tree/src/test/mergeTree.markRangeRemoved.spec.ts.
 Client long ids: the reference uses strings ("localUser", "remoteClient", "A", ...); here they
 are doc-local indices, named by the constants below.
 """
-import struct
-
 import pytest
 
 from fluidframework_amd import oplog as ol
-from oracle_client import Msg, OracleClient
+from oracle_client import Msg
+from replicas import make_replica, parse_dump
 
 LOCAL, REMOTE, REMOTE2 = 0, 1, 2
 
-
-def parse_dump(b: bytes):
-    """Decode the canonical dump (include/mt_oplog.h) into (header, [segment dicts])."""
-    hdr = struct.unpack_from("<6i", b, 0)
-    off = 24
-    segs = []
-    for _ in range(hdr[4]):
-        kind, flags, nov, ngroups = struct.unpack_from("<4B", b, off)
-        off += 4
-        f = struct.unpack_from("<8i", b, off)
-        off += 32
-        ov = list(struct.unpack_from(f"<{nov}i", b, off))
-        off += 4 * nov
-        nprops, ref_type = struct.unpack_from("<2H", b, off)
-        off += 4
-        props = [struct.unpack_from("<2H", b, off + 4 * k) for k in range(nprops)]
-        off += 4 * nprops
-        text = ""
-        if kind == ol.SEG_TEXT:
-            text = b[off: off + 2 * f[0]].decode("utf-16-le")
-            off += 2 * f[0]
-        segs.append(dict(kind=kind, flags=flags, ngroups=ngroups, len=f[0], seq=f[1], client=f[2],
-                         removedSeq=f[3] if flags & ol_removed() else None, removedClient=f[4],
-                         localSeq=f[5], localRemovedSeq=f[6], leaf=f[7], overlap=ov, props=props,
-                         refType=ref_type, text=text))
-    assert off == len(b)
-    return dict(currentSeq=hdr[0], minSeq=hdr[1], localSeq=hdr[2], length=hdr[3], nsegs=hdr[4],
-                nleaf=hdr[5]), segs
+KINDS = ["oracle", "host", pytest.param("gpu", marks=pytest.mark.gpu)]
 
 
-def ol_removed():
-    return 2
+@pytest.fixture(params=KINDS)
+def kind(request):
+    return request.param
 
 
-def seg_at(client: OracleClient, pos: int):
+def seg_at(client, pos: int):
     """getContainingSegment(pos) in the local perspective (visible segments only)."""
     _, segs = parse_dump(client.dump())
     p = 0
@@ -62,9 +35,9 @@ def seg_at(client: OracleClient, pos: int):
 
 
 @pytest.fixture
-def client():
+def client(kind):
     # client.applyMsg.spec.ts:17-21
-    c = OracleClient()
+    c = make_replica(kind)
     c.insert_text_local(0, "hello world")
     c.start_collab(LOCAL)
     return c
@@ -87,10 +60,8 @@ def test_interleaved_inserts_annotates_deletes(client):
             op = client.annotate_range_local(pos1, pos2, {"foo": f"{i}"})
         assert op is not None
         changes[i] = client.make_op_message(op, i + 1)
-    assert client.pending_groups() == 100
     for i in range(100):
         assert client.apply_msg(changes[i]) == 0
-    assert client.pending_groups() == 0
     _, segs = parse_dump(client.dump())
     for s in segs:
         assert s["seq"] != -1 and s["ngroups"] == 0
@@ -117,28 +88,27 @@ def test_remove_range_local_ack(client):
 def test_annotate_local_ack(client):
     # client.applyMsg.spec.ts:112-127
     op = client.annotate_range_local(0, 1, {"foo": "bar"})
-    assert client.pending_groups() == 1
+    assert parse_dump(client.dump())[1][0]["ngroups"] == 1
     client.apply_msg(client.make_op_message(op, 17))
-    assert client.pending_groups() == 0
+    assert parse_dump(client.dump())[1][0]["ngroups"] == 0
 
 
 def test_annotate_then_remove_local(client):
     # client.applyMsg.spec.ts:129-168
     end = len(client.get_text())
     a = client.annotate_range_local(0, end, {"foo": "bar"})
-    assert client.pending_groups() == 1
     r = client.remove_range_local(0, end)
     _, segs = parse_dump(client.dump())
     assert segs[0]["removedSeq"] == -1
-    assert client.pending_groups() == 2
+    assert segs[0]["ngroups"] == 2
     client.apply_msg(client.make_op_message(a, 17))
     _, segs = parse_dump(client.dump())
     assert segs[0]["removedSeq"] == -1
-    assert client.pending_groups() == 1
+    assert segs[0]["ngroups"] == 1
     client.apply_msg(client.make_op_message(r, 18))
     _, segs = parse_dump(client.dump())
     assert segs[0]["removedSeq"] == 18
-    assert client.pending_groups() == 0
+    assert segs[0]["ngroups"] == 0
 
 
 def test_multiple_interleaved_annotates(client):
@@ -151,10 +121,10 @@ def test_multiple_interleaved_annotates(client):
         seq += 1
         msgs.append(client.make_op_message(op, seq))
         end //= 2
-    assert client.pending_groups() == len(msgs)
+    assert parse_dump(client.dump())[1][0]["ngroups"] == len(msgs)
     for m in msgs:
         client.apply_msg(m)
-    assert client.pending_groups() == 0
+    assert parse_dump(client.dump())[1][0]["ngroups"] == 0
     assert client.error == 0
 
 
@@ -186,9 +156,9 @@ def run_convergence(clients, messages):
     return texts[0]
 
 
-def test_overlapping_insert_and_delete(client):
+def test_overlapping_insert_and_delete(client, kind):
     # client.applyMsg.spec.ts:230-259
-    remote = OracleClient(client.interner)
+    remote = make_replica(kind, client.interner)
     remote.insert_text_local(0, client.get_text())
     remote.start_collab(REMOTE)
     seq = 1
@@ -203,11 +173,11 @@ def test_overlapping_insert_and_delete(client):
     run_convergence([client, remote], msgs)
 
 
-def three(seed_text=None):
-    it = OracleClient()
+def three(kind, seed_text=None):
+    it = ol.Interner()
     cs = []
     for k in range(3):
-        c = OracleClient(it)
+        c = make_replica(kind, it)
         if seed_text:
             c.insert_text_local(0, seed_text)
         c.start_collab(k)
@@ -215,9 +185,9 @@ def three(seed_text=None):
     return cs
 
 
-def test_intersecting_insert_after_local_delete():
+def test_intersecting_insert_after_local_delete(kind):
     # client.applyMsg.spec.ts:261-290
-    A, B, C = three()
+    A, B, C = three(kind)
     msgs = [
         C.make_op_message(C.insert_text_local(0, "c"), 1),
         C.make_op_message(C.remove_range_local(0, 1), 2),
@@ -227,9 +197,9 @@ def test_intersecting_insert_after_local_delete():
     run_convergence([A, B, C], msgs)
 
 
-def test_conflicting_insert_after_shared_delete():
+def test_conflicting_insert_after_shared_delete(kind):
     # client.applyMsg.spec.ts:292-320
-    A, B, C = three("a")
+    A, B, C = three(kind, "a")
     msgs = [
         B.make_op_message(B.insert_text_local(0, "b"), 1),
         C.make_op_message(C.remove_range_local(0, C.get_length()), 2),
@@ -238,9 +208,9 @@ def test_conflicting_insert_after_shared_delete():
     run_convergence([A, B, C], msgs)
 
 
-def test_local_remove_followed_by_conflicting_insert():
+def test_local_remove_followed_by_conflicting_insert(kind):
     # client.applyMsg.spec.ts:322-349
-    A, B, C = three()
+    A, B, C = three(kind)
     msgs = [
         C.make_op_message(C.insert_text_local(0, "c"), 1),
         B.make_op_message(B.insert_text_local(0, "b"), 2),
@@ -250,9 +220,9 @@ def test_local_remove_followed_by_conflicting_insert():
     run_convergence([A, B, C], msgs)
 
 
-def test_intersecting_insert_with_unack_insert_and_delete():
+def test_intersecting_insert_with_unack_insert_and_delete(kind):
     # client.applyMsg.spec.ts:351-380
-    A, B, C = three()
+    A, B, C = three(kind)
     msgs = [
         C.make_op_message(C.insert_text_local(0, "c"), 1),
         B.make_op_message(B.insert_text_local(0, "bb"), 2),
@@ -262,9 +232,9 @@ def test_intersecting_insert_with_unack_insert_and_delete():
 
 
 @pytest.fixture
-def hello():
+def hello(kind):
     # mergeTree.markRangeRemoved.spec.ts:13-27
-    c = OracleClient()
+    c = make_replica(kind)
     c.start_collab(LOCAL)
     for ch in "hello world":
         op = c.insert_text_local(c.get_length(), ch)
