@@ -25,7 +25,7 @@
 #include "../../include/mt_oplog.h"
 
 #ifdef __HIPCC__
-#define MT_HD __host__ __device__
+#define MT_HD __host__ __device__ __attribute__((always_inline))
 #define MT_DEV __device__
 #else
 #define MT_HD
@@ -64,13 +64,11 @@ enum : uint8_t {
     RF_LRSEQ = 8,
 };
 
+/* runtime capacities that are not part of the LDS image */
 struct Caps {
-    int32_t ncap; /* nodes per doc (slots = ncap * 8) */
-    int32_t hcap; /* zamboni heap entries */
     int32_t acap; /* text arena half-size (UTF-16 units); arena holds 2 halves */
     int32_t mcap; /* segment-group membership log entries */
     int32_t gcap; /* pending segment groups (local ops in flight) */
-    int32_t ccap; /* clients per doc */
 };
 
 /* per-document scalar header */
@@ -81,96 +79,64 @@ struct DocHdr {
     int32_t heapN, memN, gqHead, gqN;
     int32_t arenaTop, arenaSide, err, errOp;
     int32_t nkeys, opsDone, hwSlots, hwHeap;
-    int32_t nrows, seqOps;      /* rows in the table (tombstones included); sequenced msgs applied */
-    int64_t sumR, sumW;         /* roofline counters: sum over sequenced msgs of rows before the op,
-                                   rows written by the op (BASELINE.md A(op) = 16 R + 32 W) */
+    int32_t nrows, seqOps, nfreeRid, gcEpoch; /* rows in the table; sequenced msgs applied */
+    int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
+                           rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
     uint16_t keys[NKEYS];
 };
 
-/* batch-wide column base pointers (per-doc stride = capacity) */
-struct Cols {
-    /* rows: ncap*8 per doc */
-    int32_t *len, *seq, *rseq, *lseq, *lrseq;
-    uint32_t *sid, *toff;
-    uint8_t *cli, *rcli, *flags, *ng, *prw;
-    uint64_t* ovl;
-    uint16_t* pv; /* NKEYS per row */
-    uint8_t* pk;  /* NKEYS per row: pendingKeyUpdateCount */
-    /* nodes: ncap per doc */
-    int16_t *nparent, *kids, *lorder, *lpos;
-    int8_t *nchild, *nlevel, *nscour;
-    /* heap: hcap per doc */
-    uint32_t* hsid;
-    int32_t* hseq;
-    /* membership log: mcap per doc */
-    int32_t* mgid;
-    uint32_t* msid;
-    /* pending group FIFO: gcap per doc (ring) */
-    int32_t* gq;
-    /* text arena: 2*acap per doc */
-    uint16_t* arena;
-    /* clients: ccap per doc, short -> long */
-    uint16_t* s2l;
-    DocHdr* hdr;
+/* Cold per-row data, indexed by a row id that does not move when the row's slot moves. */
+struct ColdRow {
+    int32_t lseq, lrseq;
+    uint32_t toff; /* text offset in the arena; a marker's refType */
+    uint8_t prw;   /* pendingRewriteCount */
+    uint8_t gc;    /* arena-GC epoch that last moved this row's text (0 = never) */
+    uint8_t _p[2];
+    uint64_t ovl;          /* removedClientOverlap: up to 8 short ids (+1), push order */
+    uint16_t pv[NKEYS];    /* property values per doc key slot (0 = absent) */
+    uint8_t pk[NKEYS];     /* pendingKeyUpdateCount per key slot */
 };
 
-/* A view of one document: column pointers already offset to this doc. */
+/* Hot per-document state with compile-time capacities: everything the per-op scans and the
+ * tree skeleton touch. On the GPU this image lives in LDS for the whole replay. */
+template <int N_, int C_ = 64>
+struct HotT {
+    static constexpr int N = N_;     /* B-tree nodes */
+    static constexpr int S = N_ * 8; /* row slots (8 per leaf node) */
+    static constexpr int H = N_ * 2; /* zamboni heap entries */
+    static constexpr int C = C_;     /* clients */
+    DocHdr h;
+    int32_t len[S], seq[S], rseq[S];
+    uint32_t sid[S];
+    int16_t rid[S];     /* slot -> cold row id */
+    int16_t freeRid[S]; /* free row-id stack */
+    uint8_t cli[S], rcli[S], flags[S], ng[S];
+    int16_t nparent[N], lorder[N], lpos[N];
+    int16_t kids[N * 8];
+    int8_t nchild[N], nlevel[N], nscour[N];
+    int8_t _pad[(16 - (3 * N) % 16) % 16];
+    uint32_t hsid[H];
+    int32_t hseq[H];
+    uint16_t s2l[C];
+};
+
+/* LDS-sized profile for config 2/3 documents (max 147 nodes / 968 slots observed) and larger
+ * global-memory profiles. */
+typedef HotT<160> HotSmall;
+typedef HotT<2048> HotMid;
+typedef HotT<16384> HotBig;
+
+/* Per-document view: the hot image (LDS or global) plus global cold/arena/log pointers. */
+template <class HT>
 struct Doc {
-    int32_t *len, *seq, *rseq, *lseq, *lrseq;
-    uint32_t *sid, *toff;
-    uint8_t *cli, *rcli, *flags, *ng, *prw;
-    uint64_t* ovl;
-    uint16_t* pv;
-    uint8_t* pk;
-    int16_t *nparent, *kids, *lorder, *lpos;
-    int8_t *nchild, *nlevel, *nscour;
-    uint32_t* hsid;
-    int32_t* hseq;
+    HT* t;
+    ColdRow* cold; /* HT::S records */
+    uint16_t* arena; /* 2 * acap */
     int32_t* mgid;
     uint32_t* msid;
     int32_t* gq;
-    uint16_t* arena;
-    uint16_t* s2l;
-    DocHdr* h;
     Caps caps;
 };
-
-MT_HD inline Doc doc_view(const Cols& c, const Caps& k, int64_t d) {
-    Doc v;
-    int64_t rs = (int64_t)k.ncap * MAXN, ns = k.ncap;
-    v.len = c.len + d * rs;
-    v.seq = c.seq + d * rs;
-    v.rseq = c.rseq + d * rs;
-    v.lseq = c.lseq + d * rs;
-    v.lrseq = c.lrseq + d * rs;
-    v.sid = c.sid + d * rs;
-    v.toff = c.toff + d * rs;
-    v.cli = c.cli + d * rs;
-    v.rcli = c.rcli + d * rs;
-    v.flags = c.flags + d * rs;
-    v.ng = c.ng + d * rs;
-    v.prw = c.prw + d * rs;
-    v.ovl = c.ovl + d * rs;
-    v.pv = c.pv + d * rs * NKEYS;
-    v.pk = c.pk + d * rs * NKEYS;
-    v.nparent = c.nparent + d * ns;
-    v.kids = c.kids + d * ns * MAXN;
-    v.lorder = c.lorder + d * ns;
-    v.lpos = c.lpos + d * ns;
-    v.nchild = c.nchild + d * ns;
-    v.nlevel = c.nlevel + d * ns;
-    v.nscour = c.nscour + d * ns;
-    v.hsid = c.hsid + d * k.hcap;
-    v.hseq = c.hseq + d * k.hcap;
-    v.mgid = c.mgid + d * k.mcap;
-    v.msid = c.msid + d * k.mcap;
-    v.gq = c.gq + d * k.gcap;
-    v.arena = c.arena + d * (int64_t)k.acap * 2;
-    v.s2l = c.s2l + d * k.ccap;
-    v.h = c.hdr + d;
-    v.caps = k;
-    return v;
-}
 
 /* Op pools of one document. */
 struct Pools {
@@ -184,63 +150,72 @@ struct Pools {
 /* ------------------------------------------------------------------------------------------
  * Replica: all operations of one document replica, executed by one wave.
  * ---------------------------------------------------------------------------------------- */
-template <class W>
+template <class W, class HT>
 struct Replica {
-    Doc d;
+    Doc<HT> d;
+    HT& z; /* the hot image */
     W w;
 
-    MT_HD Replica(const Doc& doc, const W& wave) : d(doc), w(wave) {}
+    MT_HD Replica(const Doc<HT>& doc, const W& wave) : d(doc), z(*doc.t), w(wave) {}
+
+    MT_HD ColdRow& cold(int32_t s) const { return d.cold[z.rid[s]]; }
 
     MT_HD void fail(int32_t e) {
-        if (d.h->err == E_OK) {
-            d.h->err = e;
-            d.h->errOp = d.h->opsDone;
+        if (z.h.err == E_OK) {
+            z.h.err = e;
+            z.h.errOp = z.h.opsDone;
         }
     }
 
     /* ---- node allocation ------------------------------------------------------------- */
     MT_HD int32_t alloc_node(int8_t level) {
-        int32_t n = d.h->freeHead;
+        int32_t n = z.h.freeHead;
         if (n < 0) {
             fail(E_CAPACITY);
             return -1;
         }
-        d.h->freeHead = d.nparent[n];
-        d.h->nfree--;
-        d.nparent[n] = -1;
-        d.nchild[n] = 0;
-        d.nlevel[n] = level;
-        d.nscour[n] = -1; /* needsScour undefined */
+        z.h.freeHead = z.nparent[n];
+        z.h.nfree--;
+        z.nparent[n] = -1;
+        z.nchild[n] = 0;
+        z.nlevel[n] = level;
+        z.nscour[n] = -1; /* needsScour undefined */
         return n;
     }
     MT_HD void free_node(int32_t n) {
-        d.nparent[n] = (int16_t)d.h->freeHead;
-        d.nchild[n] = 0;
-        d.h->freeHead = n;
-        d.h->nfree++;
+        z.nparent[n] = (int16_t)z.h.freeHead;
+        z.nchild[n] = 0;
+        z.h.freeHead = n;
+        z.h.nfree++;
     }
 
     /* ---- init -------------------------------------------------------------------------- */
     MT_HD void init() {
         /* node 0 = empty root leaf (initialNode, mergeTree.ts:1159-1163) */
-        int32_t ncap = d.caps.ncap;
+        int32_t ncap = HT::N;
         for (int32_t b = 0; b < ncap; b += W::N) {
             int32_t n = b + w.lane();
             if (n < ncap) {
-                d.nparent[n] = (int16_t)(n + 1 < ncap ? n + 1 : -1);
-                d.nchild[n] = 0;
-                d.nlevel[n] = 0;
-                d.nscour[n] = -1;
+                z.nparent[n] = (int16_t)(n + 1 < ncap ? n + 1 : -1);
+                z.nchild[n] = 0;
+                z.nlevel[n] = 0;
+                z.nscour[n] = -1;
             }
         }
+        for (int32_t b = 0; b < HT::S; b += W::N) {
+            int32_t i = b + w.lane();
+            if (i < HT::S) z.freeRid[i] = (int16_t)(HT::S - 1 - i);
+        }
         w.sync();
-        DocHdr* h = d.h;
+        DocHdr* h = &z.h;
+        h->nfreeRid = HT::S;
+        h->gcEpoch = 0;
         h->freeHead = 1;
         h->nfree = ncap - 1;
         h->root = 0;
-        d.nparent[0] = -1;
-        d.lorder[0] = 0;
-        d.lpos[0] = 0;
+        z.nparent[0] = -1;
+        z.lorder[0] = 0;
+        z.lpos[0] = 0;
         h->nleaf = 1;
         h->currentSeq = 0;
         h->minSeq = 0;
@@ -271,49 +246,48 @@ struct Replica {
 
     /* ---- clients (client.ts:637-661) --------------------------------------------------- */
     MT_HD int32_t short_of(int32_t longId) {
-        for (int32_t i = 0; i < d.h->nclients; i++)
-            if (d.s2l[i] == longId) return i;
+        for (int32_t i = 0; i < z.h.nclients; i++)
+            if (z.s2l[i] == longId) return i;
         return -1;
     }
     MT_HD int32_t get_or_add_short(int32_t longId) {
         int32_t s = short_of(longId);
         if (s >= 0) return s;
-        int32_t n = d.h->nclients;
-        if (n >= d.caps.ccap || n >= 0xFE) {
+        int32_t n = z.h.nclients;
+        if (n >= HT::C || n >= 0xFE) {
             fail(E_CAPACITY);
             return 0;
         }
-        d.s2l[n] = (uint16_t)longId;
-        d.h->nclients = n + 1;
+        z.s2l[n] = (uint16_t)longId;
+        z.h.nclients = n + 1;
         return n;
     }
     /* startOrUpdateCollaboration (client.ts:1053-1073) + startCollaboration (mergeTree.ts:1287) */
     MT_HD void start_collab(int32_t longId, int32_t minSeq, int32_t curSeq) {
-        if (d.h->localLong >= 0) return;
-        d.h->localLong = longId;
-        d.h->localShort = get_or_add_short(longId);
-        d.h->minSeq = minSeq;
-        d.h->currentSeq = curSeq;
-        d.h->collaborating = 1;
+        if (z.h.localLong >= 0) return;
+        z.h.localLong = longId;
+        z.h.localShort = get_or_add_short(longId);
+        z.h.minSeq = minSeq;
+        z.h.currentSeq = curSeq;
+        z.h.collaborating = 1;
     }
 
     /* ---- row helpers ------------------------------------------------------------------- */
-    MT_HD static bool removed(const Doc& d, int32_t s) { return d.rseq[s] != NOREM; }
     MT_HD bool is_local(int32_t client) const {
-        return !d.h->collaborating || client == d.h->localShort;
+        return !z.h.collaborating || client == z.h.localShort;
     }
     /* nodeLength of a leaf (mergeTree.ts:1692-1732); local perspective -> localNetLength */
     MT_HD int32_t vis(int32_t s, int32_t refSeq, int32_t client) const {
-        int32_t L = d.len[s];
-        if (is_local(client)) return d.rseq[s] == NOREM ? L : 0;
-        int32_t c = d.cli[s] == LOCAL_CLIENT ? -1 : d.cli[s];
-        int32_t sq = d.seq[s];
+        int32_t L = z.len[s];
+        if (is_local(client)) return z.rseq[s] == NOREM ? L : 0;
+        int32_t c = z.cli[s] == LOCAL_CLIENT ? -1 : z.cli[s];
+        int32_t sq = z.seq[s];
         if (!(c == client || (sq != UNASSIGNED_SEQ && sq <= refSeq))) return 0;
-        int32_t rs = d.rseq[s];
+        int32_t rs = z.rseq[s];
         if (rs != NOREM) {
-            int32_t rc = d.rcli[s] == LOCAL_CLIENT ? -1 : d.rcli[s];
+            int32_t rc = z.rcli[s] == LOCAL_CLIENT ? -1 : z.rcli[s];
             if (rc == client) return 0;
-            uint64_t ov = d.ovl[s];
+            uint64_t ov = cold(s).ovl;
             for (int k = 0; k < NOVL; k++) {
                 uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
                 if (e == 0) break;
@@ -324,41 +298,45 @@ struct Replica {
         return L;
     }
     /* localNetLength (mergeTree.ts:1195-1206) */
-    MT_HD int32_t local_len(int32_t s) const { return d.rseq[s] == NOREM ? d.len[s] : 0; }
+    MT_HD int32_t local_len(int32_t s) const { return z.rseq[s] == NOREM ? z.len[s] : 0; }
 
     MT_HD int32_t slot_at(int32_t t) const { /* t = k*8+j over lorder; -1 if not a row */
         int32_t k = t >> 3, j = t & 7;
-        if (k >= d.h->nleaf) return -1;
-        int32_t n = d.lorder[k];
-        return j < d.nchild[n] ? n * MAXN + j : -1;
+        if (k >= z.h.nleaf) return -1;
+        int32_t n = z.lorder[k];
+        return j < z.nchild[n] ? n * MAXN + j : -1;
     }
 
     /* copy every column of row a to row b (same doc) */
+    /* move row a's slot contents to slot b (hot columns + its cold row id) */
     MT_HD void copy_row(int32_t b, int32_t a) {
-        d.len[b] = d.len[a];
-        d.seq[b] = d.seq[a];
-        d.rseq[b] = d.rseq[a];
-        d.lseq[b] = d.lseq[a];
-        d.lrseq[b] = d.lrseq[a];
-        d.sid[b] = d.sid[a];
-        d.toff[b] = d.toff[a];
-        d.cli[b] = d.cli[a];
-        d.rcli[b] = d.rcli[a];
-        d.flags[b] = d.flags[a];
-        d.ng[b] = d.ng[a];
-        d.prw[b] = d.prw[a];
-        d.ovl[b] = d.ovl[a];
-        for (int k = 0; k < NKEYS; k++) {
-            d.pv[b * NKEYS + k] = d.pv[a * NKEYS + k];
-            d.pk[b * NKEYS + k] = d.pk[a * NKEYS + k];
-        }
+        z.len[b] = z.len[a];
+        z.seq[b] = z.seq[a];
+        z.rseq[b] = z.rseq[a];
+        z.sid[b] = z.sid[a];
+        z.rid[b] = z.rid[a];
+        z.cli[b] = z.cli[a];
+        z.rcli[b] = z.rcli[a];
+        z.flags[b] = z.flags[a];
+        z.ng[b] = z.ng[a];
     }
+    /* cold row ids */
+    MT_HD int32_t alloc_rid() {
+        int32_t n = z.h.nfreeRid;
+        if (n <= 0) {
+            fail(E_CAPACITY);
+            return 0;
+        }
+        z.h.nfreeRid = n - 1;
+        return z.freeRid[n - 1];
+    }
+    MT_HD void free_rid(int32_t r) { z.freeRid[z.h.nfreeRid++] = (int16_t)r; }
 
     /* ---- perspective scans ------------------------------------------------------------- */
     /* Total length under a perspective (getLength, mergeTree.ts:1610). */
     MT_HD int32_t length(int32_t refSeq, int32_t client) {
         int32_t total = 0;
-        int32_t T = d.h->nleaf * MAXN;
+        int32_t T = z.h.nleaf * MAXN;
         for (int32_t b = 0; b < T; b += W::N) {
             int32_t s = slot_at(b + w.lane());
             int32_t v = s >= 0 ? vis(s, refSeq, client) : 0;
@@ -370,7 +348,7 @@ struct Replica {
      * and P of that row. */
     MT_HD int32_t find_reach(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
         int32_t run = 0;
-        int32_t T = d.h->nleaf * MAXN;
+        int32_t T = z.h.nleaf * MAXN;
         for (int32_t b = 0; b < T; b += W::N) {
             int32_t t = b + w.lane();
             int32_t s = slot_at(t);
@@ -396,30 +374,30 @@ struct Replica {
      * remapped by `place_after_split` — callers use the returned final slot. */
     MT_HD void node_insert_child(int32_t p, int32_t idx, int32_t child) {
         /* interior node p: insert `child` at idx (insertChildNode, mergeTree.ts:2162-2172) */
-        int32_t n = d.nchild[p];
-        for (int32_t i = n; i > idx; i--) d.kids[p * MAXN + i] = d.kids[p * MAXN + i - 1];
-        d.kids[p * MAXN + idx] = (int16_t)child;
-        d.nchild[p] = (int8_t)(n + 1);
-        d.nparent[child] = (int16_t)p;
+        int32_t n = z.nchild[p];
+        for (int32_t i = n; i > idx; i--) z.kids[p * MAXN + i] = z.kids[p * MAXN + i - 1];
+        z.kids[p * MAXN + idx] = (int16_t)child;
+        z.nchild[p] = (int8_t)(n + 1);
+        z.nparent[child] = (int16_t)p;
     }
     MT_HD int32_t child_index(int32_t p, int32_t child) const {
-        for (int32_t i = 0; i < d.nchild[p]; i++)
-            if (d.kids[p * MAXN + i] == child) return i;
+        for (int32_t i = 0; i < z.nchild[p]; i++)
+            if (z.kids[p * MAXN + i] == child) return i;
         return -1;
     }
     /* insert leaf `nl` into lorder right after leaf `after` */
     MT_HD void lorder_insert_after(int32_t after, int32_t nl) {
-        int32_t k = d.lpos[after] + 1;
-        int32_t n = d.h->nleaf;
+        int32_t k = z.lpos[after] + 1;
+        int32_t n = z.h.nleaf;
         /* shift lorder[k..n-1] right by one (uniform loop; small) */
         for (int32_t i = n; i > k; i--) {
-            int32_t x = d.lorder[i - 1];
-            d.lorder[i] = (int16_t)x;
-            d.lpos[x] = (int16_t)i;
+            int32_t x = z.lorder[i - 1];
+            z.lorder[i] = (int16_t)x;
+            z.lpos[x] = (int16_t)i;
         }
-        d.lorder[k] = (int16_t)nl;
-        d.lpos[nl] = (int16_t)k;
-        d.h->nleaf = n + 1;
+        z.lorder[k] = (int16_t)nl;
+        z.lpos[nl] = (int16_t)k;
+        z.h.nleaf = n + 1;
     }
     /* split (mergeTree.ts:2509-2522) of a full node (8 children) into 4 + 4; the new node is
      * inserted after it in its parent, recursively; root split -> updateRoot (1909-1920).
@@ -428,7 +406,7 @@ struct Replica {
         int32_t first = -1;
         int32_t n = n0;
         for (;;) { /* iterative: a split may overflow the parent, up to the root */
-            int8_t lvl = d.nlevel[n];
+            int8_t lvl = z.nlevel[n];
             int32_t nn = alloc_node(lvl);
             if (nn < 0) return -1;
             if (first < 0) first = nn;
@@ -436,36 +414,36 @@ struct Replica {
                 for (int32_t i = 0; i < 4; i++) copy_row(nn * MAXN + i, n * MAXN + 4 + i);
             } else {
                 for (int32_t i = 0; i < 4; i++) {
-                    int32_t c = d.kids[n * MAXN + 4 + i];
-                    d.kids[nn * MAXN + i] = (int16_t)c;
-                    d.nparent[c] = (int16_t)nn;
+                    int32_t c = z.kids[n * MAXN + 4 + i];
+                    z.kids[nn * MAXN + i] = (int16_t)c;
+                    z.nparent[c] = (int16_t)nn;
                 }
             }
-            d.nchild[n] = 4;
-            d.nchild[nn] = 4;
+            z.nchild[n] = 4;
+            z.nchild[nn] = 4;
             if (lvl == 0) lorder_insert_after(n, nn);
-            int32_t p = d.nparent[n];
+            int32_t p = z.nparent[n];
             if (p < 0) {
                 int32_t r = alloc_node((int8_t)(lvl + 1));
                 if (r < 0) return -1;
-                d.kids[r * MAXN + 0] = (int16_t)n;
-                d.kids[r * MAXN + 1] = (int16_t)nn;
-                d.nchild[r] = 2;
-                d.nparent[n] = (int16_t)r;
-                d.nparent[nn] = (int16_t)r;
-                d.h->root = r;
+                z.kids[r * MAXN + 0] = (int16_t)n;
+                z.kids[r * MAXN + 1] = (int16_t)nn;
+                z.nchild[r] = 2;
+                z.nparent[n] = (int16_t)r;
+                z.nparent[nn] = (int16_t)r;
+                z.h.root = r;
                 return first;
             }
             node_insert_child(p, child_index(p, n) + 1, nn);
-            if (d.nchild[p] < MAXN) return first;
+            if (z.nchild[p] < MAXN) return first;
             n = p;
         }
     }
     /* Make room at child index j of leaf n; returns slot for the new row (after any split). */
     MT_HD int32_t leaf_insert_slot(int32_t n, int32_t j) {
-        int32_t c = d.nchild[n];
+        int32_t c = z.nchild[n];
         for (int32_t i = c; i > j; i--) copy_row(n * MAXN + i, n * MAXN + i - 1);
-        d.nchild[n] = (int8_t)(c + 1);
+        z.nchild[n] = (int8_t)(c + 1);
         if (c + 1 >= MAXN) {
             int32_t nn = split_node(n);
             if (nn < 0) return -1;
@@ -478,15 +456,15 @@ struct Replica {
     MT_HD uint16_t* arena_base(int32_t side) { return d.arena + (int64_t)side * d.caps.acap; }
     /* reserve n units at the arena top; compacts into the other half when full */
     MT_HD int32_t arena_alloc(int32_t n) {
-        if (d.h->arenaTop + n > d.caps.acap) {
+        if (z.h.arenaTop + n > d.caps.acap) {
             arena_gc();
-            if (d.h->arenaTop + n > d.caps.acap) {
+            if (z.h.arenaTop + n > d.caps.acap) {
                 fail(E_CAPACITY);
                 return -1;
             }
         }
-        int32_t off = d.h->arenaTop;
-        d.h->arenaTop = off + n;
+        int32_t off = z.h.arenaTop;
+        z.h.arenaTop = off + n;
         return off;
     }
     MT_HD void arena_copy(uint16_t* dst, const uint16_t* src, int32_t n) {
@@ -498,23 +476,27 @@ struct Replica {
         }
         w.sync();
     }
-    /* copy all live text rows into the other half, in document order */
+    /* copy all live text rows into the other half, in document order. A row id is moved once
+     * per GC even if its slot is transiently duplicated (scour compacts a slab in place). */
     MT_HD void arena_gc() {
-        int32_t from = d.h->arenaSide, to = from ^ 1;
+        int32_t from = z.h.arenaSide, to = from ^ 1;
         uint16_t* src = arena_base(from);
         uint16_t* dst = arena_base(to);
+        int32_t ep = z.h.gcEpoch % 255 + 1;
+        z.h.gcEpoch = ep;
         int32_t top = 0;
-        int32_t T = d.h->nleaf * MAXN;
+        int32_t T = z.h.nleaf * MAXN;
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
-            if (s < 0 || (d.flags[s] & RF_MARKER)) continue;
-            int32_t L = d.len[s];
-            arena_copy(dst + top, src + d.toff[s], L);
-            d.toff[s] = (uint32_t)top;
+            if (s < 0 || (z.flags[s] & RF_MARKER) || cold(s).gc == ep) continue;
+            int32_t L = z.len[s];
+            arena_copy(dst + top, src + cold(s).toff, L);
+            cold(s).toff = (uint32_t)top;
+            cold(s).gc = (uint8_t)ep;
             top += L;
         }
-        d.h->arenaSide = to;
-        d.h->arenaTop = top;
+        z.h.arenaSide = to;
+        z.h.arenaTop = top;
         w.sync();
     }
 
@@ -522,41 +504,53 @@ struct Replica {
     /* Split the row at lorder coordinate t at offset off (0 < off < len). Returns the slot of
      * the LEFT part afterwards (the right part is the next row in document order). */
     MT_HD int32_t split_row(int32_t t, int32_t off) {
-        int32_t n = d.lorder[t >> 3], j = t & 7;
+        int32_t n = z.lorder[t >> 3], j = t & 7;
         int32_t s0 = n * MAXN + j;
-        if (d.flags[s0] & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
-        bool willSplit = d.nchild[n] + 1 >= MAXN;
+        if (z.flags[s0] & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
+        bool willSplit = z.nchild[n] + 1 >= MAXN;
         int32_t rs = leaf_insert_slot(n, j + 1);
         if (rs < 0) return -1;
         /* the left part stays at n*8+j unless the leaf split moved children 4..7 */
         int32_t ls = n * MAXN + j;
-        if (willSplit && j >= 4) ls = d.lorder[d.lpos[n] + 1] * MAXN + (j - 4);
+        if (willSplit && j >= 4) ls = z.lorder[z.lpos[n] + 1] * MAXN + (j - 4);
         copy_row(rs, ls);
-        d.len[rs] = d.len[ls] - off;
-        d.toff[rs] = d.toff[ls] + (uint32_t)off;
-        d.len[ls] = off;
-        d.sid[rs] = (uint32_t)d.h->nextSid++;
-        d.h->nrows++;
-        d.h->sumW += 2;
+        z.rid[rs] = (int16_t)alloc_rid();
+        cold(rs) = cold(ls); /* splitAt copies every field (mergeTree.ts:523-567) */
+        z.len[rs] = z.len[ls] - off;
+        cold(rs).toff = cold(ls).toff + (uint32_t)off;
+        z.len[ls] = off;
+        z.sid[rs] = (uint32_t)z.h.nextSid++;
+        z.h.nrows++;
+        z.h.sumW += 2;
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
          * same pending groups (in the row's FIFO order = log order), appended at the end of each
          * group's segment list */
-        if (d.ng[ls]) {
-            int32_t head = d.h->gqN ? d.gq[d.h->gqHead % d.caps.gcap] : 0x7fffffff;
-            uint32_t lsid = d.sid[ls];
-            int32_t m0 = d.h->memN;
-            for (int32_t i = 0; i < m0; i++)
-                if (d.msid[i] == lsid && d.mgid[i] >= head) mem_append(d.mgid[i], d.sid[rs]);
+        if (z.ng[ls]) {
+            if (z.h.memN + z.ng[ls] > d.caps.mcap) mem_compact();
+            int32_t head = z.h.gqN ? d.gq[z.h.gqHead % d.caps.gcap] : 0x7fffffff;
+            uint32_t lsid = z.sid[ls];
+            uint32_t rsid = z.sid[rs];
+            int32_t m0 = z.h.memN;
+            for (int32_t b = 0; b < m0; b += W::N) {
+                int32_t i = b + w.lane();
+                int32_t g = i < m0 ? d.mgid[i] : -1;
+                uint64_t m = w.ballot(i < m0 && d.msid[i] == lsid && g >= head);
+                while (m) {
+                    int32_t l = W::ffs(m);
+                    m &= m - 1;
+                    mem_append(w.bcast(g, l), rsid);
+                }
+            }
         }
         return ls;
     }
 
     /* ---- segment groups ---------------------------------------------------------------- */
     MT_HD void mem_append(int32_t gid, uint32_t sid) {
-        int32_t m = d.h->memN;
+        int32_t m = z.h.memN;
         if (m >= d.caps.mcap) {
             mem_compact();
-            m = d.h->memN;
+            m = z.h.memN;
             if (m >= d.caps.mcap) {
                 fail(E_CAPACITY);
                 return;
@@ -564,40 +558,48 @@ struct Replica {
         }
         d.mgid[m] = gid;
         d.msid[m] = sid;
-        d.h->memN = m + 1;
+        z.h.memN = m + 1;
     }
+    /* drop entries of groups already acked (gid < head gid): wave stream compaction */
     MT_HD void mem_compact() {
-        /* drop entries of groups already acked (gid < head gid) */
-        int32_t head = d.h->gqN ? d.gq[d.h->gqHead % d.caps.gcap] : 0x7fffffff;
-        int32_t wpos = 0;
-        for (int32_t i = 0; i < d.h->memN; i++) {
-            if (d.mgid[i] >= head) {
-                d.mgid[wpos] = d.mgid[i];
-                d.msid[wpos] = d.msid[i];
-                wpos++;
+        int32_t head = z.h.gqN ? d.gq[z.h.gqHead % d.caps.gcap] : 0x7fffffff;
+        int32_t n = z.h.memN, wpos = 0;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            int32_t g = i < n ? d.mgid[i] : -1;
+            uint32_t sd = i < n ? d.msid[i] : 0;
+            bool keep = i < n && g >= head;
+            int32_t tot;
+            int32_t off = w.excl_scan(keep ? 1 : 0, &tot);
+            w.sync();
+            if (keep) {
+                d.mgid[wpos + off] = g;
+                d.msid[wpos + off] = sd;
             }
+            w.sync();
+            wpos += tot;
         }
-        d.h->memN = wpos;
+        z.h.memN = wpos;
     }
     /* SegmentGroupCollection.enqueue (segmentGroupCollection.ts:28-31) */
     MT_HD void row_enqueue_group(int32_t s, int32_t gid) {
-        int32_t ng = d.ng[s];
+        int32_t ng = z.ng[s];
         if (ng >= 255) {
             fail(E_CAPACITY);
             return;
         }
-        d.ng[s] = (uint8_t)(ng + 1);
-        mem_append(gid, d.sid[s]);
+        z.ng[s] = (uint8_t)(ng + 1);
+        mem_append(gid, z.sid[s]);
     }
     /* addToPendingList (mergeTree.ts:1955-1962); the group id is the op's localSeq */
     MT_HD void pending_add(int32_t s, int32_t gid, bool* created) {
         if (!*created) {
-            if (d.h->gqN >= d.caps.gcap) {
+            if (z.h.gqN >= d.caps.gcap) {
                 fail(E_CAPACITY);
                 return;
             }
-            d.gq[(d.h->gqHead + d.h->gqN) % d.caps.gcap] = gid;
-            d.h->gqN++;
+            d.gq[(z.h.gqHead + z.h.gqN) % d.caps.gcap] = gid;
+            z.h.gqN++;
             *created = true;
         }
         row_enqueue_group(s, gid);
@@ -605,63 +607,63 @@ struct Replica {
 
     /* ---- zamboni heap (collections.ts:212-264, LRUSegmentComparer mergeTree.ts:957-960) ---- */
     MT_HD void heap_add(uint32_t sid, int32_t seq) {
-        int32_t n = d.h->heapN;
-        if (n >= d.caps.hcap) {
+        int32_t n = z.h.heapN;
+        if (n >= HT::H) {
             fail(E_CAPACITY);
             return;
         }
         /* L[k] (1-based) lives at index k-1 */
         int32_t k = n + 1;
-        d.hsid[k - 1] = sid;
-        d.hseq[k - 1] = seq;
-        d.h->heapN = n + 1;
-        if (n + 1 > d.h->hwHeap) d.h->hwHeap = n + 1;
-        while (k > 1 && d.hseq[(k >> 1) - 1] - d.hseq[k - 1] > 0) {
-            uint32_t ts = d.hsid[(k >> 1) - 1];
-            int32_t tq = d.hseq[(k >> 1) - 1];
-            d.hsid[(k >> 1) - 1] = d.hsid[k - 1];
-            d.hseq[(k >> 1) - 1] = d.hseq[k - 1];
-            d.hsid[k - 1] = ts;
-            d.hseq[k - 1] = tq;
+        z.hsid[k - 1] = sid;
+        z.hseq[k - 1] = seq;
+        z.h.heapN = n + 1;
+        if (n + 1 > z.h.hwHeap) z.h.hwHeap = n + 1;
+        while (k > 1 && z.hseq[(k >> 1) - 1] - z.hseq[k - 1] > 0) {
+            uint32_t ts = z.hsid[(k >> 1) - 1];
+            int32_t tq = z.hseq[(k >> 1) - 1];
+            z.hsid[(k >> 1) - 1] = z.hsid[k - 1];
+            z.hseq[(k >> 1) - 1] = z.hseq[k - 1];
+            z.hsid[k - 1] = ts;
+            z.hseq[k - 1] = tq;
             k >>= 1;
         }
     }
     MT_HD void heap_pop(uint32_t* sid, int32_t* seq) {
-        int32_t cnt = d.h->heapN;
-        *sid = d.hsid[0];
-        *seq = d.hseq[0];
-        d.hsid[0] = d.hsid[cnt - 1];
-        d.hseq[0] = d.hseq[cnt - 1];
+        int32_t cnt = z.h.heapN;
+        *sid = z.hsid[0];
+        *seq = z.hseq[0];
+        z.hsid[0] = z.hsid[cnt - 1];
+        z.hseq[0] = z.hseq[cnt - 1];
         cnt--;
-        d.h->heapN = cnt;
+        z.h.heapN = cnt;
         int32_t k = 1;
         while ((k << 1) <= cnt) {
             int32_t j = k << 1;
-            if (j < cnt && d.hseq[j - 1] - d.hseq[j] > 0) j++;
-            if (d.hseq[k - 1] - d.hseq[j - 1] <= 0) break;
-            uint32_t ts = d.hsid[k - 1];
-            int32_t tq = d.hseq[k - 1];
-            d.hsid[k - 1] = d.hsid[j - 1];
-            d.hseq[k - 1] = d.hseq[j - 1];
-            d.hsid[j - 1] = ts;
-            d.hseq[j - 1] = tq;
+            if (j < cnt && z.hseq[j - 1] - z.hseq[j] > 0) j++;
+            if (z.hseq[k - 1] - z.hseq[j - 1] <= 0) break;
+            uint32_t ts = z.hsid[k - 1];
+            int32_t tq = z.hseq[k - 1];
+            z.hsid[k - 1] = z.hsid[j - 1];
+            z.hseq[k - 1] = z.hseq[j - 1];
+            z.hsid[j - 1] = ts;
+            z.hseq[j - 1] = tq;
             k = j;
         }
     }
     /* addToLRUSet (mergeTree.ts:1306-1316) */
     MT_HD void add_lru(int32_t s, int32_t seq) {
         int32_t n = s / MAXN;
-        if (d.nscour[n] != 1 && seq > d.h->currentSeq) {
-            d.nscour[n] = 1;
-            heap_add(d.sid[s], seq);
+        if (z.nscour[n] != 1 && seq > z.h.currentSeq) {
+            z.nscour[n] = 1;
+            heap_add(z.sid[s], seq);
         }
     }
     /* locate a row by stable id; -1 if unlinked */
     MT_HD int32_t find_sid(uint32_t sid) {
-        int32_t T = d.h->nleaf * MAXN;
+        int32_t T = z.h.nleaf * MAXN;
         for (int32_t b = 0; b < T; b += W::N) {
             int32_t s = slot_at(b + w.lane());
-            uint64_t m = w.ballot(s >= 0 && d.sid[s] == sid);
+            uint64_t m = w.ballot(s >= 0 && z.sid[s] == sid);
             if (m) return w.bcast(s, W::ffs(m));
         }
         return -1;
@@ -669,34 +671,34 @@ struct Replica {
 
     /* ---- properties (segmentPropertiesManager.ts:35-111) ---------------------------- */
     MT_HD int32_t key_slot(uint16_t key) {
-        for (int32_t i = 0; i < d.h->nkeys; i++)
-            if (d.h->keys[i] == key) return i;
-        if (d.h->nkeys >= NKEYS) {
+        for (int32_t i = 0; i < z.h.nkeys; i++)
+            if (z.h.keys[i] == key) return i;
+        if (z.h.nkeys >= NKEYS) {
             fail(E_UNSUPPORTED);
             return -1;
         }
-        d.h->keys[d.h->nkeys] = key;
-        return d.h->nkeys++;
+        z.h.keys[z.h.nkeys] = key;
+        return z.h.nkeys++;
     }
     MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
-        if (!(d.flags[s] & RF_PROPS)) {
-            d.prw[s] = 0;
-            d.flags[s] |= RF_PROPS;
+        if (!(z.flags[s] & RF_PROPS)) {
+            cold(s).prw = 0;
+            z.flags[s] |= RF_PROPS;
             for (int k = 0; k < NKEYS; k++) {
-                d.pv[s * NKEYS + k] = 0;
-                d.pk[s * NKEYS + k] = 0;
+                cold(s).pv[k] = 0;
+                cold(s).pk[k] = 0;
             }
         }
-        if (d.prw[s] > 0 && seq != UNASSIGNED_SEQ && collaborating) return;
+        if (cold(s).prw > 0 && seq != UNASSIGNED_SEQ && collaborating) return;
         if (rewrite) {
-            if (collaborating && seq == UNASSIGNED_SEQ) d.prw[s]++;
-            for (int32_t k = 0; k < d.h->nkeys; k++) {
-                if (d.pv[s * NKEYS + k] == 0) continue;
+            if (collaborating && seq == UNASSIGNED_SEQ) cold(s).prw++;
+            for (int32_t k = 0; k < z.h.nkeys; k++) {
+                if (cold(s).pv[k] == 0) continue;
                 bool inNew = false;
                 for (int32_t j = 0; j < nkv; j++)
-                    if (kv[j].key == d.h->keys[k] && kv[j].value != 0 && !(kv[j].value & MT_VALUE_FALSY)) inNew = true;
-                bool modify = seq == UNASSIGNED_SEQ || d.pk[s * NKEYS + k] == 0;
-                if (!inNew && modify) d.pv[s * NKEYS + k] = 0;
+                    if (kv[j].key == z.h.keys[k] && kv[j].value != 0 && !(kv[j].value & MT_VALUE_FALSY)) inNew = true;
+                bool modify = seq == UNASSIGNED_SEQ || cold(s).pk[k] == 0;
+                if (!inNew && modify) cold(s).pv[k] = 0;
             }
         }
         for (int32_t j = 0; j < nkv; j++) {
@@ -704,86 +706,88 @@ struct Replica {
             if (k < 0) return;
             if (collaborating) {
                 if (seq == UNASSIGNED_SEQ) {
-                    if (d.pk[s * NKEYS + k] == 0xFF) {
+                    if (cold(s).pk[k] == 0xFF) {
                         fail(E_CAPACITY);
                         return;
                     }
-                    d.pk[s * NKEYS + k]++;
-                } else if (!(d.pk[s * NKEYS + k] == 0)) {
+                    cold(s).pk[k]++;
+                } else if (!(cold(s).pk[k] == 0)) {
                     continue;
                 }
             }
-            d.pv[s * NKEYS + k] = kv[j].value;
+            cold(s).pv[k] = kv[j].value;
         }
     }
     /* ackPendingProperties (segmentPropertiesManager.ts:19-33) */
     MT_HD void ack_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite) {
-        if (rewrite) d.prw[s]--;
+        if (rewrite) cold(s).prw--;
         for (int32_t j = 0; j < nkv; j++) {
             int32_t k = key_slot(kv[j].key);
             if (k < 0) return;
-            if (d.pk[s * NKEYS + k]) d.pk[s * NKEYS + k]--;
+            if (cold(s).pk[k]) cold(s).pk[k]--;
         }
     }
     MT_HD bool match_props(int32_t a, int32_t b) const { /* matchProperties (properties.ts:61-92) */
-        bool pa = d.flags[a] & RF_PROPS, pb = d.flags[b] & RF_PROPS;
+        bool pa = z.flags[a] & RF_PROPS, pb = z.flags[b] & RF_PROPS;
         if (pa != pb) return false;
         if (!pa) return true;
         for (int k = 0; k < NKEYS; k++)
-            if (d.pv[a * NKEYS + k] != d.pv[b * NKEYS + k]) return false;
+            if (cold(a).pv[k] != cold(b).pv[k]) return false;
         return true;
     }
 
     /* ---- zamboni: scourNode / pack / zamboniSegments (mergeTree.ts:1322-1511) ---------- */
     /* canAppend (textSegment.ts:63-68) */
     MT_HD bool can_append(int32_t a, int32_t b) {
-        if (d.flags[a] & RF_MARKER) return false;
-        int32_t L = d.len[a];
-        if (L > 0 && arena_base(d.h->arenaSide)[d.toff[a] + L - 1] == '\n') return false;
-        if (d.flags[b] & RF_MARKER) return false;
-        return d.len[a] <= GRANULARITY || d.len[b] <= GRANULARITY;
+        if (z.flags[a] & RF_MARKER) return false;
+        int32_t L = z.len[a];
+        if (L > 0 && arena_base(z.h.arenaSide)[cold(a).toff + L - 1] == '\n') return false;
+        if (z.flags[b] & RF_MARKER) return false;
+        return z.len[a] <= GRANULARITY || z.len[b] <= GRANULARITY;
     }
     /* TextSegment.append (textSegment.ts:74-85): the merged text is rebuilt at the arena top */
     MT_HD void append_text(int32_t a, int32_t b) {
-        int32_t La = d.len[a], Lb = d.len[b];
-        uint16_t* base = arena_base(d.h->arenaSide);
-        if ((int32_t)d.toff[a] + La == d.h->arenaTop && d.h->arenaTop + Lb <= d.caps.acap) {
+        int32_t La = z.len[a], Lb = z.len[b];
+        uint16_t* base = arena_base(z.h.arenaSide);
+        if ((int32_t)cold(a).toff + La == z.h.arenaTop && z.h.arenaTop + Lb <= d.caps.acap) {
             int32_t off = arena_alloc(Lb);
-            arena_copy(base + off, base + d.toff[b], Lb);
-        } else if ((int32_t)d.toff[a] + La == (int32_t)d.toff[b]) {
+            arena_copy(base + off, base + cold(b).toff, Lb);
+        } else if ((int32_t)cold(a).toff + La == (int32_t)cold(b).toff) {
             /* already contiguous */
         } else {
             int32_t off = arena_alloc(La + Lb);
             if (off < 0) return;
-            base = arena_base(d.h->arenaSide); /* a GC may have switched halves */
-            arena_copy(base + off, base + d.toff[a], La);
-            arena_copy(base + off + La, base + d.toff[b], Lb);
-            d.toff[a] = (uint32_t)off;
+            base = arena_base(z.h.arenaSide); /* a GC may have switched halves */
+            arena_copy(base + off, base + cold(a).toff, La);
+            arena_copy(base + off + La, base + cold(b).toff, Lb);
+            cold(a).toff = (uint32_t)off;
         }
-        d.len[a] = La + Lb;
+        z.len[a] = La + Lb;
     }
     /* scourNode on leaf n: compacts the slab in place; returns the new child count. Rows are
      * merged into their predecessor or unlinked exactly as the reference decides. */
     MT_HD int32_t scour_leaf(int32_t n) {
-        int32_t c = d.nchild[n];
+        int32_t c = z.nchild[n];
         int32_t wpos = 0;
         int32_t prev = -1; /* slot of prevSegment in the compacted slab */
-        int32_t minSeq = d.h->minSeq;
+        int32_t minSeq = z.h.minSeq;
         for (int32_t k = 0; k < c; k++) {
             int32_t s = n * MAXN + k;
-            if (d.ng[s] == 0) {
-                if (d.rseq[s] != NOREM) {
-                    if (d.rseq[s] > minSeq) {
+            if (z.ng[s] == 0) {
+                if (z.rseq[s] != NOREM) {
+                    if (z.rseq[s] > minSeq) {
                         if (wpos != k) copy_row(n * MAXN + wpos, s);
                         wpos++;
+                    } else {
+                        free_rid(z.rid[s]); /* unlinked */
                     }
-                    /* else: unlinked */
                     prev = -1;
                 } else {
-                    if (d.seq[s] <= minSeq) {
+                    if (z.seq[s] <= minSeq) {
                         bool ok = prev >= 0 && can_append(prev, s) && match_props(prev, s) && local_len(s) > 0;
                         if (ok) {
                             append_text(prev, s);
+                            free_rid(z.rid[s]);
                         } else {
                             int32_t dst = n * MAXN + wpos;
                             if (wpos != k) copy_row(dst, s);
@@ -802,29 +806,29 @@ struct Replica {
                 prev = -1;
             }
         }
-        d.h->nrows -= c - wpos;
-        d.nchild[n] = (int8_t)wpos;
+        z.h.nrows -= c - wpos;
+        z.nchild[n] = (int8_t)wpos;
         return wpos;
     }
     /* pack (mergeTree.ts:1401-1453) of `block`'s parent */
     MT_HD void pack(int32_t block0) {
       int32_t block = block0;
       for (;;) { /* iterative: pack recurses upward while the parent underflows (1447-1452) */
-        int32_t parent = d.nparent[block];
-        int32_t pc = d.nchild[parent];
-        int8_t lvl = d.nlevel[block];
+        int32_t parent = z.nparent[block];
+        int32_t pc = z.nchild[parent];
+        int8_t lvl = z.nlevel[block];
         if (lvl == 0) {
             /* scour every sibling leaf, then redistribute their rows over new leaves */
             int32_t total = 0;
-            for (int32_t i = 0; i < pc; i++) total += scour_leaf(d.kids[parent * MAXN + i]);
+            for (int32_t i = 0; i < pc; i++) total += scour_leaf(z.kids[parent * MAXN + i]);
             int32_t cc = total / (MAXN / 2);
             if (cc > MAXN - 1) cc = MAXN - 1;
             if (cc < 1) cc = 1;
             int32_t base = total / cc, extra = total % cc;
             /* new leaves; rows move from the old slabs (old leaves are read in order) */
             int32_t oldk[MAXN];
-            for (int32_t i = 0; i < pc; i++) oldk[i] = d.kids[parent * MAXN + i];
-            int32_t firstPos = d.lpos[oldk[0]];
+            for (int32_t i = 0; i < pc; i++) oldk[i] = z.kids[parent * MAXN + i];
+            int32_t firstPos = z.lpos[oldk[0]];
             int32_t newk[MAXN];
             int32_t ri = 0, rj = 0; /* read cursor: old leaf index, child index */
             for (int32_t ni = 0; ni < cc; ni++) {
@@ -834,49 +838,49 @@ struct Replica {
                 if (nb < 0) return;
                 newk[ni] = nb;
                 for (int32_t q = 0; q < cnt; q++) {
-                    while (rj >= d.nchild[oldk[ri]]) {
+                    while (rj >= z.nchild[oldk[ri]]) {
                         ri++;
                         rj = 0;
                     }
                     copy_row(nb * MAXN + q, oldk[ri] * MAXN + rj);
                     rj++;
                 }
-                d.nchild[nb] = (int8_t)cnt;
-                d.nparent[nb] = (int16_t)parent;
+                z.nchild[nb] = (int8_t)cnt;
+                z.nparent[nb] = (int16_t)parent;
             }
             for (int32_t i = 0; i < pc; i++) free_node(oldk[i]);
             /* lorder: replace [firstPos, firstPos+pc) with the new leaves */
-            int32_t nl = d.h->nleaf;
+            int32_t nl = z.h.nleaf;
             int32_t delta = cc - pc;
             if (delta < 0) {
                 for (int32_t i = firstPos + pc; i < nl; i++) {
-                    int32_t x = d.lorder[i];
-                    d.lorder[i + delta] = (int16_t)x;
-                    d.lpos[x] = (int16_t)(i + delta);
+                    int32_t x = z.lorder[i];
+                    z.lorder[i + delta] = (int16_t)x;
+                    z.lpos[x] = (int16_t)(i + delta);
                 }
             } else if (delta > 0) {
                 for (int32_t i = nl - 1; i >= firstPos + pc; i--) {
-                    int32_t x = d.lorder[i];
-                    d.lorder[i + delta] = (int16_t)x;
-                    d.lpos[x] = (int16_t)(i + delta);
+                    int32_t x = z.lorder[i];
+                    z.lorder[i + delta] = (int16_t)x;
+                    z.lpos[x] = (int16_t)(i + delta);
                 }
             }
             for (int32_t i = 0; i < cc; i++) {
-                d.lorder[firstPos + i] = (int16_t)newk[i];
-                d.lpos[newk[i]] = (int16_t)(firstPos + i);
+                z.lorder[firstPos + i] = (int16_t)newk[i];
+                z.lpos[newk[i]] = (int16_t)(firstPos + i);
             }
-            d.h->nleaf = nl + delta;
-            for (int32_t i = 0; i < cc; i++) d.kids[parent * MAXN + i] = (int16_t)newk[i];
-            d.nchild[parent] = (int8_t)cc;
+            z.h.nleaf = nl + delta;
+            for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (int16_t)newk[i];
+            z.nchild[parent] = (int8_t)cc;
         } else {
             /* interior: collect grandchildren in order, regroup into new interior nodes */
             int16_t hold[MAXN * MAXN];
             int32_t total = 0;
             int32_t oldk[MAXN];
             for (int32_t i = 0; i < pc; i++) {
-                int32_t cb = d.kids[parent * MAXN + i];
+                int32_t cb = z.kids[parent * MAXN + i];
                 oldk[i] = cb;
-                for (int32_t q = 0; q < d.nchild[cb]; q++) hold[total++] = d.kids[cb * MAXN + q];
+                for (int32_t q = 0; q < z.nchild[cb]; q++) hold[total++] = z.kids[cb * MAXN + q];
             }
             int32_t cc = total / (MAXN / 2);
             if (cc > MAXN - 1) cc = MAXN - 1;
@@ -891,46 +895,46 @@ struct Replica {
                 if (nb < 0) return;
                 for (int32_t q = 0; q < cnt; q++) {
                     int32_t ch = hold[read++];
-                    d.kids[nb * MAXN + q] = (int16_t)ch;
-                    d.nparent[ch] = (int16_t)nb;
+                    z.kids[nb * MAXN + q] = (int16_t)ch;
+                    z.nparent[ch] = (int16_t)nb;
                 }
-                d.nchild[nb] = (int8_t)cnt;
-                d.nparent[nb] = (int16_t)parent;
-                d.kids[parent * MAXN + ni] = (int16_t)nb;
+                z.nchild[nb] = (int8_t)cnt;
+                z.nparent[nb] = (int16_t)parent;
+                z.kids[parent * MAXN + ni] = (int16_t)nb;
             }
-            d.nchild[parent] = (int8_t)cc;
+            z.nchild[parent] = (int8_t)cc;
         }
-        if (!(d.nchild[parent] < MAXN / 2 && d.nparent[parent] >= 0)) return;
+        if (!(z.nchild[parent] < MAXN / 2 && z.nparent[parent] >= 0)) return;
         block = parent;
       }
     }
     /* zamboniSegments (mergeTree.ts:1455-1511) */
     MT_HD void zamboni() {
-        if (!d.h->collaborating) return;
+        if (!z.h.collaborating) return;
         for (int i = 0; i < 2; i++) {
-            if (d.h->heapN < 1) break;
-            if (d.hseq[0] > d.h->minSeq) break;
+            if (z.h.heapN < 1) break;
+            if (z.hseq[0] > z.h.minSeq) break;
             uint32_t sid;
             int32_t mseq;
             heap_pop(&sid, &mseq);
             int32_t s = find_sid(sid);
             if (s < 0) continue;
             int32_t n = s / MAXN;
-            if (d.nscour[n] == 0) continue;
-            int32_t before = d.nchild[n];
+            if (z.nscour[n] == 0) continue;
+            int32_t before = z.nchild[n];
             int32_t after = scour_leaf(n);
-            d.nscour[n] = 0;
+            z.nscour[n] = 0;
             if (after < before) {
-                if (after < MAXN / 2 && d.nparent[n] >= 0) pack(n);
+                if (after < MAXN / 2 && z.nparent[n] >= 0) pack(n);
             }
         }
     }
     /* setMinSeq (mergeTree.ts:1751-1769) */
     MT_HD void set_min_seq(int32_t minSeq) {
-        if (!(minSeq <= d.h->currentSeq)) fail(E_ASSERT);
-        if (!(d.h->minSeq <= minSeq)) fail(E_ASSERT);
-        if (minSeq > d.h->minSeq) {
-            d.h->minSeq = minSeq;
+        if (!(minSeq <= z.h.currentSeq)) fail(E_ASSERT);
+        if (!(z.h.minSeq <= minSeq)) fail(E_ASSERT);
+        if (minSeq > z.h.minSeq) {
+            z.h.minSeq = minSeq;
             zamboni();
         }
     }
@@ -938,21 +942,21 @@ struct Replica {
     /* ---- insert (insertSegments 2001-2031, blockInsert 2174-2257) -------------------- */
     /* breakTie for a zero-length row (2281-2310) */
     MT_HD bool break_tie(int32_t s, int32_t refSeq, int32_t client) const {
-        int32_t rs = d.rseq[s];
+        int32_t rs = z.rseq[s];
         if (rs != NOREM && rs != 0 && rs <= refSeq && rs != UNASSIGNED_SEQ) return false;
-        if (client == d.h->localShort) return true;
-        return d.seq[s] != UNASSIGNED_SEQ;
+        if (client == z.h.localShort) return true;
+        return z.seq[s] != UNASSIGNED_SEQ;
     }
     /* continueFrom (2187-2194): first row after leaf lorder[k] with localNetLength > 0 is a
      * local-pending insert */
     MT_HD bool continue_from(int32_t k) {
-        int32_t T = d.h->nleaf * MAXN;
+        int32_t T = z.h.nleaf * MAXN;
         for (int32_t b = (k + 1) * MAXN; b < T; b += W::N) {
             int32_t s = slot_at(b + w.lane());
             uint64_t m = w.ballot(s >= 0 && local_len(s) > 0);
             if (m) {
                 int32_t f = w.bcast(s, W::ffs(m));
-                return d.seq[f] == UNASSIGNED_SEQ;
+                return z.seq[f] == UNASSIGNED_SEQ;
             }
         }
         return false;
@@ -987,13 +991,13 @@ struct Replica {
             }
         }
         for (;;) {
-            int32_t n = d.lorder[k];
-            int32_t c = d.nchild[n];
+            int32_t n = z.lorder[k];
+            int32_t c = z.nchild[n];
             for (; j < c; j++) {
                 int32_t s = n * MAXN + j;
                 if (vis(s, refSeq, client) > 0 || break_tie(s, refSeq, client)) return leaf_insert_slot(n, j);
             }
-            if (seq != UNASSIGNED_SEQ && k + 1 < d.h->nleaf && continue_from(k)) {
+            if (seq != UNASSIGNED_SEQ && k + 1 < z.h.nleaf && continue_from(k)) {
                 k++;
                 j = 0;
                 continue;
@@ -1005,7 +1009,7 @@ struct Replica {
         int32_t pos = op.pos1;
         ensure_boundary(pos, refSeq, client);
         bool hasL = seq == UNASSIGNED_SEQ;
-        int32_t localSeq = hasL ? ++d.h->localSeq : 0;
+        int32_t localSeq = hasL ? ++z.h.localSeq : 0;
         bool marker = op.seg_kind == MT_SEG_MARKER;
         int32_t L = marker ? 1 : op.text_len;
         if (L > 0) {
@@ -1019,51 +1023,53 @@ struct Replica {
                 fail(E_INSERT_FAILED);
                 return;
             }
-            d.len[s] = L;
-            d.seq[s] = seq;
-            d.rseq[s] = NOREM;
-            d.lseq[s] = localSeq;
-            d.lrseq[s] = 0;
-            d.cli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-            d.rcli[s] = 0;
-            d.flags[s] = (uint8_t)((marker ? RF_MARKER : 0) | (hasL ? RF_LSEQ : 0));
-            d.ng[s] = 0;
-            d.prw[s] = 0;
-            d.ovl[s] = 0;
-            d.sid[s] = (uint32_t)d.h->nextSid++;
-            d.h->nrows++;
-            d.h->sumW++;
+            z.rid[s] = (int16_t)alloc_rid();
+            cold(s).gc = 0;
+            z.len[s] = L;
+            z.seq[s] = seq;
+            z.rseq[s] = NOREM;
+            cold(s).lseq = localSeq;
+            cold(s).lrseq = 0;
+            z.cli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
+            z.rcli[s] = 0;
+            z.flags[s] = (uint8_t)((marker ? RF_MARKER : 0) | (hasL ? RF_LSEQ : 0));
+            z.ng[s] = 0;
+            cold(s).prw = 0;
+            cold(s).ovl = 0;
+            z.sid[s] = (uint32_t)z.h.nextSid++;
+            z.h.nrows++;
+            z.h.sumW++;
             if (marker) {
-                d.toff[s] = (uint32_t)op.pos2;
+                cold(s).toff = (uint32_t)op.pos2;
             } else {
-                d.toff[s] = (uint32_t)off;
-                arena_copy(arena_base(d.h->arenaSide) + off, p.text + op.text_off, L);
+                cold(s).toff = (uint32_t)off;
+                arena_copy(arena_base(z.h.arenaSide) + off, p.text + op.text_off, L);
             }
             for (int k = 0; k < NKEYS; k++) {
-                d.pv[s * NKEYS + k] = 0;
-                d.pk[s * NKEYS + k] = 0;
+                cold(s).pv[k] = 0;
+                cold(s).pk[k] = 0;
             }
             if (op.props) { /* TextSegment.make(text, props): addProperties without collab */
                 const mt_props_rec& pr = p.props[op.props - 1];
                 add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE, 0, false);
             }
-            if (d.h->collaborating) { /* saveIfLocal (2197-2212) */
-                if (seq == UNASSIGNED_SEQ && client == d.h->localShort) {
+            if (z.h.collaborating) { /* saveIfLocal (2197-2212) */
+                if (seq == UNASSIGNED_SEQ && client == z.h.localShort) {
                     bool created = false;
                     pending_add(s, localSeq, &created);
-                } else if (seq > d.h->minSeq) {
+                } else if (seq > z.h.minSeq) {
                     add_lru(s, seq);
                 }
             }
         }
-        if (d.h->collaborating && seq != UNASSIGNED_SEQ) zamboni();
+        if (z.h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
 
     /* ---- range ops: markRangeRemoved (2640-2752) / annotateRange (2598-2638) ----------- */
     template <class F>
     MT_HD void map_range(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
         int32_t run = 0;
-        int32_t T = d.h->nleaf * MAXN;
+        int32_t T = z.h.nleaf * MAXN;
         for (int32_t b = 0; b < T; b += W::N) {
             int32_t t = b + w.lane();
             int32_t s = slot_at(t);
@@ -1085,52 +1091,52 @@ struct Replica {
         ensure_boundary(start, refSeq, client);
         ensure_boundary(end, refSeq, client);
         bool hasL = seq == UNASSIGNED_SEQ;
-        int32_t localSeq = hasL ? ++d.h->localSeq : 0;
+        int32_t localSeq = hasL ? ++z.h.localSeq : 0;
         bool created = false;
         map_range(start, end, refSeq, client, [&](int32_t s) {
-            d.h->sumW++;
-            if (d.rseq[s] != NOREM) {
-                if (d.rseq[s] == UNASSIGNED_SEQ) {
-                    d.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-                    d.rseq[s] = seq;
-                    d.flags[s] &= (uint8_t)~RF_LRSEQ;
+            z.h.sumW++;
+            if (z.rseq[s] != NOREM) {
+                if (z.rseq[s] == UNASSIGNED_SEQ) {
+                    z.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
+                    z.rseq[s] = seq;
+                    z.flags[s] &= (uint8_t)~RF_LRSEQ;
                 } else {
-                    uint64_t ov = d.ovl[s];
+                    uint64_t ov = cold(s).ovl;
                     int k = 0;
                     while (k < NOVL && ((ov >> (8 * k)) & 0xFF)) k++;
                     if (k >= NOVL) {
                         fail(E_UNSUPPORTED);
                     } else {
-                        d.ovl[s] = ov | ((uint64_t)(client + 1) << (8 * k));
+                        cold(s).ovl = ov | ((uint64_t)(client + 1) << (8 * k));
                     }
                 }
             } else {
-                d.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-                d.rseq[s] = seq;
-                d.lrseq[s] = localSeq;
+                z.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
+                z.rseq[s] = seq;
+                cold(s).lrseq = localSeq;
                 if (hasL)
-                    d.flags[s] |= RF_LRSEQ;
+                    z.flags[s] |= RF_LRSEQ;
                 else
-                    d.flags[s] &= (uint8_t)~RF_LRSEQ;
+                    z.flags[s] &= (uint8_t)~RF_LRSEQ;
             }
-            if (d.h->collaborating) {
-                if (d.rseq[s] == UNASSIGNED_SEQ && client == d.h->localShort)
+            if (z.h.collaborating) {
+                if (z.rseq[s] == UNASSIGNED_SEQ && client == z.h.localShort)
                     pending_add(s, localSeq, &created);
                 else
                     add_lru(s, seq);
             }
         });
-        if (d.h->collaborating && seq != UNASSIGNED_SEQ) zamboni();
+        if (z.h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
     MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t refSeq,
                               int32_t client, int32_t seq) {
         ensure_boundary(start, refSeq, client);
         ensure_boundary(end, refSeq, client);
-        int32_t localSeq = seq == UNASSIGNED_SEQ ? ++d.h->localSeq : 0;
+        int32_t localSeq = seq == UNASSIGNED_SEQ ? ++z.h.localSeq : 0;
         bool created = false;
-        bool collab = d.h->collaborating;
+        bool collab = z.h.collaborating;
         map_range(start, end, refSeq, client, [&](int32_t s) {
-            d.h->sumW++;
+            z.h.sumW++;
             add_props(s, kv, nkv, rewrite, seq, collab);
             if (collab) {
                 if (seq == UNASSIGNED_SEQ)
@@ -1139,51 +1145,58 @@ struct Replica {
                     add_lru(s, seq);
             }
         });
-        if (d.h->collaborating && seq != UNASSIGNED_SEQ) zamboni();
+        if (z.h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
 
     /* ---- ack (mergeTree.ts:1926-1953, BaseSegment.ack 486-521) ------------------------ */
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
-        if (d.h->gqN > 0) {
-            int32_t gid = d.gq[d.h->gqHead % d.caps.gcap];
-            d.h->gqHead = (d.h->gqHead + 1) % d.caps.gcap;
-            d.h->gqN--;
-            for (int32_t i = 0; i < d.h->memN; i++) {
-                if (d.mgid[i] != gid) continue;
-                int32_t s = find_sid(d.msid[i]);
-                if (s < 0) {
-                    fail(E_ASSERT);
-                    continue;
+        if (z.h.gqN > 0) {
+            int32_t gid = d.gq[z.h.gqHead % d.caps.gcap];
+            z.h.gqHead = (z.h.gqHead + 1) % d.caps.gcap;
+            z.h.gqN--;
+            int32_t mn = z.h.memN;
+            for (int32_t b = 0; b < mn; b += W::N) {
+                int32_t i = b + w.lane();
+                uint32_t sd = i < mn ? d.msid[i] : 0;
+                uint64_t msk = w.ballot(i < mn && d.mgid[i] == gid);
+                while (msk) {
+                    int32_t l = W::ffs(msk);
+                    msk &= msk - 1;
+                    int32_t s = find_sid((uint32_t)w.bcast((int32_t)sd, l));
+                    if (s < 0) {
+                        fail(E_ASSERT);
+                        continue;
+                    }
+                    /* dequeue the row's head group (groups are acked in FIFO order: this one) */
+                    int32_t ng = z.ng[s];
+                    if (ng < 1) fail(E_ASSERT);
+                    if (ng > 0) z.ng[s] = (uint8_t)(ng - 1);
+                    if (kind == MT_OP_ANNOTATE) {
+                        if (!(z.flags[s] & RF_PROPS)) fail(E_ASSERT);
+                        ack_props(s, kv, nkv, rewrite);
+                    } else if (kind == MT_OP_INSERT) {
+                        if (z.seq[s] != UNASSIGNED_SEQ) fail(E_ASSERT);
+                        z.seq[s] = seq;
+                        z.flags[s] &= (uint8_t)~RF_LSEQ;
+                    } else if (kind == MT_OP_REMOVE) {
+                        if (z.rseq[s] == NOREM || z.rseq[s] == 0) fail(E_ASSERT);
+                        z.flags[s] &= (uint8_t)~RF_LRSEQ;
+                        if (z.rseq[s] == UNASSIGNED_SEQ) z.rseq[s] = seq;
+                    } else {
+                        fail(E_ASSERT);
+                    }
+                    add_lru(s, seq);
                 }
-                /* dequeue the row's head group (groups are acked in FIFO order, so it is this one) */
-                int32_t ng = d.ng[s];
-                if (ng < 1) fail(E_ASSERT);
-                if (ng > 0) d.ng[s] = (uint8_t)(ng - 1);
-                if (kind == MT_OP_ANNOTATE) {
-                    if (!(d.flags[s] & RF_PROPS)) fail(E_ASSERT);
-                    ack_props(s, kv, nkv, rewrite);
-                } else if (kind == MT_OP_INSERT) {
-                    if (d.seq[s] != UNASSIGNED_SEQ) fail(E_ASSERT);
-                    d.seq[s] = seq;
-                    d.flags[s] &= (uint8_t)~RF_LSEQ;
-                } else if (kind == MT_OP_REMOVE) {
-                    if (d.rseq[s] == NOREM || d.rseq[s] == 0) fail(E_ASSERT);
-                    d.flags[s] &= (uint8_t)~RF_LRSEQ;
-                    if (d.rseq[s] == UNASSIGNED_SEQ) d.rseq[s] = seq;
-                } else {
-                    fail(E_ASSERT);
-                }
-                add_lru(s, seq);
             }
-            /* drop this group's membership entries when it heads the log */
-            if (d.h->memN > 0 && d.h->memN >= d.caps.mcap / 2) mem_compact();
+            /* drop the acked group's membership entries */
+            mem_compact();
         }
         zamboni();
     }
 
     /* ---- Client.applyMsg (client.ts:797-819) / local edits ---------------------------- */
     MT_HD void apply(const mt_op_rec& op, const Pools& p) {
-        if (d.h->err) return;
+        if (z.h.err) return;
         int32_t kind = op.kind & MT_OP_KIND_MASK;
         const mt_kv* kv = 0;
         int32_t nkv = 0;
@@ -1195,9 +1208,9 @@ struct Replica {
             rw = pr.combining == MT_COMBINE_REWRITE;
         }
         if (op.kind & MT_OPF_LOCAL) {
-            int32_t client = d.h->collaborating ? d.h->localShort : -1;
-            int32_t refSeq = d.h->currentSeq;
-            int32_t seq = d.h->collaborating ? UNASSIGNED_SEQ : UNIVERSAL_SEQ;
+            int32_t client = z.h.collaborating ? z.h.localShort : -1;
+            int32_t refSeq = z.h.currentSeq;
+            int32_t seq = z.h.collaborating ? UNASSIGNED_SEQ : UNIVERSAL_SEQ;
             /* getValidOpRange (client.ts:486-548) */
             int32_t length = length_local();
             int32_t start = op.pos1, end = op.pos2;
@@ -1215,14 +1228,14 @@ struct Replica {
             } else if (kind == MT_OP_ANNOTATE) {
                 annotate_range(start, end, kv, nkv, rw, refSeq, client, seq);
             }
-            d.h->opsDone++;
+            z.h.opsDone++;
             return;
         }
         get_or_add_short(op.client);
-        d.h->seqOps++;
-        d.h->sumR += d.h->nrows;
+        z.h.seqOps++;
+        z.h.sumR += z.h.nrows;
         if (kind != MT_OP_NOOP) {
-            if ((int32_t)op.client == d.h->localLong) {
+            if ((int32_t)op.client == z.h.localLong) {
                 ack(kind, kv, nkv, rw, op.seq);
             } else {
                 int32_t client = get_or_add_short(op.client);
@@ -1232,36 +1245,36 @@ struct Replica {
                     mark_range_removed(op.pos1, op.pos2, op.ref_seq, client, op.seq);
                 else if (kind == MT_OP_ANNOTATE)
                     annotate_range(op.pos1, op.pos2, kv, nkv, rw, op.ref_seq, client, op.seq);
-                if (!(d.h->currentSeq < op.seq)) fail(E_ASSERT);
-                if (!(d.h->minSeq <= op.min_seq)) fail(E_ASSERT);
+                if (!(z.h.currentSeq < op.seq)) fail(E_ASSERT);
+                if (!(z.h.minSeq <= op.min_seq)) fail(E_ASSERT);
             }
         }
         /* updateSeqNumbers (client.ts:821-828) */
-        if (!(d.h->currentSeq <= op.seq)) fail(E_ASSERT);
-        d.h->currentSeq = op.seq;
+        if (!(z.h.currentSeq <= op.seq)) fail(E_ASSERT);
+        z.h.currentSeq = op.seq;
         if (!(op.min_seq <= op.seq)) fail(E_ASSERT);
         set_min_seq(op.min_seq);
-        d.h->opsDone++;
-        int32_t slots = d.h->nleaf * MAXN;
-        if (slots > d.h->hwSlots) d.h->hwSlots = slots;
+        z.h.opsDone++;
+        int32_t slots = z.h.nleaf * MAXN;
+        if (slots > z.h.hwSlots) z.h.hwSlots = slots;
     }
-    MT_HD int32_t length_local() { return length(d.h->currentSeq, d.h->localShort); }
+    MT_HD int32_t length_local() { return length(z.h.currentSeq, z.h.localShort); }
 
     /* ---- reads: text (MergeTreeTextHelper.getText, textSegment.ts:154-275) ------------ */
     /* Writes at most cap units; returns the text length under the perspective. */
     MT_HD int64_t get_text(int32_t refSeq, int32_t client, uint16_t* out, int64_t cap) {
         int64_t n = 0;
-        int32_t T = d.h->nleaf * MAXN;
-        const uint16_t* base = arena_base(d.h->arenaSide);
+        int32_t T = z.h.nleaf * MAXN;
+        const uint16_t* base = arena_base(z.h.arenaSide);
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
-            if (s < 0 || (d.flags[s] & RF_MARKER)) continue;
+            if (s < 0 || (z.flags[s] & RF_MARKER)) continue;
             int32_t v = vis(s, refSeq, client);
             if (v <= 0) continue;
             if (out) {
                 int32_t m = v;
                 if (n + m > cap) m = (int32_t)(cap - n > 0 ? cap - n : 0);
-                arena_copy(out + n, base + d.toff[s], m);
+                arena_copy(out + n, base + cold(s).toff, m);
             }
             n += v;
         }
@@ -1287,7 +1300,7 @@ struct Replica {
             }
         k->n += len;
     }
-    MT_HD int32_t long_of(uint8_t sh) const { return sh == LOCAL_CLIENT ? -1 : (int32_t)d.s2l[sh]; }
+    MT_HD int32_t long_of(uint8_t sh) const { return sh == LOCAL_CLIENT ? -1 : (int32_t)z.s2l[sh]; }
     /* Serial dump (only lane 0 writes the buffer); returns the byte count. */
     MT_HD int64_t dump(uint8_t* out, int64_t cap) {
         Sink k = {w.lane() == 0 ? out : 0, cap, 0, MT_FNV_OFFSET, false};
@@ -1301,59 +1314,59 @@ struct Replica {
     }
     MT_HD void dump_to(Sink* o) {
         int32_t nsegs = 0;
-        int32_t T = d.h->nleaf * MAXN;
+        int32_t T = z.h.nleaf * MAXN;
         for (int32_t t = 0; t < T; t++)
             if (slot_at(t) >= 0) nsegs++;
-        int32_t hdr[6] = {d.h->currentSeq, d.h->minSeq, d.h->localSeq, length_local(), nsegs, d.h->nleaf};
+        int32_t hdr[6] = {z.h.currentSeq, z.h.minSeq, z.h.localSeq, length_local(), nsegs, z.h.nleaf};
         put_bytes(o, hdr, sizeof(hdr));
-        const uint16_t* base = arena_base(d.h->arenaSide);
+        const uint16_t* base = arena_base(z.h.arenaSide);
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
             if (s < 0) continue;
-            uint8_t fl = d.flags[s];
-            bool rem = d.rseq[s] != NOREM;
+            uint8_t fl = z.flags[s];
+            bool rem = z.rseq[s] != NOREM;
             int nov = 0;
-            while (nov < NOVL && ((d.ovl[s] >> (8 * nov)) & 0xFF)) nov++;
+            while (nov < NOVL && ((cold(s).ovl >> (8 * nov)) & 0xFF)) nov++;
             int np = 0;
             if (fl & RF_PROPS)
                 for (int k = 0; k < NKEYS; k++)
-                    if (d.pv[s * NKEYS + k]) np++;
+                    if (cold(s).pv[k]) np++;
             uint8_t b4[4] = {(uint8_t)((fl & RF_MARKER) ? MT_SEG_MARKER : MT_SEG_TEXT),
                              (uint8_t)(((fl & RF_PROPS) ? MT_DF_HAS_PROPS : 0) | (rem ? MT_DF_REMOVED : 0) |
                                        ((fl & RF_LSEQ) ? MT_DF_LSEQ : 0) | ((fl & RF_LRSEQ) ? MT_DF_LRSEQ : 0)),
-                             (uint8_t)nov, d.ng[s]};
+                             (uint8_t)nov, z.ng[s]};
             put_bytes(o, b4, 4);
-            int32_t f[8] = {d.len[s],
-                            d.seq[s],
-                            long_of(d.cli[s]),
-                            rem ? d.rseq[s] : 0,
-                            rem ? long_of(d.rcli[s]) : 0,
-                            (fl & RF_LSEQ) ? d.lseq[s] : 0,
-                            (fl & RF_LRSEQ) ? d.lrseq[s] : 0,
+            int32_t f[8] = {z.len[s],
+                            z.seq[s],
+                            long_of(z.cli[s]),
+                            rem ? z.rseq[s] : 0,
+                            rem ? long_of(z.rcli[s]) : 0,
+                            (fl & RF_LSEQ) ? cold(s).lseq : 0,
+                            (fl & RF_LRSEQ) ? cold(s).lrseq : 0,
                             t >> 3};
             put_bytes(o, f, sizeof(f));
             for (int k = 0; k < nov; k++) {
-                int32_t lo = long_of((uint8_t)(((d.ovl[s] >> (8 * k)) & 0xFF) - 1));
+                int32_t lo = long_of((uint8_t)(((cold(s).ovl >> (8 * k)) & 0xFF) - 1));
                 put_bytes(o, &lo, 4);
             }
-            uint16_t h2[2] = {(uint16_t)np, (uint16_t)((fl & RF_MARKER) ? d.toff[s] : 0)};
+            uint16_t h2[2] = {(uint16_t)np, (uint16_t)((fl & RF_MARKER) ? cold(s).toff : 0)};
             put_bytes(o, h2, 4);
             /* props sorted by global key id */
             int32_t last = -1;
             for (int q = 0; q < np; q++) {
                 int32_t best = -1, bk = 0x7fffffff;
                 for (int k = 0; k < NKEYS; k++) {
-                    int32_t key = d.h->keys[k];
-                    if (d.pv[s * NKEYS + k] && key > last && key < bk) {
+                    int32_t key = z.h.keys[k];
+                    if (cold(s).pv[k] && key > last && key < bk) {
                         bk = key;
                         best = k;
                     }
                 }
-                uint16_t kv2[2] = {(uint16_t)bk, d.pv[s * NKEYS + best]};
+                uint16_t kv2[2] = {(uint16_t)bk, cold(s).pv[best]};
                 put_bytes(o, kv2, 4);
                 last = bk;
             }
-            if (!(fl & RF_MARKER)) put_bytes(o, base + d.toff[s], 2 * (int64_t)d.len[s]);
+            if (!(fl & RF_MARKER)) put_bytes(o, base + cold(s).toff, 2 * (int64_t)z.len[s]);
         }
     }
     MT_HD static uint64_t fnv(const uint8_t* p, int64_t n) {
@@ -1368,7 +1381,7 @@ struct Replica {
     MT_HD void replay(const Pools& p) {
         for (int64_t i = 0; i < p.nops; i++) {
             apply(p.ops[i], p);
-            if (d.h->err) break;
+            if (z.h.err) break;
         }
     }
 };

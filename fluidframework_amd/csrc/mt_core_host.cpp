@@ -18,31 +18,48 @@
 using namespace mt;
 
 struct mth_store {
-    Cols c;
-    Caps k;
+    int profile;
     int64_t ndocs;
+    Store<HotSmall> s0;
+    Store<HotMid> s1;
+    Store<HotBig> s2;
     uint8_t* mem;
 };
+
+/* call F with a Replica<WaveHost, HT> for doc d of the store's profile */
+template <class F>
+static auto with_replica(mth_store* s, int64_t d, F&& f) {
+    if (s->profile == 0) {
+        Replica<WaveHost, HotSmall> r(s->s0.doc(d), WaveHost());
+        return f(r);
+    } else if (s->profile == 1) {
+        Replica<WaveHost, HotMid> r(s->s1.doc(d), WaveHost());
+        return f(r);
+    }
+    Replica<WaveHost, HotBig> r(s->s2.doc(d), WaveHost());
+    return f(r);
+}
 
 extern "C" {
 
 mth_store* mth_create(int64_t ndocs, const int32_t* caps6) {
-    Caps k = {caps6[0], caps6[1], caps6[2], caps6[3], caps6[4], caps6[5]};
-    if (!caps_valid(k) || ndocs < 1) return nullptr;
+    /* caps6 = (ncap, hcap[ignored: 2*ncap], acap, mcap, gcap, ccap[ignored: 64]) */
+    Caps k = {caps6[2], caps6[3], caps6[4]};
+    int prof = profile_for(caps6[0]);
+    if (!caps_valid(k) || ndocs < 1 || prof < 0) return nullptr;
     mth_store* s = (mth_store*)calloc(1, sizeof(mth_store));
-    s->k = k;
+    s->profile = prof;
     s->ndocs = ndocs;
-    size_t bytes = layout(s->c, k, ndocs, nullptr);
-    s->mem = (uint8_t*)calloc(1, bytes);
+    int64_t bytes = prof == 0 ? store_layout(s->s0, k, ndocs)
+                  : prof == 1 ? store_layout(s->s1, k, ndocs)
+                              : store_layout(s->s2, k, ndocs);
+    s->mem = (uint8_t*)calloc(1, (size_t)bytes);
     if (!s->mem) {
         free(s);
         return nullptr;
     }
-    layout(s->c, k, ndocs, s->mem);
-    for (int64_t d = 0; d < ndocs; d++) {
-        Replica<WaveHost> r(doc_view(s->c, k, d), WaveHost());
-        r.init();
-    }
+    s->s0.base = s->s1.base = s->s2.base = s->mem;
+    for (int64_t d = 0; d < ndocs; d++) with_replica(s, d, [](auto& r) { r.init(); return 0; });
     return s;
 }
 
@@ -53,74 +70,82 @@ void mth_destroy(mth_store* s) {
 }
 
 void mth_start_collab(mth_store* s, int64_t doc, int32_t long_id, int32_t min_seq, int32_t cur_seq) {
-    Replica<WaveHost> r(doc_view(s->c, s->k, doc), WaveHost());
-    r.start_collab(long_id, min_seq, cur_seq);
+    with_replica(s, doc, [&](auto& r) { r.start_collab(long_id, min_seq, cur_seq); return 0; });
 }
 
 int32_t mth_apply(mth_store* s, int64_t doc, const mt_op_rec* op, const uint16_t* text, const mt_props_rec* props,
                   const mt_kv* kv) {
-    Replica<WaveHost> r(doc_view(s->c, s->k, doc), WaveHost());
-    Pools p = {op, 1, text, props, kv};
-    r.apply(*op, p);
-    return r.d.h->err;
+    return with_replica(s, doc, [&](auto& r) {
+        Pools p = {op, 1, text, props, kv};
+        r.apply(*op, p);
+        return r.z.h.err;
+    });
 }
 
 int32_t mth_replay(mth_store* s, int64_t doc, const mt_op_rec* ops, int64_t n, const uint16_t* text,
                    const mt_props_rec* props, const mt_kv* kv) {
-    Replica<WaveHost> r(doc_view(s->c, s->k, doc), WaveHost());
-    Pools p = {ops, n, text, props, kv};
-    r.replay(p);
-    return r.d.h->err;
+    return with_replica(s, doc, [&](auto& r) {
+        Pools p = {ops, n, text, props, kv};
+        r.replay(p);
+        return r.z.h.err;
+    });
 }
 
-int32_t mth_error(mth_store* s, int64_t doc) { return s->c.hdr[doc].err; }
-int32_t mth_error_op(mth_store* s, int64_t doc) { return s->c.hdr[doc].errOp; }
+int32_t mth_error(mth_store* s, int64_t doc) {
+    return with_replica(s, doc, [](auto& r) { return r.z.h.err; });
+}
+int32_t mth_error_op(mth_store* s, int64_t doc) {
+    return with_replica(s, doc, [](auto& r) { return r.z.h.errOp; });
+}
 
 int32_t mth_length(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client) {
-    Replica<WaveHost> r(doc_view(s->c, s->k, doc), WaveHost());
-    if (long_client < 0) return r.length_local();
-    int32_t sh = r.short_of(long_client);
-    if (sh < 0) sh = 0x7fff; /* an unseen client sees only sequenced content */
-    return r.length(ref_seq, sh);
+    return with_replica(s, doc, [&](auto& r) {
+        if (long_client < 0) return r.length_local();
+        int32_t sh = r.short_of(long_client);
+        if (sh < 0) sh = 0x7fff; /* an unseen client sees only sequenced content */
+        return r.length(ref_seq, sh);
+    });
 }
 int32_t mth_length_local(mth_store* s, int64_t doc) {
-    Replica<WaveHost> r(doc_view(s->c, s->k, doc), WaveHost());
-    return r.length_local();
+    return with_replica(s, doc, [](auto& r) { return r.length_local(); });
 }
 
 int64_t mth_text(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* out, int64_t cap) {
-    Replica<WaveHost> r(doc_view(s->c, s->k, doc), WaveHost());
-    int32_t sh;
-    if (long_client < 0) {
-        sh = r.d.h->localShort;
-        ref_seq = r.d.h->currentSeq;
-    } else {
-        sh = r.short_of(long_client);
-        if (sh < 0) sh = 0x7fff;
-    }
-    return r.get_text(ref_seq, sh, out, cap);
+    return with_replica(s, doc, [&](auto& r) {
+        int32_t sh;
+        int32_t rs = ref_seq;
+        if (long_client < 0) {
+            sh = r.z.h.localShort;
+            rs = r.z.h.currentSeq;
+        } else {
+            sh = r.short_of(long_client);
+            if (sh < 0) sh = 0x7fff;
+        }
+        return r.get_text(rs, sh, out, cap);
+    });
 }
 
 int64_t mth_dump(mth_store* s, int64_t doc, uint8_t* out, int64_t cap) {
-    Replica<WaveHost> r(doc_view(s->c, s->k, doc), WaveHost());
-    return r.dump(out, cap);
+    return with_replica(s, doc, [&](auto& r) { return r.dump(out, cap); });
 }
 
 uint64_t mth_digest(mth_store* s, int64_t doc) {
-    Replica<WaveHost> r(doc_view(s->c, s->k, doc), WaveHost());
-    return r.digest();
+    return with_replica(s, doc, [](auto& r) { return r.digest(); });
 }
 
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {
-    DocHdr* h = &s->c.hdr[doc];
-    out8[0] = h->nleaf;
-    out8[1] = h->hwSlots;
-    out8[2] = h->hwHeap;
-    out8[3] = h->heapN;
-    out8[4] = h->memN;
-    out8[5] = h->arenaTop;
-    out8[6] = s->k.ncap - h->nfree;
-    out8[7] = h->opsDone;
+    with_replica(s, doc, [&](auto& r) {
+        DocHdr* h = &r.z.h;
+        out8[0] = h->nleaf;
+        out8[1] = h->hwSlots;
+        out8[2] = h->hwHeap;
+        out8[3] = h->heapN;
+        out8[4] = h->memN;
+        out8[5] = h->arenaTop;
+        out8[6] = (int32_t)(sizeof(r.z.nparent) / sizeof(int16_t)) - h->nfree;
+        out8[7] = h->opsDone;
+        return 0;
+    });
 }
 
 } /* extern "C" */

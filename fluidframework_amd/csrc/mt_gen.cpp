@@ -63,43 +63,43 @@ static int32_t uni(rng_t* r, int32_t lo, int32_t hi) {
 }
 
 /* ---- model replica ---------------------------------------------------------------------- */
+template <class HT>
 struct Model {
-    Cols c;
-    Caps k;
+    Store<HT> st;
     uint8_t* mem;
-    Replica<WaveHost>* r;
+    Replica<WaveHost, HT>* r;
     const mt_props_rec* props;
     const mt_kv* kv;
     const uint16_t* text;
     bool ok;
 };
-static void model_init(Model* m, const mtg_params* P, int32_t local_long) {
-    m->k = Caps{P->model_ncap > 0 ? P->model_ncap : 2048, 0, 0, 0, 0, 64};
-    m->k.hcap = m->k.ncap * 2;
-    m->k.acap = P->model_acap > 0 ? P->model_acap : (1 << 17);
-    m->k.mcap = 1 << 14;
-    m->k.gcap = 4096;
-    size_t bytes = layout(m->c, m->k, 1, nullptr);
-    m->mem = (uint8_t*)calloc(1, bytes);
+template <class HT>
+static void model_init(Model<HT>* m, const mtg_params* P, int32_t local_long) {
+    Caps k = {P->model_acap > 0 ? P->model_acap : (1 << 17), 1 << 14, 4096};
+    int64_t bytes = store_layout(m->st, k, 1);
+    m->mem = (uint8_t*)calloc(1, (size_t)bytes);
     m->ok = m->mem != nullptr;
     if (!m->ok) return;
-    layout(m->c, m->k, 1, m->mem);
-    m->r = new Replica<WaveHost>(doc_view(m->c, m->k, 0), WaveHost());
+    m->st.base = m->mem;
+    m->r = new Replica<WaveHost, HT>(m->st.doc(0), WaveHost());
     m->r->init();
     m->r->start_collab(local_long, 0, 0);
 }
-static void model_free(Model* m) {
+template <class HT>
+static void model_free(Model<HT>* m) {
     delete m->r;
     free(m->mem);
 }
 /* length under the perspective of long client `cl` at refSeq (lp: the replica's local view) */
-static int32_t m_length(Model* m, int32_t refSeq, int32_t cl, int lp) {
+template <class HT>
+static int32_t m_length(Model<HT>* m, int32_t refSeq, int32_t cl, int lp) {
     if (lp) return m->r->length_local();
     int32_t sh = m->r->short_of(cl);
     if (sh < 0) sh = 0x7fff;
     return m->r->length(refSeq, sh);
 }
-static void m_apply(Model* m, const mt_op_rec* e) {
+template <class HT>
+static void m_apply(Model<HT>* m, const mt_op_rec* e) {
     Pools p = {e, 1, m->text, m->props, m->kv};
     m->r->apply(*e, p);
 }
@@ -130,7 +130,8 @@ static const char ALNUM[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxy
 static int ann_props(rng_t* r) { return 1 + uni(r, 0, ANN_RECORDS - 1); }
 
 /* Draw an op valid for perspective (refSeq, client); kind forced to insert on an empty view. */
-static void gen_op(const mtg_params* P, rng_t* r, Model* m, int32_t refSeq, int32_t client, int lp, Out* o,
+template <class HT>
+static void gen_op(const mtg_params* P, rng_t* r, Model<HT>* m, int32_t refSeq, int32_t client, int lp, Out* o,
                    mt_op_rec* e, int insert_index) {
     int32_t len = m_length(m, refSeq, client, lp);
     int roll = uni(r, 0, 99);
@@ -167,13 +168,14 @@ typedef struct {
     int32_t target;
 } Pending;
 
-static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {
+template <class HT>
+static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {
     rng_t r;
     seed(&r, P->seed_base + (uint64_t)doc);
     int nclients = P->nclients < 2 ? 2 : P->nclients;
     if (nclients > 32) nclients = 32;
     int me = P->mode == MTG_OBSERVER ? 0 : 1;
-    Model m;
+    Model<HT> m;
     model_init(&m, P, me);
     if (!m.ok) {
         o->overflow = 1;
@@ -186,7 +188,7 @@ static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec
     int insert_index = 0;
     int32_t seq = 0;
     if (P->mode == MTG_OBSERVER) {
-        while (seq < P->ops_per_doc && !o->overflow && !m.r->d.h->err) {
+        while (seq < P->ops_per_doc && !o->overflow && !m.r->z.h.err) {
             int client = uni(&r, 1, nclients - 1);
             int32_t ref = seq; /* refSeq = seq - 1 for the op sequenced now */
             mt_op_rec* e = emit(o);
@@ -204,8 +206,8 @@ static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec
         Pending* q = (Pending*)malloc(sizeof(Pending) * (P->ops_per_doc + 16));
         int qh = 0, qn = 0;
         int32_t lastTarget = 0, msn = 0;
-        while (seq < P->ops_per_doc && !o->overflow && !m.r->d.h->err) {
-            int32_t cur = m.r->d.h->currentSeq;
+        while (seq < P->ops_per_doc && !o->overflow && !m.r->z.h.err) {
+            int32_t cur = m.r->z.h.currentSeq;
             /* 1. a local edit, made against the local view (client.ts:164-211) */
             if (P->local_pct && uni(&r, 0, 99) < P->local_pct && qn < 4000) {
                 mt_op_rec* e = emit(o);
@@ -269,8 +271,14 @@ static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec
         }
         free(q);
     }
-    if (m.r->d.h->err) o->overflow = 2;
+    if (m.r->z.h.err) o->overflow = 2;
     model_free(&m);
+}
+static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {
+    if (P->model_ncap > HotMid::N)
+        gen_doc_t<HotBig>(P, doc, o, props, kv);
+    else
+        gen_doc_t<HotMid>(P, doc, o, props, kv);
 }
 
 /* ---- batch API --------------------------------------------------------------------------- */

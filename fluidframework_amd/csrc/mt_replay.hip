@@ -14,6 +14,8 @@
 #include <string.h>
 
 #include <string>
+#include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/mt_engine.h"
@@ -25,56 +27,86 @@ using namespace mt;
 
 #define WG 64
 
-__global__ __launch_bounds__(WG) void k_init(Cols c, Caps k, int64_t ndocs) {
+template <class HT>
+__global__ __launch_bounds__(WG) void k_init(Store<HT> st, int64_t ndocs) {
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
-    Replica<WaveGPU> r(doc_view(c, k, d), WaveGPU());
+    Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
     r.init();
 }
 
-__global__ __launch_bounds__(WG) void k_start_collab(Cols c, Caps k, int64_t ndocs, const int32_t* local_long,
+template <class HT>
+__global__ __launch_bounds__(WG) void k_start_collab(Store<HT> st, int64_t ndocs, const int32_t* local_long,
                                                     int32_t min_seq, int32_t cur_seq) {
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
-    Replica<WaveGPU> r(doc_view(c, k, d), WaveGPU());
+    Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
     r.start_collab(local_long[d], min_seq, cur_seq);
 }
 
-/* K1-K4 fused: the whole event stream of a document, one wave per document. */
-__global__ __launch_bounds__(WG) void k_replay(Cols c, Caps k, int64_t ndocs, const mt_op_rec* ops,
+/* 16-byte vector copy of a hot image by the wave (HT is a multiple of 16 bytes) */
+template <class HT>
+__device__ inline void copy_image(HT* dst, const HT* src) {
+    static_assert(sizeof(HT) % 16 == 0, "hot image must be 16-byte granular");
+    const uint4* s = (const uint4*)src;
+    uint4* d = (uint4*)dst;
+    constexpr int n = sizeof(HT) / 16;
+    for (int i = threadIdx.x; i < n; i += WG) d[i] = s[i];
+}
+
+/* K1-K4 fused: the whole event stream of a document, one wave per document. For the small
+ * profile the hot image is staged into LDS for the whole replay. */
+template <class HT, bool LDS>
+__global__ __launch_bounds__(WG) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
                                               const int64_t* kv_off) {
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
-    Replica<WaveGPU> r(doc_view(c, k, d), WaveGPU());
     Pools p;
     p.ops = ops + op_off[d];
     p.nops = op_off[d + 1] - op_off[d];
     p.text = text + text_off[d];
     p.props = props + props_off[d];
     p.kv = kv + kv_off[d];
-    r.replay(p);
+    Doc<HT> v = st.doc(d);
+    if constexpr (LDS) {
+        __shared__ __attribute__((aligned(16))) HT hot;
+        HT* g = v.t;
+        copy_image(&hot, g);
+        __syncthreads();
+        v.t = &hot;
+        Replica<WaveGPU, HT> r(v, WaveGPU());
+        r.replay(p);
+        __syncthreads();
+        copy_image(g, &hot);
+    } else {
+        Replica<WaveGPU, HT> r(v, WaveGPU());
+        r.replay(p);
+    }
 }
 
 /* K5: per-doc digest of the canonical dump */
-__global__ __launch_bounds__(WG) void k_digest(Cols c, Caps k, int64_t ndocs, uint64_t* out) {
+template <class HT>
+__global__ __launch_bounds__(WG) void k_digest(Store<HT> st, int64_t ndocs, uint64_t* out) {
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
-    Replica<WaveGPU> r(doc_view(c, k, d), WaveGPU());
+    Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
     uint64_t h = r.digest();
     if (threadIdx.x == 0) out[d] = h;
 }
 
-__global__ __launch_bounds__(WG) void k_dump(Cols c, Caps k, int64_t doc, uint8_t* out, int64_t cap, int64_t* n) {
-    Replica<WaveGPU> r(doc_view(c, k, doc), WaveGPU());
+template <class HT>
+__global__ __launch_bounds__(WG) void k_dump(Store<HT> st, int64_t doc, uint8_t* out, int64_t cap, int64_t* n) {
+    Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
     int64_t m = r.dump(out, cap);
     if (threadIdx.x == 0) *n = m;
 }
 
-__global__ __launch_bounds__(WG) void k_length(Cols c, Caps k, int64_t doc, int32_t ref_seq, int32_t long_client,
+template <class HT>
+__global__ __launch_bounds__(WG) void k_length(Store<HT> st, int64_t doc, int32_t ref_seq, int32_t long_client,
                                               int32_t* out) {
-    Replica<WaveGPU> r(doc_view(c, k, doc), WaveGPU());
+    Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
     int32_t v;
     if (long_client < 0) {
         v = r.length_local();
@@ -85,13 +117,14 @@ __global__ __launch_bounds__(WG) void k_length(Cols c, Caps k, int64_t doc, int3
     if (threadIdx.x == 0) *out = v;
 }
 
-__global__ __launch_bounds__(WG) void k_text(Cols c, Caps k, int64_t doc, int32_t ref_seq, int32_t long_client,
+template <class HT>
+__global__ __launch_bounds__(WG) void k_text(Store<HT> st, int64_t doc, int32_t ref_seq, int32_t long_client,
                                             uint16_t* out, int64_t cap, int64_t* n) {
-    Replica<WaveGPU> r(doc_view(c, k, doc), WaveGPU());
+    Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
     int32_t sh;
     if (long_client < 0) {
-        sh = r.d.h->localShort;
-        ref_seq = r.d.h->currentSeq;
+        sh = r.z.h.localShort;
+        ref_seq = r.z.h.currentSeq;
     } else {
         sh = r.short_of(long_client);
         if (sh < 0) sh = 0x7fff;
@@ -100,25 +133,24 @@ __global__ __launch_bounds__(WG) void k_text(Cols c, Caps k, int64_t doc, int32_
     if (threadIdx.x == 0) *n = m;
 }
 
-/* per-doc (seqOps, sumR, sumW) for the roofline accounting */
-__global__ void k_work(const DocHdr* h, int64_t ndocs, int64_t* out3) {
+/* per-doc header fields: errors, stats, roofline work counters */
+template <class HT>
+__global__ void k_hdr(Store<HT> st, int64_t ndocs, int32_t* err, int32_t* err_op, int32_t* stats4, int64_t* work3) {
     int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= ndocs) return;
-    out3[3 * d + 0] = h[d].seqOps;
-    out3[3 * d + 1] = h[d].sumR;
-    out3[3 * d + 2] = h[d].sumW;
-}
-
-__global__ void k_errors(const DocHdr* h, int64_t ndocs, int32_t* err, int32_t* err_op, int32_t* stats4) {
-    int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= ndocs) return;
-    if (err) err[d] = h[d].err;
-    if (err_op) err_op[d] = h[d].errOp;
+    const DocHdr& h = st.doc(d).t->h;
+    if (err) err[d] = h.err;
+    if (err_op) err_op[d] = h.errOp;
     if (stats4) {
-        stats4[4 * d + 0] = h[d].nleaf;
-        stats4[4 * d + 1] = h[d].hwSlots;
-        stats4[4 * d + 2] = h[d].hwHeap;
-        stats4[4 * d + 3] = h[d].opsDone;
+        stats4[4 * d + 0] = h.nleaf;
+        stats4[4 * d + 1] = h.hwSlots;
+        stats4[4 * d + 2] = h.hwHeap;
+        stats4[4 * d + 3] = h.opsDone;
+    }
+    if (work3) {
+        work3[3 * d + 0] = h.seqOps;
+        work3[3 * d + 1] = h.sumR;
+        work3[3 * d + 2] = h.sumW;
     }
 }
 
@@ -133,8 +165,10 @@ struct DevBuf {
 struct mt_engine {
     int device;
     int64_t ndocs;
-    Caps k;
-    Cols c;
+    int profile = 0;
+    Store<HotSmall> s0;
+    Store<HotMid> s1;
+    Store<HotBig> s2;
     void* mem = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -146,13 +180,21 @@ struct mt_engine {
     std::string err;
 };
 
+/* call f(store) for the engine's profile */
+template <class F>
+static int32_t with_store(mt_engine* e, F&& f) {
+    if (e->profile == 0) return f(e->s0);
+    if (e->profile == 1) return f(e->s1);
+    return f(e->s2);
+}
+
 static int32_t hip_fail(mt_engine* e, hipError_t st, const char* what) {
     if (e) e->err = std::string(what) + ": " + hipGetErrorString(st);
     return MT_E_HIP;
 }
-#define HIPCHK(e, x)                                     \
-    do {                                                 \
-        hipError_t st_ = (x);                            \
+#define HIPCHK(e, x)                                        \
+    do {                                                    \
+        hipError_t st_ = (x);                               \
         if (st_ != hipSuccess) return hip_fail(e, st_, #x); \
     } while (0)
 
@@ -174,36 +216,51 @@ static int32_t launch_check(mt_engine* e, const char* what) {
     return MT_OK;
 }
 
+static dim3 docs_grid(int64_t n) { return dim3((unsigned)n); }
+static dim3 flat_grid(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+static int32_t launch_init(mt_engine* e) {
+    return with_store(e, [&](auto& st) {
+        using HT = typename std::decay_t<decltype(st)>::Hot;
+        hipLaunchKernelGGL((k_init<HT>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs);
+        int32_t rc = launch_check(e, "k_init");
+        if (rc || !e->collab) return rc;
+        hipLaunchKernelGGL((k_start_collab<HT>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
+                           (const int32_t*)e->local_ids.p, e->min_seq0, e->cur_seq0);
+        return launch_check(e, "k_start_collab");
+    });
+}
+
 extern "C" {
 
 int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_engine** out) {
     if (!out || !caps || ndocs < 1 || ndocs > (int64_t)0x7fffffff) return MT_E_ARG;
     *out = nullptr;
-    Caps k = {caps->ncap, caps->hcap, caps->acap, caps->mcap, caps->gcap, caps->ccap};
-    if (!caps_valid(k)) return MT_E_ARG;
+    Caps k = {caps->acap, caps->mcap, caps->gcap};
+    int prof = profile_for(caps->ncap);
+    if (!caps_valid(k) || prof < 0 || caps->ccap > 64) return MT_E_ARG;
     mt_engine* e = new mt_engine();
     e->device = device;
     e->ndocs = ndocs;
-    e->k = k;
-    hipError_t st = hipSetDevice(device);
-    if (st != hipSuccess) {
+    e->profile = prof;
+    if (hipSetDevice(device) != hipSuccess) {
         delete e;
         return MT_E_HIP;
     }
-    size_t bytes = layout(e->c, k, ndocs, nullptr);
-    st = hipMalloc(&e->mem, bytes);
-    if (st != hipSuccess) {
+    int64_t bytes = prof == 0 ? store_layout(e->s0, k, ndocs)
+                  : prof == 1 ? store_layout(e->s1, k, ndocs)
+                              : store_layout(e->s2, k, ndocs);
+    if (hipMalloc(&e->mem, (size_t)bytes) != hipSuccess) {
         delete e;
         return MT_E_NOMEM;
     }
-    layout(e->c, k, ndocs, (uint8_t*)e->mem);
+    e->s0.base = e->s1.base = e->s2.base = (uint8_t*)e->mem;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
         mt_engine_destroy(e);
         return MT_E_HIP;
     }
-    hipLaunchKernelGGL(k_init, dim3((unsigned)ndocs), dim3(WG), 0, e->stream, e->c, k, ndocs);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess) {
+    if (launch_init(e) != MT_OK || hipStreamSynchronize(e->stream) != hipSuccess) {
         mt_engine_destroy(e);
         return MT_E_HIP;
     }
@@ -215,8 +272,8 @@ void mt_engine_destroy(mt_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    DevBuf* bufs[] = {&e->ops,   &e->op_off, &e->text, &e->text_off, &e->props,
-                      &e->props_off, &e->kv, &e->kv_off, &e->tmp, &e->local_ids};
+    DevBuf* bufs[] = {&e->ops,       &e->op_off, &e->text,   &e->text_off, &e->props,
+                      &e->props_off, &e->kv,     &e->kv_off, &e->tmp,      &e->local_ids};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (e->mem) (void)hipFree(e->mem);
@@ -241,9 +298,13 @@ int32_t mt_engine_start_collab(mt_engine* e, const int32_t* local_long_ids, int3
     e->min_seq0 = min_seq;
     e->cur_seq0 = cur_seq;
     e->collab = true;
-    hipLaunchKernelGGL(k_start_collab, dim3((unsigned)e->ndocs), dim3(WG), 0, e->stream, e->c, e->k, e->ndocs,
-                       (const int32_t*)e->local_ids.p, min_seq, cur_seq);
-    if ((rc = launch_check(e, "k_start_collab"))) return rc;
+    rc = with_store(e, [&](auto& st) {
+        using HT = typename std::decay_t<decltype(st)>::Hot;
+        hipLaunchKernelGGL((k_start_collab<HT>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
+                           (const int32_t*)e->local_ids.p, min_seq, cur_seq);
+        return launch_check(e, "k_start_collab");
+    });
+    if (rc) return rc;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return MT_OK;
 }
@@ -302,39 +363,27 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
 int32_t mt_engine_reset(mt_engine* e) {
     if (!e) return MT_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
-    hipLaunchKernelGGL(k_init, dim3((unsigned)e->ndocs), dim3(WG), 0, e->stream, e->c, e->k, e->ndocs);
-    int32_t rc = launch_check(e, "k_init");
-    if (rc) return rc;
-    if (e->collab) {
-        hipLaunchKernelGGL(k_start_collab, dim3((unsigned)e->ndocs), dim3(WG), 0, e->stream, e->c, e->k, e->ndocs,
-                           (const int32_t*)e->local_ids.p, e->min_seq0, e->cur_seq0);
-        if ((rc = launch_check(e, "k_start_collab"))) return rc;
-    }
-    return MT_OK;
-}
-
-int32_t mt_engine_work(mt_engine* e, int64_t* out3) {
-    if (!e || !out3) return MT_E_ARG;
-    HIPCHK(e, hipSetDevice(e->device));
-    int32_t rc = ensure(e, e->tmp, sizeof(int64_t) * 3 * e->ndocs);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_work, dim3((unsigned)((e->ndocs + 255) / 256)), dim3(256), 0, e->stream, e->c.hdr, e->ndocs,
-                       (int64_t*)e->tmp.p);
-    if ((rc = launch_check(e, "k_work"))) return rc;
-    HIPCHK(e, hipMemcpyAsync(out3, e->tmp.p, sizeof(int64_t) * 3 * e->ndocs, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    return MT_OK;
+    return launch_init(e);
 }
 
 int32_t mt_engine_run(mt_engine* e) {
     if (!e || !e->staged) return MT_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-    hipLaunchKernelGGL(k_replay, dim3((unsigned)e->ndocs), dim3(WG), 0, e->stream, e->c, e->k, e->ndocs,
-                       (const mt_op_rec*)e->ops.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
-                       (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p,
-                       (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p);
-    int32_t rc = launch_check(e, "k_replay");
+    int32_t rc = with_store(e, [&](auto& st) {
+        using HT = typename std::decay_t<decltype(st)>::Hot;
+        if constexpr (std::is_same_v<HT, HotSmall>)
+            hipLaunchKernelGGL((k_replay<HT, true>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
+                               (const mt_op_rec*)e->ops.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
+                               (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p,
+                               (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p);
+        else
+            hipLaunchKernelGGL((k_replay<HT, false>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
+                               (const mt_op_rec*)e->ops.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
+                               (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p,
+                               (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p);
+        return launch_check(e, "k_replay");
+    });
     if (rc) return rc;
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
     return MT_OK;
@@ -349,33 +398,40 @@ int32_t mt_engine_sync(mt_engine* e) {
     return MT_OK;
 }
 
-int32_t mt_engine_errors(mt_engine* e, int32_t* err, int32_t* err_op) {
-    if (!e) return MT_E_ARG;
+static int32_t read_hdr(mt_engine* e, int32_t* err, int32_t* err_op, int32_t* stats4, int64_t* work3) {
     HIPCHK(e, hipSetDevice(e->device));
-    int32_t rc = ensure(e, e->tmp, sizeof(int32_t) * 2 * e->ndocs);
+    int64_t n = e->ndocs;
+    int32_t rc = ensure(e, e->tmp, (size_t)n * (4 + 4 + 16 + 24));
     if (rc) return rc;
     int32_t* de = (int32_t*)e->tmp.p;
-    int32_t* deo = de + e->ndocs;
-    hipLaunchKernelGGL(k_errors, dim3((unsigned)((e->ndocs + 255) / 256)), dim3(256), 0, e->stream, e->c.hdr,
-                       e->ndocs, de, deo, (int32_t*)nullptr);
-    if ((rc = launch_check(e, "k_errors"))) return rc;
-    if (err) HIPCHK(e, hipMemcpyAsync(err, de, sizeof(int32_t) * e->ndocs, hipMemcpyDeviceToHost, e->stream));
-    if (err_op) HIPCHK(e, hipMemcpyAsync(err_op, deo, sizeof(int32_t) * e->ndocs, hipMemcpyDeviceToHost, e->stream));
+    int32_t* deo = de + n;
+    int32_t* ds = deo + n;
+    int64_t* dw = (int64_t*)(ds + 4 * n);
+    rc = with_store(e, [&](auto& st) {
+        using HT = typename std::decay_t<decltype(st)>::Hot;
+        hipLaunchKernelGGL((k_hdr<HT>), flat_grid(n), dim3(256), 0, e->stream, st, n, de, deo, ds, dw);
+        return launch_check(e, "k_hdr");
+    });
+    if (rc) return rc;
+    if (err) HIPCHK(e, hipMemcpyAsync(err, de, 4 * n, hipMemcpyDeviceToHost, e->stream));
+    if (err_op) HIPCHK(e, hipMemcpyAsync(err_op, deo, 4 * n, hipMemcpyDeviceToHost, e->stream));
+    if (stats4) HIPCHK(e, hipMemcpyAsync(stats4, ds, 16 * n, hipMemcpyDeviceToHost, e->stream));
+    if (work3) HIPCHK(e, hipMemcpyAsync(work3, dw, 24 * n, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return MT_OK;
 }
 
+int32_t mt_engine_errors(mt_engine* e, int32_t* err, int32_t* err_op) {
+    if (!e) return MT_E_ARG;
+    return read_hdr(e, err, err_op, nullptr, nullptr);
+}
 int32_t mt_engine_stats(mt_engine* e, int32_t* out4) {
     if (!e || !out4) return MT_E_ARG;
-    HIPCHK(e, hipSetDevice(e->device));
-    int32_t rc = ensure(e, e->tmp, sizeof(int32_t) * 4 * e->ndocs);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_errors, dim3((unsigned)((e->ndocs + 255) / 256)), dim3(256), 0, e->stream, e->c.hdr,
-                       e->ndocs, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)e->tmp.p);
-    if ((rc = launch_check(e, "k_errors"))) return rc;
-    HIPCHK(e, hipMemcpyAsync(out4, e->tmp.p, sizeof(int32_t) * 4 * e->ndocs, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    return MT_OK;
+    return read_hdr(e, nullptr, nullptr, out4, nullptr);
+}
+int32_t mt_engine_work(mt_engine* e, int64_t* out3) {
+    if (!e || !out3) return MT_E_ARG;
+    return read_hdr(e, nullptr, nullptr, nullptr, out3);
 }
 
 int32_t mt_engine_digests(mt_engine* e, uint64_t* out) {
@@ -383,9 +439,13 @@ int32_t mt_engine_digests(mt_engine* e, uint64_t* out) {
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc = ensure(e, e->tmp, sizeof(uint64_t) * e->ndocs);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_digest, dim3((unsigned)e->ndocs), dim3(WG), 0, e->stream, e->c, e->k, e->ndocs,
-                       (uint64_t*)e->tmp.p);
-    if ((rc = launch_check(e, "k_digest"))) return rc;
+    rc = with_store(e, [&](auto& st) {
+        using HT = typename std::decay_t<decltype(st)>::Hot;
+        hipLaunchKernelGGL((k_digest<HT>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
+                           (uint64_t*)e->tmp.p);
+        return launch_check(e, "k_digest");
+    });
+    if (rc) return rc;
     HIPCHK(e, hipMemcpyAsync(out, e->tmp.p, sizeof(uint64_t) * e->ndocs, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return MT_OK;
@@ -398,8 +458,12 @@ int64_t mt_engine_dump(mt_engine* e, int64_t doc, uint8_t* out, int64_t cap) {
     if (ensure(e, e->tmp, need)) return -MT_E_HIP;
     int64_t* dn = (int64_t*)e->tmp.p;
     uint8_t* dbuf = out ? (uint8_t*)e->tmp.p + 16 : nullptr;
-    hipLaunchKernelGGL(k_dump, dim3(1), dim3(WG), 0, e->stream, e->c, e->k, doc, dbuf, out ? cap : 0, dn);
-    if (launch_check(e, "k_dump")) return -MT_E_HIP;
+    int32_t rc = with_store(e, [&](auto& st) {
+        using HT = typename std::decay_t<decltype(st)>::Hot;
+        hipLaunchKernelGGL((k_dump<HT>), dim3(1), dim3(WG), 0, e->stream, st, doc, dbuf, out ? cap : 0, dn);
+        return launch_check(e, "k_dump");
+    });
+    if (rc) return -rc;
     int64_t n = 0;
     if (hipMemcpyAsync(&n, dn, sizeof(int64_t), hipMemcpyDeviceToHost, e->stream) != hipSuccess) return -MT_E_HIP;
     if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
@@ -415,9 +479,13 @@ int32_t mt_engine_get_length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc = ensure(e, e->tmp, 16);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_length, dim3(1), dim3(WG), 0, e->stream, e->c, e->k, doc, ref_seq, long_client,
-                       (int32_t*)e->tmp.p);
-    if ((rc = launch_check(e, "k_length"))) return rc;
+    rc = with_store(e, [&](auto& st) {
+        using HT = typename std::decay_t<decltype(st)>::Hot;
+        hipLaunchKernelGGL((k_length<HT>), dim3(1), dim3(WG), 0, e->stream, st, doc, ref_seq, long_client,
+                           (int32_t*)e->tmp.p);
+        return launch_check(e, "k_length");
+    });
+    if (rc) return rc;
     HIPCHK(e, hipMemcpyAsync(out, e->tmp.p, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return MT_OK;
@@ -430,9 +498,13 @@ int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t l
     if (ensure(e, e->tmp, 16 + 2 * (size_t)(out ? cap : 0) + 16)) return -MT_E_HIP;
     int64_t* dn = (int64_t*)e->tmp.p;
     uint16_t* dbuf = out ? (uint16_t*)((uint8_t*)e->tmp.p + 16) : nullptr;
-    hipLaunchKernelGGL(k_text, dim3(1), dim3(WG), 0, e->stream, e->c, e->k, doc, ref_seq, long_client, dbuf,
-                       out ? cap : 0, dn);
-    if (launch_check(e, "k_text")) return -MT_E_HIP;
+    int32_t rc = with_store(e, [&](auto& st) {
+        using HT = typename std::decay_t<decltype(st)>::Hot;
+        hipLaunchKernelGGL((k_text<HT>), dim3(1), dim3(WG), 0, e->stream, st, doc, ref_seq, long_client, dbuf,
+                           out ? cap : 0, dn);
+        return launch_check(e, "k_text");
+    });
+    if (rc) return -rc;
     int64_t n = 0;
     if (hipMemcpyAsync(&n, dn, sizeof(int64_t), hipMemcpyDeviceToHost, e->stream) != hipSuccess) return -MT_E_HIP;
     if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;

@@ -1,5 +1,9 @@
 /*
- * mt_store.h — column allocation for a batch of documents (host malloc or hipMalloc).
+ * mt_store.h — per-document global-memory layout for a batch of documents.
+ *
+ * Each document owns one contiguous block: [hot image (HT) | cold rows | text arena (2 halves)
+ * | membership log (gid, sid) | pending-group ring]. On the GPU the hot image is staged into
+ * LDS for the duration of a replay (small profile) or used in place (larger profiles).
  */
 #pragma once
 #include <stddef.h>
@@ -9,53 +13,58 @@
 
 namespace mt {
 
-/* bytes of every column for `ndocs` documents with capacities k; fills c from `base` */
-inline size_t layout(Cols& c, const Caps& k, int64_t ndocs, uint8_t* base) {
-    size_t off = 0;
-    auto take = [&](size_t bytes) -> uint8_t* {
-        off = (off + 255) & ~(size_t)255;
-        uint8_t* p = base ? base + off : nullptr;
-        off += bytes;
-        return p;
-    };
-    int64_t rows = (int64_t)k.ncap * MAXN * ndocs, nodes = (int64_t)k.ncap * ndocs;
-    c.len = (int32_t*)take(4 * rows);
-    c.seq = (int32_t*)take(4 * rows);
-    c.rseq = (int32_t*)take(4 * rows);
-    c.lseq = (int32_t*)take(4 * rows);
-    c.lrseq = (int32_t*)take(4 * rows);
-    c.sid = (uint32_t*)take(4 * rows);
-    c.toff = (uint32_t*)take(4 * rows);
-    c.cli = (uint8_t*)take(rows);
-    c.rcli = (uint8_t*)take(rows);
-    c.flags = (uint8_t*)take(rows);
-    c.ng = (uint8_t*)take(rows);
-    c.prw = (uint8_t*)take(rows);
-    c.ovl = (uint64_t*)take(8 * rows);
-    c.pv = (uint16_t*)take(2 * rows * NKEYS);
-    c.pk = (uint8_t*)take(rows * NKEYS);
-    c.nparent = (int16_t*)take(2 * nodes);
-    c.kids = (int16_t*)take(2 * nodes * MAXN);
-    c.lorder = (int16_t*)take(2 * nodes);
-    c.lpos = (int16_t*)take(2 * nodes);
-    c.nchild = (int8_t*)take(nodes);
-    c.nlevel = (int8_t*)take(nodes);
-    c.nscour = (int8_t*)take(nodes);
-    c.hsid = (uint32_t*)take(4 * (int64_t)k.hcap * ndocs);
-    c.hseq = (int32_t*)take(4 * (int64_t)k.hcap * ndocs);
-    c.mgid = (int32_t*)take(4 * (int64_t)k.mcap * ndocs);
-    c.msid = (uint32_t*)take(4 * (int64_t)k.mcap * ndocs);
-    c.gq = (int32_t*)take(4 * (int64_t)k.gcap * ndocs);
-    c.arena = (uint16_t*)take(2 * 2 * (int64_t)k.acap * ndocs);
-    c.s2l = (uint16_t*)take(2 * (int64_t)k.ccap * ndocs);
-    c.hdr = (DocHdr*)take(sizeof(DocHdr) * ndocs);
-    return off + 256;
+template <class HT>
+struct Store {
+    typedef HT Hot;
+    uint8_t* base;
+    int64_t stride; /* bytes per document */
+    int64_t offCold, offArena, offMgid, offMsid, offGq;
+    Caps caps;
+
+    MT_HD Doc<HT> doc(int64_t d) const {
+        uint8_t* b = base + d * stride;
+        Doc<HT> v;
+        v.t = (HT*)b;
+        v.cold = (ColdRow*)(b + offCold);
+        v.arena = (uint16_t*)(b + offArena);
+        v.mgid = (int32_t*)(b + offMgid);
+        v.msid = (uint32_t*)(b + offMsid);
+        v.gq = (int32_t*)(b + offGq);
+        v.caps = caps;
+        return v;
+    }
+};
+
+inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+/* Fill offsets/stride for capacities `caps`; returns bytes for `ndocs` documents. */
+template <class HT>
+inline int64_t store_layout(Store<HT>& st, const Caps& caps, int64_t ndocs) {
+    int64_t o = align256((int64_t)sizeof(HT));
+    st.offCold = o;
+    o = align256(o + (int64_t)sizeof(ColdRow) * HT::S);
+    st.offArena = o;
+    o = align256(o + 2 * 2 * (int64_t)caps.acap);
+    st.offMgid = o;
+    o = align256(o + 4 * (int64_t)caps.mcap);
+    st.offMsid = o;
+    o = align256(o + 4 * (int64_t)caps.mcap);
+    st.offGq = o;
+    o = align256(o + 4 * (int64_t)caps.gcap);
+    st.stride = o;
+    st.caps = caps;
+    st.base = nullptr;
+    return o * ndocs;
 }
 
-/* capacity checks shared by every entry point: node ids are int16, heap/log sizes int32 */
-inline bool caps_valid(const Caps& k) {
-    return k.ncap >= 4 && k.ncap <= 32767 && k.hcap >= 1 && k.acap >= 16 && k.mcap >= 4 && k.gcap >= 1 &&
-           k.ccap >= 1 && k.ccap <= 254;
+inline bool caps_valid(const Caps& k) { return k.acap >= 16 && k.mcap >= 4 && k.gcap >= 1; }
+
+/* profiles: 0 = HotSmall (LDS-resident on the GPU), 1 = HotMid, 2 = HotBig */
+inline int profile_for(int32_t ncap) {
+    if (ncap <= HotSmall::N) return 0;
+    if (ncap <= HotMid::N) return 1;
+    if (ncap <= HotBig::N) return 2;
+    return -1;
 }
 
 } /* namespace mt */

@@ -111,12 +111,13 @@ def generate(w: Workload, ndocs: int, doc_base: int = 0, threads: int = 0) -> ol
     op_off[1:] = np.cumsum(nops)
     text_off = np.zeros(ndocs + 1, np.int64)
     text_off[1:] = np.cumsum(ntext)
-    opi = (np.arange(ndocs, dtype=np.int64)[:, None] * op_stride + np.arange(op_stride)[None, :])
-    mask = np.arange(op_stride)[None, :] < nops[:, None]
-    ops_c = ops[opi[mask]]
-    ti = (np.arange(ndocs, dtype=np.int64)[:, None] * text_stride + np.arange(text_stride)[None, :])
-    tmask = np.arange(text_stride)[None, :] < ntext[:, None]
-    text_c = text[ti[tmask]]
+    # compact the per-doc fixed-stride buffers (slices: no index matrices, ~2x output memory)
+    ops_c = np.empty(int(op_off[-1]), ol.OP_DTYPE)
+    text_c = np.empty(int(text_off[-1]), "<u2")
+    for d in range(ndocs):
+        ops_c[op_off[d]: op_off[d + 1]] = ops[d * op_stride: d * op_stride + nops[d]]
+        text_c[text_off[d]: text_off[d + 1]] = text[d * text_stride: d * text_stride + ntext[d]]
+    del ops, text
     if len(text_c) == 0:
         text_c = np.zeros(1, "<u2")
     props, kv = props_table()

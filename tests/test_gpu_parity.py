@@ -12,15 +12,17 @@ from replicas import parse_dump
 pytestmark = pytest.mark.gpu
 
 
-def _engine(ndocs, ops_per_doc):
+def _engine(ndocs, ops_per_doc, **caps):
     from fluidframework_amd.engine import Engine, default_caps
-    return Engine(ndocs, **default_caps(ops_per_doc))
+    c = default_caps(ops_per_doc)
+    c.update(caps)
+    return Engine(ndocs, **c)
 
 
-def _check_batch(b: ol.Batch, ops_per_doc: int, ndump: int = 4):
+def _check_batch(b: ol.Batch, ops_per_doc: int, ndump: int = 4, **caps):
     secs, odig, oerr = oc.replay_batch(b, threads=8)
     assert (oerr == 0).all()
-    eng = _engine(b.ndocs, ops_per_doc)
+    eng = _engine(b.ndocs, ops_per_doc, **caps)
     eng.start_collab(b.local_long_id)
     eng.replay(b)
     err, err_op = eng.errors()
@@ -90,4 +92,4 @@ def test_large_doc_props_newlines():
     """Coalescing defeated (distinct props + trailing newlines, config 4 shape) at test size."""
     w = gen.config4(6000)
     b = gen.generate(w, 4)
-    _check_batch(b, 6000, ndump=2)
+    _check_batch(b, 6000, ndump=2, ncap=4096, hcap=8192, acap=1 << 17)
