@@ -24,7 +24,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 
 
 def log(msg: str) -> None:
-    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+    import resource
+    rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6
+    print(f"[bench] {msg} (max rss {rss:.1f} GB)", file=sys.stderr, flush=True)
 
 
 def main() -> None:
@@ -61,11 +63,13 @@ def main() -> None:
     t0 = time.time()
     batch = gen.generate(w, args.docs, doc_base=rank * args.docs, threads=args.cpu_threads)
     log(f"rank {rank}: generated {args.docs} docs, {batch.nops} events in {time.time() - t0:.1f}s")
-    local_events = int((batch.ops["kind"] & 0x80 != 0).sum())
+    local_events = int(((batch.ops["kind"] & 0x80) != 0).sum())
 
     eng = Engine(args.docs, device=device, **default_caps(args.ops_per_doc))
+    log("engine created")
     eng.start_collab(batch.local_long_id)
     eng.submit(batch)  # HtoD once: inputs are resident in HBM for every step
+    log("inputs resident in HBM")
 
     def step() -> float:
         eng.reset()
@@ -74,7 +78,7 @@ def main() -> None:
         return eng.last_run_ms
 
     for _ in range(args.warmup):
-        step()
+        log(f"warmup step: {step():.1f} ms")
     err, err_op = eng.errors()
     if (err != 0).any():
         bad = np.nonzero(err)[0]
@@ -124,7 +128,7 @@ def main() -> None:
         ns = min(args.cpu_sample_docs, args.docs)
         sample = batch.subset(range(ns))
         secs, odig, oerr = oc.replay_batch(sample, threads=args.cpu_threads)
-        s_seq = int((sample.ops["kind"] & 0x80 == 0).sum())
+        s_seq = int(((sample.ops["kind"] & 0x80) == 0).sum())
         match = bool((odig == digests[:ns]).all())
         cpu = {"value": s_seq / secs, "unit": "ops/s", "cores": args.cpu_threads, "kind": "port",
                "sample": f"first {ns} of the {args.docs} docs ({s_seq} sequenced msgs), oracle B-tree "

@@ -23,33 +23,45 @@ struct WaveHost {
 };
 
 #ifdef __HIPCC__
+/* DPP control codes (GFX9 family, gfx950 included) */
+#define MT_DPP_ROW_SHR(n) (0x110 + (n))
+#define MT_DPP_ROW_BCAST15 0x142
+#define MT_DPP_ROW_BCAST31 0x143
+
 struct WaveGPU {
     static constexpr int N = 64;
-    __device__ int lane() const { return (int)(threadIdx.x & 63); }
-    /* exclusive prefix sum across the wave (Hillis-Steele over __shfl_up) */
-    __device__ int32_t excl_scan(int32_t v, int32_t* tot) const {
+    __device__ __attribute__((always_inline)) int lane() const { return (int)(threadIdx.x & 63); }
+    /* inclusive prefix sum over the 64 lanes: 4 row_shr steps inside each 16-lane row, then
+     * row_bcast:15 / row_bcast:31 carry the row totals (the GFX9 wave64 scan sequence).
+     * Lanes without a source keep the identity (old = 0). Six VALU ops, no LDS traffic. */
+    __device__ __attribute__((always_inline)) int32_t incl_scan(int32_t v) const {
         int32_t x = v;
-        int l = lane();
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            int32_t y = __shfl_up(x, o, 64);
-            if (l >= o) x += y;
-        }
-        *tot = __shfl(x, 63, 64);
+        x += __builtin_amdgcn_update_dpp(0, x, MT_DPP_ROW_SHR(1), 0xf, 0xf, false);
+        x += __builtin_amdgcn_update_dpp(0, x, MT_DPP_ROW_SHR(2), 0xf, 0xf, false);
+        x += __builtin_amdgcn_update_dpp(0, x, MT_DPP_ROW_SHR(4), 0xf, 0xf, false);
+        x += __builtin_amdgcn_update_dpp(0, x, MT_DPP_ROW_SHR(8), 0xf, 0xf, false);
+        x += __builtin_amdgcn_update_dpp(0, x, MT_DPP_ROW_BCAST15, 0xa, 0xf, false);
+        x += __builtin_amdgcn_update_dpp(0, x, MT_DPP_ROW_BCAST31, 0xc, 0xf, false);
+        return x;
+    }
+    __device__ __attribute__((always_inline)) int32_t excl_scan(int32_t v, int32_t* tot) const {
+        int32_t x = incl_scan(v);
+        *tot = __builtin_amdgcn_readlane(x, 63);
         return x - v;
     }
-    __device__ int32_t sum(int32_t v) const {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        return v;
+    __device__ __attribute__((always_inline)) int32_t sum(int32_t v) const {
+        return __builtin_amdgcn_readlane(incl_scan(v), 63);
     }
-    __device__ uint64_t ballot(bool p) const { return __ballot(p); }
-    __device__ int32_t bcast(int32_t v, int l) const { return __shfl(v, l, 64); }
-    __device__ static int ffs(uint64_t m) { return __builtin_ctzll(m); }
-    __device__ void sync() const {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __device__ __attribute__((always_inline)) uint64_t ballot(bool p) const { return __ballot(p); }
+    /* l is wave-uniform: v_readlane, no LDS round trip */
+    __device__ __attribute__((always_inline)) int32_t bcast(int32_t v, int l) const {
+        return __builtin_amdgcn_readlane(v, l);
+    }
+    __device__ __attribute__((always_inline)) static int ffs(uint64_t m) { return __builtin_ctzll(m); }
+    __device__ __attribute__((always_inline)) void sync() const {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
 };
 #endif
