@@ -103,13 +103,12 @@ template <int N_, int C_ = 64>
 struct HotT {
     static constexpr int N = N_;     /* B-tree nodes */
     static constexpr int S = N_ * 8; /* row slots (8 per leaf node) */
-    static constexpr int H = N_ * 2; /* zamboni heap entries */
+    static constexpr int H = N_ + 64; /* zamboni heap entries (config 3 peaks at 109) */
     static constexpr int C = C_;     /* clients */
     DocHdr h;
     int32_t len[S], seq[S], rseq[S];
     uint32_t sid[S];
-    int16_t rid[S];     /* slot -> cold row id */
-    int16_t freeRid[S]; /* free row-id stack */
+    int16_t rid[S]; /* slot -> cold row id */
     uint8_t cli[S], rcli[S], flags[S], ng[S];
     int16_t nparent[N], lorder[N], lpos[N];
     int16_t kids[N * 8];
@@ -120,9 +119,10 @@ struct HotT {
     uint16_t s2l[C];
 };
 
-/* LDS-sized profile for config 2/3 documents (max 147 nodes / 968 slots observed) and larger
+/* LDS-sized profile for config 2/3 documents (<= 40 KB: 4 documents per CU; pack's transient
+ * peak reaches 160+ nodes on ~0.05% of config-3 documents) and larger
  * global-memory profiles. */
-typedef HotT<160> HotSmall;
+typedef HotT<176> HotSmall;
 typedef HotT<2048> HotMid;
 typedef HotT<16384> HotBig;
 
@@ -131,6 +131,7 @@ template <class HT>
 struct Doc {
     HT* t;
     ColdRow* cold; /* HT::S records */
+    int16_t* frid;   /* free cold-row-id stack, HT::S entries */
     uint16_t* arena; /* 2 * acap */
     int32_t* mgid;
     uint32_t* msid;
@@ -204,7 +205,7 @@ struct Replica {
         }
         for (int32_t b = 0; b < HT::S; b += W::N) {
             int32_t i = b + w.lane();
-            if (i < HT::S) z.freeRid[i] = (int16_t)(HT::S - 1 - i);
+            if (i < HT::S) d.frid[i] = (int16_t)(HT::S - 1 - i);
         }
         w.sync();
         DocHdr* h = &z.h;
@@ -328,9 +329,9 @@ struct Replica {
             return 0;
         }
         z.h.nfreeRid = n - 1;
-        return z.freeRid[n - 1];
+        return d.frid[n - 1];
     }
-    MT_HD void free_rid(int32_t r) { z.freeRid[z.h.nfreeRid++] = (int16_t)r; }
+    MT_HD void free_rid(int32_t r) { d.frid[z.h.nfreeRid++] = (int16_t)r; }
 
     /* ---- perspective scans ------------------------------------------------------------- */
     /* Total length under a perspective (getLength, mergeTree.ts:1610). */

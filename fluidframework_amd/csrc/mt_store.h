@@ -18,7 +18,7 @@ struct Store {
     typedef HT Hot;
     uint8_t* base;
     int64_t stride; /* bytes per document */
-    int64_t offCold, offArena, offMgid, offMsid, offGq;
+    int64_t offCold, offFrid, offArena, offMgid, offMsid, offGq;
     Caps caps;
 
     MT_HD Doc<HT> doc(int64_t d) const {
@@ -26,6 +26,7 @@ struct Store {
         Doc<HT> v;
         v.t = (HT*)b;
         v.cold = (ColdRow*)(b + offCold);
+        v.frid = (int16_t*)(b + offFrid);
         v.arena = (uint16_t*)(b + offArena);
         v.mgid = (int32_t*)(b + offMgid);
         v.msid = (uint32_t*)(b + offMsid);
@@ -43,6 +44,8 @@ inline int64_t store_layout(Store<HT>& st, const Caps& caps, int64_t ndocs) {
     int64_t o = align256((int64_t)sizeof(HT));
     st.offCold = o;
     o = align256(o + (int64_t)sizeof(ColdRow) * HT::S);
+    st.offFrid = o;
+    o = align256(o + 2 * (int64_t)HT::S);
     st.offArena = o;
     o = align256(o + 2 * 2 * (int64_t)caps.acap);
     st.offMgid = o;
