@@ -116,6 +116,7 @@ struct HotT {
     int8_t _pad[(16 - (3 * N) % 16) % 16];
     uint32_t hsid[H];
     int32_t hseq[H];
+    int16_t hleaf[H]; /* leaf the segment was in when queued (a lookup hint only) */
     uint16_t s2l[C];
 };
 
@@ -321,6 +322,78 @@ struct Replica {
         z.flags[b] = z.flags[a];
         z.ng[b] = z.ng[a];
     }
+    /* a row's slot contents held in registers */
+    struct HotRow {
+        int32_t len, seq, rseq;
+        uint32_t sid;
+        int16_t rid;
+        uint8_t cli, rcli, flags, ng;
+    };
+    MT_HD HotRow load_row(int32_t a) const {
+        HotRow r;
+        r.len = z.len[a];
+        r.seq = z.seq[a];
+        r.rseq = z.rseq[a];
+        r.sid = z.sid[a];
+        r.rid = z.rid[a];
+        r.cli = z.cli[a];
+        r.rcli = z.rcli[a];
+        r.flags = z.flags[a];
+        r.ng = z.ng[a];
+        return r;
+    }
+    MT_HD void store_row(int32_t b, const HotRow& r) {
+        z.len[b] = r.len;
+        z.seq[b] = r.seq;
+        z.rseq[b] = r.rseq;
+        z.sid[b] = r.sid;
+        z.rid[b] = r.rid;
+        z.cli[b] = r.cli;
+        z.rcli[b] = r.rcli;
+        z.flags[b] = r.flags;
+        z.ng[b] = r.ng;
+    }
+    /* shift slab rows [j, c) of leaf n right by one slot (wave-parallel: read all, then write) */
+    MT_HD void slab_shift_right(int32_t n, int32_t j, int32_t c) {
+        if (W::N >= MAXN) {
+            int32_t l = w.lane();
+            bool mv = l >= j && l < c;
+            HotRow r;
+            if (mv) r = load_row(n * MAXN + l);
+            w.sync();
+            if (mv) store_row(n * MAXN + l + 1, r);
+            w.sync();
+        } else {
+            for (int32_t i = c; i > j; i--) copy_row(n * MAXN + i, n * MAXN + i - 1);
+        }
+    }
+    /* copy `cnt` rows between non-overlapping slot ranges */
+    MT_HD void move_rows(int32_t dst, int32_t src, int32_t cnt) {
+        for (int32_t b = 0; b < cnt; b += W::N) {
+            int32_t i = b + w.lane();
+            if (i < cnt) store_row(dst + i, load_row(src + i));
+        }
+        w.sync();
+    }
+    /* shift lorder[from, n) by delta entries and fix lpos; chunk order never overwrites an
+     * entry before it is read */
+    MT_HD void lorder_shift(int32_t from, int32_t n, int32_t delta) {
+        int32_t cnt = n - from;
+        if (delta == 0 || cnt <= 0) return;
+        int32_t nch = (cnt + W::N - 1) / W::N;
+        for (int32_t c = 0; c < nch; c++) {
+            int32_t b = delta > 0 ? (nch - 1 - c) * W::N : c * W::N;
+            int32_t i = from + b + w.lane();
+            bool ok = i < n;
+            int32_t x = ok ? z.lorder[i] : 0;
+            w.sync();
+            if (ok) {
+                z.lorder[i + delta] = (int16_t)x;
+                z.lpos[x] = (int16_t)(i + delta);
+            }
+            w.sync();
+        }
+    }
     /* cold row ids */
     MT_HD int32_t alloc_rid() {
         int32_t n = z.h.nfreeRid;
@@ -390,12 +463,7 @@ struct Replica {
     MT_HD void lorder_insert_after(int32_t after, int32_t nl) {
         int32_t k = z.lpos[after] + 1;
         int32_t n = z.h.nleaf;
-        /* shift lorder[k..n-1] right by one (uniform loop; small) */
-        for (int32_t i = n; i > k; i--) {
-            int32_t x = z.lorder[i - 1];
-            z.lorder[i] = (int16_t)x;
-            z.lpos[x] = (int16_t)i;
-        }
+        lorder_shift(k, n, 1);
         z.lorder[k] = (int16_t)nl;
         z.lpos[nl] = (int16_t)k;
         z.h.nleaf = n + 1;
@@ -412,7 +480,7 @@ struct Replica {
             if (nn < 0) return -1;
             if (first < 0) first = nn;
             if (lvl == 0) {
-                for (int32_t i = 0; i < 4; i++) copy_row(nn * MAXN + i, n * MAXN + 4 + i);
+                move_rows(nn * MAXN, n * MAXN + 4, 4);
             } else {
                 for (int32_t i = 0; i < 4; i++) {
                     int32_t c = z.kids[n * MAXN + 4 + i];
@@ -443,7 +511,7 @@ struct Replica {
     /* Make room at child index j of leaf n; returns slot for the new row (after any split). */
     MT_HD int32_t leaf_insert_slot(int32_t n, int32_t j) {
         int32_t c = z.nchild[n];
-        for (int32_t i = c; i > j; i--) copy_row(n * MAXN + i, n * MAXN + i - 1);
+        slab_shift_right(n, j, c);
         z.nchild[n] = (int8_t)(c + 1);
         if (c + 1 >= MAXN) {
             int32_t nn = split_node(n);
@@ -607,34 +675,44 @@ struct Replica {
     }
 
     /* ---- zamboni heap (collections.ts:212-264, LRUSegmentComparer mergeTree.ts:957-960) ---- */
-    MT_HD void heap_add(uint32_t sid, int32_t seq) {
+    MT_HD void heap_swap(int32_t i, int32_t j) {
+        uint32_t ts = z.hsid[i];
+        int32_t tq = z.hseq[i];
+        int16_t tl = z.hleaf[i];
+        z.hsid[i] = z.hsid[j];
+        z.hseq[i] = z.hseq[j];
+        z.hleaf[i] = z.hleaf[j];
+        z.hsid[j] = ts;
+        z.hseq[j] = tq;
+        z.hleaf[j] = tl;
+    }
+    MT_HD void heap_add(uint32_t sid, int32_t seq, int32_t leaf) {
         int32_t n = z.h.heapN;
         if (n >= HT::H) {
             fail(E_CAPACITY);
             return;
         }
-        /* L[k] (1-based) lives at index k-1 */
+        /* L[k] (1-based) lives at index k-1; fixup (collections.ts:240-247) */
         int32_t k = n + 1;
         z.hsid[k - 1] = sid;
         z.hseq[k - 1] = seq;
+        z.hleaf[k - 1] = (int16_t)leaf;
         z.h.heapN = n + 1;
         if (n + 1 > z.h.hwHeap) z.h.hwHeap = n + 1;
         while (k > 1 && z.hseq[(k >> 1) - 1] - z.hseq[k - 1] > 0) {
-            uint32_t ts = z.hsid[(k >> 1) - 1];
-            int32_t tq = z.hseq[(k >> 1) - 1];
-            z.hsid[(k >> 1) - 1] = z.hsid[k - 1];
-            z.hseq[(k >> 1) - 1] = z.hseq[k - 1];
-            z.hsid[k - 1] = ts;
-            z.hseq[k - 1] = tq;
+            heap_swap((k >> 1) - 1, k - 1);
             k >>= 1;
         }
     }
-    MT_HD void heap_pop(uint32_t* sid, int32_t* seq) {
+    /* get (collections.ts:227-233) + fixdown (249-263) */
+    MT_HD void heap_pop(uint32_t* sid, int32_t* seq, int32_t* leaf) {
         int32_t cnt = z.h.heapN;
         *sid = z.hsid[0];
         *seq = z.hseq[0];
+        *leaf = z.hleaf[0];
         z.hsid[0] = z.hsid[cnt - 1];
         z.hseq[0] = z.hseq[cnt - 1];
+        z.hleaf[0] = z.hleaf[cnt - 1];
         cnt--;
         z.h.heapN = cnt;
         int32_t k = 1;
@@ -642,12 +720,7 @@ struct Replica {
             int32_t j = k << 1;
             if (j < cnt && z.hseq[j - 1] - z.hseq[j] > 0) j++;
             if (z.hseq[k - 1] - z.hseq[j - 1] <= 0) break;
-            uint32_t ts = z.hsid[k - 1];
-            int32_t tq = z.hseq[k - 1];
-            z.hsid[k - 1] = z.hsid[j - 1];
-            z.hseq[k - 1] = z.hseq[j - 1];
-            z.hsid[j - 1] = ts;
-            z.hseq[j - 1] = tq;
+            heap_swap(k - 1, j - 1);
             k = j;
         }
     }
@@ -656,8 +729,27 @@ struct Replica {
         int32_t n = s / MAXN;
         if (z.nscour[n] != 1 && seq > z.h.currentSeq) {
             z.nscour[n] = 1;
-            heap_add(z.sid[s], seq);
+            heap_add(z.sid[s], seq, n);
         }
+    }
+    /* locate a row by stable id, first in the leaf it was queued from (rows rarely change
+     * leaves: only leaf splits and pack move them); -1 if unlinked */
+    MT_HD int32_t find_sid_hint(uint32_t sid, int32_t leaf) {
+        if (leaf >= 0 && leaf < HT::N && z.nlevel[leaf] == 0) {
+            int32_t k = z.lpos[leaf];
+            if (k >= 0 && k < z.h.nleaf && z.lorder[k] == leaf) {
+                int32_t j = w.lane() & (MAXN - 1);
+                int32_t c = z.nchild[leaf];
+                uint64_t m = w.ballot(j < c && w.lane() < MAXN && z.sid[leaf * MAXN + j] == sid);
+                if (W::N == 1) { /* serial host build: scan the slab */
+                    for (int32_t jj = 0; jj < c; jj++)
+                        if (z.sid[leaf * MAXN + jj] == sid) return leaf * MAXN + jj;
+                } else if (m) {
+                    return leaf * MAXN + W::ffs(m);
+                }
+            }
+        }
+        return find_sid(sid);
     }
     /* locate a row by stable id; -1 if unlinked */
     MT_HD int32_t find_sid(uint32_t sid) {
@@ -826,47 +918,61 @@ struct Replica {
             if (cc > MAXN - 1) cc = MAXN - 1;
             if (cc < 1) cc = 1;
             int32_t base = total / cc, extra = total % cc;
-            /* new leaves; rows move from the old slabs (old leaves are read in order) */
+            /* Packed blocks reuse the old leaf node ids in order (ids are not observable), so
+             * pack never needs more nodes than it had; they are new blocks for needsScour. */
             int32_t oldk[MAXN];
-            for (int32_t i = 0; i < pc; i++) oldk[i] = z.kids[parent * MAXN + i];
+            int32_t ocnt[MAXN];
+            for (int32_t i = 0; i < pc; i++) {
+                oldk[i] = z.kids[parent * MAXN + i];
+                ocnt[i] = z.nchild[oldk[i]];
+            }
             int32_t firstPos = z.lpos[oldk[0]];
             int32_t newk[MAXN];
-            int32_t ri = 0, rj = 0; /* read cursor: old leaf index, child index */
+            int32_t ncnt[MAXN];
             for (int32_t ni = 0; ni < cc; ni++) {
-                int32_t cnt = base + (extra > 0 ? 1 : 0);
-                if (extra > 0) extra--;
-                int32_t nb = alloc_node(0);
-                if (nb < 0) return;
-                newk[ni] = nb;
-                for (int32_t q = 0; q < cnt; q++) {
-                    while (rj >= z.nchild[oldk[ri]]) {
-                        ri++;
-                        rj = 0;
-                    }
-                    copy_row(nb * MAXN + q, oldk[ri] * MAXN + rj);
-                    rj++;
-                }
-                z.nchild[nb] = (int8_t)cnt;
-                z.nparent[nb] = (int16_t)parent;
+                ncnt[ni] = base + (ni < extra ? 1 : 0);
+                newk[ni] = ni < pc ? oldk[ni] : alloc_node(0);
+                if (newk[ni] < 0) return;
             }
-            for (int32_t i = 0; i < pc; i++) free_node(oldk[i]);
-            /* lorder: replace [firstPos, firstPos+pc) with the new leaves */
+            /* move the held rows (<= 49) from old positions to new ones: read all, then write */
+            if (W::N >= MAXN * MAXN) {
+                int32_t q = w.lane();
+                bool has = q < total;
+                HotRow r;
+                int32_t dst = 0;
+                if (has) {
+                    int32_t i = 0, acc = 0;
+                    while (q >= acc + ocnt[i]) acc += ocnt[i++];
+                    r = load_row(oldk[i] * MAXN + (q - acc));
+                    int32_t ti = 0, tacc = 0;
+                    while (q >= tacc + ncnt[ti]) tacc += ncnt[ti++];
+                    dst = newk[ti] * MAXN + (q - tacc);
+                }
+                w.sync();
+                if (has) store_row(dst, r);
+                w.sync();
+            } else {
+                HotRow tmp[MAXN * MAXN];
+                int32_t q = 0;
+                for (int32_t i = 0; i < pc; i++)
+                    for (int32_t j = 0; j < ocnt[i]; j++) tmp[q++] = load_row(oldk[i] * MAXN + j);
+                q = 0;
+                for (int32_t i = 0; i < cc; i++)
+                    for (int32_t j = 0; j < ncnt[i]; j++) store_row(newk[i] * MAXN + j, tmp[q++]);
+            }
+            for (int32_t ni = 0; ni < cc; ni++) {
+                int32_t nb = newk[ni];
+                z.nchild[nb] = (int8_t)ncnt[ni];
+                z.nparent[nb] = (int16_t)parent;
+                z.nlevel[nb] = 0;
+                z.nscour[nb] = -1;
+            }
+            for (int32_t i = cc; i < pc; i++) free_node(oldk[i]);
+            /* lorder: [firstPos, firstPos+pc) becomes [firstPos, firstPos+cc) */
             int32_t nl = z.h.nleaf;
             int32_t delta = cc - pc;
-            if (delta < 0) {
-                for (int32_t i = firstPos + pc; i < nl; i++) {
-                    int32_t x = z.lorder[i];
-                    z.lorder[i + delta] = (int16_t)x;
-                    z.lpos[x] = (int16_t)(i + delta);
-                }
-            } else if (delta > 0) {
-                for (int32_t i = nl - 1; i >= firstPos + pc; i--) {
-                    int32_t x = z.lorder[i];
-                    z.lorder[i + delta] = (int16_t)x;
-                    z.lpos[x] = (int16_t)(i + delta);
-                }
-            }
-            for (int32_t i = 0; i < cc; i++) {
+            lorder_shift(firstPos + pc, nl, delta);
+            for (int32_t i = pc; i < cc; i++) {
                 z.lorder[firstPos + i] = (int16_t)newk[i];
                 z.lpos[newk[i]] = (int16_t)(firstPos + i);
             }
@@ -916,9 +1022,9 @@ struct Replica {
             if (z.h.heapN < 1) break;
             if (z.hseq[0] > z.h.minSeq) break;
             uint32_t sid;
-            int32_t mseq;
-            heap_pop(&sid, &mseq);
-            int32_t s = find_sid(sid);
+            int32_t mseq, hint;
+            heap_pop(&sid, &mseq, &hint);
+            int32_t s = find_sid_hint(sid, hint);
             if (s < 0) continue;
             int32_t n = s / MAXN;
             if (z.nscour[n] == 0) continue;
@@ -972,6 +1078,9 @@ struct Replica {
         if (P + v > pos) split_row(t, pos - P);
     }
     /* returns the slot of the inserted row or -1 */
+    /* Boundary split (ensureIntervalBoundary, 2274-2278) and insert placement (blockInsert,
+     * 2174-2257) from ONE perspective scan: the row reaching pos (P < pos <= P + vis) is split
+     * at pos if pos falls strictly inside it; placement then resumes right after its left part. */
     MT_HD int32_t insert_row(int32_t pos, int32_t refSeq, int32_t client, int32_t seq) {
         int32_t k, j;
         if (pos == 0) {
@@ -983,12 +1092,16 @@ struct Replica {
             if (t < 0) return -1;
             int32_t s = slot_at(t);
             int32_t v = vis(s, refSeq, client);
-            k = t >> 3;
-            j = t & 7;
-            if (P + v > pos) {
-                /* pos strictly inside (only possible for an unsplittable segment): insert before */
+            if (P + v > pos && !(z.flags[s] & RF_MARKER)) {
+                int32_t ls = split_row(t, pos - P);
+                if (ls < 0) return -1;
+                k = z.lpos[ls / MAXN];
+                j = (ls & (MAXN - 1)) + 1;
             } else {
-                j++;
+                k = t >> 3;
+                j = t & 7;
+                /* pos strictly inside an unsplittable segment: insert before it */
+                if (!(P + v > pos)) j++;
             }
         }
         for (;;) {
@@ -1008,11 +1121,11 @@ struct Replica {
     }
     MT_HD void insert_segments(const mt_op_rec& op, const Pools& p, int32_t refSeq, int32_t client, int32_t seq) {
         int32_t pos = op.pos1;
-        ensure_boundary(pos, refSeq, client);
         bool hasL = seq == UNASSIGNED_SEQ;
         int32_t localSeq = hasL ? ++z.h.localSeq : 0;
         bool marker = op.seg_kind == MT_SEG_MARKER;
         int32_t L = marker ? 1 : op.text_len;
+        if (L <= 0) ensure_boundary(pos, refSeq, client); /* the split still happens (2004) */
         if (L > 0) {
             int32_t off = 0;
             if (!marker) {
