@@ -107,23 +107,24 @@ struct HotT {
     static constexpr int C = C_;     /* clients */
     DocHdr h;
     int32_t len[S], seq[S], rseq[S];
-    uint32_t sid[S];
-    int16_t rid[S]; /* slot -> cold row id */
+    int16_t rid[S];   /* slot -> row id (stable identity of a segment; cold data index) */
+    int16_t rleaf[S]; /* row id -> leaf node currently holding it */
     uint8_t cli[S], rcli[S], flags[S], ng[S];
+    uint8_t rgen[S]; /* row id -> generation, bumped when the id is freed */
     int16_t nparent[N], lorder[N], lpos[N];
     int16_t kids[N * 8];
     int8_t nchild[N], nlevel[N], nscour[N];
     int8_t _pad[(16 - (3 * N) % 16) % 16];
-    uint32_t hsid[H];
     int32_t hseq[H];
-    int16_t hleaf[H]; /* leaf the segment was in when queued (a lookup hint only) */
+    int16_t hrid[H];  /* segment (row id) queued for scouring */
+    uint8_t hgen[H];  /* its row-id generation when queued: a mismatch means it was unlinked */
     uint16_t s2l[C];
 };
 
-/* LDS-sized profile for config 2/3 documents (<= 40 KB: 4 documents per CU; pack's transient
- * peak reaches 160+ nodes on ~0.05% of config-3 documents) and larger
+/* LDS-sized profile for config 2/3 documents (39.5 KB <= 160 KB / 4: 4 documents per CU; the
+ * node high-water of config-3 documents has a tail reaching ~180 nodes) and larger
  * global-memory profiles. */
-typedef HotT<176> HotSmall;
+typedef HotT<192> HotSmall;
 typedef HotT<2048> HotMid;
 typedef HotT<16384> HotBig;
 
@@ -135,7 +136,7 @@ struct Doc {
     int16_t* frid;   /* free cold-row-id stack, HT::S entries */
     uint16_t* arena; /* 2 * acap */
     int32_t* mgid;
-    uint32_t* msid;
+    int32_t* mrid; /* row id of each membership entry */
     int32_t* gq;
     Caps caps;
 };
@@ -206,7 +207,10 @@ struct Replica {
         }
         for (int32_t b = 0; b < HT::S; b += W::N) {
             int32_t i = b + w.lane();
-            if (i < HT::S) d.frid[i] = (int16_t)(HT::S - 1 - i);
+            if (i < HT::S) {
+                d.frid[i] = (int16_t)(HT::S - 1 - i);
+                z.rgen[i] = 0;
+            }
         }
         w.sync();
         DocHdr* h = &z.h;
@@ -315,7 +319,6 @@ struct Replica {
         z.len[b] = z.len[a];
         z.seq[b] = z.seq[a];
         z.rseq[b] = z.rseq[a];
-        z.sid[b] = z.sid[a];
         z.rid[b] = z.rid[a];
         z.cli[b] = z.cli[a];
         z.rcli[b] = z.rcli[a];
@@ -325,7 +328,6 @@ struct Replica {
     /* a row's slot contents held in registers */
     struct HotRow {
         int32_t len, seq, rseq;
-        uint32_t sid;
         int16_t rid;
         uint8_t cli, rcli, flags, ng;
     };
@@ -334,7 +336,6 @@ struct Replica {
         r.len = z.len[a];
         r.seq = z.seq[a];
         r.rseq = z.rseq[a];
-        r.sid = z.sid[a];
         r.rid = z.rid[a];
         r.cli = z.cli[a];
         r.rcli = z.rcli[a];
@@ -346,7 +347,6 @@ struct Replica {
         z.len[b] = r.len;
         z.seq[b] = r.seq;
         z.rseq[b] = r.rseq;
-        z.sid[b] = r.sid;
         z.rid[b] = r.rid;
         z.cli[b] = r.cli;
         z.rcli[b] = r.rcli;
@@ -404,7 +404,33 @@ struct Replica {
         z.h.nfreeRid = n - 1;
         return d.frid[n - 1];
     }
-    MT_HD void free_rid(int32_t r) { d.frid[z.h.nfreeRid++] = (int16_t)r; }
+    MT_HD void free_rid(int32_t r) {
+        z.rgen[r]++;
+        d.frid[z.h.nfreeRid++] = (int16_t)r;
+    }
+    /* record leaf n as the holder of its first `cnt` rows */
+    MT_HD void set_leaf_of_rows(int32_t n, int32_t cnt) {
+        for (int32_t b = 0; b < cnt; b += W::N) {
+            int32_t j = b + w.lane();
+            int32_t r = j < cnt ? z.rid[n * MAXN + j] : -1;
+            if (r >= 0) z.rleaf[r] = (int16_t)n;
+        }
+        w.sync();
+    }
+    /* slot of a live row id (its leaf is rleaf[rid]); -1 if the id was freed since `gen` */
+    MT_HD int32_t slot_of(int32_t rid, int32_t gen) {
+        if (gen >= 0 && z.rgen[rid] != (uint8_t)gen) return -1;
+        int32_t leaf = z.rleaf[rid];
+        int32_t c = z.nchild[leaf];
+        if (W::N == 1) {
+            for (int32_t j = 0; j < c; j++)
+                if (z.rid[leaf * MAXN + j] == rid) return leaf * MAXN + j;
+            return -1;
+        }
+        int32_t j = w.lane();
+        uint64_t m = w.ballot(j < c && z.rid[leaf * MAXN + (j & (MAXN - 1))] == rid);
+        return m ? leaf * MAXN + W::ffs(m) : -1;
+    }
 
     /* ---- perspective scans ------------------------------------------------------------- */
     /* Total length under a perspective (getLength, mergeTree.ts:1610). */
@@ -481,6 +507,7 @@ struct Replica {
             if (first < 0) first = nn;
             if (lvl == 0) {
                 move_rows(nn * MAXN, n * MAXN + 4, 4);
+                set_leaf_of_rows(nn, 4);
             } else {
                 for (int32_t i = 0; i < 4; i++) {
                     int32_t c = z.kids[n * MAXN + 4 + i];
@@ -512,6 +539,7 @@ struct Replica {
     MT_HD int32_t leaf_insert_slot(int32_t n, int32_t j) {
         int32_t c = z.nchild[n];
         slab_shift_right(n, j, c);
+        z.rid[n * MAXN + j] = -1; /* not a row yet: the caller assigns one */
         z.nchild[n] = (int8_t)(c + 1);
         if (c + 1 >= MAXN) {
             int32_t nn = split_node(n);
@@ -584,11 +612,11 @@ struct Replica {
         if (willSplit && j >= 4) ls = z.lorder[z.lpos[n] + 1] * MAXN + (j - 4);
         copy_row(rs, ls);
         z.rid[rs] = (int16_t)alloc_rid();
+        z.rleaf[z.rid[rs]] = (int16_t)(rs / MAXN);
         cold(rs) = cold(ls); /* splitAt copies every field (mergeTree.ts:523-567) */
         z.len[rs] = z.len[ls] - off;
         cold(rs).toff = cold(ls).toff + (uint32_t)off;
         z.len[ls] = off;
-        z.sid[rs] = (uint32_t)z.h.nextSid++;
         z.h.nrows++;
         z.h.sumW += 2;
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
@@ -597,17 +625,17 @@ struct Replica {
         if (z.ng[ls]) {
             if (z.h.memN + z.ng[ls] > d.caps.mcap) mem_compact();
             int32_t head = z.h.gqN ? d.gq[z.h.gqHead % d.caps.gcap] : 0x7fffffff;
-            uint32_t lsid = z.sid[ls];
-            uint32_t rsid = z.sid[rs];
+            int32_t lrid = z.rid[ls];
+            int32_t rrid = z.rid[rs];
             int32_t m0 = z.h.memN;
             for (int32_t b = 0; b < m0; b += W::N) {
                 int32_t i = b + w.lane();
                 int32_t g = i < m0 ? d.mgid[i] : -1;
-                uint64_t m = w.ballot(i < m0 && d.msid[i] == lsid && g >= head);
+                uint64_t m = w.ballot(i < m0 && d.mrid[i] == lrid && g >= head);
                 while (m) {
                     int32_t l = W::ffs(m);
                     m &= m - 1;
-                    mem_append(w.bcast(g, l), rsid);
+                    mem_append(w.bcast(g, l), rrid);
                 }
             }
         }
@@ -615,7 +643,7 @@ struct Replica {
     }
 
     /* ---- segment groups ---------------------------------------------------------------- */
-    MT_HD void mem_append(int32_t gid, uint32_t sid) {
+    MT_HD void mem_append(int32_t gid, int32_t rid) {
         int32_t m = z.h.memN;
         if (m >= d.caps.mcap) {
             mem_compact();
@@ -626,7 +654,7 @@ struct Replica {
             }
         }
         d.mgid[m] = gid;
-        d.msid[m] = sid;
+        d.mrid[m] = rid;
         z.h.memN = m + 1;
     }
     /* drop entries of groups already acked (gid < head gid): wave stream compaction */
@@ -636,14 +664,14 @@ struct Replica {
         for (int32_t b = 0; b < n; b += W::N) {
             int32_t i = b + w.lane();
             int32_t g = i < n ? d.mgid[i] : -1;
-            uint32_t sd = i < n ? d.msid[i] : 0;
+            int32_t sd = i < n ? d.mrid[i] : 0;
             bool keep = i < n && g >= head;
             int32_t tot;
             int32_t off = w.excl_scan(keep ? 1 : 0, &tot);
             w.sync();
             if (keep) {
                 d.mgid[wpos + off] = g;
-                d.msid[wpos + off] = sd;
+                d.mrid[wpos + off] = sd;
             }
             w.sync();
             wpos += tot;
@@ -658,7 +686,7 @@ struct Replica {
             return;
         }
         z.ng[s] = (uint8_t)(ng + 1);
-        mem_append(gid, z.sid[s]);
+        mem_append(gid, z.rid[s]);
     }
     /* addToPendingList (mergeTree.ts:1955-1962); the group id is the op's localSeq */
     MT_HD void pending_add(int32_t s, int32_t gid, bool* created) {
@@ -676,17 +704,17 @@ struct Replica {
 
     /* ---- zamboni heap (collections.ts:212-264, LRUSegmentComparer mergeTree.ts:957-960) ---- */
     MT_HD void heap_swap(int32_t i, int32_t j) {
-        uint32_t ts = z.hsid[i];
+        int16_t tr = z.hrid[i];
         int32_t tq = z.hseq[i];
-        int16_t tl = z.hleaf[i];
-        z.hsid[i] = z.hsid[j];
+        uint8_t tg = z.hgen[i];
+        z.hrid[i] = z.hrid[j];
         z.hseq[i] = z.hseq[j];
-        z.hleaf[i] = z.hleaf[j];
-        z.hsid[j] = ts;
+        z.hgen[i] = z.hgen[j];
+        z.hrid[j] = tr;
         z.hseq[j] = tq;
-        z.hleaf[j] = tl;
+        z.hgen[j] = tg;
     }
-    MT_HD void heap_add(uint32_t sid, int32_t seq, int32_t leaf) {
+    MT_HD void heap_add(int32_t rid, int32_t seq) {
         int32_t n = z.h.heapN;
         if (n >= HT::H) {
             fail(E_CAPACITY);
@@ -694,9 +722,9 @@ struct Replica {
         }
         /* L[k] (1-based) lives at index k-1; fixup (collections.ts:240-247) */
         int32_t k = n + 1;
-        z.hsid[k - 1] = sid;
+        z.hrid[k - 1] = (int16_t)rid;
         z.hseq[k - 1] = seq;
-        z.hleaf[k - 1] = (int16_t)leaf;
+        z.hgen[k - 1] = z.rgen[rid];
         z.h.heapN = n + 1;
         if (n + 1 > z.h.hwHeap) z.h.hwHeap = n + 1;
         while (k > 1 && z.hseq[(k >> 1) - 1] - z.hseq[k - 1] > 0) {
@@ -705,14 +733,14 @@ struct Replica {
         }
     }
     /* get (collections.ts:227-233) + fixdown (249-263) */
-    MT_HD void heap_pop(uint32_t* sid, int32_t* seq, int32_t* leaf) {
+    MT_HD void heap_pop(int32_t* rid, int32_t* seq, int32_t* gen) {
         int32_t cnt = z.h.heapN;
-        *sid = z.hsid[0];
+        *rid = z.hrid[0];
         *seq = z.hseq[0];
-        *leaf = z.hleaf[0];
-        z.hsid[0] = z.hsid[cnt - 1];
+        *gen = z.hgen[0];
+        z.hrid[0] = z.hrid[cnt - 1];
         z.hseq[0] = z.hseq[cnt - 1];
-        z.hleaf[0] = z.hleaf[cnt - 1];
+        z.hgen[0] = z.hgen[cnt - 1];
         cnt--;
         z.h.heapN = cnt;
         int32_t k = 1;
@@ -729,37 +757,8 @@ struct Replica {
         int32_t n = s / MAXN;
         if (z.nscour[n] != 1 && seq > z.h.currentSeq) {
             z.nscour[n] = 1;
-            heap_add(z.sid[s], seq, n);
+            heap_add(z.rid[s], seq);
         }
-    }
-    /* locate a row by stable id, first in the leaf it was queued from (rows rarely change
-     * leaves: only leaf splits and pack move them); -1 if unlinked */
-    MT_HD int32_t find_sid_hint(uint32_t sid, int32_t leaf) {
-        if (leaf >= 0 && leaf < HT::N && z.nlevel[leaf] == 0) {
-            int32_t k = z.lpos[leaf];
-            if (k >= 0 && k < z.h.nleaf && z.lorder[k] == leaf) {
-                int32_t j = w.lane() & (MAXN - 1);
-                int32_t c = z.nchild[leaf];
-                uint64_t m = w.ballot(j < c && w.lane() < MAXN && z.sid[leaf * MAXN + j] == sid);
-                if (W::N == 1) { /* serial host build: scan the slab */
-                    for (int32_t jj = 0; jj < c; jj++)
-                        if (z.sid[leaf * MAXN + jj] == sid) return leaf * MAXN + jj;
-                } else if (m) {
-                    return leaf * MAXN + W::ffs(m);
-                }
-            }
-        }
-        return find_sid(sid);
-    }
-    /* locate a row by stable id; -1 if unlinked */
-    MT_HD int32_t find_sid(uint32_t sid) {
-        int32_t T = z.h.nleaf * MAXN;
-        for (int32_t b = 0; b < T; b += W::N) {
-            int32_t s = slot_at(b + w.lane());
-            uint64_t m = w.ballot(s >= 0 && z.sid[s] == sid);
-            if (m) return w.bcast(s, W::ffs(m));
-        }
-        return -1;
     }
 
     /* ---- properties (segmentPropertiesManager.ts:35-111) ---------------------------- */
@@ -949,7 +948,10 @@ struct Replica {
                     dst = newk[ti] * MAXN + (q - tacc);
                 }
                 w.sync();
-                if (has) store_row(dst, r);
+                if (has) {
+                    store_row(dst, r);
+                    z.rleaf[r.rid] = (int16_t)(dst / MAXN);
+                }
                 w.sync();
             } else {
                 HotRow tmp[MAXN * MAXN];
@@ -958,7 +960,10 @@ struct Replica {
                     for (int32_t j = 0; j < ocnt[i]; j++) tmp[q++] = load_row(oldk[i] * MAXN + j);
                 q = 0;
                 for (int32_t i = 0; i < cc; i++)
-                    for (int32_t j = 0; j < ncnt[i]; j++) store_row(newk[i] * MAXN + j, tmp[q++]);
+                    for (int32_t j = 0; j < ncnt[i]; j++) {
+                        store_row(newk[i] * MAXN + j, tmp[q]);
+                        z.rleaf[tmp[q++].rid] = (int16_t)newk[i];
+                    }
             }
             for (int32_t ni = 0; ni < cc; ni++) {
                 int32_t nb = newk[ni];
@@ -1021,10 +1026,9 @@ struct Replica {
         for (int i = 0; i < 2; i++) {
             if (z.h.heapN < 1) break;
             if (z.hseq[0] > z.h.minSeq) break;
-            uint32_t sid;
-            int32_t mseq, hint;
-            heap_pop(&sid, &mseq, &hint);
-            int32_t s = find_sid_hint(sid, hint);
+            int32_t rid, mseq, gen;
+            heap_pop(&rid, &mseq, &gen);
+            int32_t s = slot_of(rid, gen); /* -1: unlinked or merged away since it was queued */
             if (s < 0) continue;
             int32_t n = s / MAXN;
             if (z.nscour[n] == 0) continue;
@@ -1150,7 +1154,7 @@ struct Replica {
             z.ng[s] = 0;
             cold(s).prw = 0;
             cold(s).ovl = 0;
-            z.sid[s] = (uint32_t)z.h.nextSid++;
+            z.rleaf[z.rid[s]] = (int16_t)(s / MAXN);
             z.h.nrows++;
             z.h.sumW++;
             if (marker) {
@@ -1271,12 +1275,12 @@ struct Replica {
             int32_t mn = z.h.memN;
             for (int32_t b = 0; b < mn; b += W::N) {
                 int32_t i = b + w.lane();
-                uint32_t sd = i < mn ? d.msid[i] : 0;
+                int32_t rd = i < mn ? d.mrid[i] : 0;
                 uint64_t msk = w.ballot(i < mn && d.mgid[i] == gid);
                 while (msk) {
                     int32_t l = W::ffs(msk);
                     msk &= msk - 1;
-                    int32_t s = find_sid((uint32_t)w.bcast((int32_t)sd, l));
+                    int32_t s = slot_of(w.bcast(rd, l), -1);
                     if (s < 0) {
                         fail(E_ASSERT);
                         continue;

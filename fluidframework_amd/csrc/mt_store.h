@@ -2,7 +2,7 @@
  * mt_store.h — per-document global-memory layout for a batch of documents.
  *
  * Each document owns one contiguous block: [hot image (HT) | cold rows | text arena (2 halves)
- * | membership log (gid, sid) | pending-group ring]. On the GPU the hot image is staged into
+ * | membership log (gid, row id) | pending-group ring]. On the GPU the hot image is staged into
  * LDS for the duration of a replay (small profile) or used in place (larger profiles).
  */
 #pragma once
@@ -18,7 +18,7 @@ struct Store {
     typedef HT Hot;
     uint8_t* base;
     int64_t stride; /* bytes per document */
-    int64_t offCold, offFrid, offArena, offMgid, offMsid, offGq;
+    int64_t offCold, offFrid, offArena, offMgid, offMrid, offGq;
     Caps caps;
 
     MT_HD Doc<HT> doc(int64_t d) const {
@@ -29,7 +29,7 @@ struct Store {
         v.frid = (int16_t*)(b + offFrid);
         v.arena = (uint16_t*)(b + offArena);
         v.mgid = (int32_t*)(b + offMgid);
-        v.msid = (uint32_t*)(b + offMsid);
+        v.mrid = (int32_t*)(b + offMrid);
         v.gq = (int32_t*)(b + offGq);
         v.caps = caps;
         return v;
@@ -50,7 +50,7 @@ inline int64_t store_layout(Store<HT>& st, const Caps& caps, int64_t ndocs) {
     o = align256(o + 2 * 2 * (int64_t)caps.acap);
     st.offMgid = o;
     o = align256(o + 4 * (int64_t)caps.mcap);
-    st.offMsid = o;
+    st.offMrid = o;
     o = align256(o + 4 * (int64_t)caps.mcap);
     st.offGq = o;
     o = align256(o + 4 * (int64_t)caps.gcap);

@@ -75,8 +75,8 @@ def _p(a: np.ndarray):
 def default_caps(ops_per_doc: int) -> dict:
     """Capacities sized for the synthetic configs (high-water marks measured with the oracle)."""
     if ops_per_doc <= 20_000:
-        # LDS-resident profile (HotSmall: 176 nodes / 1408 slots)
-        return dict(ncap=176, hcap=240, acap=1 << 16, mcap=1024, gcap=1024, ccap=64)
+        # LDS-resident profile (HotSmall: 192 nodes / 1536 slots)
+        return dict(ncap=192, hcap=256, acap=1 << 16, mcap=1024, gcap=1024, ccap=64)
     return dict(ncap=16384, hcap=32768, acap=1 << 22, mcap=4096, gcap=1024, ccap=64)
 
 

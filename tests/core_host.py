@@ -45,7 +45,7 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-DEFAULT_CAPS = (176, 240, 1 << 16, 4096, 1024, 64)
+DEFAULT_CAPS = (192, 256, 1 << 16, 4096, 1024, 64)
 
 
 class HostStore:
