@@ -62,6 +62,7 @@ enum : uint8_t {
     RF_PROPS = 2, /* properties !== undefined (and propertyManager exists) */
     RF_LSEQ = 4,
     RF_LRSEQ = 8,
+    RF_OVL = 16, /* removedClientOverlap is non-empty (its list lives in the cold row) */
 };
 
 /* runtime capacities that are not part of the LDS image */
@@ -293,11 +294,13 @@ struct Replica {
         if (rs != NOREM) {
             int32_t rc = z.rcli[s] == LOCAL_CLIENT ? -1 : z.rcli[s];
             if (rc == client) return 0;
-            uint64_t ov = cold(s).ovl;
-            for (int k = 0; k < NOVL; k++) {
-                uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
-                if (e == 0) break;
-                if ((int32_t)e - 1 == client) return 0;
+            if (z.flags[s] & RF_OVL) { /* cold read only for the rare overlapping remove */
+                uint64_t ov = cold(s).ovl;
+                for (int k = 0; k < NOVL; k++) {
+                    uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
+                    if (e == 0) break;
+                    if ((int32_t)e - 1 == client) return 0;
+                }
             }
             if (rs != UNASSIGNED_SEQ && rs <= refSeq) return 0;
         }
@@ -876,7 +879,13 @@ struct Replica {
                     prev = -1;
                 } else {
                     if (z.seq[s] <= minSeq) {
-                        bool ok = prev >= 0 && can_append(prev, s) && match_props(prev, s) && local_len(s) > 0;
+                        /* hot predicates first; the cold ones (props values, trailing newline) are
+                         * only read for a candidate pair. Same conjunction as mergeTree.ts:1355-1360. */
+                        bool ok = prev >= 0 && local_len(s) > 0 && !(z.flags[prev] & RF_MARKER) &&
+                                  !(z.flags[s] & RF_MARKER) &&
+                                  (z.len[prev] <= GRANULARITY || z.len[s] <= GRANULARITY) &&
+                                  ((z.flags[prev] ^ z.flags[s]) & RF_PROPS) == 0 && match_props(prev, s) &&
+                                  can_append(prev, s);
                         if (ok) {
                             append_text(prev, s);
                             free_rid(z.rid[s]);
@@ -1226,6 +1235,7 @@ struct Replica {
                         fail(E_UNSUPPORTED);
                     } else {
                         cold(s).ovl = ov | ((uint64_t)(client + 1) << (8 * k));
+                        z.flags[s] |= RF_OVL;
                     }
                 }
             } else {

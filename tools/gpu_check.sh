@@ -13,3 +13,14 @@ timeout -k 10 300 python -u bench.py --docs $DOCS --steps 3 --warmup 1 > "$OUT/b
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --docs $DOCS --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" || { echo "rocprof failed rc=$?"; tail -30 "$OUT/prof_bench.err"; exit 1; }
 tail -3 "$OUT/pytest_gpu.txt"; cat "$OUT/smoke.txt" | tail -2; cat "$OUT/bench.json"
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \;
+# optional PMC passes (one counter group per run; each bounded)
+if [ -n "$PMC" ]; then
+  P=0
+  for CTRS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" \
+              "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT" \
+              "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+    P=$((P+1))
+    timeout -s KILL 240 rocprofv3 --pmc $CTRS -d "$OUT/pmc$P" -o run --output-format csv -- python3 bench.py --docs $DOCS --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc${P}.json" 2> "$OUT/pmc${P}.err" || { echo "pmc pass $P failed rc=$?"; exit 1; }
+  done
+  echo "pmc done"
+fi
