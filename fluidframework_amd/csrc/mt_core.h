@@ -81,10 +81,16 @@ struct DocHdr {
     int32_t arenaTop, arenaSide, err, errOp;
     int32_t nkeys, opsDone, hwSlots, hwHeap;
     int32_t nrows, seqOps, nfreeRid, gcEpoch; /* rows in the table; sequenced msgs applied */
+    int32_t localLen, _r0, _r1, _r2; /* root.cachedLength: Client.getLength() (client.ts:1051) */
     int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
-    uint16_t keys[NKEYS];
 };
+/* every int32 field of DocHdr (the replica keeps them in registers while it runs) */
+#define MT_HDR_FIELDS(X)                                                                          \
+    X(root) X(nleaf) X(freeHead) X(nfree) X(currentSeq) X(minSeq) X(localSeq) X(collaborating)   \
+    X(localShort) X(localLong) X(nclients) X(nextSid) X(heapN) X(memN) X(gqHead) X(gqN)          \
+    X(arenaTop) X(arenaSide) X(err) X(errOp) X(nkeys) X(opsDone) X(hwSlots) X(hwHeap) X(nrows)   \
+    X(seqOps) X(nfreeRid) X(gcEpoch) X(localLen)
 
 /* Cold per-row data, indexed by a row id that does not move when the row's slot moves. */
 struct ColdRow {
@@ -107,10 +113,17 @@ struct HotT {
     static constexpr int H = N_ + 64; /* zamboni heap entries (config 3 peaks at 109) */
     static constexpr int C = C_;     /* clients */
     DocHdr h;
-    int32_t len[S], seq[S], rseq[S];
+    /* len is 0 in every slot that holds no row (rows always have len >= 1), so a scan needs no
+     * child count; the three int32 columns are read 4 slots at a time (16-byte LDS reads) */
+    alignas(16) int32_t len[S];
+    alignas(16) int32_t seq[S];
+    alignas(16) int32_t rseq[S];
     int16_t rid[S];   /* slot -> row id (stable identity of a segment; cold data index) */
     int16_t rleaf[S]; /* row id -> leaf node currently holding it */
-    uint8_t cli[S], rcli[S], flags[S], ng[S];
+    alignas(4) uint8_t cli[S];
+    alignas(4) uint8_t rcli[S];
+    alignas(4) uint8_t flags[S];
+    alignas(4) uint8_t ng[S];
     uint8_t rgen[S]; /* row id -> generation, bumped when the id is freed */
     int16_t nparent[N], lorder[N], lpos[N];
     int16_t kids[N * 8];
@@ -119,7 +132,9 @@ struct HotT {
     int32_t hseq[H];
     int16_t hrid[H];  /* segment (row id) queued for scouring */
     uint8_t hgen[H];  /* its row-id generation when queued: a mismatch means it was unlinked */
-    uint16_t s2l[C];
+    uint16_t s2l[C];  /* short client id -> long id (client.ts:637-661) */
+    uint8_t l2s[C];   /* long id (< C) -> short id, 0xFF = not seen yet */
+    uint16_t keys[NKEYS]; /* property key id of each doc key slot */
 };
 
 /* LDS-sized profile for config 2/3 documents (39.5 KB <= 160 KB / 4: 4 documents per CU; the
@@ -128,6 +143,15 @@ struct HotT {
 typedef HotT<192> HotSmall;
 typedef HotT<2048> HotMid;
 typedef HotT<16384> HotBig;
+
+struct alignas(16) I4 {
+    int32_t x[4];
+};
+struct alignas(4) B4 {
+    uint8_t x[4];
+};
+MT_HD I4 ld4(const int32_t* p) { return *(const I4*)p; } /* p 16-byte aligned */
+MT_HD B4 ldb4(const uint8_t* p) { return *(const B4*)p; } /* p 4-byte aligned */
 
 /* Per-document view: the hot image (LDS or global) plus global cold/arena/log pointers. */
 template <class HT>
@@ -160,37 +184,66 @@ struct Replica {
     HT& z; /* the hot image */
     W w;
 
-    MT_HD Replica(const Doc<HT>& doc, const W& wave) : d(doc), z(*doc.t), w(wave) {}
+    DocHdr h; /* the document header, held in registers (SGPRs on the GPU) while the replica runs */
+
+    MT_HD Replica(const Doc<HT>& doc, const W& wave) : d(doc), z(*doc.t), w(wave) { load_hdr(); }
+
+    MT_HD void load_hdr() {
+#define MT_HF(f) h.f = w.uniform(z.h.f);
+        MT_HDR_FIELDS(MT_HF)
+#undef MT_HF
+        h.sumR = z.h.sumR;
+        h.sumW = z.h.sumW;
+    }
+    /* write the register header back to the image; every mutating entry point ends with it */
+    MT_HD void commit() {
+#define MT_HF(f) z.h.f = h.f;
+        MT_HDR_FIELDS(MT_HF)
+#undef MT_HF
+        z.h.sumR = h.sumR;
+        z.h.sumW = h.sumW;
+        w.sync();
+    }
 
     MT_HD ColdRow& cold(int32_t s) const { return d.cold[z.rid[s]]; }
 
     MT_HD void fail(int32_t e) {
-        if (z.h.err == E_OK) {
-            z.h.err = e;
-            z.h.errOp = z.h.opsDone;
+        if (h.err == E_OK) {
+            h.err = e;
+            h.errOp = h.opsDone;
         }
     }
 
     /* ---- node allocation ------------------------------------------------------------- */
     MT_HD int32_t alloc_node(int8_t level) {
-        int32_t n = z.h.freeHead;
+        int32_t n = h.freeHead;
         if (n < 0) {
             fail(E_CAPACITY);
             return -1;
         }
-        z.h.freeHead = z.nparent[n];
-        z.h.nfree--;
+        h.freeHead = z.nparent[n];
+        h.nfree--;
         z.nparent[n] = -1;
         z.nchild[n] = 0;
         z.nlevel[n] = level;
         z.nscour[n] = -1; /* needsScour undefined */
+        clear_slots(n * MAXN, MAXN);
         return n;
     }
+    /* mark `cnt` slots from `s` as holding no row */
+    MT_HD void clear_slots(int32_t s, int32_t cnt) {
+        w.sync();
+        for (int32_t b = 0; b < cnt; b += W::N) {
+            int32_t i = b + w.lane();
+            if (i < cnt) z.len[s + i] = 0;
+        }
+        w.sync();
+    }
     MT_HD void free_node(int32_t n) {
-        z.nparent[n] = (int16_t)z.h.freeHead;
+        z.nparent[n] = (int16_t)h.freeHead;
         z.nchild[n] = 0;
-        z.h.freeHead = n;
-        z.h.nfree++;
+        h.freeHead = n;
+        h.nfree++;
     }
 
     /* ---- init -------------------------------------------------------------------------- */
@@ -211,77 +264,88 @@ struct Replica {
             if (i < HT::S) {
                 d.frid[i] = (int16_t)(HT::S - 1 - i);
                 z.rgen[i] = 0;
+                z.len[i] = 0;
             }
         }
         w.sync();
-        DocHdr* h = &z.h;
-        h->nfreeRid = HT::S;
-        h->gcEpoch = 0;
-        h->freeHead = 1;
-        h->nfree = ncap - 1;
-        h->root = 0;
+        h.nfreeRid = HT::S;
+        h.gcEpoch = 0;
+        h.freeHead = 1;
+        h.nfree = ncap - 1;
+        h.root = 0;
         z.nparent[0] = -1;
         z.lorder[0] = 0;
         z.lpos[0] = 0;
-        h->nleaf = 1;
-        h->currentSeq = 0;
-        h->minSeq = 0;
-        h->localSeq = 0;
-        h->collaborating = 0;
-        h->localShort = -1; /* collabWindow.clientId = LocalClientId */
-        h->localLong = -1;
-        h->nclients = 0;
-        h->nextSid = 1;
-        h->heapN = 0;
-        h->memN = 0;
-        h->gqHead = 0;
-        h->gqN = 0;
-        h->arenaTop = 0;
-        h->arenaSide = 0;
-        h->err = 0;
-        h->errOp = -1;
-        h->nkeys = 0;
-        h->opsDone = 0;
-        h->hwSlots = 0;
-        h->hwHeap = 0;
-        h->nrows = 0;
-        h->seqOps = 0;
-        h->sumR = 0;
-        h->sumW = 0;
+        h.nleaf = 1;
+        h.currentSeq = 0;
+        h.minSeq = 0;
+        h.localSeq = 0;
+        h.collaborating = 0;
+        h.localShort = -1; /* collabWindow.clientId = LocalClientId */
+        h.localLong = -1;
+        h.nclients = 0;
+        h.nextSid = 1;
+        h.heapN = 0;
+        h.memN = 0;
+        h.gqHead = 0;
+        h.gqN = 0;
+        h.arenaTop = 0;
+        h.arenaSide = 0;
+        h.err = 0;
+        h.errOp = -1;
+        h.nkeys = 0;
+        h.opsDone = 0;
+        h.hwSlots = 0;
+        h.hwHeap = 0;
+        h.nrows = 0;
+        h.seqOps = 0;
+        h.sumR = 0;
+        h.sumW = 0;
+        h.localLen = 0;
+        h._r0 = h._r1 = h._r2 = 0;
+        for (int32_t b = 0; b < HT::C; b += W::N) {
+            int32_t i = b + w.lane();
+            if (i < HT::C) z.l2s[i] = 0xFF;
+        }
         w.sync();
     }
 
     /* ---- clients (client.ts:637-661) --------------------------------------------------- */
     MT_HD int32_t short_of(int32_t longId) {
-        for (int32_t i = 0; i < z.h.nclients; i++)
+        if ((uint32_t)longId < (uint32_t)HT::C) {
+            int32_t s = z.l2s[longId];
+            return s == 0xFF ? -1 : s;
+        }
+        for (int32_t i = 0; i < h.nclients; i++)
             if (z.s2l[i] == longId) return i;
         return -1;
     }
     MT_HD int32_t get_or_add_short(int32_t longId) {
         int32_t s = short_of(longId);
         if (s >= 0) return s;
-        int32_t n = z.h.nclients;
+        int32_t n = h.nclients;
         if (n >= HT::C || n >= 0xFE) {
             fail(E_CAPACITY);
             return 0;
         }
         z.s2l[n] = (uint16_t)longId;
-        z.h.nclients = n + 1;
+        if ((uint32_t)longId < (uint32_t)HT::C) z.l2s[longId] = (uint8_t)n;
+        h.nclients = n + 1;
         return n;
     }
     /* startOrUpdateCollaboration (client.ts:1053-1073) + startCollaboration (mergeTree.ts:1287) */
     MT_HD void start_collab(int32_t longId, int32_t minSeq, int32_t curSeq) {
-        if (z.h.localLong >= 0) return;
-        z.h.localLong = longId;
-        z.h.localShort = get_or_add_short(longId);
-        z.h.minSeq = minSeq;
-        z.h.currentSeq = curSeq;
-        z.h.collaborating = 1;
+        if (h.localLong >= 0) return;
+        h.localLong = longId;
+        h.localShort = get_or_add_short(longId);
+        h.minSeq = minSeq;
+        h.currentSeq = curSeq;
+        h.collaborating = 1;
     }
 
     /* ---- row helpers ------------------------------------------------------------------- */
     MT_HD bool is_local(int32_t client) const {
-        return !z.h.collaborating || client == z.h.localShort;
+        return !h.collaborating || client == h.localShort;
     }
     /* nodeLength of a leaf (mergeTree.ts:1692-1732); local perspective -> localNetLength */
     MT_HD int32_t vis(int32_t s, int32_t refSeq, int32_t client) const {
@@ -311,7 +375,7 @@ struct Replica {
 
     MT_HD int32_t slot_at(int32_t t) const { /* t = k*8+j over lorder; -1 if not a row */
         int32_t k = t >> 3, j = t & 7;
-        if (k >= z.h.nleaf) return -1;
+        if (k >= h.nleaf) return -1;
         int32_t n = z.lorder[k];
         return j < z.nchild[n] ? n * MAXN + j : -1;
     }
@@ -399,17 +463,17 @@ struct Replica {
     }
     /* cold row ids */
     MT_HD int32_t alloc_rid() {
-        int32_t n = z.h.nfreeRid;
+        int32_t n = h.nfreeRid;
         if (n <= 0) {
             fail(E_CAPACITY);
             return 0;
         }
-        z.h.nfreeRid = n - 1;
+        h.nfreeRid = n - 1;
         return d.frid[n - 1];
     }
     MT_HD void free_rid(int32_t r) {
         z.rgen[r]++;
-        d.frid[z.h.nfreeRid++] = (int16_t)r;
+        d.frid[h.nfreeRid++] = (int16_t)r;
     }
     /* record leaf n as the holder of its first `cnt` rows */
     MT_HD void set_leaf_of_rows(int32_t n, int32_t cnt) {
@@ -436,14 +500,64 @@ struct Replica {
     }
 
     /* ---- perspective scans ------------------------------------------------------------- */
+    /* The scans walk the document-order slot space t = k * 8 + j (leaf lorder[k], child j). A lane
+     * covers a quad of 4 consecutive slots (half a leaf slab, contiguous in the SoA columns), so one
+     * pass of the wave covers 256 slots with one lorder read and one 16-byte read per int32 column,
+     * and the position search is a per-lane 4-step prefix plus one wavefront exclusive scan. */
+    MT_HD int32_t quad_slot(int32_t t0) const { /* t0 % 4 == 0; -1 past the last leaf */
+        int32_t k = t0 >> 3;
+        if (k >= h.nleaf) return -1;
+        return z.lorder[k] * MAXN + (t0 & 4);
+    }
+    MT_HD bool ovl_has(int32_t s, int32_t client) const {
+        uint64_t ov = cold(s).ovl;
+        for (int k = 0; k < NOVL; k++) {
+            uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
+            if (e == 0) break;
+            if ((int32_t)e - 1 == client) return true;
+        }
+        return false;
+    }
+    /* nodeLength (mergeTree.ts:1692-1732) of the 4 slots from s0 under (refSeq, client); 0 for
+     * empty slots */
+    MT_HD void quad_vis(int32_t s0, int32_t refSeq, int32_t client, int32_t v[4]) const {
+        if (s0 < 0) {
+            v[0] = v[1] = v[2] = v[3] = 0;
+            return;
+        }
+        I4 L = ld4(&z.len[s0]);
+        I4 R = ld4(&z.rseq[s0]);
+        if (is_local(client)) { /* localNetLength (mergeTree.ts:1195-1206) */
+            for (int q = 0; q < 4; q++) v[q] = R.x[q] == NOREM ? L.x[q] : 0;
+            return;
+        }
+        I4 Q = ld4(&z.seq[s0]);
+        B4 C = ldb4(&z.cli[s0]);
+        B4 RC = ldb4(&z.rcli[s0]);
+        B4 F = ldb4(&z.flags[s0]);
+        for (int q = 0; q < 4; q++) {
+            int32_t c = C.x[q] == LOCAL_CLIENT ? -1 : (int32_t)C.x[q];
+            int32_t sq = Q.x[q];
+            bool ok = L.x[q] > 0 && (c == client || (sq != UNASSIGNED_SEQ && sq <= refSeq));
+            int32_t rs = R.x[q];
+            if (ok && rs != NOREM) {
+                int32_t rc = RC.x[q] == LOCAL_CLIENT ? -1 : (int32_t)RC.x[q];
+                if (rc == client || (rs != UNASSIGNED_SEQ && rs <= refSeq))
+                    ok = false;
+                else if (F.x[q] & RF_OVL)
+                    ok = !ovl_has(s0 + q, client);
+            }
+            v[q] = ok ? L.x[q] : 0;
+        }
+    }
     /* Total length under a perspective (getLength, mergeTree.ts:1610). */
     MT_HD int32_t length(int32_t refSeq, int32_t client) {
         int32_t total = 0;
-        int32_t T = z.h.nleaf * MAXN;
-        for (int32_t b = 0; b < T; b += W::N) {
-            int32_t s = slot_at(b + w.lane());
-            int32_t v = s >= 0 ? vis(s, refSeq, client) : 0;
-            total += w.sum(v);
+        int32_t T = h.nleaf * MAXN;
+        for (int32_t b = 0; b < T; b += 4 * W::N) {
+            int32_t v[4];
+            quad_vis(quad_slot(b + 4 * w.lane()), refSeq, client, v);
+            total += w.sum(v[0] + v[1] + v[2] + v[3]);
         }
         return total;
     }
@@ -451,19 +565,25 @@ struct Replica {
      * and P of that row. */
     MT_HD int32_t find_reach(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
         int32_t run = 0;
-        int32_t T = z.h.nleaf * MAXN;
-        for (int32_t b = 0; b < T; b += W::N) {
-            int32_t t = b + w.lane();
-            int32_t s = slot_at(t);
-            int32_t v = s >= 0 ? vis(s, refSeq, client) : 0;
+        int32_t T = h.nleaf * MAXN;
+        for (int32_t b = 0; b < T; b += 4 * W::N) {
+            int32_t v[4];
+            quad_vis(quad_slot(b + 4 * w.lane()), refSeq, client, v);
             int32_t tot;
-            int32_t P = run + w.excl_scan(v, &tot);
-            bool hit = s >= 0 && P < pos && pos <= P + v;
-            uint64_t m = w.ballot(hit);
+            int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
+            int32_t hq = -1, hp = 0;
+            for (int q = 0; q < 4; q++) {
+                if (hq < 0 && p < pos && pos <= p + v[q]) {
+                    hq = q;
+                    hp = p;
+                }
+                p += v[q];
+            }
+            uint64_t m = w.ballot(hq >= 0);
             if (m) {
                 int32_t l = W::ffs(m);
-                *Pout = w.bcast(P, l);
-                return b + l;
+                *Pout = w.bcast(hp, l);
+                return b + 4 * l + w.bcast(hq, l);
             }
             run += tot;
             if (run >= pos && pos > 0) break;
@@ -491,11 +611,11 @@ struct Replica {
     /* insert leaf `nl` into lorder right after leaf `after` */
     MT_HD void lorder_insert_after(int32_t after, int32_t nl) {
         int32_t k = z.lpos[after] + 1;
-        int32_t n = z.h.nleaf;
+        int32_t n = h.nleaf;
         lorder_shift(k, n, 1);
         z.lorder[k] = (int16_t)nl;
         z.lpos[nl] = (int16_t)k;
-        z.h.nleaf = n + 1;
+        h.nleaf = n + 1;
     }
     /* split (mergeTree.ts:2509-2522) of a full node (8 children) into 4 + 4; the new node is
      * inserted after it in its parent, recursively; root split -> updateRoot (1909-1920).
@@ -511,6 +631,7 @@ struct Replica {
             if (lvl == 0) {
                 move_rows(nn * MAXN, n * MAXN + 4, 4);
                 set_leaf_of_rows(nn, 4);
+                clear_slots(n * MAXN + 4, 4);
             } else {
                 for (int32_t i = 0; i < 4; i++) {
                     int32_t c = z.kids[n * MAXN + 4 + i];
@@ -530,7 +651,7 @@ struct Replica {
                 z.nchild[r] = 2;
                 z.nparent[n] = (int16_t)r;
                 z.nparent[nn] = (int16_t)r;
-                z.h.root = r;
+                h.root = r;
                 return first;
             }
             node_insert_child(p, child_index(p, n) + 1, nn);
@@ -556,15 +677,15 @@ struct Replica {
     MT_HD uint16_t* arena_base(int32_t side) { return d.arena + (int64_t)side * d.caps.acap; }
     /* reserve n units at the arena top; compacts into the other half when full */
     MT_HD int32_t arena_alloc(int32_t n) {
-        if (z.h.arenaTop + n > d.caps.acap) {
+        if (h.arenaTop + n > d.caps.acap) {
             arena_gc();
-            if (z.h.arenaTop + n > d.caps.acap) {
+            if (h.arenaTop + n > d.caps.acap) {
                 fail(E_CAPACITY);
                 return -1;
             }
         }
-        int32_t off = z.h.arenaTop;
-        z.h.arenaTop = off + n;
+        int32_t off = h.arenaTop;
+        h.arenaTop = off + n;
         return off;
     }
     MT_HD void arena_copy(uint16_t* dst, const uint16_t* src, int32_t n) {
@@ -579,13 +700,13 @@ struct Replica {
     /* copy all live text rows into the other half, in document order. A row id is moved once
      * per GC even if its slot is transiently duplicated (scour compacts a slab in place). */
     MT_HD void arena_gc() {
-        int32_t from = z.h.arenaSide, to = from ^ 1;
+        int32_t from = h.arenaSide, to = from ^ 1;
         uint16_t* src = arena_base(from);
         uint16_t* dst = arena_base(to);
-        int32_t ep = z.h.gcEpoch % 255 + 1;
-        z.h.gcEpoch = ep;
+        int32_t ep = h.gcEpoch % 255 + 1;
+        h.gcEpoch = ep;
         int32_t top = 0;
-        int32_t T = z.h.nleaf * MAXN;
+        int32_t T = h.nleaf * MAXN;
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
             if (s < 0 || (z.flags[s] & RF_MARKER) || cold(s).gc == ep) continue;
@@ -595,8 +716,8 @@ struct Replica {
             cold(s).gc = (uint8_t)ep;
             top += L;
         }
-        z.h.arenaSide = to;
-        z.h.arenaTop = top;
+        h.arenaSide = to;
+        h.arenaTop = top;
         w.sync();
     }
 
@@ -620,17 +741,17 @@ struct Replica {
         z.len[rs] = z.len[ls] - off;
         cold(rs).toff = cold(ls).toff + (uint32_t)off;
         z.len[ls] = off;
-        z.h.nrows++;
-        z.h.sumW += 2;
+        h.nrows++;
+        h.sumW += 2;
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
          * same pending groups (in the row's FIFO order = log order), appended at the end of each
          * group's segment list */
         if (z.ng[ls]) {
-            if (z.h.memN + z.ng[ls] > d.caps.mcap) mem_compact();
-            int32_t head = z.h.gqN ? d.gq[z.h.gqHead % d.caps.gcap] : 0x7fffffff;
+            if (h.memN + z.ng[ls] > d.caps.mcap) mem_compact();
+            int32_t head = h.gqN ? d.gq[h.gqHead % d.caps.gcap] : 0x7fffffff;
             int32_t lrid = z.rid[ls];
             int32_t rrid = z.rid[rs];
-            int32_t m0 = z.h.memN;
+            int32_t m0 = h.memN;
             for (int32_t b = 0; b < m0; b += W::N) {
                 int32_t i = b + w.lane();
                 int32_t g = i < m0 ? d.mgid[i] : -1;
@@ -647,10 +768,10 @@ struct Replica {
 
     /* ---- segment groups ---------------------------------------------------------------- */
     MT_HD void mem_append(int32_t gid, int32_t rid) {
-        int32_t m = z.h.memN;
+        int32_t m = h.memN;
         if (m >= d.caps.mcap) {
             mem_compact();
-            m = z.h.memN;
+            m = h.memN;
             if (m >= d.caps.mcap) {
                 fail(E_CAPACITY);
                 return;
@@ -658,12 +779,12 @@ struct Replica {
         }
         d.mgid[m] = gid;
         d.mrid[m] = rid;
-        z.h.memN = m + 1;
+        h.memN = m + 1;
     }
     /* drop entries of groups already acked (gid < head gid): wave stream compaction */
     MT_HD void mem_compact() {
-        int32_t head = z.h.gqN ? d.gq[z.h.gqHead % d.caps.gcap] : 0x7fffffff;
-        int32_t n = z.h.memN, wpos = 0;
+        int32_t head = h.gqN ? d.gq[h.gqHead % d.caps.gcap] : 0x7fffffff;
+        int32_t n = h.memN, wpos = 0;
         for (int32_t b = 0; b < n; b += W::N) {
             int32_t i = b + w.lane();
             int32_t g = i < n ? d.mgid[i] : -1;
@@ -679,7 +800,7 @@ struct Replica {
             w.sync();
             wpos += tot;
         }
-        z.h.memN = wpos;
+        h.memN = wpos;
     }
     /* SegmentGroupCollection.enqueue (segmentGroupCollection.ts:28-31) */
     MT_HD void row_enqueue_group(int32_t s, int32_t gid) {
@@ -694,12 +815,12 @@ struct Replica {
     /* addToPendingList (mergeTree.ts:1955-1962); the group id is the op's localSeq */
     MT_HD void pending_add(int32_t s, int32_t gid, bool* created) {
         if (!*created) {
-            if (z.h.gqN >= d.caps.gcap) {
+            if (h.gqN >= d.caps.gcap) {
                 fail(E_CAPACITY);
                 return;
             }
-            d.gq[(z.h.gqHead + z.h.gqN) % d.caps.gcap] = gid;
-            z.h.gqN++;
+            d.gq[(h.gqHead + h.gqN) % d.caps.gcap] = gid;
+            h.gqN++;
             *created = true;
         }
         row_enqueue_group(s, gid);
@@ -718,7 +839,7 @@ struct Replica {
         z.hgen[j] = tg;
     }
     MT_HD void heap_add(int32_t rid, int32_t seq) {
-        int32_t n = z.h.heapN;
+        int32_t n = h.heapN;
         if (n >= HT::H) {
             fail(E_CAPACITY);
             return;
@@ -728,8 +849,8 @@ struct Replica {
         z.hrid[k - 1] = (int16_t)rid;
         z.hseq[k - 1] = seq;
         z.hgen[k - 1] = z.rgen[rid];
-        z.h.heapN = n + 1;
-        if (n + 1 > z.h.hwHeap) z.h.hwHeap = n + 1;
+        h.heapN = n + 1;
+        if (n + 1 > h.hwHeap) h.hwHeap = n + 1;
         while (k > 1 && z.hseq[(k >> 1) - 1] - z.hseq[k - 1] > 0) {
             heap_swap((k >> 1) - 1, k - 1);
             k >>= 1;
@@ -737,7 +858,7 @@ struct Replica {
     }
     /* get (collections.ts:227-233) + fixdown (249-263) */
     MT_HD void heap_pop(int32_t* rid, int32_t* seq, int32_t* gen) {
-        int32_t cnt = z.h.heapN;
+        int32_t cnt = h.heapN;
         *rid = z.hrid[0];
         *seq = z.hseq[0];
         *gen = z.hgen[0];
@@ -745,7 +866,7 @@ struct Replica {
         z.hseq[0] = z.hseq[cnt - 1];
         z.hgen[0] = z.hgen[cnt - 1];
         cnt--;
-        z.h.heapN = cnt;
+        h.heapN = cnt;
         int32_t k = 1;
         while ((k << 1) <= cnt) {
             int32_t j = k << 1;
@@ -758,7 +879,7 @@ struct Replica {
     /* addToLRUSet (mergeTree.ts:1306-1316) */
     MT_HD void add_lru(int32_t s, int32_t seq) {
         int32_t n = s / MAXN;
-        if (z.nscour[n] != 1 && seq > z.h.currentSeq) {
+        if (z.nscour[n] != 1 && seq > h.currentSeq) {
             z.nscour[n] = 1;
             heap_add(z.rid[s], seq);
         }
@@ -766,14 +887,14 @@ struct Replica {
 
     /* ---- properties (segmentPropertiesManager.ts:35-111) ---------------------------- */
     MT_HD int32_t key_slot(uint16_t key) {
-        for (int32_t i = 0; i < z.h.nkeys; i++)
-            if (z.h.keys[i] == key) return i;
-        if (z.h.nkeys >= NKEYS) {
+        for (int32_t i = 0; i < h.nkeys; i++)
+            if (z.keys[i] == key) return i;
+        if (h.nkeys >= NKEYS) {
             fail(E_UNSUPPORTED);
             return -1;
         }
-        z.h.keys[z.h.nkeys] = key;
-        return z.h.nkeys++;
+        z.keys[h.nkeys] = key;
+        return h.nkeys++;
     }
     MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
         if (!(z.flags[s] & RF_PROPS)) {
@@ -787,11 +908,11 @@ struct Replica {
         if (cold(s).prw > 0 && seq != UNASSIGNED_SEQ && collaborating) return;
         if (rewrite) {
             if (collaborating && seq == UNASSIGNED_SEQ) cold(s).prw++;
-            for (int32_t k = 0; k < z.h.nkeys; k++) {
+            for (int32_t k = 0; k < h.nkeys; k++) {
                 if (cold(s).pv[k] == 0) continue;
                 bool inNew = false;
                 for (int32_t j = 0; j < nkv; j++)
-                    if (kv[j].key == z.h.keys[k] && kv[j].value != 0 && !(kv[j].value & MT_VALUE_FALSY)) inNew = true;
+                    if (kv[j].key == z.keys[k] && kv[j].value != 0 && !(kv[j].value & MT_VALUE_FALSY)) inNew = true;
                 bool modify = seq == UNASSIGNED_SEQ || cold(s).pk[k] == 0;
                 if (!inNew && modify) cold(s).pv[k] = 0;
             }
@@ -836,15 +957,15 @@ struct Replica {
     MT_HD bool can_append(int32_t a, int32_t b) {
         if (z.flags[a] & RF_MARKER) return false;
         int32_t L = z.len[a];
-        if (L > 0 && arena_base(z.h.arenaSide)[cold(a).toff + L - 1] == '\n') return false;
+        if (L > 0 && arena_base(h.arenaSide)[cold(a).toff + L - 1] == '\n') return false;
         if (z.flags[b] & RF_MARKER) return false;
         return z.len[a] <= GRANULARITY || z.len[b] <= GRANULARITY;
     }
     /* TextSegment.append (textSegment.ts:74-85): the merged text is rebuilt at the arena top */
     MT_HD void append_text(int32_t a, int32_t b) {
         int32_t La = z.len[a], Lb = z.len[b];
-        uint16_t* base = arena_base(z.h.arenaSide);
-        if ((int32_t)cold(a).toff + La == z.h.arenaTop && z.h.arenaTop + Lb <= d.caps.acap) {
+        uint16_t* base = arena_base(h.arenaSide);
+        if ((int32_t)cold(a).toff + La == h.arenaTop && h.arenaTop + Lb <= d.caps.acap) {
             int32_t off = arena_alloc(Lb);
             arena_copy(base + off, base + cold(b).toff, Lb);
         } else if ((int32_t)cold(a).toff + La == (int32_t)cold(b).toff) {
@@ -852,7 +973,7 @@ struct Replica {
         } else {
             int32_t off = arena_alloc(La + Lb);
             if (off < 0) return;
-            base = arena_base(z.h.arenaSide); /* a GC may have switched halves */
+            base = arena_base(h.arenaSide); /* a GC may have switched halves */
             arena_copy(base + off, base + cold(a).toff, La);
             arena_copy(base + off + La, base + cold(b).toff, Lb);
             cold(a).toff = (uint32_t)off;
@@ -865,7 +986,7 @@ struct Replica {
         int32_t c = z.nchild[n];
         int32_t wpos = 0;
         int32_t prev = -1; /* slot of prevSegment in the compacted slab */
-        int32_t minSeq = z.h.minSeq;
+        int32_t minSeq = h.minSeq;
         for (int32_t k = 0; k < c; k++) {
             int32_t s = n * MAXN + k;
             if (z.ng[s] == 0) {
@@ -907,8 +1028,9 @@ struct Replica {
                 prev = -1;
             }
         }
-        z.h.nrows -= c - wpos;
+        h.nrows -= c - wpos;
         z.nchild[n] = (int8_t)wpos;
+        if (wpos < c) clear_slots(n * MAXN + wpos, c - wpos);
         return wpos;
     }
     /* pack (mergeTree.ts:1401-1453) of `block`'s parent */
@@ -980,17 +1102,18 @@ struct Replica {
                 z.nparent[nb] = (int16_t)parent;
                 z.nlevel[nb] = 0;
                 z.nscour[nb] = -1;
+                if (ncnt[ni] < MAXN) clear_slots(nb * MAXN + ncnt[ni], MAXN - ncnt[ni]);
             }
             for (int32_t i = cc; i < pc; i++) free_node(oldk[i]);
             /* lorder: [firstPos, firstPos+pc) becomes [firstPos, firstPos+cc) */
-            int32_t nl = z.h.nleaf;
+            int32_t nl = h.nleaf;
             int32_t delta = cc - pc;
             lorder_shift(firstPos + pc, nl, delta);
             for (int32_t i = pc; i < cc; i++) {
                 z.lorder[firstPos + i] = (int16_t)newk[i];
                 z.lpos[newk[i]] = (int16_t)(firstPos + i);
             }
-            z.h.nleaf = nl + delta;
+            h.nleaf = nl + delta;
             for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (int16_t)newk[i];
             z.nchild[parent] = (int8_t)cc;
         } else {
@@ -1031,10 +1154,10 @@ struct Replica {
     }
     /* zamboniSegments (mergeTree.ts:1455-1511) */
     MT_HD void zamboni() {
-        if (!z.h.collaborating) return;
+        if (!h.collaborating) return;
         for (int i = 0; i < 2; i++) {
-            if (z.h.heapN < 1) break;
-            if (z.hseq[0] > z.h.minSeq) break;
+            if (h.heapN < 1) break;
+            if (z.hseq[0] > h.minSeq) break;
             int32_t rid, mseq, gen;
             heap_pop(&rid, &mseq, &gen);
             int32_t s = slot_of(rid, gen); /* -1: unlinked or merged away since it was queued */
@@ -1051,10 +1174,10 @@ struct Replica {
     }
     /* setMinSeq (mergeTree.ts:1751-1769) */
     MT_HD void set_min_seq(int32_t minSeq) {
-        if (!(minSeq <= z.h.currentSeq)) fail(E_ASSERT);
-        if (!(z.h.minSeq <= minSeq)) fail(E_ASSERT);
-        if (minSeq > z.h.minSeq) {
-            z.h.minSeq = minSeq;
+        if (!(minSeq <= h.currentSeq)) fail(E_ASSERT);
+        if (!(h.minSeq <= minSeq)) fail(E_ASSERT);
+        if (minSeq > h.minSeq) {
+            h.minSeq = minSeq;
             zamboni();
         }
     }
@@ -1064,20 +1187,28 @@ struct Replica {
     MT_HD bool break_tie(int32_t s, int32_t refSeq, int32_t client) const {
         int32_t rs = z.rseq[s];
         if (rs != NOREM && rs != 0 && rs <= refSeq && rs != UNASSIGNED_SEQ) return false;
-        if (client == z.h.localShort) return true;
+        if (client == h.localShort) return true;
         return z.seq[s] != UNASSIGNED_SEQ;
     }
     /* continueFrom (2187-2194): first row after leaf lorder[k] with localNetLength > 0 is a
      * local-pending insert */
     MT_HD bool continue_from(int32_t k) {
-        int32_t T = z.h.nleaf * MAXN;
-        for (int32_t b = (k + 1) * MAXN; b < T; b += W::N) {
-            int32_t s = slot_at(b + w.lane());
-            uint64_t m = w.ballot(s >= 0 && local_len(s) > 0);
-            if (m) {
-                int32_t f = w.bcast(s, W::ffs(m));
-                return z.seq[f] == UNASSIGNED_SEQ;
+        int32_t T = h.nleaf * MAXN;
+        for (int32_t b = (k + 1) * MAXN; b < T; b += 4 * W::N) {
+            int32_t s0 = quad_slot(b + 4 * w.lane());
+            int32_t fq = -1, fseq = 0;
+            if (s0 >= 0) {
+                I4 L = ld4(&z.len[s0]);
+                I4 R = ld4(&z.rseq[s0]);
+                I4 Q = ld4(&z.seq[s0]);
+                for (int q = 3; q >= 0; q--)
+                    if (L.x[q] > 0 && R.x[q] == NOREM) {
+                        fq = q;
+                        fseq = Q.x[q];
+                    }
             }
+            uint64_t m = w.ballot(fq >= 0);
+            if (m) return w.bcast(fseq, W::ffs(m)) == UNASSIGNED_SEQ;
         }
         return false;
     }
@@ -1124,7 +1255,7 @@ struct Replica {
                 int32_t s = n * MAXN + j;
                 if (vis(s, refSeq, client) > 0 || break_tie(s, refSeq, client)) return leaf_insert_slot(n, j);
             }
-            if (seq != UNASSIGNED_SEQ && k + 1 < z.h.nleaf && continue_from(k)) {
+            if (seq != UNASSIGNED_SEQ && k + 1 < h.nleaf && continue_from(k)) {
                 k++;
                 j = 0;
                 continue;
@@ -1135,7 +1266,7 @@ struct Replica {
     MT_HD void insert_segments(const mt_op_rec& op, const Pools& p, int32_t refSeq, int32_t client, int32_t seq) {
         int32_t pos = op.pos1;
         bool hasL = seq == UNASSIGNED_SEQ;
-        int32_t localSeq = hasL ? ++z.h.localSeq : 0;
+        int32_t localSeq = hasL ? ++h.localSeq : 0;
         bool marker = op.seg_kind == MT_SEG_MARKER;
         int32_t L = marker ? 1 : op.text_len;
         if (L <= 0) ensure_boundary(pos, refSeq, client); /* the split still happens (2004) */
@@ -1164,13 +1295,14 @@ struct Replica {
             cold(s).prw = 0;
             cold(s).ovl = 0;
             z.rleaf[z.rid[s]] = (int16_t)(s / MAXN);
-            z.h.nrows++;
-            z.h.sumW++;
+            h.nrows++;
+            h.sumW++;
+            h.localLen += L;
             if (marker) {
                 cold(s).toff = (uint32_t)op.pos2;
             } else {
                 cold(s).toff = (uint32_t)off;
-                arena_copy(arena_base(z.h.arenaSide) + off, p.text + op.text_off, L);
+                arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
             }
             for (int k = 0; k < NKEYS; k++) {
                 cold(s).pv[k] = 0;
@@ -1180,35 +1312,45 @@ struct Replica {
                 const mt_props_rec& pr = p.props[op.props - 1];
                 add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE, 0, false);
             }
-            if (z.h.collaborating) { /* saveIfLocal (2197-2212) */
-                if (seq == UNASSIGNED_SEQ && client == z.h.localShort) {
+            if (h.collaborating) { /* saveIfLocal (2197-2212) */
+                if (seq == UNASSIGNED_SEQ && client == h.localShort) {
                     bool created = false;
                     pending_add(s, localSeq, &created);
-                } else if (seq > z.h.minSeq) {
+                } else if (seq > h.minSeq) {
                     add_lru(s, seq);
                 }
             }
         }
-        if (z.h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
+        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
 
     /* ---- range ops: markRangeRemoved (2640-2752) / annotateRange (2598-2638) ----------- */
     template <class F>
     MT_HD void map_range(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
         int32_t run = 0;
-        int32_t T = z.h.nleaf * MAXN;
-        for (int32_t b = 0; b < T; b += W::N) {
-            int32_t t = b + w.lane();
-            int32_t s = slot_at(t);
-            int32_t v = s >= 0 ? vis(s, refSeq, client) : 0;
+        int32_t T = h.nleaf * MAXN;
+        for (int32_t b = 0; b < T; b += 4 * W::N) {
+            int32_t s0 = quad_slot(b + 4 * w.lane());
+            int32_t v[4];
+            quad_vis(s0, refSeq, client, v);
             int32_t tot;
-            int32_t P = run + w.excl_scan(v, &tot);
-            bool hit = s >= 0 && v > 0 && P < end && P + v > start;
-            uint64_t m = w.ballot(hit);
+            int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
+            int32_t hm = 0;
+            for (int q = 0; q < 4; q++) {
+                if (v[q] > 0 && p < end && p + v[q] > start) hm |= 1 << q;
+                p += v[q];
+            }
+            uint64_t m = w.ballot(hm != 0);
             while (m) {
                 int32_t l = W::ffs(m);
                 m &= m - 1;
-                leaf(w.bcast(s, l));
+                int32_t bits = w.bcast(hm, l);
+                int32_t sb = w.bcast(s0, l);
+                while (bits) {
+                    int32_t q = __builtin_ctz((unsigned)bits);
+                    bits &= bits - 1;
+                    leaf(sb + q);
+                }
             }
             run += tot;
             if (run >= end) break;
@@ -1218,10 +1360,10 @@ struct Replica {
         ensure_boundary(start, refSeq, client);
         ensure_boundary(end, refSeq, client);
         bool hasL = seq == UNASSIGNED_SEQ;
-        int32_t localSeq = hasL ? ++z.h.localSeq : 0;
+        int32_t localSeq = hasL ? ++h.localSeq : 0;
         bool created = false;
         map_range(start, end, refSeq, client, [&](int32_t s) {
-            z.h.sumW++;
+            h.sumW++;
             if (z.rseq[s] != NOREM) {
                 if (z.rseq[s] == UNASSIGNED_SEQ) {
                     z.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
@@ -1239,6 +1381,7 @@ struct Replica {
                     }
                 }
             } else {
+                h.localLen -= z.len[s]; /* the row leaves the local view */
                 z.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
                 z.rseq[s] = seq;
                 cold(s).lrseq = localSeq;
@@ -1247,24 +1390,24 @@ struct Replica {
                 else
                     z.flags[s] &= (uint8_t)~RF_LRSEQ;
             }
-            if (z.h.collaborating) {
-                if (z.rseq[s] == UNASSIGNED_SEQ && client == z.h.localShort)
+            if (h.collaborating) {
+                if (z.rseq[s] == UNASSIGNED_SEQ && client == h.localShort)
                     pending_add(s, localSeq, &created);
                 else
                     add_lru(s, seq);
             }
         });
-        if (z.h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
+        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
     MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t refSeq,
                               int32_t client, int32_t seq) {
         ensure_boundary(start, refSeq, client);
         ensure_boundary(end, refSeq, client);
-        int32_t localSeq = seq == UNASSIGNED_SEQ ? ++z.h.localSeq : 0;
+        int32_t localSeq = seq == UNASSIGNED_SEQ ? ++h.localSeq : 0;
         bool created = false;
-        bool collab = z.h.collaborating;
+        bool collab = h.collaborating;
         map_range(start, end, refSeq, client, [&](int32_t s) {
-            z.h.sumW++;
+            h.sumW++;
             add_props(s, kv, nkv, rewrite, seq, collab);
             if (collab) {
                 if (seq == UNASSIGNED_SEQ)
@@ -1273,16 +1416,16 @@ struct Replica {
                     add_lru(s, seq);
             }
         });
-        if (z.h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
+        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
 
     /* ---- ack (mergeTree.ts:1926-1953, BaseSegment.ack 486-521) ------------------------ */
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
-        if (z.h.gqN > 0) {
-            int32_t gid = d.gq[z.h.gqHead % d.caps.gcap];
-            z.h.gqHead = (z.h.gqHead + 1) % d.caps.gcap;
-            z.h.gqN--;
-            int32_t mn = z.h.memN;
+        if (h.gqN > 0) {
+            int32_t gid = d.gq[h.gqHead % d.caps.gcap];
+            h.gqHead = (h.gqHead + 1) % d.caps.gcap;
+            h.gqN--;
+            int32_t mn = h.memN;
             for (int32_t b = 0; b < mn; b += W::N) {
                 int32_t i = b + w.lane();
                 int32_t rd = i < mn ? d.mrid[i] : 0;
@@ -1324,7 +1467,7 @@ struct Replica {
 
     /* ---- Client.applyMsg (client.ts:797-819) / local edits ---------------------------- */
     MT_HD void apply(const mt_op_rec& op, const Pools& p) {
-        if (z.h.err) return;
+        if (h.err) return;
         int32_t kind = op.kind & MT_OP_KIND_MASK;
         const mt_kv* kv = 0;
         int32_t nkv = 0;
@@ -1336,9 +1479,9 @@ struct Replica {
             rw = pr.combining == MT_COMBINE_REWRITE;
         }
         if (op.kind & MT_OPF_LOCAL) {
-            int32_t client = z.h.collaborating ? z.h.localShort : -1;
-            int32_t refSeq = z.h.currentSeq;
-            int32_t seq = z.h.collaborating ? UNASSIGNED_SEQ : UNIVERSAL_SEQ;
+            int32_t client = h.collaborating ? h.localShort : -1;
+            int32_t refSeq = h.currentSeq;
+            int32_t seq = h.collaborating ? UNASSIGNED_SEQ : UNIVERSAL_SEQ;
             /* getValidOpRange (client.ts:486-548) */
             int32_t length = length_local();
             int32_t start = op.pos1, end = op.pos2;
@@ -1356,14 +1499,14 @@ struct Replica {
             } else if (kind == MT_OP_ANNOTATE) {
                 annotate_range(start, end, kv, nkv, rw, refSeq, client, seq);
             }
-            z.h.opsDone++;
+            h.opsDone++;
             return;
         }
         get_or_add_short(op.client);
-        z.h.seqOps++;
-        z.h.sumR += z.h.nrows;
+        h.seqOps++;
+        h.sumR += h.nrows;
         if (kind != MT_OP_NOOP) {
-            if ((int32_t)op.client == z.h.localLong) {
+            if ((int32_t)op.client == h.localLong) {
                 ack(kind, kv, nkv, rw, op.seq);
             } else {
                 int32_t client = get_or_add_short(op.client);
@@ -1373,27 +1516,28 @@ struct Replica {
                     mark_range_removed(op.pos1, op.pos2, op.ref_seq, client, op.seq);
                 else if (kind == MT_OP_ANNOTATE)
                     annotate_range(op.pos1, op.pos2, kv, nkv, rw, op.ref_seq, client, op.seq);
-                if (!(z.h.currentSeq < op.seq)) fail(E_ASSERT);
-                if (!(z.h.minSeq <= op.min_seq)) fail(E_ASSERT);
+                if (!(h.currentSeq < op.seq)) fail(E_ASSERT);
+                if (!(h.minSeq <= op.min_seq)) fail(E_ASSERT);
             }
         }
         /* updateSeqNumbers (client.ts:821-828) */
-        if (!(z.h.currentSeq <= op.seq)) fail(E_ASSERT);
-        z.h.currentSeq = op.seq;
+        if (!(h.currentSeq <= op.seq)) fail(E_ASSERT);
+        h.currentSeq = op.seq;
         if (!(op.min_seq <= op.seq)) fail(E_ASSERT);
         set_min_seq(op.min_seq);
-        z.h.opsDone++;
-        int32_t slots = z.h.nleaf * MAXN;
-        if (slots > z.h.hwSlots) z.h.hwSlots = slots;
+        h.opsDone++;
+        int32_t slots = h.nleaf * MAXN;
+        if (slots > h.hwSlots) h.hwSlots = slots;
     }
-    MT_HD int32_t length_local() { return length(z.h.currentSeq, z.h.localShort); }
+    /* Client.getLength(): the local view's length, kept incrementally like root.cachedLength */
+    MT_HD int32_t length_local() const { return h.localLen; }
 
     /* ---- reads: text (MergeTreeTextHelper.getText, textSegment.ts:154-275) ------------ */
     /* Writes at most cap units; returns the text length under the perspective. */
     MT_HD int64_t get_text(int32_t refSeq, int32_t client, uint16_t* out, int64_t cap) {
         int64_t n = 0;
-        int32_t T = z.h.nleaf * MAXN;
-        const uint16_t* base = arena_base(z.h.arenaSide);
+        int32_t T = h.nleaf * MAXN;
+        const uint16_t* base = arena_base(h.arenaSide);
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
             if (s < 0 || (z.flags[s] & RF_MARKER)) continue;
@@ -1442,12 +1586,12 @@ struct Replica {
     }
     MT_HD void dump_to(Sink* o) {
         int32_t nsegs = 0;
-        int32_t T = z.h.nleaf * MAXN;
+        int32_t T = h.nleaf * MAXN;
         for (int32_t t = 0; t < T; t++)
             if (slot_at(t) >= 0) nsegs++;
-        int32_t hdr[6] = {z.h.currentSeq, z.h.minSeq, z.h.localSeq, length_local(), nsegs, z.h.nleaf};
+        int32_t hdr[6] = {h.currentSeq, h.minSeq, h.localSeq, length_local(), nsegs, h.nleaf};
         put_bytes(o, hdr, sizeof(hdr));
-        const uint16_t* base = arena_base(z.h.arenaSide);
+        const uint16_t* base = arena_base(h.arenaSide);
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
             if (s < 0) continue;
@@ -1484,7 +1628,7 @@ struct Replica {
             for (int q = 0; q < np; q++) {
                 int32_t best = -1, bk = 0x7fffffff;
                 for (int k = 0; k < NKEYS; k++) {
-                    int32_t key = z.h.keys[k];
+                    int32_t key = z.keys[k];
                     if (cold(s).pv[k] && key > last && key < bk) {
                         bk = key;
                         best = k;
@@ -1509,7 +1653,7 @@ struct Replica {
     MT_HD void replay(const Pools& p) {
         for (int64_t i = 0; i < p.nops; i++) {
             apply(p.ops[i], p);
-            if (z.h.err) break;
+            if (h.err) break;
         }
     }
 };

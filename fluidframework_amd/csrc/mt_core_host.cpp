@@ -29,15 +29,22 @@ struct mth_store {
 /* call F with a Replica<WaveHost, HT> for doc d of the store's profile */
 template <class F>
 static auto with_replica(mth_store* s, int64_t d, F&& f) {
+    /* every call ends with commit(): the replica's register header goes back to the image */
     if (s->profile == 0) {
         Replica<WaveHost, HotSmall> r(s->s0.doc(d), WaveHost());
-        return f(r);
+        auto res = f(r);
+        r.commit();
+        return res;
     } else if (s->profile == 1) {
         Replica<WaveHost, HotMid> r(s->s1.doc(d), WaveHost());
-        return f(r);
+        auto res = f(r);
+        r.commit();
+        return res;
     }
     Replica<WaveHost, HotBig> r(s->s2.doc(d), WaveHost());
-    return f(r);
+    auto res = f(r);
+    r.commit();
+    return res;
 }
 
 extern "C" {
@@ -78,7 +85,7 @@ int32_t mth_apply(mth_store* s, int64_t doc, const mt_op_rec* op, const uint16_t
     return with_replica(s, doc, [&](auto& r) {
         Pools p = {op, 1, text, props, kv};
         r.apply(*op, p);
-        return r.z.h.err;
+        return r.h.err;
     });
 }
 
@@ -87,15 +94,15 @@ int32_t mth_replay(mth_store* s, int64_t doc, const mt_op_rec* ops, int64_t n, c
     return with_replica(s, doc, [&](auto& r) {
         Pools p = {ops, n, text, props, kv};
         r.replay(p);
-        return r.z.h.err;
+        return r.h.err;
     });
 }
 
 int32_t mth_error(mth_store* s, int64_t doc) {
-    return with_replica(s, doc, [](auto& r) { return r.z.h.err; });
+    return with_replica(s, doc, [](auto& r) { return r.h.err; });
 }
 int32_t mth_error_op(mth_store* s, int64_t doc) {
-    return with_replica(s, doc, [](auto& r) { return r.z.h.errOp; });
+    return with_replica(s, doc, [](auto& r) { return r.h.errOp; });
 }
 
 int32_t mth_length(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client) {
@@ -115,8 +122,8 @@ int64_t mth_text(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client
         int32_t sh;
         int32_t rs = ref_seq;
         if (long_client < 0) {
-            sh = r.z.h.localShort;
-            rs = r.z.h.currentSeq;
+            sh = r.h.localShort;
+            rs = r.h.currentSeq;
         } else {
             sh = r.short_of(long_client);
             if (sh < 0) sh = 0x7fff;
@@ -135,7 +142,7 @@ uint64_t mth_digest(mth_store* s, int64_t doc) {
 
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {
     with_replica(s, doc, [&](auto& r) {
-        DocHdr* h = &r.z.h;
+        DocHdr* h = &r.h;
         out8[0] = h->nleaf;
         out8[1] = h->hwSlots;
         out8[2] = h->hwHeap;

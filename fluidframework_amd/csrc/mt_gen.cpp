@@ -188,7 +188,7 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
     int insert_index = 0;
     int32_t seq = 0;
     if (P->mode == MTG_OBSERVER) {
-        while (seq < P->ops_per_doc && !o->overflow && !m.r->z.h.err) {
+        while (seq < P->ops_per_doc && !o->overflow && !m.r->h.err) {
             int client = uni(&r, 1, nclients - 1);
             int32_t ref = seq; /* refSeq = seq - 1 for the op sequenced now */
             mt_op_rec* e = emit(o);
@@ -206,8 +206,8 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
         Pending* q = (Pending*)malloc(sizeof(Pending) * (P->ops_per_doc + 16));
         int qh = 0, qn = 0;
         int32_t lastTarget = 0, msn = 0;
-        while (seq < P->ops_per_doc && !o->overflow && !m.r->z.h.err) {
-            int32_t cur = m.r->z.h.currentSeq;
+        while (seq < P->ops_per_doc && !o->overflow && !m.r->h.err) {
+            int32_t cur = m.r->h.currentSeq;
             /* 1. a local edit, made against the local view (client.ts:164-211) */
             if (P->local_pct && uni(&r, 0, 99) < P->local_pct && qn < 4000) {
                 mt_op_rec* e = emit(o);
@@ -271,7 +271,7 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
         }
         free(q);
     }
-    if (m.r->z.h.err) o->overflow = 2;
+    if (m.r->h.err) o->overflow = 2;
     model_free(&m);
 }
 static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {

@@ -33,6 +33,7 @@ __global__ __launch_bounds__(WG) void k_init(Store<HT> st, int64_t ndocs) {
     if (d >= ndocs) return;
     Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
     r.init();
+    r.commit();
 }
 
 template <class HT>
@@ -42,6 +43,7 @@ __global__ __launch_bounds__(WG) void k_start_collab(Store<HT> st, int64_t ndocs
     if (d >= ndocs) return;
     Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
     r.start_collab(local_long[d], min_seq, cur_seq);
+    r.commit();
 }
 
 /* 16-byte vector copy of a hot image by the wave (HT is a multiple of 16 bytes) */
@@ -78,11 +80,13 @@ __global__ __launch_bounds__(WG) void k_replay(Store<HT> st, int64_t ndocs, cons
         v.t = &hot;
         Replica<WaveGPU, HT> r(v, WaveGPU());
         r.replay(p);
+        r.commit();
         __syncthreads();
         copy_image(g, &hot);
     } else {
         Replica<WaveGPU, HT> r(v, WaveGPU());
         r.replay(p);
+        r.commit();
     }
 }
 
@@ -123,8 +127,8 @@ __global__ __launch_bounds__(WG) void k_text(Store<HT> st, int64_t doc, int32_t 
     Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
     int32_t sh;
     if (long_client < 0) {
-        sh = r.z.h.localShort;
-        ref_seq = r.z.h.currentSeq;
+        sh = r.h.localShort;
+        ref_seq = r.h.currentSeq;
     } else {
         sh = r.short_of(long_client);
         if (sh < 0) sh = 0x7fff;

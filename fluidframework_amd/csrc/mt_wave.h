@@ -18,6 +18,7 @@ struct WaveHost {
     int32_t sum(int32_t v) const { return v; }
     uint64_t ballot(bool p) const { return p ? 1ull : 0ull; }
     int32_t bcast(int32_t v, int) const { return v; }
+    static int32_t uniform(int32_t v) { return v; }
     static int ffs(uint64_t m) { return __builtin_ctzll(m); }
     void sync() const {}
 };
@@ -53,6 +54,10 @@ struct WaveGPU {
         return __builtin_amdgcn_readlane(incl_scan(v), 63);
     }
     __device__ __attribute__((always_inline)) uint64_t ballot(bool p) const { return __ballot(p); }
+    /* a value every lane holds equally, moved to an SGPR */
+    __device__ __attribute__((always_inline)) static int32_t uniform(int32_t v) {
+        return __builtin_amdgcn_readfirstlane(v);
+    }
     /* l is wave-uniform: v_readlane, no LDS round trip */
     __device__ __attribute__((always_inline)) int32_t bcast(int32_t v, int l) const {
         return __builtin_amdgcn_readlane(v, l);
