@@ -175,6 +175,21 @@ struct Pools {
     const mt_kv* kv;
 };
 
+/* Phase clock for the profiling build only (-DMT_PROF, tools/phase_profile.py): shader-clock
+ * cycles accumulated per phase in registers and written out per document. */
+enum { PH_APPLY, PH_ZAMBONI, PH_FIND, PH_MAP, PH_SPLIT, PH_ACK, PH_TEXT, PH_HEAP, PH_N };
+#if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
+struct ProfScope {
+    uint64_t* acc;
+    uint64_t t0;
+    __device__ ProfScope(uint64_t* a) : acc(a), t0(__builtin_amdgcn_s_memtime()) {}
+    __device__ ~ProfScope() { *acc += __builtin_amdgcn_s_memtime() - t0; }
+};
+#define MT_PROF_SCOPE(i) ProfScope _ps##i(&prof[i])
+#else
+#define MT_PROF_SCOPE(i)
+#endif
+
 /* ------------------------------------------------------------------------------------------
  * Replica: all operations of one document replica, executed by one wave.
  * ---------------------------------------------------------------------------------------- */
@@ -185,6 +200,9 @@ struct Replica {
     W w;
 
     DocHdr h; /* the document header, held in registers (SGPRs on the GPU) while the replica runs */
+#ifdef MT_PROF
+    uint64_t prof[PH_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave) : d(doc), z(*doc.t), w(wave) { load_hdr(); }
 
@@ -564,6 +582,7 @@ struct Replica {
     /* First row (document order) with P < pos <= P + vis; returns t (lorder coordinate) or -1,
      * and P of that row. */
     MT_HD int32_t find_reach(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+        MT_PROF_SCOPE(PH_FIND);
         int32_t run = 0;
         int32_t T = h.nleaf * MAXN;
         for (int32_t b = 0; b < T; b += 4 * W::N) {
@@ -725,6 +744,7 @@ struct Replica {
     /* Split the row at lorder coordinate t at offset off (0 < off < len). Returns the slot of
      * the LEFT part afterwards (the right part is the next row in document order). */
     MT_HD int32_t split_row(int32_t t, int32_t off) {
+        MT_PROF_SCOPE(PH_SPLIT);
         int32_t n = z.lorder[t >> 3], j = t & 7;
         int32_t s0 = n * MAXN + j;
         if (z.flags[s0] & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
@@ -839,6 +859,7 @@ struct Replica {
         z.hgen[j] = tg;
     }
     MT_HD void heap_add(int32_t rid, int32_t seq) {
+        MT_PROF_SCOPE(PH_HEAP);
         int32_t n = h.heapN;
         if (n >= HT::H) {
             fail(E_CAPACITY);
@@ -858,6 +879,7 @@ struct Replica {
     }
     /* get (collections.ts:227-233) + fixdown (249-263) */
     MT_HD void heap_pop(int32_t* rid, int32_t* seq, int32_t* gen) {
+        MT_PROF_SCOPE(PH_HEAP);
         int32_t cnt = h.heapN;
         *rid = z.hrid[0];
         *seq = z.hseq[0];
@@ -1154,6 +1176,7 @@ struct Replica {
     }
     /* zamboniSegments (mergeTree.ts:1455-1511) */
     MT_HD void zamboni() {
+        MT_PROF_SCOPE(PH_ZAMBONI);
         if (!h.collaborating) return;
         for (int i = 0; i < 2; i++) {
             if (h.heapN < 1) break;
@@ -1273,6 +1296,7 @@ struct Replica {
         if (L > 0) {
             int32_t off = 0;
             if (!marker) {
+                MT_PROF_SCOPE(PH_TEXT);
                 off = arena_alloc(L);
                 if (off < 0) return;
             }
@@ -1301,6 +1325,7 @@ struct Replica {
             if (marker) {
                 cold(s).toff = (uint32_t)op.pos2;
             } else {
+                MT_PROF_SCOPE(PH_TEXT);
                 cold(s).toff = (uint32_t)off;
                 arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
             }
@@ -1327,6 +1352,7 @@ struct Replica {
     /* ---- range ops: markRangeRemoved (2640-2752) / annotateRange (2598-2638) ----------- */
     template <class F>
     MT_HD void map_range(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
+        MT_PROF_SCOPE(PH_MAP);
         int32_t run = 0;
         int32_t T = h.nleaf * MAXN;
         for (int32_t b = 0; b < T; b += 4 * W::N) {
@@ -1422,6 +1448,7 @@ struct Replica {
     /* ---- ack (mergeTree.ts:1926-1953, BaseSegment.ack 486-521) ------------------------ */
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
         if (h.gqN > 0) {
+            MT_PROF_SCOPE(PH_ACK);
             int32_t gid = d.gq[h.gqHead % d.caps.gcap];
             h.gqHead = (h.gqHead + 1) % d.caps.gcap;
             h.gqN--;
@@ -1467,6 +1494,7 @@ struct Replica {
 
     /* ---- Client.applyMsg (client.ts:797-819) / local edits ---------------------------- */
     MT_HD void apply(const mt_op_rec& op, const Pools& p) {
+        MT_PROF_SCOPE(PH_APPLY);
         if (h.err) return;
         int32_t kind = op.kind & MT_OP_KIND_MASK;
         const mt_kv* kv = 0;

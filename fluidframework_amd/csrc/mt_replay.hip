@@ -62,7 +62,7 @@ template <class HT, bool LDS>
 __global__ __launch_bounds__(WG) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
-                                              const int64_t* kv_off) {
+                                              const int64_t* kv_off, uint64_t* prof) {
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
     Pools p;
@@ -81,12 +81,20 @@ __global__ __launch_bounds__(WG) void k_replay(Store<HT> st, int64_t ndocs, cons
         Replica<WaveGPU, HT> r(v, WaveGPU());
         r.replay(p);
         r.commit();
+#ifdef MT_PROF
+        if (prof && threadIdx.x == 0)
+            for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
+#endif
         __syncthreads();
         copy_image(g, &hot);
     } else {
         Replica<WaveGPU, HT> r(v, WaveGPU());
         r.replay(p);
         r.commit();
+#ifdef MT_PROF
+        if (prof && threadIdx.x == 0)
+            for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
+#endif
     }
 }
 
@@ -178,7 +186,7 @@ struct mt_engine {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f;
     bool staged = false;
-    DevBuf ops, op_off, text, text_off, props, props_off, kv, kv_off, tmp, local_ids;
+    DevBuf ops, op_off, text, text_off, props, props_off, kv, kv_off, tmp, local_ids, prof;
     int32_t min_seq0 = 0, cur_seq0 = 0;
     bool collab = false;
     std::string err;
@@ -276,8 +284,8 @@ void mt_engine_destroy(mt_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    DevBuf* bufs[] = {&e->ops,       &e->op_off, &e->text,   &e->text_off, &e->props,
-                      &e->props_off, &e->kv,     &e->kv_off, &e->tmp,      &e->local_ids};
+    DevBuf* bufs[] = {&e->ops,    &e->op_off, &e->text, &e->text_off, &e->props,     &e->props_off,
+                      &e->kv,     &e->kv_off, &e->tmp,  &e->local_ids, &e->prof};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (e->mem) (void)hipFree(e->mem);
@@ -373,6 +381,9 @@ int32_t mt_engine_reset(mt_engine* e) {
 int32_t mt_engine_run(mt_engine* e) {
     if (!e || !e->staged) return MT_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
+#ifdef MT_PROF
+    if (ensure(e, e->prof, sizeof(uint64_t) * PH_N * e->ndocs)) return MT_E_NOMEM;
+#endif
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     int32_t rc = with_store(e, [&](auto& st) {
         using HT = typename std::decay_t<decltype(st)>::Hot;
@@ -380,12 +391,12 @@ int32_t mt_engine_run(mt_engine* e) {
             hipLaunchKernelGGL((k_replay<HT, true>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
                                (const mt_op_rec*)e->ops.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
                                (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p,
-                               (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p);
+                               (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p, (uint64_t*)e->prof.p);
         else
             hipLaunchKernelGGL((k_replay<HT, false>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
                                (const mt_op_rec*)e->ops.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
                                (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p,
-                               (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p);
+                               (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p, (uint64_t*)e->prof.p);
         return launch_check(e, "k_replay");
     });
     if (rc) return rc;
@@ -519,5 +530,14 @@ int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t l
     }
     return n;
 }
+
+#ifdef MT_PROF
+/* profiling build only: per-doc phase cycles of the last run (PH_* order in mt_core.h) */
+int32_t mt_engine_profile(mt_engine* e, uint64_t* out) {
+    if (!e || !out || !e->prof.p) return MT_E_ARG;
+    HIPCHK(e, hipMemcpy(out, e->prof.p, sizeof(uint64_t) * PH_N * e->ndocs, hipMemcpyDeviceToHost));
+    return MT_OK;
+}
+#endif
 
 } /* extern "C" */

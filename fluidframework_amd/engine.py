@@ -35,7 +35,7 @@ _LIB = None
 def lib() -> ctypes.CDLL:
     global _LIB
     if _LIB is None:
-        path = native.lib_path("libmtreplay.so")
+        path = os.environ.get("MT_REPLAY_LIB") or native.lib_path("libmtreplay.so")
         if not os.path.exists(path):
             raise EngineError(f"HIP replay library missing: {path} (run __graft_entry__.build())")
         L = ctypes.CDLL(path)

@@ -1,0 +1,51 @@
+"""Per-phase cycle breakdown of the replay kernel (profiling build, -DMT_PROF).
+
+Builds fluidframework_amd/build/libmtreplay_prof.so, replays a config-3 batch on cuda:0 and prints
+where each document's shader-clock cycles went (phases nest: HEAP inside ZAMBONI/MAP, SPLIT inside
+FIND callers, etc.). Usage: python tools/phase_profile.py [--build-only] [--docs N]
+"""
+import argparse, ctypes, os, subprocess, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from fluidframework_amd import native
+
+PHASES = ["APPLY", "ZAMBONI", "FIND", "MAP", "SPLIT", "ACK", "TEXT", "HEAP"]
+LIB = native.lib_path("libmtreplay_prof.so")
+
+
+def build():
+    src = os.path.join(native.CSRC, "mt_replay.hip")
+    subprocess.run([native.hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMT_PROF",
+                    "-o", LIB, src], check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--docs", type=int, default=2048)
+    ap.add_argument("--ops", type=int, default=4096)
+    a = ap.parse_args()
+    if a.build_only:
+        build()
+        return
+    import numpy as np
+    os.environ["MT_REPLAY_LIB"] = LIB
+    from fluidframework_amd import gen
+    from fluidframework_amd.engine import Engine, default_caps, lib
+    b = gen.generate(gen.config3(a.ops), a.docs)
+    eng = Engine(b.ndocs, **default_caps(a.ops))
+    eng.start_collab(b.local_long_id)
+    eng.replay(b)
+    L = lib()
+    L.mt_engine_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    out = np.zeros((b.ndocs, len(PHASES)), np.uint64)
+    assert L.mt_engine_profile(eng.h, out.ctypes.data) == 0
+    tot = out.sum(0).astype(np.float64)
+    ev = b.nops
+    print(f"docs {b.ndocs} events {ev} kernel {eng.last_run_ms:.1f} ms")
+    for i, n in enumerate(PHASES):
+        print(f"{n:8s} {tot[i] / ev:10.0f} cycles/event  {100 * tot[i] / tot[0]:5.1f}% of APPLY")
+
+
+if __name__ == "__main__":
+    main()
