@@ -177,7 +177,8 @@ struct Pools {
 
 /* Phase clock for the profiling build only (-DMT_PROF, tools/phase_profile.py): shader-clock
  * cycles accumulated per phase in registers and written out per document. */
-enum { PH_APPLY, PH_ZAMBONI, PH_FIND, PH_MAP, PH_SPLIT, PH_ACK, PH_TEXT, PH_HEAP, PH_N };
+enum { PH_APPLY, PH_ZAMBONI, PH_FIND, PH_MAP, PH_SPLIT, PH_ACK, PH_TEXT, PH_HEAP, PH_SCOUR, PH_PACK, PH_APPEND,
+       PH_CAND, PH_N };
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {
     uint64_t* acc;
@@ -201,7 +202,7 @@ struct Replica {
 
     DocHdr h; /* the document header, held in registers (SGPRs on the GPU) while the replica runs */
 #ifdef MT_PROF
-    uint64_t prof[PH_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t prof[PH_N] = {};
 #endif
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave) : d(doc), z(*doc.t), w(wave) { load_hdr(); }
@@ -965,7 +966,8 @@ struct Replica {
             if (cold(s).pk[k]) cold(s).pk[k]--;
         }
     }
-    MT_HD bool match_props(int32_t a, int32_t b) const { /* matchProperties (properties.ts:61-92) */
+    MT_HD bool match_props(int32_t a, int32_t b) { /* matchProperties (properties.ts:61-92) */
+        MT_PROF_SCOPE(PH_CAND);
         bool pa = z.flags[a] & RF_PROPS, pb = z.flags[b] & RF_PROPS;
         if (pa != pb) return false;
         if (!pa) return true;
@@ -977,14 +979,21 @@ struct Replica {
     /* ---- zamboni: scourNode / pack / zamboniSegments (mergeTree.ts:1322-1511) ---------- */
     /* canAppend (textSegment.ts:63-68) */
     MT_HD bool can_append(int32_t a, int32_t b) {
+        MT_PROF_SCOPE(PH_CAND);
         if (z.flags[a] & RF_MARKER) return false;
         int32_t L = z.len[a];
         if (L > 0 && arena_base(h.arenaSide)[cold(a).toff + L - 1] == '\n') return false;
         if (z.flags[b] & RF_MARKER) return false;
         return z.len[a] <= GRANULARITY || z.len[b] <= GRANULARITY;
     }
+    /* the text of the row in slot a (current length La) ends with "\n" (textSegment.ts:64) */
+    MT_HD bool ends_nl(int32_t a, int32_t La) {
+        MT_PROF_SCOPE(PH_CAND);
+        return La > 0 && arena_base(h.arenaSide)[cold(a).toff + La - 1] == '\n';
+    }
     /* TextSegment.append (textSegment.ts:74-85): the merged text is rebuilt at the arena top */
     MT_HD void append_text(int32_t a, int32_t b) {
+        MT_PROF_SCOPE(PH_APPEND);
         int32_t La = z.len[a], Lb = z.len[b];
         uint16_t* base = arena_base(h.arenaSide);
         if ((int32_t)cold(a).toff + La == h.arenaTop && h.arenaTop + Lb <= d.caps.acap) {
@@ -1005,6 +1014,7 @@ struct Replica {
     /* scourNode on leaf n: compacts the slab in place; returns the new child count. Rows are
      * merged into their predecessor or unlinked exactly as the reference decides. */
     MT_HD int32_t scour_leaf(int32_t n) {
+        MT_PROF_SCOPE(PH_SCOUR);
         int32_t c = z.nchild[n];
         int32_t wpos = 0;
         int32_t prev = -1; /* slot of prevSegment in the compacted slab */
@@ -1055,8 +1065,111 @@ struct Replica {
         if (wpos < c) clear_slots(n * MAXN + wpos, c - wpos);
         return wpos;
     }
+
+    /* scourNode (mergeTree.ts:1322-1398), wave-parallel form, over nl <= 8 leaves at once: lane q
+     * holds child q & 7 of leaf q >> 3. Every row's hot fields are loaded in one pass; the keep /
+     * unlink / append decisions are the reference's sequential walk, taken on scalar copies of those
+     * fields (v_readlane), with cold data (props values, the trailing character) read only for a
+     * candidate pair; the frees and the slab compaction are again one parallel pass. cnt[i] gets the
+     * new child count of leaf i. Same result as scour_leaf on each leaf in turn. */
+    MT_HD void scour_par(const int32_t* leaves, int32_t nl, int32_t* cnt) {
+        MT_PROF_SCOPE(PH_SCOUR);
+        int32_t q = w.lane();
+        int32_t li = q >> 3, j = q & (MAXN - 1);
+        int32_t n = -1;
+        for (int32_t i = 0; i < MAXN; i++)
+            if (i == li && i < nl) n = leaves[i];
+        int32_t c = n >= 0 ? z.nchild[n] : 0;
+        bool valid = j < c;
+        HotRow r = {};
+        if (valid) r = load_row(n * MAXN + j);
+        int32_t minSeq = h.minSeq;
+        /* 0: no row; 1: held, resets prevSegment; 2: unlinked, resets prevSegment; 3: merge candidate */
+        int32_t code = 0;
+        if (valid) {
+            if (r.ng)
+                code = 1;
+            else if (r.rseq != NOREM)
+                code = r.rseq > minSeq ? 1 : 2;
+            else
+                code = r.seq > minSeq ? 1 : 3;
+        }
+        int32_t nlen = r.len;
+        uint64_t vmask = w.ballot(valid);
+        uint64_t keep = 0;
+        int32_t prev = -1, prevLen = 0, prevFl = 0, curLeaf = -1;
+        uint64_t m = vmask;
+        while (m) {
+            int32_t k = W::ffs(m);
+            m &= m - 1;
+            if ((k >> 3) != curLeaf) { /* prevSegment is local to one scourNode call */
+                curLeaf = k >> 3;
+                prev = -1;
+            }
+            int32_t ck = w.bcast(code, k);
+            if (ck != 3) {
+                if (ck == 1) keep |= 1ull << k;
+                prev = -1;
+                continue;
+            }
+            int32_t lk = w.bcast(r.len, k);
+            int32_t fk = w.bcast(r.flags, k);
+            bool ok = false;
+            if (prev >= 0 && !(prevFl & RF_MARKER) && !(fk & RF_MARKER) &&
+                (prevLen <= GRANULARITY || lk <= GRANULARITY) && ((prevFl ^ fk) & RF_PROPS) == 0) {
+                int32_t sp = w.bcast(n, prev) * MAXN + (prev & (MAXN - 1));
+                int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
+                ok = match_props(sp, sk) && !ends_nl(sp, prevLen);
+                if (ok) {
+                    append_text(sp, sk); /* updates z.len[sp], read by a GC inside it */
+                    prevLen += lk;
+                    nlen = w.writelane(prevLen, prev, nlen);
+                }
+            }
+            if (!ok) {
+                keep |= 1ull << k;
+                prev = k; /* a non-removed row always has localNetLength > 0 */
+                prevLen = lk;
+                prevFl = fk;
+            }
+        }
+        /* frees: every valid row not kept (unlinked or appended) */
+        uint64_t drop = vmask & ~keep;
+        uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
+        if ((drop >> q) & 1) {
+            int32_t pos = h.nfreeRid + __builtin_popcountll(drop & below);
+            z.rgen[r.rid]++;
+            d.frid[pos] = (int16_t)r.rid;
+        }
+        int32_t ndrop = __builtin_popcountll(drop);
+        h.nfreeRid += ndrop;
+        h.nrows -= ndrop;
+        /* compaction: kept rows move down within their leaf; vacated slots get length 0 */
+        uint64_t lmask = n >= 0 ? (0xFFull << (8 * li)) : 0ull;
+        int32_t newc = __builtin_popcountll(keep & lmask);
+        w.sync();
+        if ((keep >> q) & 1) {
+            r.len = nlen;
+            store_row(n * MAXN + __builtin_popcountll(keep & lmask & below), r);
+        }
+        if (valid && j >= newc) z.len[n * MAXN + j] = 0; /* disjoint from every kept row's target */
+        if (n >= 0 && j == 0) z.nchild[n] = (int8_t)newc;
+        w.sync();
+        for (int32_t i = 0; i < nl; i++) cnt[i] = __builtin_popcountll(keep & (0xFFull << (8 * i)));
+    }
+    /* scourNode of one leaf: the parallel form on the GPU, the serial walk on the host */
+    MT_HD int32_t scour_one(int32_t n) {
+        if constexpr (W::N >= MAXN * MAXN) {
+            int32_t cnt[1];
+            scour_par(&n, 1, cnt);
+            return cnt[0];
+        } else {
+            return scour_leaf(n);
+        }
+    }
     /* pack (mergeTree.ts:1401-1453) of `block`'s parent */
     MT_HD void pack(int32_t block0) {
+        MT_PROF_SCOPE(PH_PACK);
       int32_t block = block0;
       for (;;) { /* iterative: pack recurses upward while the parent underflows (1447-1452) */
         int32_t parent = z.nparent[block];
@@ -1065,7 +1178,14 @@ struct Replica {
         if (lvl == 0) {
             /* scour every sibling leaf, then redistribute their rows over new leaves */
             int32_t total = 0;
-            for (int32_t i = 0; i < pc; i++) total += scour_leaf(z.kids[parent * MAXN + i]);
+            if constexpr (W::N >= MAXN * MAXN) {
+                int32_t sib[MAXN], cnt[MAXN];
+                for (int32_t i = 0; i < MAXN; i++) sib[i] = i < pc ? z.kids[parent * MAXN + i] : -1;
+                scour_par(sib, pc, cnt);
+                for (int32_t i = 0; i < pc; i++) total += cnt[i];
+            } else {
+                for (int32_t i = 0; i < pc; i++) total += scour_leaf(z.kids[parent * MAXN + i]);
+            }
             int32_t cc = total / (MAXN / 2);
             if (cc > MAXN - 1) cc = MAXN - 1;
             if (cc < 1) cc = 1;
@@ -1188,7 +1308,7 @@ struct Replica {
             int32_t n = s / MAXN;
             if (z.nscour[n] == 0) continue;
             int32_t before = z.nchild[n];
-            int32_t after = scour_leaf(n);
+            int32_t after = scour_one(n);
             z.nscour[n] = 0;
             if (after < before) {
                 if (after < MAXN / 2 && z.nparent[n] >= 0) pack(n);

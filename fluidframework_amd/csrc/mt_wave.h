@@ -19,6 +19,7 @@ struct WaveHost {
     uint64_t ballot(bool p) const { return p ? 1ull : 0ull; }
     int32_t bcast(int32_t v, int) const { return v; }
     static int32_t uniform(int32_t v) { return v; }
+    int32_t writelane(int32_t v, int, int32_t) const { return v; }
     static int ffs(uint64_t m) { return __builtin_ctzll(m); }
     void sync() const {}
 };
@@ -57,6 +58,10 @@ struct WaveGPU {
     /* a value every lane holds equally, moved to an SGPR */
     __device__ __attribute__((always_inline)) static int32_t uniform(int32_t v) {
         return __builtin_amdgcn_readfirstlane(v);
+    }
+    /* lane l (wave-uniform) of the result takes v; other lanes keep old */
+    __device__ __attribute__((always_inline)) int32_t writelane(int32_t v, int l, int32_t old) const {
+        return lane() == l ? v : old;
     }
     /* l is wave-uniform: v_readlane, no LDS round trip */
     __device__ __attribute__((always_inline)) int32_t bcast(int32_t v, int l) const {
