@@ -68,10 +68,15 @@ struct WaveGPU {
         return __builtin_amdgcn_readlane(v, l);
     }
     __device__ __attribute__((always_inline)) static int ffs(uint64_t m) { return __builtin_ctzll(m); }
+    /* Order the wave's memory accesses between lanes. One wavefront replays one document, so every
+     * hand-off is between lanes of the same wave: its LDS operations execute in program order and so
+     * do its vector-memory operations to one address, so only the compiler has to be kept from
+     * moving accesses across this point. (A workgroup-scope fence would also wait for every
+     * outstanding global store, s_waitcnt vmcnt(0), at each call.) */
     __device__ __attribute__((always_inline)) void sync() const {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }
 };
 #endif
