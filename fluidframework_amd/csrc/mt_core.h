@@ -63,6 +63,8 @@ enum : uint8_t {
     RF_LSEQ = 4,
     RF_LRSEQ = 8,
     RF_OVL = 16, /* removedClientOverlap is non-empty (its list lives in the cold row) */
+    RF_NLK = 32, /* RF_NL is known: a cache of the text's last unit, so zamboni rarely reads it */
+    RF_NL = 64,  /* the text ends with "\n" (textSegment.ts:64 canAppend) */
 };
 
 /* runtime capacities that are not part of the LDS image */
@@ -178,7 +180,7 @@ struct Pools {
 /* Phase clock for the profiling build only (-DMT_PROF, tools/phase_profile.py): shader-clock
  * cycles accumulated per phase in registers and written out per document. */
 enum { PH_APPLY, PH_ZAMBONI, PH_FIND, PH_MAP, PH_SPLIT, PH_ACK, PH_TEXT, PH_HEAP, PH_SCOUR, PH_PACK, PH_APPEND,
-       PH_CAND, PH_N };
+       PH_CAND, PH_S1, PH_S2, PH_S3, PH_N };
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {
     uint64_t* acc;
@@ -708,14 +710,18 @@ struct Replica {
         h.arenaTop = off + n;
         return off;
     }
-    MT_HD void arena_copy(uint16_t* dst, const uint16_t* src, int32_t n) {
+    /* copy n units (wave-parallel); returns the last unit copied (0 if n == 0) */
+    MT_HD int32_t arena_copy(uint16_t* dst, const uint16_t* src, int32_t n) {
+        int32_t last = 0;
         for (int32_t b = 0; b < n; b += W::N) {
             int32_t i = b + w.lane();
             uint16_t v = i < n ? src[i] : 0;
             w.sync();
             if (i < n) dst[i] = v;
+            if (b + W::N >= n) last = w.bcast(v, n - 1 - b);
         }
         w.sync();
+        return last;
     }
     /* copy all live text rows into the other half, in document order. A row id is moved once
      * per GC even if its slot is transiently duplicated (scour compacts a slab in place). */
@@ -762,6 +768,7 @@ struct Replica {
         z.len[rs] = z.len[ls] - off;
         cold(rs).toff = cold(ls).toff + (uint32_t)off;
         z.len[ls] = off;
+        z.flags[ls] &= (uint8_t)~RF_NLK; /* the left part's last unit is not known any more */
         h.nrows++;
         h.sumW += 2;
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
@@ -981,15 +988,18 @@ struct Replica {
     MT_HD bool can_append(int32_t a, int32_t b) {
         MT_PROF_SCOPE(PH_CAND);
         if (z.flags[a] & RF_MARKER) return false;
-        int32_t L = z.len[a];
-        if (L > 0 && arena_base(h.arenaSide)[cold(a).toff + L - 1] == '\n') return false;
+        if (ends_nl(a, z.len[a])) return false;
         if (z.flags[b] & RF_MARKER) return false;
         return z.len[a] <= GRANULARITY || z.len[b] <= GRANULARITY;
     }
     /* the text of the row in slot a (current length La) ends with "\n" (textSegment.ts:64) */
     MT_HD bool ends_nl(int32_t a, int32_t La) {
+        int32_t f = z.flags[a];
+        if (f & RF_NLK) return (f & RF_NL) != 0;
         MT_PROF_SCOPE(PH_CAND);
-        return La > 0 && arena_base(h.arenaSide)[cold(a).toff + La - 1] == '\n';
+        bool nl = La > 0 && arena_base(h.arenaSide)[cold(a).toff + La - 1] == '\n';
+        z.flags[a] = (uint8_t)(f | RF_NLK | (nl ? RF_NL : 0));
+        return nl;
     }
     /* TextSegment.append (textSegment.ts:74-85): the merged text is rebuilt at the arena top */
     MT_HD void append_text(int32_t a, int32_t b) {
@@ -1010,6 +1020,8 @@ struct Replica {
             cold(a).toff = (uint32_t)off;
         }
         z.len[a] = La + Lb;
+        /* the merged text ends where b's did */
+        z.flags[a] = (uint8_t)((z.flags[a] & ~(RF_NLK | RF_NL)) | (z.flags[b] & (RF_NLK | RF_NL)));
     }
     /* scourNode on leaf n: compacts the slab in place; returns the new child count. Rows are
      * merged into their predecessor or unlinked exactly as the reference decides. */
@@ -1074,6 +1086,9 @@ struct Replica {
      * new child count of leaf i. Same result as scour_leaf on each leaf in turn. */
     MT_HD void scour_par(const int32_t* leaves, int32_t nl, int32_t* cnt) {
         MT_PROF_SCOPE(PH_SCOUR);
+#if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
+        uint64_t _t0 = __builtin_amdgcn_s_memtime();
+#endif
         int32_t q = w.lane();
         int32_t li = q >> 3, j = q & (MAXN - 1);
         int32_t n = -1;
@@ -1096,35 +1111,47 @@ struct Replica {
         }
         int32_t nlen = r.len;
         uint64_t vmask = w.ballot(valid);
-        uint64_t keep = 0;
-        int32_t prev = -1, prevLen = 0, prevFl = 0, curLeaf = -1;
-        uint64_t m = vmask;
+#if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
+        uint64_t _t1 = __builtin_amdgcn_s_memtime();
+        prof[PH_S1] += _t1 - _t0;
+#endif
+        /* Only a candidate whose predecessor in the same leaf is a candidate can be appended; every
+         * other row is decided by its own code: held rows (1) are kept, unlinked rows (2) are
+         * dropped, and a candidate after a non-candidate starts a run as prevSegment (kept). */
+        uint64_t cand = w.ballot(code == 3);
+        uint64_t pairs = cand & (cand << 1) & ~0x0101010101010101ull;
+        uint64_t keep = w.ballot(code == 1) | (cand & ~pairs);
+        int32_t fl = r.flags;
+        int32_t prev = -1, prevLen = 0, prevFl = 0;
+        uint64_t m = pairs;
         while (m) {
             int32_t k = W::ffs(m);
             m &= m - 1;
-            if ((k >> 3) != curLeaf) { /* prevSegment is local to one scourNode call */
-                curLeaf = k >> 3;
-                prev = -1;
-            }
-            int32_t ck = w.bcast(code, k);
-            if (ck != 3) {
-                if (ck == 1) keep |= 1ull << k;
-                prev = -1;
-                continue;
+            if (!((pairs >> (k - 1)) & 1)) { /* k - 1 opened this run */
+                prev = k - 1;
+                prevLen = w.bcast(r.len, prev);
+                prevFl = w.bcast(fl, prev);
             }
             int32_t lk = w.bcast(r.len, k);
-            int32_t fk = w.bcast(r.flags, k);
+            int32_t fk = w.bcast(fl, k);
             bool ok = false;
-            if (prev >= 0 && !(prevFl & RF_MARKER) && !(fk & RF_MARKER) &&
-                (prevLen <= GRANULARITY || lk <= GRANULARITY) && ((prevFl ^ fk) & RF_PROPS) == 0) {
+            if (!(prevFl & RF_MARKER) && !(fk & RF_MARKER) && (prevLen <= GRANULARITY || lk <= GRANULARITY) &&
+                ((prevFl ^ fk) & RF_PROPS) == 0) {
                 int32_t sp = w.bcast(n, prev) * MAXN + (prev & (MAXN - 1));
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
-                ok = match_props(sp, sk) && !ends_nl(sp, prevLen);
+                ok = match_props(sp, sk);
                 if (ok) {
-                    append_text(sp, sk); /* updates z.len[sp], read by a GC inside it */
+                    bool nl = ends_nl(sp, prevLen); /* caches RF_NLK/RF_NL in z.flags[sp] */
+                    prevFl = (prevFl & ~(RF_NLK | RF_NL)) | RF_NLK | (nl ? RF_NL : 0);
+                    ok = !nl;
+                }
+                if (ok) {
+                    append_text(sp, sk); /* updates z.len[sp] (read by a GC inside it) and its NL bits */
                     prevLen += lk;
+                    prevFl = (prevFl & ~(RF_NLK | RF_NL)) | (fk & (RF_NLK | RF_NL));
                     nlen = w.writelane(prevLen, prev, nlen);
                 }
+                fl = w.writelane(prevFl, prev, fl);
             }
             if (!ok) {
                 keep |= 1ull << k;
@@ -1133,6 +1160,10 @@ struct Replica {
                 prevFl = fk;
             }
         }
+#if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
+        uint64_t _t2 = __builtin_amdgcn_s_memtime();
+        prof[PH_S2] += _t2 - _t1;
+#endif
         /* frees: every valid row not kept (unlinked or appended) */
         uint64_t drop = vmask & ~keep;
         uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
@@ -1150,12 +1181,16 @@ struct Replica {
         w.sync();
         if ((keep >> q) & 1) {
             r.len = nlen;
+            r.flags = (uint8_t)fl;
             store_row(n * MAXN + __builtin_popcountll(keep & lmask & below), r);
         }
         if (valid && j >= newc) z.len[n * MAXN + j] = 0; /* disjoint from every kept row's target */
         if (n >= 0 && j == 0) z.nchild[n] = (int8_t)newc;
         w.sync();
         for (int32_t i = 0; i < nl; i++) cnt[i] = __builtin_popcountll(keep & (0xFFull << (8 * i)));
+#if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
+        prof[PH_S3] += __builtin_amdgcn_s_memtime() - _t2;
+#endif
     }
     /* scourNode of one leaf: the parallel form on the GPU, the serial walk on the host */
     MT_HD int32_t scour_one(int32_t n) {
@@ -1434,7 +1469,7 @@ struct Replica {
             cold(s).lrseq = 0;
             z.cli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
             z.rcli[s] = 0;
-            z.flags[s] = (uint8_t)((marker ? RF_MARKER : 0) | (hasL ? RF_LSEQ : 0));
+            int32_t fl = (marker ? RF_MARKER : 0) | (hasL ? RF_LSEQ : 0);
             z.ng[s] = 0;
             cold(s).prw = 0;
             cold(s).ovl = 0;
@@ -1447,8 +1482,10 @@ struct Replica {
             } else {
                 MT_PROF_SCOPE(PH_TEXT);
                 cold(s).toff = (uint32_t)off;
-                arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
+                int32_t last = arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
+                fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
             }
+            z.flags[s] = (uint8_t)fl;
             for (int k = 0; k < NKEYS; k++) {
                 cold(s).pv[k] = 0;
                 cold(s).pk[k] = 0;
