@@ -180,7 +180,7 @@ struct Pools {
 /* Phase clock for the profiling build only (-DMT_PROF, tools/phase_profile.py): shader-clock
  * cycles accumulated per phase in registers and written out per document. */
 enum { PH_APPLY, PH_ZAMBONI, PH_FIND, PH_MAP, PH_SPLIT, PH_ACK, PH_TEXT, PH_HEAP, PH_SCOUR, PH_PACK, PH_APPEND,
-       PH_CAND, PH_S1, PH_S2, PH_S3, PH_N };
+       PH_CAND, PH_S1, PH_S2, PH_S3, PH_P1, PH_P2, PH_N };
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {
     uint64_t* acc;
@@ -1221,6 +1221,7 @@ struct Replica {
             } else {
                 for (int32_t i = 0; i < pc; i++) total += scour_leaf(z.kids[parent * MAXN + i]);
             }
+            MT_PROF_SCOPE(PH_P1);
             int32_t cc = total / (MAXN / 2);
             if (cc > MAXN - 1) cc = MAXN - 1;
             if (cc < 1) cc = 1;
@@ -1294,36 +1295,82 @@ struct Replica {
             for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (int16_t)newk[i];
             z.nchild[parent] = (int8_t)cc;
         } else {
-            /* interior: collect grandchildren in order, regroup into new interior nodes */
-            int16_t hold[MAXN * MAXN];
-            int32_t total = 0;
-            int32_t oldk[MAXN];
-            for (int32_t i = 0; i < pc; i++) {
-                int32_t cb = z.kids[parent * MAXN + i];
-                oldk[i] = cb;
-                for (int32_t q = 0; q < z.nchild[cb]; q++) hold[total++] = z.kids[cb * MAXN + q];
-            }
-            int32_t cc = total / (MAXN / 2);
-            if (cc > MAXN - 1) cc = MAXN - 1;
-            if (cc < 1) cc = 1;
-            int32_t base = total / cc, extra = total % cc;
-            for (int32_t i = 0; i < pc; i++) free_node(oldk[i]);
-            int32_t read = 0;
-            for (int32_t ni = 0; ni < cc; ni++) {
-                int32_t cnt = base + (extra > 0 ? 1 : 0);
-                if (extra > 0) extra--;
-                int32_t nb = alloc_node(lvl);
-                if (nb < 0) return;
-                for (int32_t q = 0; q < cnt; q++) {
-                    int32_t ch = hold[read++];
-                    z.kids[nb * MAXN + q] = (int16_t)ch;
+            MT_PROF_SCOPE(PH_P2);
+            if constexpr (W::N >= MAXN * MAXN) {
+                /* interior, wave-parallel: lane q reads grandchild q & 7 of child q >> 3 in one pass,
+                 * its rank among all grandchildren places it in the regrouped nodes */
+                int32_t q = w.lane();
+                int32_t i = q >> 3, j = q & (MAXN - 1);
+                int32_t cb = i < pc ? z.kids[parent * MAXN + i] : -1;
+                int32_t cn = cb >= 0 ? z.nchild[cb] : 0;
+                bool has = j < cn;
+                int32_t ch = has ? z.kids[cb * MAXN + j] : -1;
+                uint64_t vm = w.ballot(has);
+                int32_t total = __builtin_popcountll(vm);
+                uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
+                int32_t rank = __builtin_popcountll(vm & below);
+                int32_t cc = total / (MAXN / 2);
+                if (cc > MAXN - 1) cc = MAXN - 1;
+                if (cc < 1) cc = 1;
+                int32_t base = total / cc, extra = total % cc;
+                int32_t oldk[MAXN];
+                for (int32_t k = 0; k < pc; k++) oldk[k] = w.bcast(cb, k * MAXN);
+                for (int32_t k = 0; k < pc; k++) free_node(oldk[k]);
+                int32_t nbk[MAXN];
+                for (int32_t ni = 0; ni < cc; ni++) {
+                    nbk[ni] = alloc_node(lvl);
+                    if (nbk[ni] < 0) return;
+                }
+                /* the first `extra` nodes take base + 1 children */
+                int32_t big = extra * (base + 1);
+                int32_t ni = rank < big ? rank / (base + 1) : extra + (rank - big) / base;
+                int32_t slot = rank < big ? rank - ni * (base + 1) : rank - big - (ni - extra) * base;
+                int32_t nb = -1;
+                for (int32_t k = 0; k < MAXN; k++)
+                    if (k == ni && k < cc) nb = nbk[k];
+                w.sync();
+                if (has) {
+                    z.kids[nb * MAXN + slot] = (int16_t)ch;
                     z.nparent[ch] = (int16_t)nb;
                 }
-                z.nchild[nb] = (int8_t)cnt;
-                z.nparent[nb] = (int16_t)parent;
-                z.kids[parent * MAXN + ni] = (int16_t)nb;
+                w.sync();
+                for (int32_t k = 0; k < cc; k++) {
+                    z.nchild[nbk[k]] = (int8_t)(base + (k < extra ? 1 : 0));
+                    z.nparent[nbk[k]] = (int16_t)parent;
+                    z.kids[parent * MAXN + k] = (int16_t)nbk[k];
+                }
+                z.nchild[parent] = (int8_t)cc;
+            } else {
+                int16_t hold[MAXN * MAXN];
+                int32_t total = 0;
+                int32_t oldk[MAXN];
+                for (int32_t i = 0; i < pc; i++) {
+                    int32_t cb = z.kids[parent * MAXN + i];
+                    oldk[i] = cb;
+                    for (int32_t q = 0; q < z.nchild[cb]; q++) hold[total++] = z.kids[cb * MAXN + q];
+                }
+                int32_t cc = total / (MAXN / 2);
+                if (cc > MAXN - 1) cc = MAXN - 1;
+                if (cc < 1) cc = 1;
+                int32_t base = total / cc, extra = total % cc;
+                for (int32_t i = 0; i < pc; i++) free_node(oldk[i]);
+                int32_t read = 0;
+                for (int32_t ni = 0; ni < cc; ni++) {
+                    int32_t cnt = base + (extra > 0 ? 1 : 0);
+                    if (extra > 0) extra--;
+                    int32_t nb = alloc_node(lvl);
+                    if (nb < 0) return;
+                    for (int32_t q = 0; q < cnt; q++) {
+                        int32_t ch = hold[read++];
+                        z.kids[nb * MAXN + q] = (int16_t)ch;
+                        z.nparent[ch] = (int16_t)nb;
+                    }
+                    z.nchild[nb] = (int8_t)cnt;
+                    z.nparent[nb] = (int16_t)parent;
+                    z.kids[parent * MAXN + ni] = (int16_t)nb;
+                }
+                z.nchild[parent] = (int8_t)cc;
             }
-            z.nchild[parent] = (int8_t)cc;
         }
         if (!(z.nchild[parent] < MAXN / 2 && z.nparent[parent] >= 0)) return;
         block = parent;
