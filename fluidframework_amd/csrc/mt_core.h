@@ -180,7 +180,7 @@ struct Pools {
 /* Phase clock for the profiling build only (-DMT_PROF, tools/phase_profile.py): shader-clock
  * cycles accumulated per phase in registers and written out per document. */
 enum { PH_APPLY, PH_ZAMBONI, PH_FIND, PH_MAP, PH_SPLIT, PH_ACK, PH_TEXT, PH_HEAP, PH_SCOUR, PH_PACK, PH_APPEND,
-       PH_CAND, PH_S1, PH_S2, PH_S3, PH_P1, PH_P2, PH_N };
+       PH_CAND, PH_S1, PH_S2, PH_S3, PH_P1, PH_P2, PH_INSROW, PH_LEAFINS, PH_N };
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {
     uint64_t* acc;
@@ -683,6 +683,7 @@ struct Replica {
     }
     /* Make room at child index j of leaf n; returns slot for the new row (after any split). */
     MT_HD int32_t leaf_insert_slot(int32_t n, int32_t j) {
+        MT_PROF_SCOPE(PH_LEAFINS);
         int32_t c = z.nchild[n];
         slab_shift_right(n, j, c);
         z.rid[n * MAXN + j] = -1; /* not a row yet: the caller assigns one */
@@ -1451,6 +1452,7 @@ struct Replica {
      * 2174-2257) from ONE perspective scan: the row reaching pos (P < pos <= P + vis) is split
      * at pos if pos falls strictly inside it; placement then resumes right after its left part. */
     MT_HD int32_t insert_row(int32_t pos, int32_t refSeq, int32_t client, int32_t seq) {
+        MT_PROF_SCOPE(PH_INSROW);
         int32_t k, j;
         if (pos == 0) {
             k = 0;
@@ -1882,10 +1884,24 @@ struct Replica {
         return h;
     }
 
+    /* Apply a whole event stream. The records are fetched W::N at a time, one per lane (8 dwords
+     * each), and handed to apply() through lane broadcasts, so the stream costs one global-memory
+     * round trip per W::N events instead of one per event. */
     MT_HD void replay(const Pools& p) {
-        for (int64_t i = 0; i < p.nops; i++) {
-            apply(p.ops[i], p);
-            if (h.err) break;
+        static_assert(sizeof(mt_op_rec) == 32, "op record is 8 dwords");
+        for (int64_t b = 0; b < p.nops; b += W::N) {
+            int64_t i = b + w.lane();
+            int32_t rec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (i < p.nops) __builtin_memcpy(rec, &p.ops[i], sizeof(rec));
+            int64_t cnt = p.nops - b < W::N ? p.nops - b : W::N;
+            for (int64_t k = 0; k < cnt; k++) {
+                int32_t u[8];
+                for (int q = 0; q < 8; q++) u[q] = w.bcast(rec[q], (int)k);
+                mt_op_rec op;
+                __builtin_memcpy(&op, u, sizeof(op));
+                apply(op, p);
+                if (h.err) return;
+            }
         }
     }
 };

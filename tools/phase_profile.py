@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from fluidframework_amd import native
 
-PHASES = ["APPLY", "ZAMBONI", "FIND", "MAP", "SPLIT", "ACK", "TEXT", "HEAP", "SCOUR", "PACK", "APPEND", "CAND", "S1load", "S2walk", "S3compact", "P1leaf", "P2interior"]
+PHASES = ["APPLY", "ZAMBONI", "FIND", "MAP", "SPLIT", "ACK", "TEXT", "HEAP", "SCOUR", "PACK", "APPEND", "CAND", "S1load", "S2walk", "S3compact", "P1leaf", "P2interior", "INSROW", "LEAFINS"]
 LIB = native.lib_path("libmtreplay_prof.so")
 
 
