@@ -36,7 +36,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--docs", type=int, default=65536, help="documents per rank")
     ap.add_argument("--ops-per-doc", type=int, default=4096, help="sequenced messages per document")
-    ap.add_argument("--cpu-sample-docs", type=int, default=2048)
+    ap.add_argument("--cpu-sample-docs", type=int, default=8192)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -171,7 +171,30 @@ class Batch:
         )
 
     def subset(self, docs: Sequence[int]) -> "Batch":
-        return Batch.from_arrays([self.doc(d) for d in docs], [int(self.local_long_id[d]) for d in docs])
+        """A batch of the given documents. A pool that is one segment per document (offsets
+        increasing to the pool's end) is sliced per document; a pool all documents share (equal
+        offsets) stays shared."""
+        docs = [int(d) for d in docs]
+
+        def pool(arr, off):
+            if len(off) and np.all(off == off[0]):
+                return np.ascontiguousarray(arr[off[0]:]), np.zeros(len(docs) + 1, np.int64)
+            if np.all(np.diff(off) >= 0):
+                parts = [arr[off[d]: off[d + 1]] for d in docs]
+                o = np.zeros(len(docs) + 1, np.int64)
+                o[1:] = np.cumsum([len(x) for x in parts])
+                cat = np.concatenate(parts) if parts else arr[:0]
+                return (np.ascontiguousarray(cat) if len(cat) else arr[:1].copy()), o
+            raise ValueError("pool offsets are neither per-document segments nor shared")
+
+        ops = np.concatenate([self.ops[self.op_off[d]: self.op_off[d + 1]] for d in docs]) if docs else self.ops[:0]
+        op_off = np.zeros(len(docs) + 1, np.int64)
+        op_off[1:] = np.cumsum([self.op_off[d + 1] - self.op_off[d] for d in docs])
+        text, text_off = pool(self.text, self.text_off)
+        props, props_off = pool(self.props, self.props_off)
+        kv, kv_off = pool(self.kv, self.kv_off)
+        return Batch(np.ascontiguousarray(ops), op_off, text, text_off, props, props_off, kv, kv_off,
+                     np.asarray([self.local_long_id[d] for d in docs], np.int32))
 
     @staticmethod
     def from_arrays(per_doc, local_ids) -> "Batch":
