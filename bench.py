@@ -44,7 +44,7 @@ def main() -> None:
     import numpy as np
     import torch
 
-    from fluidframework_amd import gen
+    from fluidframework_amd import gen, shard
     from fluidframework_amd.engine import Engine, default_caps
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -61,7 +61,8 @@ def main() -> None:
     # ---- synthetic workload (config 3), this rank's shard of documents ----
     w = gen.config3(args.ops_per_doc)
     t0 = time.time()
-    batch = gen.generate(w, args.docs, doc_base=rank * args.docs, threads=args.cpu_threads)
+    doc_base, ndocs = shard.doc_range(rank, args.docs)
+    batch = gen.generate(w, ndocs, doc_base=doc_base, threads=args.cpu_threads)
     log(f"rank {rank}: generated {args.docs} docs, {batch.nops} events in {time.time() - t0:.1f}s")
     local_events = int(((batch.ops["kind"] & 0x80) != 0).sum())
 
@@ -102,16 +103,11 @@ def main() -> None:
     digests = eng.digests()
 
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        n = torch.tensor([seq_ops], dtype=torch.int64, device=f"cuda:{device}")
-        dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        total_seq_ops = int(n.item())
+        dev = f"cuda:{device}"
+        elapsed = shard.max_over_ranks(elapsed, dist, dev)
+        total_seq_ops = shard.sum_over_ranks(seq_ops, dist, dev)
         # the one collective of the design: all-gather per-document digests (verification)
-        dg = torch.from_numpy(digests.view(np.int64)).to(f"cuda:{device}")
-        gathered = [torch.empty_like(dg) for _ in range(world)]
-        dist.all_gather(gathered, dg)
+        shard.gather_digests(digests, dist, dev)
     else:
         total_seq_ops = seq_ops
 
