@@ -751,7 +751,7 @@ struct Replica {
     /* ---- splitAt (mergeTree.ts:523-567, textSegment.ts:103-111) ------------------------ */
     /* Split the row at lorder coordinate t at offset off (0 < off < len). Returns the slot of
      * the LEFT part afterwards (the right part is the next row in document order). */
-    MT_HD int32_t split_row(int32_t t, int32_t off) {
+    MT_HD int32_t split_row(int32_t t, int32_t off, int32_t* rsOut = nullptr) {
         MT_PROF_SCOPE(PH_SPLIT);
         int32_t n = z.lorder[t >> 3], j = t & 7;
         int32_t s0 = n * MAXN + j;
@@ -792,6 +792,7 @@ struct Replica {
                 }
             }
         }
+        if (rsOut) *rsOut = rs;
         return ls;
     }
 
@@ -1588,13 +1589,113 @@ struct Replica {
             if (run >= end) break;
         }
     }
+
+    /* Boundaries and visit of a range op in ONE perspective scan. The reference splits at start
+     * (ensureIntervalBoundary, mergeTree.ts:2274-2278), then at end, then visits the rows with
+     * length > 0 in [start, end) (nodeMap, 2936-2998). The rows it visits are exactly the rows with
+     * vis > 0 overlapping [start, end) before the splits — a contiguous run in document order — with
+     * the first replaced by its right part if start falls inside it and the last cut at end. So one
+     * scan finds the first and the last overlapping row, the two splits are made in the reference's
+     * order, and the visit walks document order from the first row to the last. */
+    template <class F>
+    MT_HD void range_op(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
+        MT_PROF_SCOPE(PH_MAP);
+        int32_t run = 0;
+        int32_t T = h.nleaf * MAXN;
+        int32_t tf = -1, Pf = 0, vf = 0, tg = -1, Pg = 0, vg = 0;
+        {
+            MT_PROF_SCOPE(PH_FIND);
+            for (int32_t b = 0; b < T; b += 4 * W::N) {
+                int32_t v[4];
+                quad_vis(quad_slot(b + 4 * w.lane()), refSeq, client, v);
+                int32_t tot;
+                int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
+                int32_t hf = -1, pf = 0, lf = 0, hl = -1, pl = 0, ll = 0;
+                for (int q = 0; q < 4; q++) {
+                    if (v[q] > 0 && p < end && p + v[q] > start) {
+                        if (hf < 0) {
+                            hf = q;
+                            pf = p;
+                            lf = v[q];
+                        }
+                        hl = q;
+                        pl = p;
+                        ll = v[q];
+                    }
+                    p += v[q];
+                }
+                uint64_t m = w.ballot(hf >= 0);
+                if (m) {
+                    if (tf < 0) {
+                        int32_t l = W::ffs(m);
+                        tf = b + 4 * l + w.bcast(hf, l);
+                        Pf = w.bcast(pf, l);
+                        vf = w.bcast(lf, l);
+                    }
+                    int32_t l2 = 63 - __builtin_clzll(m);
+                    tg = b + 4 * l2 + w.bcast(hl, l2);
+                    Pg = w.bcast(pl, l2);
+                    vg = w.bcast(ll, l2);
+                }
+                run += tot;
+                if (run >= end) break;
+            }
+        }
+        if (tf < 0) return;
+        int32_t ridLast = z.rid[slot_at(tg)];
+        int32_t ridFirst = z.rid[slot_at(tf)];
+        if (Pf < start) { /* start falls inside the first row: split it; its right part is first */
+            int32_t rs = -1;
+            if (split_row(tf, start - Pf, &rs) < 0 || rs < 0) return;
+            if (tf == tg) {
+                ridLast = z.rid[rs];
+                vg = Pf + vf - start;
+                Pg = start;
+            }
+            ridFirst = z.rid[rs];
+        }
+        if (Pg + vg > end) { /* end falls inside the last row: split it; its left part keeps the id */
+            int32_t sg = slot_of(ridLast, -1);
+            if (sg < 0) {
+                fail(E_ASSERT);
+                return;
+            }
+            if (split_row(z.lpos[sg / MAXN] * MAXN + (sg & (MAXN - 1)), end - Pg) < 0) return;
+        }
+        int32_t sa = slot_of(ridFirst, -1), sb = slot_of(ridLast, -1);
+        if (sa < 0 || sb < 0) {
+            fail(E_ASSERT);
+            return;
+        }
+        int32_t ta = z.lpos[sa / MAXN] * MAXN + (sa & (MAXN - 1));
+        int32_t tb = z.lpos[sb / MAXN] * MAXN + (sb & (MAXN - 1));
+        for (int32_t b = ta & ~3; b <= tb; b += 4 * W::N) {
+            int32_t t0 = b + 4 * w.lane();
+            int32_t s0 = quad_slot(t0);
+            int32_t v[4];
+            quad_vis(s0, refSeq, client, v);
+            int32_t hm = 0;
+            for (int q = 0; q < 4; q++)
+                if (v[q] > 0 && t0 + q >= ta && t0 + q <= tb) hm |= 1 << q;
+            uint64_t m = w.ballot(hm != 0);
+            while (m) {
+                int32_t l = W::ffs(m);
+                m &= m - 1;
+                int32_t bits = w.bcast(hm, l);
+                int32_t sbase = w.bcast(s0, l);
+                while (bits) {
+                    int32_t q = __builtin_ctz((unsigned)bits);
+                    bits &= bits - 1;
+                    leaf(sbase + q);
+                }
+            }
+        }
+    }
     MT_HD void mark_range_removed(int32_t start, int32_t end, int32_t refSeq, int32_t client, int32_t seq) {
-        ensure_boundary(start, refSeq, client);
-        ensure_boundary(end, refSeq, client);
         bool hasL = seq == UNASSIGNED_SEQ;
         int32_t localSeq = hasL ? ++h.localSeq : 0;
         bool created = false;
-        map_range(start, end, refSeq, client, [&](int32_t s) {
+        range_op(start, end, refSeq, client, [&](int32_t s) {
             h.sumW++;
             if (z.rseq[s] != NOREM) {
                 if (z.rseq[s] == UNASSIGNED_SEQ) {
@@ -1633,12 +1734,10 @@ struct Replica {
     }
     MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t refSeq,
                               int32_t client, int32_t seq) {
-        ensure_boundary(start, refSeq, client);
-        ensure_boundary(end, refSeq, client);
         int32_t localSeq = seq == UNASSIGNED_SEQ ? ++h.localSeq : 0;
         bool created = false;
         bool collab = h.collaborating;
-        map_range(start, end, refSeq, client, [&](int32_t s) {
+        range_op(start, end, refSeq, client, [&](int32_t s) {
             h.sumW++;
             add_props(s, kv, nkv, rewrite, seq, collab);
             if (collab) {
