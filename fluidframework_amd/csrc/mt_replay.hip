@@ -178,6 +178,7 @@ struct mt_engine {
     int device;
     int64_t ndocs;
     int profile = 0;
+    bool lds = true; /* small profile: stage the hot image in LDS (MT_REPLAY_GLOBAL=1 runs it in HBM) */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
@@ -254,6 +255,8 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     mt_engine* e = new mt_engine();
     e->device = device;
     e->ndocs = ndocs;
+    const char* g = getenv("MT_REPLAY_GLOBAL");
+    e->lds = !(g && g[0] == '1');
     e->profile = prof;
     if (hipSetDevice(device) != hipSuccess) {
         delete e;
@@ -387,7 +390,7 @@ int32_t mt_engine_run(mt_engine* e) {
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     int32_t rc = with_store(e, [&](auto& st) {
         using HT = typename std::decay_t<decltype(st)>::Hot;
-        if constexpr (std::is_same_v<HT, HotSmall>)
+        if (std::is_same_v<HT, HotSmall> && e->lds)
             hipLaunchKernelGGL((k_replay<HT, true>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
                                (const mt_op_rec*)e->ops.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
                                (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p,
