@@ -390,16 +390,21 @@ int32_t mt_engine_run(mt_engine* e) {
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     int32_t rc = with_store(e, [&](auto& st) {
         using HT = typename std::decay_t<decltype(st)>::Hot;
-        if (std::is_same_v<HT, HotSmall> && e->lds)
-            hipLaunchKernelGGL((k_replay<HT, true>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
+        auto launch = [&](auto kern) {
+            hipLaunchKernelGGL(kern, docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
                                (const mt_op_rec*)e->ops.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
                                (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p,
-                               (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p, (uint64_t*)e->prof.p);
-        else
-            hipLaunchKernelGGL((k_replay<HT, false>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
-                               (const mt_op_rec*)e->ops.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
-                               (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p,
-                               (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p, (uint64_t*)e->prof.p);
+                               (const int64_t*)e->props_off.p, (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p,
+                               (uint64_t*)e->prof.p);
+        };
+        if constexpr (std::is_same_v<HT, HotSmall>) {
+            if (e->lds)
+                launch(k_replay<HT, true>);
+            else
+                launch(k_replay<HT, false>);
+        } else {
+            launch(k_replay<HT, false>);
+        }
         return launch_check(e, "k_replay");
     });
     if (rc) return rc;
