@@ -58,8 +58,8 @@ __device__ inline void copy_image(HT* dst, const HT* src) {
 
 /* K1-K4 fused: the whole event stream of a document, one wave per document. For the small
  * profile the hot image is staged into LDS for the whole replay. */
-template <class HT, bool LDS>
-__global__ __launch_bounds__(WG) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
+template <class HT, bool LDS, int MINW = 1>
+__global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
                                               const int64_t* kv_off, uint64_t* prof) {
@@ -179,6 +179,7 @@ struct mt_engine {
     int64_t ndocs;
     int profile = 0;
     bool lds = true; /* small profile: stage the hot image in LDS (MT_REPLAY_GLOBAL=1 runs it in HBM) */
+    int minw = 1;    /* MT_REPLAY_WAVES: minimum waves per SIMD the HBM-resident kernel is built for */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
@@ -257,6 +258,8 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->ndocs = ndocs;
     const char* g = getenv("MT_REPLAY_GLOBAL");
     e->lds = !(g && g[0] == '1');
+    const char* mw = getenv("MT_REPLAY_WAVES");
+    e->minw = mw ? atoi(mw) : 1;
     e->profile = prof;
     if (hipSetDevice(device) != hipSuccess) {
         delete e;
@@ -400,6 +403,14 @@ int32_t mt_engine_run(mt_engine* e) {
         if constexpr (std::is_same_v<HT, HotSmall>) {
             if (e->lds)
                 launch(k_replay<HT, true>);
+            else if (e->minw == 2)
+                launch(k_replay<HT, false, 2>);
+            else if (e->minw == 4)
+                launch(k_replay<HT, false, 4>);
+            else if (e->minw == 6)
+                launch(k_replay<HT, false, 6>);
+            else if (e->minw == 8)
+                launch(k_replay<HT, false, 8>);
             else
                 launch(k_replay<HT, false>);
         } else {
