@@ -178,8 +178,7 @@ struct mt_engine {
     int device;
     int64_t ndocs;
     int profile = 0;
-    bool lds = true; /* small profile: stage the hot image in LDS (MT_REPLAY_GLOBAL=1 runs it in HBM) */
-    int minw = 1;    /* MT_REPLAY_WAVES: minimum waves per SIMD the HBM-resident kernel is built for */
+    bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
@@ -256,10 +255,8 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     mt_engine* e = new mt_engine();
     e->device = device;
     e->ndocs = ndocs;
-    const char* g = getenv("MT_REPLAY_GLOBAL");
-    e->lds = !(g && g[0] == '1');
-    const char* mw = getenv("MT_REPLAY_WAVES");
-    e->minw = mw ? atoi(mw) : 1;
+    const char* g = getenv("MT_REPLAY_LDS");
+    e->lds = g && g[0] == '1';
     e->profile = prof;
     if (hipSetDevice(device) != hipSuccess) {
         delete e;
@@ -401,18 +398,14 @@ int32_t mt_engine_run(mt_engine* e) {
                                (uint64_t*)e->prof.p);
         };
         if constexpr (std::is_same_v<HT, HotSmall>) {
+            /* Default: the hot image stays in HBM and the kernel is built for 8 waves per SIMD, so
+             * 8,192 documents are in flight (32 per CU): at one wavefront per document the replay is
+             * bound by the latency of its dependent accesses, and occupancy hides more of it than
+             * LDS residency (4 documents per CU) saves. MT_REPLAY_LDS=1 selects the LDS-staged form. */
             if (e->lds)
                 launch(k_replay<HT, true>);
-            else if (e->minw == 2)
-                launch(k_replay<HT, false, 2>);
-            else if (e->minw == 4)
-                launch(k_replay<HT, false, 4>);
-            else if (e->minw == 6)
-                launch(k_replay<HT, false, 6>);
-            else if (e->minw == 8)
-                launch(k_replay<HT, false, 8>);
             else
-                launch(k_replay<HT, false>);
+                launch(k_replay<HT, false, 8>);
         } else {
             launch(k_replay<HT, false>);
         }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Replay throughput of the small profile: LDS-staged vs HBM-resident at several occupancy targets.
+# Replay throughput of the small profile: HBM-resident at 8 waves/SIMD (default) vs LDS-staged.
 export TMPDIR=/tmp
 D=${DOCS:-16384}
 run() {  # name env...
@@ -7,7 +7,5 @@ run() {  # name env...
   env "$@" timeout -k 10 400 python -u bench.py --docs $D --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/occ_$name.json 2> gpurun_out/occ_$name.err || { tail gpurun_out/occ_$name.err; exit 1; }
   python3 -c "import json; d = json.load(open('gpurun_out/occ_$name.json')); print('$name', round(d['value'] / 1e6, 2), 'Mops/s', round(d['ms_per_step'], 1), 'ms')"
 }
-run lds MT_REPLAY_GLOBAL=0
-run glb1 MT_REPLAY_GLOBAL=1 MT_REPLAY_WAVES=1
-run glb6 MT_REPLAY_GLOBAL=1 MT_REPLAY_WAVES=6
-run glb8 MT_REPLAY_GLOBAL=1 MT_REPLAY_WAVES=8
+run hbm8 MT_REPLAY_LDS=0
+run lds MT_REPLAY_LDS=1
