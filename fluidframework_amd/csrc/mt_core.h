@@ -83,7 +83,9 @@ struct DocHdr {
     int32_t arenaTop, arenaSide, err, errOp;
     int32_t nkeys, opsDone, hwSlots, hwHeap;
     int32_t nrows, seqOps, nfreeRid, gcEpoch; /* rows in the table; sequenced msgs applied */
-    int32_t localLen, _r0, _r1, _r2; /* root.cachedLength: Client.getLength() (client.ts:1051) */
+    int32_t localLen;      /* root.cachedLength: Client.getLength() (client.ts:1051) */
+    int32_t heapTop;       /* maxSeq of the heap's root (valid when heapN > 0) */
+    int32_t _r1, _r2;
     int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
 };
@@ -92,7 +94,7 @@ struct DocHdr {
     X(root) X(nleaf) X(freeHead) X(nfree) X(currentSeq) X(minSeq) X(localSeq) X(collaborating)   \
     X(localShort) X(localLong) X(nclients) X(nextSid) X(heapN) X(memN) X(gqHead) X(gqN)          \
     X(arenaTop) X(arenaSide) X(err) X(errOp) X(nkeys) X(opsDone) X(hwSlots) X(hwHeap) X(nrows)   \
-    X(seqOps) X(nfreeRid) X(gcEpoch) X(localLen)
+    X(seqOps) X(nfreeRid) X(gcEpoch) X(localLen) X(heapTop)
 
 /* Cold per-row data, indexed by a row id that does not move when the row's slot moves. */
 struct ColdRow {
@@ -323,7 +325,8 @@ struct Replica {
         h.sumR = 0;
         h.sumW = 0;
         h.localLen = 0;
-        h._r0 = h._r1 = h._r2 = 0;
+        h.heapTop = 0;
+        h._r1 = h._r2 = 0;
         for (int32_t b = 0; b < HT::C; b += W::N) {
             int32_t i = b + w.lane();
             if (i < HT::C) z.l2s[i] = 0xFF;
@@ -868,6 +871,10 @@ struct Replica {
         z.hseq[j] = tq;
         z.hgen[j] = tg;
     }
+    /* Heap.add + fixup (collections.ts:221-225, 240-247). On the GPU the sift-up is one step: the
+     * ancestors of the new leaf position are read in parallel (lane i: the (i+1)-th ancestor), the
+     * ones it passes are exactly the leading run with maxSeq greater than it (ancestors are ordered
+     * along a path), and they all move down one level at once. */
     MT_HD void heap_add(int32_t rid, int32_t seq) {
         MT_PROF_SCOPE(PH_HEAP);
         int32_t n = h.heapN;
@@ -875,37 +882,138 @@ struct Replica {
             fail(E_CAPACITY);
             return;
         }
-        /* L[k] (1-based) lives at index k-1; fixup (collections.ts:240-247) */
-        int32_t k = n + 1;
-        z.hrid[k - 1] = (int16_t)rid;
-        z.hseq[k - 1] = seq;
-        z.hgen[k - 1] = z.rgen[rid];
+        int32_t k = n + 1; /* L[k] (1-based) lives at index k-1 */
         h.heapN = n + 1;
         if (n + 1 > h.hwHeap) h.hwHeap = n + 1;
-        while (k > 1 && z.hseq[(k >> 1) - 1] - z.hseq[k - 1] > 0) {
-            heap_swap((k >> 1) - 1, k - 1);
-            k >>= 1;
+        uint8_t gen = z.rgen[rid];
+        if constexpr (W::N >= 32) {
+            int32_t l = w.lane();
+            int32_t a = l < 31 ? (k >> (l + 1)) : 0; /* ancestor l+1 (0 = none) */
+            int32_t as = a >= 1 ? z.hseq[a - 1] : 0;
+            uint64_t m = w.ballot(a >= 1 && as - seq > 0);
+            int32_t up = __builtin_ctzll(~m); /* length of the leading run */
+            int16_t ar = 0;
+            uint8_t ag = 0;
+            if (l < up) {
+                ar = z.hrid[a - 1];
+                ag = z.hgen[a - 1];
+            }
+            w.sync();
+            if (l < up) { /* ancestor l+1 moves to ancestor l (ancestor 0 = position k) */
+                int32_t dst = (k >> l) - 1;
+                z.hrid[dst] = ar;
+                z.hseq[dst] = as;
+                z.hgen[dst] = ag;
+            }
+            int32_t fin = k >> up;
+            if (l == 0) {
+                z.hrid[fin - 1] = (int16_t)rid;
+                z.hseq[fin - 1] = seq;
+                z.hgen[fin - 1] = gen;
+            }
+            w.sync();
+            if (fin == 1) h.heapTop = seq;
+        } else {
+            z.hrid[k - 1] = (int16_t)rid;
+            z.hseq[k - 1] = seq;
+            z.hgen[k - 1] = gen;
+            while (k > 1 && z.hseq[(k >> 1) - 1] - z.hseq[k - 1] > 0) {
+                heap_swap((k >> 1) - 1, k - 1);
+                k >>= 1;
+            }
+            h.heapTop = z.hseq[0];
         }
     }
-    /* get (collections.ts:227-233) + fixdown (249-263) */
+    /* Heap.get (collections.ts:227-233) + fixdown (249-263). On the GPU every maxSeq is read in one
+     * pass (lane = index mod 64, one register per 64 entries), the descent is taken on scalars, and
+     * the entries on the path move up one level in one parallel pass. */
     MT_HD void heap_pop(int32_t* rid, int32_t* seq, int32_t* gen) {
         MT_PROF_SCOPE(PH_HEAP);
         int32_t cnt = h.heapN;
-        *rid = z.hrid[0];
-        *seq = z.hseq[0];
-        *gen = z.hgen[0];
-        z.hrid[0] = z.hrid[cnt - 1];
-        z.hseq[0] = z.hseq[cnt - 1];
-        z.hgen[0] = z.hgen[cnt - 1];
-        cnt--;
-        h.heapN = cnt;
-        int32_t k = 1;
-        while ((k << 1) <= cnt) {
-            int32_t j = k << 1;
-            if (j < cnt && z.hseq[j - 1] - z.hseq[j] > 0) j++;
-            if (z.hseq[k - 1] - z.hseq[j - 1] <= 0) break;
-            heap_swap(k - 1, j - 1);
-            k = j;
+        if constexpr (W::N == 64 && HT::H <= 256) {
+            int32_t l = w.lane();
+            int32_t c0 = l < cnt ? z.hseq[l] : 0;
+            int32_t c1 = 64 + l < cnt ? z.hseq[64 + l] : 0;
+            int32_t c2 = 128 + l < cnt ? z.hseq[128 + l] : 0;
+            int32_t c3 = 192 + l < cnt ? z.hseq[192 + l] : 0;
+            int32_t last = cnt - 1; /* index of the entry that moves to the root */
+            int16_t xr = z.hrid[last];
+            uint8_t xg = z.hgen[last];
+            *rid = z.hrid[0];
+            *gen = z.hgen[0];
+            auto L = [&](int32_t i) -> int32_t { /* maxSeq at 1-based position i (i >= 2) */
+                int32_t x = i - 1, c = x >> 6;
+                int32_t v = c == 0 ? c0 : c == 1 ? c1 : c == 2 ? c2 : c3;
+                return w.bcast(v, x & 63);
+            };
+            *seq = w.bcast(c0, 0);
+            int32_t xs = L(cnt >= 2 ? cnt : 2);
+            if (cnt < 2) xs = *seq;
+            cnt--;
+            h.heapN = cnt;
+            if (cnt == 0) return;
+            int32_t path[8];
+            int32_t d = 0, k = 1;
+            while ((k << 1) <= cnt) {
+                int32_t j = k << 1;
+                int32_t sj = L(j);
+                if (j < cnt) {
+                    int32_t s2 = L(j + 1);
+                    if (sj - s2 > 0) {
+                        j++;
+                        sj = s2;
+                    }
+                }
+                if (xs - sj <= 0) break;
+                path[d++] = j;
+                k = j;
+            }
+            /* lane t < d: the entry at path[t] moves to its parent (path[t-1], or the root) */
+            int32_t src = 0, dst = 0;
+            for (int32_t t = 0; t < 8; t++)
+                if (t == l && t < d) {
+                    src = path[t];
+                    dst = t == 0 ? 1 : path[t - 1];
+                }
+            int16_t mr = 0;
+            uint8_t mg = 0;
+            int32_t ms = 0;
+            if (l < d) {
+                mr = z.hrid[src - 1];
+                mg = z.hgen[src - 1];
+                ms = z.hseq[src - 1];
+            }
+            w.sync();
+            if (l < d) {
+                z.hrid[dst - 1] = mr;
+                z.hseq[dst - 1] = ms;
+                z.hgen[dst - 1] = mg;
+            }
+            if (l == 0) {
+                z.hrid[k - 1] = xr;
+                z.hseq[k - 1] = xs;
+                z.hgen[k - 1] = xg;
+            }
+            w.sync();
+            h.heapTop = d > 0 ? w.bcast(ms, 0) : xs;
+        } else {
+            *rid = z.hrid[0];
+            *seq = z.hseq[0];
+            *gen = z.hgen[0];
+            z.hrid[0] = z.hrid[cnt - 1];
+            z.hseq[0] = z.hseq[cnt - 1];
+            z.hgen[0] = z.hgen[cnt - 1];
+            cnt--;
+            h.heapN = cnt;
+            int32_t k = 1;
+            while ((k << 1) <= cnt) {
+                int32_t j = k << 1;
+                if (j < cnt && z.hseq[j - 1] - z.hseq[j] > 0) j++;
+                if (z.hseq[k - 1] - z.hseq[j - 1] <= 0) break;
+                heap_swap(k - 1, j - 1);
+                k = j;
+            }
+            if (cnt > 0) h.heapTop = z.hseq[0];
         }
     }
     /* addToLRUSet (mergeTree.ts:1306-1316) */
@@ -1384,7 +1492,7 @@ struct Replica {
         if (!h.collaborating) return;
         for (int i = 0; i < 2; i++) {
             if (h.heapN < 1) break;
-            if (z.hseq[0] > h.minSeq) break;
+            if (h.heapTop > h.minSeq) break; /* peek (mergeTree.ts:1465-1468) */
             int32_t rid, mseq, gen;
             heap_pop(&rid, &mseq, &gen);
             int32_t s = slot_of(rid, gen); /* -1: unlinked or merged away since it was queued */
