@@ -209,7 +209,24 @@ struct Replica {
     uint64_t prof[PH_N] = {};
 #endif
 
-    MT_HD Replica(const Doc<HT>& doc, const W& wave) : d(doc), z(*doc.t), w(wave) { load_hdr(); }
+    /* The tree skeleton's small per-node arrays and the zamboni heap are reached through these
+     * pointers: they point into the image by default, and the HBM-resident GPU kernel points them
+     * at LDS copies for the duration of a replay (latency-critical, 3.5 KB per document). */
+    int16_t* lo;  /* lorder */
+    int16_t* lp;  /* lpos */
+    int16_t* npar;
+    int8_t* nch;
+    int8_t* nlev;
+    int8_t* nsc;
+    int32_t* hsq;
+    int16_t* hrd;
+    uint8_t* hgn;
+
+    MT_HD Replica(const Doc<HT>& doc, const W& wave)
+        : d(doc), z(*doc.t), w(wave), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
+          nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen) {
+        load_hdr();
+    }
 
     MT_HD void load_hdr() {
 #define MT_HF(f) h.f = w.uniform(z.h.f);
@@ -244,12 +261,12 @@ struct Replica {
             fail(E_CAPACITY);
             return -1;
         }
-        h.freeHead = z.nparent[n];
+        h.freeHead = npar[n];
         h.nfree--;
-        z.nparent[n] = -1;
-        z.nchild[n] = 0;
-        z.nlevel[n] = level;
-        z.nscour[n] = -1; /* needsScour undefined */
+        npar[n] = -1;
+        nch[n] = 0;
+        nlev[n] = level;
+        nsc[n] = -1; /* needsScour undefined */
         clear_slots(n * MAXN, MAXN);
         return n;
     }
@@ -263,8 +280,8 @@ struct Replica {
         w.sync();
     }
     MT_HD void free_node(int32_t n) {
-        z.nparent[n] = (int16_t)h.freeHead;
-        z.nchild[n] = 0;
+        npar[n] = (int16_t)h.freeHead;
+        nch[n] = 0;
         h.freeHead = n;
         h.nfree++;
     }
@@ -276,10 +293,10 @@ struct Replica {
         for (int32_t b = 0; b < ncap; b += W::N) {
             int32_t n = b + w.lane();
             if (n < ncap) {
-                z.nparent[n] = (int16_t)(n + 1 < ncap ? n + 1 : -1);
-                z.nchild[n] = 0;
-                z.nlevel[n] = 0;
-                z.nscour[n] = -1;
+                npar[n] = (int16_t)(n + 1 < ncap ? n + 1 : -1);
+                nch[n] = 0;
+                nlev[n] = 0;
+                nsc[n] = -1;
             }
         }
         for (int32_t b = 0; b < HT::S; b += W::N) {
@@ -296,9 +313,9 @@ struct Replica {
         h.freeHead = 1;
         h.nfree = ncap - 1;
         h.root = 0;
-        z.nparent[0] = -1;
-        z.lorder[0] = 0;
-        z.lpos[0] = 0;
+        npar[0] = -1;
+        lo[0] = 0;
+        lp[0] = 0;
         h.nleaf = 1;
         h.currentSeq = 0;
         h.minSeq = 0;
@@ -400,8 +417,8 @@ struct Replica {
     MT_HD int32_t slot_at(int32_t t) const { /* t = k*8+j over lorder; -1 if not a row */
         int32_t k = t >> 3, j = t & 7;
         if (k >= h.nleaf) return -1;
-        int32_t n = z.lorder[k];
-        return j < z.nchild[n] ? n * MAXN + j : -1;
+        int32_t n = lo[k];
+        return j < nch[n] ? n * MAXN + j : -1;
     }
 
     /* copy every column of row a to row b (same doc) */
@@ -476,11 +493,11 @@ struct Replica {
             int32_t b = delta > 0 ? (nch - 1 - c) * W::N : c * W::N;
             int32_t i = from + b + w.lane();
             bool ok = i < n;
-            int32_t x = ok ? z.lorder[i] : 0;
+            int32_t x = ok ? lo[i] : 0;
             w.sync();
             if (ok) {
-                z.lorder[i + delta] = (int16_t)x;
-                z.lpos[x] = (int16_t)(i + delta);
+                lo[i + delta] = (int16_t)x;
+                lp[x] = (int16_t)(i + delta);
             }
             w.sync();
         }
@@ -512,7 +529,7 @@ struct Replica {
     MT_HD int32_t slot_of(int32_t rid, int32_t gen) {
         if (gen >= 0 && z.rgen[rid] != (uint8_t)gen) return -1;
         int32_t leaf = z.rleaf[rid];
-        int32_t c = z.nchild[leaf];
+        int32_t c = nch[leaf];
         if (W::N == 1) {
             for (int32_t j = 0; j < c; j++)
                 if (z.rid[leaf * MAXN + j] == rid) return leaf * MAXN + j;
@@ -531,7 +548,7 @@ struct Replica {
     MT_HD int32_t quad_slot(int32_t t0) const { /* t0 % 4 == 0; -1 past the last leaf */
         int32_t k = t0 >> 3;
         if (k >= h.nleaf) return -1;
-        return z.lorder[k] * MAXN + (t0 & 4);
+        return lo[k] * MAXN + (t0 & 4);
     }
     MT_HD bool ovl_has(int32_t s, int32_t client) const {
         uint64_t ov = cold(s).ovl;
@@ -622,24 +639,24 @@ struct Replica {
      * remapped by `place_after_split` — callers use the returned final slot. */
     MT_HD void node_insert_child(int32_t p, int32_t idx, int32_t child) {
         /* interior node p: insert `child` at idx (insertChildNode, mergeTree.ts:2162-2172) */
-        int32_t n = z.nchild[p];
+        int32_t n = nch[p];
         for (int32_t i = n; i > idx; i--) z.kids[p * MAXN + i] = z.kids[p * MAXN + i - 1];
         z.kids[p * MAXN + idx] = (int16_t)child;
-        z.nchild[p] = (int8_t)(n + 1);
-        z.nparent[child] = (int16_t)p;
+        nch[p] = (int8_t)(n + 1);
+        npar[child] = (int16_t)p;
     }
     MT_HD int32_t child_index(int32_t p, int32_t child) const {
-        for (int32_t i = 0; i < z.nchild[p]; i++)
+        for (int32_t i = 0; i < nch[p]; i++)
             if (z.kids[p * MAXN + i] == child) return i;
         return -1;
     }
     /* insert leaf `nl` into lorder right after leaf `after` */
     MT_HD void lorder_insert_after(int32_t after, int32_t nl) {
-        int32_t k = z.lpos[after] + 1;
+        int32_t k = lp[after] + 1;
         int32_t n = h.nleaf;
         lorder_shift(k, n, 1);
-        z.lorder[k] = (int16_t)nl;
-        z.lpos[nl] = (int16_t)k;
+        lo[k] = (int16_t)nl;
+        lp[nl] = (int16_t)k;
         h.nleaf = n + 1;
     }
     /* split (mergeTree.ts:2509-2522) of a full node (8 children) into 4 + 4; the new node is
@@ -649,7 +666,7 @@ struct Replica {
         int32_t first = -1;
         int32_t n = n0;
         for (;;) { /* iterative: a split may overflow the parent, up to the root */
-            int8_t lvl = z.nlevel[n];
+            int8_t lvl = nlev[n];
             int32_t nn = alloc_node(lvl);
             if (nn < 0) return -1;
             if (first < 0) first = nn;
@@ -661,36 +678,36 @@ struct Replica {
                 for (int32_t i = 0; i < 4; i++) {
                     int32_t c = z.kids[n * MAXN + 4 + i];
                     z.kids[nn * MAXN + i] = (int16_t)c;
-                    z.nparent[c] = (int16_t)nn;
+                    npar[c] = (int16_t)nn;
                 }
             }
-            z.nchild[n] = 4;
-            z.nchild[nn] = 4;
+            nch[n] = 4;
+            nch[nn] = 4;
             if (lvl == 0) lorder_insert_after(n, nn);
-            int32_t p = z.nparent[n];
+            int32_t p = npar[n];
             if (p < 0) {
                 int32_t r = alloc_node((int8_t)(lvl + 1));
                 if (r < 0) return -1;
                 z.kids[r * MAXN + 0] = (int16_t)n;
                 z.kids[r * MAXN + 1] = (int16_t)nn;
-                z.nchild[r] = 2;
-                z.nparent[n] = (int16_t)r;
-                z.nparent[nn] = (int16_t)r;
+                nch[r] = 2;
+                npar[n] = (int16_t)r;
+                npar[nn] = (int16_t)r;
                 h.root = r;
                 return first;
             }
             node_insert_child(p, child_index(p, n) + 1, nn);
-            if (z.nchild[p] < MAXN) return first;
+            if (nch[p] < MAXN) return first;
             n = p;
         }
     }
     /* Make room at child index j of leaf n; returns slot for the new row (after any split). */
     MT_HD int32_t leaf_insert_slot(int32_t n, int32_t j) {
         MT_PROF_SCOPE(PH_LEAFINS);
-        int32_t c = z.nchild[n];
+        int32_t c = nch[n];
         slab_shift_right(n, j, c);
         z.rid[n * MAXN + j] = -1; /* not a row yet: the caller assigns one */
-        z.nchild[n] = (int8_t)(c + 1);
+        nch[n] = (int8_t)(c + 1);
         if (c + 1 >= MAXN) {
             int32_t nn = split_node(n);
             if (nn < 0) return -1;
@@ -756,15 +773,15 @@ struct Replica {
      * the LEFT part afterwards (the right part is the next row in document order). */
     MT_HD int32_t split_row(int32_t t, int32_t off, int32_t* rsOut = nullptr) {
         MT_PROF_SCOPE(PH_SPLIT);
-        int32_t n = z.lorder[t >> 3], j = t & 7;
+        int32_t n = lo[t >> 3], j = t & 7;
         int32_t s0 = n * MAXN + j;
         if (z.flags[s0] & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
-        bool willSplit = z.nchild[n] + 1 >= MAXN;
+        bool willSplit = nch[n] + 1 >= MAXN;
         int32_t rs = leaf_insert_slot(n, j + 1);
         if (rs < 0) return -1;
         /* the left part stays at n*8+j unless the leaf split moved children 4..7 */
         int32_t ls = n * MAXN + j;
-        if (willSplit && j >= 4) ls = z.lorder[z.lpos[n] + 1] * MAXN + (j - 4);
+        if (willSplit && j >= 4) ls = lo[lp[n] + 1] * MAXN + (j - 4);
         copy_row(rs, ls);
         z.rid[rs] = (int16_t)alloc_rid();
         z.rleaf[z.rid[rs]] = (int16_t)(rs / MAXN);
@@ -861,15 +878,15 @@ struct Replica {
 
     /* ---- zamboni heap (collections.ts:212-264, LRUSegmentComparer mergeTree.ts:957-960) ---- */
     MT_HD void heap_swap(int32_t i, int32_t j) {
-        int16_t tr = z.hrid[i];
-        int32_t tq = z.hseq[i];
-        uint8_t tg = z.hgen[i];
-        z.hrid[i] = z.hrid[j];
-        z.hseq[i] = z.hseq[j];
-        z.hgen[i] = z.hgen[j];
-        z.hrid[j] = tr;
-        z.hseq[j] = tq;
-        z.hgen[j] = tg;
+        int16_t tr = hrd[i];
+        int32_t tq = hsq[i];
+        uint8_t tg = hgn[i];
+        hrd[i] = hrd[j];
+        hsq[i] = hsq[j];
+        hgn[i] = hgn[j];
+        hrd[j] = tr;
+        hsq[j] = tq;
+        hgn[j] = tg;
     }
     /* Heap.add + fixup (collections.ts:221-225, 240-247). On the GPU the sift-up is one step: the
      * ancestors of the new leaf position are read in parallel (lane i: the (i+1)-th ancestor), the
@@ -889,39 +906,39 @@ struct Replica {
         if constexpr (W::N >= 32) {
             int32_t l = w.lane();
             int32_t a = l < 31 ? (k >> (l + 1)) : 0; /* ancestor l+1 (0 = none) */
-            int32_t as = a >= 1 ? z.hseq[a - 1] : 0;
+            int32_t as = a >= 1 ? hsq[a - 1] : 0;
             uint64_t m = w.ballot(a >= 1 && as - seq > 0);
             int32_t up = __builtin_ctzll(~m); /* length of the leading run */
             int16_t ar = 0;
             uint8_t ag = 0;
             if (l < up) {
-                ar = z.hrid[a - 1];
-                ag = z.hgen[a - 1];
+                ar = hrd[a - 1];
+                ag = hgn[a - 1];
             }
             w.sync();
             if (l < up) { /* ancestor l+1 moves to ancestor l (ancestor 0 = position k) */
                 int32_t dst = (k >> l) - 1;
-                z.hrid[dst] = ar;
-                z.hseq[dst] = as;
-                z.hgen[dst] = ag;
+                hrd[dst] = ar;
+                hsq[dst] = as;
+                hgn[dst] = ag;
             }
             int32_t fin = k >> up;
             if (l == 0) {
-                z.hrid[fin - 1] = (int16_t)rid;
-                z.hseq[fin - 1] = seq;
-                z.hgen[fin - 1] = gen;
+                hrd[fin - 1] = (int16_t)rid;
+                hsq[fin - 1] = seq;
+                hgn[fin - 1] = gen;
             }
             w.sync();
             if (fin == 1) h.heapTop = seq;
         } else {
-            z.hrid[k - 1] = (int16_t)rid;
-            z.hseq[k - 1] = seq;
-            z.hgen[k - 1] = gen;
-            while (k > 1 && z.hseq[(k >> 1) - 1] - z.hseq[k - 1] > 0) {
+            hrd[k - 1] = (int16_t)rid;
+            hsq[k - 1] = seq;
+            hgn[k - 1] = gen;
+            while (k > 1 && hsq[(k >> 1) - 1] - hsq[k - 1] > 0) {
                 heap_swap((k >> 1) - 1, k - 1);
                 k >>= 1;
             }
-            h.heapTop = z.hseq[0];
+            h.heapTop = hsq[0];
         }
     }
     /* Heap.get (collections.ts:227-233) + fixdown (249-263). On the GPU every maxSeq is read in one
@@ -932,15 +949,15 @@ struct Replica {
         int32_t cnt = h.heapN;
         if constexpr (W::N == 64 && HT::H <= 256) {
             int32_t l = w.lane();
-            int32_t c0 = l < cnt ? z.hseq[l] : 0;
-            int32_t c1 = 64 + l < cnt ? z.hseq[64 + l] : 0;
-            int32_t c2 = 128 + l < cnt ? z.hseq[128 + l] : 0;
-            int32_t c3 = 192 + l < cnt ? z.hseq[192 + l] : 0;
+            int32_t c0 = l < cnt ? hsq[l] : 0;
+            int32_t c1 = 64 + l < cnt ? hsq[64 + l] : 0;
+            int32_t c2 = 128 + l < cnt ? hsq[128 + l] : 0;
+            int32_t c3 = 192 + l < cnt ? hsq[192 + l] : 0;
             int32_t last = cnt - 1; /* index of the entry that moves to the root */
-            int16_t xr = z.hrid[last];
-            uint8_t xg = z.hgen[last];
-            *rid = z.hrid[0];
-            *gen = z.hgen[0];
+            int16_t xr = hrd[last];
+            uint8_t xg = hgn[last];
+            *rid = hrd[0];
+            *gen = hgn[0];
             auto L = [&](int32_t i) -> int32_t { /* maxSeq at 1-based position i (i >= 2) */
                 int32_t x = i - 1, c = x >> 6;
                 int32_t v = c == 0 ? c0 : c == 1 ? c1 : c == 2 ? c2 : c3;
@@ -979,48 +996,48 @@ struct Replica {
             uint8_t mg = 0;
             int32_t ms = 0;
             if (l < d) {
-                mr = z.hrid[src - 1];
-                mg = z.hgen[src - 1];
-                ms = z.hseq[src - 1];
+                mr = hrd[src - 1];
+                mg = hgn[src - 1];
+                ms = hsq[src - 1];
             }
             w.sync();
             if (l < d) {
-                z.hrid[dst - 1] = mr;
-                z.hseq[dst - 1] = ms;
-                z.hgen[dst - 1] = mg;
+                hrd[dst - 1] = mr;
+                hsq[dst - 1] = ms;
+                hgn[dst - 1] = mg;
             }
             if (l == 0) {
-                z.hrid[k - 1] = xr;
-                z.hseq[k - 1] = xs;
-                z.hgen[k - 1] = xg;
+                hrd[k - 1] = xr;
+                hsq[k - 1] = xs;
+                hgn[k - 1] = xg;
             }
             w.sync();
             h.heapTop = d > 0 ? w.bcast(ms, 0) : xs;
         } else {
-            *rid = z.hrid[0];
-            *seq = z.hseq[0];
-            *gen = z.hgen[0];
-            z.hrid[0] = z.hrid[cnt - 1];
-            z.hseq[0] = z.hseq[cnt - 1];
-            z.hgen[0] = z.hgen[cnt - 1];
+            *rid = hrd[0];
+            *seq = hsq[0];
+            *gen = hgn[0];
+            hrd[0] = hrd[cnt - 1];
+            hsq[0] = hsq[cnt - 1];
+            hgn[0] = hgn[cnt - 1];
             cnt--;
             h.heapN = cnt;
             int32_t k = 1;
             while ((k << 1) <= cnt) {
                 int32_t j = k << 1;
-                if (j < cnt && z.hseq[j - 1] - z.hseq[j] > 0) j++;
-                if (z.hseq[k - 1] - z.hseq[j - 1] <= 0) break;
+                if (j < cnt && hsq[j - 1] - hsq[j] > 0) j++;
+                if (hsq[k - 1] - hsq[j - 1] <= 0) break;
                 heap_swap(k - 1, j - 1);
                 k = j;
             }
-            if (cnt > 0) h.heapTop = z.hseq[0];
+            if (cnt > 0) h.heapTop = hsq[0];
         }
     }
     /* addToLRUSet (mergeTree.ts:1306-1316) */
     MT_HD void add_lru(int32_t s, int32_t seq) {
         int32_t n = s / MAXN;
-        if (z.nscour[n] != 1 && seq > h.currentSeq) {
-            z.nscour[n] = 1;
+        if (nsc[n] != 1 && seq > h.currentSeq) {
+            nsc[n] = 1;
             heap_add(z.rid[s], seq);
         }
     }
@@ -1137,7 +1154,7 @@ struct Replica {
      * merged into their predecessor or unlinked exactly as the reference decides. */
     MT_HD int32_t scour_leaf(int32_t n) {
         MT_PROF_SCOPE(PH_SCOUR);
-        int32_t c = z.nchild[n];
+        int32_t c = nch[n];
         int32_t wpos = 0;
         int32_t prev = -1; /* slot of prevSegment in the compacted slab */
         int32_t minSeq = h.minSeq;
@@ -1183,7 +1200,7 @@ struct Replica {
             }
         }
         h.nrows -= c - wpos;
-        z.nchild[n] = (int8_t)wpos;
+        nch[n] = (int8_t)wpos;
         if (wpos < c) clear_slots(n * MAXN + wpos, c - wpos);
         return wpos;
     }
@@ -1204,7 +1221,7 @@ struct Replica {
         int32_t n = -1;
         for (int32_t i = 0; i < MAXN; i++)
             if (i == li && i < nl) n = leaves[i];
-        int32_t c = n >= 0 ? z.nchild[n] : 0;
+        int32_t c = n >= 0 ? nch[n] : 0;
         bool valid = j < c;
         HotRow r = {};
         if (valid) r = load_row(n * MAXN + j);
@@ -1295,7 +1312,7 @@ struct Replica {
             store_row(n * MAXN + __builtin_popcountll(keep & lmask & below), r);
         }
         if (valid && j >= newc) z.len[n * MAXN + j] = 0; /* disjoint from every kept row's target */
-        if (n >= 0 && j == 0) z.nchild[n] = (int8_t)newc;
+        if (n >= 0 && j == 0) nch[n] = (int8_t)newc;
         w.sync();
         for (int32_t i = 0; i < nl; i++) cnt[i] = __builtin_popcountll(keep & (0xFFull << (8 * i)));
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
@@ -1317,9 +1334,9 @@ struct Replica {
         MT_PROF_SCOPE(PH_PACK);
       int32_t block = block0;
       for (;;) { /* iterative: pack recurses upward while the parent underflows (1447-1452) */
-        int32_t parent = z.nparent[block];
-        int32_t pc = z.nchild[parent];
-        int8_t lvl = z.nlevel[block];
+        int32_t parent = npar[block];
+        int32_t pc = nch[parent];
+        int8_t lvl = nlev[block];
         if (lvl == 0) {
             /* scour every sibling leaf, then redistribute their rows over new leaves */
             int32_t total = 0;
@@ -1342,9 +1359,9 @@ struct Replica {
             int32_t ocnt[MAXN];
             for (int32_t i = 0; i < pc; i++) {
                 oldk[i] = z.kids[parent * MAXN + i];
-                ocnt[i] = z.nchild[oldk[i]];
+                ocnt[i] = nch[oldk[i]];
             }
-            int32_t firstPos = z.lpos[oldk[0]];
+            int32_t firstPos = lp[oldk[0]];
             int32_t newk[MAXN];
             int32_t ncnt[MAXN];
             for (int32_t ni = 0; ni < cc; ni++) {
@@ -1386,10 +1403,10 @@ struct Replica {
             }
             for (int32_t ni = 0; ni < cc; ni++) {
                 int32_t nb = newk[ni];
-                z.nchild[nb] = (int8_t)ncnt[ni];
-                z.nparent[nb] = (int16_t)parent;
-                z.nlevel[nb] = 0;
-                z.nscour[nb] = -1;
+                nch[nb] = (int8_t)ncnt[ni];
+                npar[nb] = (int16_t)parent;
+                nlev[nb] = 0;
+                nsc[nb] = -1;
                 if (ncnt[ni] < MAXN) clear_slots(nb * MAXN + ncnt[ni], MAXN - ncnt[ni]);
             }
             for (int32_t i = cc; i < pc; i++) free_node(oldk[i]);
@@ -1398,12 +1415,12 @@ struct Replica {
             int32_t delta = cc - pc;
             lorder_shift(firstPos + pc, nl, delta);
             for (int32_t i = pc; i < cc; i++) {
-                z.lorder[firstPos + i] = (int16_t)newk[i];
-                z.lpos[newk[i]] = (int16_t)(firstPos + i);
+                lo[firstPos + i] = (int16_t)newk[i];
+                lp[newk[i]] = (int16_t)(firstPos + i);
             }
             h.nleaf = nl + delta;
             for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (int16_t)newk[i];
-            z.nchild[parent] = (int8_t)cc;
+            nch[parent] = (int8_t)cc;
         } else {
             MT_PROF_SCOPE(PH_P2);
             if constexpr (W::N >= MAXN * MAXN) {
@@ -1412,7 +1429,7 @@ struct Replica {
                 int32_t q = w.lane();
                 int32_t i = q >> 3, j = q & (MAXN - 1);
                 int32_t cb = i < pc ? z.kids[parent * MAXN + i] : -1;
-                int32_t cn = cb >= 0 ? z.nchild[cb] : 0;
+                int32_t cn = cb >= 0 ? nch[cb] : 0;
                 bool has = j < cn;
                 int32_t ch = has ? z.kids[cb * MAXN + j] : -1;
                 uint64_t vm = w.ballot(has);
@@ -1441,15 +1458,15 @@ struct Replica {
                 w.sync();
                 if (has) {
                     z.kids[nb * MAXN + slot] = (int16_t)ch;
-                    z.nparent[ch] = (int16_t)nb;
+                    npar[ch] = (int16_t)nb;
                 }
                 w.sync();
                 for (int32_t k = 0; k < cc; k++) {
-                    z.nchild[nbk[k]] = (int8_t)(base + (k < extra ? 1 : 0));
-                    z.nparent[nbk[k]] = (int16_t)parent;
+                    nch[nbk[k]] = (int8_t)(base + (k < extra ? 1 : 0));
+                    npar[nbk[k]] = (int16_t)parent;
                     z.kids[parent * MAXN + k] = (int16_t)nbk[k];
                 }
-                z.nchild[parent] = (int8_t)cc;
+                nch[parent] = (int8_t)cc;
             } else {
                 int16_t hold[MAXN * MAXN];
                 int32_t total = 0;
@@ -1457,7 +1474,7 @@ struct Replica {
                 for (int32_t i = 0; i < pc; i++) {
                     int32_t cb = z.kids[parent * MAXN + i];
                     oldk[i] = cb;
-                    for (int32_t q = 0; q < z.nchild[cb]; q++) hold[total++] = z.kids[cb * MAXN + q];
+                    for (int32_t q = 0; q < nch[cb]; q++) hold[total++] = z.kids[cb * MAXN + q];
                 }
                 int32_t cc = total / (MAXN / 2);
                 if (cc > MAXN - 1) cc = MAXN - 1;
@@ -1473,16 +1490,16 @@ struct Replica {
                     for (int32_t q = 0; q < cnt; q++) {
                         int32_t ch = hold[read++];
                         z.kids[nb * MAXN + q] = (int16_t)ch;
-                        z.nparent[ch] = (int16_t)nb;
+                        npar[ch] = (int16_t)nb;
                     }
-                    z.nchild[nb] = (int8_t)cnt;
-                    z.nparent[nb] = (int16_t)parent;
+                    nch[nb] = (int8_t)cnt;
+                    npar[nb] = (int16_t)parent;
                     z.kids[parent * MAXN + ni] = (int16_t)nb;
                 }
-                z.nchild[parent] = (int8_t)cc;
+                nch[parent] = (int8_t)cc;
             }
         }
-        if (!(z.nchild[parent] < MAXN / 2 && z.nparent[parent] >= 0)) return;
+        if (!(nch[parent] < MAXN / 2 && npar[parent] >= 0)) return;
         block = parent;
       }
     }
@@ -1498,12 +1515,12 @@ struct Replica {
             int32_t s = slot_of(rid, gen); /* -1: unlinked or merged away since it was queued */
             if (s < 0) continue;
             int32_t n = s / MAXN;
-            if (z.nscour[n] == 0) continue;
-            int32_t before = z.nchild[n];
+            if (nsc[n] == 0) continue;
+            int32_t before = nch[n];
             int32_t after = scour_one(n);
-            z.nscour[n] = 0;
+            nsc[n] = 0;
             if (after < before) {
-                if (after < MAXN / 2 && z.nparent[n] >= 0) pack(n);
+                if (after < MAXN / 2 && npar[n] >= 0) pack(n);
             }
         }
     }
@@ -1575,7 +1592,7 @@ struct Replica {
             if (P + v > pos && !(z.flags[s] & RF_MARKER)) {
                 int32_t ls = split_row(t, pos - P);
                 if (ls < 0) return -1;
-                k = z.lpos[ls / MAXN];
+                k = lp[ls / MAXN];
                 j = (ls & (MAXN - 1)) + 1;
             } else {
                 k = t >> 3;
@@ -1585,8 +1602,8 @@ struct Replica {
             }
         }
         for (;;) {
-            int32_t n = z.lorder[k];
-            int32_t c = z.nchild[n];
+            int32_t n = lo[k];
+            int32_t c = nch[n];
             for (; j < c; j++) {
                 int32_t s = n * MAXN + j;
                 if (vis(s, refSeq, client) > 0 || break_tie(s, refSeq, client)) return leaf_insert_slot(n, j);
@@ -1768,15 +1785,15 @@ struct Replica {
                 fail(E_ASSERT);
                 return;
             }
-            if (split_row(z.lpos[sg / MAXN] * MAXN + (sg & (MAXN - 1)), end - Pg) < 0) return;
+            if (split_row(lp[sg / MAXN] * MAXN + (sg & (MAXN - 1)), end - Pg) < 0) return;
         }
         int32_t sa = slot_of(ridFirst, -1), sb = slot_of(ridLast, -1);
         if (sa < 0 || sb < 0) {
             fail(E_ASSERT);
             return;
         }
-        int32_t ta = z.lpos[sa / MAXN] * MAXN + (sa & (MAXN - 1));
-        int32_t tb = z.lpos[sb / MAXN] * MAXN + (sb & (MAXN - 1));
+        int32_t ta = lp[sa / MAXN] * MAXN + (sa & (MAXN - 1));
+        int32_t tb = lp[sb / MAXN] * MAXN + (sb & (MAXN - 1));
         for (int32_t b = ta & ~3; b <= tb; b += 4 * W::N) {
             int32_t t0 = b + 4 * w.lane();
             int32_t s0 = quad_slot(t0);

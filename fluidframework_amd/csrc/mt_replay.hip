@@ -56,8 +56,37 @@ __device__ inline void copy_image(HT* dst, const HT* src) {
     for (int i = threadIdx.x; i < n; i += WG) d[i] = s[i];
 }
 
-/* K1-K4 fused: the whole event stream of a document, one wave per document. For the small
- * profile the hot image is staged into LDS for the whole replay. */
+/* The tree skeleton's per-node arrays and the zamboni heap of one document: staged into LDS by the
+ * HBM-resident kernel (the rest of the hot image stays in HBM). */
+template <class HT>
+struct Skel {
+    int16_t lorder[HT::N], lpos[HT::N], nparent[HT::N];
+    int8_t nchild[HT::N], nlevel[HT::N], nscour[HT::N];
+    int32_t hseq[HT::H];
+    int16_t hrid[HT::H];
+    uint8_t hgen[HT::H];
+};
+template <class T>
+__device__ inline void wave_copy(T* dst, const T* src, int n) {
+    for (int i = threadIdx.x; i < n; i += WG) dst[i] = src[i];
+}
+template <class HT>
+__device__ inline void skel_move(Skel<HT>& k, HT& z, bool in) {
+    constexpr int N = HT::N, H = HT::H;
+    if (in) {
+        wave_copy(k.lorder, z.lorder, N), wave_copy(k.lpos, z.lpos, N), wave_copy(k.nparent, z.nparent, N);
+        wave_copy(k.nchild, z.nchild, N), wave_copy(k.nlevel, z.nlevel, N), wave_copy(k.nscour, z.nscour, N);
+        wave_copy(k.hseq, z.hseq, H), wave_copy(k.hrid, z.hrid, H), wave_copy(k.hgen, z.hgen, H);
+    } else {
+        wave_copy(z.lorder, k.lorder, N), wave_copy(z.lpos, k.lpos, N), wave_copy(z.nparent, k.nparent, N);
+        wave_copy(z.nchild, k.nchild, N), wave_copy(z.nlevel, k.nlevel, N), wave_copy(z.nscour, k.nscour, N);
+        wave_copy(z.hseq, k.hseq, H), wave_copy(z.hrid, k.hrid, H), wave_copy(z.hgen, k.hgen, H);
+    }
+}
+
+/* K1-K4 fused: the whole event stream of a document, one wave per document. LDS = true stages the
+ * whole small-profile hot image in LDS; otherwise the image stays in HBM and only the skeleton and
+ * the heap (Skel, 3.5 KB for the small profile) are staged. */
 template <class HT, bool LDS, int MINW = 1>
 __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
@@ -87,6 +116,21 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
 #endif
         __syncthreads();
         copy_image(g, &hot);
+    } else if constexpr (sizeof(Skel<HT>) <= 4096) {
+        __shared__ __attribute__((aligned(16))) Skel<HT> sk;
+        skel_move(sk, *v.t, true);
+        __syncthreads();
+        Replica<WaveGPU, HT> r(v, WaveGPU());
+        r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild, r.nlev = sk.nlevel;
+        r.nsc = sk.nscour, r.hsq = sk.hseq, r.hrd = sk.hrid, r.hgn = sk.hgen;
+        r.replay(p);
+        r.commit();
+        __syncthreads();
+        skel_move(sk, *v.t, false);
+#ifdef MT_PROF
+        if (prof && threadIdx.x == 0)
+            for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
+#endif
     } else {
         Replica<WaveGPU, HT> r(v, WaveGPU());
         r.replay(p);
