@@ -223,6 +223,7 @@ struct mt_engine {
     int64_t ndocs;
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
+    int waves = 8;    /* occupancy target of the HBM-resident kernel (MT_REPLAY_WAVES=6|7|8) */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
@@ -301,6 +302,8 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->ndocs = ndocs;
     const char* g = getenv("MT_REPLAY_LDS");
     e->lds = g && g[0] == '1';
+    const char* wv = getenv("MT_REPLAY_WAVES");
+    e->waves = wv ? atoi(wv) : 8;
     e->profile = prof;
     if (hipSetDevice(device) != hipSuccess) {
         delete e;
@@ -448,6 +451,10 @@ int32_t mt_engine_run(mt_engine* e) {
              * LDS residency (4 documents per CU) saves. MT_REPLAY_LDS=1 selects the LDS-staged form. */
             if (e->lds)
                 launch(k_replay<HT, true>);
+            else if (e->waves == 6)
+                launch(k_replay<HT, false, 6>);
+            else if (e->waves == 7)
+                launch(k_replay<HT, false, 7>);
             else
                 launch(k_replay<HT, false, 8>);
         } else {
