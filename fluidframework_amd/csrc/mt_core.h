@@ -2108,11 +2108,24 @@ struct Replica {
         return h;
     }
 
-    /* Apply a whole event stream, in order. */
+    /* Apply a whole event stream. The records are fetched W::N at a time, one per lane (8 dwords
+     * each), and handed to apply() through lane broadcasts, so the stream costs one global-memory
+     * round trip per W::N events instead of one per event. */
     MT_HD void replay(const Pools& p) {
-        for (int64_t i = 0; i < p.nops; i++) {
-            apply(p.ops[i], p);
-            if (h.err) break;
+        static_assert(sizeof(mt_op_rec) == 32, "op record is 8 dwords");
+        for (int64_t b = 0; b < p.nops; b += W::N) {
+            int64_t i = b + w.lane();
+            int32_t rec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (i < p.nops) __builtin_memcpy(rec, &p.ops[i], sizeof(rec));
+            int64_t cnt = p.nops - b < W::N ? p.nops - b : W::N;
+            for (int64_t k = 0; k < cnt; k++) {
+                int32_t u[8];
+                for (int q = 0; q < 8; q++) u[q] = w.bcast(rec[q], (int)k);
+                mt_op_rec op;
+                __builtin_memcpy(&op, u, sizeof(op));
+                apply(op, p);
+                if (h.err) return;
+            }
         }
     }
 };
