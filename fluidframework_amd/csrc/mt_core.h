@@ -212,7 +212,6 @@ struct Replica {
     /* The tree skeleton's small per-node arrays and the zamboni heap are reached through these
      * pointers: they point into the image by default, and the HBM-resident GPU kernel points them
      * at LDS copies for the duration of a replay (latency-critical, 3.5 KB per document). */
-    int16_t* kid; /* kids (8 per node) */
     int16_t* lo;  /* lorder */
     int16_t* lp;  /* lpos */
     int16_t* npar;
@@ -224,7 +223,7 @@ struct Replica {
     uint8_t* hgn;
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
-        : d(doc), z(*doc.t), w(wave), kid(z.kids), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
+        : d(doc), z(*doc.t), w(wave), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
           nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen) {
         load_hdr();
     }
@@ -641,30 +640,15 @@ struct Replica {
     MT_HD void node_insert_child(int32_t p, int32_t idx, int32_t child) {
         /* interior node p: insert `child` at idx (insertChildNode, mergeTree.ts:2162-2172) */
         int32_t n = nch[p];
-        if constexpr (W::N >= MAXN) { /* shift children idx..n-1 right by one, all at once */
-            int32_t l = w.lane();
-            int32_t c = l >= idx && l < n ? kid[p * MAXN + l] : 0;
-            w.sync();
-            if (l >= idx && l < n) kid[p * MAXN + l + 1] = (int16_t)c;
-            w.sync();
-        } else {
-            for (int32_t i = n; i > idx; i--) kid[p * MAXN + i] = kid[p * MAXN + i - 1];
-        }
-        kid[p * MAXN + idx] = (int16_t)child;
+        for (int32_t i = n; i > idx; i--) z.kids[p * MAXN + i] = z.kids[p * MAXN + i - 1];
+        z.kids[p * MAXN + idx] = (int16_t)child;
         nch[p] = (int8_t)(n + 1);
         npar[child] = (int16_t)p;
     }
     MT_HD int32_t child_index(int32_t p, int32_t child) const {
-        int32_t n = nch[p];
-        if constexpr (W::N >= MAXN) {
-            int32_t l = w.lane();
-            uint64_t m = w.ballot(l < n && kid[p * MAXN + (l & (MAXN - 1))] == child);
-            return m ? W::ffs(m) : -1;
-        } else {
-            for (int32_t i = 0; i < n; i++)
-                if (kid[p * MAXN + i] == child) return i;
-            return -1;
-        }
+        for (int32_t i = 0; i < nch[p]; i++)
+            if (z.kids[p * MAXN + i] == child) return i;
+        return -1;
     }
     /* insert leaf `nl` into lorder right after leaf `after` */
     MT_HD void lorder_insert_after(int32_t after, int32_t nl) {
@@ -692,8 +676,8 @@ struct Replica {
                 clear_slots(n * MAXN + 4, 4);
             } else {
                 for (int32_t i = 0; i < 4; i++) {
-                    int32_t c = kid[n * MAXN + 4 + i];
-                    kid[nn * MAXN + i] = (int16_t)c;
+                    int32_t c = z.kids[n * MAXN + 4 + i];
+                    z.kids[nn * MAXN + i] = (int16_t)c;
                     npar[c] = (int16_t)nn;
                 }
             }
@@ -704,8 +688,8 @@ struct Replica {
             if (p < 0) {
                 int32_t r = alloc_node((int8_t)(lvl + 1));
                 if (r < 0) return -1;
-                kid[r * MAXN + 0] = (int16_t)n;
-                kid[r * MAXN + 1] = (int16_t)nn;
+                z.kids[r * MAXN + 0] = (int16_t)n;
+                z.kids[r * MAXN + 1] = (int16_t)nn;
                 nch[r] = 2;
                 npar[n] = (int16_t)r;
                 npar[nn] = (int16_t)r;
@@ -1358,11 +1342,11 @@ struct Replica {
             int32_t total = 0;
             if constexpr (W::N >= MAXN * MAXN) {
                 int32_t sib[MAXN], cnt[MAXN];
-                for (int32_t i = 0; i < MAXN; i++) sib[i] = i < pc ? kid[parent * MAXN + i] : -1;
+                for (int32_t i = 0; i < MAXN; i++) sib[i] = i < pc ? z.kids[parent * MAXN + i] : -1;
                 scour_par(sib, pc, cnt);
                 for (int32_t i = 0; i < pc; i++) total += cnt[i];
             } else {
-                for (int32_t i = 0; i < pc; i++) total += scour_leaf(kid[parent * MAXN + i]);
+                for (int32_t i = 0; i < pc; i++) total += scour_leaf(z.kids[parent * MAXN + i]);
             }
             MT_PROF_SCOPE(PH_P1);
             int32_t cc = total / (MAXN / 2);
@@ -1374,7 +1358,7 @@ struct Replica {
             int32_t oldk[MAXN];
             int32_t ocnt[MAXN];
             for (int32_t i = 0; i < pc; i++) {
-                oldk[i] = kid[parent * MAXN + i];
+                oldk[i] = z.kids[parent * MAXN + i];
                 ocnt[i] = nch[oldk[i]];
             }
             int32_t firstPos = lp[oldk[0]];
@@ -1435,7 +1419,7 @@ struct Replica {
                 lp[newk[i]] = (int16_t)(firstPos + i);
             }
             h.nleaf = nl + delta;
-            for (int32_t i = 0; i < cc; i++) kid[parent * MAXN + i] = (int16_t)newk[i];
+            for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (int16_t)newk[i];
             nch[parent] = (int8_t)cc;
         } else {
             MT_PROF_SCOPE(PH_P2);
@@ -1444,10 +1428,10 @@ struct Replica {
                  * its rank among all grandchildren places it in the regrouped nodes */
                 int32_t q = w.lane();
                 int32_t i = q >> 3, j = q & (MAXN - 1);
-                int32_t cb = i < pc ? kid[parent * MAXN + i] : -1;
+                int32_t cb = i < pc ? z.kids[parent * MAXN + i] : -1;
                 int32_t cn = cb >= 0 ? nch[cb] : 0;
                 bool has = j < cn;
-                int32_t ch = has ? kid[cb * MAXN + j] : -1;
+                int32_t ch = has ? z.kids[cb * MAXN + j] : -1;
                 uint64_t vm = w.ballot(has);
                 int32_t total = __builtin_popcountll(vm);
                 uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
@@ -1473,14 +1457,14 @@ struct Replica {
                     if (k == ni && k < cc) nb = nbk[k];
                 w.sync();
                 if (has) {
-                    kid[nb * MAXN + slot] = (int16_t)ch;
+                    z.kids[nb * MAXN + slot] = (int16_t)ch;
                     npar[ch] = (int16_t)nb;
                 }
                 w.sync();
                 for (int32_t k = 0; k < cc; k++) {
                     nch[nbk[k]] = (int8_t)(base + (k < extra ? 1 : 0));
                     npar[nbk[k]] = (int16_t)parent;
-                    kid[parent * MAXN + k] = (int16_t)nbk[k];
+                    z.kids[parent * MAXN + k] = (int16_t)nbk[k];
                 }
                 nch[parent] = (int8_t)cc;
             } else {
@@ -1488,9 +1472,9 @@ struct Replica {
                 int32_t total = 0;
                 int32_t oldk[MAXN];
                 for (int32_t i = 0; i < pc; i++) {
-                    int32_t cb = kid[parent * MAXN + i];
+                    int32_t cb = z.kids[parent * MAXN + i];
                     oldk[i] = cb;
-                    for (int32_t q = 0; q < nch[cb]; q++) hold[total++] = kid[cb * MAXN + q];
+                    for (int32_t q = 0; q < nch[cb]; q++) hold[total++] = z.kids[cb * MAXN + q];
                 }
                 int32_t cc = total / (MAXN / 2);
                 if (cc > MAXN - 1) cc = MAXN - 1;
@@ -1505,12 +1489,12 @@ struct Replica {
                     if (nb < 0) return;
                     for (int32_t q = 0; q < cnt; q++) {
                         int32_t ch = hold[read++];
-                        kid[nb * MAXN + q] = (int16_t)ch;
+                        z.kids[nb * MAXN + q] = (int16_t)ch;
                         npar[ch] = (int16_t)nb;
                     }
                     nch[nb] = (int8_t)cnt;
                     npar[nb] = (int16_t)parent;
-                    kid[parent * MAXN + ni] = (int16_t)nb;
+                    z.kids[parent * MAXN + ni] = (int16_t)nb;
                 }
                 nch[parent] = (int8_t)cc;
             }

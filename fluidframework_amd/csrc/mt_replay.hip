@@ -60,7 +60,6 @@ __device__ inline void copy_image(HT* dst, const HT* src) {
  * HBM-resident kernel (the rest of the hot image stays in HBM). */
 template <class HT>
 struct Skel {
-    int16_t kids[HT::N * 8];
     int16_t lorder[HT::N], lpos[HT::N], nparent[HT::N];
     int8_t nchild[HT::N], nlevel[HT::N], nscour[HT::N];
     int32_t hseq[HT::H];
@@ -75,12 +74,10 @@ template <class HT>
 __device__ inline void skel_move(Skel<HT>& k, HT& z, bool in) {
     constexpr int N = HT::N, H = HT::H;
     if (in) {
-        wave_copy(k.kids, z.kids, N * 8);
         wave_copy(k.lorder, z.lorder, N), wave_copy(k.lpos, z.lpos, N), wave_copy(k.nparent, z.nparent, N);
         wave_copy(k.nchild, z.nchild, N), wave_copy(k.nlevel, z.nlevel, N), wave_copy(k.nscour, z.nscour, N);
         wave_copy(k.hseq, z.hseq, H), wave_copy(k.hrid, z.hrid, H), wave_copy(k.hgen, z.hgen, H);
     } else {
-        wave_copy(z.kids, k.kids, N * 8);
         wave_copy(z.lorder, k.lorder, N), wave_copy(z.lpos, k.lpos, N), wave_copy(z.nparent, k.nparent, N);
         wave_copy(z.nchild, k.nchild, N), wave_copy(z.nlevel, k.nlevel, N), wave_copy(z.nscour, k.nscour, N);
         wave_copy(z.hseq, k.hseq, H), wave_copy(z.hrid, k.hrid, H), wave_copy(z.hgen, k.hgen, H);
@@ -89,7 +86,7 @@ __device__ inline void skel_move(Skel<HT>& k, HT& z, bool in) {
 
 /* K1-K4 fused: the whole event stream of a document, one wave per document. LDS = true stages the
  * whole small-profile hot image in LDS; otherwise the image stays in HBM and only the skeleton and
- * the heap (Skel, 6.6 KB for the small profile: 24 documents per CU) are staged. */
+ * the heap (Skel, 3.5 KB for the small profile) are staged. */
 template <class HT, bool LDS, int MINW = 1>
 __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
@@ -119,12 +116,12 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
 #endif
         __syncthreads();
         copy_image(g, &hot);
-    } else if constexpr (sizeof(Skel<HT>) <= 8192) {
+    } else if constexpr (sizeof(Skel<HT>) <= 4096) {
         __shared__ __attribute__((aligned(16))) Skel<HT> sk;
         skel_move(sk, *v.t, true);
         __syncthreads();
         Replica<WaveGPU, HT> r(v, WaveGPU());
-        r.kid = sk.kids, r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild, r.nlev = sk.nlevel;
+        r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild, r.nlev = sk.nlevel;
         r.nsc = sk.nscour, r.hsq = sk.hseq, r.hrd = sk.hrid, r.hgn = sk.hgen;
         r.replay(p);
         r.commit();
@@ -226,6 +223,7 @@ struct mt_engine {
     int64_t ndocs;
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
+    int waves = 6;    /* occupancy target of the HBM-resident kernel (MT_REPLAY_WAVES=6|7|8) */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
@@ -304,6 +302,8 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->ndocs = ndocs;
     const char* g = getenv("MT_REPLAY_LDS");
     e->lds = g && g[0] == '1';
+    const char* wv = getenv("MT_REPLAY_WAVES");
+    e->waves = wv ? atoi(wv) : 6;
     e->profile = prof;
     if (hipSetDevice(device) != hipSuccess) {
         delete e;
@@ -449,11 +449,14 @@ int32_t mt_engine_run(mt_engine* e) {
              * for 6 waves per SIMD, so 6,144 documents are in flight (24 per CU): at one wavefront per
              * document the replay is bound by the latency of its dependent accesses, and occupancy
              * hides more of it than full LDS residency (4 documents per CU) saves; 6 beats 7 and 8
-             * because the register cap of 8 waves spills (tools/gpu_occupancy.sh, measured before the
-             * kids array joined the LDS skeleton, which now caps the kernel at 24 workgroups per CU).
+             * because the register cap of 8 waves spills (tools/gpu_occupancy.sh).
              * MT_REPLAY_LDS=1 selects the fully LDS-staged form. */
             if (e->lds)
                 launch(k_replay<HT, true>);
+            else if (e->waves == 8)
+                launch(k_replay<HT, false, 8>);
+            else if (e->waves == 7)
+                launch(k_replay<HT, false, 7>);
             else
                 launch(k_replay<HT, false, 6>);
         } else {

@@ -8,4 +8,5 @@ run() {  # name env...
   python3 -c "import json; d = json.load(open('gpurun_out/occ_$name.json')); print('$name', round(d['value'] / 1e6, 2), 'Mops/s', round(d['ms_per_step'], 1), 'ms')"
 }
 run hbm6 MT_REPLAY_LDS=0
-run lds MT_REPLAY_LDS=1
+run hbm8 MT_REPLAY_WAVES=8
+run hbm7 MT_REPLAY_WAVES=7
