@@ -7,7 +7,11 @@ per doc) is applied on the GPU. Inputs are resident in HBM before the timed regi
 shard across ranks with no data-path collective ("scaling": "weak": each rank replays its own
 65,536 documents); RCCL is used once, after timing, to all-gather per-document digests.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--docs D] [--ops-per-doc O]
+`--config 5` instead measures BASELINE.json's config 5 (SharedMatrix PermutationVector replay:
+16,384 matrices x 2 vectors = 32,768 replicas, annotate-heavy PermutationSegment ops); the
+default (the line the driver records) is config 3.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--docs D] [--ops-per-doc O] [--config 3|5]
 """
 from __future__ import annotations
 
@@ -23,6 +27,13 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
+WORKLOADS = {
+    3: "config3: docs x {ops} sequenced msgs, 8 clients, lag<=64, local-pending replica",
+    5: "config5: SharedMatrix rows+cols PermutationVector replicas x {ops} sequenced msgs each, "
+       "8 clients, lag<=64, local-pending, 50% annotate",
+}
+
+
 def log(msg: str) -> None:
     import resource
     rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6
@@ -34,7 +45,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--docs", type=int, default=65536, help="documents per rank")
+    ap.add_argument("--config", type=int, default=3, choices=(3, 5))
+    ap.add_argument("--docs", type=int, default=0, help="documents per rank (default 65536; config 5: 32768)")
     ap.add_argument("--ops-per-doc", type=int, default=4096, help="sequenced messages per document")
     ap.add_argument("--cpu-sample-docs", type=int, default=8192)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -58,15 +70,17 @@ def main() -> None:
         dist.init_process_group("nccl")
     device = local_rank
 
-    # ---- synthetic workload (config 3), this rank's shard of documents ----
-    w = gen.config3(args.ops_per_doc)
+    # ---- synthetic workload (config 3 or 5), this rank's shard of documents ----
+    if args.docs <= 0:
+        args.docs = 65536 if args.config == 3 else 32768
+    w = gen.config3(args.ops_per_doc) if args.config == 3 else gen.config5(args.ops_per_doc)
     t0 = time.time()
     doc_base, ndocs = shard.doc_range(rank, args.docs)
     batch = gen.generate(w, ndocs, doc_base=doc_base, threads=args.cpu_threads)
     log(f"rank {rank}: generated {args.docs} docs, {batch.nops} events in {time.time() - t0:.1f}s")
     local_events = int(((batch.ops["kind"] & 0x80) != 0).sum())
 
-    eng = Engine(args.docs, device=device, **default_caps(args.ops_per_doc))
+    eng = Engine(args.docs, device=device, **default_caps(args.ops_per_doc, config=args.config))
     log("engine created")
     eng.start_collab(batch.local_long_id)
     eng.submit(batch)  # HtoD once: inputs are resident in HBM for every step
@@ -144,7 +158,7 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (mt_gen: splitmix64(0x5EED0000+doc) xoshiro256**)",
-            "config": {"workload": "config3: docs x 4096 sequenced msgs, 8 clients, lag<=64, local-pending replica",
+            "config": {"workload": WORKLOADS[args.config].format(ops=args.ops_per_doc),
                        "docs_per_gpu": args.docs, "ops_per_doc": args.ops_per_doc,
                        "local_edits_per_gpu": local_events, "parallelism": f"docs sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -65,6 +65,8 @@ enum : uint8_t {
     RF_OVL = 16, /* removedClientOverlap is non-empty (its list lives in the cold row) */
     RF_NLK = 32, /* RF_NL is known: a cache of the text's last unit, so zamboni rarely reads it */
     RF_NL = 64,  /* the text ends with "\n" (textSegment.ts:64 canAppend) */
+    RF_PERM = 128, /* PermutationSegment (permutationvector.ts:36-122): no text, handle unallocated */
+    RF_NOTEXT = RF_MARKER | RF_PERM,
 };
 
 /* runtime capacities that are not part of the LDS image */
@@ -145,6 +147,7 @@ struct HotT {
  * node high-water of config-3 documents has a tail reaching ~180 nodes) and larger
  * global-memory profiles. */
 typedef HotT<192> HotSmall;
+typedef HotT<640> HotMat; /* config 5: PermutationVector replicas peak at ~540 nodes */
 typedef HotT<2048> HotMid;
 typedef HotT<16384> HotBig;
 
@@ -756,7 +759,7 @@ struct Replica {
         int32_t T = h.nleaf * MAXN;
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
-            if (s < 0 || (z.flags[s] & RF_MARKER) || cold(s).gc == ep) continue;
+            if (s < 0 || (z.flags[s] & RF_NOTEXT) || cold(s).gc == ep) continue;
             int32_t L = z.len[s];
             arena_copy(dst + top, src + cold(s).toff, L);
             cold(s).toff = (uint32_t)top;
@@ -1114,6 +1117,8 @@ struct Replica {
     /* canAppend (textSegment.ts:63-68) */
     MT_HD bool can_append(int32_t a, int32_t b) {
         MT_PROF_SCOPE(PH_CAND);
+        /* PermutationSegment.canAppend (permutationvector.ts:87-93): both handles unallocated */
+        if ((z.flags[a] | z.flags[b]) & RF_PERM) return (z.flags[a] & z.flags[b] & RF_PERM) != 0;
         if (z.flags[a] & RF_MARKER) return false;
         if (ends_nl(a, z.len[a])) return false;
         if (z.flags[b] & RF_MARKER) return false;
@@ -1132,6 +1137,10 @@ struct Replica {
     MT_HD void append_text(int32_t a, int32_t b) {
         MT_PROF_SCOPE(PH_APPEND);
         int32_t La = z.len[a], Lb = z.len[b];
+        if (z.flags[a] & RF_PERM) { /* PermutationSegment.append (permutationvector.ts:95-101) */
+            z.len[a] = La + Lb;
+            return;
+        }
         uint16_t* base = arena_base(h.arenaSide);
         if ((int32_t)cold(a).toff + La == h.arenaTop && h.arenaTop + Lb <= d.caps.acap) {
             int32_t off = arena_alloc(Lb);
@@ -1173,9 +1182,10 @@ struct Replica {
                     if (z.seq[s] <= minSeq) {
                         /* hot predicates first; the cold ones (props values, trailing newline) are
                          * only read for a candidate pair. Same conjunction as mergeTree.ts:1355-1360. */
-                        bool ok = prev >= 0 && local_len(s) > 0 && !(z.flags[prev] & RF_MARKER) &&
-                                  !(z.flags[s] & RF_MARKER) &&
-                                  (z.len[prev] <= GRANULARITY || z.len[s] <= GRANULARITY) &&
+                        bool ok = prev >= 0 && local_len(s) > 0 &&
+                                  ((z.flags[prev] & z.flags[s] & RF_PERM) ||
+                                   (!((z.flags[prev] | z.flags[s]) & RF_NOTEXT) &&
+                                    (z.len[prev] <= GRANULARITY || z.len[s] <= GRANULARITY))) &&
                                   ((z.flags[prev] ^ z.flags[s]) & RF_PROPS) == 0 && match_props(prev, s) &&
                                   can_append(prev, s);
                         if (ok) {
@@ -1262,12 +1272,13 @@ struct Replica {
             int32_t lk = w.bcast(r.len, k);
             int32_t fk = w.bcast(fl, k);
             bool ok = false;
-            if (!(prevFl & RF_MARKER) && !(fk & RF_MARKER) && (prevLen <= GRANULARITY || lk <= GRANULARITY) &&
+            bool permPair = (prevFl & fk & RF_PERM) != 0;
+            if ((permPair || (!((prevFl | fk) & RF_NOTEXT) && (prevLen <= GRANULARITY || lk <= GRANULARITY))) &&
                 ((prevFl ^ fk) & RF_PROPS) == 0) {
                 int32_t sp = w.bcast(n, prev) * MAXN + (prev & (MAXN - 1));
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
                 ok = match_props(sp, sk);
-                if (ok) {
+                if (ok && !permPair) {
                     bool nl = ends_nl(sp, prevLen); /* caches RF_NLK/RF_NL in z.flags[sp] */
                     prevFl = (prevFl & ~(RF_NLK | RF_NL)) | RF_NLK | (nl ? RF_NL : 0);
                     ok = !nl;
@@ -1621,11 +1632,12 @@ struct Replica {
         bool hasL = seq == UNASSIGNED_SEQ;
         int32_t localSeq = hasL ? ++h.localSeq : 0;
         bool marker = op.seg_kind == MT_SEG_MARKER;
+        bool perm = op.seg_kind == MT_SEG_PERM; /* PermutationSegment(length) (permutationvector.ts:47-51) */
         int32_t L = marker ? 1 : op.text_len;
         if (L <= 0) ensure_boundary(pos, refSeq, client); /* the split still happens (2004) */
         if (L > 0) {
             int32_t off = 0;
-            if (!marker) {
+            if (!marker && !perm) {
                 MT_PROF_SCOPE(PH_TEXT);
                 off = arena_alloc(L);
                 if (off < 0) return;
@@ -1644,7 +1656,7 @@ struct Replica {
             cold(s).lrseq = 0;
             z.cli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
             z.rcli[s] = 0;
-            int32_t fl = (marker ? RF_MARKER : 0) | (hasL ? RF_LSEQ : 0);
+            int32_t fl = (marker ? RF_MARKER : 0) | (perm ? RF_PERM : 0) | (hasL ? RF_LSEQ : 0);
             z.ng[s] = 0;
             cold(s).prw = 0;
             cold(s).ovl = 0;
@@ -1654,6 +1666,8 @@ struct Replica {
             h.localLen += L;
             if (marker) {
                 cold(s).toff = (uint32_t)op.pos2;
+            } else if (perm) {
+                cold(s).toff = 0;
             } else {
                 MT_PROF_SCOPE(PH_TEXT);
                 cold(s).toff = (uint32_t)off;
@@ -1998,7 +2012,7 @@ struct Replica {
         const uint16_t* base = arena_base(h.arenaSide);
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
-            if (s < 0 || (z.flags[s] & RF_MARKER)) continue;
+            if (s < 0 || (z.flags[s] & RF_NOTEXT)) continue;
             int32_t v = vis(s, refSeq, client);
             if (v <= 0) continue;
             if (out) {
@@ -2061,7 +2075,7 @@ struct Replica {
             if (fl & RF_PROPS)
                 for (int k = 0; k < NKEYS; k++)
                     if (cold(s).pv[k]) np++;
-            uint8_t b4[4] = {(uint8_t)((fl & RF_MARKER) ? MT_SEG_MARKER : MT_SEG_TEXT),
+            uint8_t b4[4] = {(uint8_t)((fl & RF_MARKER) ? MT_SEG_MARKER : (fl & RF_PERM) ? MT_SEG_PERM : MT_SEG_TEXT),
                              (uint8_t)(((fl & RF_PROPS) ? MT_DF_HAS_PROPS : 0) | (rem ? MT_DF_REMOVED : 0) |
                                        ((fl & RF_LSEQ) ? MT_DF_LSEQ : 0) | ((fl & RF_LRSEQ) ? MT_DF_LRSEQ : 0)),
                              (uint8_t)nov, z.ng[s]};
@@ -2096,7 +2110,7 @@ struct Replica {
                 put_bytes(o, kv2, 4);
                 last = bk;
             }
-            if (!(fl & RF_MARKER)) put_bytes(o, base + cold(s).toff, 2 * (int64_t)z.len[s]);
+            if (!(fl & RF_NOTEXT)) put_bytes(o, base + cold(s).toff, 2 * (int64_t)z.len[s]);
         }
     }
     MT_HD static uint64_t fnv(const uint8_t* p, int64_t n) {

@@ -23,6 +23,7 @@ struct mth_store {
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
+    Store<HotMat> s3;
     uint8_t* mem;
 };
 
@@ -32,6 +33,11 @@ static auto with_replica(mth_store* s, int64_t d, F&& f) {
     /* every call ends with commit(): the replica's register header goes back to the image */
     if (s->profile == 0) {
         Replica<WaveHost, HotSmall> r(s->s0.doc(d), WaveHost());
+        auto res = f(r);
+        r.commit();
+        return res;
+    } else if (s->profile == 3) {
+        Replica<WaveHost, HotMat> r(s->s3.doc(d), WaveHost());
         auto res = f(r);
         r.commit();
         return res;
@@ -59,13 +65,14 @@ mth_store* mth_create(int64_t ndocs, const int32_t* caps6) {
     s->ndocs = ndocs;
     int64_t bytes = prof == 0 ? store_layout(s->s0, k, ndocs)
                   : prof == 1 ? store_layout(s->s1, k, ndocs)
+                  : prof == 3 ? store_layout(s->s3, k, ndocs)
                               : store_layout(s->s2, k, ndocs);
     s->mem = (uint8_t*)calloc(1, (size_t)bytes);
     if (!s->mem) {
         free(s);
         return nullptr;
     }
-    s->s0.base = s->s1.base = s->s2.base = s->mem;
+    s->s0.base = s->s1.base = s->s2.base = s->s3.base = s->mem;
     for (int64_t d = 0; d < ndocs; d++) with_replica(s, d, [](auto& r) { r.init(); return 0; });
     return s;
 }

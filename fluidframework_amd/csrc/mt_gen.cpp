@@ -13,6 +13,11 @@
  *                  refSeq = MSN = seq - 1.
  *   MTG_LAGGED    (config 3): replica = long id 1 with local edits acked up to ack_lag later;
  *                  remote refSeq lag U{0..max_lag}; MSN = min over clients' last refSeq.
+ *   MTG_MATRIX    (config 5): one SharedMatrix = two PermutationVector replicas (rows, cols)
+ *                  fed from ONE sequenced stream: every message targets one vector
+ *                  (SharedMatrix.processCore, matrix.ts:568-578), so each vector sees the
+ *                  matrix's sequence numbers with gaps, and refSeq/MSN are matrix-global.
+ *                  Doc 2m is matrix m's rows vector, doc 2m+1 its cols vector.
  * Both take an op mix, insert/remove length ranges and optional coalescing defeaters
  * (distinct insert props, trailing newlines) used by the large-doc config.
  */
@@ -143,7 +148,13 @@ static void gen_op(const mtg_params* P, rng_t* r, Model<HT>* m, int32_t refSeq, 
     else
         kind = MT_OP_ANNOTATE;
     e->kind = (uint8_t)kind;
-    if (kind == MT_OP_INSERT) {
+    if (kind == MT_OP_INSERT && P->perm) { /* PermutationVector.insert(start, length) (147-151) */
+        e->pos1 = uni(r, 0, len);
+        e->seg_kind = MT_SEG_PERM;
+        e->text_off = 0;
+        e->text_len = (uint16_t)uni(r, 1, P->max_ins_len);
+        if (P->distinct_props) e->props = (uint16_t)(1 + ANN_RECORDS + (insert_index % 4096));
+    } else if (kind == MT_OP_INSERT) {
         e->pos1 = uni(r, 0, len);
         int tl = uni(r, 1, P->max_ins_len);
         if (o->ntext + tl > o->tcap) {
@@ -274,8 +285,117 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
     if (m.r->h.err) o->overflow = 2;
     model_free(&m);
 }
+/* MTG_MATRIX: matrix `doc >> 1`, emitting only the events of vector `doc & 1` (the other
+ * vector's model is still driven, so both docs of a matrix draw the same random stream). */
+template <class HT>
+static void gen_matrix_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {
+    rng_t r;
+    seed(&r, P->seed_base + (uint64_t)(doc >> 1));
+    int which = (int)(doc & 1);
+    int nclients = P->nclients < 2 ? 2 : P->nclients;
+    if (nclients > 32) nclients = 32;
+    const int me = 1;
+    Model<HT> m[2];
+    Out scratch = {(mt_op_rec*)malloc(sizeof(mt_op_rec) * o->cap), 0, o->cap, NULL, 0, 0, 0};
+    Out* out[2];
+    out[which] = o;
+    out[which ^ 1] = &scratch;
+    for (int t = 0; t < 2; t++) {
+        model_init(&m[t], P, me);
+        if (!m[t].ok || !scratch.ops) {
+            o->overflow = 1;
+            return;
+        }
+        m[t].props = props;
+        m[t].kv = kv;
+        m[t].text = o->text;
+    }
+    Pending* q = (Pending*)malloc(sizeof(Pending) * (2 * P->ops_per_doc + 16));
+    int32_t lastRef[32] = {0};
+    int insert_index[2] = {0, 0};
+    int32_t nseq[2] = {0, 0}; /* sequenced messages per vector */
+    int32_t seq = 0, msn = 0, lastTarget = 0;
+    int qh = 0, qn = 0;
+    while ((nseq[0] < P->ops_per_doc || nseq[1] < P->ops_per_doc) && !o->overflow && !scratch.overflow &&
+           !m[0].r->h.err && !m[1].r->h.err) {
+        int t = uni(&r, 0, 1);
+        if (nseq[t] >= P->ops_per_doc) t ^= 1;
+        /* 1. a local edit of vector t (PermutationVector.insert/remove, permutationvector.ts:147-157) */
+        if (P->local_pct && uni(&r, 0, 99) < P->local_pct && qn < 4000) {
+            mt_op_rec* e = emit(out[t]);
+            if (!e) break;
+            int32_t cur = m[t].r->h.currentSeq;
+            gen_op(P, &r, &m[t], cur, me, 1, out[t], e, insert_index[t]);
+            e->kind |= MT_OPF_LOCAL;
+            e->client = (uint16_t)me;
+            e->seq = -1;
+            e->ref_seq = cur;
+            if ((e->kind & MT_OP_KIND_MASK) == MT_OP_INSERT) insert_index[t]++;
+            m_apply(&m[t], e);
+            int32_t target = seq + uni(&r, 1, P->ack_lag > 0 ? P->ack_lag : 1);
+            if (target <= lastTarget) target = lastTarget + 1;
+            lastTarget = target;
+            Pending pe;
+            pe.op = *e;
+            pe.op.kind &= (uint8_t)~MT_OPF_LOCAL;
+            pe.op.ref_seq = seq; /* the matrix-global refSeq the runtime stamps */
+            pe.target = target * 2 + t;
+            q[qh + qn++] = pe;
+            continue;
+        }
+        /* 2. the next sequenced message of the matrix: our own op (ack) when due, else remote */
+        seq++;
+        if (qn > 0 && (q[qh].target >> 1) <= seq) {
+            Pending pe = q[qh++];
+            qn--;
+            int tt = pe.target & 1;
+            mt_op_rec* e = emit(out[tt]);
+            if (!e) break;
+            if (pe.op.ref_seq > lastRef[me]) lastRef[me] = pe.op.ref_seq;
+            int32_t mn = INT32_MAX;
+            for (int k = 0; k < nclients; k++)
+                if (lastRef[k] < mn) mn = lastRef[k];
+            if (mn > msn) msn = mn;
+            *e = pe.op;
+            e->seq = seq;
+            e->min_seq = msn;
+            m_apply(&m[tt], e);
+            nseq[tt]++;
+        } else {
+            mt_op_rec* e = emit(out[t]);
+            if (!e) break;
+            int client = uni(&r, 0, nclients - 2);
+            if (client >= me) client++;
+            int32_t ref = (seq - 1) - uni(&r, 0, P->max_lag);
+            if (ref < lastRef[client]) ref = lastRef[client];
+            if (ref < msn) ref = msn;
+            lastRef[client] = ref;
+            int32_t mn = INT32_MAX;
+            for (int k = 0; k < nclients; k++)
+                if (lastRef[k] < mn) mn = lastRef[k];
+            if (mn > msn) msn = mn;
+            gen_op(P, &r, &m[t], ref, client, 0, out[t], e, insert_index[t]);
+            e->client = (uint16_t)client;
+            e->seq = seq;
+            e->ref_seq = ref;
+            e->min_seq = msn;
+            if (e->kind == MT_OP_INSERT) insert_index[t]++;
+            m_apply(&m[t], e);
+            nseq[t]++;
+        }
+    }
+    if (scratch.overflow) o->overflow = 1;
+    if (m[0].r->h.err || m[1].r->h.err) o->overflow = 2;
+    free(q);
+    free(scratch.ops);
+    model_free(&m[0]);
+    model_free(&m[1]);
+}
+
 static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {
-    if (P->model_ncap > HotMid::N)
+    if (P->mode == MTG_MATRIX)
+        gen_matrix_t<HotMid>(P, doc, o, props, kv);
+    else if (P->model_ncap > HotMid::N)
         gen_doc_t<HotBig>(P, doc, o, props, kv);
     else
         gen_doc_t<HotMid>(P, doc, o, props, kv);

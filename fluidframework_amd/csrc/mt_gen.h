@@ -6,9 +6,9 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
-enum { MTG_OBSERVER = 2, MTG_LAGGED = 3 };
+enum { MTG_OBSERVER = 2, MTG_LAGGED = 3, MTG_MATRIX = 5 };
 typedef struct mtg_params {
-    int32_t mode;          /* MTG_OBSERVER / MTG_LAGGED                                  */
+    int32_t mode;          /* MTG_OBSERVER / MTG_LAGGED / MTG_MATRIX                     */
     int32_t ops_per_doc;   /* sequenced messages per document                             */
     int32_t nclients;      /* clients per document, replica included (<= 32)              */
     int32_t max_lag;       /* remote refSeq lag upper bound (MTG_LAGGED)                  */
@@ -21,6 +21,7 @@ typedef struct mtg_params {
     int32_t newline_pct;   /* % of inserts whose last unit is '\n' (defeats coalescing)    */
     int32_t model_ncap;    /* model replica node capacity (0: default 2048)                */
     int32_t model_acap;    /* model replica text arena half-size (0: default 128K units)  */
+    int32_t perm;          /* inserts are PermutationSegments of U{1..max_ins_len} rows    */
     uint64_t seed_base;    /* doc d uses splitmix64 seed seed_base + d                     */
 } mtg_params;
 int mtg_generate(const mtg_params* P, int64_t doc_base, int64_t ndocs, int64_t op_stride, int64_t text_stride,

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
 #endif
         __syncthreads();
         copy_image(g, &hot);
-    } else if constexpr (sizeof(Skel<HT>) <= 4096) {
+    } else if constexpr (sizeof(Skel<HT>) <= 12288) {
         __shared__ __attribute__((aligned(16))) Skel<HT> sk;
         skel_move(sk, *v.t, true);
         __syncthreads();
@@ -227,6 +227,7 @@ struct mt_engine {
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
+    Store<HotMat> s3;
     void* mem = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -243,6 +244,7 @@ template <class F>
 static int32_t with_store(mt_engine* e, F&& f) {
     if (e->profile == 0) return f(e->s0);
     if (e->profile == 1) return f(e->s1);
+    if (e->profile == 3) return f(e->s3);
     return f(e->s2);
 }
 
@@ -311,12 +313,13 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     }
     int64_t bytes = prof == 0 ? store_layout(e->s0, k, ndocs)
                   : prof == 1 ? store_layout(e->s1, k, ndocs)
+                  : prof == 3 ? store_layout(e->s3, k, ndocs)
                               : store_layout(e->s2, k, ndocs);
     if (hipMalloc(&e->mem, (size_t)bytes) != hipSuccess) {
         delete e;
         return MT_E_NOMEM;
     }
-    e->s0.base = e->s1.base = e->s2.base = (uint8_t*)e->mem;
+    e->s0.base = e->s1.base = e->s2.base = e->s3.base = (uint8_t*)e->mem;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
         mt_engine_destroy(e);
@@ -459,6 +462,9 @@ int32_t mt_engine_run(mt_engine* e) {
                 launch(k_replay<HT, false, 7>);
             else
                 launch(k_replay<HT, false, 6>);
+        } else if constexpr (std::is_same_v<HT, HotMat>) {
+            /* skeleton + heap in LDS (10.7 KB): LDS caps residency at 14 documents per CU */
+            launch(k_replay<HT, false, 4>);
         } else {
             launch(k_replay<HT, false>);
         }

@@ -62,9 +62,10 @@ inline int64_t store_layout(Store<HT>& st, const Caps& caps, int64_t ndocs) {
 
 inline bool caps_valid(const Caps& k) { return k.acap >= 16 && k.mcap >= 4 && k.gcap >= 1; }
 
-/* profiles: 0 = HotSmall (LDS-resident on the GPU), 1 = HotMid, 2 = HotBig */
+/* profiles: 0 = HotSmall (LDS-resident on the GPU), 3 = HotMat, 1 = HotMid, 2 = HotBig */
 inline int profile_for(int32_t ncap) {
     if (ncap <= HotSmall::N) return 0;
+    if (ncap <= HotMat::N) return 3;
     if (ncap <= HotMid::N) return 1;
     if (ncap <= HotBig::N) return 2;
     return -1;

@@ -72,8 +72,13 @@ def _p(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def default_caps(ops_per_doc: int) -> dict:
+def default_caps(ops_per_doc: int, config: int = 3) -> dict:
     """Capacities sized for the synthetic configs (high-water marks measured with the oracle)."""
+    if config == 5 and ops_per_doc <= 5_000:
+        # PermutationVector replicas (HotMat: 640 nodes / 5120 slots; peak ~540 nodes at 4,096)
+        return dict(ncap=640, hcap=1024, acap=1 << 4, mcap=1024, gcap=1024, ccap=64)
+    if config == 5:
+        return dict(ncap=2048, hcap=4096, acap=1 << 4, mcap=2048, gcap=1024, ccap=64)
     if ops_per_doc <= 20_000:
         # LDS-resident profile (HotSmall: 192 nodes / 1536 slots)
         return dict(ncap=192, hcap=256, acap=1 << 16, mcap=1024, gcap=1024, ccap=64)

@@ -10,14 +10,14 @@ import numpy as np
 from . import native
 from . import oplog as ol
 
-MTG_OBSERVER, MTG_LAGGED = 2, 3
+MTG_OBSERVER, MTG_LAGGED, MTG_MATRIX = 2, 3, 5
 
 
 class _Params(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "mode", "ops_per_doc", "nclients", "max_lag", "local_pct", "ack_lag", "pct_insert",
         "pct_remove", "max_ins_len", "max_rem_len", "distinct_props", "newline_pct", "model_ncap",
-        "model_acap")] + [
+        "model_acap", "perm")] + [
         ("seed_base", ctypes.c_uint64)]
 
 
@@ -37,6 +37,7 @@ class Workload:
     newline_pct: int = 0
     model_ncap: int = 0
     model_acap: int = 0
+    perm: int = 0
     seed_base: int = 0x5EED0000
 
 
@@ -55,6 +56,14 @@ def config4(ops_per_doc: int = 1_000_000) -> Workload:
     """256 large docs, lag 64, 70/25/5, coalescing defeated by distinct props + newlines."""
     return Workload(MTG_LAGGED, ops_per_doc, max_lag=64, local_pct=0, pct_insert=70, pct_remove=25,
                     distinct_props=1, newline_pct=25, model_ncap=32000, model_acap=1 << 22)
+
+
+def config5(ops_per_doc: int = 4_096) -> Workload:
+    """SharedMatrix PermutationVector replay: docs 2m / 2m+1 = rows / cols vectors of matrix m,
+    one sequenced stream per matrix, PermutationSegment inserts of U{1..8} rows, removes of
+    U{1..4}, 50% annotate; 8 clients, lag <= 64, local-pending replica."""
+    return Workload(MTG_MATRIX, ops_per_doc, max_lag=64, local_pct=12, ack_lag=64, pct_insert=32,
+                    pct_remove=18, max_ins_len=8, max_rem_len=4, perm=1)
 
 
 _LIB = None

@@ -43,6 +43,8 @@ enum {
 enum {
     MT_SEG_TEXT = 0,   /* TextSegment   (textSegment.ts:16-112)            */
     MT_SEG_MARKER = 1, /* Marker, length 1 (mergeTree.ts:668-832)          */
+    MT_SEG_PERM = 2,   /* PermutationSegment (matrix permutationvector.ts:36-122): length =
+                          text_len, no text, handle unallocated; any two such rows can append */
 };
 
 /* combining ops for annotate (ops.ts ICombiningOp); only none and "rewrite" are supported */
@@ -61,7 +63,7 @@ typedef struct mt_op_rec {
     int32_t pos1;      /* insert position / range start                                      */
     int32_t pos2;      /* range end (exclusive); insert of a marker: its refType             */
     uint32_t text_off; /* insert text: offset in UTF-16 units into the doc text pool         */
-    uint16_t text_len; /* insert text: length in UTF-16 units                                */
+    uint16_t text_len; /* insert text: length in UTF-16 units; MT_SEG_PERM: the row count     */
     uint16_t props;    /* 0 = none, else 1-based index into the doc props table              */
 } mt_op_rec;
 

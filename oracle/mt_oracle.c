@@ -282,6 +282,9 @@ static Seg* newSeg(mto_client* c, int kind, const uint16_t* text, int len, int r
         s->text = xmalloc(sizeof(uint16_t) * s->tcap);
         if (len) memcpy(s->text, text, sizeof(uint16_t) * len);
         s->hdr.cachedLength = len; /* textSegment.ts:43-46 */
+    } else if (kind == MT_SEG_PERM) {
+        /* PermutationSegment(length, start = Handle.unallocated) (permutationvector.ts:47-51) */
+        s->hdr.cachedLength = len;
     } else {
         s->hdr.cachedLength = 1; /* Marker constructor (mergeTree.ts:685-688) */
     }
@@ -889,8 +892,13 @@ static int matchProperties(const Seg* a, const Seg* b) {
     return b->hasProps ? 0 : 1;
 }
 
-/* TextSegment.canAppend (textSegment.ts:63-68); Marker/others: false */
+/* TextSegment.canAppend (textSegment.ts:63-68); Marker: false (BaseSegment.canAppend);
+ * PermutationSegment.canAppend (permutationvector.ts:87-93): this.start === unallocated ?
+ * other.start === unallocated : contiguous handles. Handles are never allocated on the replay
+ * path (getAllocatedHandle is a SharedMatrix cell-op action), so two PermutationSegments always
+ * append; a non-permutation segment has start === undefined and never matches. */
 static int canAppend(const Seg* a, const Seg* b) {
+    if (a->kind == MT_SEG_PERM) return b->kind == MT_SEG_PERM;
     if (a->kind != MT_SEG_TEXT) return 0;
     int len = a->hdr.cachedLength;
     if (len > 0 && a->text[len - 1] == '\n') return 0;
@@ -900,6 +908,10 @@ static int canAppend(const Seg* a, const Seg* b) {
 /* TextSegment.append (textSegment.ts:74-85) */
 static void segAppend(Seg* a, const Seg* b) {
     int n = a->hdr.cachedLength + b->hdr.cachedLength;
+    if (a->kind == MT_SEG_PERM) { /* PermutationSegment.append (permutationvector.ts:95-101) */
+        a->hdr.cachedLength = n;
+        return;
+    }
     if (n > a->tcap) {
         int cap = a->tcap * 2;
         if (cap < n) cap = n;
@@ -926,9 +938,12 @@ static void segGroupsEnqueue(Seg* s, Group* g) {
 /* BaseSegment.splitAt (mergeTree.ts:523-567) + TextSegment.createSplitSegmentAt (103-111) */
 static Seg* splitAt(mto_client* c, Seg* s, int pos) {
     if (!(pos > 0)) return NULL;
-    if (s->kind != MT_SEG_TEXT) return NULL; /* Marker.createSplitSegmentAt -> undefined */
+    if (s->kind == MT_SEG_MARKER) return NULL; /* Marker.createSplitSegmentAt -> undefined */
     int len = s->hdr.cachedLength;
-    Seg* r = newSeg(c, MT_SEG_TEXT, s->text + pos, len - pos, 0);
+    /* PermutationSegment.createSplitSegmentAt (permutationvector.ts:103-114): unallocated stays
+     * unallocated */
+    Seg* r = s->kind == MT_SEG_PERM ? newSeg(c, MT_SEG_PERM, NULL, len - pos, 0)
+                                    : newSeg(c, MT_SEG_TEXT, s->text + pos, len - pos, 0);
     s->hdr.cachedLength = pos;
     /* propertyManager.copyTo (segmentPropertiesManager.ts:113-128) */
     if (s->hasProps) {
@@ -1622,6 +1637,8 @@ static Seg* specToSegment(mto_client* c, const mt_op_rec* op) { /* textSegment.t
     Seg* s;
     if (op->seg_kind == MT_SEG_MARKER)
         s = newSeg(c, MT_SEG_MARKER, NULL, 0, op->pos2);
+    else if (op->seg_kind == MT_SEG_PERM) /* PermutationVector.insert (permutationvector.ts:147-151) */
+        s = newSeg(c, MT_SEG_PERM, NULL, op->text_len, 0);
     else
         s = newSeg(c, MT_SEG_TEXT, c->textPool + op->text_off, op->text_len, 0);
     if (op->props) { /* TextSegment.make(text, props) -> addProperties(props) (no collab window) */

@@ -10,16 +10,20 @@ import core_host
 import oracle_client as oc
 
 
-@pytest.mark.parametrize("name,w,ndocs", [
-    ("config2", gen.config2(3000), 24),
-    ("config3", gen.config3(2048), 48),
-    ("config4", gen.config4(4000), 3),
+CAPS = (2048, 4096, 1 << 17, 8192, 1024, 64)
+
+
+@pytest.mark.parametrize("name,w,ndocs,caps", [
+    ("config2", gen.config2(3000), 24, CAPS),
+    ("config3", gen.config3(2048), 48, CAPS),
+    ("config4", gen.config4(4000), 3, CAPS),
+    # PermutationVector replicas in the 640-node profile the engine uses for config 5
+    ("config5", gen.config5(4096), 32, (640, 1024, 16, 1024, 1024, 64)),
 ])
-def test_host_core_matches_oracle(name, w, ndocs):
+def test_host_core_matches_oracle(name, w, ndocs, caps):
     b = gen.generate(w, ndocs)
     _, odig, oerr = oc.replay_batch(b, threads=8)
     assert (oerr == 0).all()
-    caps = (2048, 4096, 1 << 17, 8192, 1024, 64)
     hdig, herr, st = core_host.replay_batch(b, caps)
     assert (herr == 0).all(), herr
     bad = np.nonzero(hdig != odig)[0]

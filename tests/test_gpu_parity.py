@@ -93,3 +93,19 @@ def test_large_doc_props_newlines():
     w = gen.config4(6000)
     b = gen.generate(w, 4)
     _check_batch(b, 6000, ndump=2, ncap=4096, hcap=8192, acap=1 << 17)
+
+
+def test_matrix_permutation_vectors_config5():
+    """Config 5: SharedMatrix rows/cols PermutationVector replicas (PermutationSegment rows,
+    annotate-heavy) in the 640-node profile; perspective lengths of remote clients agree too."""
+    from fluidframework_amd.engine import default_caps
+    b = gen.generate(gen.config5(4096), 64)
+    eng = _check_batch(b, 4096, **default_caps(4096, config=5))
+    for d in range(3):
+        ops, text, props, kv = b.doc(d)
+        c = oc.OracleClient()
+        c.start_collab(int(b.local_long_id[d]))
+        c.replay_arrays(ops, text, props, kv)
+        cur = c.current_seq
+        for k in (0, 3):
+            assert eng.get_length(d, cur - 5, k) == c.get_length_at(cur - 5, k)
