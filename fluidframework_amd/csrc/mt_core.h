@@ -119,17 +119,24 @@ struct HotT {
     static constexpr int H = N_ + 64; /* zamboni heap entries (config 3 peaks at 109) */
     static constexpr int C = C_;     /* clients */
     DocHdr h;
-    /* len is 0 in every slot that holds no row (rows always have len >= 1), so a scan needs no
-     * child count; the three int32 columns are read 4 slots at a time (16-byte LDS reads) */
-    alignas(16) int32_t len[S];
-    alignas(16) int32_t seq[S];
-    alignas(16) int32_t rseq[S];
+    /* The scan columns of one leaf's 8 slots share one 128-byte line (leaf-major SoA): a
+     * perspective scan that visits a leaf touches one cache line, not one line per column.
+     * len is 0 in every slot that holds no row (rows always have len >= 1), so a scan needs no
+     * child count; the int32 columns are read 4 slots at a time (16-byte reads). */
+    struct alignas(128) Leaf {
+        int32_t len[8], seq[8], rseq[8];
+        uint8_t cli[8], rcli[8], flags[8], ng[8];
+    };
+    Leaf lf[N];
+    MT_HD int32_t& len(int s) { return lf[s >> 3].len[s & 7]; }
+    MT_HD int32_t& seq(int s) { return lf[s >> 3].seq[s & 7]; }
+    MT_HD int32_t& rseq(int s) { return lf[s >> 3].rseq[s & 7]; }
+    MT_HD uint8_t& cli(int s) { return lf[s >> 3].cli[s & 7]; }
+    MT_HD uint8_t& rcli(int s) { return lf[s >> 3].rcli[s & 7]; }
+    MT_HD uint8_t& flags(int s) { return lf[s >> 3].flags[s & 7]; }
+    MT_HD uint8_t& ng(int s) { return lf[s >> 3].ng[s & 7]; }
     int16_t rid[S];   /* slot -> row id (stable identity of a segment; cold data index) */
     int16_t rleaf[S]; /* row id -> leaf node currently holding it */
-    alignas(4) uint8_t cli[S];
-    alignas(4) uint8_t rcli[S];
-    alignas(4) uint8_t flags[S];
-    alignas(4) uint8_t ng[S];
     uint8_t rgen[S]; /* row id -> generation, bumped when the id is freed */
     int16_t nparent[N], lorder[N], lpos[N];
     int16_t kids[N * 8];
@@ -157,8 +164,19 @@ struct alignas(16) I4 {
 struct alignas(4) B4 {
     uint8_t x[4];
 };
-MT_HD I4 ld4(const int32_t* p) { return *(const I4*)p; } /* p 16-byte aligned */
-MT_HD B4 ldb4(const uint8_t* p) { return *(const B4*)p; } /* p 4-byte aligned */
+/* 16-byte / 4-byte column reads. memcpy, not a pointer cast: the columns are members of the leaf
+ * line struct, and an I4/B4-typed load of them would be "no alias" for type-based alias analysis,
+ * letting the compiler move it above a store to the same slot. */
+MT_HD I4 ld4(const int32_t* p) { /* p 16-byte aligned */
+    I4 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 16), sizeof v);
+    return v;
+}
+MT_HD B4 ldb4(const uint8_t* p) { /* p 4-byte aligned */
+    B4 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), sizeof v);
+    return v;
+}
 
 /* Per-document view: the hot image (LDS or global) plus global cold/arena/log pointers. */
 template <class HT>
@@ -278,7 +296,7 @@ struct Replica {
         w.sync();
         for (int32_t b = 0; b < cnt; b += W::N) {
             int32_t i = b + w.lane();
-            if (i < cnt) z.len[s + i] = 0;
+            if (i < cnt) z.len(s + i) = 0;
         }
         w.sync();
     }
@@ -307,7 +325,14 @@ struct Replica {
             if (i < HT::S) {
                 d.frid[i] = (int16_t)(HT::S - 1 - i);
                 z.rgen[i] = 0;
-                z.len[i] = 0;
+                z.len(i) = 0;
+                z.seq(i) = 0;
+                z.rseq(i) = 0;
+                z.cli(i) = 0;
+                z.rcli(i) = 0;
+                z.flags(i) = 0;
+                z.ng(i) = 0;
+                z.rid[i] = 0;
             }
         }
         w.sync();
@@ -393,16 +418,16 @@ struct Replica {
     }
     /* nodeLength of a leaf (mergeTree.ts:1692-1732); local perspective -> localNetLength */
     MT_HD int32_t vis(int32_t s, int32_t refSeq, int32_t client) const {
-        int32_t L = z.len[s];
-        if (is_local(client)) return z.rseq[s] == NOREM ? L : 0;
-        int32_t c = z.cli[s] == LOCAL_CLIENT ? -1 : z.cli[s];
-        int32_t sq = z.seq[s];
+        int32_t L = z.len(s);
+        if (is_local(client)) return z.rseq(s) == NOREM ? L : 0;
+        int32_t c = z.cli(s) == LOCAL_CLIENT ? -1 : z.cli(s);
+        int32_t sq = z.seq(s);
         if (!(c == client || (sq != UNASSIGNED_SEQ && sq <= refSeq))) return 0;
-        int32_t rs = z.rseq[s];
+        int32_t rs = z.rseq(s);
         if (rs != NOREM) {
-            int32_t rc = z.rcli[s] == LOCAL_CLIENT ? -1 : z.rcli[s];
+            int32_t rc = z.rcli(s) == LOCAL_CLIENT ? -1 : z.rcli(s);
             if (rc == client) return 0;
-            if (z.flags[s] & RF_OVL) { /* cold read only for the rare overlapping remove */
+            if (z.flags(s) & RF_OVL) { /* cold read only for the rare overlapping remove */
                 uint64_t ov = cold(s).ovl;
                 for (int k = 0; k < NOVL; k++) {
                     uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
@@ -415,7 +440,7 @@ struct Replica {
         return L;
     }
     /* localNetLength (mergeTree.ts:1195-1206) */
-    MT_HD int32_t local_len(int32_t s) const { return z.rseq[s] == NOREM ? z.len[s] : 0; }
+    MT_HD int32_t local_len(int32_t s) const { return z.rseq(s) == NOREM ? z.len(s) : 0; }
 
     MT_HD int32_t slot_at(int32_t t) const { /* t = k*8+j over lorder; -1 if not a row */
         int32_t k = t >> 3, j = t & 7;
@@ -427,14 +452,14 @@ struct Replica {
     /* copy every column of row a to row b (same doc) */
     /* move row a's slot contents to slot b (hot columns + its cold row id) */
     MT_HD void copy_row(int32_t b, int32_t a) {
-        z.len[b] = z.len[a];
-        z.seq[b] = z.seq[a];
-        z.rseq[b] = z.rseq[a];
+        z.len(b) = z.len(a);
+        z.seq(b) = z.seq(a);
+        z.rseq(b) = z.rseq(a);
         z.rid[b] = z.rid[a];
-        z.cli[b] = z.cli[a];
-        z.rcli[b] = z.rcli[a];
-        z.flags[b] = z.flags[a];
-        z.ng[b] = z.ng[a];
+        z.cli(b) = z.cli(a);
+        z.rcli(b) = z.rcli(a);
+        z.flags(b) = z.flags(a);
+        z.ng(b) = z.ng(a);
     }
     /* a row's slot contents held in registers */
     struct HotRow {
@@ -444,25 +469,25 @@ struct Replica {
     };
     MT_HD HotRow load_row(int32_t a) const {
         HotRow r;
-        r.len = z.len[a];
-        r.seq = z.seq[a];
-        r.rseq = z.rseq[a];
+        r.len = z.len(a);
+        r.seq = z.seq(a);
+        r.rseq = z.rseq(a);
         r.rid = z.rid[a];
-        r.cli = z.cli[a];
-        r.rcli = z.rcli[a];
-        r.flags = z.flags[a];
-        r.ng = z.ng[a];
+        r.cli = z.cli(a);
+        r.rcli = z.rcli(a);
+        r.flags = z.flags(a);
+        r.ng = z.ng(a);
         return r;
     }
     MT_HD void store_row(int32_t b, const HotRow& r) {
-        z.len[b] = r.len;
-        z.seq[b] = r.seq;
-        z.rseq[b] = r.rseq;
+        z.len(b) = r.len;
+        z.seq(b) = r.seq;
+        z.rseq(b) = r.rseq;
         z.rid[b] = r.rid;
-        z.cli[b] = r.cli;
-        z.rcli[b] = r.rcli;
-        z.flags[b] = r.flags;
-        z.ng[b] = r.ng;
+        z.cli(b) = r.cli;
+        z.rcli(b) = r.rcli;
+        z.flags(b) = r.flags;
+        z.ng(b) = r.ng;
     }
     /* shift slab rows [j, c) of leaf n right by one slot (wave-parallel: read all, then write) */
     MT_HD void slab_shift_right(int32_t n, int32_t j, int32_t c) {
@@ -569,16 +594,16 @@ struct Replica {
             v[0] = v[1] = v[2] = v[3] = 0;
             return;
         }
-        I4 L = ld4(&z.len[s0]);
-        I4 R = ld4(&z.rseq[s0]);
+        I4 L = ld4(&z.len(s0));
+        I4 R = ld4(&z.rseq(s0));
         if (is_local(client)) { /* localNetLength (mergeTree.ts:1195-1206) */
             for (int q = 0; q < 4; q++) v[q] = R.x[q] == NOREM ? L.x[q] : 0;
             return;
         }
-        I4 Q = ld4(&z.seq[s0]);
-        B4 C = ldb4(&z.cli[s0]);
-        B4 RC = ldb4(&z.rcli[s0]);
-        B4 F = ldb4(&z.flags[s0]);
+        I4 Q = ld4(&z.seq(s0));
+        B4 C = ldb4(&z.cli(s0));
+        B4 RC = ldb4(&z.rcli(s0));
+        B4 F = ldb4(&z.flags(s0));
         for (int q = 0; q < 4; q++) {
             int32_t c = C.x[q] == LOCAL_CLIENT ? -1 : (int32_t)C.x[q];
             int32_t sq = Q.x[q];
@@ -759,8 +784,8 @@ struct Replica {
         int32_t T = h.nleaf * MAXN;
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
-            if (s < 0 || (z.flags[s] & RF_NOTEXT) || cold(s).gc == ep) continue;
-            int32_t L = z.len[s];
+            if (s < 0 || (z.flags(s) & RF_NOTEXT) || cold(s).gc == ep) continue;
+            int32_t L = z.len(s);
             arena_copy(dst + top, src + cold(s).toff, L);
             cold(s).toff = (uint32_t)top;
             cold(s).gc = (uint8_t)ep;
@@ -778,7 +803,7 @@ struct Replica {
         MT_PROF_SCOPE(PH_SPLIT);
         int32_t n = lo[t >> 3], j = t & 7;
         int32_t s0 = n * MAXN + j;
-        if (z.flags[s0] & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
+        if (z.flags(s0) & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
         bool willSplit = nch[n] + 1 >= MAXN;
         int32_t rs = leaf_insert_slot(n, j + 1);
         if (rs < 0) return -1;
@@ -789,17 +814,17 @@ struct Replica {
         z.rid[rs] = (int16_t)alloc_rid();
         z.rleaf[z.rid[rs]] = (int16_t)(rs / MAXN);
         cold(rs) = cold(ls); /* splitAt copies every field (mergeTree.ts:523-567) */
-        z.len[rs] = z.len[ls] - off;
+        z.len(rs) = z.len(ls) - off;
         cold(rs).toff = cold(ls).toff + (uint32_t)off;
-        z.len[ls] = off;
-        z.flags[ls] &= (uint8_t)~RF_NLK; /* the left part's last unit is not known any more */
+        z.len(ls) = off;
+        z.flags(ls) &= (uint8_t)~RF_NLK; /* the left part's last unit is not known any more */
         h.nrows++;
         h.sumW += 2;
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
          * same pending groups (in the row's FIFO order = log order), appended at the end of each
          * group's segment list */
-        if (z.ng[ls]) {
-            if (h.memN + z.ng[ls] > d.caps.mcap) mem_compact();
+        if (z.ng(ls)) {
+            if (h.memN + z.ng(ls) > d.caps.mcap) mem_compact();
             int32_t head = h.gqN ? d.gq[h.gqHead % d.caps.gcap] : 0x7fffffff;
             int32_t lrid = z.rid[ls];
             int32_t rrid = z.rid[rs];
@@ -857,12 +882,12 @@ struct Replica {
     }
     /* SegmentGroupCollection.enqueue (segmentGroupCollection.ts:28-31) */
     MT_HD void row_enqueue_group(int32_t s, int32_t gid) {
-        int32_t ng = z.ng[s];
+        int32_t ng = z.ng(s);
         if (ng >= 255) {
             fail(E_CAPACITY);
             return;
         }
-        z.ng[s] = (uint8_t)(ng + 1);
+        z.ng(s) = (uint8_t)(ng + 1);
         mem_append(gid, z.rid[s]);
     }
     /* addToPendingList (mergeTree.ts:1955-1962); the group id is the op's localSeq */
@@ -1057,9 +1082,9 @@ struct Replica {
         return h.nkeys++;
     }
     MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
-        if (!(z.flags[s] & RF_PROPS)) {
+        if (!(z.flags(s) & RF_PROPS)) {
             cold(s).prw = 0;
-            z.flags[s] |= RF_PROPS;
+            z.flags(s) |= RF_PROPS;
             for (int k = 0; k < NKEYS; k++) {
                 cold(s).pv[k] = 0;
                 cold(s).pk[k] = 0;
@@ -1105,7 +1130,7 @@ struct Replica {
     }
     MT_HD bool match_props(int32_t a, int32_t b) { /* matchProperties (properties.ts:61-92) */
         MT_PROF_SCOPE(PH_CAND);
-        bool pa = z.flags[a] & RF_PROPS, pb = z.flags[b] & RF_PROPS;
+        bool pa = z.flags(a) & RF_PROPS, pb = z.flags(b) & RF_PROPS;
         if (pa != pb) return false;
         if (!pa) return true;
         for (int k = 0; k < NKEYS; k++)
@@ -1118,27 +1143,27 @@ struct Replica {
     MT_HD bool can_append(int32_t a, int32_t b) {
         MT_PROF_SCOPE(PH_CAND);
         /* PermutationSegment.canAppend (permutationvector.ts:87-93): both handles unallocated */
-        if ((z.flags[a] | z.flags[b]) & RF_PERM) return (z.flags[a] & z.flags[b] & RF_PERM) != 0;
-        if (z.flags[a] & RF_MARKER) return false;
-        if (ends_nl(a, z.len[a])) return false;
-        if (z.flags[b] & RF_MARKER) return false;
-        return z.len[a] <= GRANULARITY || z.len[b] <= GRANULARITY;
+        if ((z.flags(a) | z.flags(b)) & RF_PERM) return (z.flags(a) & z.flags(b) & RF_PERM) != 0;
+        if (z.flags(a) & RF_MARKER) return false;
+        if (ends_nl(a, z.len(a))) return false;
+        if (z.flags(b) & RF_MARKER) return false;
+        return z.len(a) <= GRANULARITY || z.len(b) <= GRANULARITY;
     }
     /* the text of the row in slot a (current length La) ends with "\n" (textSegment.ts:64) */
     MT_HD bool ends_nl(int32_t a, int32_t La) {
-        int32_t f = z.flags[a];
+        int32_t f = z.flags(a);
         if (f & RF_NLK) return (f & RF_NL) != 0;
         MT_PROF_SCOPE(PH_CAND);
         bool nl = La > 0 && arena_base(h.arenaSide)[cold(a).toff + La - 1] == '\n';
-        z.flags[a] = (uint8_t)(f | RF_NLK | (nl ? RF_NL : 0));
+        z.flags(a) = (uint8_t)(f | RF_NLK | (nl ? RF_NL : 0));
         return nl;
     }
     /* TextSegment.append (textSegment.ts:74-85): the merged text is rebuilt at the arena top */
     MT_HD void append_text(int32_t a, int32_t b) {
         MT_PROF_SCOPE(PH_APPEND);
-        int32_t La = z.len[a], Lb = z.len[b];
-        if (z.flags[a] & RF_PERM) { /* PermutationSegment.append (permutationvector.ts:95-101) */
-            z.len[a] = La + Lb;
+        int32_t La = z.len(a), Lb = z.len(b);
+        if (z.flags(a) & RF_PERM) { /* PermutationSegment.append (permutationvector.ts:95-101) */
+            z.len(a) = La + Lb;
             return;
         }
         uint16_t* base = arena_base(h.arenaSide);
@@ -1155,9 +1180,9 @@ struct Replica {
             arena_copy(base + off + La, base + cold(b).toff, Lb);
             cold(a).toff = (uint32_t)off;
         }
-        z.len[a] = La + Lb;
+        z.len(a) = La + Lb;
         /* the merged text ends where b's did */
-        z.flags[a] = (uint8_t)((z.flags[a] & ~(RF_NLK | RF_NL)) | (z.flags[b] & (RF_NLK | RF_NL)));
+        z.flags(a) = (uint8_t)((z.flags(a) & ~(RF_NLK | RF_NL)) | (z.flags(b) & (RF_NLK | RF_NL)));
     }
     /* scourNode on leaf n: compacts the slab in place; returns the new child count. Rows are
      * merged into their predecessor or unlinked exactly as the reference decides. */
@@ -1169,9 +1194,9 @@ struct Replica {
         int32_t minSeq = h.minSeq;
         for (int32_t k = 0; k < c; k++) {
             int32_t s = n * MAXN + k;
-            if (z.ng[s] == 0) {
-                if (z.rseq[s] != NOREM) {
-                    if (z.rseq[s] > minSeq) {
+            if (z.ng(s) == 0) {
+                if (z.rseq(s) != NOREM) {
+                    if (z.rseq(s) > minSeq) {
                         if (wpos != k) copy_row(n * MAXN + wpos, s);
                         wpos++;
                     } else {
@@ -1179,14 +1204,14 @@ struct Replica {
                     }
                     prev = -1;
                 } else {
-                    if (z.seq[s] <= minSeq) {
+                    if (z.seq(s) <= minSeq) {
                         /* hot predicates first; the cold ones (props values, trailing newline) are
                          * only read for a candidate pair. Same conjunction as mergeTree.ts:1355-1360. */
                         bool ok = prev >= 0 && local_len(s) > 0 &&
-                                  ((z.flags[prev] & z.flags[s] & RF_PERM) ||
-                                   (!((z.flags[prev] | z.flags[s]) & RF_NOTEXT) &&
-                                    (z.len[prev] <= GRANULARITY || z.len[s] <= GRANULARITY))) &&
-                                  ((z.flags[prev] ^ z.flags[s]) & RF_PROPS) == 0 && match_props(prev, s) &&
+                                  ((z.flags(prev) & z.flags(s) & RF_PERM) ||
+                                   (!((z.flags(prev) | z.flags(s)) & RF_NOTEXT) &&
+                                    (z.len(prev) <= GRANULARITY || z.len(s) <= GRANULARITY))) &&
+                                  ((z.flags(prev) ^ z.flags(s)) & RF_PROPS) == 0 && match_props(prev, s) &&
                                   can_append(prev, s);
                         if (ok) {
                             append_text(prev, s);
@@ -1279,12 +1304,12 @@ struct Replica {
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
                 ok = match_props(sp, sk);
                 if (ok && !permPair) {
-                    bool nl = ends_nl(sp, prevLen); /* caches RF_NLK/RF_NL in z.flags[sp] */
+                    bool nl = ends_nl(sp, prevLen); /* caches RF_NLK/RF_NL in z.flags(sp) */
                     prevFl = (prevFl & ~(RF_NLK | RF_NL)) | RF_NLK | (nl ? RF_NL : 0);
                     ok = !nl;
                 }
                 if (ok) {
-                    append_text(sp, sk); /* updates z.len[sp] (read by a GC inside it) and its NL bits */
+                    append_text(sp, sk); /* updates z.len(sp) (read by a GC inside it) and its NL bits */
                     prevLen += lk;
                     prevFl = (prevFl & ~(RF_NLK | RF_NL)) | (fk & (RF_NLK | RF_NL));
                     nlen = w.writelane(prevLen, prev, nlen);
@@ -1322,7 +1347,7 @@ struct Replica {
             r.flags = (uint8_t)fl;
             store_row(n * MAXN + __builtin_popcountll(keep & lmask & below), r);
         }
-        if (valid && j >= newc) z.len[n * MAXN + j] = 0; /* disjoint from every kept row's target */
+        if (valid && j >= newc) z.len(n * MAXN + j) = 0; /* disjoint from every kept row's target */
         if (n >= 0 && j == 0) nch[n] = (int8_t)newc;
         w.sync();
         for (int32_t i = 0; i < nl; i++) cnt[i] = __builtin_popcountll(keep & (0xFFull << (8 * i)));
@@ -1548,10 +1573,10 @@ struct Replica {
     /* ---- insert (insertSegments 2001-2031, blockInsert 2174-2257) -------------------- */
     /* breakTie for a zero-length row (2281-2310) */
     MT_HD bool break_tie(int32_t s, int32_t refSeq, int32_t client) const {
-        int32_t rs = z.rseq[s];
+        int32_t rs = z.rseq(s);
         if (rs != NOREM && rs != 0 && rs <= refSeq && rs != UNASSIGNED_SEQ) return false;
         if (client == h.localShort) return true;
-        return z.seq[s] != UNASSIGNED_SEQ;
+        return z.seq(s) != UNASSIGNED_SEQ;
     }
     /* continueFrom (2187-2194): first row after leaf lorder[k] with localNetLength > 0 is a
      * local-pending insert */
@@ -1561,9 +1586,9 @@ struct Replica {
             int32_t s0 = quad_slot(b + 4 * w.lane());
             int32_t fq = -1, fseq = 0;
             if (s0 >= 0) {
-                I4 L = ld4(&z.len[s0]);
-                I4 R = ld4(&z.rseq[s0]);
-                I4 Q = ld4(&z.seq[s0]);
+                I4 L = ld4(&z.len(s0));
+                I4 R = ld4(&z.rseq(s0));
+                I4 Q = ld4(&z.seq(s0));
                 for (int q = 3; q >= 0; q--)
                     if (L.x[q] > 0 && R.x[q] == NOREM) {
                         fq = q;
@@ -1600,7 +1625,7 @@ struct Replica {
             if (t < 0) return -1;
             int32_t s = slot_at(t);
             int32_t v = vis(s, refSeq, client);
-            if (P + v > pos && !(z.flags[s] & RF_MARKER)) {
+            if (P + v > pos && !(z.flags(s) & RF_MARKER)) {
                 int32_t ls = split_row(t, pos - P);
                 if (ls < 0) return -1;
                 k = lp[ls / MAXN];
@@ -1649,15 +1674,15 @@ struct Replica {
             }
             z.rid[s] = (int16_t)alloc_rid();
             cold(s).gc = 0;
-            z.len[s] = L;
-            z.seq[s] = seq;
-            z.rseq[s] = NOREM;
+            z.len(s) = L;
+            z.seq(s) = seq;
+            z.rseq(s) = NOREM;
             cold(s).lseq = localSeq;
             cold(s).lrseq = 0;
-            z.cli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-            z.rcli[s] = 0;
+            z.cli(s) = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
+            z.rcli(s) = 0;
             int32_t fl = (marker ? RF_MARKER : 0) | (perm ? RF_PERM : 0) | (hasL ? RF_LSEQ : 0);
-            z.ng[s] = 0;
+            z.ng(s) = 0;
             cold(s).prw = 0;
             cold(s).ovl = 0;
             z.rleaf[z.rid[s]] = (int16_t)(s / MAXN);
@@ -1674,7 +1699,7 @@ struct Replica {
                 int32_t last = arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
                 fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
             }
-            z.flags[s] = (uint8_t)fl;
+            z.flags(s) = (uint8_t)fl;
             for (int k = 0; k < NKEYS; k++) {
                 cold(s).pv[k] = 0;
                 cold(s).pk[k] = 0;
@@ -1836,11 +1861,11 @@ struct Replica {
         bool created = false;
         range_op(start, end, refSeq, client, [&](int32_t s) {
             h.sumW++;
-            if (z.rseq[s] != NOREM) {
-                if (z.rseq[s] == UNASSIGNED_SEQ) {
-                    z.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-                    z.rseq[s] = seq;
-                    z.flags[s] &= (uint8_t)~RF_LRSEQ;
+            if (z.rseq(s) != NOREM) {
+                if (z.rseq(s) == UNASSIGNED_SEQ) {
+                    z.rcli(s) = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
+                    z.rseq(s) = seq;
+                    z.flags(s) &= (uint8_t)~RF_LRSEQ;
                 } else {
                     uint64_t ov = cold(s).ovl;
                     int k = 0;
@@ -1849,21 +1874,21 @@ struct Replica {
                         fail(E_UNSUPPORTED);
                     } else {
                         cold(s).ovl = ov | ((uint64_t)(client + 1) << (8 * k));
-                        z.flags[s] |= RF_OVL;
+                        z.flags(s) |= RF_OVL;
                     }
                 }
             } else {
-                h.localLen -= z.len[s]; /* the row leaves the local view */
-                z.rcli[s] = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-                z.rseq[s] = seq;
+                h.localLen -= z.len(s); /* the row leaves the local view */
+                z.rcli(s) = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
+                z.rseq(s) = seq;
                 cold(s).lrseq = localSeq;
                 if (hasL)
-                    z.flags[s] |= RF_LRSEQ;
+                    z.flags(s) |= RF_LRSEQ;
                 else
-                    z.flags[s] &= (uint8_t)~RF_LRSEQ;
+                    z.flags(s) &= (uint8_t)~RF_LRSEQ;
             }
             if (h.collaborating) {
-                if (z.rseq[s] == UNASSIGNED_SEQ && client == h.localShort)
+                if (z.rseq(s) == UNASSIGNED_SEQ && client == h.localShort)
                     pending_add(s, localSeq, &created);
                 else
                     add_lru(s, seq);
@@ -1910,20 +1935,20 @@ struct Replica {
                         continue;
                     }
                     /* dequeue the row's head group (groups are acked in FIFO order: this one) */
-                    int32_t ng = z.ng[s];
+                    int32_t ng = z.ng(s);
                     if (ng < 1) fail(E_ASSERT);
-                    if (ng > 0) z.ng[s] = (uint8_t)(ng - 1);
+                    if (ng > 0) z.ng(s) = (uint8_t)(ng - 1);
                     if (kind == MT_OP_ANNOTATE) {
-                        if (!(z.flags[s] & RF_PROPS)) fail(E_ASSERT);
+                        if (!(z.flags(s) & RF_PROPS)) fail(E_ASSERT);
                         ack_props(s, kv, nkv, rewrite);
                     } else if (kind == MT_OP_INSERT) {
-                        if (z.seq[s] != UNASSIGNED_SEQ) fail(E_ASSERT);
-                        z.seq[s] = seq;
-                        z.flags[s] &= (uint8_t)~RF_LSEQ;
+                        if (z.seq(s) != UNASSIGNED_SEQ) fail(E_ASSERT);
+                        z.seq(s) = seq;
+                        z.flags(s) &= (uint8_t)~RF_LSEQ;
                     } else if (kind == MT_OP_REMOVE) {
-                        if (z.rseq[s] == NOREM || z.rseq[s] == 0) fail(E_ASSERT);
-                        z.flags[s] &= (uint8_t)~RF_LRSEQ;
-                        if (z.rseq[s] == UNASSIGNED_SEQ) z.rseq[s] = seq;
+                        if (z.rseq(s) == NOREM || z.rseq(s) == 0) fail(E_ASSERT);
+                        z.flags(s) &= (uint8_t)~RF_LRSEQ;
+                        if (z.rseq(s) == UNASSIGNED_SEQ) z.rseq(s) = seq;
                     } else {
                         fail(E_ASSERT);
                     }
@@ -2012,7 +2037,7 @@ struct Replica {
         const uint16_t* base = arena_base(h.arenaSide);
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
-            if (s < 0 || (z.flags[s] & RF_NOTEXT)) continue;
+            if (s < 0 || (z.flags(s) & RF_NOTEXT)) continue;
             int32_t v = vis(s, refSeq, client);
             if (v <= 0) continue;
             if (out) {
@@ -2067,8 +2092,8 @@ struct Replica {
         for (int32_t t = 0; t < T; t++) {
             int32_t s = slot_at(t);
             if (s < 0) continue;
-            uint8_t fl = z.flags[s];
-            bool rem = z.rseq[s] != NOREM;
+            uint8_t fl = z.flags(s);
+            bool rem = z.rseq(s) != NOREM;
             int nov = 0;
             while (nov < NOVL && ((cold(s).ovl >> (8 * nov)) & 0xFF)) nov++;
             int np = 0;
@@ -2078,13 +2103,13 @@ struct Replica {
             uint8_t b4[4] = {(uint8_t)((fl & RF_MARKER) ? MT_SEG_MARKER : (fl & RF_PERM) ? MT_SEG_PERM : MT_SEG_TEXT),
                              (uint8_t)(((fl & RF_PROPS) ? MT_DF_HAS_PROPS : 0) | (rem ? MT_DF_REMOVED : 0) |
                                        ((fl & RF_LSEQ) ? MT_DF_LSEQ : 0) | ((fl & RF_LRSEQ) ? MT_DF_LRSEQ : 0)),
-                             (uint8_t)nov, z.ng[s]};
+                             (uint8_t)nov, z.ng(s)};
             put_bytes(o, b4, 4);
-            int32_t f[8] = {z.len[s],
-                            z.seq[s],
-                            long_of(z.cli[s]),
-                            rem ? z.rseq[s] : 0,
-                            rem ? long_of(z.rcli[s]) : 0,
+            int32_t f[8] = {z.len(s),
+                            z.seq(s),
+                            long_of(z.cli(s)),
+                            rem ? z.rseq(s) : 0,
+                            rem ? long_of(z.rcli(s)) : 0,
                             (fl & RF_LSEQ) ? cold(s).lseq : 0,
                             (fl & RF_LRSEQ) ? cold(s).lrseq : 0,
                             t >> 3};
@@ -2110,7 +2135,7 @@ struct Replica {
                 put_bytes(o, kv2, 4);
                 last = bk;
             }
-            if (!(fl & RF_NOTEXT)) put_bytes(o, base + cold(s).toff, 2 * (int64_t)z.len[s]);
+            if (!(fl & RF_NOTEXT)) put_bytes(o, base + cold(s).toff, 2 * (int64_t)z.len(s));
         }
     }
     MT_HD static uint64_t fnv(const uint8_t* p, int64_t n) {

@@ -67,7 +67,7 @@ mth_store* mth_create(int64_t ndocs, const int32_t* caps6) {
                   : prof == 1 ? store_layout(s->s1, k, ndocs)
                   : prof == 3 ? store_layout(s->s3, k, ndocs)
                               : store_layout(s->s2, k, ndocs);
-    s->mem = (uint8_t*)calloc(1, (size_t)bytes);
+    s->mem = host_store_alloc(bytes);
     if (!s->mem) {
         free(s);
         return nullptr;

@@ -82,7 +82,7 @@ template <class HT>
 static void model_init(Model<HT>* m, const mtg_params* P, int32_t local_long) {
     Caps k = {P->model_acap > 0 ? P->model_acap : (1 << 17), 1 << 14, 4096};
     int64_t bytes = store_layout(m->st, k, 1);
-    m->mem = (uint8_t*)calloc(1, (size_t)bytes);
+    m->mem = host_store_alloc(bytes);
     m->ok = m->mem != nullptr;
     if (!m->ok) return;
     m->st.base = m->mem;

@@ -147,7 +147,12 @@ template <class HT>
 __global__ __launch_bounds__(WG) void k_digest(Store<HT> st, int64_t ndocs, uint64_t* out) {
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
+    /* A compiler memory barrier first: without it, the store-free read kernels let the compiler
+     * fetch the document through scalar (SMEM) loads, which returned wrong values for some
+     * documents on gfx950 with the leaf-line layout; vector loads are correct. */
+    __asm__ volatile("" ::: "memory");
     Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
+    __asm__ volatile("" ::: "memory");
     uint64_t h = r.digest();
     if (threadIdx.x == 0) out[d] = h;
 }
@@ -162,7 +167,9 @@ __global__ __launch_bounds__(WG) void k_dump(Store<HT> st, int64_t doc, uint8_t*
 template <class HT>
 __global__ __launch_bounds__(WG) void k_length(Store<HT> st, int64_t doc, int32_t ref_seq, int32_t long_client,
                                               int32_t* out) {
+    __asm__ volatile("" ::: "memory"); /* vector loads only (see k_digest) */
     Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
+    __asm__ volatile("" ::: "memory");
     int32_t v;
     if (long_client < 0) {
         v = r.length_local();
@@ -318,6 +325,11 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     if (hipMalloc(&e->mem, (size_t)bytes) != hipSuccess) {
         delete e;
         return MT_E_NOMEM;
+    }
+    if (hipMemset(e->mem, 0, (size_t)bytes) != hipSuccess) {
+        (void)hipFree(e->mem);
+        delete e;
+        return MT_E_HIP;
     }
     e->s0.base = e->s1.base = e->s2.base = e->s3.base = (uint8_t*)e->mem;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||

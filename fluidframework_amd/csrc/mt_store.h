@@ -8,6 +8,8 @@
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "mt_core.h"
 
@@ -37,6 +39,13 @@ struct Store {
 };
 
 inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+/* zeroed host block for a store (the hot image's leaf lines are 128-byte aligned); free() it */
+inline uint8_t* host_store_alloc(int64_t bytes) {
+    void* p = aligned_alloc(256, (size_t)align256(bytes));
+    if (p) memset(p, 0, (size_t)align256(bytes));
+    return (uint8_t*)p;
+}
 
 /* Fill offsets/stride for capacities `caps`; returns bytes for `ndocs` documents. */
 template <class HT>
