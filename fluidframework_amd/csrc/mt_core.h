@@ -125,16 +125,17 @@ struct HotT {
      * child count; the int32 columns are read 4 slots at a time (16-byte reads). */
     struct alignas(128) Leaf {
         int32_t len[8], seq[8], rseq[8];
-        uint8_t cli[8], rcli[8], flags[8], ng[8];
+        uint8_t b[8][4]; /* per slot {cli, rcli, flags, ng}: a quad's byte columns in one 16-byte read */
     };
     Leaf lf[N];
     MT_HD int32_t& len(int s) { return lf[s >> 3].len[s & 7]; }
     MT_HD int32_t& seq(int s) { return lf[s >> 3].seq[s & 7]; }
     MT_HD int32_t& rseq(int s) { return lf[s >> 3].rseq[s & 7]; }
-    MT_HD uint8_t& cli(int s) { return lf[s >> 3].cli[s & 7]; }
-    MT_HD uint8_t& rcli(int s) { return lf[s >> 3].rcli[s & 7]; }
-    MT_HD uint8_t& flags(int s) { return lf[s >> 3].flags[s & 7]; }
-    MT_HD uint8_t& ng(int s) { return lf[s >> 3].ng[s & 7]; }
+    MT_HD uint8_t& cli(int s) { return lf[s >> 3].b[s & 7][0]; }
+    MT_HD uint8_t& rcli(int s) { return lf[s >> 3].b[s & 7][1]; }
+    MT_HD uint8_t& flags(int s) { return lf[s >> 3].b[s & 7][2]; }
+    MT_HD uint8_t& ng(int s) { return lf[s >> 3].b[s & 7][3]; }
+    MT_HD const int32_t* bytes4(int s) { return (const int32_t*)&lf[s >> 3].b[s & 7][0]; }
     int16_t rid[S];   /* slot -> row id (stable identity of a segment; cold data index) */
     int16_t rleaf[S]; /* row id -> leaf node currently holding it */
     uint8_t rgen[S]; /* row id -> generation, bumped when the id is freed */
@@ -601,19 +602,19 @@ struct Replica {
             return;
         }
         I4 Q = ld4(&z.seq(s0));
-        B4 C = ldb4(&z.cli(s0));
-        B4 RC = ldb4(&z.rcli(s0));
-        B4 F = ldb4(&z.flags(s0));
+        I4 BY = ld4(z.bytes4(s0)); /* {cli, rcli, flags, ng} of the 4 slots */
         for (int q = 0; q < 4; q++) {
-            int32_t c = C.x[q] == LOCAL_CLIENT ? -1 : (int32_t)C.x[q];
+            uint32_t by = (uint32_t)BY.x[q];
+            uint8_t cq = (uint8_t)by, rcq = (uint8_t)(by >> 8), fq = (uint8_t)(by >> 16);
+            int32_t c = cq == LOCAL_CLIENT ? -1 : (int32_t)cq;
             int32_t sq = Q.x[q];
             bool ok = L.x[q] > 0 && (c == client || (sq != UNASSIGNED_SEQ && sq <= refSeq));
             int32_t rs = R.x[q];
             if (ok && rs != NOREM) {
-                int32_t rc = RC.x[q] == LOCAL_CLIENT ? -1 : (int32_t)RC.x[q];
+                int32_t rc = rcq == LOCAL_CLIENT ? -1 : (int32_t)rcq;
                 if (rc == client || (rs != UNASSIGNED_SEQ && rs <= refSeq))
                     ok = false;
-                else if (F.x[q] & RF_OVL)
+                else if (fq & RF_OVL)
                     ok = !ovl_has(s0 + q, client);
             }
             v[q] = ok ? L.x[q] : 0;
