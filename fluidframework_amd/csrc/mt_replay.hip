@@ -230,7 +230,7 @@ struct mt_engine {
     int64_t ndocs;
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
-    int waves = 6;    /* occupancy target of the HBM-resident kernel (MT_REPLAY_WAVES=6|7|8) */
+    int waves = 7;    /* occupancy target of the HBM-resident kernel (MT_REPLAY_WAVES=6|7|8) */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
@@ -312,7 +312,7 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     const char* g = getenv("MT_REPLAY_LDS");
     e->lds = g && g[0] == '1';
     const char* wv = getenv("MT_REPLAY_WAVES");
-    e->waves = wv ? atoi(wv) : 6;
+    e->waves = wv ? atoi(wv) : 7;
     e->profile = prof;
     if (hipSetDevice(device) != hipSuccess) {
         delete e;
@@ -461,19 +461,19 @@ int32_t mt_engine_run(mt_engine* e) {
         };
         if constexpr (std::is_same_v<HT, HotSmall>) {
             /* Default: the hot image stays in HBM (skeleton and heap in LDS) and the kernel is built
-             * for 6 waves per SIMD, so 6,144 documents are in flight (24 per CU): at one wavefront per
+             * for 7 waves per SIMD, so 7,168 documents are in flight (28 per CU): at one wavefront per
              * document the replay is bound by the latency of its dependent accesses, and occupancy
-             * hides more of it than full LDS residency (4 documents per CU) saves; 6 beats 7 and 8
-             * because the register cap of 8 waves spills (tools/gpu_occupancy.sh).
-             * MT_REPLAY_LDS=1 selects the fully LDS-staged form. */
+             * hides more of it than full LDS residency (4 documents per CU) saves. With the leaf-line
+             * layout 7 beats 6 and 8 (174 / 161 / 168 Mops/s at 32k docs; 8 spills registers;
+             * tools/gpu_occupancy.sh). MT_REPLAY_LDS=1 selects the fully LDS-staged form. */
             if (e->lds)
                 launch(k_replay<HT, true>);
             else if (e->waves == 8)
                 launch(k_replay<HT, false, 8>);
-            else if (e->waves == 7)
-                launch(k_replay<HT, false, 7>);
-            else
+            else if (e->waves == 6)
                 launch(k_replay<HT, false, 6>);
+            else
+                launch(k_replay<HT, false, 7>);
         } else if constexpr (std::is_same_v<HT, HotMat>) {
             /* skeleton + heap in LDS (10.7 KB): LDS caps residency at 14 documents per CU */
             launch(k_replay<HT, false, 4>);

@@ -95,6 +95,14 @@ def test_large_doc_props_newlines():
     _check_batch(b, 6000, ndump=2, ncap=4096, hcap=8192, acap=1 << 17)
 
 
+def test_large_doc_29k_rows():
+    """Config-4 shape at 20k ops/doc: ~29k rows (tombstones included) and ~6k leaves per document in
+    the 16,384-node profile — the deepest flat scans the engine runs."""
+    w = gen.config4(20000)
+    b = gen.generate(w, 2)
+    _check_batch(b, 20000, ndump=2, ncap=16384, hcap=16384, acap=1 << 20)
+
+
 def test_matrix_permutation_vectors_config5():
     """Config 5: SharedMatrix rows/cols PermutationVector replicas (PermutationSegment rows,
     annotate-heavy) in the 640-node profile; perspective lengths of remote clients agree too."""
