@@ -87,7 +87,7 @@ __device__ inline void skel_move(Skel<HT>& k, HT& z, bool in) {
 /* K1-K4 fused: the whole event stream of a document, one wave per document. LDS = true stages the
  * whole small-profile hot image in LDS; otherwise the image stays in HBM and only the skeleton and
  * the heap (Skel, 3.5 KB for the small profile) are staged. */
-template <class HT, bool LDS, int MINW = 1>
+template <class HT, bool LDS, int MINW = 1, bool SKEL = true>
 __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
 #endif
         __syncthreads();
         copy_image(g, &hot);
-    } else if constexpr (sizeof(Skel<HT>) <= 12288) {
+    } else if constexpr (SKEL && sizeof(Skel<HT>) <= 12288) {
         __shared__ __attribute__((aligned(16))) Skel<HT> sk;
         skel_move(sk, *v.t, true);
         __syncthreads();
@@ -231,6 +231,7 @@ struct mt_engine {
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
     int waves = 7;    /* occupancy target of the HBM-resident kernel (MT_REPLAY_WAVES=6|7|8) */
+    bool mat_skel = true; /* config-5 profile stages skeleton + heap in LDS (MT_REPLAY_MAT_SKEL) */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
@@ -313,6 +314,8 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->lds = g && g[0] == '1';
     const char* wv = getenv("MT_REPLAY_WAVES");
     e->waves = wv ? atoi(wv) : 7;
+    const char* ms = getenv("MT_REPLAY_MAT_SKEL");
+    e->mat_skel = !(ms && ms[0] == '0');
     e->profile = prof;
     if (hipSetDevice(device) != hipSuccess) {
         delete e;
@@ -475,8 +478,12 @@ int32_t mt_engine_run(mt_engine* e) {
             else
                 launch(k_replay<HT, false, 7>);
         } else if constexpr (std::is_same_v<HT, HotMat>) {
-            /* skeleton + heap in LDS (10.7 KB): LDS caps residency at 14 documents per CU */
-            launch(k_replay<HT, false, 4>);
+            /* skeleton + heap in LDS (10.7 KB): LDS caps residency at 14 documents per CU;
+             * MT_REPLAY_MAT_SKEL=0 keeps them in HBM and runs 7 waves per SIMD instead */
+            if (e->mat_skel)
+                launch(k_replay<HT, false, 4>);
+            else
+                launch(k_replay<HT, false, 7, false>);
         } else {
             launch(k_replay<HT, false>);
         }
