@@ -66,6 +66,13 @@ struct Skel {
     int16_t hrid[HT::H];
     uint8_t hgen[HT::H];
 };
+/* The scan-critical subset of the skeleton (document order, child counts, parents): staged alone
+ * where the whole Skel would cap residency through LDS (config-5 profile). */
+template <class HT>
+struct SkelLite {
+    int16_t lorder[HT::N], lpos[HT::N], nparent[HT::N];
+    int8_t nchild[HT::N];
+};
 template <class T>
 __device__ inline void wave_copy(T* dst, const T* src, int n) {
     for (int i = threadIdx.x; i < n; i += WG) dst[i] = src[i];
@@ -84,10 +91,22 @@ __device__ inline void skel_move(Skel<HT>& k, HT& z, bool in) {
     }
 }
 
+template <class HT>
+__device__ inline void skel_lite_move(SkelLite<HT>& k, HT& z, bool in) {
+    constexpr int N = HT::N;
+    if (in) {
+        wave_copy(k.lorder, z.lorder, N), wave_copy(k.lpos, z.lpos, N), wave_copy(k.nparent, z.nparent, N);
+        wave_copy(k.nchild, z.nchild, N);
+    } else {
+        wave_copy(z.lorder, k.lorder, N), wave_copy(z.lpos, k.lpos, N), wave_copy(z.nparent, k.nparent, N);
+        wave_copy(z.nchild, k.nchild, N);
+    }
+}
+
 /* K1-K4 fused: the whole event stream of a document, one wave per document. LDS = true stages the
  * whole small-profile hot image in LDS; otherwise the image stays in HBM and only the skeleton and
  * the heap (Skel, 3.5 KB for the small profile) are staged. */
-template <class HT, bool LDS, int MINW = 1, bool SKEL = true>
+template <class HT, bool LDS, int MINW = 1, int SKM = 1> /* SKM: 1 Skel, 2 SkelLite, 0 none */
 __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
@@ -116,7 +135,21 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
 #endif
         __syncthreads();
         copy_image(g, &hot);
-    } else if constexpr (SKEL && sizeof(Skel<HT>) <= 12288) {
+    } else if constexpr (SKM == 2) {
+        __shared__ __attribute__((aligned(16))) SkelLite<HT> sk;
+        skel_lite_move(sk, *v.t, true);
+        __syncthreads();
+        Replica<WaveGPU, HT> r(v, WaveGPU());
+        r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild;
+        r.replay(p);
+        r.commit();
+        __syncthreads();
+        skel_lite_move(sk, *v.t, false);
+#ifdef MT_PROF
+        if (prof && threadIdx.x == 0)
+            for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
+#endif
+    } else if constexpr (SKM == 1 && sizeof(Skel<HT>) <= 12288) {
         __shared__ __attribute__((aligned(16))) Skel<HT> sk;
         skel_move(sk, *v.t, true);
         __syncthreads();
@@ -231,7 +264,7 @@ struct mt_engine {
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
     int waves = 7;    /* occupancy target of the HBM-resident kernel (MT_REPLAY_WAVES=6|7|8) */
-    bool mat_skel = true; /* config-5 profile stages skeleton + heap in LDS (MT_REPLAY_MAT_SKEL) */
+    int mat_skel = 2; /* config-5 profile: 2 SkelLite in LDS, 1 Skel, 0 none (MT_REPLAY_MAT_SKEL) */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;
@@ -315,7 +348,7 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     const char* wv = getenv("MT_REPLAY_WAVES");
     e->waves = wv ? atoi(wv) : 7;
     const char* ms = getenv("MT_REPLAY_MAT_SKEL");
-    e->mat_skel = !(ms && ms[0] == '0');
+    e->mat_skel = ms ? atoi(ms) : 2;
     e->profile = prof;
     if (hipSetDevice(device) != hipSuccess) {
         delete e;
@@ -478,12 +511,15 @@ int32_t mt_engine_run(mt_engine* e) {
             else
                 launch(k_replay<HT, false, 7>);
         } else if constexpr (std::is_same_v<HT, HotMat>) {
-            /* skeleton + heap in LDS (10.7 KB): LDS caps residency at 14 documents per CU;
-             * MT_REPLAY_MAT_SKEL=0 keeps them in HBM and runs 7 waves per SIMD instead */
-            if (e->mat_skel)
+            /* Default (MT_REPLAY_MAT_SKEL=2): only SkelLite (4.5 KB) in LDS, 7 waves per SIMD
+             * (116 Mops/s at 16k replicas). =1 stages the whole Skel (10.7 KB), which caps residency
+             * at 14 documents per CU through LDS (103 Mops/s); =0 stages nothing (104 Mops/s). */
+            if (e->mat_skel == 1)
                 launch(k_replay<HT, false, 4>);
+            else if (e->mat_skel == 2)
+                launch(k_replay<HT, false, 7, 2>);
             else
-                launch(k_replay<HT, false, 7, false>);
+                launch(k_replay<HT, false, 7, 0>);
         } else {
             launch(k_replay<HT, false>);
         }
