@@ -1,17 +1,23 @@
 """Bench: batched merge-tree replay on MI355X (BASELINE.json metric).
 
-One step = one full replay of this rank's synthetic workload: every document's replica is reset
-to an empty collaborating state and its whole event stream (config 3 of BASELINE.json: 8
-clients, refSeq lag <= 64, local-pending edits acked <= 64 seqs later, 4,096 sequenced messages
-per doc) is applied on the GPU. Inputs are resident in HBM before the timed region. Documents
-shard across ranks with no data-path collective ("scaling": "weak": each rank replays its own
-65,536 documents); RCCL is used once, after timing, to all-gather per-document digests.
+One step = one full replay of this rank's synthetic workload: every document's replica is reset to
+an empty collaborating state and its whole event stream is applied on the GPU (Client.applyMsg
+for sequenced messages, the *Local edits for local ones). Inputs are resident in HBM before the
+timed region. `value` = sequenced messages applied per second over all ranks.
 
-`--config 5` instead measures BASELINE.json's config 5 (SharedMatrix PermutationVector replay:
-16,384 matrices x 2 vectors = 32,768 replicas, annotate-heavy PermutationSegment ops); the
-default (the line the driver records) is config 3.
+Workloads (BASELINE.json configs; --config):
+  3 (default, the metric's line): 65,536 documents per node, 8 clients, refSeq lag <= 64,
+    local-pending replica with acks, 4,096 sequenced messages per document.
+  1: the reference's TestClient conflict farm: 1 document x 8 replicas x 10k ops in rounds of 100.
+  2: 4,096 documents x 10k ops, observer replica, refSeq = MSN = seq - 1.
+  5: SharedMatrix PermutationVector replay: 16,384 matrices x 2 vectors = 32,768 replicas.
+Multi-GPU (one process per GPU, torchrun): --docs is the NODE total and the documents are split
+over the ranks by cost bin-packing (shard.assign; "scaling": "strong", the metric's "ops/s per
+node at 65k docs"); --scaling weak gives every rank --docs documents of its own instead. No
+data-path collective; RCCL all-gathers per-document digests once, after timing.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--docs D] [--ops-per-doc O] [--config 3|5]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|5] [--docs D]
+                       [--ops-per-doc O] [--scaling strong|weak] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -26,11 +32,14 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
-
-WORKLOADS = {
-    3: "config3: docs x {ops} sequenced msgs, 8 clients, lag<=64, local-pending replica",
-    5: "config5: SharedMatrix rows+cols PermutationVector replicas x {ops} sequenced msgs each, "
-       "8 clients, lag<=64, local-pending, 50% annotate",
+# config -> (default node docs, default ops per doc, workload description)
+CONFIGS = {
+    1: (8, 10_000, "config1: TestClient conflict farm, 1 doc x {docs} replicas (client 0 observes), {ops} ops "
+                   "in rounds of 100, MSN = round start"),
+    2: (4096, 10_000, "config2: docs x {ops} sequenced msgs, observer replica, refSeq = MSN = seq-1, 60/30/10"),
+    3: (65536, 4096, "config3: docs x {ops} sequenced msgs, 8 clients, lag<=64, local-pending replica"),
+    5: (32768, 4096, "config5: SharedMatrix rows+cols PermutationVector replicas x {ops} sequenced msgs each, "
+                     "8 clients, lag<=64, local-pending, 50% annotate"),
 }
 
 
@@ -40,16 +49,57 @@ def log(msg: str) -> None:
     print(f"[bench] {msg} (max rss {rss:.1f} GB)", file=sys.stderr, flush=True)
 
 
+def cpu_workers() -> int:
+    """Host cores this process may use: its CPU affinity, capped by OMP_NUM_THREADS when set (the
+    GPU box sets it to the job's CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def workload(config: int, ops: int):
+    from fluidframework_amd import gen
+    return {1: gen.config1, 2: gen.config2, 3: gen.config3, 5: gen.config5}[config](ops)
+
+
+def cpu_baseline(batch, gpu_digests, workers: int, target_s: float = 15.0):
+    """The oracle (CPU restatement of the reference algorithm, test infrastructure) on `workers`
+    host threads over a bounded prefix of this rank's documents, sized for ~target_s seconds."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_client as oc
+
+    nd = batch.ndocs
+    probe = min(nd, max(workers, 2 * workers))
+    secs, _, _ = oc.replay_batch(batch.subset(range(probe)), threads=workers)
+    ns = probe
+    if secs > 0 and secs < target_s:
+        ns = int(min(nd, max(probe, probe * target_s / secs)))
+    sample = batch.subset(range(ns))
+    secs, odig, oerr = oc.replay_batch(sample, threads=workers)
+    s_seq = int(((sample.ops["kind"] & 0x80) == 0).sum())
+    match = bool((odig == gpu_digests[:ns]).all()) and bool((oerr == 0).all())
+    return {"value": s_seq / secs, "unit": "ops/s", "cores": workers, "kind": "port",
+            "sample": f"first {ns} of this rank's {nd} docs ({s_seq} sequenced msgs), oracle/ C restatement "
+                      f"of the reference B-tree (PartialSequenceLengths, zamboni), one document per thread, "
+                      f"{workers} threads, {secs:.1f}s; digests match GPU: {match}"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=3, choices=(3, 5))
-    ap.add_argument("--docs", type=int, default=0, help="documents per rank (default 65536; config 5: 32768)")
-    ap.add_argument("--ops-per-doc", type=int, default=4096, help="sequenced messages per document")
-    ap.add_argument("--cpu-sample-docs", type=int, default=8192)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--docs", type=int, default=0, help="documents per node (strong) or per rank (weak)")
+    ap.add_argument("--ops-per-doc", type=int, default=0, help="sequenced messages per document")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (default: host share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -62,6 +112,11 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit(f"--gpus {args.gpus} needs one process per GPU: run under "
+                             f"torch.distributed.run --nproc-per-node {args.gpus}")
+        raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -70,17 +125,28 @@ def main() -> None:
         dist.init_process_group("nccl")
     device = local_rank
 
-    # ---- synthetic workload (config 3 or 5), this rank's shard of documents ----
-    if args.docs <= 0:
-        args.docs = 65536 if args.config == 3 else 32768
-    w = gen.config3(args.ops_per_doc) if args.config == 3 else gen.config5(args.ops_per_doc)
+    ndef, odef, desc = CONFIGS[args.config]
+    docs = args.docs or ndef
+    ops = args.ops_per_doc or odef
+    w = workload(args.config, ops)
+
+    # ---- this rank's documents ----
+    if args.scaling == "strong":
+        # cost model: every document of a config draws the same number of sequenced messages, so
+        # the LPT bin-packing (shard.assign) gives an even split; farms (config 1) stay whole
+        unit = w.nclients if args.config == 1 else 1
+        groups = shard.assign(np.full(docs // unit, float(ops)), world)
+        mine = np.concatenate([g[:, None] * unit + np.arange(unit) for g in groups[rank:rank + 1]]).ravel()
+        node_docs = docs
+    else:
+        mine = shard.weak_ids(rank, docs)
+        node_docs = docs * world
     t0 = time.time()
-    doc_base, ndocs = shard.doc_range(rank, args.docs)
-    batch = gen.generate(w, ndocs, doc_base=doc_base, threads=args.cpu_threads)
-    log(f"rank {rank}: generated {args.docs} docs, {batch.nops} events in {time.time() - t0:.1f}s")
+    batch = gen.generate(w, ids=mine, threads=cpu_workers())
+    log(f"rank {rank}: generated {batch.ndocs} docs, {batch.nops} events in {time.time() - t0:.1f}s")
     local_events = int(((batch.ops["kind"] & 0x80) != 0).sum())
 
-    eng = Engine(args.docs, device=device, **default_caps(args.ops_per_doc, config=args.config))
+    eng = Engine(batch.ndocs, device=device, **default_caps(ops, config=args.config))
     log("engine created")
     eng.start_collab(batch.local_long_id)
     eng.submit(batch)  # HtoD once: inputs are resident in HBM for every step
@@ -120,10 +186,12 @@ def main() -> None:
         dev = f"cuda:{device}"
         elapsed = shard.max_over_ranks(elapsed, dist, dev)
         total_seq_ops = shard.sum_over_ranks(seq_ops, dist, dev)
+        total_alg = shard.sum_over_ranks(alg_bytes, dist, dev)
         # the one collective of the design: all-gather per-document digests (verification)
         shard.gather_digests(digests, dist, dev)
     else:
         total_seq_ops = seq_ops
+        total_alg = alg_bytes
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_seq_ops * args.steps / elapsed
@@ -132,17 +200,7 @@ def main() -> None:
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_client as oc
-
-        ns = min(args.cpu_sample_docs, args.docs)
-        sample = batch.subset(range(ns))
-        secs, odig, oerr = oc.replay_batch(sample, threads=args.cpu_threads)
-        s_seq = int(((sample.ops["kind"] & 0x80) == 0).sum())
-        match = bool((odig == digests[:ns]).all())
-        cpu = {"value": s_seq / secs, "unit": "ops/s", "cores": args.cpu_threads, "kind": "port",
-               "sample": f"first {ns} of the {args.docs} docs ({s_seq} sequenced msgs), oracle B-tree "
-                         f"restatement, {args.cpu_threads} threads, {secs:.1f}s; digests match GPU: {match}"}
+        cpu = cpu_baseline(batch, digests, args.cpu_threads or cpu_workers())
 
     if rank == 0:
         out = {
@@ -154,17 +212,20 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (mt_gen: splitmix64(0x5EED0000+doc) xoshiro256**)",
-            "config": {"workload": WORKLOADS[args.config].format(ops=args.ops_per_doc),
-                       "docs_per_gpu": args.docs, "ops_per_doc": args.ops_per_doc,
-                       "local_edits_per_gpu": local_events, "parallelism": f"docs sharded x{world}"},
+            "config": {"workload": desc.format(ops=ops, docs=docs), "config": args.config,
+                       "docs_per_node": node_docs, "docs_rank0": int(batch.ndocs), "ops_per_doc": ops,
+                       "local_edits_rank0": local_events, "parallelism": f"docs bin-packed x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "traffic_note": "PMC counters cannot be read inside this process; FETCH_SIZE/WRITE_SIZE "
+                                         "of k_replay on this command are in profiles/*_traffic.json "
+                                         "(tools/gpu_bench.sh PMC=1)",
                          "kernel": "k_replay", "kernel_ms": avg_kernel_ms,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes, "alg_bytes_node": total_alg},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -9,6 +9,12 @@
  * mergeTree.ts:1610). Per-doc PRNG: xoshiro256** seeded with splitmix64(seed_base + doc).
  *
  * Workloads (configs in BASELINE.json):
+ *   MTG_FARM      (config 1): the reference's TestClient conflict farm
+ *                  (test/mergeTreeOperationRunner.ts:58-178): nclients replicas of ONE document,
+ *                  clients 1..n-1 make local edits, client 0 only observes; each round first makes
+ *                  round_ops local edits (refSeq = the editor's currentSeq, MSN = round start), then
+ *                  sequences them in order and applies every message to every replica. Doc
+ *                  f * nclients + c is replica c of farm f (its local edits and every message).
  *   MTG_OBSERVER  (config 2): clients 1..n-1 edit, the replica (long id 0) only observes;
  *                  refSeq = MSN = seq - 1.
  *   MTG_LAGGED    (config 3): replica = long id 1 with local edits acked up to ack_lag later;
@@ -132,6 +138,8 @@ static const char ALNUM[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxy
 /* fixed props table: annotate {key in b,i,u,c : value in 0,1,2,3,null} -> records 1..20;
  * insert props {s: v} for v in 0..4095 -> records 21..4116 (see mtg_props_table). */
 #define ANN_RECORDS 20
+#define INS_RECORDS 4096
+#define CLIENT_RECORDS 32 /* {client: "<name>"} for the farm's annotateRange (mergeTreeOperationRunner.ts:22-24) */
 static int ann_props(rng_t* r) { return 1 + uni(r, 0, ANN_RECORDS - 1); }
 
 /* Draw an op valid for perspective (refSeq, client); kind forced to insert on an empty view. */
@@ -392,8 +400,107 @@ static void gen_matrix_t(const mtg_params* P, int64_t doc, Out* o, const mt_prop
     model_free(&m[1]);
 }
 
+
+/* MTG_FARM (config 1): runMergeTreeOperationRunner / generateOperationMessagesForClients /
+ * applyMessages (mergeTreeOperationRunner.ts:58-178) with the farm's op set
+ * [removeRange, annotateRange, insert] (client.conflictFarm.spec.ts:25-29; the insert is
+ * position-based, insertSegmentLocal, instead of insertAtReferencePosition). Every replica is
+ * modelled; doc `doc` emits the stream of replica doc % nclients of farm doc / nclients. */
+template <class HT>
+static void gen_farm_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {
+    int n = P->nclients < 2 ? 2 : P->nclients;
+    if (n > 32) n = 32;
+    int me = (int)(doc % n);
+    rng_t r;
+    seed(&r, P->seed_base + (uint64_t)(doc / n));
+    Model<HT>* m = new Model<HT>[n];
+    for (int c = 0; c < n; c++) {
+        model_init(&m[c], P, c);
+        if (!m[c].ok) {
+            o->overflow = 1;
+            delete[] m;
+            return;
+        }
+        m[c].props = props;
+        m[c].kv = kv;
+        m[c].text = o->text;
+    }
+    int round_ops = P->round_ops > 0 ? P->round_ops : 100;
+    mt_op_rec* round = (mt_op_rec*)malloc(sizeof(mt_op_rec) * round_ops);
+    int32_t seq = 0;
+    int done = 0;
+    bool bad = false;
+    while (done < P->ops_per_doc && !o->overflow && !bad) {
+        int32_t msn = seq; /* minimumSequenceNumber = the round's starting seq (runner.ts:103, 138) */
+        int nr = 0;
+        for (int i = 0; i < round_ops && done + nr < P->ops_per_doc; i++) {
+            int c = uni(&r, 1, n - 1);
+            int32_t len = m[c].r->length_local();
+            mt_op_rec e;
+            memset(&e, 0, sizeof e);
+            int kind;
+            int32_t start, end = 0;
+            if (len == 0 || len < P->min_length) {
+                kind = MT_OP_INSERT;
+                start = uni(&r, 0, len);
+            } else {
+                int oi = uni(&r, 0, 2); /* [removeRange, annotateRange, insert] */
+                start = uni(&r, 0, len - 1);
+                end = uni(&r, start + 1, len);
+                kind = oi == 0 ? MT_OP_REMOVE : oi == 1 ? MT_OP_ANNOTATE : MT_OP_INSERT;
+            }
+            e.kind = (uint8_t)kind;
+            e.pos1 = start;
+            if (kind == MT_OP_INSERT) { /* text = longClientId.repeat(1..3) (runner.ts:29, 113) */
+                int rep = uni(&r, 1, 3);
+                if (o->ntext + rep > o->tcap) {
+                    o->overflow = 1;
+                    break;
+                }
+                e.text_off = (uint32_t)o->ntext;
+                for (int k = 0; k < rep; k++) o->text[o->ntext++] = (uint16_t)ALNUM[c];
+                e.text_len = (uint16_t)rep;
+            } else {
+                e.pos2 = end;
+                if (kind == MT_OP_ANNOTATE) e.props = (uint16_t)(1 + ANN_RECORDS + INS_RECORDS + c);
+            }
+            e.client = (uint16_t)c;
+            e.seq = -1;
+            e.ref_seq = m[c].r->h.currentSeq; /* makeOpMessage: getCurrentSeq() (testClient.ts:213-234) */
+            e.min_seq = msn;
+            mt_op_rec loc = e;
+            loc.kind |= MT_OPF_LOCAL;
+            m_apply(&m[c], &loc);
+            if (c == me) {
+                mt_op_rec* x = emit(o);
+                if (!x) break;
+                *x = loc;
+            }
+            round[nr++] = e;
+        }
+        /* applyMessages: sequence in order, every replica applies every message */
+        for (int i = 0; i < nr && !o->overflow; i++) {
+            mt_op_rec e = round[i];
+            e.seq = ++seq;
+            for (int c = 0; c < n; c++) m_apply(&m[c], &e);
+            mt_op_rec* x = emit(o);
+            if (!x) break;
+            *x = e;
+        }
+        done += nr;
+        for (int c = 0; c < n; c++)
+            if (m[c].r->h.err) bad = true;
+    }
+    if (bad) o->overflow = 2;
+    free(round);
+    for (int c = 0; c < n; c++) model_free(&m[c]);
+    delete[] m;
+}
+
 static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {
-    if (P->mode == MTG_MATRIX)
+    if (P->mode == MTG_FARM)
+        gen_farm_t<HotMid>(P, doc, o, props, kv);
+    else if (P->mode == MTG_MATRIX)
         gen_matrix_t<HotMid>(P, doc, o, props, kv);
     else if (P->model_ncap > HotMid::N)
         gen_doc_t<HotBig>(P, doc, o, props, kv);
@@ -404,6 +511,7 @@ static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec
 /* ---- batch API --------------------------------------------------------------------------- */
 typedef struct {
     const mtg_params* P;
+    const int64_t* ids; /* document ids to generate (nullptr: doc_base + i) */
     int64_t doc_base, ndocs, op_stride, text_stride;
     int tid, threads;
     mt_op_rec* ops;
@@ -418,36 +526,47 @@ static void* worker(void* p) {
     Job* j = (Job*)p;
     for (int64_t d = j->tid; d < j->ndocs; d += j->threads) {
         Out o = {j->ops + d * j->op_stride, 0, j->op_stride, j->text + d * j->text_stride, 0, j->text_stride, 0};
-        gen_doc(j->P, j->doc_base + d, &o, j->props, j->kv);
+        gen_doc(j->P, j->ids ? j->ids[d] : j->doc_base + d, &o, j->props, j->kv);
         j->nops[d] = o.nops;
         j->ntext[d] = o.ntext;
         if (o.overflow) *j->status = o.overflow == 2 ? -2 : -1;
     }
     return NULL;
 }
-extern "C" int mtg_generate(const mtg_params* P, int64_t doc_base, int64_t ndocs, int64_t op_stride,
-                            int64_t text_stride, mt_op_rec* ops, int64_t* nops, uint16_t* text, int64_t* ntext,
-                            int threads) {
+static int generate(const mtg_params* P, const int64_t* ids, int64_t doc_base, int64_t ndocs, int64_t op_stride,
+                    int64_t text_stride, mt_op_rec* ops, int64_t* nops, uint16_t* text, int64_t* ntext, int threads) {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
-    static mt_props_rec props[20 + 4096];
-    static mt_kv kv[20 + 4096];
+    static mt_props_rec props[ANN_RECORDS + INS_RECORDS + CLIENT_RECORDS];
+    static mt_kv kv[ANN_RECORDS + INS_RECORDS + CLIENT_RECORDS];
     mtg_props_table(props, kv);
     pthread_t th[256];
     Job jobs[256];
     int status = 0;
     for (int t = 0; t < threads; t++) {
-        jobs[t] = Job{P, doc_base, ndocs, op_stride, text_stride, t, threads, ops, nops, text, ntext, &status,
+        jobs[t] = Job{P, ids, doc_base, ndocs, op_stride, text_stride, t, threads, ops, nops, text, ntext, &status,
                       props, kv};
         pthread_create(&th[t], NULL, worker, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     return status;
 }
+extern "C" int mtg_generate(const mtg_params* P, int64_t doc_base, int64_t ndocs, int64_t op_stride,
+                            int64_t text_stride, mt_op_rec* ops, int64_t* nops, uint16_t* text, int64_t* ntext,
+                            int threads) {
+    return generate(P, nullptr, doc_base, ndocs, op_stride, text_stride, ops, nops, text, ntext, threads);
+}
+/* the same for an explicit list of document ids (a rank's bin-packed shard, shard.assign) */
+extern "C" int mtg_generate_ids(const mtg_params* P, const int64_t* ids, int64_t ndocs, int64_t op_stride,
+                                int64_t text_stride, mt_op_rec* ops, int64_t* nops, uint16_t* text, int64_t* ntext,
+                                int threads) {
+    return generate(P, ids, 0, ndocs, op_stride, text_stride, ops, nops, text, ntext, threads);
+}
 
 /* The fixed props table every generated doc shares: records 1..20 annotate one key of
  * {b,i,u,c} (key ids 1..4) with value ids for JSON 0,1,2,3 (value id = v + 1; "0" is falsy)
- * or null; records 21..4116 are insert props {s: v}, key id 5, v in 0..4095. */
+ * or null; records 21..4116 are insert props {s: v}, key id 5, v in 0..4095; records
+ * 4117..4148 are the farm's {client: "<name of client k>"}, key id 6, value id 4097 + k. */
 extern "C" int mtg_props_table(mt_props_rec* props, mt_kv* kv) {
     int n = 0;
     for (int k = 0; k < 4; k++)
@@ -467,6 +586,15 @@ extern "C" int mtg_props_table(mt_props_rec* props, mt_kv* kv) {
         props[n]._pad = 0;
         kv[n].key = 5;
         kv[n].value = (uint16_t)((v + 1) | (v == 0 ? MT_VALUE_FALSY : 0));
+        n++;
+    }
+    for (int k = 0; k < CLIENT_RECORDS; k++) {
+        props[n].kv_off = (uint32_t)n;
+        props[n].nkv = 1;
+        props[n].combining = MT_COMBINE_NONE;
+        props[n]._pad = 0;
+        kv[n].key = 6;
+        kv[n].value = (uint16_t)(INS_RECORDS + 1 + k);
         n++;
     }
     return n;

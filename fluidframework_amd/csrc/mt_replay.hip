@@ -180,12 +180,12 @@ template <class HT>
 __global__ __launch_bounds__(WG) void k_digest(Store<HT> st, int64_t ndocs, uint64_t* out) {
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
-    /* A compiler memory barrier first: without it, the store-free read kernels let the compiler
-     * fetch the document through scalar (SMEM) loads, which returned wrong values for some
-     * documents on gfx950 with the leaf-line layout; vector loads are correct. */
-    __asm__ volatile("" ::: "memory");
+    /* The compiler reads the document here with scalar (SMEM) loads, including the
+     * base + SGPR-offset + immediate form no other kernel uses. Round 1 put a compiler barrier here
+     * after a digest mismatch; tools/smem_probe.hip shows that form (compiler- and asm-emitted)
+     * returns what vector loads return, the round-1 failing case is clean without the barrier, and
+     * tests/test_gpu_parity.py checks this digest against FNV-1a of k_dump for every document. */
     Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
-    __asm__ volatile("" ::: "memory");
     uint64_t h = r.digest();
     if (threadIdx.x == 0) out[d] = h;
 }
@@ -200,9 +200,7 @@ __global__ __launch_bounds__(WG) void k_dump(Store<HT> st, int64_t doc, uint8_t*
 template <class HT>
 __global__ __launch_bounds__(WG) void k_length(Store<HT> st, int64_t doc, int32_t ref_seq, int32_t long_client,
                                               int32_t* out) {
-    __asm__ volatile("" ::: "memory"); /* vector loads only (see k_digest) */
     Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
-    __asm__ volatile("" ::: "memory");
     int32_t v;
     if (long_client < 0) {
         v = r.length_local();
@@ -345,8 +343,13 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->ndocs = ndocs;
     const char* g = getenv("MT_REPLAY_LDS");
     e->lds = g && g[0] == '1';
+    /* Occupancy of the HBM-resident small-profile kernel: documents are replayed one per wave and
+     * a document's events are sequential, so a batch runs in "rounds" of 1,024 x waves documents
+     * (256 CUs x 4 SIMDs). 7 waves/SIMD is fastest per wave (8 spills registers: 168 vs 174 Mops/s
+     * at 32k docs), but a small batch (a strong-scaled shard: 8,192 or 16,384 docs per GPU) is
+     * better served by 8, which runs it in 1 or 2 full rounds instead of a last partial one. */
     const char* wv = getenv("MT_REPLAY_WAVES");
-    e->waves = wv ? atoi(wv) : 7;
+    e->waves = wv ? atoi(wv) : (ndocs <= 16384 ? 8 : 7);
     const char* ms = getenv("MT_REPLAY_MAT_SKEL");
     e->mat_skel = ms ? atoi(ms) : 2;
     e->profile = prof;

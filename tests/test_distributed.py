@@ -1,8 +1,13 @@
-"""The N > 1 path on CPU (gloo, world size 2): each rank replays its own shard of documents
-(shard.doc_range) with no data-path collective, then the per-document digests are all-gathered
-(shard.gather_digests) and must equal a single-process replay of all documents. The replay here is
-the CPU oracle (no GPU in this tier); bench.py runs the same shard/gather code over RCCL with the
-HIP engine."""
+"""The N > 1 path on CPU (gloo, world size 2).
+
+- Weak form: each rank replays its own block of documents (shard.weak_ids).
+- Strong form (bench.py's default for N > 1): one set of documents of UNEQUAL sizes is split over
+  the ranks by cost bin-packing (shard.assign), each rank replays only its shard, and the digests
+  are all-gathered (shard.gather_digests, ranks holding different counts) and put back in document
+  order (shard.in_doc_order).
+Either way the gathered digests must equal a single-process replay of all documents. The replay
+here is the CPU oracle (no GPU in this tier); bench.py runs the same shard/gather code over RCCL
+with the HIP engine."""
 import os
 import socket
 
@@ -10,9 +15,11 @@ import numpy as np
 import torch.multiprocessing as mp
 
 from fluidframework_amd import gen, shard
+from fluidframework_amd import oplog as ol
 
 DOCS_PER_RANK = 24
 OPS = 400
+STRONG_DOCS = 37
 
 
 def _free_port():
@@ -23,17 +30,32 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out):
-    import sys
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    import torch.distributed as dist
-    import oracle_client as oc
+def _unequal_batch() -> ol.Batch:
+    """STRONG_DOCS config-3 logs cut to very different lengths (a prefix of a replica's event
+    stream is itself a valid stream)."""
+    full = gen.generate(gen.config3(OPS), STRONG_DOCS, threads=2)
+    per = []
+    for d in range(STRONG_DOCS):
+        ops, text, props, kv = full.doc(d)
+        keep = 20 + (d * 97) % (len(ops) - 20)
+        per.append((ops[:keep], text, props, kv))
+    return ol.Batch.from_arrays(per, full.local_long_id)
 
+
+def _init(rank, world, port):
+    import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    base, n = shard.doc_range(rank, DOCS_PER_RANK)
-    b = gen.generate(gen.config3(OPS), n, doc_base=base, threads=2)
+    return dist
+
+
+def _weak_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle_client as oc
+    dist = _init(rank, world, port)
+    b = gen.generate(gen.config3(OPS), ids=shard.weak_ids(rank, DOCS_PER_RANK), threads=2)
     secs, dig, err = oc.replay_batch(b, threads=2)
     assert (err == 0).all()
     allg = shard.gather_digests(dig, dist)
@@ -47,12 +69,30 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_rank_shards_match_single_process(tmp_path):
+def _strong_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle_client as oc
+    dist = _init(rank, world, port)
+    full = _unequal_batch()
+    costs = np.diff(full.op_off)
+    parts = shard.assign(costs, world)
+    mine = full.subset(parts[rank])
+    _, dig, err = oc.replay_batch(mine, threads=2)
+    assert (err == 0).all()
+    allg = shard.in_doc_order(shard.gather_digests(dig, dist), parts, full.ndocs)
+    if rank == 0:
+        np.save(out, allg)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_weak_shards_match_single_process(tmp_path):
     import oracle_client as oc
 
     out = str(tmp_path / "dig.npy")
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_weak_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     gathered = np.load(out)
     full = gen.generate(gen.config3(OPS), DOCS_PER_RANK * world, threads=2)
     _, want, err = oc.replay_batch(full, threads=2)
@@ -61,3 +101,31 @@ def test_two_rank_shards_match_single_process(tmp_path):
     assert (gathered == want).all()
     tmax, total = open(out + ".meta").read().split()
     assert float(tmax) > 0 and int(total) == full.nops
+
+
+def test_two_rank_binpacked_unequal_docs_match_single_process(tmp_path):
+    import oracle_client as oc
+
+    out = str(tmp_path / "dig.npy")
+    world = 2
+    mp.spawn(_strong_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    full = _unequal_batch()
+    _, want, err = oc.replay_batch(full, threads=2)
+    assert (err == 0).all()
+    assert (np.load(out) == want).all()
+
+
+def test_assign_balances_and_covers():
+    rng = np.random.default_rng(7)
+    for world in (1, 2, 3, 8):
+        costs = rng.integers(1, 1000, size=101)
+        parts = shard.assign(costs, world)
+        ids = np.sort(np.concatenate(parts))
+        assert (ids == np.arange(101)).all()  # every document exactly once
+        ld = shard.loads(costs, parts)
+        lower = max(costs.sum() / world, costs.max())
+        assert ld.max() <= 4 / 3 * lower + 1e-9  # LPT bound
+        assert shard.assign(costs, world)[0].tolist() == parts[0].tolist()  # deterministic
+    # equal costs: an even split
+    parts = shard.assign(np.ones(65536), 8)
+    assert all(len(p) == 8192 for p in parts)

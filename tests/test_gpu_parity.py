@@ -19,7 +19,27 @@ def _engine(ndocs, ops_per_doc, **caps):
     return Engine(ndocs, **c)
 
 
-def _check_batch(b: ol.Batch, ops_per_doc: int, ndump: int = 4, **caps):
+def fnv1a64(bs: bytes) -> int:
+    h = 0xcbf29ce484222325
+    for x in bs:
+        h = ((h ^ x) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def _check_every_doc(eng, b: ol.Batch, gdig: np.ndarray):
+    """For EVERY document: the device digest (k_digest) is FNV-1a-64 of the device's own canonical
+    dump (k_dump), and the device text and local length equal the oracle's."""
+    for d in range(b.ndocs):
+        dump = eng.dump(d)
+        assert fnv1a64(dump) == int(gdig[d]), f"doc {d}: k_digest != FNV-1a(k_dump)"
+        c = oc.OracleClient()
+        c.start_collab(int(b.local_long_id[d]))
+        c.replay_arrays(*b.doc(d))
+        assert eng.get_text(d) == c.get_text(), f"doc {d}: text"
+        assert eng.get_length(d) == c.get_length(), f"doc {d}: length"
+
+
+def _check_batch(b: ol.Batch, ops_per_doc: int, ndump: int = 4, every: bool = False, **caps):
     secs, odig, oerr = oc.replay_batch(b, threads=8)
     assert (oerr == 0).all()
     eng = _engine(b.ndocs, ops_per_doc, **caps)
@@ -38,6 +58,8 @@ def _check_batch(b: ol.Batch, ops_per_doc: int, ndump: int = 4, **caps):
         ho, so = parse_dump(c.dump())
         hg, sg = parse_dump(eng.dump(d))
         raise AssertionError(f"{len(bad)} docs differ; doc {d}: oracle hdr {ho} gpu hdr {hg}")
+    if every:
+        _check_every_doc(eng, b, gdig)
     for d in range(min(ndump, b.ndocs)):
         ops, text, props, kv = b.doc(d)
         c = oc.OracleClient()
@@ -51,12 +73,12 @@ def _check_batch(b: ol.Batch, ops_per_doc: int, ndump: int = 4, **caps):
 
 def test_observer_config2_small():
     b = gen.generate(gen.config2(2000), 96)
-    _check_batch(b, 2000)
+    _check_batch(b, 2000, every=True)
 
 
 def test_lagged_local_config3_small():
     b = gen.generate(gen.config3(2048), 128)
-    eng = _check_batch(b, 2048)
+    eng = _check_batch(b, 2048, every=True)
     # perspective lengths for a few remote clients at the current seq
     for d in range(4):
         ops, text, props, kv = b.doc(d)
@@ -67,6 +89,16 @@ def test_lagged_local_config3_small():
         for k in (0, 2, 5):
             assert eng.get_length(d, cur, k) == c.get_length_at(cur, k)
             assert eng.get_text(d, cur, k) == c.get_text_at(cur, k)
+
+
+def test_farm_config1():
+    """Config 1: the reference's conflict farm (8 replicas of one document, rounds of 100 local
+    edits then sequencing); every replica matches the oracle and all replicas converge."""
+    b = gen.generate(gen.config1(10000), 16)
+    eng = _check_batch(b, 10000, every=True)
+    for f in range(2):
+        texts = {eng.get_text(8 * f + c) for c in range(8)}
+        assert len(texts) == 1
 
 
 def test_incremental_submits_match_one_shot():
@@ -108,7 +140,7 @@ def test_matrix_permutation_vectors_config5():
     annotate-heavy) in the 640-node profile; perspective lengths of remote clients agree too."""
     from fluidframework_amd.engine import default_caps
     b = gen.generate(gen.config5(4096), 64)
-    eng = _check_batch(b, 4096, **default_caps(4096, config=5))
+    eng = _check_batch(b, 4096, every=True, **default_caps(4096, config=5))
     for d in range(3):
         ops, text, props, kv = b.doc(d)
         c = oc.OracleClient()
