@@ -1,0 +1,207 @@
+// ref_replay.mjs — replays packed op logs (include/mt_oplog.h) through the REFERENCE merge-tree
+// (packages/dds/merge-tree/src, type-erased by tools/ts_erase.py into a scratch dir outside the
+// repo) and writes each replica's canonical segment dump (include/mt_oplog.h, the format
+// oracle/mt_oracle.c mto_dump emits). TEST INFRASTRUCTURE: golden-vector generation only
+// (tools/make_ref_goldens.py); nothing in the product path runs it and it never reaches the GPU box.
+//
+// usage: node ref_replay.mjs <erased-dir> <batch-dir> [--time]
+//   batch-dir: ops.bin op_off.bin text.bin text_off.bin props.bin props_off.bin kv.bin kv_off.bin
+//              local.bin meta.json (written by make_ref_goldens.py)
+//   writes batch-dir/ref_dumps.bin + ref_dump_off.bin (+ ref_err.json: per-doc thrown errors)
+import fs from "fs";
+import path from "path";
+
+const [erased, dir] = process.argv.slice(2);
+const timeOnly = process.argv.includes("--time");
+let Client, TextSegment, Marker, PermutationSegment; // bound in main() (Node 12 has no top-level await)
+
+const rd = (f) => fs.readFileSync(path.join(dir, f));
+const meta = JSON.parse(rd("meta.json"));
+const ops = rd("ops.bin"), text = rd("text.bin"), props = rd("props.bin"), kv = rd("kv.bin");
+const i64 = (f) => { const b = rd(f); return Array.from({ length: b.length / 8 }, (_, i) => Number(b.readBigInt64LE(8 * i))); };
+const opOff = i64("op_off.bin"), textOff = i64("text_off.bin"), propsOff = i64("props_off.bin"), kvOff = i64("kv_off.bin");
+const localIds = rd("local.bin");
+const keys = meta.keys, values = meta.values; // interner tables: id -> key string / canonical JSON
+const keyId = new Map(keys.map((k, i) => [k, i]));
+const valueId = new Map(values.map((v, i) => [v, i]));
+const FALSY = 0x8000;
+
+const name = (longId) => `c${longId}`;
+const longOfName = (s) => (s === "original" ? -1 : Number(s.slice(1)));
+
+function canonical(v) {
+    if (v === null || typeof v !== "object") return JSON.stringify(v);
+    if (Array.isArray(v)) return "[" + v.map(canonical).join(",") + "]";
+    return "{" + Object.keys(v).sort().map((k) => JSON.stringify(k) + ":" + canonical(v[k])).join(",") + "}";
+}
+
+function propSet(doc, idx) {
+    if (!idx) return undefined;
+    const p = (propsOff[doc] + idx - 1) * 8;
+    const off = props.readUInt32LE(p), nkv = props.readUInt16LE(p + 4), comb = props.readUInt8(p + 6);
+    const set = {};
+    for (let j = 0; j < nkv; j++) {
+        const q = (kvOff[doc] + off + j) * 4;
+        const k = kv.readUInt16LE(q), v = kv.readUInt16LE(q + 2) & ~FALSY;
+        set[keys[k]] = v === 0 ? null : JSON.parse(values[v]);
+    }
+    return { set, combiningOp: comb === 1 ? { name: "rewrite" } : undefined };
+}
+
+function textOf(doc, rec) {
+    const off = textOff[doc] + rec.text_off;
+    let s = "";
+    for (let j = 0; j < rec.text_len; j++) s += String.fromCharCode(text.readUInt16LE(2 * (off + j)));
+    return s;
+}
+
+function record(i) {
+    const b = 32 * i;
+    return {
+        kind: ops.readUInt8(b), seg_kind: ops.readUInt8(b + 1), client: ops.readUInt16LE(b + 2),
+        seq: ops.readInt32LE(b + 4), ref_seq: ops.readInt32LE(b + 8), min_seq: ops.readInt32LE(b + 12),
+        pos1: ops.readInt32LE(b + 16), pos2: ops.readInt32LE(b + 20), text_off: ops.readUInt32LE(b + 24),
+        text_len: ops.readUInt16LE(b + 28), props: ops.readUInt16LE(b + 30),
+    };
+}
+
+// the wire op (IMergeTreeOp, ops.ts:63-102) a record stands for
+function wireOp(doc, rec) {
+    const kind = rec.kind & 7;
+    const ps = propSet(doc, rec.props);
+    if (kind === 0) {
+        let seg;
+        if (rec.seg_kind === 2) return { type: 0, pos1: rec.pos1, seg: new PermutationSegment(rec.text_len).toJSONObject() };
+        if (rec.seg_kind === 1) seg = { marker: { refType: rec.pos2 } };
+        else seg = ps ? { text: textOf(doc, rec) } : textOf(doc, rec);
+        if (ps) seg.props = ps.set;
+        return { type: 0, pos1: rec.pos1, seg };
+    }
+    if (kind === 1) return { type: 1, pos1: rec.pos1, pos2: rec.pos2 };
+    const op = { type: 2, pos1: rec.pos1, pos2: rec.pos2, props: ps ? ps.set : {} };
+    if (ps && ps.combiningOp) op.combiningOp = ps.combiningOp;
+    return op;
+}
+
+// SharedString's specToSegment; PermutationVector's (PermutationSegment.fromJSONObject) for array specs
+const specToSegment = (spec) => (Array.isArray(spec) ? PermutationSegment.fromJSONObject(spec)
+    : TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec));
+const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+
+function replayDoc(doc) {
+    const client = new Client(specToSegment, logger);
+    const local = localIds.readInt32LE(4 * doc);
+    if (local >= 0) client.startOrUpdateCollaboration(name(local));
+    for (let i = opOff[doc]; i < opOff[doc + 1]; i++) {
+        const rec = record(i);
+        const kind = rec.kind & 7;
+        if (rec.kind & 0x80) { // local edit: insertSegmentLocal / removeRangeLocal / annotateRangeLocal
+            if (kind === 0) {
+                const ps = propSet(doc, rec.props);
+                const seg = rec.seg_kind === 2 ? new PermutationSegment(rec.text_len)
+                    : rec.seg_kind === 1 ? Marker.make(rec.pos2, ps && ps.set) : TextSegment.make(textOf(doc, rec), ps && ps.set);
+                if (rec.seg_kind === 2 && ps) seg.addProperties(ps.set);
+                client.insertSegmentLocal(rec.pos1, seg);
+            } else if (kind === 1) {
+                client.removeRangeLocal(rec.pos1, rec.pos2);
+            } else if (kind === 2) {
+                const ps = propSet(doc, rec.props);
+                client.annotateRangeLocal(rec.pos1, rec.pos2, ps ? ps.set : {}, ps ? ps.combiningOp : undefined);
+            }
+            continue;
+        }
+        client.applyMsg({
+            clientId: name(rec.client), sequenceNumber: rec.seq, referenceSequenceNumber: rec.ref_seq,
+            minimumSequenceNumber: rec.min_seq, type: kind === 4 ? "noop" : "op",
+            contents: kind === 4 ? undefined : wireOp(doc, rec),
+        });
+    }
+    return client;
+}
+
+// ---- canonical dump (include/mt_oplog.h; the order and fields of oracle/mt_oracle.c mto_dump) ----
+class Out {
+    constructor() { this.parts = []; }
+    i32(v) { const b = Buffer.alloc(4); b.writeInt32LE(v); this.parts.push(b); }
+    u16(v) { const b = Buffer.alloc(2); b.writeUInt16LE(v); this.parts.push(b); }
+    u8(v) { this.parts.push(Buffer.from([v])); }
+    buf() { return Buffer.concat(this.parts); }
+}
+
+function dump(client) {
+    const mt = client.mergeTree;
+    const longOf = (shortId) => (shortId < 0 ? -1 : longOfName(client.getLongClientId(shortId)));
+    const leaves = [];
+    const walk = (b) => {
+        if (b.childCount === 0 || b.children[0].isLeaf()) { leaves.push(b); return; }
+        for (let i = 0; i < b.childCount; i++) walk(b.children[i]);
+    };
+    walk(mt.root);
+    let nsegs = 0;
+    for (const b of leaves) nsegs += b.childCount;
+    const o = new Out();
+    const cw = mt.collabWindow;
+    o.i32(cw.currentSeq); o.i32(cw.minSeq); o.i32(cw.localSeq); o.i32(mt.root.cachedLength);
+    o.i32(nsegs); o.i32(leaves.length);
+    leaves.forEach((b, li) => {
+        for (let i = 0; i < b.childCount; i++) {
+            const s = b.children[i];
+            const isText = s.type === "TextSegment", isMarker = s.type === "Marker";
+            const kind = isText ? 0 : isMarker ? 1 : 2;
+            const hasProps = s.properties !== undefined;
+            const removed = s.removedSeq !== undefined;
+            const ov = s.removedClientOverlap || [];
+            o.u8(kind);
+            o.u8((hasProps ? 1 : 0) | (removed ? 2 : 0) | (s.localSeq !== undefined ? 4 : 0) | (s.localRemovedSeq !== undefined ? 8 : 0));
+            o.u8(ov.length);
+            o.u8(s.segmentGroups.size);
+            o.i32(s.cachedLength); o.i32(s.seq); o.i32(longOf(s.clientId));
+            o.i32(removed ? s.removedSeq : 0); o.i32(removed ? longOf(s.removedClientId) : 0);
+            o.i32(s.localSeq !== undefined ? s.localSeq : 0);
+            o.i32(s.localRemovedSeq !== undefined ? s.localRemovedSeq : 0);
+            o.i32(li);
+            for (const c of ov) o.i32(longOf(c));
+            const pk = hasProps ? Object.keys(s.properties).map((k) => [keyId.get(k), s.properties[k]]).sort((a, b) => a[0] - b[0]) : [];
+            o.u16(pk.length);
+            o.u16(isMarker ? s.refType : 0);
+            for (const [k, v] of pk) {
+                const id = valueId.get(canonical(v));
+                if (k === undefined || id === undefined) throw new Error(`property not in the interner: ${k} ${canonical(v)}`);
+                const falsy = v !== null && typeof v !== "object" && !v;
+                o.u16(k); o.u16(id | (falsy ? FALSY : 0));
+            }
+            if (isText) for (let j = 0; j < s.text.length; j++) o.u16(s.text.charCodeAt(j));
+        }
+    });
+    return o.buf();
+}
+
+async function main() {
+const MT = await import(path.join(erased, "index.mjs"));
+({ Client, TextSegment, Marker } = MT);
+({ PermutationSegment } = await import(path.join(erased, "permutationSegment.mjs")));
+const ndocs = opOff.length - 1;
+const t0 = process.hrtime.bigint();
+const dumps = [], errs = {};
+for (let d = 0; d < ndocs; d++) {
+    try {
+        const c = replayDoc(d);
+        dumps.push(timeOnly ? Buffer.alloc(0) : dump(c));
+    } catch (e) {
+        errs[d] = String(e && e.message || e);
+        dumps.push(Buffer.alloc(0));
+    }
+}
+const secs = Number(process.hrtime.bigint() - t0) / 1e9;
+if (!timeOnly) {
+    const off = Buffer.alloc(8 * (ndocs + 1));
+    let acc = 0;
+    dumps.forEach((b, d) => { off.writeBigInt64LE(BigInt(acc), 8 * d); acc += b.length; });
+    off.writeBigInt64LE(BigInt(acc), 8 * ndocs);
+    fs.writeFileSync(path.join(dir, "ref_dumps.bin"), Buffer.concat(dumps));
+    fs.writeFileSync(path.join(dir, "ref_dump_off.bin"), off);
+}
+fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
+console.log(JSON.stringify({ ndocs, errors: Object.keys(errs).length, seconds: secs }));
+}
+main().catch((e) => { console.error(e); process.exit(1); });
