@@ -84,7 +84,13 @@ def cpu_baseline(batch, gpu_digests, workers: int, target_s: float = 15.0):
     secs, odig, oerr = oc.replay_batch(sample, threads=workers)
     s_seq = int(((sample.ops["kind"] & 0x80) == 0).sum())
     match = bool((odig == gpu_digests[:ns]).all()) and bool((oerr == 0).all())
+    calib = None
+    cpath = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
+    if os.path.exists(cpath):  # reference (type-erased TS under node) vs this restatement, one thread each
+        c = json.load(open(cpath))["cases"]
+        calib = {k: round(v["oracle_over_reference"], 2) for k, v in c.items()}
     return {"value": s_seq / secs, "unit": "ops/s", "cores": workers, "kind": "port",
+            "restatement_over_reference_speed": calib,
             "sample": f"first {ns} of this rank's {nd} docs ({s_seq} sequenced msgs), oracle/ C restatement "
                       f"of the reference B-tree (PartialSequenceLengths, zamboni), one document per thread, "
                       f"{workers} threads, {secs:.1f}s; digests match GPU: {match}"}
