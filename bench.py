@@ -10,13 +10,15 @@ Workloads (BASELINE.json configs; --config):
     local-pending replica with acks, 4,096 sequenced messages per document.
   1: the reference's TestClient conflict farm: 1 document x 8 replicas x 10k ops in rounds of 100.
   2: 4,096 documents x 10k ops, observer replica, refSeq = MSN = seq - 1.
+  4: 256 large documents x 1M sequenced messages (>400k live rows each at the end): the tiled
+    profile, one workgroup per document.
   5: SharedMatrix PermutationVector replay: 16,384 matrices x 2 vectors = 32,768 replicas.
 Multi-GPU (one process per GPU, torchrun): --docs is the NODE total and the documents are split
 over the ranks by cost bin-packing (shard.assign; "scaling": "strong", the metric's "ops/s per
 node at 65k docs"); --scaling weak gives every rank --docs documents of its own instead. No
 data-path collective; RCCL all-gathers per-document digests once, after timing.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|5] [--docs D]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|4|5] [--docs D]
                        [--ops-per-doc O] [--scaling strong|weak] [--no-cpu-baseline]
 """
 from __future__ import annotations
@@ -38,6 +40,9 @@ CONFIGS = {
                    "in rounds of 100, MSN = round start"),
     2: (4096, 10_000, "config2: docs x {ops} sequenced msgs, observer replica, refSeq = MSN = seq-1, 60/30/10"),
     3: (65536, 4096, "config3: docs x {ops} sequenced msgs, 8 clients, lag<=64, local-pending replica"),
+    4: (256, 1_000_000, "config4: {docs} large docs x {ops} sequenced msgs, lag<=64, 70/25/5, coalescing defeated "
+                        "(distinct insert props, 25% trailing newlines): >400k live rows per doc; tiled position "
+                        "index, one workgroup per doc"),
     5: (32768, 4096, "config5: SharedMatrix rows+cols PermutationVector replicas x {ops} sequenced msgs each, "
                      "8 clients, lag<=64, local-pending, 50% annotate"),
 }
@@ -64,7 +69,7 @@ def cpu_workers() -> int:
 
 def workload(config: int, ops: int):
     from fluidframework_amd import gen
-    return {1: gen.config1, 2: gen.config2, 3: gen.config3, 5: gen.config5}[config](ops)
+    return {1: gen.config1, 2: gen.config2, 3: gen.config3, 4: gen.config4, 5: gen.config5}[config](ops)
 
 
 def cpu_baseline(batch, gpu_digests, workers: int, target_s: float = 15.0):
@@ -75,13 +80,14 @@ def cpu_baseline(batch, gpu_digests, workers: int, target_s: float = 15.0):
     import oracle_client as oc
 
     nd = batch.ndocs
-    probe = min(nd, max(workers, 2 * workers))
-    secs, _, _ = oc.replay_batch(batch.subset(range(probe)), threads=workers)
-    ns = probe
-    if secs > 0 and secs < target_s:
-        ns = int(min(nd, max(probe, probe * target_s / secs)))
-    sample = batch.subset(range(ns))
+    probe = min(nd, workers)
+    sample = batch.subset(range(probe))
     secs, odig, oerr = oc.replay_batch(sample, threads=workers)
+    ns = probe
+    if secs > 0 and secs < target_s / 2 and probe < nd:
+        ns = int(min(nd, max(probe, probe * target_s / secs)))
+        sample = batch.subset(range(ns))
+        secs, odig, oerr = oc.replay_batch(sample, threads=workers)
     s_seq = int(((sample.ops["kind"] & 0x80) == 0).sum())
     match = bool((odig == gpu_digests[:ns]).all()) and bool((oerr == 0).all())
     calib = None
@@ -231,7 +237,10 @@ def main() -> None:
                                          "of k_replay on this command are in profiles/*_traffic.json "
                                          "(tools/gpu_bench.sh PMC=1)",
                          "kernel": "k_replay", "kernel_ms": avg_kernel_ms,
-                         "alg_bytes_per_launch": alg_bytes, "alg_bytes_node": total_alg},
+                         "alg_bytes_per_launch": alg_bytes, "alg_bytes_node": total_alg,
+                         "alg_formula": ("tile summaries (BASELINE.md): A(op) = 4 B x chunks + 64 B x window rows "
+                                         "+ 640 B + 32 B x rows written" if args.config == 4 else
+                                         "flat scan (BASELINE.md): A(op) = 16 B x rows + 32 B x rows written")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -22,6 +22,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/mt_oplog.h"
 
 #ifdef __HIPCC__
@@ -110,14 +112,58 @@ struct ColdRow {
     uint8_t pk[NKEYS];     /* pendingKeyUpdateCount per key slot */
 };
 
+/* Position index of the large-document profile ("tiled", config 4: >100k live rows).
+ *
+ * Leaf order is a two-level rope instead of one dense array (a dense `lorder` costs O(leaves) per
+ * leaf split): chunks of <= 64 leaves, kept in document order by `cord` (chunk ids by position).
+ * Each row is STABLE (settled at the current MSN and not removed: visible with its full length in
+ * every perspective the protocol can use, refSeq >= minSeq, and in the local one), W (in the
+ * collaboration window: seq or removedSeq above minSeq, or local-pending; evaluated exactly per
+ * op) or DEAD (removed at or below minSeq: invisible everywhere). Summaries hold only STABLE
+ * lengths: `lst` per leaf, `cst` per chunk position — the flattened, window-free part of the
+ * reference's PartialSequenceLengths (partialLengths.ts:218-274 `fromLeaves` splits a block's rows
+ * the same way: segments at or below minSeq fold into `minLength`, newer ones into partials).
+ * The W rows are a small set (`wrid`) re-evaluated under each op's perspective and scattered onto
+ * the chunk summaries; a position search is then chunk scan -> leaf scan -> row scan. */
+template <int N, bool T>
+struct TileState {
+    static constexpr int NCH = 1, WCAP = 1;
+};
+template <int N>
+struct TileState<N, true> {
+    static constexpr int CH = 64;       /* leaves per chunk */
+    static constexpr int NCH = N / 32;  /* chunk capacity (the kernel's LDS scratch holds NCH counters) */
+    static constexpr int WCAP = 4096;   /* window-set capacity (rows; ~500 in use at lag 64) */
+    int32_t nchunk, wN, cfree, nfreeChunk;
+    int32_t lst[N];         /* leaf node -> sum of its STABLE rows' lengths */
+    int32_t lch[N];         /* leaf node -> chunk id */
+    uint8_t lix[N];         /* leaf node -> index in its chunk */
+    uint8_t xf[N * 8];      /* slot -> XF_* state of the row it holds */
+    int32_t cord[NCH];      /* chunk ids in document order */
+    int32_t cst[NCH];       /* sum of lst over the chunk at each position */
+    int32_t cpos[NCH];      /* chunk id -> position (free chunks: next free id) */
+    int32_t ccnt[NCH];      /* chunk id -> leaf count */
+    int32_t cleaf[NCH][CH]; /* chunk id -> its leaves in order */
+    int32_t wrid[WCAP];     /* window set: row ids */
+    uint8_t wgen[WCAP];     /* their generations when added */
+    /* host-build scratch of a position search (the GPU kernel uses LDS instead) */
+    int32_t sdel[NCH];
+    int32_t swcp[WCAP], swvs[WCAP];
+    uint8_t swlx[WCAP];
+};
+enum : uint8_t { XF_STABLE = 1, XF_W = 2 };
+
 /* Hot per-document state with compile-time capacities: everything the per-op scans and the
- * tree skeleton touch. On the GPU this image lives in LDS for the whole replay. */
-template <int N_, int C_ = 64>
+ * tree skeleton touch. */
+template <int N_, int C_ = 64, bool TILED_ = false>
 struct HotT {
     static constexpr int N = N_;     /* B-tree nodes */
     static constexpr int S = N_ * 8; /* row slots (8 per leaf node) */
     static constexpr int H = N_ + 64; /* zamboni heap entries (config 3 peaks at 109) */
     static constexpr int C = C_;     /* clients */
+    static constexpr bool TILED = TILED_;
+    typedef typename std::conditional<TILED_, int32_t, int16_t>::type IX; /* node / row-id type */
+    typedef TileState<N_, TILED_> TL;
     DocHdr h;
     /* The scan columns of one leaf's 8 slots share one 128-byte line (leaf-major SoA): a
      * perspective scan that visits a leaf touches one cache line, not one line per column.
@@ -136,19 +182,20 @@ struct HotT {
     MT_HD uint8_t& flags(int s) { return lf[s >> 3].b[s & 7][2]; }
     MT_HD uint8_t& ng(int s) { return lf[s >> 3].b[s & 7][3]; }
     MT_HD const int32_t* bytes4(int s) { return (const int32_t*)&lf[s >> 3].b[s & 7][0]; }
-    int16_t rid[S];   /* slot -> row id (stable identity of a segment; cold data index) */
-    int16_t rleaf[S]; /* row id -> leaf node currently holding it */
+    IX rid[S];   /* slot -> row id (stable identity of a segment; cold data index) */
+    IX rleaf[S]; /* row id -> leaf node currently holding it */
     uint8_t rgen[S]; /* row id -> generation, bumped when the id is freed */
-    int16_t nparent[N], lorder[N], lpos[N];
-    int16_t kids[N * 8];
+    IX nparent[N], lorder[N], lpos[N]; /* lorder / lpos: dense leaf order (not used when TILED) */
+    IX kids[N * 8];
     int8_t nchild[N], nlevel[N], nscour[N];
     int8_t _pad[(16 - (3 * N) % 16) % 16];
     int32_t hseq[H];
-    int16_t hrid[H];  /* segment (row id) queued for scouring */
+    IX hrid[H];  /* segment (row id) queued for scouring */
     uint8_t hgen[H];  /* its row-id generation when queued: a mismatch means it was unlinked */
     uint16_t s2l[C];  /* short client id -> long id (client.ts:637-661) */
     uint8_t l2s[C];   /* long id (< C) -> short id, 0xFF = not seen yet */
     uint16_t keys[NKEYS]; /* property key id of each doc key slot */
+    TileState<N_, TILED_> tl;
 };
 
 /* LDS-sized profile for config 2/3 documents (39.5 KB <= 160 KB / 4: 4 documents per CU; the
@@ -158,6 +205,7 @@ typedef HotT<192> HotSmall;
 typedef HotT<640> HotMat; /* config 5: PermutationVector replicas peak at ~540 nodes */
 typedef HotT<2048> HotMid;
 typedef HotT<16384> HotBig;
+typedef HotT<(1 << 18), 64, true> HotHuge; /* config 4: tiled position index, 32-bit ids (1M-op docs: ~112k nodes) */
 
 struct alignas(16) I4 {
     int32_t x[4];
@@ -184,7 +232,7 @@ template <class HT>
 struct Doc {
     HT* t;
     ColdRow* cold; /* HT::S records */
-    int16_t* frid;   /* free cold-row-id stack, HT::S entries */
+    typename HT::IX* frid; /* free cold-row-id stack, HT::S entries */
     uint16_t* arena; /* 2 * acap */
     int32_t* mgid;
     int32_t* mrid; /* row id of each membership entry */
@@ -222,6 +270,8 @@ struct ProfScope {
  * ---------------------------------------------------------------------------------------- */
 template <class W, class HT>
 struct Replica {
+    typedef typename HT::IX IX;
+    static constexpr bool TILED = HT::TILED;
     Doc<HT> d;
     HT& z; /* the hot image */
     W w;
@@ -234,19 +284,33 @@ struct Replica {
     /* The tree skeleton's small per-node arrays and the zamboni heap are reached through these
      * pointers: they point into the image by default, and the HBM-resident GPU kernel points them
      * at LDS copies for the duration of a replay (latency-critical, 3.5 KB per document). */
-    int16_t* lo;  /* lorder */
-    int16_t* lp;  /* lpos */
-    int16_t* npar;
+    IX* lo;  /* lorder */
+    IX* lp;  /* lpos */
+    IX* npar;
     int8_t* nch;
     int8_t* nlev;
     int8_t* nsc;
     int32_t* hsq;
-    int16_t* hrd;
+    IX* hrd;
     uint8_t* hgn;
+    /* tiled profile: scratch of a position search — per-chunk window deltas (all zero between
+     * searches) and per window row its chunk position, leaf index and perspective length. The image
+     * holds host copies; the GPU kernel points them at LDS. */
+    int32_t* cdel;
+    int32_t* wcp;
+    int32_t* wvs;
+    uint8_t* wlx;
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
         : d(doc), z(*doc.t), w(wave), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
-          nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen) {
+          nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen), cdel(nullptr), wcp(nullptr), wvs(nullptr),
+          wlx(nullptr) {
+        if constexpr (TILED) {
+            cdel = z.tl.sdel;
+            wcp = z.tl.swcp;
+            wvs = z.tl.swvs;
+            wlx = z.tl.swlx;
+        }
         load_hdr();
     }
 
@@ -289,6 +353,7 @@ struct Replica {
         nch[n] = 0;
         nlev[n] = level;
         nsc[n] = -1; /* needsScour undefined */
+        if constexpr (TILED) z.tl.lst[n] = 0;
         clear_slots(n * MAXN, MAXN);
         return n;
     }
@@ -302,7 +367,7 @@ struct Replica {
         w.sync();
     }
     MT_HD void free_node(int32_t n) {
-        npar[n] = (int16_t)h.freeHead;
+        npar[n] = (IX)h.freeHead;
         nch[n] = 0;
         h.freeHead = n;
         h.nfree++;
@@ -315,7 +380,7 @@ struct Replica {
         for (int32_t b = 0; b < ncap; b += W::N) {
             int32_t n = b + w.lane();
             if (n < ncap) {
-                npar[n] = (int16_t)(n + 1 < ncap ? n + 1 : -1);
+                npar[n] = (IX)(n + 1 < ncap ? n + 1 : -1);
                 nch[n] = 0;
                 nlev[n] = 0;
                 nsc[n] = -1;
@@ -324,7 +389,7 @@ struct Replica {
         for (int32_t b = 0; b < HT::S; b += W::N) {
             int32_t i = b + w.lane();
             if (i < HT::S) {
-                d.frid[i] = (int16_t)(HT::S - 1 - i);
+                d.frid[i] = (IX)(HT::S - 1 - i);
                 z.rgen[i] = 0;
                 z.len(i) = 0;
                 z.seq(i) = 0;
@@ -334,9 +399,11 @@ struct Replica {
                 z.flags(i) = 0;
                 z.ng(i) = 0;
                 z.rid[i] = 0;
+                if constexpr (TILED) z.tl.xf[i] = 0;
             }
         }
         w.sync();
+        if constexpr (TILED) rope_init();
         h.nfreeRid = HT::S;
         h.gcEpoch = 0;
         h.freeHead = 1;
@@ -443,16 +510,45 @@ struct Replica {
     /* localNetLength (mergeTree.ts:1195-1206) */
     MT_HD int32_t local_len(int32_t s) const { return z.rseq(s) == NOREM ? z.len(s) : 0; }
 
-    MT_HD int32_t slot_at(int32_t t) const { /* t = k*8+j over lorder; -1 if not a row */
+    MT_HD int32_t slot_at(int32_t t) const { /* t = k*8+j over the leaf order; -1 if not a row */
         int32_t k = t >> 3, j = t & 7;
-        if (k >= h.nleaf) return -1;
-        int32_t n = lo[k];
+        if (!kvalid(k)) return -1;
+        int32_t n = leaf_at(k);
         return j < nch[n] ? n * MAXN + j : -1;
+    }
+
+    /* ---- leaf order: the dense `lorder`, or the tiled rope (TileState) ------------------ */
+    /* A leaf position k is an index into lorder, or (chunk position << 6 | index in chunk) when
+     * TILED; positions increase in document order (with gaps when tiled). */
+    MT_HD int32_t leaf_at(int32_t k) const {
+        if constexpr (TILED)
+            return z.tl.cleaf[z.tl.cord[k >> 6]][k & 63];
+        else
+            return lo[k];
+    }
+    MT_HD int32_t kpos(int32_t n) const {
+        if constexpr (TILED)
+            return (z.tl.cpos[z.tl.lch[n]] << 6) | z.tl.lix[n];
+        else
+            return lp[n];
+    }
+    MT_HD bool kvalid(int32_t k) const {
+        if constexpr (TILED)
+            return k >= 0 && (k >> 6) < z.tl.nchunk && (k & 63) < z.tl.ccnt[z.tl.cord[k >> 6]];
+        else
+            return k < h.nleaf;
+    }
+    MT_HD int32_t knext(int32_t k) const {
+        if constexpr (TILED)
+            return (k & 63) + 1 < z.tl.ccnt[z.tl.cord[k >> 6]] ? k + 1 : ((k >> 6) + 1) << 6;
+        else
+            return k + 1;
     }
 
     /* copy every column of row a to row b (same doc) */
     /* move row a's slot contents to slot b (hot columns + its cold row id) */
     MT_HD void copy_row(int32_t b, int32_t a) {
+        if constexpr (TILED) z.tl.xf[b] = z.tl.xf[a];
         z.len(b) = z.len(a);
         z.seq(b) = z.seq(a);
         z.rseq(b) = z.rseq(a);
@@ -465,8 +561,9 @@ struct Replica {
     /* a row's slot contents held in registers */
     struct HotRow {
         int32_t len, seq, rseq;
-        int16_t rid;
+        IX rid;
         uint8_t cli, rcli, flags, ng;
+        uint8_t xf; /* tiled profile: XF_* */
     };
     MT_HD HotRow load_row(int32_t a) const {
         HotRow r;
@@ -478,6 +575,8 @@ struct Replica {
         r.rcli = z.rcli(a);
         r.flags = z.flags(a);
         r.ng = z.ng(a);
+        r.xf = 0;
+        if constexpr (TILED) r.xf = z.tl.xf[a];
         return r;
     }
     MT_HD void store_row(int32_t b, const HotRow& r) {
@@ -489,6 +588,7 @@ struct Replica {
         z.rcli(b) = r.rcli;
         z.flags(b) = r.flags;
         z.ng(b) = r.ng;
+        if constexpr (TILED) z.tl.xf[b] = r.xf;
     }
     /* shift slab rows [j, c) of leaf n right by one slot (wave-parallel: read all, then write) */
     MT_HD void slab_shift_right(int32_t n, int32_t j, int32_t c) {
@@ -525,8 +625,8 @@ struct Replica {
             int32_t x = ok ? lo[i] : 0;
             w.sync();
             if (ok) {
-                lo[i + delta] = (int16_t)x;
-                lp[x] = (int16_t)(i + delta);
+                lo[i + delta] = (IX)x;
+                lp[x] = (IX)(i + delta);
             }
             w.sync();
         }
@@ -543,14 +643,14 @@ struct Replica {
     }
     MT_HD void free_rid(int32_t r) {
         z.rgen[r]++;
-        d.frid[h.nfreeRid++] = (int16_t)r;
+        d.frid[h.nfreeRid++] = (IX)r;
     }
     /* record leaf n as the holder of its first `cnt` rows */
     MT_HD void set_leaf_of_rows(int32_t n, int32_t cnt) {
         for (int32_t b = 0; b < cnt; b += W::N) {
             int32_t j = b + w.lane();
             int32_t r = j < cnt ? z.rid[n * MAXN + j] : -1;
-            if (r >= 0) z.rleaf[r] = (int16_t)n;
+            if (r >= 0) z.rleaf[r] = (IX)n;
         }
         w.sync();
     }
@@ -567,6 +667,409 @@ struct Replica {
         int32_t j = w.lane();
         uint64_t m = w.ballot(j < c && z.rid[leaf * MAXN + (j & (MAXN - 1))] == rid);
         return m ? leaf * MAXN + W::ffs(m) : -1;
+    }
+
+    /* ---- tiled profile: rope of leaves, STABLE summaries, window set ------------------- */
+    MT_HD void rope_init() {
+        auto& t = z.tl;
+        constexpr int NCH = HT::TL::NCH;
+        for (int32_t b = 0; b < NCH; b += W::N) {
+            int32_t i = b + w.lane();
+            if (i < NCH) {
+                t.cpos[i] = i + 1; /* free list */
+                t.ccnt[i] = 0;
+                t.sdel[i] = 0;
+            }
+        }
+        w.sync();
+        t.nchunk = 1;
+        t.cord[0] = 0;
+        t.cpos[0] = 0;
+        t.cst[0] = 0;
+        t.ccnt[0] = 1;
+        t.cleaf[0][0] = 0;
+        t.cfree = 1;
+        t.nfreeChunk = NCH - 1;
+        t.lch[0] = 0;
+        t.lix[0] = 0;
+        t.lst[0] = 0;
+        t.wN = 0;
+        w.sync();
+    }
+    MT_HD int32_t chunk_alloc() {
+        auto& t = z.tl;
+        int32_t c = t.cfree;
+        if (c >= HT::TL::NCH) {
+            fail(E_CAPACITY);
+            return -1;
+        }
+        t.cfree = t.cpos[c];
+        t.nfreeChunk--;
+        t.ccnt[c] = 0;
+        return c;
+    }
+    MT_HD void chunk_free(int32_t c) {
+        auto& t = z.tl;
+        t.cpos[c] = t.cfree;
+        t.cfree = c;
+        t.nfreeChunk++;
+    }
+    /* move chunk positions [from, nchunk) by delta (+1 / -1) with their summaries; fix cpos */
+    MT_HD void cord_shift(int32_t from, int32_t delta) {
+        auto& t = z.tl;
+        int32_t n = t.nchunk, cnt = n - from;
+        if (cnt <= 0) return;
+        int32_t np = (cnt + W::N - 1) / W::N;
+        for (int32_t c = 0; c < np; c++) {
+            int32_t b = delta > 0 ? (np - 1 - c) * W::N : c * W::N;
+            if (W::N == 1) b = delta > 0 ? cnt - 1 - c : c;
+            int32_t i = from + b + (W::N == 1 ? 0 : w.lane());
+            bool ok = i < n && i >= from;
+            int32_t id = ok ? t.cord[i] : 0, sm = ok ? t.cst[i] : 0;
+            w.sync();
+            if (ok) {
+                t.cord[i + delta] = id;
+                t.cst[i + delta] = sm;
+                t.cpos[id] = i + delta;
+            }
+            w.sync();
+        }
+    }
+    /* shift leaves [i0, cnt) of chunk c by delta (+1 / -1), fixing lix (<= 64 entries) */
+    MT_HD void chunk_shift(int32_t c, int32_t i0, int32_t cnt, int32_t delta) {
+        auto& t = z.tl;
+        if constexpr (W::N >= 64) {
+            int32_t i = i0 + w.lane();
+            bool ok = i < cnt;
+            int32_t lf = ok ? t.cleaf[c][i] : 0;
+            w.sync();
+            if (ok) {
+                t.cleaf[c][i + delta] = lf;
+                t.lix[lf] = (uint8_t)(i + delta);
+            }
+            w.sync();
+        } else {
+            for (int32_t q = 0; q < cnt - i0; q++) {
+                int32_t i = delta > 0 ? cnt - 1 - q : i0 + q;
+                int32_t lf = t.cleaf[c][i];
+                t.cleaf[c][i + delta] = lf;
+                t.lix[lf] = (uint8_t)(i + delta);
+            }
+        }
+    }
+    /* leaf b goes right after leaf a in document order (a full chunk splits 32 + 32) */
+    MT_HD void rope_insert_after(int32_t a, int32_t b) {
+        auto& t = z.tl;
+        constexpr int32_t CH = HT::TL::CH, HALF = CH / 2;
+        int32_t c = t.lch[a], i = t.lix[a] + 1;
+        if (t.ccnt[c] >= CH) {
+            int32_t c2 = chunk_alloc();
+            if (c2 < 0) return;
+            int32_t p = t.cpos[c];
+            cord_shift(p + 1, 1);
+            t.nchunk++;
+            t.cord[p + 1] = c2;
+            t.cpos[c2] = p + 1;
+            int32_t moved = 0;
+            for (int32_t bb = 0; bb < HALF; bb += W::N) {
+                int32_t l = bb + w.lane();
+                int32_t v = 0;
+                if (l < HALF) {
+                    int32_t lf = t.cleaf[c][HALF + l];
+                    t.cleaf[c2][l] = lf;
+                    t.lch[lf] = c2;
+                    t.lix[lf] = (uint8_t)l;
+                    v = t.lst[lf];
+                }
+                moved += w.sum(v);
+            }
+            w.sync();
+            t.ccnt[c2] = HALF;
+            t.ccnt[c] = HALF;
+            t.cst[p + 1] = moved;
+            t.cst[p] -= moved;
+            if (i >= HALF) {
+                c = c2;
+                i -= HALF;
+            }
+        }
+        int32_t cnt = t.ccnt[c];
+        chunk_shift(c, i, cnt, 1);
+        t.cleaf[c][i] = b;
+        t.lch[b] = c;
+        t.lix[b] = (uint8_t)i;
+        t.ccnt[c] = cnt + 1;
+        t.cst[t.cpos[c]] += t.lst[b];
+        w.sync();
+    }
+    /* leaf b leaves the document order (its STABLE length leaves its chunk's summary) */
+    MT_HD void rope_remove(int32_t b) {
+        auto& t = z.tl;
+        int32_t c = t.lch[b], i = t.lix[b], p = t.cpos[c];
+        t.cst[p] -= t.lst[b];
+        t.lst[b] = 0;
+        int32_t cnt = t.ccnt[c];
+        chunk_shift(c, i + 1, cnt, -1);
+        t.ccnt[c] = cnt - 1;
+        if (cnt - 1 == 0) {
+            cord_shift(p + 1, -1);
+            t.nchunk--;
+            chunk_free(c);
+        }
+        w.sync();
+    }
+    MT_HD void lst_add(int32_t n, int32_t d) {
+        auto& t = z.tl;
+        t.lst[n] += d;
+        t.cst[t.cpos[t.lch[n]]] += d;
+    }
+    /* recompute leaf n's STABLE length from its rows */
+    MT_HD void leaf_restat(int32_t n) {
+        int32_t c = nch[n];
+        int32_t v = 0;
+        for (int32_t b = 0; b < c; b += W::N) {
+            int32_t j = b + w.lane();
+            int32_t x = 0;
+            if (j < c && (z.tl.xf[n * MAXN + j] & XF_STABLE)) x = z.len(n * MAXN + j);
+            v += w.sum(x);
+        }
+        lst_add(n, v - z.tl.lst[n]);
+        w.sync();
+    }
+    /* a row is settled when its insert and (if any) its removal are sequenced at or below minSeq */
+    MT_HD bool settled(int32_t s) const {
+        int32_t sq = z.seq(s), rs = z.rseq(s);
+        return sq != UNASSIGNED_SEQ && sq <= h.minSeq && (rs == NOREM || (rs != UNASSIGNED_SEQ && rs <= h.minSeq));
+    }
+    MT_HD void win_add(int32_t rid) {
+        auto& t = z.tl;
+        if (t.wN >= HT::TL::WCAP) {
+            fail(E_CAPACITY);
+            return;
+        }
+        t.wrid[t.wN] = rid;
+        t.wgen[t.wN] = z.rgen[rid];
+        t.wN++;
+    }
+    /* a row just placed (insert): STABLE if already settled (non-collaborating edits), else W */
+    MT_HD void row_enter(int32_t s) {
+        if (settled(s)) {
+            z.tl.xf[s] = z.rseq(s) == NOREM ? XF_STABLE : 0;
+            if (z.rseq(s) == NOREM) lst_add(s / MAXN, z.len(s));
+        } else {
+            z.tl.xf[s] = XF_W;
+            win_add(z.rid[s]);
+        }
+    }
+    /* a row just marked removed: leaves the STABLE summaries; W unless the removal is settled */
+    MT_HD void row_removed(int32_t s) {
+        uint8_t x = z.tl.xf[s];
+        if (x & XF_STABLE) {
+            lst_add(s / MAXN, -z.len(s));
+            x = 0;
+        }
+        if (!(x & XF_W) && !settled(s)) {
+            x = XF_W;
+            win_add(z.rid[s]);
+        }
+        z.tl.xf[s] = x;
+    }
+    /* Evaluate the window set under (refSeq, client): rows the MSN has passed settle into the
+     * STABLE summaries (or DEAD), entries of freed rows drop out, and every remaining row's chunk
+     * position, leaf index and perspective length go to the scratch, its length scattered onto
+     * cdel[chunk position]. Returns the sum of those lengths. */
+    MT_HD int32_t win_pass(int32_t refSeq, int32_t client) {
+        auto& t = z.tl;
+        int32_t n = t.wN, wpos = 0, total = 0;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            bool ok = i < n;
+            int32_t rd = ok ? t.wrid[i] : 0;
+            int32_t g = ok ? t.wgen[i] : 0;
+            int32_t s = -1;
+            if (ok && z.rgen[rd] == (uint8_t)g) {
+                int32_t lf = z.rleaf[rd], c = nch[lf];
+                for (int32_t j = 0; j < MAXN; j++)
+                    if (j < c && z.rid[lf * MAXN + j] == rd) s = lf * MAXN + j;
+            }
+            bool settle = s >= 0 && settled(s);
+            bool keep = s >= 0 && !settle;
+            int32_t v = 0, cp = 0, lx = 0;
+            if (keep) {
+                v = vis(s, refSeq, client);
+                int32_t lf = s / MAXN;
+                cp = t.cpos[t.lch[lf]];
+                lx = t.lix[lf];
+            }
+            uint64_t m = w.ballot(settle);
+            while (m) { /* a few rows per op: serial */
+                int32_t l = W::ffs(m);
+                m &= m - 1;
+                int32_t ss = w.bcast(s, l);
+                if (z.rseq(ss) == NOREM) {
+                    t.xf[ss] = XF_STABLE;
+                    lst_add(ss / MAXN, z.len(ss));
+                } else {
+                    t.xf[ss] = 0;
+                }
+            }
+            int32_t tot;
+            int32_t off = w.excl_scan(keep ? 1 : 0, &tot);
+            w.sync();
+            if (keep) {
+                int32_t o = wpos + off;
+                t.wrid[o] = rd;
+                t.wgen[o] = (uint8_t)g;
+                wcp[o] = cp;
+                wlx[o] = (uint8_t)lx;
+                wvs[o] = v;
+                if (v) W::atomic_add(&cdel[cp], v);
+            }
+            w.sync();
+            wpos += tot;
+            total += w.sum(v);
+        }
+        t.wN = wpos;
+        return total;
+    }
+    /* zero the chunk deltas of the last win_pass */
+    MT_HD void win_clear() {
+        int32_t n = z.tl.wN;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            if (i < n) cdel[wcp[i]] = 0;
+        }
+        w.sync();
+    }
+    /* Leaf position k and start offset P of the leaf holding the first row with
+     * P < pos <= P + vis, from the chunk and leaf summaries plus the window scratch of the last
+     * win_pass (same perspective). -1 if pos is beyond the length. */
+    MT_HD int32_t tile_find(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+        auto& t = z.tl;
+        int32_t nc = t.nchunk;
+        int32_t run = 0, cpf = -1;
+        for (int32_t b = 0; b < nc; b += 4 * W::N) {
+            int32_t p0 = b + 4 * w.lane();
+            int32_t v[4];
+            for (int q = 0; q < 4; q++) v[q] = p0 + q < nc ? t.cst[p0 + q] + cdel[p0 + q] : 0;
+            int32_t tot;
+            int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
+            int32_t hq = -1, hp = 0;
+            for (int q = 0; q < 4; q++) {
+                if (hq < 0 && p < pos && pos <= p + v[q]) {
+                    hq = q;
+                    hp = p;
+                }
+                p += v[q];
+            }
+            uint64_t m = w.ballot(hq >= 0);
+            if (m) {
+                int32_t l = W::ffs(m);
+                run = w.bcast(hp, l);
+                cpf = b + 4 * l + w.bcast(hq, l);
+                break;
+            }
+            run += tot;
+        }
+        if (cpf < 0) return -1;
+        /* leaves of the chunk: STABLE lengths + the window rows that sit in them */
+        int32_t c = t.cord[cpf], cnt = t.ccnt[c];
+        int32_t nw = t.wN;
+        int32_t ldel[HT::TL::CH / (W::N < 64 ? W::N : 64) + 1] = {};
+        for (int32_t b = 0; b < nw; b += W::N) {
+            int32_t i = b + w.lane();
+            uint64_t m = w.ballot(i < nw && wcp[i] == cpf);
+            while (m) {
+                int32_t l = W::ffs(m);
+                m &= m - 1;
+                int32_t lx = w.bcast(i < nw ? wlx[i] : 0, l);
+                int32_t vv = w.bcast(i < nw ? wvs[i] : 0, l);
+                if constexpr (W::N >= 64) {
+                    if (w.lane() == lx) ldel[0] += vv;
+                } else {
+                    ldel[lx] += vv;
+                }
+            }
+        }
+        for (int32_t b = 0; b < cnt; b += W::N) {
+            int32_t l = b + w.lane();
+            int32_t v = 0;
+            if (l < cnt) v = t.lst[t.cleaf[c][l]] + (W::N >= 64 ? ldel[0] : ldel[l]);
+            int32_t tot;
+            int32_t p = run + w.excl_scan(v, &tot);
+            uint64_t m = w.ballot(l < cnt && p < pos && pos <= p + v);
+            if (m) {
+                int32_t ll = W::ffs(m);
+                *Pout = w.bcast(p, ll);
+                return (cpf << 6) | (b + ll);
+            }
+            run += tot;
+        }
+        fail(E_ASSERT); /* the chunk's leaves must add up to its summary */
+        return -1;
+    }
+    /* within leaf position k (start offset P): the row t = k*8+j with P < pos <= P + vis */
+    MT_HD int32_t leaf_find(int32_t k, int32_t P, int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+        int32_t n = leaf_at(k), c = nch[n];
+        int32_t run = P;
+        for (int32_t j = 0; j < c; j++) {
+            int32_t v = vis(n * MAXN + j, refSeq, client);
+            if (run < pos && pos <= run + v) {
+                *Pout = run;
+                return k * MAXN + j;
+            }
+            run += v;
+        }
+        fail(E_ASSERT);
+        return -1;
+    }
+    /* perspectives the summaries cannot answer: a remote refSeq below minSeq (reads only) */
+    MT_HD bool tiles_cover(int32_t refSeq, int32_t client) const {
+        return is_local(client) || refSeq >= h.minSeq;
+    }
+    /* find_reach by a walk over every leaf (any perspective; O(rows)) */
+    MT_HD int32_t find_reach_walk(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+        int32_t run = 0;
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+            int32_t n = leaf_at(k), c = nch[n];
+            for (int32_t j = 0; j < c; j++) {
+                int32_t v = vis(n * MAXN + j, refSeq, client);
+                if (run < pos && pos <= run + v) {
+                    *Pout = run;
+                    return k * MAXN + j;
+                }
+                run += v;
+            }
+        }
+        return -1;
+    }
+    MT_HD int32_t find_reach_tiled(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+        if (pos <= 0) return -1;
+        if (!tiles_cover(refSeq, client)) return find_reach_walk(pos, refSeq, client, Pout);
+        win_pass(refSeq, client);
+        int32_t P;
+        int32_t k = tile_find(pos, refSeq, client, &P);
+        win_clear();
+        if (k < 0) return -1;
+        return leaf_find(k, P, pos, refSeq, client, Pout);
+    }
+    MT_HD int32_t length_tiled(int32_t refSeq, int32_t client) {
+        if (!tiles_cover(refSeq, client)) {
+            int32_t total = 0;
+            for (int32_t k = 0; kvalid(k); k = knext(k)) {
+                int32_t n = leaf_at(k), c = nch[n];
+                for (int32_t j = 0; j < c; j++) total += vis(n * MAXN + j, refSeq, client);
+            }
+            return total;
+        }
+        int32_t total = win_pass(refSeq, client);
+        win_clear();
+        int32_t nc = z.tl.nchunk;
+        for (int32_t b = 0; b < nc; b += W::N) {
+            int32_t p = b + w.lane();
+            total += w.sum(p < nc ? z.tl.cst[p] : 0);
+        }
+        return total;
     }
 
     /* ---- perspective scans ------------------------------------------------------------- */
@@ -622,6 +1125,7 @@ struct Replica {
     }
     /* Total length under a perspective (getLength, mergeTree.ts:1610). */
     MT_HD int32_t length(int32_t refSeq, int32_t client) {
+        if constexpr (TILED) return length_tiled(refSeq, client);
         int32_t total = 0;
         int32_t T = h.nleaf * MAXN;
         for (int32_t b = 0; b < T; b += 4 * W::N) {
@@ -635,6 +1139,7 @@ struct Replica {
      * and P of that row. */
     MT_HD int32_t find_reach(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
         MT_PROF_SCOPE(PH_FIND);
+        if constexpr (TILED) return find_reach_tiled(pos, refSeq, client, Pout);
         int32_t run = 0;
         int32_t T = h.nleaf * MAXN;
         for (int32_t b = 0; b < T; b += 4 * W::N) {
@@ -670,9 +1175,9 @@ struct Replica {
         /* interior node p: insert `child` at idx (insertChildNode, mergeTree.ts:2162-2172) */
         int32_t n = nch[p];
         for (int32_t i = n; i > idx; i--) z.kids[p * MAXN + i] = z.kids[p * MAXN + i - 1];
-        z.kids[p * MAXN + idx] = (int16_t)child;
+        z.kids[p * MAXN + idx] = (IX)child;
         nch[p] = (int8_t)(n + 1);
-        npar[child] = (int16_t)p;
+        npar[child] = (IX)p;
     }
     MT_HD int32_t child_index(int32_t p, int32_t child) const {
         for (int32_t i = 0; i < nch[p]; i++)
@@ -681,11 +1186,16 @@ struct Replica {
     }
     /* insert leaf `nl` into lorder right after leaf `after` */
     MT_HD void lorder_insert_after(int32_t after, int32_t nl) {
+        if constexpr (TILED) {
+            rope_insert_after(after, nl);
+            h.nleaf++;
+            return;
+        }
         int32_t k = lp[after] + 1;
         int32_t n = h.nleaf;
         lorder_shift(k, n, 1);
-        lo[k] = (int16_t)nl;
-        lp[nl] = (int16_t)k;
+        lo[k] = (IX)nl;
+        lp[nl] = (IX)k;
         h.nleaf = n + 1;
     }
     /* split (mergeTree.ts:2509-2522) of a full node (8 children) into 4 + 4; the new node is
@@ -706,22 +1216,28 @@ struct Replica {
             } else {
                 for (int32_t i = 0; i < 4; i++) {
                     int32_t c = z.kids[n * MAXN + 4 + i];
-                    z.kids[nn * MAXN + i] = (int16_t)c;
-                    npar[c] = (int16_t)nn;
+                    z.kids[nn * MAXN + i] = (IX)c;
+                    npar[c] = (IX)nn;
                 }
             }
             nch[n] = 4;
             nch[nn] = 4;
             if (lvl == 0) lorder_insert_after(n, nn);
+            if constexpr (TILED) {
+                if (lvl == 0) {
+                    leaf_restat(n);
+                    leaf_restat(nn);
+                }
+            }
             int32_t p = npar[n];
             if (p < 0) {
                 int32_t r = alloc_node((int8_t)(lvl + 1));
                 if (r < 0) return -1;
-                z.kids[r * MAXN + 0] = (int16_t)n;
-                z.kids[r * MAXN + 1] = (int16_t)nn;
+                z.kids[r * MAXN + 0] = (IX)n;
+                z.kids[r * MAXN + 1] = (IX)nn;
                 nch[r] = 2;
-                npar[n] = (int16_t)r;
-                npar[nn] = (int16_t)r;
+                npar[n] = (IX)r;
+                npar[nn] = (IX)r;
                 h.root = r;
                 return first;
             }
@@ -736,6 +1252,7 @@ struct Replica {
         int32_t c = nch[n];
         slab_shift_right(n, j, c);
         z.rid[n * MAXN + j] = -1; /* not a row yet: the caller assigns one */
+        if constexpr (TILED) z.tl.xf[n * MAXN + j] = 0;
         nch[n] = (int8_t)(c + 1);
         if (c + 1 >= MAXN) {
             int32_t nn = split_node(n);
@@ -782,15 +1299,17 @@ struct Replica {
         int32_t ep = h.gcEpoch % 255 + 1;
         h.gcEpoch = ep;
         int32_t top = 0;
-        int32_t T = h.nleaf * MAXN;
-        for (int32_t t = 0; t < T; t++) {
-            int32_t s = slot_at(t);
-            if (s < 0 || (z.flags(s) & RF_NOTEXT) || cold(s).gc == ep) continue;
-            int32_t L = z.len(s);
-            arena_copy(dst + top, src + cold(s).toff, L);
-            cold(s).toff = (uint32_t)top;
-            cold(s).gc = (uint8_t)ep;
-            top += L;
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+            int32_t n = leaf_at(k), c = nch[n];
+            for (int32_t j = 0; j < c; j++) {
+                int32_t s = n * MAXN + j;
+                if ((z.flags(s) & RF_NOTEXT) || cold(s).gc == ep) continue;
+                int32_t L = z.len(s);
+                arena_copy(dst + top, src + cold(s).toff, L);
+                cold(s).toff = (uint32_t)top;
+                cold(s).gc = (uint8_t)ep;
+                top += L;
+            }
         }
         h.arenaSide = to;
         h.arenaTop = top;
@@ -802,18 +1321,19 @@ struct Replica {
      * the LEFT part afterwards (the right part is the next row in document order). */
     MT_HD int32_t split_row(int32_t t, int32_t off, int32_t* rsOut = nullptr) {
         MT_PROF_SCOPE(PH_SPLIT);
-        int32_t n = lo[t >> 3], j = t & 7;
+        int32_t n = leaf_at(t >> 3), j = t & 7;
         int32_t s0 = n * MAXN + j;
         if (z.flags(s0) & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
         bool willSplit = nch[n] + 1 >= MAXN;
         int32_t rs = leaf_insert_slot(n, j + 1);
         if (rs < 0) return -1;
-        /* the left part stays at n*8+j unless the leaf split moved children 4..7 */
+        /* the left part stays at n*8+j unless the leaf split moved children 4..7 (then it sits just
+         * before the new slot, in the new leaf) */
         int32_t ls = n * MAXN + j;
-        if (willSplit && j >= 4) ls = lo[lp[n] + 1] * MAXN + (j - 4);
+        if (willSplit && j >= 4) ls = rs - 1;
         copy_row(rs, ls);
-        z.rid[rs] = (int16_t)alloc_rid();
-        z.rleaf[z.rid[rs]] = (int16_t)(rs / MAXN);
+        z.rid[rs] = (IX)alloc_rid();
+        z.rleaf[z.rid[rs]] = (IX)(rs / MAXN);
         cold(rs) = cold(ls); /* splitAt copies every field (mergeTree.ts:523-567) */
         z.len(rs) = z.len(ls) - off;
         cold(rs).toff = cold(ls).toff + (uint32_t)off;
@@ -821,6 +1341,13 @@ struct Replica {
         z.flags(ls) &= (uint8_t)~RF_NLK; /* the left part's last unit is not known any more */
         h.nrows++;
         h.sumW += 2;
+        if constexpr (TILED) {
+            if (z.tl.xf[rs] & XF_W) win_add(z.rid[rs]);
+            if (z.tl.xf[rs] & XF_STABLE) { /* the halves may sit in two leaves after a leaf split */
+                leaf_restat(ls / MAXN);
+                if (rs / MAXN != ls / MAXN) leaf_restat(rs / MAXN);
+            }
+        }
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
          * same pending groups (in the row's FIFO order = log order), appended at the end of each
          * group's segment list */
@@ -907,7 +1434,7 @@ struct Replica {
 
     /* ---- zamboni heap (collections.ts:212-264, LRUSegmentComparer mergeTree.ts:957-960) ---- */
     MT_HD void heap_swap(int32_t i, int32_t j) {
-        int16_t tr = hrd[i];
+        IX tr = hrd[i];
         int32_t tq = hsq[i];
         uint8_t tg = hgn[i];
         hrd[i] = hrd[j];
@@ -938,7 +1465,7 @@ struct Replica {
             int32_t as = a >= 1 ? hsq[a - 1] : 0;
             uint64_t m = w.ballot(a >= 1 && as - seq > 0);
             int32_t up = __builtin_ctzll(~m); /* length of the leading run */
-            int16_t ar = 0;
+            IX ar = 0;
             uint8_t ag = 0;
             if (l < up) {
                 ar = hrd[a - 1];
@@ -953,14 +1480,14 @@ struct Replica {
             }
             int32_t fin = k >> up;
             if (l == 0) {
-                hrd[fin - 1] = (int16_t)rid;
+                hrd[fin - 1] = (IX)rid;
                 hsq[fin - 1] = seq;
                 hgn[fin - 1] = gen;
             }
             w.sync();
             if (fin == 1) h.heapTop = seq;
         } else {
-            hrd[k - 1] = (int16_t)rid;
+            hrd[k - 1] = (IX)rid;
             hsq[k - 1] = seq;
             hgn[k - 1] = gen;
             while (k > 1 && hsq[(k >> 1) - 1] - hsq[k - 1] > 0) {
@@ -983,7 +1510,7 @@ struct Replica {
             int32_t c2 = 128 + l < cnt ? hsq[128 + l] : 0;
             int32_t c3 = 192 + l < cnt ? hsq[192 + l] : 0;
             int32_t last = cnt - 1; /* index of the entry that moves to the root */
-            int16_t xr = hrd[last];
+            IX xr = hrd[last];
             uint8_t xg = hgn[last];
             *rid = hrd[0];
             *gen = hgn[0];
@@ -1021,7 +1548,7 @@ struct Replica {
                     src = path[t];
                     dst = t == 0 ? 1 : path[t - 1];
                 }
-            int16_t mr = 0;
+            IX mr = 0;
             uint8_t mg = 0;
             int32_t ms = 0;
             if (l < d) {
@@ -1163,6 +1690,11 @@ struct Replica {
     MT_HD void append_text(int32_t a, int32_t b) {
         MT_PROF_SCOPE(PH_APPEND);
         int32_t La = z.len(a), Lb = z.len(b);
+        if constexpr (TILED) { /* b's length joins a's row: keep the leaf's STABLE sum exact */
+            bool sa = z.tl.xf[a] & XF_STABLE, sb = z.tl.xf[b] & XF_STABLE;
+            if (sa && !sb) lst_add(a / MAXN, Lb);
+            if (!sa && sb) lst_add(a / MAXN, -Lb);
+        }
         if (z.flags(a) & RF_PERM) { /* PermutationSegment.append (permutationvector.ts:95-101) */
             z.len(a) = La + Lb;
             return;
@@ -1334,7 +1866,7 @@ struct Replica {
         if ((drop >> q) & 1) {
             int32_t pos = h.nfreeRid + __builtin_popcountll(drop & below);
             z.rgen[r.rid]++;
-            d.frid[pos] = (int16_t)r.rid;
+            d.frid[pos] = (IX)r.rid;
         }
         int32_t ndrop = __builtin_popcountll(drop);
         h.nfreeRid += ndrop;
@@ -1398,7 +1930,7 @@ struct Replica {
                 oldk[i] = z.kids[parent * MAXN + i];
                 ocnt[i] = nch[oldk[i]];
             }
-            int32_t firstPos = lp[oldk[0]];
+            int32_t firstPos = TILED ? 0 : lp[oldk[0]];
             int32_t newk[MAXN];
             int32_t ncnt[MAXN];
             for (int32_t ni = 0; ni < cc; ni++) {
@@ -1423,7 +1955,7 @@ struct Replica {
                 w.sync();
                 if (has) {
                     store_row(dst, r);
-                    z.rleaf[r.rid] = (int16_t)(dst / MAXN);
+                    z.rleaf[r.rid] = (IX)(dst / MAXN);
                 }
                 w.sync();
             } else {
@@ -1435,28 +1967,35 @@ struct Replica {
                 for (int32_t i = 0; i < cc; i++)
                     for (int32_t j = 0; j < ncnt[i]; j++) {
                         store_row(newk[i] * MAXN + j, tmp[q]);
-                        z.rleaf[tmp[q++].rid] = (int16_t)newk[i];
+                        z.rleaf[tmp[q++].rid] = (IX)newk[i];
                     }
             }
             for (int32_t ni = 0; ni < cc; ni++) {
                 int32_t nb = newk[ni];
                 nch[nb] = (int8_t)ncnt[ni];
-                npar[nb] = (int16_t)parent;
+                npar[nb] = (IX)parent;
                 nlev[nb] = 0;
                 nsc[nb] = -1;
                 if (ncnt[ni] < MAXN) clear_slots(nb * MAXN + ncnt[ni], MAXN - ncnt[ni]);
             }
-            for (int32_t i = cc; i < pc; i++) free_node(oldk[i]);
-            /* lorder: [firstPos, firstPos+pc) becomes [firstPos, firstPos+cc) */
             int32_t nl = h.nleaf;
             int32_t delta = cc - pc;
-            lorder_shift(firstPos + pc, nl, delta);
-            for (int32_t i = pc; i < cc; i++) {
-                lo[firstPos + i] = (int16_t)newk[i];
-                lp[newk[i]] = (int16_t)(firstPos + i);
+            if constexpr (TILED) { /* the rope: extra leaves after the kept ones, surplus ones out */
+                for (int32_t i = pc; i < cc; i++) rope_insert_after(newk[i - 1], newk[i]);
+                for (int32_t i = cc; i < pc; i++) rope_remove(oldk[i]);
+                for (int32_t i = 0; i < cc; i++) leaf_restat(newk[i]);
+            }
+            for (int32_t i = cc; i < pc; i++) free_node(oldk[i]);
+            if constexpr (!TILED) {
+                /* lorder: [firstPos, firstPos+pc) becomes [firstPos, firstPos+cc) */
+                lorder_shift(firstPos + pc, nl, delta);
+                for (int32_t i = pc; i < cc; i++) {
+                    lo[firstPos + i] = (IX)newk[i];
+                    lp[newk[i]] = (IX)(firstPos + i);
+                }
             }
             h.nleaf = nl + delta;
-            for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (int16_t)newk[i];
+            for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (IX)newk[i];
             nch[parent] = (int8_t)cc;
         } else {
             MT_PROF_SCOPE(PH_P2);
@@ -1494,18 +2033,18 @@ struct Replica {
                     if (k == ni && k < cc) nb = nbk[k];
                 w.sync();
                 if (has) {
-                    z.kids[nb * MAXN + slot] = (int16_t)ch;
-                    npar[ch] = (int16_t)nb;
+                    z.kids[nb * MAXN + slot] = (IX)ch;
+                    npar[ch] = (IX)nb;
                 }
                 w.sync();
                 for (int32_t k = 0; k < cc; k++) {
                     nch[nbk[k]] = (int8_t)(base + (k < extra ? 1 : 0));
-                    npar[nbk[k]] = (int16_t)parent;
-                    z.kids[parent * MAXN + k] = (int16_t)nbk[k];
+                    npar[nbk[k]] = (IX)parent;
+                    z.kids[parent * MAXN + k] = (IX)nbk[k];
                 }
                 nch[parent] = (int8_t)cc;
             } else {
-                int16_t hold[MAXN * MAXN];
+                IX hold[MAXN * MAXN];
                 int32_t total = 0;
                 int32_t oldk[MAXN];
                 for (int32_t i = 0; i < pc; i++) {
@@ -1526,12 +2065,12 @@ struct Replica {
                     if (nb < 0) return;
                     for (int32_t q = 0; q < cnt; q++) {
                         int32_t ch = hold[read++];
-                        z.kids[nb * MAXN + q] = (int16_t)ch;
-                        npar[ch] = (int16_t)nb;
+                        z.kids[nb * MAXN + q] = (IX)ch;
+                        npar[ch] = (IX)nb;
                     }
                     nch[nb] = (int8_t)cnt;
-                    npar[nb] = (int16_t)parent;
-                    z.kids[parent * MAXN + ni] = (int16_t)nb;
+                    npar[nb] = (IX)parent;
+                    z.kids[parent * MAXN + ni] = (IX)nb;
                 }
                 nch[parent] = (int8_t)cc;
             }
@@ -1582,6 +2121,23 @@ struct Replica {
     /* continueFrom (2187-2194): first row after leaf lorder[k] with localNetLength > 0 is a
      * local-pending insert */
     MT_HD bool continue_from(int32_t k) {
+        if constexpr (TILED) { /* walk the following leaves in order (the first visible row is near) */
+            for (int32_t kk = knext(k); kvalid(kk); kk = knext(kk)) {
+                int32_t n = leaf_at(kk), c = nch[n];
+                int32_t fj = -1;
+                if constexpr (W::N >= MAXN) {
+                    int32_t j = w.lane();
+                    bool hit = j < c && z.len(n * MAXN + (j & 7)) > 0 && z.rseq(n * MAXN + (j & 7)) == NOREM;
+                    uint64_t m = w.ballot(hit);
+                    if (m) fj = W::ffs(m);
+                } else {
+                    for (int32_t j = 0; j < c && fj < 0; j++)
+                        if (z.len(n * MAXN + j) > 0 && z.rseq(n * MAXN + j) == NOREM) fj = j;
+                }
+                if (fj >= 0) return z.seq(n * MAXN + fj) == UNASSIGNED_SEQ;
+            }
+            return false;
+        }
         int32_t T = h.nleaf * MAXN;
         for (int32_t b = (k + 1) * MAXN; b < T; b += 4 * W::N) {
             int32_t s0 = quad_slot(b + 4 * w.lane());
@@ -1629,7 +2185,7 @@ struct Replica {
             if (P + v > pos && !(z.flags(s) & RF_MARKER)) {
                 int32_t ls = split_row(t, pos - P);
                 if (ls < 0) return -1;
-                k = lp[ls / MAXN];
+                k = kpos(ls / MAXN);
                 j = (ls & (MAXN - 1)) + 1;
             } else {
                 k = t >> 3;
@@ -1639,14 +2195,14 @@ struct Replica {
             }
         }
         for (;;) {
-            int32_t n = lo[k];
+            int32_t n = leaf_at(k);
             int32_t c = nch[n];
             for (; j < c; j++) {
                 int32_t s = n * MAXN + j;
                 if (vis(s, refSeq, client) > 0 || break_tie(s, refSeq, client)) return leaf_insert_slot(n, j);
             }
-            if (seq != UNASSIGNED_SEQ && k + 1 < h.nleaf && continue_from(k)) {
-                k++;
+            if (seq != UNASSIGNED_SEQ && kvalid(knext(k)) && continue_from(k)) {
+                k = knext(k);
                 j = 0;
                 continue;
             }
@@ -1673,7 +2229,7 @@ struct Replica {
                 fail(E_INSERT_FAILED);
                 return;
             }
-            z.rid[s] = (int16_t)alloc_rid();
+            z.rid[s] = (IX)alloc_rid();
             cold(s).gc = 0;
             z.len(s) = L;
             z.seq(s) = seq;
@@ -1686,7 +2242,7 @@ struct Replica {
             z.ng(s) = 0;
             cold(s).prw = 0;
             cold(s).ovl = 0;
-            z.rleaf[z.rid[s]] = (int16_t)(s / MAXN);
+            z.rleaf[z.rid[s]] = (IX)(s / MAXN);
             h.nrows++;
             h.sumW++;
             h.localLen += L;
@@ -1701,6 +2257,7 @@ struct Replica {
                 fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
             }
             z.flags(s) = (uint8_t)fl;
+            if constexpr (TILED) row_enter(s);
             for (int k = 0; k < NKEYS; k++) {
                 cold(s).pv[k] = 0;
                 cold(s).pk[k] = 0;
@@ -1722,39 +2279,6 @@ struct Replica {
     }
 
     /* ---- range ops: markRangeRemoved (2640-2752) / annotateRange (2598-2638) ----------- */
-    template <class F>
-    MT_HD void map_range(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
-        MT_PROF_SCOPE(PH_MAP);
-        int32_t run = 0;
-        int32_t T = h.nleaf * MAXN;
-        for (int32_t b = 0; b < T; b += 4 * W::N) {
-            int32_t s0 = quad_slot(b + 4 * w.lane());
-            int32_t v[4];
-            quad_vis(s0, refSeq, client, v);
-            int32_t tot;
-            int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
-            int32_t hm = 0;
-            for (int q = 0; q < 4; q++) {
-                if (v[q] > 0 && p < end && p + v[q] > start) hm |= 1 << q;
-                p += v[q];
-            }
-            uint64_t m = w.ballot(hm != 0);
-            while (m) {
-                int32_t l = W::ffs(m);
-                m &= m - 1;
-                int32_t bits = w.bcast(hm, l);
-                int32_t sb = w.bcast(s0, l);
-                while (bits) {
-                    int32_t q = __builtin_ctz((unsigned)bits);
-                    bits &= bits - 1;
-                    leaf(sb + q);
-                }
-            }
-            run += tot;
-            if (run >= end) break;
-        }
-    }
-
     /* Boundaries and visit of a range op in ONE perspective scan. The reference splits at start
      * (ensureIntervalBoundary, mergeTree.ts:2274-2278), then at end, then visits the rows with
      * length > 0 in [start, end) (nodeMap, 2936-2998). The rows it visits are exactly the rows with
@@ -1765,6 +2289,10 @@ struct Replica {
     template <class F>
     MT_HD void range_op(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
         MT_PROF_SCOPE(PH_MAP);
+        if constexpr (TILED) {
+            range_op_tiled(start, end, refSeq, client, leaf);
+            return;
+        }
         int32_t run = 0;
         int32_t T = h.nleaf * MAXN;
         int32_t tf = -1, Pf = 0, vf = 0, tg = -1, Pg = 0, vg = 0;
@@ -1825,15 +2353,15 @@ struct Replica {
                 fail(E_ASSERT);
                 return;
             }
-            if (split_row(lp[sg / MAXN] * MAXN + (sg & (MAXN - 1)), end - Pg) < 0) return;
+            if (split_row(kpos(sg / MAXN) * MAXN + (sg & (MAXN - 1)), end - Pg) < 0) return;
         }
         int32_t sa = slot_of(ridFirst, -1), sb = slot_of(ridLast, -1);
         if (sa < 0 || sb < 0) {
             fail(E_ASSERT);
             return;
         }
-        int32_t ta = lp[sa / MAXN] * MAXN + (sa & (MAXN - 1));
-        int32_t tb = lp[sb / MAXN] * MAXN + (sb & (MAXN - 1));
+        int32_t ta = kpos(sa / MAXN) * MAXN + (sa & (MAXN - 1));
+        int32_t tb = kpos(sb / MAXN) * MAXN + (sb & (MAXN - 1));
         for (int32_t b = ta & ~3; b <= tb; b += 4 * W::N) {
             int32_t t0 = b + 4 * w.lane();
             int32_t s0 = quad_slot(t0);
@@ -1856,6 +2384,78 @@ struct Replica {
             }
         }
     }
+    /* range_op for the tiled profile: the first and last rows overlapping [start, end) are the rows
+     * reaching start + 1 and min(end, length) (one window pass, two summary searches); the same
+     * two splits; then the rows with length > 0 between them are visited leaf by leaf. */
+    template <class F>
+    MT_HD void range_op_tiled(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
+        int32_t tf, Pf, tg, Pg;
+        if (tiles_cover(refSeq, client)) {
+            int32_t total = win_pass(refSeq, client);
+            int32_t nc = z.tl.nchunk;
+            for (int32_t b = 0; b < nc; b += W::N) {
+                int32_t p = b + w.lane();
+                total += w.sum(p < nc ? z.tl.cst[p] : 0);
+            }
+            if (start >= total || end <= start) {
+                win_clear();
+                return;
+            }
+            int32_t last = end < total ? end : total;
+            int32_t P1, P2;
+            int32_t k1 = tile_find(start + 1, refSeq, client, &P1);
+            int32_t k2 = tile_find(last, refSeq, client, &P2);
+            win_clear();
+            if (k1 < 0 || k2 < 0) {
+                fail(E_ASSERT);
+                return;
+            }
+            tf = leaf_find(k1, P1, start + 1, refSeq, client, &Pf);
+            tg = leaf_find(k2, P2, last, refSeq, client, &Pg);
+        } else {
+            int32_t total = length_tiled(refSeq, client);
+            if (start >= total || end <= start) return;
+            tf = find_reach_walk(start + 1, refSeq, client, &Pf);
+            tg = find_reach_walk(end < total ? end : total, refSeq, client, &Pg);
+        }
+        if (tf < 0 || tg < 0) return;
+        int32_t vf = vis(slot_at(tf), refSeq, client), vg = vis(slot_at(tg), refSeq, client);
+        int32_t ridLast = z.rid[slot_at(tg)];
+        int32_t ridFirst = z.rid[slot_at(tf)];
+        if (Pf < start) {
+            int32_t rs = -1;
+            if (split_row(tf, start - Pf, &rs) < 0 || rs < 0) return;
+            if (tf == tg) {
+                ridLast = z.rid[rs];
+                vg = Pf + vf - start;
+                Pg = start;
+            }
+            ridFirst = z.rid[rs];
+        }
+        if (Pg + vg > end) {
+            int32_t sg = slot_of(ridLast, -1);
+            if (sg < 0) {
+                fail(E_ASSERT);
+                return;
+            }
+            if (split_row(kpos(sg / MAXN) * MAXN + (sg & (MAXN - 1)), end - Pg) < 0) return;
+        }
+        int32_t sa = slot_of(ridFirst, -1), sb = slot_of(ridLast, -1);
+        if (sa < 0 || sb < 0) {
+            fail(E_ASSERT);
+            return;
+        }
+        int32_t ka = kpos(sa / MAXN), kb = kpos(sb / MAXN);
+        for (int32_t k = ka;; k = knext(k)) {
+            int32_t n = leaf_at(k), c = nch[n];
+            int32_t j0 = k == ka ? (sa & (MAXN - 1)) : 0;
+            int32_t j1 = k == kb ? (sb & (MAXN - 1)) : c - 1;
+            for (int32_t j = j0; j <= j1; j++)
+                if (vis(n * MAXN + j, refSeq, client) > 0) leaf(n * MAXN + j);
+            if (k == kb || !kvalid(knext(k))) break;
+        }
+    }
+
     MT_HD void mark_range_removed(int32_t start, int32_t end, int32_t refSeq, int32_t client, int32_t seq) {
         bool hasL = seq == UNASSIGNED_SEQ;
         int32_t localSeq = hasL ? ++h.localSeq : 0;
@@ -1888,6 +2488,7 @@ struct Replica {
                 else
                     z.flags(s) &= (uint8_t)~RF_LRSEQ;
             }
+            if constexpr (TILED) row_removed(s);
             if (h.collaborating) {
                 if (z.rseq(s) == UNASSIGNED_SEQ && client == h.localShort)
                     pending_add(s, localSeq, &created);
@@ -2002,7 +2603,11 @@ struct Replica {
         }
         get_or_add_short(op.client);
         h.seqOps++;
-        h.sumR += h.nrows;
+        if constexpr (TILED) /* BASELINE.md tile formula, in 16-byte units: 4 B per chunk summary,
+                                64 B per window row, 640 B for the target chunk's leaves + leaf line */
+            h.sumR += (4 * z.tl.nchunk + 64 * z.tl.wN + 640) / 16;
+        else
+            h.sumR += h.nrows;
         if (kind != MT_OP_NOOP) {
             if ((int32_t)op.client == h.localLong) {
                 ack(kind, kv, nkv, rw, op.seq);
@@ -2034,19 +2639,21 @@ struct Replica {
     /* Writes at most cap units; returns the text length under the perspective. */
     MT_HD int64_t get_text(int32_t refSeq, int32_t client, uint16_t* out, int64_t cap) {
         int64_t n = 0;
-        int32_t T = h.nleaf * MAXN;
         const uint16_t* base = arena_base(h.arenaSide);
-        for (int32_t t = 0; t < T; t++) {
-            int32_t s = slot_at(t);
-            if (s < 0 || (z.flags(s) & RF_NOTEXT)) continue;
-            int32_t v = vis(s, refSeq, client);
-            if (v <= 0) continue;
-            if (out) {
-                int32_t m = v;
-                if (n + m > cap) m = (int32_t)(cap - n > 0 ? cap - n : 0);
-                arena_copy(out + n, base + cold(s).toff, m);
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+            int32_t lf = leaf_at(k), c = nch[lf];
+            for (int32_t j = 0; j < c; j++) {
+                int32_t s = lf * MAXN + j;
+                if (z.flags(s) & RF_NOTEXT) continue;
+                int32_t v = vis(s, refSeq, client);
+                if (v <= 0) continue;
+                if (out) {
+                    int32_t m = v;
+                    if (n + m > cap) m = (int32_t)(cap - n > 0 ? cap - n : 0);
+                    arena_copy(out + n, base + cold(s).toff, m);
+                }
+                n += v;
             }
-            n += v;
         }
         return n;
     }
@@ -2084,15 +2691,16 @@ struct Replica {
     }
     MT_HD void dump_to(Sink* o) {
         int32_t nsegs = 0;
-        int32_t T = h.nleaf * MAXN;
-        for (int32_t t = 0; t < T; t++)
-            if (slot_at(t) >= 0) nsegs++;
+        for (int32_t k = 0; kvalid(k); k = knext(k)) nsegs += nch[leaf_at(k)];
         int32_t hdr[6] = {h.currentSeq, h.minSeq, h.localSeq, length_local(), nsegs, h.nleaf};
         put_bytes(o, hdr, sizeof(hdr));
         const uint16_t* base = arena_base(h.arenaSide);
-        for (int32_t t = 0; t < T; t++) {
-            int32_t s = slot_at(t);
-            if (s < 0) continue;
+        int32_t ordinal = -1;
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+          ordinal++;
+          int32_t lfn = leaf_at(k), lc = nch[lfn];
+          for (int32_t jj = 0; jj < lc; jj++) {
+            int32_t s = lfn * MAXN + jj;
             uint8_t fl = z.flags(s);
             bool rem = z.rseq(s) != NOREM;
             int nov = 0;
@@ -2113,7 +2721,7 @@ struct Replica {
                             rem ? long_of(z.rcli(s)) : 0,
                             (fl & RF_LSEQ) ? cold(s).lseq : 0,
                             (fl & RF_LRSEQ) ? cold(s).lrseq : 0,
-                            t >> 3};
+                            ordinal};
             put_bytes(o, f, sizeof(f));
             for (int k = 0; k < nov; k++) {
                 int32_t lo = long_of((uint8_t)(((cold(s).ovl >> (8 * k)) & 0xFF) - 1));
@@ -2137,6 +2745,7 @@ struct Replica {
                 last = bk;
             }
             if (!(fl & RF_NOTEXT)) put_bytes(o, base + cold(s).toff, 2 * (int64_t)z.len(s));
+          }
         }
     }
     MT_HD static uint64_t fnv(const uint8_t* p, int64_t n) {

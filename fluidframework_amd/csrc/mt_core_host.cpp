@@ -24,6 +24,7 @@ struct mth_store {
     Store<HotMid> s1;
     Store<HotBig> s2;
     Store<HotMat> s3;
+    Store<HotHuge> s4;
     uint8_t* mem;
 };
 
@@ -43,6 +44,11 @@ static auto with_replica(mth_store* s, int64_t d, F&& f) {
         return res;
     } else if (s->profile == 1) {
         Replica<WaveHost, HotMid> r(s->s1.doc(d), WaveHost());
+        auto res = f(r);
+        r.commit();
+        return res;
+    } else if (s->profile == 4) {
+        Replica<WaveHost, HotHuge> r(s->s4.doc(d), WaveHost());
         auto res = f(r);
         r.commit();
         return res;
@@ -66,13 +72,14 @@ mth_store* mth_create(int64_t ndocs, const int32_t* caps6) {
     int64_t bytes = prof == 0 ? store_layout(s->s0, k, ndocs)
                   : prof == 1 ? store_layout(s->s1, k, ndocs)
                   : prof == 3 ? store_layout(s->s3, k, ndocs)
+                  : prof == 4 ? store_layout(s->s4, k, ndocs)
                               : store_layout(s->s2, k, ndocs);
     s->mem = host_store_alloc(bytes);
     if (!s->mem) {
         free(s);
         return nullptr;
     }
-    s->s0.base = s->s1.base = s->s2.base = s->s3.base = s->mem;
+    s->s0.base = s->s1.base = s->s2.base = s->s3.base = s->s4.base = s->mem;
     for (int64_t d = 0; d < ndocs; d++) with_replica(s, d, [](auto& r) { r.init(); return 0; });
     return s;
 }
@@ -156,7 +163,7 @@ void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {
         out8[3] = h->heapN;
         out8[4] = h->memN;
         out8[5] = h->arenaTop;
-        out8[6] = (int32_t)(sizeof(r.z.nparent) / sizeof(int16_t)) - h->nfree;
+        out8[6] = (int32_t)(sizeof(r.z.nparent) / sizeof(r.z.nparent[0])) - h->nfree;
         out8[7] = h->opsDone;
         return 0;
     });

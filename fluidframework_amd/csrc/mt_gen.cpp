@@ -222,6 +222,9 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
             m_apply(&m, e);
         }
     } else { /* MTG_LAGGED */
+        /* A replica that never edits (local_pct == 0) is a caught-up reader: its refSeq follows the
+         * stream (the service learns it from the client's noops), so it never holds the MSN back. */
+        bool me_in_msn = P->local_pct > 0;
         Pending* q = (Pending*)malloc(sizeof(Pending) * (P->ops_per_doc + 16));
         int qh = 0, qn = 0;
         int32_t lastTarget = 0, msn = 0;
@@ -277,7 +280,7 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
                 lastRef[client] = ref;
                 int32_t mn = INT32_MAX;
                 for (int k = 0; k < nclients; k++)
-                    if (lastRef[k] < mn) mn = lastRef[k];
+                    if (lastRef[k] < mn && (k != me || me_in_msn)) mn = lastRef[k];
                 if (mn > msn) msn = mn;
                 gen_op(P, &r, &m, ref, client, 0, o, e, insert_index);
                 e->client = (uint16_t)client;
@@ -502,6 +505,8 @@ static void gen_doc(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec
         gen_farm_t<HotMid>(P, doc, o, props, kv);
     else if (P->mode == MTG_MATRIX)
         gen_matrix_t<HotMid>(P, doc, o, props, kv);
+    else if (P->model_ncap > HotBig::N)
+        gen_doc_t<HotHuge>(P, doc, o, props, kv);
     else if (P->model_ncap > HotMid::N)
         gen_doc_t<HotBig>(P, doc, o, props, kv);
     else

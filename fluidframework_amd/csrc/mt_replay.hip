@@ -175,6 +175,43 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
     }
 }
 
+/* Config 4 (large documents, the tiled profile): one workgroup per document, which has the CU's LDS to
+ * itself for the position-search scratch: per-chunk window deltas (NCH counters, all zero between
+ * searches) and each window row's chunk position / leaf index / perspective length. The image, the
+ * rope and the summaries stay in HBM (~0.2 GB per 1M-op document). */
+template <class HT>
+__global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
+                                                     const int64_t* op_off, const uint16_t* text,
+                                                     const int64_t* text_off, const mt_props_rec* props,
+                                                     const int64_t* props_off, const mt_kv* kv, const int64_t* kv_off,
+                                                     uint64_t* prof) {
+    static_assert(HT::TILED, "tiled profile only");
+    __shared__ int32_t cdel[HT::TL::NCH];
+    __shared__ int32_t wcp[HT::TL::WCAP], wvs[HT::TL::WCAP];
+    __shared__ uint8_t wlx[HT::TL::WCAP];
+    int64_t d = blockIdx.x;
+    if (d >= ndocs) return;
+    for (int i = threadIdx.x; i < HT::TL::NCH; i += WG) cdel[i] = 0;
+    __syncthreads();
+    Pools p;
+    p.ops = ops + op_off[d];
+    p.nops = op_off[d + 1] - op_off[d];
+    p.text = text + text_off[d];
+    p.props = props + props_off[d];
+    p.kv = kv + kv_off[d];
+    Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
+    r.cdel = cdel;
+    r.wcp = wcp;
+    r.wvs = wvs;
+    r.wlx = wlx;
+    r.replay(p);
+    r.commit();
+#ifdef MT_PROF
+    if (prof && threadIdx.x == 0)
+        for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
+#endif
+}
+
 /* K5: per-doc digest of the canonical dump */
 template <class HT>
 __global__ __launch_bounds__(WG) void k_digest(Store<HT> st, int64_t ndocs, uint64_t* out) {
@@ -267,6 +304,7 @@ struct mt_engine {
     Store<HotMid> s1;
     Store<HotBig> s2;
     Store<HotMat> s3;
+    Store<HotHuge> s4;
     void* mem = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -284,6 +322,7 @@ static int32_t with_store(mt_engine* e, F&& f) {
     if (e->profile == 0) return f(e->s0);
     if (e->profile == 1) return f(e->s1);
     if (e->profile == 3) return f(e->s3);
+    if (e->profile == 4) return f(e->s4);
     return f(e->s2);
 }
 
@@ -360,6 +399,7 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     int64_t bytes = prof == 0 ? store_layout(e->s0, k, ndocs)
                   : prof == 1 ? store_layout(e->s1, k, ndocs)
                   : prof == 3 ? store_layout(e->s3, k, ndocs)
+                  : prof == 4 ? store_layout(e->s4, k, ndocs)
                               : store_layout(e->s2, k, ndocs);
     if (hipMalloc(&e->mem, (size_t)bytes) != hipSuccess) {
         delete e;
@@ -370,7 +410,7 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
         delete e;
         return MT_E_HIP;
     }
-    e->s0.base = e->s1.base = e->s2.base = e->s3.base = (uint8_t*)e->mem;
+    e->s0.base = e->s1.base = e->s2.base = e->s3.base = e->s4.base = (uint8_t*)e->mem;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
         mt_engine_destroy(e);
@@ -523,6 +563,8 @@ int32_t mt_engine_run(mt_engine* e) {
                 launch(k_replay<HT, false, 7, 2>);
             else
                 launch(k_replay<HT, false, 7, 0>);
+        } else if constexpr (HT::TILED) {
+            launch(k_replay_tiled<HT>);
         } else {
             launch(k_replay<HT, false>);
         }

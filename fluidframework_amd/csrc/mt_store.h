@@ -28,7 +28,7 @@ struct Store {
         Doc<HT> v;
         v.t = (HT*)b;
         v.cold = (ColdRow*)(b + offCold);
-        v.frid = (int16_t*)(b + offFrid);
+        v.frid = (typename HT::IX*)(b + offFrid);
         v.arena = (uint16_t*)(b + offArena);
         v.mgid = (int32_t*)(b + offMgid);
         v.mrid = (int32_t*)(b + offMrid);
@@ -54,7 +54,7 @@ inline int64_t store_layout(Store<HT>& st, const Caps& caps, int64_t ndocs) {
     st.offCold = o;
     o = align256(o + (int64_t)sizeof(ColdRow) * HT::S);
     st.offFrid = o;
-    o = align256(o + 2 * (int64_t)HT::S);
+    o = align256(o + (int64_t)sizeof(typename HT::IX) * HT::S);
     st.offArena = o;
     o = align256(o + 2 * 2 * (int64_t)caps.acap);
     st.offMgid = o;
@@ -71,12 +71,13 @@ inline int64_t store_layout(Store<HT>& st, const Caps& caps, int64_t ndocs) {
 
 inline bool caps_valid(const Caps& k) { return k.acap >= 16 && k.mcap >= 4 && k.gcap >= 1; }
 
-/* profiles: 0 = HotSmall (LDS-resident on the GPU), 3 = HotMat, 1 = HotMid, 2 = HotBig */
+/* profiles: 0 = HotSmall, 3 = HotMat, 1 = HotMid, 2 = HotBig, 4 = HotHuge (tiled, config 4) */
 inline int profile_for(int32_t ncap) {
     if (ncap <= HotSmall::N) return 0;
     if (ncap <= HotMat::N) return 3;
     if (ncap <= HotMid::N) return 1;
     if (ncap <= HotBig::N) return 2;
+    if (ncap <= HotHuge::N) return 4;
     return -1;
 }
 

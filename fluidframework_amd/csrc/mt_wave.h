@@ -22,6 +22,7 @@ struct WaveHost {
     int32_t writelane(int32_t v, int, int32_t) const { return v; }
     static int ffs(uint64_t m) { return __builtin_ctzll(m); }
     void sync() const {}
+    static void atomic_add(int32_t* p, int32_t v) { *p += v; }
 };
 
 #ifdef __HIPCC__
@@ -68,6 +69,8 @@ struct WaveGPU {
         return __builtin_amdgcn_readlane(v, l);
     }
     __device__ __attribute__((always_inline)) static int ffs(uint64_t m) { return __builtin_ctzll(m); }
+    /* per-lane add into wave-shared scratch (LDS in the tiled replay kernel) */
+    __device__ __attribute__((always_inline)) static void atomic_add(int32_t* p, int32_t v) { atomicAdd(p, v); }
     /* Order the wave's memory accesses between lanes. One wavefront replays one document, so every
      * hand-off is between lanes of the same wave: its LDS operations execute in program order and so
      * do its vector-memory operations to one address, so only the compiler has to be kept from

@@ -74,6 +74,10 @@ def _p(a: np.ndarray):
 
 def default_caps(ops_per_doc: int, config: int = 3) -> dict:
     """Capacities sized for the synthetic configs (high-water marks measured with the oracle)."""
+    if config == 4:
+        # tiled large-document profile (HotHuge: 262,144 nodes, 32-bit ids); a 1M-op config-4
+        # document peaks at ~112k nodes, 422k rows and 3.2M text units
+        return dict(ncap=1 << 18, hcap=1 << 12, acap=1 << 22, mcap=4096, gcap=1024, ccap=64)
     if config == 5 and ops_per_doc <= 5_000:
         # PermutationVector replicas (HotMat: 640 nodes / 5120 slots; peak ~540 nodes at 4,096)
         return dict(ncap=640, hcap=1024, acap=1 << 4, mcap=1024, gcap=1024, ccap=64)

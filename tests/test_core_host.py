@@ -38,3 +38,43 @@ def test_host_core_matches_oracle(name, w, ndocs, caps):
         cur = c.current_seq
         for k in (0, 2, 5):
             assert st.text(d, cur - 3, k) == c.get_text_at(cur - 3, k)
+
+
+TILED = (1 << 18, 0, 1 << 20, 8192, 1024, 64)  # the config-4 profile (HotHuge): rope + STABLE summaries
+
+
+@pytest.mark.parametrize("name,w,ndocs", [
+    ("config1", gen.config1(3000), 8),
+    ("config2", gen.config2(3000), 6),
+    ("config3", gen.config3(2048), 8),
+    ("config5", gen.config5(2000), 6),
+])
+def test_tiled_profile_matches_oracle_on_every_shape(name, w, ndocs):
+    """The large-document profile's position index (chunk rope, STABLE summaries, window set) gives
+    the same replay as the oracle on every config shape, including local-pending edits and acks."""
+    b = gen.generate(w, ndocs)
+    _, odig, oerr = oc.replay_batch(b, threads=8)
+    hdig, herr, st = core_host.replay_batch(b, TILED)
+    assert (herr == 0).all(), herr
+    assert (hdig == odig).all(), f"{name}: docs {np.nonzero(hdig != odig)[0][:5]} differ"
+    d = 0
+    ops, text, props, kv = b.doc(d)
+    c = oc.OracleClient()
+    c.start_collab(int(b.local_long_id[d]))
+    c.replay_arrays(ops, text, props, kv)
+    cur = c.current_seq
+    for k in (0, 2, 5):  # perspectives the summaries answer, and one below minSeq (walk fallback)
+        for ref in (cur, cur - 3, max(0, c.min_seq - 5)):
+            assert st.text(d, ref, k) == c.get_text_at(ref, k)
+
+
+def test_tiled_profile_config4_60k_ops():
+    """Config 4 shape at 60k sequenced messages (25k live rows, 5k leaves, ~100 chunks)."""
+    b = gen.generate(gen.config4(60000), 1)
+    c = oc.OracleClient()
+    c.start_collab(1)
+    c.replay_arrays(*b.doc(0))
+    hdig, herr, st = core_host.replay_batch(b, (1 << 18, 0, 1 << 22, 8192, 1024, 64))
+    assert herr[0] == 0
+    assert int(hdig[0]) == c.digest()
+    assert c.stats()["nlive"] > 20000

@@ -127,12 +127,32 @@ def test_large_doc_props_newlines():
     _check_batch(b, 6000, ndump=2, ncap=4096, hcap=8192, acap=1 << 17)
 
 
-def test_large_doc_29k_rows():
-    """Config-4 shape at 20k ops/doc: ~29k rows (tombstones included) and ~6k leaves per document in
-    the 16,384-node profile — the deepest flat scans the engine runs."""
+def test_large_doc_flat_profile_20k():
+    """Config-4 shape at 20k ops/doc in the flat 16,384-node profile (~8.5k rows, ~1.8k leaves)."""
     w = gen.config4(20000)
     b = gen.generate(w, 2)
     _check_batch(b, 20000, ndump=2, ncap=16384, hcap=16384, acap=1 << 20)
+
+
+def test_config4_tiled_over_100k_live_rows():
+    """Config 4 on the tiled large-document profile (chunk rope + STABLE summaries + window set, one
+    workgroup per document): two documents of 300k sequenced messages end with >100k live rows
+    each, and replay bit-exact against the oracle."""
+    from fluidframework_amd.engine import default_caps
+    b = gen.generate(gen.config4(300_000), 2)
+    for d in range(2):
+        c = oc.OracleClient()
+        c.start_collab(1)
+        c.replay_arrays(*b.doc(d))
+        assert c.stats()["nlive"] > 100_000
+    _check_batch(b, 300_000, ndump=1, **default_caps(300_000, config=4))
+
+
+def test_tiled_profile_local_pending_config3():
+    """The tiled profile on config-3 documents (local-pending edits, acks, lag): same digests."""
+    from fluidframework_amd.engine import default_caps
+    b = gen.generate(gen.config3(2048), 16)
+    _check_batch(b, 2048, ndump=2, every=True, **default_caps(2048, config=4))
 
 
 def test_matrix_permutation_vectors_config5():

@@ -47,7 +47,7 @@ SETS = {
     "c2_observer": (gen.config2(2000), list(range(96))),
     "c3_lagged": (gen.config3(1500), list(range(128))),
     "c3_lagged_long": (gen.config3(4096), list(range(1000, 1032))),         # the bench's doc length
-    "c4_scaled": (gen.config4(3000), list(range(6))),                       # coalescing defeated
+    "c4_scaled": (gen.config4(20000), list(range(4))),                      # coalescing defeated, MSN advancing
     "c5_perm": (gen.config5(1500), list(range(64))),                        # PermutationSegment rows
 }
 
