@@ -2602,8 +2602,10 @@ struct Replica {
             return;
         }
         get_or_add_short(op.client);
-        h.seqOps++;
-        if constexpr (TILED) /* BASELINE.md tile formula, in 16-byte units: 4 B per chunk summary,
+        bool grouped = (op.kind & MT_OPF_GROUPED) != 0; /* a group member before the last (mt_oplog.h) */
+        if (!grouped) h.seqOps++; /* one sequenced message per group */
+        if (grouped) {
+        } else if constexpr (TILED) /* BASELINE.md tile formula, in 16-byte units: 4 B per chunk summary,
                                 64 B per window row, 640 B for the target chunk's leaves + leaf line */
             h.sumR += (4 * z.tl.nchunk + 64 * z.tl.wN + 640) / 16;
         else
@@ -2622,6 +2624,10 @@ struct Replica {
                 if (!(h.currentSeq < op.seq)) fail(E_ASSERT);
                 if (!(h.minSeq <= op.min_seq)) fail(E_ASSERT);
             }
+        }
+        if (grouped) { /* the message's seq update waits for its last member (client.ts:782-790, 615-622) */
+            h.opsDone++;
+            return;
         }
         /* updateSeqNumbers (client.ts:821-828) */
         if (!(h.currentSeq <= op.seq)) fail(E_ASSERT);

@@ -28,6 +28,7 @@
  * (distinct insert props, trailing newlines) used by the large-doc config.
  */
 #include <pthread.h>
+#include <initializer_list>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -183,9 +184,36 @@ static void gen_op(const mtg_params* P, rng_t* r, Model<HT>* m, int32_t refSeq, 
 }
 
 typedef struct {
-    mt_op_rec op;
-    int32_t target;
+    mt_op_rec op, op2; /* op2: the remove of a replaceRange group (nmem == 2) */
+    int32_t target, nmem;
 } Pending;
+
+/* SharedString.replaceRange (sequence.ts:455-469) as the generator issues it: under perspective
+ * (refSeq, client) of a document of length len > 0, insert text at end, then remove [start, end)
+ * (positions of the client's view after its own insert). Fills the two member ops; the caller
+ * applies the first before drawing the second is not needed: [start, end) precedes the insert. */
+static void gen_replace(const mtg_params* P, rng_t* r, int32_t len, Out* o, mt_op_rec* ins, mt_op_rec* rem,
+                        int insert_index) {
+    int32_t start = uni(r, 0, len - 1);
+    int32_t end = start + uni(r, 1, P->max_rem_len);
+    if (end > len) end = len;
+    memset(ins, 0, sizeof *ins);
+    memset(rem, 0, sizeof *rem);
+    ins->kind = MT_OP_INSERT;
+    ins->pos1 = end;
+    int tl = uni(r, 1, P->max_ins_len);
+    if (o->ntext + tl > o->tcap) {
+        o->overflow = 1;
+        tl = 0;
+    }
+    ins->text_off = (uint32_t)o->ntext;
+    for (int i = 0; i < tl; i++) o->text[o->ntext++] = (uint16_t)ALNUM[uni(r, 0, 61)];
+    ins->text_len = (uint16_t)tl;
+    if (P->distinct_props) ins->props = (uint16_t)(1 + ANN_RECORDS + (insert_index % 4096));
+    rem->kind = MT_OP_REMOVE;
+    rem->pos1 = start;
+    rem->pos2 = end;
+}
 
 template <class HT>
 static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_rec* props, const mt_kv* kv) {
@@ -232,6 +260,37 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
             int32_t cur = m.r->h.currentSeq;
             /* 1. a local edit, made against the local view (client.ts:164-211) */
             if (P->local_pct && uni(&r, 0, 99) < P->local_pct && qn < 4000) {
+                int32_t llen = m_length(&m, cur, me, 1);
+                if (P->group_pct && llen > 0 && uni(&r, 0, 99) < P->group_pct) { /* local replaceRange */
+                    mt_op_rec ins, rem;
+                    gen_replace(P, &r, llen, o, &ins, &rem, insert_index);
+                    if (ins.text_len == 0) continue;
+                    insert_index++;
+                    mt_op_rec* e1 = emit(o);
+                    mt_op_rec* e2 = e1 ? emit(o) : NULL;
+                    if (!e2) break;
+                    *e1 = ins;
+                    *e2 = rem;
+                    for (mt_op_rec* e : {e1, e2}) {
+                        e->kind |= MT_OPF_LOCAL;
+                        e->client = (uint16_t)me;
+                        e->seq = -1;
+                        e->ref_seq = cur;
+                        m_apply(&m, e);
+                    }
+                    int32_t target = cur + uni(&r, 1, P->ack_lag > 0 ? P->ack_lag : 1);
+                    if (target <= lastTarget) target = lastTarget + 1;
+                    lastTarget = target;
+                    Pending pe;
+                    pe.op = ins;
+                    pe.op2 = rem;
+                    pe.op.ref_seq = pe.op2.ref_seq = cur;
+                    pe.op.client = pe.op2.client = (uint16_t)me;
+                    pe.target = target;
+                    pe.nmem = 2;
+                    q[qh + qn++] = pe;
+                    continue;
+                }
                 mt_op_rec* e = emit(o);
                 if (!e) break;
                 gen_op(P, &r, &m, cur, me, 1, o, e, insert_index);
@@ -253,6 +312,7 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
                 pe.op.kind &= (uint8_t)~MT_OPF_LOCAL;
                 pe.op.ref_seq = cur;
                 pe.target = target;
+                pe.nmem = 1;
                 q[qh + qn++] = pe;
                 continue;
             }
@@ -271,6 +331,15 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
                 *e = pe.op;
                 e->seq = seq;
                 e->min_seq = msn;
+                if (pe.nmem == 2) { /* the group's first member, then the last (below) */
+                    e->kind |= MT_OPF_GROUPED;
+                    m_apply(&m, e);
+                    e = emit(o);
+                    if (!e) break;
+                    *e = pe.op2;
+                    e->seq = seq;
+                    e->min_seq = msn;
+                }
             } else {
                 int client = uni(&r, 0, nclients - 2);
                 if (client >= me) client++;
@@ -282,12 +351,35 @@ static void gen_doc_t(const mtg_params* P, int64_t doc, Out* o, const mt_props_r
                 for (int k = 0; k < nclients; k++)
                     if (lastRef[k] < mn && (k != me || me_in_msn)) mn = lastRef[k];
                 if (mn > msn) msn = mn;
-                gen_op(P, &r, &m, ref, client, 0, o, e, insert_index);
-                e->client = (uint16_t)client;
-                e->seq = seq;
-                e->ref_seq = ref;
-                e->min_seq = msn;
-                if (e->kind == MT_OP_INSERT) insert_index++;
+                int32_t rlen = P->group_pct ? m_length(&m, ref, client, 0) : 0;
+                if (P->group_pct && rlen > 0 && uni(&r, 0, 99) < P->group_pct) { /* remote replaceRange */
+                    mt_op_rec ins, rem;
+                    gen_replace(P, &r, rlen, o, &ins, &rem, insert_index);
+                    insert_index++;
+                    for (mt_op_rec* x : {&ins, &rem}) {
+                        x->client = (uint16_t)client;
+                        x->seq = seq;
+                        x->ref_seq = ref;
+                        x->min_seq = msn;
+                    }
+                    if (ins.text_len == 0) { /* nothing to insert: a plain remove message */
+                        *e = rem;
+                    } else {
+                        *e = ins;
+                        e->kind |= MT_OPF_GROUPED;
+                        m_apply(&m, e);
+                        e = emit(o);
+                        if (!e) break;
+                        *e = rem;
+                    }
+                } else {
+                    gen_op(P, &r, &m, ref, client, 0, o, e, insert_index);
+                    e->client = (uint16_t)client;
+                    e->seq = seq;
+                    e->ref_seq = ref;
+                    e->min_seq = msn;
+                    if (e->kind == MT_OP_INSERT) insert_index++;
+                }
             }
             m_apply(&m, e);
         }

@@ -24,6 +24,8 @@ typedef struct mtg_params {
     int32_t perm;          /* inserts are PermutationSegments of U{1..max_ins_len} rows    */
     int32_t round_ops;     /* MTG_FARM: ops generated per round before any is sequenced    */
     int32_t min_length;    /* MTG_FARM: below this local length a client only inserts      */
+    int32_t group_pct;     /* MTG_LAGGED: % of edits that are replaceRange groups (insert + remove,
+                              one sequenced GROUP message; sequence.ts:455-469)             */
     uint64_t seed_base;    /* doc d uses splitmix64 seed seed_base + d                     */
 } mtg_params;
 int mtg_generate(const mtg_params* P, int64_t doc_base, int64_t ndocs, int64_t op_stride, int64_t text_stride,

@@ -19,7 +19,7 @@ class _Params(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "mode", "ops_per_doc", "nclients", "max_lag", "local_pct", "ack_lag", "pct_insert",
         "pct_remove", "max_ins_len", "max_rem_len", "distinct_props", "newline_pct", "model_ncap",
-        "model_acap", "perm", "round_ops", "min_length")] + [
+        "model_acap", "perm", "round_ops", "min_length", "group_pct")] + [
         ("seed_base", ctypes.c_uint64)]
 
 
@@ -42,6 +42,7 @@ class Workload:
     perm: int = 0
     round_ops: int = 0
     min_length: int = 0
+    group_pct: int = 0
     seed_base: int = 0x5EED0000
 
 
@@ -60,8 +61,9 @@ def config2(ops_per_doc: int = 10_000) -> Workload:
 
 
 def config3(ops_per_doc: int = 4_096) -> Workload:
-    """65,536 docs, 8 clients, lag <= 64, local-pending replica (~1/8 local edits)."""
-    return Workload(MTG_LAGGED, ops_per_doc, max_lag=64, local_pct=12, ack_lag=64)
+    """65,536 docs, 8 clients, lag <= 64, local-pending replica (~1/8 local edits); 4% of the edits
+    (local and remote) are SharedString.replaceRange groups (insert + remove in one message)."""
+    return Workload(MTG_LAGGED, ops_per_doc, max_lag=64, local_pct=12, ack_lag=64, group_pct=4)
 
 
 def config4(ops_per_doc: int = 1_000_000) -> Workload:

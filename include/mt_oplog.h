@@ -38,6 +38,12 @@ enum {
 };
 #define MT_OP_KIND_MASK 0x07
 #define MT_OPF_LOCAL 0x80 /* unsequenced local edit made by this replica */
+/* A group op (MergeTreeDeltaType.GROUP, ops.ts:33, 100; e.g. SharedString.replaceRange,
+ * sequence.ts:464) is one sequenced message carrying several member ops: it is sent as its member
+ * records in order, all with the message's client/seq/ref_seq/min_seq, every member but the last
+ * flagged MT_OPF_GROUPED. Members apply (or, for this replica's own message, ack) one after another
+ * under the one seq (client.ts:782-790, 615-622); the message's updateSeqNumbers runs after the last. */
+#define MT_OPF_GROUPED 0x40
 
 /* segment kinds */
 enum {

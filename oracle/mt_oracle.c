@@ -1718,6 +1718,9 @@ int mto_apply(mto_client* c, const mt_op_rec* op, const uint16_t* text, const mt
             applyOp(c, op, 0, sid, op->ref_seq, op->seq);
         }
     }
+    /* a group member other than the last: the message's seq update comes after its last member
+     * (applyRemoteOp recursion client.ts:782-790, ackPendingSegment loop 615-622) */
+    if (op->kind & MT_OPF_GROUPED) return c->err;
     /* updateSeqNumbers (821-828) */
     if (!(c->cw.currentSeq <= op->seq)) FAIL(c, MTO_ERR_ASSERT);
     c->cw.currentSeq = op->seq;

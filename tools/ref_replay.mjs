@@ -92,6 +92,7 @@ function replayDoc(doc) {
     const client = new Client(specToSegment, logger);
     const local = localIds.readInt32LE(4 * doc);
     if (local >= 0) client.startOrUpdateCollaboration(name(local));
+    let members = []; // members of a group message so far (records flagged GROUPED, mt_oplog.h)
     for (let i = opOff[doc]; i < opOff[doc + 1]; i++) {
         const rec = record(i);
         const kind = rec.kind & 7;
@@ -110,10 +111,12 @@ function replayDoc(doc) {
             }
             continue;
         }
+        if (rec.kind & 0x40) { members.push(wireOp(doc, rec)); continue; }
+        let contents = kind === 4 ? undefined : wireOp(doc, rec);
+        if (members.length) { contents = { type: 3, ops: [...members, contents] }; members = []; } // createGroupOp (opBuilder.ts:128-134)
         client.applyMsg({
             clientId: name(rec.client), sequenceNumber: rec.seq, referenceSequenceNumber: rec.ref_seq,
-            minimumSequenceNumber: rec.min_seq, type: kind === 4 ? "noop" : "op",
-            contents: kind === 4 ? undefined : wireOp(doc, rec),
+            minimumSequenceNumber: rec.min_seq, type: kind === 4 ? "noop" : "op", contents,
         });
     }
     return client;
