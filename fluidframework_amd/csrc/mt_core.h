@@ -2664,6 +2664,55 @@ struct Replica {
         return n;
     }
 
+    /* ---- reads: getContainingSegment / getPosition (mergeTree.ts:1656-1667, 1619-1636) ---- */
+    /* The row holding position pos under the perspective (searchBlock descends to the first child
+     * with pos < length: the first row with P <= pos < P + vis); *off = pos - P. -1 if none. */
+    MT_HD int32_t containing(int32_t pos, int32_t refSeq, int32_t client, int32_t* off) {
+        if (pos < 0) return -1;
+        int32_t P = 0;
+        int32_t t = find_reach(pos + 1, refSeq, client, &P);
+        if (t < 0) return -1;
+        *off = pos - P;
+        return slot_at(t);
+    }
+    /* getPosition: the summed perspective lengths of every row before slot s in document order */
+    MT_HD int32_t position_of(int32_t s, int32_t refSeq, int32_t client) {
+        int32_t k0 = kpos(s / MAXN), j0 = s & (MAXN - 1);
+        int32_t total = 0;
+        if constexpr (TILED) {
+            if (tiles_cover(refSeq, client)) { /* chunks before, leaves before in the chunk, rows before */
+                auto& t = z.tl;
+                win_pass(refSeq, client);
+                int32_t cp = k0 >> 6, li = k0 & 63, c = t.cord[cp];
+                for (int32_t b = 0; b < cp; b += W::N) {
+                    int32_t p = b + w.lane();
+                    total += w.sum(p < cp ? t.cst[p] + cdel[p] : 0);
+                }
+                for (int32_t b = 0; b < li; b += W::N) {
+                    int32_t l = b + w.lane();
+                    total += w.sum(l < li ? t.lst[t.cleaf[c][l]] : 0);
+                }
+                int32_t nw = t.wN;
+                for (int32_t b = 0; b < nw; b += W::N) {
+                    int32_t i = b + w.lane();
+                    total += w.sum(i < nw && wcp[i] == cp && wlx[i] < li ? wvs[i] : 0);
+                }
+                win_clear();
+                int32_t n = leaf_at(k0);
+                for (int32_t j = 0; j < j0; j++) total += vis(n * MAXN + j, refSeq, client);
+                return total;
+            }
+        }
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+            int32_t n = leaf_at(k), c = nch[n];
+            for (int32_t j = 0; j < c; j++) {
+                if (k == k0 && j == j0) return total;
+                total += vis(n * MAXN + j, refSeq, client);
+            }
+        }
+        return total;
+    }
+
     /* ---- canonical dump (include/mt_oplog.h) ------------------------------------------- */
     /* byte sink: writes into a buffer (if any) and/or folds FNV-1a-64 */
     struct Sink {

@@ -146,6 +146,27 @@ int64_t mth_text(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client
     });
 }
 
+/* getContainingSegment + getPosition of the found row: out6 = {found, offset, length, seq, long client,
+ * position} (the layout of the oracle's mto_get_containing) */
+int32_t mth_containing(mth_store* s, int64_t doc, int32_t pos, int32_t ref_seq, int32_t long_client, int32_t* out6) {
+    return with_replica(s, doc, [&](auto& r) {
+        int32_t sh = long_client < 0 ? r.h.localShort : r.short_of(long_client);
+        int32_t rs = long_client < 0 ? r.h.currentSeq : ref_seq;
+        if (sh < 0) sh = 0x7fff;
+        for (int i = 0; i < 6; i++) out6[i] = 0;
+        int32_t off = 0;
+        int32_t slot = r.containing(pos, rs, sh, &off);
+        if (slot < 0) return 0;
+        out6[0] = 1;
+        out6[1] = off;
+        out6[2] = r.z.len(slot);
+        out6[3] = r.z.seq(slot);
+        out6[4] = r.long_of(r.z.cli(slot));
+        out6[5] = r.position_of(slot, rs, sh);
+        return 1;
+    });
+}
+
 int64_t mth_dump(mth_store* s, int64_t doc, uint8_t* out, int64_t cap) {
     return with_replica(s, doc, [&](auto& r) { return r.dump(out, cap); });
 }

@@ -21,6 +21,7 @@ int64_t mth_text(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client
 int64_t mth_dump(mth_store* s, int64_t doc, uint8_t* out, int64_t cap);
 uint64_t mth_digest(mth_store* s, int64_t doc);
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8);
+int32_t mth_containing(mth_store* s, int64_t doc, int32_t pos, int32_t ref_seq, int32_t long_client, int32_t* out6);
 #ifdef __cplusplus
 }
 #endif

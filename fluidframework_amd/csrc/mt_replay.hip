@@ -264,6 +264,45 @@ __global__ __launch_bounds__(WG) void k_text(Store<HT> st, int64_t doc, int32_t 
     if (threadIdx.x == 0) *n = m;
 }
 
+/* getContainingSegment (mode 0: a = pos) / getPosition (mode 1: a = rid, b = gen) of one document;
+ * out[0] = status (1 found / 0 none), then mt_seg_ref fields or the position */
+template <class HT>
+__global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t mode, int32_t a, int32_t b,
+                                           int32_t ref_seq, int32_t long_client, int32_t* out) {
+    Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
+    int32_t sh;
+    if (long_client < 0) {
+        sh = r.h.localShort;
+        ref_seq = r.h.currentSeq;
+    } else {
+        sh = r.short_of(long_client);
+        if (sh < 0) sh = 0x7fff; /* a client the replica has not seen: sequenced content only */
+    }
+    int32_t res[7] = {0, -1, 0, 0, 0, 0, 0};
+    if (mode == 0) {
+        int32_t off = 0;
+        int32_t s = r.containing(a, ref_seq, sh, &off);
+        if (s >= 0) {
+            int32_t rid = r.z.rid[s];
+            res[0] = 1;
+            res[1] = rid;
+            res[2] = r.z.rgen[rid];
+            res[3] = off;
+            res[4] = r.z.len(s);
+            res[5] = r.z.seq(s);
+            res[6] = r.long_of(r.z.cli(s));
+        }
+    } else {
+        int32_t s = (a >= 0 && a < HT::S) ? r.slot_of(a, b) : -1;
+        if (s >= 0) {
+            res[0] = 1;
+            res[1] = r.position_of(s, ref_seq, sh);
+        }
+    }
+    if (threadIdx.x == 0)
+        for (int i = 0; i < 7; i++) out[i] = res[i];
+}
+
 /* per-doc header fields: errors, stats, roofline work counters */
 template <class HT>
 __global__ void k_hdr(Store<HT> st, int64_t ndocs, int32_t* err, int32_t* err_op, int32_t* stats4, int64_t* work3) {
@@ -700,6 +739,50 @@ int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t l
         if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
     }
     return n;
+}
+
+static int32_t seg_query(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,
+                         int32_t long_client, int32_t* res7) {
+    if (!e || doc < 0 || doc >= e->ndocs) return MT_E_ARG;
+    HIPCHK(e, hipSetDevice(e->device));
+    int32_t rc = ensure(e, e->tmp, 64);
+    if (rc) return rc;
+    rc = with_store(e, [&](auto& st) {
+        using HT = typename std::decay_t<decltype(st)>::Hot;
+        hipLaunchKernelGGL((k_seg<HT>), dim3(1), dim3(WG), 0, e->stream, st, doc, mode, a, b, ref_seq, long_client,
+                           (int32_t*)e->tmp.p);
+        return launch_check(e, "k_seg");
+    });
+    if (rc) return rc;
+    HIPCHK(e, hipMemcpyAsync(res7, e->tmp.p, 7 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return MT_OK;
+}
+
+int32_t mt_engine_get_containing_segment(mt_engine* e, int64_t doc, int32_t pos, int32_t ref_seq, int32_t long_client,
+                                         mt_seg_ref* out) {
+    if (!out) return MT_E_ARG;
+    int32_t r[7];
+    int32_t rc = seg_query(e, doc, 0, pos, 0, ref_seq, long_client, r);
+    if (rc) return rc;
+    out->rid = r[0] ? r[1] : -1;
+    out->gen = r[2];
+    out->offset = r[3];
+    out->length = r[4];
+    out->seq = r[5];
+    out->client = r[6];
+    return MT_OK;
+}
+
+int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t gen, int32_t ref_seq,
+                               int32_t long_client, int32_t* out) {
+    if (!out) return MT_E_ARG;
+    int32_t r[7];
+    int32_t rc = seg_query(e, doc, 1, rid, gen, ref_seq, long_client, r);
+    if (rc) return rc;
+    if (!r[0]) return MT_E_ARG;
+    *out = r[1];
+    return MT_OK;
 }
 
 #ifdef MT_PROF

@@ -25,6 +25,11 @@ class EngineError(RuntimeError):
     pass
 
 
+class SegRef(ctypes.Structure):
+    """mt_seg_ref: a segment handle (row id + generation) and where the position falls in it."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("rid", "gen", "offset", "length", "seq", "client")]
+
+
 class _Caps(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("ncap", "hcap", "acap", "mcap", "gcap", "ccap")]
 
@@ -62,6 +67,8 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_get_text.argtypes = [vp, i64, i32, i32, vp, i64]
         L.mt_engine_get_text.restype = i64
         L.mt_engine_stats.argtypes = [vp, vp]
+        L.mt_engine_get_containing_segment.argtypes = [vp, i64, i32, i32, i32, ctypes.POINTER(SegRef)]
+        L.mt_engine_get_position.argtypes = [vp, i64, i32, i32, i32, i32, ctypes.POINTER(i32)]
         L.mt_engine_ndocs.argtypes = [vp]
         L.mt_engine_ndocs.restype = i64
         _LIB = L
@@ -190,6 +197,21 @@ class Engine:
         buf = np.zeros(max(n, 1), "<u2")
         self.L.mt_engine_get_text(self.h, doc, ref_seq, long_client, _p(buf), n)
         return buf[:n].tobytes().decode("utf-16-le")
+
+    def get_containing_segment(self, doc: int, pos: int, ref_seq: int = 0, long_client: int = -1) -> Optional[SegRef]:
+        """MergeTree.getContainingSegment (mergeTree.ts:1656-1667); long_client < 0 = the local view
+        (Client.getContainingSegment). None where the reference returns `segment: undefined`."""
+        r = SegRef()
+        self._check(self.L.mt_engine_get_containing_segment(self.h, doc, pos, ref_seq, long_client, ctypes.byref(r)),
+                    "get_containing_segment")
+        return None if r.rid < 0 else r
+
+    def get_position(self, doc: int, seg: SegRef, ref_seq: int = 0, long_client: int = -1) -> int:
+        """MergeTree.getPosition of a segment handle (mergeTree.ts:1619-1636)."""
+        v = ctypes.c_int32()
+        self._check(self.L.mt_engine_get_position(self.h, doc, seg.rid, seg.gen, ref_seq, long_client, ctypes.byref(v)),
+                    "get_position")
+        return v.value
 
     def stats(self) -> np.ndarray:
         out = np.zeros((self.ndocs, 4), np.int32)

@@ -93,6 +93,25 @@ int32_t mt_engine_get_length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t
  * local view. Returns the length in UTF-16 units (writes at most cap), <0 on error. */
 int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* out,
                            int64_t cap);
+/* A segment handle (the reference returns live ISegment objects, mergeTree.ts:87-117): the row's
+ * stable id and its generation. A handle stops resolving once zamboni merges the row into its
+ * neighbour or unlinks it (mergeTree.ts:1322-1398), as a detached reference segment would. */
+typedef struct mt_seg_ref {
+    int32_t rid;    /* row id, -1: no segment at the position (the reference's `segment: undefined`) */
+    int32_t gen;    /* row-id generation */
+    int32_t offset; /* position - the segment's start */
+    int32_t length; /* cachedLength */
+    int32_t seq;    /* the segment's seq (-1: local, unacked) */
+    int32_t client; /* long client index of its inserter, -1 = LocalClientId */
+} mt_seg_ref;
+/* MergeTree.getContainingSegment(pos, refSeq, clientId) (mergeTree.ts:1656-1667); long_client < 0 =
+ * Client.getContainingSegment, the local view (client.ts:1006-1008). */
+int32_t mt_engine_get_containing_segment(mt_engine* e, int64_t doc, int32_t pos, int32_t ref_seq, int32_t long_client,
+                                         mt_seg_ref* out);
+/* MergeTree.getPosition(segment, refSeq, clientId) (mergeTree.ts:1619-1636) of a handle;
+ * MT_E_ARG if the handle no longer resolves. long_client < 0 = Client.getPosition (client.ts:291). */
+int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t gen, int32_t ref_seq,
+                               int32_t long_client, int32_t* out);
 /* Per-doc counters: nleaf, high-water row slots, high-water heap, events applied. */
 int32_t mt_engine_stats(mt_engine* e, int32_t* out4_per_doc);
 int64_t mt_engine_ndocs(const mt_engine* e);

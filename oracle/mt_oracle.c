@@ -1850,6 +1850,55 @@ int64_t mto_dump(mto_client* c, uint8_t* out, int64_t cap) {
     dumpWalk(c, c->root, &o, &l2, &s2);
     return o.n;
 }
+/* getContainingSegment (mergeTree.ts:1656-1667) through searchBlock (1830-1862) */
+static Seg* searchBlock(mto_client* c, Block* b, int pos, int refSeq, int clientId, int* offOut) {
+    for (int i = 0; i < b->childCount; i++) {
+        Node* child = b->children[i];
+        int len = nodeLength(c, child, refSeq, clientId);
+        if (pos < len) {
+            if (!child->isLeaf) return searchBlock(c, (Block*)child, pos, refSeq, clientId, offOut);
+            *offOut = pos;
+            return (Seg*)child;
+        }
+        pos -= len;
+    }
+    return NULL;
+}
+/* getPosition (mergeTree.ts:1619-1636) */
+static int getPosition(mto_client* c, Node* node, int refSeq, int clientId) {
+    int total = 0;
+    Block* parent = node->parent;
+    Node* prev = NULL;
+    while (parent) {
+        for (int i = 0; i < parent->childCount; i++) {
+            Node* child = parent->children[i];
+            if ((prev && child == prev) || child == node) break;
+            total += nodeLength(c, child, refSeq, clientId);
+        }
+        prev = &parent->hdr;
+        parent = parent->hdr.parent;
+    }
+    return total;
+}
+int mto_get_containing(mto_client* c, int pos, int refSeq, int shortClient, int32_t* out6) {
+    int cid = shortClient;
+    if (shortClient == -100) { /* Client.getContainingSegment: the local view (client.ts:1006-1008) */
+        cid = c->cw.clientId;
+        refSeq = c->cw.currentSeq;
+    }
+    int off = 0;
+    Seg* s = pos >= 0 ? searchBlock(c, c->root, pos, refSeq, cid, &off) : NULL;
+    for (int i = 0; i < 6; i++) out6[i] = 0;
+    if (!s) return 0;
+    out6[0] = 1;
+    out6[1] = off;
+    out6[2] = s->hdr.cachedLength;
+    out6[3] = s->seq;
+    out6[4] = longOf(c, s->clientId);
+    out6[5] = getPosition(c, &s->hdr, refSeq, cid);
+    return 1;
+}
+
 uint64_t mto_digest(mto_client* c) {
     int64_t n = mto_dump(c, NULL, 0);
     uint8_t* buf = xmalloc(n);

@@ -63,6 +63,9 @@ int mto_pending_groups(const mto_client* c);
 
 /* canonical binary dump (mt_oplog.h); returns bytes needed; writes if cap large enough */
 int64_t mto_dump(mto_client* c, uint8_t* out, int64_t cap);
+/* getContainingSegment(pos) under (refSeq, short client; -100 = the local view) and getPosition of
+ * that segment: out6 = {found, offset, length, seq, long client, position}; returns found. */
+int mto_get_containing(mto_client* c, int pos, int ref_seq, int short_client, int32_t* out6);
 uint64_t mto_digest(mto_client* c);
 
 /* statistics for sizing: number of segments / leaf blocks / tree height */

@@ -37,6 +37,7 @@ def lib():
         L.mth_digest.argtypes = [vp, i64]
         L.mth_digest.restype = ctypes.c_uint64
         L.mth_stats.argtypes = [vp, i64, vp]
+        L.mth_containing.argtypes = [vp, i64, i32, i32, i32, vp]
         _L = L
     return _L
 
@@ -88,6 +89,11 @@ class HostStore:
         buf = np.zeros(max(n, 1), "<u2")
         self.L.mth_text(self.h, doc, ref_seq, long_client, _p(buf), n)
         return buf[:n].tobytes().decode("utf-16-le")
+
+    def containing(self, doc, pos, ref_seq=0, long_client=-1):
+        out = np.zeros(6, np.int32)
+        self.L.mth_containing(self.h, doc, pos, ref_seq, long_client, _p(out))
+        return tuple(int(x) for x in out)
 
     def stats(self, doc):
         out = np.zeros(8, np.int32)

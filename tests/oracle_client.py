@@ -51,6 +51,7 @@ def lib():
         L.mto_digest.restype = ctypes.c_uint64
         L.mto_stats.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int)] * 4
         L.mto_check_partials.argtypes = [vp, i32, i32]
+        L.mto_get_containing.argtypes = [vp, i32, i32, i32, vp]
         L.mto_replay_batch.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp]
         L.mto_replay_batch.restype = ctypes.c_double
         _LIB = L
@@ -188,6 +189,16 @@ class OracleClient:
         buf = np.zeros(max(n, 1), "<u2")
         self.L.mto_get_text(self.h, ref_seq, short, _p(buf), n)
         return buf[:n].tobytes().decode("utf-16-le")
+
+    def containing(self, pos: int, ref_seq: int = 0, long_client: Optional[int] = None):
+        """(found, offset, length, seq, long client, position): getContainingSegment(pos) and
+        getPosition of that segment (mergeTree.ts:1656-1667, 1619-1636); None client = local view."""
+        out = np.zeros(6, np.int32)
+        short = -100 if long_client is None else self.short_id(long_client)
+        if long_client is not None and short < 0:
+            short = 0x7fff
+        self.L.mto_get_containing(self.h, pos, ref_seq, short, _p(out))
+        return tuple(int(x) for x in out)
 
     def pending_groups(self) -> int:
         return self.L.mto_pending_groups(self.h)

@@ -78,3 +78,30 @@ def test_tiled_profile_config4_60k_ops():
     assert herr[0] == 0
     assert int(hdig[0]) == c.digest()
     assert c.stats()["nlive"] > 20000
+
+
+@pytest.mark.parametrize("caps", [CAPS, TILED], ids=["flat", "tiled"])
+def test_containing_segment_and_position_match_oracle(caps):
+    """getContainingSegment / getPosition (mergeTree.ts:1656-1667, 1619-1636) under the local view
+    (Client.getContainingSegment / getPosition) and every client's view at the current seq.
+
+    Read queries at an arbitrary past perspective are not compared: there the reference answers from
+    its block PartialSequenceLengths, which for some (refSeq, client) pairs that no op is applied under
+    differ from the sum of the leaf lengths (e.g. config-3 doc 0, refSeq 2022, client 3:
+    the reference gives position 529, its own leaf predicate 530), while the engine sums the leaves.
+    Every op-time perspective agrees (the replay digests)."""
+    b = gen.generate(gen.config3(2048), 3)
+    _, _, st = core_host.replay_batch(b, caps)
+    rng = np.random.default_rng(5)
+    for d in range(3):
+        c = oc.OracleClient()
+        c.start_collab(int(b.local_long_id[d]))
+        c.replay_arrays(*b.doc(d))
+        cur, msn = c.current_seq, c.min_seq
+        views = [(0, None)] + [(cur, k) for k in range(8)]
+        for ref, k in views:
+            n = c.get_length() if k is None else c.get_length_at(ref, k)
+            for pos in list(rng.integers(0, max(n, 1), 12)) + [0, n - 1, n, n + 3]:
+                want = c.containing(int(pos), ref, k)
+                got = st.containing(d, int(pos), ref, -1 if k is None else k)
+                assert got == want, (d, ref, k, pos, got, want)

@@ -169,3 +169,39 @@ def test_matrix_permutation_vectors_config5():
         cur = c.current_seq
         for k in (0, 3):
             assert eng.get_length(d, cur - 5, k) == c.get_length_at(cur - 5, k)
+
+
+def test_containing_segment_and_position():
+    """getContainingSegment / getPosition through the C ABI (mt_engine_get_containing_segment /
+    mt_engine_get_position) against the oracle, flat and tiled profiles, local and current views;
+    a handle round-trips: getPosition(handle) + offset == pos."""
+    from fluidframework_amd.engine import default_caps
+    b = gen.generate(gen.config3(2048), 3)
+    rng = np.random.default_rng(9)
+    for caps in (default_caps(2048), default_caps(2048, config=4)):
+        eng = Engine_(b, caps)
+        for d in range(3):
+            c = oc.OracleClient()
+            c.start_collab(int(b.local_long_id[d]))
+            c.replay_arrays(*b.doc(d))
+            cur = c.current_seq
+            for k in (None, 0, 2, 5):
+                n = c.get_length() if k is None else c.get_length_at(cur, k)
+                for pos in list(rng.integers(0, max(n, 1), 8)) + [0, n - 1, n]:
+                    want = c.containing(int(pos), cur, k)
+                    lc = -1 if k is None else k
+                    seg = eng.get_containing_segment(d, int(pos), cur, lc)
+                    if not want[0]:
+                        assert seg is None
+                        continue
+                    got = (1, seg.offset, seg.length, seg.seq, seg.client, eng.get_position(d, seg, cur, lc))
+                    assert got == want, (d, k, pos, got, want)
+                    assert got[5] + got[1] == pos
+
+
+def Engine_(b, caps):
+    from fluidframework_amd.engine import Engine
+    eng = Engine(b.ndocs, **caps)
+    eng.start_collab(b.local_long_id)
+    eng.replay(b)
+    return eng

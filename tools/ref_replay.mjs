@@ -184,11 +184,26 @@ const MT = await import(path.join(erased, "index.mjs"));
 ({ Client, TextSegment, Marker } = MT);
 ({ PermutationSegment } = await import(path.join(erased, "permutationSegment.mjs")));
 const ndocs = opOff.length - 1;
+// optional read queries (queries.json: [[doc, pos, refSeq, longClient | -1 = local view], ...]):
+// getContainingSegment + getPosition (mergeTree.ts:1656-1667, 1619-1636) after the doc's replay
+const qpath = path.join(dir, "queries.json");
+const queries = fs.existsSync(qpath) ? JSON.parse(fs.readFileSync(qpath)) : [];
+const answers = [];
 const t0 = process.hrtime.bigint();
 const dumps = [], errs = {};
 for (let d = 0; d < ndocs; d++) {
     try {
         const c = replayDoc(d);
+        for (const [qd, pos, ref, cl] of queries) {
+            if (qd !== d) continue;
+            const mt = c.mergeTree;
+            const local = cl < 0;
+            const refSeq = local ? mt.collabWindow.currentSeq : ref;
+            const cid = local ? mt.collabWindow.clientId : c.getOrAddShortClientId(name(cl));
+            const { segment, offset } = mt.getContainingSegment(pos, refSeq, cid);
+            answers.push(segment === undefined ? [0, 0, 0, 0, 0, 0] : [1, offset, segment.cachedLength, segment.seq,
+                segment.clientId < 0 ? -1 : longOfName(c.getLongClientId(segment.clientId)), mt.getPosition(segment, refSeq, cid)]);
+        }
         dumps.push(timeOnly ? Buffer.alloc(0) : dump(c));
     } catch (e) {
         errs[d] = String(e && e.message || e);
@@ -205,6 +220,7 @@ if (!timeOnly) {
     fs.writeFileSync(path.join(dir, "ref_dump_off.bin"), off);
 }
 fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
+if (queries.length) fs.writeFileSync(path.join(dir, "ref_answers.json"), JSON.stringify(answers));
 console.log(JSON.stringify({ ndocs, errors: Object.keys(errs).length, seconds: secs }));
 }
 main().catch((e) => { console.error(e); process.exit(1); });
