@@ -1,0 +1,248 @@
+"use strict";
+/*
+ * mergetree_gpu.js — JavaScript facade over the MI355X replay engine (Node-API addon mt_napi.node ->
+ * libmtreplay.so, include/mt_engine.h). It keeps the part of the reference merge-tree Client surface
+ * the north star names (packages/dds/merge-tree/src/client.ts:43): startOrUpdateCollaboration,
+ * applyMsg (with group ops), insertTextLocal / insertMarkerLocal / removeRangeLocal /
+ * annotateRangeLocal, getLength, getText, getContainingSegment, getPosition, getCurrentSeq.
+ *
+ * A ReplayEngine holds a batch of documents on one GPU; engine.client(doc) is that document's
+ * replica. Edits and sequenced messages are queued per document in the packed record format
+ * (include/mt_oplog.h) and applied by the GPU at the next read (flush = submit + run + sync), so a
+ * stream of messages costs one launch per read, not one per message. Errors the engine latches for a
+ * document (insert failed, assert, invalid local range; client.ts:462-465, 527-544,
+ * mergeTree.ts:2243-2249) are thrown at that document's next read, as the reference throws
+ * synchronously. Node 12, CommonJS, no dependencies.
+ */
+const path = require("path");
+
+const addon = require(process.env.MT_NAPI_ADDON || path.join(__dirname, "..", "build", "mt_napi.node"));
+
+const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, GROUP: 3, NOOP: 4 };
+const OPF_LOCAL = 0x80;
+const OPF_GROUPED = 0x40;
+const SEG = { TEXT: 0, MARKER: 1 };
+const VALUE_FALSY = 0x8000;
+const ERRORS = { 1: "MergeTree insert failed", 2: "assertion", 3: "invalid op range", 4: "unsupported",
+    5: "capacity exceeded" };
+
+const DEFAULT_CAPS = { ncap: 192, hcap: 256, acap: 1 << 16, mcap: 1024, gcap: 1024, ccap: 64 };
+
+function canonical(v) {
+    if (v === null || typeof v !== "object") return JSON.stringify(v);
+    if (Array.isArray(v)) return "[" + v.map(canonical).join(",") + "]";
+    return "{" + Object.keys(v).sort().map((k) => JSON.stringify(k) + ":" + canonical(v[k])).join(",") + "}";
+}
+
+/* batch-global property key / value tables (value id 0 = null = delete, segmentPropertiesManager.ts:102-106) */
+class Interner {
+    constructor() { this.keys = new Map(); this.values = new Map(); this.nk = 1; this.nv = 1; }
+    key(k) {
+        let i = this.keys.get(k);
+        if (i === undefined) { i = this.nk++; this.keys.set(k, i); }
+        return i;
+    }
+    value(v) {
+        if (v === null || v === undefined) return 0;
+        const s = canonical(v);
+        let i = this.values.get(s);
+        if (i === undefined) { i = this.nv++; this.values.set(s, i); }
+        const falsy = typeof v !== "object" && !v;
+        return i | (falsy ? VALUE_FALSY : 0);
+    }
+}
+
+class DocQueue {
+    constructor() { this.recs = []; this.text = []; this.props = []; this.kv = []; }
+}
+
+class ReplayEngine {
+    constructor(ndocs, caps = DEFAULT_CAPS, device = 0) {
+        this.h = addon.create(device, ndocs, caps);
+        this.ndocs = ndocs;
+        this.interner = new Interner();
+        this.clientIds = new Map(); // long client id (string) -> engine long-client index
+        this.queues = Array.from({ length: ndocs }, () => new DocQueue());
+        this.localNames = new Array(ndocs).fill(undefined);
+        this.collab = false;
+        this.currentSeq = new Array(ndocs).fill(0);
+    }
+
+    longIndex(name) {
+        let i = this.clientIds.get(name);
+        if (i === undefined) { i = this.clientIds.size; this.clientIds.set(name, i); }
+        return i;
+    }
+
+    client(doc) { return new GpuClient(this, doc); }
+
+    /* startOrUpdateCollaboration for every document at once (mt_engine_start_collab) */
+    startCollaboration(localNames, minSeq = 0, currentSeq = 0) {
+        const ids = new Int32Array(this.ndocs);
+        for (let d = 0; d < this.ndocs; d++) {
+            this.localNames[d] = localNames[d];
+            ids[d] = this.longIndex(localNames[d]);
+            this.currentSeq[d] = currentSeq;
+        }
+        addon.startCollab(this.h, ids, minSeq, currentSeq);
+        this.collab = true;
+    }
+
+    enqueue(doc, kind, fields, segOrProps) {
+        const q = this.queues[doc];
+        const r = { kind, seg_kind: 0, client: 0, seq: 0, ref_seq: 0, min_seq: 0, pos1: 0, pos2: 0, text_off: 0,
+            text_len: 0, props: 0, ...fields };
+        const k = kind & 7;
+        if (k === OP.INSERT) {
+            const seg = segOrProps;
+            let props;
+            if (typeof seg === "string") {
+                r.text_off = q.text.length; r.text_len = seg.length;
+                for (let i = 0; i < seg.length; i++) q.text.push(seg.charCodeAt(i));
+            } else if (seg && seg.marker) {
+                r.seg_kind = SEG.MARKER; r.pos2 = seg.marker.refType; props = seg.props;
+            } else if (seg && typeof seg.text === "string") {
+                r.text_off = q.text.length; r.text_len = seg.text.length; props = seg.props;
+                for (let i = 0; i < seg.text.length; i++) q.text.push(seg.text.charCodeAt(i));
+            } else {
+                throw new Error("unsupported segment spec");
+            }
+            if (props) r.props = this.propsRecord(q, props, undefined);
+        } else if (k === OP.ANNOTATE) {
+            r.props = this.propsRecord(q, segOrProps.props, segOrProps.combiningOp);
+        }
+        q.recs.push(r);
+    }
+
+    propsRecord(q, props, combiningOp) {
+        const off = q.kv.length;
+        const keys = Object.keys(props);
+        for (const k of keys) q.kv.push([this.interner.key(k), this.interner.value(props[k])]);
+        if (combiningOp && combiningOp.name !== "rewrite") throw new Error(`combiningOp ${combiningOp.name} unsupported`);
+        q.props.push([off, keys.length, combiningOp ? 1 : 0]);
+        return q.props.length;
+    }
+
+    /* submit every queued event of every document, replay on the GPU, wait */
+    flush() {
+        let nrec = 0, ntext = 0, nprops = 0, nkv = 0;
+        for (const q of this.queues) { nrec += q.recs.length; ntext += q.text.length; nprops += q.props.length; nkv += q.kv.length; }
+        if (nrec === 0) return;
+        const ops = new Uint8Array(32 * nrec), dv = new DataView(ops.buffer);
+        const text = new Uint16Array(Math.max(ntext, 1));
+        const props = new Uint8Array(8 * Math.max(nprops, 1)), pv = new DataView(props.buffer);
+        const kv = new Uint8Array(4 * Math.max(nkv, 1)), kvv = new DataView(kv.buffer);
+        const opOff = new BigInt64Array(this.ndocs + 1), textOff = new BigInt64Array(this.ndocs + 1);
+        const propsOff = new BigInt64Array(this.ndocs + 1), kvOff = new BigInt64Array(this.ndocs + 1);
+        let ro = 0, to = 0, po = 0, ko = 0;
+        this.queues.forEach((q, d) => {
+            opOff[d] = BigInt(ro); textOff[d] = BigInt(to); propsOff[d] = BigInt(po); kvOff[d] = BigInt(ko);
+            for (const r of q.recs) {
+                const b = 32 * ro++;
+                dv.setUint8(b, r.kind); dv.setUint8(b + 1, r.seg_kind); dv.setUint16(b + 2, r.client, true);
+                dv.setInt32(b + 4, r.seq, true); dv.setInt32(b + 8, r.ref_seq, true); dv.setInt32(b + 12, r.min_seq, true);
+                dv.setInt32(b + 16, r.pos1, true); dv.setInt32(b + 20, r.pos2, true); dv.setUint32(b + 24, r.text_off, true);
+                dv.setUint16(b + 28, r.text_len, true); dv.setUint16(b + 30, r.props, true);
+            }
+            text.set(q.text, to); to += q.text.length;
+            for (const [off, n, comb] of q.props) {
+                pv.setUint32(8 * po, off, true); pv.setUint16(8 * po + 4, n, true); pv.setUint8(8 * po + 6, comb); po++;
+            }
+            for (const [k, v] of q.kv) { kvv.setUint16(4 * ko, k, true); kvv.setUint16(4 * ko + 2, v, true); ko++; }
+            q.recs = []; q.text = []; q.props = []; q.kv = [];
+        });
+        opOff[this.ndocs] = BigInt(ro); textOff[this.ndocs] = BigInt(to);
+        propsOff[this.ndocs] = BigInt(po); kvOff[this.ndocs] = BigInt(ko);
+        addon.submit(this.h, ops, opOff, text, textOff, props, propsOff, kv, kvOff);
+        addon.run(this.h);
+        addon.sync(this.h);
+    }
+
+    checkDoc(doc) {
+        const [err, errOp] = addon.errors(this.h);
+        if (err[doc] !== 0) throw new Error(`document ${doc}: ${ERRORS[err[doc]] || err[doc]} at event ${errOp[doc]}`);
+    }
+
+    digests() { this.flush(); return addon.digests(this.h); }
+}
+
+/* one replica: the reference Client's surface (client.ts:43) */
+class GpuClient {
+    constructor(engine, doc) { this.engine = engine; this.doc = doc; }
+
+    get longClientId() { return this.engine.localNames[this.doc]; }
+
+    getCurrentSeq() { return this.engine.currentSeq[this.doc]; }
+
+    /* Client.applyMsg (client.ts:797-819): group ops become GROUPED member records (mt_oplog.h) */
+    applyMsg(msg) {
+        const e = this.engine;
+        const base = { client: e.longIndex(msg.clientId), seq: msg.sequenceNumber,
+            ref_seq: msg.referenceSequenceNumber, min_seq: msg.minimumSequenceNumber };
+        if (msg.type !== "op") {
+            e.enqueue(this.doc, OP.NOOP, base);
+        } else {
+            const op = msg.contents;
+            const members = op.type === OP.GROUP ? op.ops : [op];
+            members.forEach((m, i) => {
+                const flag = i < members.length - 1 ? OPF_GROUPED : 0;
+                if (m.type === OP.INSERT) e.enqueue(this.doc, OP.INSERT | flag, { ...base, pos1: m.pos1 }, m.seg);
+                else if (m.type === OP.REMOVE) e.enqueue(this.doc, OP.REMOVE | flag, { ...base, pos1: m.pos1, pos2: m.pos2 });
+                else if (m.type === OP.ANNOTATE) {
+                    e.enqueue(this.doc, OP.ANNOTATE | flag, { ...base, pos1: m.pos1, pos2: m.pos2 }, m);
+                } else throw new Error(`op type ${m.type} unsupported`);
+            });
+        }
+        e.currentSeq[this.doc] = msg.sequenceNumber;
+    }
+
+    /* local edits (client.ts:164-211): return the op to submit, as the reference does */
+    insertTextLocal(pos, text, props) {
+        if (text.length === 0) return undefined;
+        const seg = props ? { text, props } : text;
+        this.engine.enqueue(this.doc, OP.INSERT | OPF_LOCAL, { pos1: pos }, seg);
+        return { type: OP.INSERT, pos1: pos, seg };
+    }
+
+    insertMarkerLocal(pos, refType, props) {
+        const seg = { marker: { refType } };
+        if (props) seg.props = props;
+        this.engine.enqueue(this.doc, OP.INSERT | OPF_LOCAL, { pos1: pos }, seg);
+        return { type: OP.INSERT, pos1: pos, seg };
+    }
+
+    removeRangeLocal(start, end) {
+        this.engine.enqueue(this.doc, OP.REMOVE | OPF_LOCAL, { pos1: start, pos2: end });
+        return { type: OP.REMOVE, pos1: start, pos2: end };
+    }
+
+    annotateRangeLocal(start, end, props, combiningOp) {
+        const op = { type: OP.ANNOTATE, pos1: start, pos2: end, props };
+        if (combiningOp) op.combiningOp = combiningOp;
+        this.engine.enqueue(this.doc, OP.ANNOTATE | OPF_LOCAL, { pos1: start, pos2: end }, op);
+        return op;
+    }
+
+    /* reads flush the queued events first */
+    read() { this.engine.flush(); this.engine.checkDoc(this.doc); return this.engine.h; }
+
+    getLength() { return addon.getLength(this.read(), this.doc, 0, -1); }
+
+    getText() { return addon.getText(this.read(), this.doc, 0, -1); }
+
+    /* MergeTree.getLength / getText under (refSeq, clientId) (mergeTree.ts:1610, textSegment.ts:154) */
+    getLengthAt(refSeq, longClientId) { return addon.getLength(this.read(), this.doc, refSeq, this.engine.longIndex(longClientId)); }
+
+    getTextAt(refSeq, longClientId) { return addon.getText(this.read(), this.doc, refSeq, this.engine.longIndex(longClientId)); }
+
+    /* Client.getContainingSegment (client.ts:1006-1008): {segment: handle | undefined, offset} */
+    getContainingSegment(pos) {
+        const r = addon.getContainingSegment(this.read(), this.doc, pos, 0, -1);
+        return r === undefined ? { segment: undefined, offset: undefined } : { segment: r, offset: r.offset };
+    }
+
+    /* Client.getPosition (client.ts:291) of a handle from getContainingSegment */
+    getPosition(segment) { return addon.getPosition(this.read(), this.doc, segment.rid, segment.gen, 0, -1); }
+}
+
+module.exports = { ReplayEngine, GpuClient, Interner, addon, OP, DEFAULT_CAPS };

@@ -1,0 +1,324 @@
+/*
+ * mt_napi.cc — the Node-API addon over the engine's C ABI (include/mt_engine.h).
+ *
+ * The reference's hot path is the TypeScript module @fluidframework/merge-tree; its callers
+ * (SharedSegmentSequence, sequence.ts:579-616; SharedMatrix, matrix.ts:568-578) would reach the
+ * MI355X engine through this addon and the JS facade next to it (../js/mergetree_gpu.js), which
+ * keeps the Client surface (applyMsg, the *Local edits, getLength, getText,
+ * getContainingSegment, getPosition). The addon is a thin, synchronous marshalling layer: typed
+ * arrays in, numbers / strings / typed arrays out, one engine handle per batch of documents (an
+ * external with a finalizer). Engine status codes become thrown JS errors, as the reference throws
+ * synchronously (client.ts:462-465, mergeTree.ts:2243-2249).
+ *
+ * Build: g++ -shared -fPIC against the vendored Node-API headers (include/, NAPI 8, node 12),
+ * linked to libmtreplay.so with an $ORIGIN rpath (native.build_napi). napi_* symbols resolve from
+ * the node binary at load time.
+ */
+#define NAPI_VERSION 8
+#include <node_api.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mt_engine.h"
+
+#define NAPI_OK(call)                                                     \
+    do {                                                                  \
+        if ((call) != napi_ok) {                                          \
+            napi_throw_error(env, nullptr, "N-API call failed: " #call); \
+            return nullptr;                                               \
+        }                                                                 \
+    } while (0)
+
+static napi_value throw_status(napi_env env, mt_engine* e, int32_t rc, const char* what) {
+    std::string msg = std::string(what) + " failed: status " + std::to_string(rc);
+    if (e) msg += std::string(": ") + mt_engine_last_error(e);
+    napi_throw_error(env, nullptr, msg.c_str());
+    return nullptr;
+}
+
+static void finalize_engine(napi_env, void* data, void*) { mt_engine_destroy((mt_engine*)data); }
+
+static bool get_args(napi_env env, napi_callback_info info, size_t want, napi_value* argv) {
+    size_t argc = want;
+    if (napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr) != napi_ok || argc < want) {
+        napi_throw_type_error(env, nullptr, "missing arguments");
+        return false;
+    }
+    return true;
+}
+
+static mt_engine* engine_of(napi_env env, napi_value v) {
+    void* p = nullptr;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+        napi_throw_type_error(env, nullptr, "not an engine handle");
+        return nullptr;
+    }
+    return (mt_engine*)p;
+}
+
+static bool i32_of(napi_env env, napi_value v, int32_t* out) {
+    if (napi_get_value_int32(env, v, out) != napi_ok) {
+        napi_throw_type_error(env, nullptr, "expected a number");
+        return false;
+    }
+    return true;
+}
+static bool i64_of(napi_env env, napi_value v, int64_t* out) {
+    if (napi_get_value_int64(env, v, out) != napi_ok) {
+        napi_throw_type_error(env, nullptr, "expected a number");
+        return false;
+    }
+    return true;
+}
+
+/* any typed array: its bytes and element count */
+static bool view_of(napi_env env, napi_value v, void** data, size_t* len, napi_typedarray_type want) {
+    napi_typedarray_type t;
+    napi_value ab;
+    size_t off;
+    if (napi_get_typedarray_info(env, v, &t, len, data, &ab, &off) != napi_ok || t != want) {
+        napi_throw_type_error(env, nullptr, "unexpected typed array type");
+        return false;
+    }
+    return true;
+}
+
+static napi_value num(napi_env env, double x) {
+    napi_value v;
+    napi_create_double(env, x, &v);
+    return v;
+}
+
+/* create(device, ndocs, {ncap, hcap, acap, mcap, gcap, ccap}) -> handle */
+static napi_value js_create(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    int32_t device;
+    int64_t ndocs;
+    if (!i32_of(env, argv[0], &device) || !i64_of(env, argv[1], &ndocs)) return nullptr;
+    mt_caps caps;
+    const char* names[6] = {"ncap", "hcap", "acap", "mcap", "gcap", "ccap"};
+    int32_t* fields[6] = {&caps.ncap, &caps.hcap, &caps.acap, &caps.mcap, &caps.gcap, &caps.ccap};
+    for (int i = 0; i < 6; i++) {
+        napi_value f;
+        NAPI_OK(napi_get_named_property(env, argv[2], names[i], &f));
+        if (!i32_of(env, f, fields[i])) return nullptr;
+    }
+    mt_engine* e = nullptr;
+    int32_t rc = mt_engine_create(device, ndocs, &caps, &e);
+    if (rc) return throw_status(env, nullptr, rc, "mt_engine_create");
+    napi_value h;
+    NAPI_OK(napi_create_external(env, e, finalize_engine, nullptr, &h));
+    return h;
+}
+
+/* startCollab(h, Int32Array localLongIds, minSeq, curSeq) */
+static napi_value js_start_collab(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    void* ids;
+    size_t n;
+    int32_t mn, cur;
+    if (!e || !view_of(env, argv[1], &ids, &n, napi_int32_array) || !i32_of(env, argv[2], &mn) ||
+        !i32_of(env, argv[3], &cur))
+        return nullptr;
+    if ((int64_t)n != mt_engine_ndocs(e)) return throw_status(env, e, MT_E_ARG, "startCollab (one id per doc)");
+    int32_t rc = mt_engine_start_collab(e, (const int32_t*)ids, mn, cur);
+    if (rc) return throw_status(env, e, rc, "mt_engine_start_collab");
+    return nullptr;
+}
+
+/* submit(h, Uint8Array ops, BigInt64Array opOff, Uint16Array text, BigInt64Array textOff,
+ *        Uint8Array props, BigInt64Array propsOff, Uint8Array kv, BigInt64Array kvOff) */
+static napi_value js_submit(napi_env env, napi_callback_info info) {
+    napi_value argv[9];
+    if (!get_args(env, info, 9, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    void *ops, *op_off, *text, *text_off, *props, *props_off, *kv, *kv_off;
+    size_t nops_b, noo, ntext, nto, nprops_b, npo, nkv_b, nko;
+    if (!view_of(env, argv[1], &ops, &nops_b, napi_uint8_array) ||
+        !view_of(env, argv[2], &op_off, &noo, napi_bigint64_array) ||
+        !view_of(env, argv[3], &text, &ntext, napi_uint16_array) ||
+        !view_of(env, argv[4], &text_off, &nto, napi_bigint64_array) ||
+        !view_of(env, argv[5], &props, &nprops_b, napi_uint8_array) ||
+        !view_of(env, argv[6], &props_off, &npo, napi_bigint64_array) ||
+        !view_of(env, argv[7], &kv, &nkv_b, napi_uint8_array) ||
+        !view_of(env, argv[8], &kv_off, &nko, napi_bigint64_array))
+        return nullptr;
+    int64_t nd = mt_engine_ndocs(e);
+    if ((int64_t)noo != nd + 1 || (int64_t)nto < nd || (int64_t)npo < nd || (int64_t)nko < nd ||
+        nops_b % sizeof(mt_op_rec) || nprops_b % sizeof(mt_props_rec) || nkv_b % sizeof(mt_kv) ||
+        ((const int64_t*)op_off)[nd] * (int64_t)sizeof(mt_op_rec) > (int64_t)nops_b)
+        return throw_status(env, e, MT_E_ARG, "submit (array shapes)");
+    int32_t rc = mt_engine_submit(e, (const mt_op_rec*)ops, (const int64_t*)op_off, (const uint16_t*)text,
+                                  (int64_t)ntext, (const int64_t*)text_off, (const mt_props_rec*)props,
+                                  (int64_t)(nprops_b / sizeof(mt_props_rec)), (const int64_t*)props_off,
+                                  (const mt_kv*)kv, (int64_t)(nkv_b / sizeof(mt_kv)), (const int64_t*)kv_off);
+    if (rc) return throw_status(env, e, rc, "mt_engine_submit");
+    return nullptr;
+}
+
+#define SIMPLE(name, call)                                            \
+    static napi_value name(napi_env env, napi_callback_info info) {   \
+        napi_value argv[1];                                           \
+        if (!get_args(env, info, 1, argv)) return nullptr;            \
+        mt_engine* e = engine_of(env, argv[0]);                       \
+        if (!e) return nullptr;                                       \
+        int32_t rc = call(e);                                         \
+        if (rc) return throw_status(env, e, rc, #call);               \
+        return nullptr;                                               \
+    }
+SIMPLE(js_run, mt_engine_run)
+SIMPLE(js_sync, mt_engine_sync)
+SIMPLE(js_reset, mt_engine_reset)
+
+/* errors(h) -> [Int32Array err, Int32Array errOp] */
+static napi_value js_errors(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    int64_t nd = mt_engine_ndocs(e);
+    napi_value out, ab[2], ta[2];
+    void* p[2];
+    for (int i = 0; i < 2; i++) {
+        NAPI_OK(napi_create_arraybuffer(env, 4 * nd, &p[i], &ab[i]));
+        NAPI_OK(napi_create_typedarray(env, napi_int32_array, nd, ab[i], 0, &ta[i]));
+    }
+    int32_t rc = mt_engine_errors(e, (int32_t*)p[0], (int32_t*)p[1]);
+    if (rc) return throw_status(env, e, rc, "mt_engine_errors");
+    NAPI_OK(napi_create_array_with_length(env, 2, &out));
+    NAPI_OK(napi_set_element(env, out, 0, ta[0]));
+    NAPI_OK(napi_set_element(env, out, 1, ta[1]));
+    return out;
+}
+
+/* digests(h) -> BigUint64Array */
+static napi_value js_digests(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    int64_t nd = mt_engine_ndocs(e);
+    napi_value ab, ta;
+    void* p;
+    NAPI_OK(napi_create_arraybuffer(env, 8 * nd, &p, &ab));
+    NAPI_OK(napi_create_typedarray(env, napi_biguint64_array, nd, ab, 0, &ta));
+    int32_t rc = mt_engine_digests(e, (uint64_t*)p);
+    if (rc) return throw_status(env, e, rc, "mt_engine_digests");
+    return ta;
+}
+
+/* getLength(h, doc, refSeq, longClient) -> number (longClient < 0: Client.getLength) */
+static napi_value js_get_length(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t ref, cl, out = 0;
+    if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &ref) || !i32_of(env, argv[3], &cl)) return nullptr;
+    int32_t rc = mt_engine_get_length(e, doc, ref, cl, &out);
+    if (rc) return throw_status(env, e, rc, "mt_engine_get_length");
+    return num(env, out);
+}
+
+/* getText(h, doc, refSeq, longClient) -> string */
+static napi_value js_get_text(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t ref, cl;
+    if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &ref) || !i32_of(env, argv[3], &cl)) return nullptr;
+    int64_t n = mt_engine_get_text(e, doc, ref, cl, nullptr, 0);
+    if (n < 0) return throw_status(env, e, (int32_t)-n, "mt_engine_get_text");
+    std::vector<uint16_t> buf((size_t)n + 1);
+    int64_t m = mt_engine_get_text(e, doc, ref, cl, buf.data(), n);
+    if (m < 0) return throw_status(env, e, (int32_t)-m, "mt_engine_get_text");
+    napi_value s;
+    NAPI_OK(napi_create_string_utf16(env, (const char16_t*)buf.data(), (size_t)n, &s));
+    return s;
+}
+
+/* getContainingSegment(h, doc, pos, refSeq, longClient) -> {rid, gen, offset, length, seq, client} | undefined */
+static napi_value js_get_containing(napi_env env, napi_callback_info info) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t pos, ref, cl;
+    if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &pos) || !i32_of(env, argv[3], &ref) ||
+        !i32_of(env, argv[4], &cl))
+        return nullptr;
+    mt_seg_ref r;
+    int32_t rc = mt_engine_get_containing_segment(e, doc, pos, ref, cl, &r);
+    if (rc) return throw_status(env, e, rc, "mt_engine_get_containing_segment");
+    napi_value out;
+    if (r.rid < 0) {
+        NAPI_OK(napi_get_undefined(env, &out));
+        return out;
+    }
+    NAPI_OK(napi_create_object(env, &out));
+    const char* names[6] = {"rid", "gen", "offset", "length", "seq", "client"};
+    int32_t vals[6] = {r.rid, r.gen, r.offset, r.length, r.seq, r.client};
+    for (int i = 0; i < 6; i++) NAPI_OK(napi_set_named_property(env, out, names[i], num(env, vals[i])));
+    return out;
+}
+
+/* getPosition(h, doc, rid, gen, refSeq, longClient) -> number */
+static napi_value js_get_position(napi_env env, napi_callback_info info) {
+    napi_value argv[6];
+    if (!get_args(env, info, 6, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t rid, gen, ref, cl, out = 0;
+    if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &rid) || !i32_of(env, argv[3], &gen) ||
+        !i32_of(env, argv[4], &ref) || !i32_of(env, argv[5], &cl))
+        return nullptr;
+    int32_t rc = mt_engine_get_position(e, doc, rid, gen, ref, cl, &out);
+    if (rc) return throw_status(env, e, rc, "mt_engine_get_position (stale segment handle?)");
+    return num(env, out);
+}
+
+static napi_value js_ndocs(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    return num(env, (double)mt_engine_ndocs(e));
+}
+
+static napi_value js_last_run_ms(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    return num(env, mt_engine_last_run_ms(e));
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+    struct {
+        const char* name;
+        napi_callback cb;
+    } fns[] = {{"create", js_create},       {"startCollab", js_start_collab}, {"submit", js_submit},
+               {"run", js_run},             {"sync", js_sync},                {"reset", js_reset},
+               {"errors", js_errors},       {"digests", js_digests},          {"getLength", js_get_length},
+               {"getText", js_get_text},    {"getContainingSegment", js_get_containing},
+               {"getPosition", js_get_position}, {"ndocs", js_ndocs},        {"lastRunMs", js_last_run_ms}};
+    for (auto& f : fns) {
+        napi_value fn;
+        NAPI_OK(napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn));
+        NAPI_OK(napi_set_named_property(env, exports, f.name, fn));
+    }
+    napi_value sz;
+    NAPI_OK(napi_create_int32(env, (int32_t)sizeof(mt_op_rec), &sz));
+    NAPI_OK(napi_set_named_property(env, exports, "OP_RECORD_BYTES", sz));
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

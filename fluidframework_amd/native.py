@@ -63,7 +63,23 @@ def build_replay(force: bool = False) -> str:
     return out
 
 
+def build_napi(force: bool = False) -> str:
+    """The Node-API addon (napi/mt_napi.cc, vendored Node-API headers) over libmtreplay.so: what a
+    JavaScript host (the reference's callers) loads; napi_* symbols resolve from node at load."""
+    out = lib_path("mt_napi.node")
+    napi = os.path.join(PKG, "napi")
+    srcs = [os.path.join(napi, "mt_napi.cc"), os.path.join(ROOT, "include", "mt_engine.h"),
+            os.path.join(ROOT, "include", "mt_oplog.h"), lib_path("libmtreplay.so")]
+    if force or _stale(out, srcs):
+        os.makedirs(BUILD, exist_ok=True)
+        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-DNODE_GYP_MODULE_NAME=mt_napi",
+                        "-I", os.path.join(napi, "include"), "-o", out, srcs[0], "-L", BUILD, "-l:libmtreplay.so",
+                        "-Wl,-rpath,$ORIGIN"], check=True)
+    return out
+
+
 def build_all() -> None:
     build_gen()
     build_core_host()
     build_replay()
+    build_napi()

@@ -1,0 +1,75 @@
+"""The Node-API addon (fluidframework_amd/napi/mt_napi.cc -> build/mt_napi.node) and its JavaScript
+facade (fluidframework_amd/js/mergetree_gpu.js), under node 12.
+
+CPU tier: node loads the addon (and through it libmtreplay.so), which exports the engine's entry
+points; the facade loads; creating an engine without a GPU fails loudly (no CPU fallback).
+GPU tier: known-answer scenarios of the reference's specs driven from JavaScript (tests/napi_kat.js)
+through facade -> addon -> HIP engine, with the facade's group ops, local edits + acks and segment
+queries.
+"""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from fluidframework_amd import native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
+
+EXPORTS = ["create", "startCollab", "submit", "run", "sync", "reset", "errors", "digests", "getLength", "getText",
+           "getContainingSegment", "getPosition", "ndocs", "lastRunMs"]
+
+
+def _node(script: str) -> str:
+    r = subprocess.run([NODE, "-e", script], capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.strip()
+
+
+def test_addon_loads_and_exports_entry_points():
+    addon = native.build_napi()
+    out = json.loads(_node(f"const a = require({json.dumps(addon)}); "
+                           "console.log(JSON.stringify({keys: Object.keys(a), rec: a.OP_RECORD_BYTES}))"))
+    assert set(EXPORTS) <= set(out["keys"])
+    assert out["rec"] == 32
+
+
+def test_facade_loads():
+    native.build_napi()
+    out = _node("const f = require('./fluidframework_amd/js/mergetree_gpu.js'); "
+                "console.log([typeof f.ReplayEngine, typeof f.GpuClient, Object.keys(f.OP).join()].join(' '))")
+    assert out == "function function INSERT,REMOVE,ANNOTATE,GROUP,NOOP"
+
+
+def test_create_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    native.build_napi()
+    out = _node("const f = require('./fluidframework_amd/js/mergetree_gpu.js'); "
+                "try { new f.ReplayEngine(2); console.log('created'); } catch (e) { console.log(e.message); }")
+    assert "mt_engine_create failed" in out
+
+
+@pytest.mark.gpu
+def test_known_answers_through_node():
+    native.build_napi()
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "napi_kat.js")], capture_output=True, text=True,
+                       cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    # client.applyMsg.spec.ts:88-98: the local insert is unacked (-1) until its message (seq 17)
+    assert out["insertBeforeAck"] == "abchello world"
+    assert out["insertSeqBeforeAck"] == -1 and out["insertSeqAfterAck"] == 17
+    assert out["positionOfSecond"] == 3
+    # client.applyMsg.spec.ts:100-110
+    assert out["removeBeforeAck"] == "ello world" and out["removeAfterAck"] == "ello world"
+    # concurrent inserts around a locally deleted segment (oracle-pinned answer)
+    assert out["intersecting"] == "bc"
+    # a remote replaceRange group (sequence.ts:455-469): insert "!" at 11, remove [5, 11)
+    assert out["groupReplace"] == "hello!" and out["groupLength"] == 6
+    assert len(out["digests"]) == 4
