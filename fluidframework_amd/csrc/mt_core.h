@@ -155,7 +155,7 @@ enum : uint8_t { XF_STABLE = 1, XF_W = 2 };
 
 /* Hot per-document state with compile-time capacities: everything the per-op scans and the
  * tree skeleton touch. */
-template <int N_, int C_ = 64, bool TILED_ = false>
+template <int N_, int C_ = 256, bool TILED_ = false>
 struct HotT {
     static constexpr int N = N_;     /* B-tree nodes */
     static constexpr int S = N_ * 8; /* row slots (8 per leaf node) */
@@ -205,7 +205,7 @@ typedef HotT<192> HotSmall;
 typedef HotT<640> HotMat; /* config 5: PermutationVector replicas peak at ~540 nodes */
 typedef HotT<2048> HotMid;
 typedef HotT<16384> HotBig;
-typedef HotT<(1 << 18), 64, true> HotHuge; /* config 4: tiled position index, 32-bit ids (1M-op docs: ~112k nodes) */
+typedef HotT<(1 << 18), 256, true> HotHuge; /* config 4: tiled position index, 32-bit ids (1M-op docs: ~112k nodes) */
 
 struct alignas(16) I4 {
     int32_t x[4];

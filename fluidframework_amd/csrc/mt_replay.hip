@@ -415,7 +415,7 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     *out = nullptr;
     Caps k = {caps->acap, caps->mcap, caps->gcap};
     int prof = profile_for(caps->ncap);
-    if (!caps_valid(k) || prof < 0 || caps->ccap > 64) return MT_E_ARG;
+    if (!caps_valid(k) || prof < 0 || caps->ccap > 254) return MT_E_ARG; /* short ids are bytes; 0xFF = LocalClientId */
     mt_engine* e = new mt_engine();
     e->device = device;
     e->ndocs = ndocs;

@@ -84,16 +84,16 @@ def default_caps(ops_per_doc: int, config: int = 3) -> dict:
     if config == 4:
         # tiled large-document profile (HotHuge: 262,144 nodes, 32-bit ids); a 1M-op config-4
         # document peaks at ~112k nodes, 422k rows and 3.2M text units
-        return dict(ncap=1 << 18, hcap=1 << 12, acap=1 << 22, mcap=4096, gcap=1024, ccap=64)
+        return dict(ncap=1 << 18, hcap=1 << 12, acap=1 << 22, mcap=4096, gcap=1024, ccap=254)
     if config == 5 and ops_per_doc <= 5_000:
         # PermutationVector replicas (HotMat: 640 nodes / 5120 slots; peak ~540 nodes at 4,096)
-        return dict(ncap=640, hcap=1024, acap=1 << 4, mcap=1024, gcap=1024, ccap=64)
+        return dict(ncap=640, hcap=1024, acap=1 << 4, mcap=1024, gcap=1024, ccap=254)
     if config == 5:
-        return dict(ncap=2048, hcap=4096, acap=1 << 4, mcap=2048, gcap=1024, ccap=64)
+        return dict(ncap=2048, hcap=4096, acap=1 << 4, mcap=2048, gcap=1024, ccap=254)
     if ops_per_doc <= 20_000:
         # LDS-resident profile (HotSmall: 192 nodes / 1536 slots)
-        return dict(ncap=192, hcap=256, acap=1 << 16, mcap=1024, gcap=1024, ccap=64)
-    return dict(ncap=16384, hcap=32768, acap=1 << 22, mcap=4096, gcap=1024, ccap=64)
+        return dict(ncap=192, hcap=256, acap=1 << 16, mcap=1024, gcap=1024, ccap=254)
+    return dict(ncap=16384, hcap=32768, acap=1 << 22, mcap=4096, gcap=1024, ccap=254)
 
 
 class Engine:

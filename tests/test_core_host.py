@@ -105,3 +105,42 @@ def test_containing_segment_and_position_match_oracle(caps):
                 want = c.containing(int(pos), ref, k)
                 got = st.containing(d, int(pos), ref, -1 if k is None else k)
                 assert got == want, (d, ref, k, pos, got, want)
+
+
+def many_clients_batch(nclients=250, nops=3000, ndocs=2, seed=3):
+    """Observer replicas of documents edited by `nclients` distinct clients (every session of a real
+    document gets a new client id): sequential inserts / removes / annotates, refSeq = MSN = seq - 1."""
+    from fluidframework_amd import oplog as ol
+    it = gen.generator_interner()
+    logs = []
+    rng = np.random.default_rng(seed)
+    for d in range(ndocs):
+        lg = ol.DocLog(it, local_long_id=0)
+        n = 0
+        for seq in range(1, nops + 1):
+            cl = 1 + (seq * 7 + d) % nclients if seq > nclients else seq  # every client shows up
+            r = rng.integers(0, 10)
+            if n == 0 or r < 6:
+                t = "".join(chr(65 + x) for x in rng.integers(0, 26, rng.integers(1, 6)))
+                lg.add(0, client=cl, seq=seq, ref_seq=seq - 1, min_seq=seq - 1, pos1=int(rng.integers(0, n + 1)), text=t)
+                n += len(t)
+            elif r < 9:
+                a = int(rng.integers(0, n))
+                b = min(n, a + int(rng.integers(1, 8)))
+                lg.add(1, client=cl, seq=seq, ref_seq=seq - 1, min_seq=seq - 1, pos1=a, pos2=b)
+                n -= b - a
+            else:
+                a = int(rng.integers(0, n))
+                lg.add(2, client=cl, seq=seq, ref_seq=seq - 1, min_seq=seq - 1, pos1=a, pos2=min(n, a + 5),
+                       props={"b": int(rng.integers(0, 4))})
+        logs.append(lg)
+    return ol.Batch.from_logs(logs)
+
+
+def test_250_client_ids_match_oracle():
+    b = many_clients_batch()
+    _, odig, oerr = oc.replay_batch(b, threads=4)
+    assert (oerr == 0).all()
+    for caps in (CAPS, TILED):
+        hdig, herr, _ = core_host.replay_batch(b, caps)
+        assert (herr == 0).all() and (hdig == odig).all()

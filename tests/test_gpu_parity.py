@@ -205,3 +205,10 @@ def Engine_(b, caps):
     eng.start_collab(b.local_long_id)
     eng.replay(b)
     return eng
+
+
+def test_250_client_ids():
+    """Documents edited by 250 distinct client ids (short ids are bytes: up to 254 per document)."""
+    from test_core_host import many_clients_batch
+    b = many_clients_batch()
+    _check_batch(b, 3000, ndump=2, every=True)
