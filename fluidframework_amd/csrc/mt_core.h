@@ -53,7 +53,7 @@ enum : int32_t {
     E_OK = 0,
     E_INSERT_FAILED = 1, /* mergeTree.ts:2243-2249 */
     E_ASSERT = 2,
-    E_INVALID_RANGE = 3, /* client.ts:486-548 (local op rejected) */
+    E_INVALID_RANGE = 3, /* reserved: a local op getValidOpRange rejects (client.ts:486-548) is a no-op */
     E_UNSUPPORTED = 4,
     E_CAPACITY = 5,
 };
@@ -89,7 +89,8 @@ struct DocHdr {
     int32_t nrows, seqOps, nfreeRid, gcEpoch; /* rows in the table; sequenced msgs applied */
     int32_t localLen;      /* root.cachedLength: Client.getLength() (client.ts:1051) */
     int32_t heapTop;       /* maxSeq of the heap's root (valid when heapN > 0) */
-    int32_t _r1, _r2;
+    int32_t loadPos;       /* snapshot load: the next position of the open loadBody batch (mt_oplog.h) */
+    int32_t _r2;
     int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
 };
@@ -98,7 +99,7 @@ struct DocHdr {
     X(root) X(nleaf) X(freeHead) X(nfree) X(currentSeq) X(minSeq) X(localSeq) X(collaborating)   \
     X(localShort) X(localLong) X(nclients) X(nextSid) X(heapN) X(memN) X(gqHead) X(gqN)          \
     X(arenaTop) X(arenaSide) X(err) X(errOp) X(nkeys) X(opsDone) X(hwSlots) X(hwHeap) X(nrows)   \
-    X(seqOps) X(nfreeRid) X(gcEpoch) X(localLen) X(heapTop)
+    X(seqOps) X(nfreeRid) X(gcEpoch) X(localLen) X(heapTop) X(loadPos)
 
 /* Cold per-row data, indexed by a row id that does not move when the row's slot moves. */
 struct ColdRow {
@@ -300,11 +301,12 @@ struct Replica {
     int32_t* wcp;
     int32_t* wvs;
     uint8_t* wlx;
+    int64_t cur; /* index of the record being applied in the current Pools (snapshot reload reads ahead) */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
         : d(doc), z(*doc.t), w(wave), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
           nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen), cdel(nullptr), wcp(nullptr), wvs(nullptr),
-          wlx(nullptr) {
+          wlx(nullptr), cur(0) {
         if constexpr (TILED) {
             cdel = z.tl.sdel;
             wcp = z.tl.swcp;
@@ -439,7 +441,7 @@ struct Replica {
         h.sumW = 0;
         h.localLen = 0;
         h.heapTop = 0;
-        h._r1 = h._r2 = 0;
+        h.loadPos = h._r2 = 0;
         for (int32_t b = 0; b < HT::C; b += W::N) {
             int32_t i = b + w.lane();
             if (i < HT::C) z.l2s[i] = 0xFF;
@@ -472,7 +474,7 @@ struct Replica {
     }
     /* startOrUpdateCollaboration (client.ts:1053-1073) + startCollaboration (mergeTree.ts:1287) */
     MT_HD void start_collab(int32_t longId, int32_t minSeq, int32_t curSeq) {
-        if (h.localLong >= 0) return;
+        if (h.localLong >= 0 || longId < 0) return; /* longId < 0: stays detached (a snapshot load follows) */
         h.localLong = longId;
         h.localShort = get_or_add_short(longId);
         h.minSeq = minSeq;
@@ -2209,13 +2211,21 @@ struct Replica {
             return leaf_insert_slot(n, c);
         }
     }
-    MT_HD void insert_segments(const mt_op_rec& op, const Pools& p, int32_t refSeq, int32_t client, int32_t seq) {
+    /* a segment record's length (mt_oplog.h): text_len, or pos2 for snapshot-load records */
+    MT_HD static int32_t seg_len(const mt_op_rec& op) {
+        if (op.seg_kind == MT_SEG_MARKER) return 1;
+        return (op.kind & MT_OP_KIND_MASK) >= MT_OP_RELOAD ? op.pos2 : op.text_len;
+    }
+    /* insertSegments (mergeTree.ts:2001-2040) of one segment; preRseq > 0: the segment arrives
+     * already removed (a loaded segment's merge info, snapshotLoader.ts:101-106) */
+    MT_HD void insert_segments(const mt_op_rec& op, const Pools& p, int32_t refSeq, int32_t client, int32_t seq,
+                               int32_t preRseq = 0, uint8_t preRcli = 0) {
         int32_t pos = op.pos1;
         bool hasL = seq == UNASSIGNED_SEQ;
         int32_t localSeq = hasL ? ++h.localSeq : 0;
         bool marker = op.seg_kind == MT_SEG_MARKER;
         bool perm = op.seg_kind == MT_SEG_PERM; /* PermutationSegment(length) (permutationvector.ts:47-51) */
-        int32_t L = marker ? 1 : op.text_len;
+        int32_t L = seg_len(op);
         if (L <= 0) ensure_boundary(pos, refSeq, client); /* the split still happens (2004) */
         if (L > 0) {
             int32_t off = 0;
@@ -2245,7 +2255,12 @@ struct Replica {
             z.rleaf[z.rid[s]] = (IX)(s / MAXN);
             h.nrows++;
             h.sumW++;
-            h.localLen += L;
+            if (preRseq > 0) {
+                z.rseq(s) = preRseq;
+                z.rcli(s) = preRcli;
+            } else {
+                h.localLen += L;
+            }
             if (marker) {
                 cold(s).toff = (uint32_t)op.pos2;
             } else if (perm) {
@@ -2577,6 +2592,11 @@ struct Replica {
             nkv = pr.nkv;
             rw = pr.combining == MT_COMBINE_REWRITE;
         }
+        if (kind >= MT_OP_RELOAD && !(op.kind & MT_OPF_LOCAL)) {
+            apply_load(op, p);
+            h.opsDone++;
+            return;
+        }
         if (op.kind & MT_OPF_LOCAL) {
             int32_t client = h.collaborating ? h.localShort : -1;
             int32_t refSeq = h.currentSeq;
@@ -2586,8 +2606,8 @@ struct Replica {
             int32_t start = op.pos1, end = op.pos2;
             bool bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
             if (kind != MT_OP_INSERT && end <= start) bad = true;
-            if (bad) {
-                fail(E_INVALID_RANGE);
+            if (bad) { /* rejected: no effect (the reference logs InvalidOpRange and returns undefined) */
+                h.opsDone++;
                 return;
             }
             if (kind == MT_OP_INSERT) {
@@ -2638,6 +2658,141 @@ struct Replica {
         int32_t slots = h.nleaf * MAXN;
         if (slots > h.hwSlots) h.hwSlots = slots;
     }
+    /* ---- snapshot load (SnapshotLoader, snapshotLoader.ts:86-228; records in mt_oplog.h) ------- */
+    /* the fields of a loaded segment (SnapshotLoader.specToSegment, snapshotLoader.ts:96-126) on an
+     * already placed row s whose text / props the insert path has set */
+    MT_HD int32_t loader_client(uint16_t longId) {
+        return longId == MT_CLIENT_NONCOLLAB ? -1 : get_or_add_short(longId); /* NonCollab: never a real client */
+    }
+    /* reloadFromSegments (mergeTree.ts:1229-1284) of records [cur, cur + n): leaf blocks of 7 rows in
+     * order, then interior levels of 7 blocks, bottom-up (the single block of a level is the root) */
+    MT_HD void reload(const Pools& p, int32_t n) {
+        if (h.collaborating || h.nrows != 0 || h.nleaf != 1 || cur + n > p.nops) {
+            fail(E_ASSERT); /* assert(!collaborating) (1231), on an empty replica, whole header at hand */
+            return;
+        }
+        constexpr int32_t K = MAXN - 1;
+        int32_t leaf = leaf_at(0), prevLeaf = -1;
+        for (int32_t i = 0; i < n; i++) {
+            const mt_op_rec op = p.ops[cur + i];
+            if ((op.kind & MT_OP_KIND_MASK) != MT_OP_RELOAD) {
+                fail(E_ASSERT);
+                return;
+            }
+            int32_t j = i % K;
+            if (j == 0 && i > 0) {
+                prevLeaf = leaf;
+                leaf = alloc_node(0);
+                if (leaf < 0) return;
+                lorder_insert_after(prevLeaf, leaf);
+            }
+            if (!place_loaded(op, p, leaf * MAXN + j)) return;
+            nch[leaf] = (int8_t)(j + 1);
+        }
+        if constexpr (TILED)
+            for (int32_t k = 0; kvalid(k); k = knext(k)) leaf_restat(leaf_at(k));
+        /* interior levels; the previous level's nodes in order go through the (empty) heap arrays */
+        int32_t cnt = 0;
+        for (int32_t k = 0; kvalid(k); k = knext(k)) hrd[cnt++] = (IX)leaf_at(k);
+        int8_t lvl = 1;
+        while (cnt > 1) {
+            int32_t m = (cnt + K - 1) / K;
+            for (int32_t bi = 0; bi < m; bi++) {
+                int32_t nb = alloc_node(lvl);
+                if (nb < 0) return;
+                int32_t c = 0;
+                for (int32_t i = bi * K; i < cnt && c < K; i++, c++) {
+                    int32_t ch = hrd[i];
+                    z.kids[nb * MAXN + c] = (IX)ch;
+                    npar[ch] = (IX)nb;
+                }
+                nch[nb] = (int8_t)c;
+                hrd[bi] = (IX)nb; /* bi <= i: written after its block's children were read */
+            }
+            cnt = m;
+            lvl++;
+        }
+        h.root = hrd[0];
+        npar[h.root] = -1;
+    }
+    /* one loaded segment into slot s (a fresh row): text / marker / permutation, props, merge info */
+    MT_HD bool place_loaded(const mt_op_rec& op, const Pools& p, int32_t s) {
+        bool marker = op.seg_kind == MT_SEG_MARKER, perm = op.seg_kind == MT_SEG_PERM;
+        int32_t L = seg_len(op);
+        if (L <= 0) {
+            fail(E_UNSUPPORTED); /* a snapshot holds no empty segments */
+            return false;
+        }
+        int32_t off = 0;
+        if (!marker && !perm) {
+            off = arena_alloc(L);
+            if (off < 0) return false;
+        }
+        z.rid[s] = (IX)alloc_rid();
+        cold(s).gc = 0;
+        z.len(s) = L;
+        z.seq(s) = op.seq;
+        int32_t cl = loader_client(op.client);
+        z.cli(s) = (uint8_t)(cl < 0 ? LOCAL_CLIENT : cl);
+        z.rseq(s) = NOREM;
+        z.rcli(s) = 0;
+        if (op.ref_seq > 0) { /* removed above the snapshot's MSN */
+            int32_t rc = loader_client((uint16_t)op.min_seq);
+            z.rseq(s) = op.ref_seq;
+            z.rcli(s) = (uint8_t)(rc < 0 ? LOCAL_CLIENT : rc);
+        }
+        z.ng(s) = 0;
+        cold(s).lseq = 0;
+        cold(s).lrseq = 0;
+        cold(s).prw = 0;
+        cold(s).ovl = 0;
+        z.rleaf[z.rid[s]] = (IX)(s / MAXN);
+        int32_t fl = (marker ? RF_MARKER : 0) | (perm ? RF_PERM : 0);
+        if (marker) {
+            cold(s).toff = (uint32_t)op.pos2;
+        } else if (perm) {
+            cold(s).toff = 0;
+        } else {
+            cold(s).toff = (uint32_t)off;
+            int32_t last = arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
+            fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
+        }
+        z.flags(s) = (uint8_t)fl;
+        for (int k = 0; k < NKEYS; k++) {
+            cold(s).pv[k] = 0;
+            cold(s).pk[k] = 0;
+        }
+        if (op.props) {
+            const mt_props_rec& pr = p.props[op.props - 1];
+            add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE, 0, false);
+        }
+        if constexpr (TILED) z.tl.xf[s] = 0;
+        h.nrows++;
+        if (z.rseq(s) == NOREM) h.localLen += L;
+        if constexpr (TILED) row_enter(s);
+        return true;
+    }
+    MT_HD void apply_load(const mt_op_rec& op, const Pools& p) {
+        int32_t kind = op.kind & MT_OP_KIND_MASK;
+        if (kind == MT_OP_RELOAD) {
+            if (h.nrows == 0 && !h.collaborating) reload(p, op.pos1); /* the first of the header's records */
+        } else if (kind == MT_OP_COLLAB) {
+            start_collab(op.client, op.min_seq, op.seq);
+        } else { /* MT_OP_APPEND: loadBody's insertSegments(root.cachedLength, segs, 0, client, seq) */
+            /* a batch of segments (one insertSegments call, blockInsert 2226-2256) starts at the local
+             * length; its later members (GROUPED) go at the previous position + the previous
+             * segment's whole length, removed or not */
+            mt_op_rec ins = op;
+            ins.pos1 = (op.kind & MT_OPF_GROUPED) ? h.loadPos : h.localLen;
+            h.loadPos = ins.pos1 + seg_len(op);
+            int32_t cl = loader_client(op.client);
+            int32_t rc = op.ref_seq > 0 ? loader_client((uint16_t)op.min_seq) : 0;
+            if (h.err) return;
+            insert_segments(ins, p, UNIVERSAL_SEQ, cl, op.seq, op.ref_seq > 0 ? op.ref_seq : 0,
+                            (uint8_t)(rc < 0 ? LOCAL_CLIENT : rc));
+        }
+    }
+
     /* Client.getLength(): the local view's length, kept incrementally like root.cachedLength */
     MT_HD int32_t length_local() const { return h.localLen; }
 
@@ -2827,6 +2982,7 @@ struct Replica {
                 for (int q = 0; q < 8; q++) u[q] = w.bcast(rec[q], (int)k);
                 mt_op_rec op;
                 __builtin_memcpy(&op, u, sizeof(op));
+                cur = b + k;
                 apply(op, p);
                 if (h.err) return;
             }

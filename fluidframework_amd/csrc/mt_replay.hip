@@ -444,14 +444,17 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
         delete e;
         return MT_E_NOMEM;
     }
-    if (hipMemset(e->mem, 0, (size_t)bytes) != hipSuccess) {
-        (void)hipFree(e->mem);
-        delete e;
-        return MT_E_HIP;
-    }
     e->s0.base = e->s1.base = e->s2.base = e->s3.base = e->s4.base = (uint8_t*)e->mem;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
+        mt_engine_destroy(e);
+        return MT_E_HIP;
+    }
+    /* The zero fill goes on the engine's own stream, ahead of k_init. A hipMemset on the null
+     * stream is not ordered with a non-blocking stream: a large store's fill could still be running
+     * when k_init wrote the last documents' headers, and zeroed them after it (round 2: the last
+     * documents of a 3.2 GB tiled store failed at their first events, only in long test runs). */
+    if (hipMemsetAsync(e->mem, 0, (size_t)bytes, e->stream) != hipSuccess) {
         mt_engine_destroy(e);
         return MT_E_HIP;
     }
@@ -523,6 +526,10 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
             int kind = o.kind & MT_OP_KIND_MASK;
             if (kind == MT_OP_INSERT && o.seg_kind == MT_SEG_TEXT &&
                 text_off[d] + (int64_t)o.text_off + o.text_len > text_units)
+                return MT_E_ARG;
+            /* snapshot-load records carry the segment length in pos2 (mt_oplog.h) */
+            if ((kind == MT_OP_RELOAD || kind == MT_OP_APPEND) && o.seg_kind == MT_SEG_TEXT &&
+                (o.pos2 < 0 || text_off[d] + (int64_t)o.text_off + o.pos2 > text_units))
                 return MT_E_ARG;
             if (o.props) {
                 if (props_off[d] + (int64_t)o.props > nprops) return MT_E_ARG;
@@ -789,7 +796,8 @@ int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t g
 /* profiling build only: per-doc phase cycles of the last run (PH_* order in mt_core.h) */
 int32_t mt_engine_profile(mt_engine* e, uint64_t* out) {
     if (!e || !out || !e->prof.p) return MT_E_ARG;
-    HIPCHK(e, hipMemcpy(out, e->prof.p, sizeof(uint64_t) * PH_N * e->ndocs, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpyAsync(out, e->prof.p, sizeof(uint64_t) * PH_N * e->ndocs, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     return MT_OK;
 }
 #endif

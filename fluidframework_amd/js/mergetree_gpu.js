@@ -78,6 +78,7 @@ class ReplayEngine {
 
     /* startOrUpdateCollaboration for every document at once (mt_engine_start_collab) */
     startCollaboration(localNames, minSeq = 0, currentSeq = 0) {
+        this.flush(); // edits queued before collaboration apply as non-collaborating local edits
         const ids = new Int32Array(this.ndocs);
         for (let d = 0; d < this.ndocs; d++) {
             this.localNames[d] = localNames[d];

@@ -9,14 +9,19 @@ with per-document offsets; it is what the HIP replay engine (``libmtreplay.so``)
 from __future__ import annotations
 
 import json
+import struct
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
 
 OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 4
+OP_RELOAD, OP_COLLAB, OP_APPEND = 5, 6, 7  # snapshot load records (mt_oplog.h)
 OPF_LOCAL = 0x80
-SEG_TEXT, SEG_MARKER = 0, 1
+OPF_GROUPED = 0x40
+SEG_TEXT, SEG_MARKER, SEG_PERM = 0, 1, 2
+CLIENT_NONCOLLAB = 0xFFFF
+_SEGMENT_KINDS = (OP_INSERT, OP_RELOAD, OP_APPEND)
 COMBINE_NONE, COMBINE_REWRITE = 0, 1
 VALUE_FALSY = 0x8000
 
@@ -89,6 +94,50 @@ class Interner:
         return json.loads(self.values[i & ~VALUE_FALSY])
 
 
+def concat_records(a, b):
+    """Two record streams (ops, text, props, kv) of one document as one: b's pool references are
+    re-based past a's pools (e.g. a snapshot's load records followed by the ops after it)."""
+    ao, at, ap, akv = a
+    bo, bt, bp, bkv = b
+    bo = bo.copy()
+    bo["text_off"] += np.uint32(len(at))
+    has = bo["props"] != 0
+    bo["props"][has] += np.uint16(len(ap))
+    bp = bp.copy()
+    bp["kv_off"] += np.uint32(len(akv))
+    return (np.concatenate([ao, bo]), np.concatenate([at, bt]), np.concatenate([ap, bp]),
+            np.concatenate([akv, bkv]))
+
+
+def parse_dump(b: bytes):
+    """Decode the canonical dump (include/mt_oplog.h) into (header dict, [segment dicts])."""
+    hdr = struct.unpack_from("<6i", b, 0)
+    off = 24
+    segs = []
+    for _ in range(hdr[4]):
+        kind, flags, nov, ngroups = struct.unpack_from("<4B", b, off)
+        off += 4
+        f = struct.unpack_from("<8i", b, off)
+        off += 32
+        ov = list(struct.unpack_from(f"<{nov}i", b, off))
+        off += 4 * nov
+        nprops, ref_type = struct.unpack_from("<2H", b, off)
+        off += 4
+        props = [struct.unpack_from("<2H", b, off + 4 * k) for k in range(nprops)]
+        off += 4 * nprops
+        text = ""
+        if kind == SEG_TEXT:
+            text = b[off: off + 2 * f[0]].decode("utf-16-le")
+            off += 2 * f[0]
+        segs.append(dict(kind=kind, flags=flags, ngroups=ngroups, len=f[0], seq=f[1], client=f[2],
+                         removedSeq=f[3] if flags & 2 else None, removedClient=f[4], localSeq=f[5],
+                         localRemovedSeq=f[6], leaf=f[7], overlap=ov, props=props, refType=ref_type, text=text))
+    if off != len(b):
+        raise ValueError("trailing bytes after the canonical dump")
+    return dict(currentSeq=hdr[0], minSeq=hdr[1], localSeq=hdr[2], length=hdr[3], nsegs=hdr[4],
+                nleaf=hdr[5]), segs
+
+
 @dataclass
 class DocLog:
     """One replica's event stream plus its text / props pools."""
@@ -118,15 +167,22 @@ class DocLog:
 
     def add(self, kind: int, *, client: int = 0, seq: int = 0, ref_seq: int = 0, min_seq: int = 0,
             pos1: int = 0, pos2: int = 0, text: Optional[str] = None, marker: Optional[int] = None,
-            props: Optional[Dict[str, Any]] = None, combining: int = COMBINE_NONE) -> None:
+            props: Optional[Dict[str, Any]] = None, combining: int = COMBINE_NONE,
+            perm: Optional[int] = None) -> None:
+        """One record; `perm` = the row count of a PermutationSegment insert / loaded segment."""
         seg_kind = SEG_TEXT
         toff = tlen = 0
-        if kind & 7 == OP_INSERT:
-            if marker is not None:
+        if kind & 7 in _SEGMENT_KINDS:
+            if perm is not None:
+                seg_kind = SEG_PERM
+                tlen = perm
+            elif marker is not None:
                 seg_kind = SEG_MARKER
                 pos2 = marker
             else:
                 toff, tlen = self._text(text or "")
+        if kind & 7 in (OP_RELOAD, OP_APPEND) and seg_kind != SEG_MARKER:
+            pos2, tlen = tlen, 0  # load records carry the length in pos2 (mt_oplog.h)
         pidx = self._props(props, combining)
         self.ops.append((kind, seg_kind, client, seq, ref_seq, min_seq, pos1, pos2, toff, tlen, pidx))
 
@@ -169,6 +225,17 @@ class Batch:
             self.props[self.props_off[d]:],
             self.kv[self.kv_off[d]:],
         )
+
+    def doc_arrays(self, d: int):
+        """(ops, text, props, kv) of document d with pools cut to the document's own segment (a pool
+        every document shares is returned whole)."""
+        def pool(arr, off):
+            if np.all(off == off[0]) or off[d + 1] < off[d]:
+                return arr[off[d]:]
+            seg = arr[off[d]: off[d + 1]]
+            return seg if len(seg) else arr[:1]
+        return (self.ops[self.op_off[d]: self.op_off[d + 1]], pool(self.text, self.text_off),
+                pool(self.props, self.props_off), pool(self.kv, self.kv_off))
 
     def subset(self, docs: Sequence[int]) -> "Batch":
         """A batch of the given documents. A pool that is one segment per document (offsets

@@ -1,0 +1,247 @@
+"""Merge-tree snapshots: the v1 summary format <-> the engine.
+
+Emit (SnapshotV1.extractSync + emit, packages/dds/merge-tree/src/snapshotV1.ts:156-234, 82-154):
+the engine's canonical segment dump (mt_engine_dump, include/mt_oplog.h — read back from HBM) is
+walked in document order; unacked segments and segments removed at or below the MSN are elided;
+settled segments are coalesced (canAppend + matchProperties, as the reference's clone/append);
+window segments keep their merge info ({json, seq, client, removedSeq, removedClient}); segments are
+cut into chunks of ~chunkSize characters (getSeqLengthSegs, 59-81) and serialized as the v1 chunk
+JSON (serializeAsMaxSupportedVersion). The result is the ITree of blobs the reference produces.
+
+Load (SnapshotLoader, snapshotLoader.ts:86-228): the header chunk's segments become MT_OP_RELOAD
+records (the engine rebuilds them as reloadFromSegments does, 7 children per block bottom-up,
+mergeTree.ts:1229-1284), then MT_OP_COLLAB (startOrUpdateCollaboration with the header's
+minSeq/currentSeq), then the body chunks' segments as MT_OP_APPEND records (loadBody's
+insertSegments at the end of the local view). The records go through the normal replay path
+(mt_engine_submit / mt_engine_run), so a batch of documents loads and then keeps replaying on the GPU.
+"""
+from __future__ import annotations
+
+import json
+from typing import Any, Dict, List, Optional
+
+from . import oplog as ol
+
+HEADER = "header"           # SnapshotLegacy.header (snapshotlegacy.ts:55)
+BODY = "body"               # SnapshotLegacy.body
+CHUNK_SIZE = 10000          # SnapshotV1.chunkSize (snapshotV1.ts:40)
+TEXT_GRANULARITY = 256      # TextSegmentGranularity (mergeTree.ts:1093)
+UNALLOCATED = -0x80000000   # Handle.unallocated (matrix handletable.ts:11)
+
+
+def _js(v: Any) -> str:
+    """JSON.stringify for the JSON-shaped values of a snapshot."""
+    return json.dumps(v, separators=(",", ":"), ensure_ascii=False)
+
+
+# ---- emit -------------------------------------------------------------------------------------
+def _props(seg, interner: ol.Interner) -> Optional[Dict[str, Any]]:
+    if not seg["flags"] & 1:  # MT_DF_HAS_PROPS: properties !== undefined
+        return None
+    return {interner.key_str(k): interner.value_obj(v) for k, v in seg["props"]}
+
+
+def _json_spec(seg, props):
+    """ISegment.toJSONObject: TextSegment (textSegment.ts:48-54), Marker (mergeTree.ts:690-694),
+    PermutationSegment (permutationvector.ts:77-79)."""
+    if seg["kind"] == ol.SEG_TEXT:
+        return {"text": seg["text"], "props": props} if props is not None else seg["text"]
+    if seg["kind"] == ol.SEG_MARKER:
+        j = {"marker": {"refType": seg["refType"]}}
+        if props is not None:
+            j["props"] = props
+        return j
+    return [seg["len"], UNALLOCATED]
+
+
+def _can_append(a, b) -> bool:
+    if a["kind"] == ol.SEG_PERM or b["kind"] == ol.SEG_PERM:  # PermutationSegment.canAppend: both unallocated
+        return a["kind"] == b["kind"]
+    if a["kind"] != ol.SEG_TEXT or b["kind"] != ol.SEG_TEXT:  # Marker.canAppend is false
+        return False
+    return not a["text"].endswith("\n") and (a["len"] <= TEXT_GRANULARITY or b["len"] <= TEXT_GRANULARITY)
+
+
+def extract_segments(hdr, segs, interner: ol.Interner, long_name) -> List[tuple]:
+    """SnapshotV1.extractSync (snapshotV1.ts:156-234) over a parsed canonical dump: a list of
+    (json spec, length). `long_name(i)` gives the long client id string of long-client index i."""
+    min_seq = hdr["minSeq"]
+    out: List[tuple] = []
+    prev = None
+
+    def push(p):
+        if p is not None:
+            out.append((_json_spec(p, p["_props"]), p["len"]))
+
+    for s in segs:
+        removed = s["removedSeq"] is not None
+        if s["seq"] == -1 or (removed and s["removedSeq"] <= min_seq):
+            continue  # unacked, or removed at/below the MSN (a pending removal, -1, is elided too)
+        props = _props(s, interner)
+        if s["seq"] <= min_seq and not removed:
+            cur = dict(s, _props=props)
+            if prev is None:
+                prev = cur
+            elif _can_append(prev, cur) and prev["_props"] == cur["_props"]:
+                prev = dict(prev, len=prev["len"] + cur["len"],
+                            text=(prev["text"] + cur["text"]) if prev["kind"] == ol.SEG_TEXT else None)
+            else:
+                push(prev)
+                prev = cur
+        else:
+            push(prev)
+            prev = None
+            raw: Dict[str, Any] = {"json": _json_spec(s, props)}
+            if s["seq"] > min_seq:
+                raw["seq"] = s["seq"]
+                raw["client"] = long_name(s["client"])
+            if removed:
+                raw["removedSeq"] = s["removedSeq"]
+                raw["removedClient"] = long_name(s["removedClient"])
+            out.append((raw, s["len"]))
+    push(prev)
+    return out
+
+
+def emit_v1(hdr, segs, interner: ol.Interner, long_name, chunk_size: int = CHUNK_SIZE) -> dict:
+    """SnapshotV1.emit (snapshotV1.ts:82-154): the ITree of a merge-tree snapshot (header blob, then
+    body_<i> blobs), contents serialized like serializeAsMaxSupportedVersion with JSON.stringify."""
+    specs = extract_segments(hdr, segs, interner, long_name)
+    chunks = []
+    start = 0
+    while True:
+        seg_list, length, count = [], 0, 0
+        while length < chunk_size and start + count < len(specs):  # getSeqLengthSegs (59-81)
+            seg_list.append(specs[start + count][0])
+            length += specs[start + count][1]
+            count += 1
+        chunks.append({"version": "1", "segmentCount": count, "length": length, "segments": seg_list,
+                       "startIndex": start})
+        start += count
+        if start >= len(specs):
+            break
+    meta = {"minSequenceNumber": hdr["minSeq"], "sequenceNumber": hdr["currentSeq"],
+            "orderedChunkMetadata": [{"id": HEADER}], "totalLength": sum(c["length"] for c in chunks),
+            "totalSegmentCount": sum(c["segmentCount"] for c in chunks)}
+    body = []
+    for i, c in enumerate(chunks[1:]):
+        cid = f"{BODY}_{i}"
+        meta["orderedChunkMetadata"].append({"id": cid})
+        body.append(_blob(cid, c))
+    # the header is serialized last, so it lists every body chunk id (snapshotV1.ts:111-151)
+    return {"entries": [_blob(HEADER, dict(chunks[0], headerMetadata=meta))] + body, "id": None}
+
+
+def _blob(path: str, chunk: dict) -> dict:
+    return {"mode": "100644", "path": path, "type": "Blob", "value": {"contents": _js(chunk), "encoding": "utf-8"}}
+
+
+def emit_from_dump(dump: bytes, interner: ol.Interner, long_name, chunk_size: int = CHUNK_SIZE) -> dict:
+    """emit_v1 over an engine / oracle canonical dump (bytes)."""
+    hdr, segs = ol.parse_dump(dump)
+    return emit_v1(hdr, segs, interner, long_name, chunk_size)
+
+
+# ---- load -------------------------------------------------------------------------------------
+def _blobs(tree: dict) -> Dict[str, str]:
+    """path -> contents of a merge-tree snapshot tree; a SharedString's tree holds it under `content`."""
+    out = {}
+    for e in tree["entries"]:
+        if e["type"] == "Tree" and e["path"] == "content":
+            return _blobs(e["value"])
+        if e["type"] == "Blob":
+            out[e["path"]] = e["value"]["contents"]
+    return out
+
+
+def _latest(path: str, chunk: dict) -> dict:
+    """toLatestVersion (snapshotChunks.ts:136-163): a legacy chunk (no version) in the v1 shape; a
+    legacy header without headerMetadata gets buildHeaderMetadataForLegecyChunk's (165-185)."""
+    if chunk.get("version") == "1":
+        return chunk
+    if chunk.get("version") is not None:
+        raise ValueError(f"Unsupported chunk path: {path} version: {chunk['version']}")
+    md = None
+    if path == HEADER:
+        md = chunk.get("headerMetadata")
+        if md is None:
+            ids = [{"id": HEADER}]
+            if chunk["chunkLengthChars"] < chunk["totalLengthChars"]:
+                ids.append({"id": BODY})
+            md = {"orderedChunkMetadata": ids, "minSequenceNumber": chunk.get("chunkMinSequenceNumber"),
+                  "sequenceNumber": chunk.get("chunkSequenceNumber"), "totalLength": chunk["totalLengthChars"],
+                  "totalSegmentCount": chunk["totalSegmentCount"]}
+    return {"version": "1", "segmentCount": chunk["chunkSegmentCount"], "length": chunk["chunkLengthChars"],
+            "segments": chunk["segmentTexts"], "startIndex": chunk["chunkStartSegmentIndex"], "headerMetadata": md}
+
+
+def _chunks(tree: dict):
+    """(header chunk, body chunks in orderedChunkMetadata order, catch-up messages) of a snapshot
+    (SnapshotLoader.initialize / loadBodyAndCatchupOps, snapshotLoader.ts:36-84)."""
+    blobs = _blobs(tree)
+    head = _latest(HEADER, json.loads(blobs[HEADER]))
+    md = head["headerMetadata"]
+    ids = [c["id"] for c in md["orderedChunkMetadata"]]
+    body = [_latest(i, json.loads(blobs[i])) for i in ids[1:]]
+    rest = [p for p in blobs if p not in ids]
+    if len(rest) > 1:
+        raise ValueError("Unexpected blobs in snapshot")
+    catchup = json.loads(blobs[rest[0]]) if rest else []  # the legacy catch-up ops blob (loadCatchupOps)
+    return head, body, catchup
+
+
+def load_records(tree: dict, log: ol.DocLog, client_index, local_client: Optional[str] = "snapshot") -> dict:
+    """Append a snapshot's load records to `log` (one document's event stream); returns the header
+    metadata. `client_index(name)` maps a long client id to the batch's long-client index;
+    `local_client` is the id startOrUpdateCollaboration gets (None: a detached load, no collaboration,
+    snapshotLoader.ts:135-151)."""
+    head, chunks, catchup = _chunks(tree)
+    md = head["headerMetadata"]
+    body = [spec for c in chunks for spec in c["segments"]]
+
+    batch = [False]  # an open loadBody batch (snapshotLoader.ts:215-226)
+
+    def add(kind, spec, countdown=0):
+        info = {}
+        if isinstance(spec, dict) and "json" in spec:  # IJSONSegmentWithMergeInfo (snapshotChunks.ts:60-73)
+            info, spec = spec, spec["json"]
+        if kind == ol.OP_APPEND:
+            # segments without seq and client batch into one insertSegments call: members after the
+            # first continue at the previous member's position (MT_OPF_GROUPED, mt_oplog.h)
+            batchable = info.get("seq") is None and info.get("client") is None
+            if batchable and batch[0]:
+                kind |= ol.OPF_GROUPED
+            batch[0] = batchable
+        seq = info.get("seq", 0)
+        client = client_index(info["client"]) if info.get("client") is not None else ol.CLIENT_NONCOLLAB
+        rseq = info.get("removedSeq", 0) or 0
+        rcl = client_index(info["removedClient"]) if info.get("removedClient") is not None else 0
+        common = dict(client=client, seq=seq, ref_seq=rseq, min_seq=rcl, pos1=countdown)
+        if isinstance(spec, str):
+            log.add(kind, text=spec, **common)
+        elif isinstance(spec, list):  # PermutationSegment [length, start]
+            log.add(kind, perm=spec[0], **common)
+        elif "marker" in spec:
+            log.add(kind, marker=spec["marker"]["refType"], props=spec.get("props"), **common)
+        else:
+            log.add(kind, text=spec["text"], props=spec.get("props"), **common)
+
+    hs = head["segments"]
+    for i, spec in enumerate(hs):
+        add(ol.OP_RELOAD, spec, countdown=len(hs) - i)
+    if local_client is not None:
+        msn = md.get("minSequenceNumber")
+        log.add(ol.OP_COLLAB, client=client_index(local_client), seq=md["sequenceNumber"],
+                min_seq=msn if msn is not None else md["sequenceNumber"])
+    for spec in body:
+        add(ol.OP_APPEND, spec)
+    if catchup:  # the messages SharedString applies after loading (sequence.ts loadContent)
+        from . import wire
+        wire.add_messages(log, catchup, client_index)
+    return md
+
+
+def segment_specs(tree: dict) -> List[Any]:
+    """Every segment spec of a snapshot in order (header chunk, then the body chunks)."""
+    head, chunks, _ = _chunks(tree)
+    return list(head["segments"]) + [spec for c in chunks for spec in c["segments"]]

@@ -38,7 +38,7 @@ enum {
     MT_OK = 0,
     MT_E_INSERT_FAILED = 1, /* per doc: mergeTree.ts:2243-2249 "MergeTree insert failed"       */
     MT_E_ASSERT = 2,        /* per doc: a reference `assert` would have thrown                 */
-    MT_E_INVALID_RANGE = 3, /* per doc: local op rejected by getValidOpRange (client.ts:486)   */
+    MT_E_INVALID_RANGE = 3, /* reserved (a local op getValidOpRange rejects is a no-op, client.ts:486) */
     MT_E_UNSUPPORTED = 4,   /* per doc: >8 property keys or >8 overlapping removers            */
     MT_E_CAPACITY = 5,      /* per doc: a capacity in mt_caps was exceeded                     */
     MT_E_ARG = 16,          /* engine: bad argument                                            */

@@ -35,7 +35,25 @@ enum {
     MT_OP_REMOVE = 1,
     MT_OP_ANNOTATE = 2,
     MT_OP_NOOP = 4, /* sequenced message that is not a merge-tree op: advances currentSeq/MSN only */
+    /* Snapshot load (SnapshotLoader, snapshotLoader.ts:86-228), on an empty non-collaborating replica:
+     *   RELOAD: one header segment; pos1 counts down n..1 over the header's n records, and the whole
+     *           header becomes the tree at once (reloadFromSegments, mergeTree.ts:1229-1284: blocks of
+     *           MaxNodesInBlock-1 = 7 children built bottom-up);
+     *   COLLAB: startOrUpdateCollaboration(client, minSeq = min_seq, currentSeq = seq) (1053-1073);
+     *   APPEND: one body segment (loadBody, 160-227): insertSegments(localLength, [seg], refSeq 0, client,
+ *           seq); consecutive segments without seq/client go in one batch insertSegments call whose
+ *           members after the first are flagged MT_OPF_GROUPED (placed at the previous member's
+ *           position + its length, blockInsert mergeTree.ts:2226-2256).
+     * Segment fields of RELOAD / APPEND: seg_kind, text_off, props; pos2 = the segment's length in
+     * UTF-16 units (TEXT) or rows (PERM), a marker's refType (MARKER) — a loaded segment may exceed
+     * text_len's 16 bits; seq (0 = UniversalSequenceNumber); client = the spec's long client,
+     * MT_CLIENT_NONCOLLAB if absent; ref_seq = removedSeq (> 0) or 0 if not removed; min_seq = the
+     * removing long client. */
+    MT_OP_RELOAD = 5,
+    MT_OP_COLLAB = 6,
+    MT_OP_APPEND = 7,
 };
+#define MT_CLIENT_NONCOLLAB 0xFFFF /* NonCollabClient (constants.ts:15) */
 #define MT_OP_KIND_MASK 0x07
 #define MT_OPF_LOCAL 0x80 /* unsequenced local edit made by this replica */
 /* A group op (MergeTreeDeltaType.GROUP, ops.ts:33, 100; e.g. SharedString.replaceRange,

@@ -146,6 +146,10 @@ struct mto_client {
     int err;
     int verify;
     Alloc alloc;
+    /* snapshot header being reloaded (MT_OP_RELOAD records) */
+    int nreload, reloadcap;
+    Node** reload;
+    int loadPos; /* next insert position of the open loadBody batch */
     /* replay scratch: op text/props */
     const uint16_t* textPool;
     const mt_props_rec* propsPool;
@@ -1401,11 +1405,9 @@ static Group* addToPendingList(mto_client* c, Seg* s, Group* g, int localSeq) {
     return g;
 }
 
-/* insertSegments (2001-2031) + blockInsert (2174-2257) for a single new segment */
-static void insertSegments(mto_client* c, int pos, Seg* seg, int refSeq, int clientId, int seq) {
-    ensureIntervalBoundary(c, pos, refSeq, clientId);
-    int hasLocalSeq = seq == UnassignedSequenceNumber;
-    int localSeq = hasLocalSeq ? ++c->cw.localSeq : 0;
+/* blockInsert (2174-2257) of a single new segment */
+static void blockInsert(mto_client* c, int pos, Seg* seg, int refSeq, int clientId, int seq, int hasLocalSeq,
+                        int localSeq) {
     if (seg->hdr.cachedLength > 0) {
         seg->seq = seq;
         seg->hasLocalSeq = hasLocalSeq;
@@ -1428,8 +1430,14 @@ static void insertSegments(mto_client* c, int pos, Seg* seg, int refSeq, int cli
             }
         }
     }
-    if (c->cw.collaborating && seq != UnassignedSequenceNumber) zamboniSegments(c);
 }
+static void insertSegments(mto_client* c, int pos, Seg* seg, int refSeq, int clientId, int seq) {
+    ensureIntervalBoundary(c, pos, refSeq, clientId);
+    int hasLocalSeq = seq == UnassignedSequenceNumber;
+    int localSeq = hasLocalSeq ? ++c->cw.localSeq : 0;
+    blockInsert(c, pos, seg, refSeq, clientId, seq, hasLocalSeq, localSeq);
+    if (c->cw.collaborating && seq != UnassignedSequenceNumber) zamboniSegments(c);
+} /* insertSegments (2001-2031) of a single new segment */
 
 /* markRangeRemoved (2640-2752) */
 typedef struct RemoveCtx {
@@ -1612,6 +1620,7 @@ void mto_destroy(mto_client* c) {
     free(c->alloc.p);
     free(c->alloc.tag);
     free(c->pending.a);
+    free(c->reload);
     free(c->scour.L);
     free(c->shortToLong);
     free(c->longToShort);
@@ -1619,7 +1628,7 @@ void mto_destroy(mto_client* c) {
 }
 
 int mto_start_collab(mto_client* c, int longId, int minSeq, int curSeq) { /* 1053-1073 */
-    if (c->longClientId < 0) {
+    if (c->longClientId < 0 && longId >= 0) { /* longId < 0: the replica stays detached (a snapshot load) */
         c->longClientId = longId;
         addLongClientId(c, longId);
         /* startCollaboration (mergeTree.ts:1287-1304) */
@@ -1635,12 +1644,13 @@ int mto_start_collab(mto_client* c, int longId, int minSeq, int curSeq) { /* 105
 
 static Seg* specToSegment(mto_client* c, const mt_op_rec* op) { /* textSegment.ts:31-39 / Marker.make */
     Seg* s;
+    int len = (op->kind & MT_OP_KIND_MASK) >= MT_OP_RELOAD ? op->pos2 : op->text_len; /* mt_oplog.h */
     if (op->seg_kind == MT_SEG_MARKER)
         s = newSeg(c, MT_SEG_MARKER, NULL, 0, op->pos2);
     else if (op->seg_kind == MT_SEG_PERM) /* PermutationVector.insert (permutationvector.ts:147-151) */
-        s = newSeg(c, MT_SEG_PERM, NULL, op->text_len, 0);
+        s = newSeg(c, MT_SEG_PERM, NULL, len, 0);
     else
-        s = newSeg(c, MT_SEG_TEXT, c->textPool + op->text_off, op->text_len, 0);
+        s = newSeg(c, MT_SEG_TEXT, c->textPool + op->text_off, len, 0);
     if (op->props) { /* TextSegment.make(text, props) -> addProperties(props) (no collab window) */
         const mt_props_rec* pr = &c->propsPool[op->props - 1];
         segAddProperties(s, c->kvPool + pr->kv_off, pr->nkv, pr->combining == MT_COMBINE_REWRITE, 0, 0);
@@ -1661,10 +1671,7 @@ static void applyOp(mto_client* c, const mt_op_rec* op, int isLocal, int clientI
         int length = c->root->hdr.cachedLength;
         int bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
         if (kind != MT_OP_INSERT && end <= start) bad = 1;
-        if (bad) {
-            FAIL(c, MTO_ERR_INVALID_RANGE);
-            return;
-        }
+        if (bad) return; /* logs InvalidOpRange and returns undefined: the op has no effect */
     }
     if (kind == MT_OP_INSERT) {
         Seg* s = specToSegment(c, op);
@@ -1689,6 +1696,67 @@ static void applyOp(mto_client* c, const mt_op_rec* op, int isLocal, int clientI
     }
 }
 
+/* SnapshotLoader.specToSegment (snapshotLoader.ts:96-126) for a RELOAD / APPEND record */
+static Seg* loaderSegment(mto_client* c, const mt_op_rec* op) {
+    Seg* s = specToSegment(c, op);
+    s->clientId = op->client == MT_CLIENT_NONCOLLAB ? NonCollabClient : getOrAddShortClientId(c, op->client);
+    s->seq = op->seq;
+    if (op->ref_seq > 0) {
+        s->hasRemoved = 1;
+        s->removedSeq = op->ref_seq;
+        s->removedClientId = getOrAddShortClientId(c, op->min_seq);
+    }
+    return s;
+}
+/* reloadFromSegments (mergeTree.ts:1229-1284): blocks of 7 children, built bottom-up */
+static Block* buildMergeBlock(mto_client* c, Node** nodes, int n) {
+    const int maxChildren = MaxNodesInBlock - 1;
+    int blockCount = (n + maxChildren - 1) / maxChildren;
+    Node** blocks = xmalloc(sizeof(Node*) * blockCount);
+    for (int nodeIndex = 0, bi = 0; bi < blockCount; bi++) {
+        Block* b = makeBlock(c, 0);
+        for (int ci = 0; ci < maxChildren && nodeIndex < n; ci++, nodeIndex++) {
+            int index = b->childCount++; /* addNode (1224-1227) */
+            assignChild(b, nodes[nodeIndex], index);
+        }
+        blockUpdate(b);
+        blocks[bi] = &b->hdr;
+    }
+    Block* r = blockCount == 1 ? (Block*)blocks[0] : buildMergeBlock(c, blocks, blockCount);
+    free(blocks);
+    return r;
+}
+static void applyLoad(mto_client* c, const mt_op_rec* op) {
+    int kind = op->kind & MT_OP_KIND_MASK;
+    if (kind == MT_OP_RELOAD) {
+        if (c->cw.collaborating) FAIL(c, MTO_ERR_ASSERT); /* assert(!collaborating) (1231) */
+        if (c->nreload == c->reloadcap) {
+            c->reloadcap = c->reloadcap ? 2 * c->reloadcap : 64;
+            c->reload = realloc(c->reload, sizeof(Node*) * c->reloadcap);
+        }
+        c->reload[c->nreload++] = &loaderSegment(c, op)->hdr;
+        if (op->pos1 == 1) { /* the header's last segment: build the tree */
+            c->root = buildMergeBlock(c, c->reload, c->nreload);
+            c->root->hdr.parent = NULL;
+            c->nreload = 0;
+        }
+    } else if (kind == MT_OP_COLLAB) {
+        mto_start_collab(c, op->client, op->min_seq, op->seq);
+    } else { /* MT_OP_APPEND: loadBody (snapshotLoader.ts:160-227) */
+        Seg* s = loaderSegment(c, op);
+        if (op->kind & MT_OPF_GROUPED) { /* a later member of a batch: blockInsert's insertPos (2226-2256) */
+            int pos = c->loadPos;
+            c->loadPos += s->hdr.cachedLength;
+            blockInsert(c, pos, s, UniversalSequenceNumber, s->clientId, s->seq, 0, 0);
+            /* (the batch's one zamboniSegments pass runs after its first member: with minSeq fixed
+             * during a load and members never entering the LRU set, later passes find nothing) */
+        } else {
+            c->loadPos = c->root->hdr.cachedLength + s->hdr.cachedLength;
+            insertSegments(c, c->root->hdr.cachedLength, s, UniversalSequenceNumber, s->clientId, s->seq);
+        }
+    }
+}
+
 int mto_apply(mto_client* c, const mt_op_rec* op, const uint16_t* text, const mt_props_rec* props,
               const mt_kv* kv) {
     if (c->err) return c->err;
@@ -1698,6 +1766,10 @@ int mto_apply(mto_client* c, const mt_op_rec* op, const uint16_t* text, const mt
     int kind = op->kind & MT_OP_KIND_MASK;
     if (op->kind & MT_OPF_LOCAL) {
         applyOp(c, op, 1, c->cw.clientId, c->cw.currentSeq, seqNumberLocal(c));
+        return c->err;
+    }
+    if (kind >= MT_OP_RELOAD) {
+        applyLoad(c, op);
         return c->err;
     }
     /* applyMsg (client.ts:797-819) */

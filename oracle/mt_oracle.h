@@ -28,7 +28,7 @@ enum {
     MTO_OK = 0,
     MTO_ERR_INSERT_FAILED = 1,   /* mergeTree.ts:2243-2249 "MergeTree insert failed" */
     MTO_ERR_ASSERT = 2,          /* an `assert` of the reference would have thrown   */
-    MTO_ERR_INVALID_RANGE = 3,   /* local op rejected by getValidOpRange (client.ts:486-548) */
+    MTO_ERR_INVALID_RANGE = 3,   /* reserved: a local op rejected by getValidOpRange (client.ts:486-548) is a no-op */
     MTO_ERR_UNSUPPORTED = 4,
 };
 

@@ -75,6 +75,9 @@ class HostStore:
     def error(self, doc):
         return self.L.mth_error(self.h, doc)
 
+    def error_op(self, doc):
+        return self.L.mth_error_op(self.h, doc)
+
     def dump(self, doc) -> bytes:
         n = self.L.mth_dump(self.h, doc, None, 0)
         buf = np.zeros(n, np.uint8)

@@ -6,40 +6,11 @@ three implementations, so the reference's known-answer scenarios run unchanged a
 """
 from __future__ import annotations
 
-import struct
-
 import numpy as np
 
 from fluidframework_amd import oplog as ol
+from fluidframework_amd.oplog import parse_dump  # noqa: F401 (re-exported for the tests)
 from oracle_client import Msg, OracleClient
-
-
-def parse_dump(b: bytes):
-    """Decode the canonical dump (include/mt_oplog.h) into (header dict, [segment dicts])."""
-    hdr = struct.unpack_from("<6i", b, 0)
-    off = 24
-    segs = []
-    for _ in range(hdr[4]):
-        kind, flags, nov, ngroups = struct.unpack_from("<4B", b, off)
-        off += 4
-        f = struct.unpack_from("<8i", b, off)
-        off += 32
-        ov = list(struct.unpack_from(f"<{nov}i", b, off))
-        off += 4 * nov
-        nprops, ref_type = struct.unpack_from("<2H", b, off)
-        off += 4
-        props = [struct.unpack_from("<2H", b, off + 4 * k) for k in range(nprops)]
-        off += 4 * nprops
-        text = ""
-        if kind == ol.SEG_TEXT:
-            text = b[off: off + 2 * f[0]].decode("utf-16-le")
-            off += 2 * f[0]
-        segs.append(dict(kind=kind, flags=flags, ngroups=ngroups, len=f[0], seq=f[1], client=f[2],
-                         removedSeq=f[3] if flags & 2 else None, removedClient=f[4], localSeq=f[5],
-                         localRemovedSeq=f[6], leaf=f[7], overlap=ov, props=props, refType=ref_type, text=text))
-    assert off == len(b)
-    return dict(currentSeq=hdr[0], minSeq=hdr[1], localSeq=hdr[2], length=hdr[3], nsegs=hdr[4],
-                nleaf=hdr[5]), segs
 
 
 class _LogReplica:
@@ -81,11 +52,6 @@ class _LogReplica:
     @property
     def current_seq(self):
         return parse_dump(self.dump())[0]["currentSeq"]
-
-    def pending_groups(self):
-        # number of distinct pending groups = localSeq values still referenced by segments
-        _, segs = parse_dump(self.dump())
-        return self._pending
 
     def get_length(self):
         return parse_dump(self.dump())[0]["length"]

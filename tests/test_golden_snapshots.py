@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 from fluidframework_amd import oplog as ol
+from fluidframework_amd import snapshot as sn
 import oracle_client as oc
 from replicas import parse_dump
 
@@ -87,56 +88,39 @@ def _golden_segments(name):
 
 
 def _snapshot_segments(dump: bytes, it: ol.Interner):
-    """SnapshotV1.extractSync's coalescing over the canonical dump (non-collaborating doc: every
-    segment has seq 0 <= minSeq 0 and none is removed, so every one is a coalescing candidate)."""
-    _, segs = parse_dump(dump)
-    out = []
-    prev = None  # [kind, text, props dict or None, refType]
-
-    def props_of(s):
-        if not (s["flags"] & 1):
-            return None
-        return {it.key_str(k): it.value_obj(v) for k, v in s["props"]}
-
-    def spec(p):
-        if p[0] == ol.SEG_MARKER:
-            o = {"marker": {"refType": p[3]}}
-            if p[2] is not None:
-                o["props"] = p[2]
-            return o
-        return {"text": p[1], "props": p[2]} if p[2] is not None else p[1]
-
-    for s in segs:
-        assert s["removedSeq"] is None and s["seq"] == 0
-        cur = [s["kind"], s["text"], props_of(s), s["refType"]]
-        if prev is None:
-            prev = cur
-        elif (prev[0] == ol.SEG_TEXT and cur[0] == ol.SEG_TEXT and not prev[1].endswith("\n")
-              and (len(prev[1]) <= TEXT_GRANULARITY or len(cur[1]) <= TEXT_GRANULARITY)
-              and prev[2] == cur[2]):
-            prev = [prev[0], prev[1] + cur[1], prev[2], prev[3]]
-        else:
-            out.append(spec(prev))
-            prev = cur
-    if prev is not None:
-        out.append(spec(prev))
-    return out
+    """The product's SnapshotV1.extractSync (fluidframework_amd/snapshot.py) over a dump, as specs."""
+    hdr, segs = parse_dump(dump)
+    return [spec for spec, _ in sn.extract_segments(hdr, segs, it, _long_name)]
 
 
-def _replay(kind, d: _Doc) -> bytes:
-    ops, text, props, kv = d.log.arrays()
+def _long_name(i):
+    return f"c{i}"
+
+
+def _contents(tree):
+    return {k: v for k, v in sn._blobs(tree).items()}
+
+
+def _replay(kind, d: _Doc, local: int = 0) -> bytes:
+    return _replay_arrays(kind, d.it, d.log.arrays(), local)
+
+
+def _replay_arrays(kind, it, arrays, local):
+    ops, text, props, kv = arrays
     if kind == "oracle":
-        c = oc.OracleClient(d.it)
+        c = oc.OracleClient(it)
         assert c.replay_arrays(ops, text, props, kv) == 0
         return c.dump()
     if kind == "host":
         import core_host
         st = core_host.HostStore(1, (16384, 32768, 1 << 18, 1024, 64, 64))
+        st.start_collab(0, local)
         assert st.replay(0, ops, text, props, kv) == 0
         return st.dump(0)
     from fluidframework_amd.engine import Engine
     eng = Engine(1, ncap=16384, hcap=32768, acap=1 << 18, mcap=1024, gcap=64, ccap=64)
-    eng.replay(ol.Batch.from_arrays([(ops, text, props, kv)], [0]))
+    eng.start_collab([local])
+    eng.replay(ol.Batch.from_arrays([(ops, text, props, kv)], [local]))
     err, _ = eng.errors()
     assert err[0] == 0
     return eng.dump(0)
@@ -149,7 +133,53 @@ NAMES = ["headerOnly", "headerAndBody", "largeBody", "withMarkers", "withAnnotat
 @pytest.mark.parametrize("name", NAMES)
 def test_snapshot_golden(name, kind):
     d = _script(name)
-    got = _snapshot_segments(_replay(kind, d), d.it)
+    dump = _replay(kind, d, local=-1)  # a detached SharedString: no collaboration
+    got = _snapshot_segments(dump, d.it)
     want = _golden_segments(name)
     assert len(got) == len(want)
     assert got == want
+    # the whole emitted tree (SnapshotV1.emit: chunking, header metadata, JSON text) byte for byte
+    tree = json.load(open(os.path.join(GOLD, name + ".json")))
+    assert _contents(sn.emit_from_dump(dump, d.it, _long_name)) == _contents(tree)
+
+
+@pytest.mark.parametrize("kind", ["oracle", "host", pytest.param("gpu", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("name", NAMES)
+def test_snapshot_golden_load_roundtrip(name, kind):
+    """SnapshotLoader (snapshotLoader.ts:86-228) of the fixture as load records: header reload
+    (7-child blocks bottom-up), startOrUpdateCollaboration("snapshot"), body appends; the loaded
+    replica's text is the fixture's, and emitting it again reproduces the fixture exactly."""
+    tree = json.load(open(os.path.join(GOLD, name + ".json")))
+    it = ol.Interner()
+    log = ol.DocLog(it)
+    md = sn.load_records(tree, log, lambda n: {"snapshot": 0}[n], "snapshot")
+    dump = _replay_arrays(kind, it, log.arrays(), -1)
+    hdr, segs = parse_dump(dump)
+    assert hdr["length"] == md["totalLength"] and hdr["currentSeq"] == md["sequenceNumber"]
+    text = "".join(s["text"] if s["kind"] == ol.SEG_TEXT else "" for s in segs)
+    want = "".join(x if isinstance(x, str) else x.get("text", "") for x in sn.segment_specs(tree))
+    assert text == want
+    nhead = json.loads(sn._blobs(tree)["header"])["segmentCount"]
+    assert hdr["nleaf"] >= -(-nhead // 7)  # reloadFromSegments' leaf blocks hold <= 7 segments
+    assert _contents(sn.emit_from_dump(dump, it, lambda i: "snapshot")) == _contents(tree)
+
+
+LEGACY = {"legacy": os.path.join(os.path.dirname(GOLD), "sequence_snapshots_legacy"),
+          "legacyWithCatchUp": os.path.join(os.path.dirname(GOLD), "sequence_snapshots_legacy_catchup")}
+
+
+@pytest.mark.parametrize("kind", ["oracle", "host", pytest.param("gpu", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("fmt", sorted(LEGACY))
+@pytest.mark.parametrize("name", NAMES)
+def test_legacy_snapshot_loads(name, fmt, kind):
+    """The reference's legacy-format fixtures (packages/dds/sequence/src/test/snapshots/legacy*,
+    snapshotVersion.spec.ts): chunks converted by toLatestVersion (snapshotChunks.ts:136-185), the
+    catch-up ops blob applied after the body; the loaded document emits as the v1 fixture of the
+    same content, byte for byte."""
+    tree = json.load(open(os.path.join(LEGACY[fmt], name + ".json")))
+    it = ol.Interner()
+    log = ol.DocLog(it)
+    sn.load_records(tree, log, lambda n: {"snapshot": 0}[n], "snapshot")
+    dump = _replay_arrays(kind, it, log.arrays(), -1)
+    v1 = json.load(open(os.path.join(GOLD, name + ".json")))
+    assert _contents(sn.emit_from_dump(dump, it, lambda i: "snapshot")) == _contents(v1)

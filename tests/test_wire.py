@@ -1,0 +1,139 @@
+"""Wire-format ingestion (fluidframework_amd/wire.py) pinned to the reference.
+
+Each sequenced message of a reference fixture's logs is written as the JSON the reference receives
+(ISequencedDocumentMessage + IMergeTreeOp, group ops as {type: 3, ops}), ingested back through
+wire.add_message, and the rebuilt logs must replay to the REFERENCE's digests (tests/golden/ref_*.npz)
+on the oracle (CPU) and the HIP engine (GPU). Local edits are API calls, not messages: their records
+pass through unchanged.
+"""
+import json
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import gen
+from fluidframework_amd import oplog as ol
+from fluidframework_amd import wire
+import oracle_client as oc
+from test_ref_goldens import caps_for, regenerate
+
+
+def _seg(rec, text, it, props):
+    ps = _props(rec, it, props)
+    if rec["seg_kind"] == ol.SEG_PERM:
+        return [int(rec["text_len"]), -0x80000000]
+    if rec["seg_kind"] == ol.SEG_MARKER:
+        s = {"marker": {"refType": int(rec["pos2"])}}
+        if ps is not None:
+            s["props"] = ps[0]
+        return s
+    t = text[rec["text_off"]: rec["text_off"] + rec["text_len"]].tobytes().decode("utf-16-le")
+    return {"text": t, "props": ps[0]} if ps is not None else t
+
+
+def _props(rec, it, props):
+    if not rec["props"]:
+        return None
+    p, kv = props
+    pr = p[rec["props"] - 1]
+    d = {}
+    for k, v in kv[pr["kv_off"]: pr["kv_off"] + pr["nkv"]]:
+        d[it.key_str(int(k))] = None if v == 0 else it.value_obj(int(v))
+    return d, int(pr["combining"])
+
+
+def _wire_op(rec, text, it, props):
+    kind = rec["kind"] & 7
+    if kind == ol.OP_INSERT:
+        return {"type": 0, "pos1": int(rec["pos1"]), "seg": _seg(rec, text, it, props)}
+    if kind == ol.OP_REMOVE:
+        return {"type": 1, "pos1": int(rec["pos1"]), "pos2": int(rec["pos2"])}
+    ps = _props(rec, it, props) or ({}, 0)
+    op = {"type": 2, "pos1": int(rec["pos1"]), "pos2": int(rec["pos2"]), "props": ps[0]}
+    if ps[1] == ol.COMBINE_REWRITE:
+        op["combiningOp"] = {"name": "rewrite"}
+    return op
+
+
+def rebuild(b: ol.Batch, d: int, it: ol.Interner):
+    """Document d's log rebuilt through the wire path: (arrays, number of messages)."""
+    ops, text, props, kv = b.doc_arrays(d)
+    log = ol.DocLog(it, local_long_id=int(b.local_long_id[d]))
+    members, nmsg = [], 0
+    for rec in ops:
+        if rec["kind"] & ol.OPF_LOCAL:  # an API call, kept as is
+            log.ops.append(tuple(rec.tolist()))
+            continue
+        if rec["kind"] & ol.OPF_GROUPED:
+            members.append(_wire_op(rec, text, it, (props, kv)))
+            continue
+        msg = {"clientId": f"c{rec['client']}", "sequenceNumber": int(rec["seq"]),
+               "referenceSequenceNumber": int(rec["ref_seq"]), "minimumSequenceNumber": int(rec["min_seq"]),
+               "type": "op" if rec["kind"] & 7 != ol.OP_NOOP else "noop"}
+        if msg["type"] == "op":
+            op = _wire_op(rec, text, it, (props, kv))
+            msg["contents"] = {"type": 3, "ops": members + [op]} if members else op
+        members = []
+        wire.add_message(log, json.loads(json.dumps(msg)), lambda n: int(n[1:]))
+        nmsg += 1
+    # local records reference the original pools: rebuild them on top of the original text/props
+    a = log.arrays()
+    return (a[0], np.concatenate([text, a[1]]), props, kv, len(text), a), nmsg
+
+
+def _arrays(r):
+    ops, text, props, kv, ntext, a = r
+    # wire records carry text offsets into the log's own pool (appended after the original text);
+    # wire props index the log's own props table, which equals the original one only through the
+    # interner, so rebuild props too: original table first, then the log's
+    out = ops.copy()
+    wired = (out["kind"] & ol.OPF_LOCAL) == 0
+    out["text_off"][wired] += np.uint32(ntext)
+    lp, lkv = a[2], a[3]
+    has = wired & (out["props"] != 0)
+    out["props"][has] += np.uint16(len(props))
+    lp = lp.copy()
+    lp["kv_off"] += np.uint32(len(kv))
+    return out, text, np.concatenate([props, lp]), np.concatenate([kv, lkv])
+
+
+@pytest.mark.parametrize("name", ["c1_farm", "c3_lagged", "c5_perm"])
+def test_wire_ingestion_replays_to_reference_digests(name):
+    z, w, b = regenerate(name)
+    it = gen.generator_interner()
+    for d in range(b.ndocs):
+        r, nmsg = rebuild(b, d, it)
+        assert nmsg > 0
+        c = oc.OracleClient(it)
+        c.start_collab(int(b.local_long_id[d]))
+        assert c.replay_arrays(*_arrays(r)) == 0
+        assert c.digest() == int(z["digests"][d]), f"doc {d}"
+
+
+def test_unsupported_wire_ops_raise():
+    log = ol.DocLog(ol.Interner())
+    base = {"clientId": "a", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+            "type": "op"}
+    with pytest.raises(ValueError):
+        wire.add_message(log, dict(base, contents={"type": 1, "relativePos1": {"id": "m"}, "pos2": 3}), wire.ClientNames())
+    with pytest.raises(ValueError):
+        wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
+                                                   "combiningOp": {"name": "incr"}}), wire.ClientNames())
+    names = wire.ClientNames(["x"])
+    wire.add_message(log, dict(base, clientId="y", type="noop"), names)
+    assert names.name(1) == "y" and log.ops[-1][0] == ol.OP_NOOP
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c3_lagged", "c5_perm"])
+def test_gpu_wire_ingestion_matches_reference(name):
+    from fluidframework_amd.engine import Engine
+    z, w, b = regenerate(name)
+    it = gen.generator_interner()
+    per = [_arrays(rebuild(b, d, it)[0]) for d in range(b.ndocs)]
+    eng = Engine(b.ndocs, **caps_for(w))
+    eng.start_collab(b.local_long_id)
+    eng.replay(ol.Batch.from_arrays(per, b.local_long_id))
+    err, _ = eng.errors()
+    assert (err == 0).all()
+    assert (eng.digests() == z["digests"]).all()

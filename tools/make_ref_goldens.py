@@ -85,8 +85,35 @@ def fnv1a64(bs: bytes) -> int:
     return h
 
 
-def run_reference(b: ol.Batch, d: str, node: str):
-    write_batch(b, gen.generator_interner(), d)
+def snapshot_cut(ops: np.ndarray, local: int, frac: float = 0.55) -> int:
+    """A record index at which the replica has no pending local op and no group message is open, as
+    close to `frac` of the log as possible: a snapshot drops unacked segments (snapshotV1.ts:187-192),
+    so the rest of the log must not ack anything sent before the cut."""
+    kind = ops["kind"]
+    is_local = (kind & ol.OPF_LOCAL) != 0
+    closes = (kind & ol.OPF_GROUPED) == 0
+    sent = np.cumsum(is_local & closes)
+    acked = np.cumsum(~is_local & closes & (ops["client"] == local) & ((kind & 7) != ol.OP_NOOP))
+    ok = np.zeros(len(ops) + 1, bool)
+    ok[0] = True
+    ok[1:] = (sent == acked) & closes
+    cand = np.nonzero(ok)[0]
+    return int(cand[np.argmin(np.abs(cand - frac * len(ops)))])
+
+
+def canonical_tree(tree: dict) -> str:
+    """Order-insensitive form of a snapshot tree: each blob's JSON re-serialized with sorted keys
+    (property-set key order is insertion order in the reference, key-id order here)."""
+    from fluidframework_amd import snapshot as sn
+    blobs = sn._blobs(tree)
+    return json.dumps({k: json.loads(v) for k, v in blobs.items()}, sort_keys=True, separators=(",", ":"))
+
+
+def run_reference(b: ol.Batch, d: str, node: str, cuts=None, interner=None):
+    write_batch(b, interner or gen.generator_interner(), d)
+    if cuts is not None:
+        with open(os.path.join(d, "snapshots.json"), "w") as f:
+            json.dump([[i, int(c), int(b.local_long_id[i])] for i, c in enumerate(cuts)], f)
     t0 = time.time()
     r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d], capture_output=True,
                        text=True)
@@ -99,7 +126,110 @@ def run_reference(b: ol.Batch, d: str, node: str):
     blob = np.fromfile(os.path.join(d, "ref_dumps.bin"), np.uint8)
     off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
     dumps = [blob[off[i]: off[i + 1]].tobytes() for i in range(b.ndocs)]
-    return dumps, info, time.time() - t0
+    snaps = None
+    if cuts is not None:
+        sj = json.load(open(os.path.join(d, "ref_snapshots.json")))
+        if sj["errors"]:
+            raise RuntimeError(f"reference snapshot/load threw on {len(sj['errors'])} docs: {list(sj['errors'].items())[:2]}")
+        lb = np.fromfile(os.path.join(d, "ref_loaded_dumps.bin"), np.uint8)
+        lo = np.fromfile(os.path.join(d, "ref_loaded_off.bin"), "<i8")
+        tail_err = np.full(b.ndocs, -1, np.int64)  # record (tail-relative) at which the loaded client threw
+        for k, (at, _msg) in sj["tailErrors"].items():
+            tail_err[int(k)] = at
+        load_err = np.zeros(b.ndocs, bool)  # the reference could not load the snapshot it emitted
+        for k in sj["loadErrors"]:
+            load_err[int(k)] = True
+        snaps = ([sj["trees"][str(i)] for i in range(b.ndocs)], [lb[lo[i]: lo[i + 1]].tobytes() for i in range(b.ndocs)],
+                 tail_err, sj["tailErrors"], load_err, sj["loadErrors"])
+    return dumps, info, time.time() - t0, snaps
+
+
+def snap_body_logs(ndocs: int = 8, nmsg: int = 480, lag: int = 32):
+    """Documents whose snapshot has a BODY holding collaboration-window segments (SURVEY.md §8(f)
+    f1). Three 4,000-character inserts make a header chunk that stays below the MSN; every later edit
+    (insert / remove / annotate, refSeq lagging up to `lag`) lands at or after position 12,000, so
+    window segments only ever appear in body chunks. Even documents have one editing client that edits
+    near the end (window segments trail the body, which the reference's loadBody can insert); odd
+    documents have two editing anywhere after the header (its insertSegments under a
+    (UniversalSequenceNumber, client) perspective then fails on the other client's window segments,
+    snapshotLoader.ts:200-213). The replica is an observer (long id 0); positions come from an
+    oracle replica's perspective lengths."""
+    import oracle_client as oc
+    it = gen.generator_interner()
+    logs = []
+    for d in range(ndocs):
+        rng = np.random.default_rng(7100 + d)
+        editors = [1] if d % 2 == 0 else [1, 2]
+        log = ol.DocLog(it, local_long_id=0)
+        obs = oc.OracleClient(it)
+        obs.start_collab(0)
+        st = {"seq": 0, "msn": 0}
+        last_ref = {c: 0 for c in editors}
+        seen = set()
+
+        def send(kind, client, ref, **kw):
+            st["seq"] += 1
+            last_ref[client] = ref
+            st["msn"] = min(last_ref.values())
+            log.add(kind, client=client, seq=st["seq"], ref_seq=ref, min_seq=st["msn"], **kw)
+            ops, text, props, kv = log.arrays()
+            assert obs.replay_arrays(ops[-1:], text, props, kv) == 0
+            seen.add(client)
+
+        letters = np.array(list("abcdefghijklmnopqrstuvwxyz"))
+        for k in range(3):
+            send(ol.OP_INSERT, 1, st["seq"], pos1=4000 * k, text="".join(rng.choice(letters, 4000)))
+        for _ in range(nmsg):
+            c = int(rng.choice(editors))
+            cur = st["seq"]
+            ref = int(rng.integers(max(last_ref[c], st["msn"], cur - lag), cur + 1))
+            if c not in seen:  # a client's first op sees the whole header text
+                send(ol.OP_INSERT, c, cur, pos1=12000, text="first")
+                continue
+            L = obs.get_length_at(ref, c)
+            lo = 12000 if len(editors) > 1 else max(12000, L - 40)  # one editor: edits near the end
+            r = rng.random()
+            if r < 0.6 or L <= 12001:
+                t = "".join(rng.choice(letters, int(rng.integers(1, 20))))
+                if rng.random() < 0.2:
+                    t += "\n"
+                send(ol.OP_INSERT, c, ref, pos1=L if len(editors) == 1 else int(rng.integers(lo, L + 1)), text=t)
+            elif r < 0.9:
+                a = int(rng.integers(lo, L))
+                send(ol.OP_REMOVE, c, ref, pos1=a, pos2=min(L, a + int(rng.integers(1, 16))))
+            else:
+                a = int(rng.integers(lo, L))
+                send(ol.OP_ANNOTATE, c, ref, pos1=a, pos2=min(L, a + int(rng.integers(1, 40))),
+                     props={"bold": bool(rng.random() < 0.5), "size": int(rng.integers(8, 12))})
+        logs.append(log)
+    return ol.Batch.from_logs(logs), it
+
+
+def make_snap_body(node: str) -> None:
+    b, it = snap_body_logs()
+    cuts = [snapshot_cut(b.doc(i)[0], 0, frac=0.85) for i in range(b.ndocs)]
+    dumps, info, secs, (trees, loaded, tail_err, tail_msgs, load_err, load_msgs) = run_reference(
+        b, os.path.join(SCRATCH, "snap_body"), node, cuts, interner=it)
+    print(f"snap_body: {b.ndocs} docs; reference load failures on docs {np.nonzero(load_err)[0].tolist()}, "
+          f"tail failures on {np.nonzero(tail_err >= 0)[0].tolist()}", flush=True)
+    bodies = [len(sn_blobs(t)) - 1 for t in trees]
+    print(f"  body chunks per doc: {bodies}")
+    np.savez_compressed(
+        os.path.join(GOLDEN, "refsnap_body.npz"),
+        ops=b.ops, op_off=b.op_off, text=b.text, text_off=b.text_off, props=b.props, props_off=b.props_off,
+        kv=b.kv, kv_off=b.kv_off, local=b.local_long_id, interner=json.dumps({"keys": it.keys, "values": it.values}),
+        digests=np.asarray([fnv1a64(x) for x in dumps], np.uint64),
+        snap_cut=np.asarray(cuts, np.int64),
+        snap_sha256=np.asarray([hashlib.sha256(canonical_tree(t).encode()).hexdigest() for t in trees]),
+        snap_loaded_digests=np.asarray([fnv1a64(x) for x in loaded], np.uint64),
+        snap_tail_error=tail_err, snap_load_error=load_err, snap_trees=json.dumps(trees),
+        source="tools/make_ref_goldens.py snap_body_logs + the reference's SnapshotV1 / SnapshotLoader under node",
+    )
+
+
+def sn_blobs(tree):
+    from fluidframework_amd import snapshot as sn
+    return sn._blobs(tree)
 
 
 def main() -> None:
@@ -109,12 +239,24 @@ def main() -> None:
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
     import oracle_client as oc
+    if "snap_body" in args.sets.split(","):
+        make_snap_body(args.node)
 
     os.makedirs(GOLDEN, exist_ok=True)
     for name in args.sets.split(","):
+        if name == "snap_body":
+            continue
         w, ids = SETS[name]
         b = gen.generate(w, ids=ids, threads=8)
-        dumps, info, secs = run_reference(b, os.path.join(SCRATCH, name), args.node)
+        cuts = [snapshot_cut(b.doc(i)[0], int(b.local_long_id[i])) for i in range(b.ndocs)]
+        dumps, info, secs, (trees, loaded, tail_err, tail_msgs, load_err, load_msgs) = run_reference(
+            b, os.path.join(SCRATCH, name), args.node, cuts)
+        if load_msgs:
+            print(f"  reference: {len(load_msgs)} snapshots do not load in the reference itself: "
+                  f"{sorted(set(m for m in load_msgs.values()))[:2]}")
+        if tail_msgs:
+            print(f"  reference: {len(tail_msgs)} loaded replicas cannot apply the rest of their log: "
+                  f"{sorted(set(m for _, m in tail_msgs.values()))[:3]}")
         digests = np.asarray([fnv1a64(x) for x in dumps], np.uint64)
         _, odig, oerr = oc.replay_batch(b, threads=8)
         agree = int((odig == digests).sum())
@@ -129,6 +271,15 @@ def main() -> None:
             keep_local=keep.local_long_id,
             keep_dumps=np.frombuffer(b"".join(dumps[: keep.ndocs]), np.uint8),
             keep_dump_off=np.concatenate([[0], np.cumsum([len(x) for x in dumps[: keep.ndocs]])]).astype(np.int64),
+            # snapshots: the replica after records [0, cut) summarized by SnapshotV1, loaded by a fresh
+            # client (same long id) that applies [cut, end): canonical tree hashes, loaded digests, and
+            # the trees of the first docs
+            snap_cut=np.asarray(cuts, np.int64),
+            snap_sha256=np.asarray([hashlib.sha256(canonical_tree(t).encode()).hexdigest() for t in trees]),
+            snap_loaded_digests=np.asarray([fnv1a64(x) for x in loaded], np.uint64),
+            snap_tail_error=tail_err,
+            snap_load_error=load_err,
+            keep_snap_trees=json.dumps(trees[: keep.ndocs]),
             source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py, run under node "
                     f"{subprocess.run([args.node, '--version'], capture_output=True, text=True).stdout.strip()} by "
                     "tools/ref_replay.mjs)"),

@@ -8,12 +8,14 @@
 //   batch-dir: ops.bin op_off.bin text.bin text_off.bin props.bin props_off.bin kv.bin kv_off.bin
 //              local.bin meta.json (written by make_ref_goldens.py)
 //   writes batch-dir/ref_dumps.bin + ref_dump_off.bin (+ ref_err.json: per-doc thrown errors)
+//   optional batch-dir/snapshots.json -> ref_snapshots.json (the emitted trees) + ref_loaded_dumps.bin /
+//   ref_loaded_off.bin (dumps of the clients that loaded them and applied the rest of the log)
 import fs from "fs";
 import path from "path";
 
 const [erased, dir] = process.argv.slice(2);
 const timeOnly = process.argv.includes("--time");
-let Client, TextSegment, Marker, PermutationSegment; // bound in main() (Node 12 has no top-level await)
+let Client, TextSegment, Marker, PermutationSegment, SnapshotV1; // bound in main() (Node 12 has no top-level await)
 
 const rd = (f) => fs.readFileSync(path.join(dir, f));
 const meta = JSON.parse(rd("meta.json"));
@@ -88,12 +90,12 @@ const specToSegment = (spec) => (Array.isArray(spec) ? PermutationSegment.fromJS
     : TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec));
 const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
 
-function replayDoc(doc) {
-    const client = new Client(specToSegment, logger);
-    const local = localIds.readInt32LE(4 * doc);
-    if (local >= 0) client.startOrUpdateCollaboration(name(local));
+// apply records [from, to) of `doc` to `client` (applyMsg / the local-edit entry points)
+let applying = -1; // the record being applied (for error reports)
+function applyRange(client, doc, from, to) {
     let members = []; // members of a group message so far (records flagged GROUPED, mt_oplog.h)
-    for (let i = opOff[doc]; i < opOff[doc + 1]; i++) {
+    for (let i = from; i < to; i++) {
+        applying = i;
         const rec = record(i);
         const kind = rec.kind & 7;
         if (rec.kind & 0x80) { // local edit: insertSegmentLocal / removeRangeLocal / annotateRangeLocal
@@ -119,7 +121,51 @@ function replayDoc(doc) {
             minimumSequenceNumber: rec.min_seq, type: kind === 4 ? "noop" : "op", contents,
         });
     }
+}
+
+function replayDoc(doc, to = opOff[doc + 1]) {
+    const client = new Client(specToSegment, logger);
+    const local = localIds.readInt32LE(4 * doc);
+    if (local >= 0) client.startOrUpdateCollaboration(name(local));
+    applyRange(client, doc, opOff[doc], to);
     return client;
+}
+
+// ---- snapshots (snapshots.json: [[doc, cut, loadLong], ...]) --------------------------------------
+// The replica after records [0, cut) is summarized (SnapshotV1.extractSync + emit, snapshotV1.ts); a
+// fresh Client loads that tree (Client.load -> SnapshotLoader, snapshotLoader.ts) as client
+// name(loadLong) and applies records [cut, end); its dump is the "loaded" dump.
+const storageOf = (tree) => {
+    const blobs = new Map(tree.entries.map((e) => [e.path, e.value.contents]));
+    return {
+        read: async (p) => Buffer.from(blobs.get(p), "utf8").toString("base64"),
+        list: async () => [...blobs.keys()],
+        contains: async (p) => blobs.has(p),
+    };
+};
+const runtimeOf = (clientId) => ({
+    options: {}, documentId: "doc", clientId, attachState: "Attached", IFluidSerializer: undefined,
+    IFluidHandleContext: undefined,
+    logger: { ...logger, shipAssert(cond, ev) { if (!cond) throw new Error(`shipAssert ${JSON.stringify(ev)}`); } },
+});
+async function snapshotDoc(doc, cut, loadLong) {
+    const a = replayDoc(doc, opOff[doc] + cut);
+    const snap = new SnapshotV1(a.mergeTree, logger);
+    snap.extractSync();
+    const tree = snap.emit();
+    const b = new Client(specToSegment, logger);
+    try {
+        const { catchupOpsP } = await b.load(runtimeOf(name(loadLong)), storageOf(tree));
+        await catchupOpsP;
+    } catch (e) { // the reference cannot load its own snapshot (e.g. loadBody's insert fails)
+        return { tree, loaded: Buffer.alloc(0), loadError: String(e && e.message || e) };
+    }
+    try {
+        applyRange(b, doc, opOff[doc] + cut, opOff[doc + 1]);
+    } catch (e) { // the loaded replica cannot apply the rest of the log: report where (tail-relative)
+        return { tree, loaded: Buffer.alloc(0), tailError: [applying - opOff[doc] - cut, String(e && e.message || e)] };
+    }
+    return { tree, loaded: dump(b) };
 }
 
 // ---- canonical dump (include/mt_oplog.h; the order and fields of oracle/mt_oracle.c mto_dump) ----
@@ -183,6 +229,7 @@ async function main() {
 const MT = await import(path.join(erased, "index.mjs"));
 ({ Client, TextSegment, Marker } = MT);
 ({ PermutationSegment } = await import(path.join(erased, "permutationSegment.mjs")));
+({ SnapshotV1 } = await import(path.join(erased, "snapshotV1.mjs")));
 const ndocs = opOff.length - 1;
 // optional read queries (queries.json: [[doc, pos, refSeq, longClient | -1 = local view], ...]):
 // getContainingSegment + getPosition (mergeTree.ts:1656-1667, 1619-1636) after the doc's replay
@@ -211,6 +258,29 @@ for (let d = 0; d < ndocs; d++) {
     }
 }
 const secs = Number(process.hrtime.bigint() - t0) / 1e9;
+const spath = path.join(dir, "snapshots.json");
+if (fs.existsSync(spath)) {
+    const trees = {}, loaded = [], serr = {}, tailErrors = {}, loadErrors = {};
+    for (const [d, cut, loadLong] of JSON.parse(fs.readFileSync(spath))) {
+        try {
+            const r = await snapshotDoc(d, cut, loadLong);
+            trees[d] = r.tree;
+            loaded.push(r.loaded);
+            if (r.tailError) tailErrors[d] = r.tailError;
+            if (r.loadError) loadErrors[d] = r.loadError;
+        } catch (e) {
+            serr[d] = String(e && e.stack || e);
+            loaded.push(Buffer.alloc(0));
+        }
+    }
+    const off = Buffer.alloc(8 * (loaded.length + 1));
+    let acc = 0;
+    loaded.forEach((b, i) => { off.writeBigInt64LE(BigInt(acc), 8 * i); acc += b.length; });
+    off.writeBigInt64LE(BigInt(acc), 8 * loaded.length);
+    fs.writeFileSync(path.join(dir, "ref_loaded_dumps.bin"), Buffer.concat(loaded));
+    fs.writeFileSync(path.join(dir, "ref_loaded_off.bin"), off);
+    fs.writeFileSync(path.join(dir, "ref_snapshots.json"), JSON.stringify({ trees, errors: serr, tailErrors, loadErrors }));
+}
 if (!timeOnly) {
     const off = Buffer.alloc(8 * (ndocs + 1));
     let acc = 0;
