@@ -88,7 +88,7 @@ def cpu_baseline(batch, gpu_digests, workers: int, target_s: float = 15.0):
         ns = int(min(nd, max(probe, probe * target_s / secs)))
         sample = batch.subset(range(ns))
         secs, odig, oerr = oc.replay_batch(sample, threads=workers)
-    s_seq = int(((sample.ops["kind"] & 0x80) == 0).sum())
+    s_seq = int(((sample.ops["kind"] & 0xC0) == 0).sum())  # sequenced messages (a group counts once)
     match = bool((odig == gpu_digests[:ns]).all()) and bool((oerr == 0).all())
     calib = None
     cpath = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")

@@ -43,8 +43,8 @@ enum : int32_t {
     NONE = INT32_MIN,
     MAXN = 8,          /* MaxNodesInBlock (mergeTree.ts:333) */
     GRANULARITY = 256, /* TextSegmentGranularity (mergeTree.ts:1093) */
-    NKEYS = 8,         /* property key slots per document */
-    NOVL = 8,          /* removedClientOverlap entries per row */
+    NOVL = 8,          /* removedClientOverlap entries per row held inline; more go to the overflow pool */
+    OVB = 64,          /* overflow blocks per document (8 overlap entries each) */
 };
 enum : uint8_t { LOCAL_CLIENT = 0xFF }; /* short id of LocalClientId (-1) */
 
@@ -90,27 +90,32 @@ struct DocHdr {
     int32_t localLen;      /* root.cachedLength: Client.getLength() (client.ts:1051) */
     int32_t heapTop;       /* maxSeq of the heap's root (valid when heapN > 0) */
     int32_t loadPos;       /* snapshot load: the next position of the open loadBody batch (mt_oplog.h) */
+    int32_t ovTop, ovFree; /* overlap overflow pool: next never-used block, free-list head (0 = none) */
     int32_t _r2;
     int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
 };
-/* every int32 field of DocHdr (the replica keeps them in registers while it runs) */
+/* the int32 fields of DocHdr the replica keeps in registers while it runs; the rarely used ones
+ * (nclients, nextSid, errOp, nkeys, hwSlots, gcEpoch, loadPos, ovTop, ovFree) stay in the image
+ * and are read and written there (z.h), which keeps the replay loop's scalar registers for the
+ * fields every event touches */
 #define MT_HDR_FIELDS(X)                                                                          \
     X(root) X(nleaf) X(freeHead) X(nfree) X(currentSeq) X(minSeq) X(localSeq) X(collaborating)   \
-    X(localShort) X(localLong) X(nclients) X(nextSid) X(heapN) X(memN) X(gqHead) X(gqN)          \
-    X(arenaTop) X(arenaSide) X(err) X(errOp) X(nkeys) X(opsDone) X(hwSlots) X(hwHeap) X(nrows)   \
-    X(seqOps) X(nfreeRid) X(gcEpoch) X(localLen) X(heapTop) X(loadPos)
+    X(localShort) X(localLong) X(heapN) X(memN) X(gqHead) X(gqN) X(arenaTop) X(arenaSide) X(err) \
+    X(opsDone) X(hwHeap) X(nrows) X(seqOps) X(nfreeRid) X(localLen) X(heapTop)
 
-/* Cold per-row data, indexed by a row id that does not move when the row's slot moves. */
-struct ColdRow {
+/* Cold per-row data, indexed by a row id that does not move when the row's slot moves. K = the
+ * profile's property key slots per document. */
+template <int K>
+struct ColdRowT {
     int32_t lseq, lrseq;
     uint32_t toff; /* text offset in the arena; a marker's refType */
     uint8_t prw;   /* pendingRewriteCount */
     uint8_t gc;    /* arena-GC epoch that last moved this row's text (0 = never) */
-    uint8_t _p[2];
-    uint64_t ovl;          /* removedClientOverlap: up to 8 short ids (+1), push order */
-    uint16_t pv[NKEYS];    /* property values per doc key slot (0 = absent) */
-    uint8_t pk[NKEYS];     /* pendingKeyUpdateCount per key slot */
+    uint16_t ovx;  /* first overflow block of removedClientOverlap past the inline 8 (0 = none) */
+    uint64_t ovl;  /* removedClientOverlap: the first 8 short ids (+1), push order */
+    uint16_t pv[K]; /* property values per doc key slot (0 = absent) */
+    uint8_t pk[K];  /* pendingKeyUpdateCount per key slot */
 };
 
 /* Position index of the large-document profile ("tiled", config 4: >100k live rows).
@@ -156,8 +161,10 @@ enum : uint8_t { XF_STABLE = 1, XF_W = 2 };
 
 /* Hot per-document state with compile-time capacities: everything the per-op scans and the
  * tree skeleton touch. */
-template <int N_, int C_ = 256, bool TILED_ = false>
+template <int N_, int C_ = 256, bool TILED_ = false, int K_ = 8>
 struct HotT {
+    static constexpr int K = K_;     /* property key slots per document */
+    typedef ColdRowT<K_> Cold;
     static constexpr int N = N_;     /* B-tree nodes */
     static constexpr int S = N_ * 8; /* row slots (8 per leaf node) */
     static constexpr int H = N_ + 64; /* zamboni heap entries (config 3 peaks at 109) */
@@ -195,7 +202,10 @@ struct HotT {
     uint8_t hgen[H];  /* its row-id generation when queued: a mismatch means it was unlinked */
     uint16_t s2l[C];  /* short client id -> long id (client.ts:637-661) */
     uint8_t l2s[C];   /* long id (< C) -> short id, 0xFF = not seen yet */
-    uint16_t keys[NKEYS]; /* property key id of each doc key slot */
+    uint16_t keys[K_]; /* property key id of each doc key slot */
+    uint16_t ovn[OVB];  /* overlap overflow pool: next block of a chain (0 = end) / of the free list */
+    int8_t _pad2[(16 - (2 * K_ + 2 * OVB) % 16) % 16];
+    uint64_t ovp[OVB];  /* 8 more removedClientOverlap entries (short id + 1) per block */
     TileState<N_, TILED_> tl;
 };
 
@@ -204,9 +214,9 @@ struct HotT {
  * global-memory profiles. */
 typedef HotT<192> HotSmall;
 typedef HotT<640> HotMat; /* config 5: PermutationVector replicas peak at ~540 nodes */
-typedef HotT<2048> HotMid;
-typedef HotT<16384> HotBig;
-typedef HotT<(1 << 18), 256, true> HotHuge; /* config 4: tiled position index, 32-bit ids (1M-op docs: ~112k nodes) */
+typedef HotT<2048, 256, false, 24> HotMid; /* the larger profiles hold 24 property keys per document */
+typedef HotT<16384, 256, false, 24> HotBig;
+typedef HotT<(1 << 18), 256, true, 24> HotHuge; /* config 4: tiled position index, 32-bit ids (1M-op docs: ~112k nodes) */
 
 struct alignas(16) I4 {
     int32_t x[4];
@@ -228,17 +238,31 @@ MT_HD B4 ldb4(const uint8_t* p) { /* p 4-byte aligned */
     return v;
 }
 
-/* Per-document view: the hot image (LDS or global) plus global cold/arena/log pointers. */
+MT_HD constexpr int64_t align256c(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+/* Per-document view: the hot image (LDS or global) plus the document's global block. The block is
+ * [hot image | cold rows | free row-id stack | text arena (2 halves) | membership log gid | rid |
+ * pending-group ring]; the first three offsets are compile-time constants of the profile and the
+ * rest follow from the caps, so a replica keeps one block pointer (and the caps) in registers
+ * instead of one pointer per region. */
 template <class HT>
 struct Doc {
-    HT* t;
-    ColdRow* cold; /* HT::S records */
-    typename HT::IX* frid; /* free cold-row-id stack, HT::S entries */
-    uint16_t* arena; /* 2 * acap */
-    int32_t* mgid;
-    int32_t* mrid; /* row id of each membership entry */
-    int32_t* gq;
+    HT* t;      /* hot image: the block itself, or its LDS copy */
+    uint8_t* b; /* the document's global block */
     Caps caps;
+    static constexpr int64_t OFF_COLD = align256c((int64_t)sizeof(HT));
+    static constexpr int64_t OFF_FRID = align256c(OFF_COLD + (int64_t)sizeof(typename HT::Cold) * HT::S);
+    static constexpr int64_t OFF_ARENA = align256c(OFF_FRID + (int64_t)sizeof(typename HT::IX) * HT::S);
+    MT_HD static int64_t off_mgid(const Caps& c) { return OFF_ARENA + align256c(4 * (int64_t)c.acap); }
+    MT_HD static int64_t off_mrid(const Caps& c) { return off_mgid(c) + align256c(4 * (int64_t)c.mcap); }
+    MT_HD static int64_t off_gq(const Caps& c) { return off_mrid(c) + align256c(4 * (int64_t)c.mcap); }
+    MT_HD static int64_t stride(const Caps& c) { return off_gq(c) + align256c(4 * (int64_t)c.gcap); }
+    MT_HD typename HT::Cold* cold() const { return (typename HT::Cold*)(b + OFF_COLD); } /* HT::S records */
+    MT_HD typename HT::IX* frid() const { return (typename HT::IX*)(b + OFF_FRID); } /* free row-id stack */
+    MT_HD uint16_t* arena() const { return (uint16_t*)(b + OFF_ARENA); } /* 2 * acap */
+    MT_HD int32_t* mgid() const { return (int32_t*)(b + off_mgid(caps)); }
+    MT_HD int32_t* mrid() const { return (int32_t*)(b + off_mrid(caps)); } /* row id of each membership entry */
+    MT_HD int32_t* gq() const { return (int32_t*)(b + off_gq(caps)); }
 };
 
 /* Op pools of one document. */
@@ -333,12 +357,12 @@ struct Replica {
         w.sync();
     }
 
-    MT_HD ColdRow& cold(int32_t s) const { return d.cold[z.rid[s]]; }
+    MT_HD typename HT::Cold& cold(int32_t s) const { return d.cold()[z.rid[s]]; }
 
     MT_HD void fail(int32_t e) {
         if (h.err == E_OK) {
             h.err = e;
-            h.errOp = h.opsDone;
+            z.h.errOp = h.opsDone;
         }
     }
 
@@ -391,7 +415,7 @@ struct Replica {
         for (int32_t b = 0; b < HT::S; b += W::N) {
             int32_t i = b + w.lane();
             if (i < HT::S) {
-                d.frid[i] = (IX)(HT::S - 1 - i);
+                d.frid()[i] = (IX)(HT::S - 1 - i);
                 z.rgen[i] = 0;
                 z.len(i) = 0;
                 z.seq(i) = 0;
@@ -407,7 +431,7 @@ struct Replica {
         w.sync();
         if constexpr (TILED) rope_init();
         h.nfreeRid = HT::S;
-        h.gcEpoch = 0;
+        z.h.gcEpoch = 0;
         h.freeHead = 1;
         h.nfree = ncap - 1;
         h.root = 0;
@@ -421,8 +445,8 @@ struct Replica {
         h.collaborating = 0;
         h.localShort = -1; /* collabWindow.clientId = LocalClientId */
         h.localLong = -1;
-        h.nclients = 0;
-        h.nextSid = 1;
+        z.h.nclients = 0;
+        z.h.nextSid = 1;
         h.heapN = 0;
         h.memN = 0;
         h.gqHead = 0;
@@ -430,10 +454,10 @@ struct Replica {
         h.arenaTop = 0;
         h.arenaSide = 0;
         h.err = 0;
-        h.errOp = -1;
-        h.nkeys = 0;
+        z.h.errOp = -1;
+        z.h.nkeys = 0;
         h.opsDone = 0;
-        h.hwSlots = 0;
+        z.h.hwSlots = 0;
         h.hwHeap = 0;
         h.nrows = 0;
         h.seqOps = 0;
@@ -441,7 +465,9 @@ struct Replica {
         h.sumW = 0;
         h.localLen = 0;
         h.heapTop = 0;
-        h.loadPos = h._r2 = 0;
+        z.h.loadPos = h._r2 = 0;
+        z.h.ovTop = 1; /* block 0 is the null link */
+        z.h.ovFree = 0;
         for (int32_t b = 0; b < HT::C; b += W::N) {
             int32_t i = b + w.lane();
             if (i < HT::C) z.l2s[i] = 0xFF;
@@ -455,21 +481,21 @@ struct Replica {
             int32_t s = z.l2s[longId];
             return s == 0xFF ? -1 : s;
         }
-        for (int32_t i = 0; i < h.nclients; i++)
+        for (int32_t i = 0; i < z.h.nclients; i++)
             if (z.s2l[i] == longId) return i;
         return -1;
     }
     MT_HD int32_t get_or_add_short(int32_t longId) {
         int32_t s = short_of(longId);
         if (s >= 0) return s;
-        int32_t n = h.nclients;
+        int32_t n = z.h.nclients;
         if (n >= HT::C || n >= 0xFE) {
             fail(E_CAPACITY);
             return 0;
         }
         z.s2l[n] = (uint16_t)longId;
         if ((uint32_t)longId < (uint32_t)HT::C) z.l2s[longId] = (uint8_t)n;
-        h.nclients = n + 1;
+        z.h.nclients = n + 1;
         return n;
     }
     /* startOrUpdateCollaboration (client.ts:1053-1073) + startCollaboration (mergeTree.ts:1287) */
@@ -497,14 +523,7 @@ struct Replica {
         if (rs != NOREM) {
             int32_t rc = z.rcli(s) == LOCAL_CLIENT ? -1 : z.rcli(s);
             if (rc == client) return 0;
-            if (z.flags(s) & RF_OVL) { /* cold read only for the rare overlapping remove */
-                uint64_t ov = cold(s).ovl;
-                for (int k = 0; k < NOVL; k++) {
-                    uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
-                    if (e == 0) break;
-                    if ((int32_t)e - 1 == client) return 0;
-                }
-            }
+            if ((z.flags(s) & RF_OVL) && ovl_has(s, client)) return 0; /* cold read: rare */
             if (rs != UNASSIGNED_SEQ && rs <= refSeq) return 0;
         }
         return L;
@@ -641,11 +660,11 @@ struct Replica {
             return 0;
         }
         h.nfreeRid = n - 1;
-        return d.frid[n - 1];
+        return d.frid()[n - 1];
     }
     MT_HD void free_rid(int32_t r) {
         z.rgen[r]++;
-        d.frid[h.nfreeRid++] = (IX)r;
+        d.frid()[h.nfreeRid++] = (IX)r;
     }
     /* record leaf n as the holder of its first `cnt` rows */
     MT_HD void set_leaf_of_rows(int32_t n, int32_t cnt) {
@@ -1084,14 +1103,119 @@ struct Replica {
         if (k >= h.nleaf) return -1;
         return lo[k] * MAXN + (t0 & 4);
     }
+    /* ---- removedClientOverlap: 8 entries inline in the cold row, then chains of 8-entry blocks
+     * in a per-document pool (entries are short id + 1; 0 ends a list) ------------------------ */
     MT_HD bool ovl_has(int32_t s, int32_t client) const {
         uint64_t ov = cold(s).ovl;
-        for (int k = 0; k < NOVL; k++) {
-            uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
-            if (e == 0) break;
-            if ((int32_t)e - 1 == client) return true;
+        for (int32_t b = cold(s).ovx;; b = z.ovn[b]) {
+            for (int k = 0; k < NOVL; k++) {
+                uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
+                if (e == 0) return false;
+                if ((int32_t)e - 1 == client) return true;
+            }
+            if (!b) return false;
+            ov = z.ovp[b];
         }
-        return false;
+    }
+    /* the k-th entry (short id) of row s's overlap list; -1 past its end */
+    MT_HD int32_t ovl_at(int32_t s, int32_t k) const {
+        uint64_t ov = cold(s).ovl;
+        int32_t b = cold(s).ovx;
+        while (k >= NOVL) {
+            if (!b) return -1;
+            ov = z.ovp[b];
+            b = z.ovn[b];
+            k -= NOVL;
+        }
+        uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
+        return e ? (int32_t)e - 1 : -1;
+    }
+    MT_HD int32_t ovl_count(int32_t s) const {
+        int32_t n = 0;
+        while (ovl_at(s, n) >= 0) n++;
+        return n;
+    }
+    /* removedClientOverlap.push(client) */
+    MT_HD void ovl_push(int32_t s, int32_t client) {
+        uint64_t e = (uint64_t)(client + 1);
+        int32_t k = 0;
+        uint64_t ov = cold(s).ovl;
+        while (k < NOVL && ((ov >> (8 * k)) & 0xFF)) k++;
+        if (k < NOVL) {
+            cold(s).ovl = ov | (e << (8 * k));
+            return;
+        }
+        int32_t b = cold(s).ovx, last = 0;
+        while (b) {
+            last = b;
+            b = z.ovn[b];
+        }
+        if (last) {
+            ov = z.ovp[last];
+            for (k = 0; k < NOVL && ((ov >> (8 * k)) & 0xFF); k++) {
+            }
+            if (k < NOVL) {
+                z.ovp[last] = ov | (e << (8 * k));
+                return;
+            }
+        }
+        int32_t nb = ovb_alloc();
+        if (!nb) return;
+        z.ovp[nb] = e;
+        if (last)
+            z.ovn[last] = (uint16_t)nb;
+        else
+            cold(s).ovx = (uint16_t)nb;
+    }
+    /* a split's right part gets its own copy of the left part's overflow chain */
+    MT_HD void ovl_clone(int32_t rs, int32_t ls) {
+        cold(rs).ovx = 0;
+        int32_t prev = 0;
+        for (int32_t src = cold(ls).ovx; src; src = z.ovn[src]) {
+            int32_t nb = ovb_alloc(); /* a sweep here keeps both chains: rs holds what is linked */
+            if (!nb) return;
+            z.ovp[nb] = z.ovp[src];
+            if (prev)
+                z.ovn[prev] = (uint16_t)nb;
+            else
+                cold(rs).ovx = (uint16_t)nb;
+            prev = nb;
+        }
+    }
+    MT_HD int32_t ovb_alloc() {
+        if (!z.h.ovFree && z.h.ovTop >= OVB) ovb_sweep();
+        int32_t b;
+        if (z.h.ovFree) {
+            b = z.h.ovFree;
+            z.h.ovFree = z.ovn[b];
+        } else if (z.h.ovTop < OVB) {
+            b = z.h.ovTop++;
+        } else {
+            fail(E_CAPACITY);
+            return 0;
+        }
+        z.ovn[b] = 0;
+        z.ovp[b] = 0;
+        return b;
+    }
+    /* blocks no live row's chain reaches (their rows were unlinked or their ids reused) return to
+     * the free list */
+    MT_HD void ovb_sweep() {
+        uint64_t used = 1;
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+            int32_t n = leaf_at(k), c = nch[n];
+            for (int32_t j = 0; j < c; j++) {
+                int32_t s = n * MAXN + j;
+                if (z.flags(s) & RF_OVL)
+                    for (int32_t b = cold(s).ovx; b; b = z.ovn[b]) used |= 1ull << b;
+            }
+        }
+        z.h.ovFree = 0;
+        for (int32_t b = OVB - 1; b >= 1; b--)
+            if (!((used >> b) & 1)) {
+                z.ovn[b] = (uint16_t)z.h.ovFree;
+                z.h.ovFree = b;
+            }
     }
     /* nodeLength (mergeTree.ts:1692-1732) of the 4 slots from s0 under (refSeq, client); 0 for
      * empty slots */
@@ -1191,6 +1315,7 @@ struct Replica {
         if constexpr (TILED) {
             rope_insert_after(after, nl);
             h.nleaf++;
+            note_leaves();
             return;
         }
         int32_t k = lp[after] + 1;
@@ -1199,6 +1324,7 @@ struct Replica {
         lo[k] = (IX)nl;
         lp[nl] = (IX)k;
         h.nleaf = n + 1;
+        note_leaves();
     }
     /* split (mergeTree.ts:2509-2522) of a full node (8 children) into 4 + 4; the new node is
      * inserted after it in its parent, recursively; root split -> updateRoot (1909-1920).
@@ -1265,7 +1391,7 @@ struct Replica {
     }
 
     /* ---- text arena -------------------------------------------------------------------- */
-    MT_HD uint16_t* arena_base(int32_t side) { return d.arena + (int64_t)side * d.caps.acap; }
+    MT_HD uint16_t* arena_base(int32_t side) { return d.arena() + (int64_t)side * d.caps.acap; }
     /* reserve n units at the arena top; compacts into the other half when full */
     MT_HD int32_t arena_alloc(int32_t n) {
         if (h.arenaTop + n > d.caps.acap) {
@@ -1298,8 +1424,8 @@ struct Replica {
         int32_t from = h.arenaSide, to = from ^ 1;
         uint16_t* src = arena_base(from);
         uint16_t* dst = arena_base(to);
-        int32_t ep = h.gcEpoch % 255 + 1;
-        h.gcEpoch = ep;
+        int32_t ep = z.h.gcEpoch % 255 + 1;
+        z.h.gcEpoch = ep;
         int32_t top = 0;
         for (int32_t k = 0; kvalid(k); k = knext(k)) {
             int32_t n = leaf_at(k), c = nch[n];
@@ -1337,6 +1463,7 @@ struct Replica {
         z.rid[rs] = (IX)alloc_rid();
         z.rleaf[z.rid[rs]] = (IX)(rs / MAXN);
         cold(rs) = cold(ls); /* splitAt copies every field (mergeTree.ts:523-567) */
+        if (cold(ls).ovx) ovl_clone(rs, ls);
         z.len(rs) = z.len(ls) - off;
         cold(rs).toff = cold(ls).toff + (uint32_t)off;
         z.len(ls) = off;
@@ -1355,14 +1482,14 @@ struct Replica {
          * group's segment list */
         if (z.ng(ls)) {
             if (h.memN + z.ng(ls) > d.caps.mcap) mem_compact();
-            int32_t head = h.gqN ? d.gq[h.gqHead % d.caps.gcap] : 0x7fffffff;
+            int32_t head = h.gqN ? d.gq()[h.gqHead % d.caps.gcap] : 0x7fffffff;
             int32_t lrid = z.rid[ls];
             int32_t rrid = z.rid[rs];
             int32_t m0 = h.memN;
             for (int32_t b = 0; b < m0; b += W::N) {
                 int32_t i = b + w.lane();
-                int32_t g = i < m0 ? d.mgid[i] : -1;
-                uint64_t m = w.ballot(i < m0 && d.mrid[i] == lrid && g >= head);
+                int32_t g = i < m0 ? d.mgid()[i] : -1;
+                uint64_t m = w.ballot(i < m0 && d.mrid()[i] == lrid && g >= head);
                 while (m) {
                     int32_t l = W::ffs(m);
                     m &= m - 1;
@@ -1385,25 +1512,25 @@ struct Replica {
                 return;
             }
         }
-        d.mgid[m] = gid;
-        d.mrid[m] = rid;
+        d.mgid()[m] = gid;
+        d.mrid()[m] = rid;
         h.memN = m + 1;
     }
     /* drop entries of groups already acked (gid < head gid): wave stream compaction */
     MT_HD void mem_compact() {
-        int32_t head = h.gqN ? d.gq[h.gqHead % d.caps.gcap] : 0x7fffffff;
+        int32_t head = h.gqN ? d.gq()[h.gqHead % d.caps.gcap] : 0x7fffffff;
         int32_t n = h.memN, wpos = 0;
         for (int32_t b = 0; b < n; b += W::N) {
             int32_t i = b + w.lane();
-            int32_t g = i < n ? d.mgid[i] : -1;
-            int32_t sd = i < n ? d.mrid[i] : 0;
+            int32_t g = i < n ? d.mgid()[i] : -1;
+            int32_t sd = i < n ? d.mrid()[i] : 0;
             bool keep = i < n && g >= head;
             int32_t tot;
             int32_t off = w.excl_scan(keep ? 1 : 0, &tot);
             w.sync();
             if (keep) {
-                d.mgid[wpos + off] = g;
-                d.mrid[wpos + off] = sd;
+                d.mgid()[wpos + off] = g;
+                d.mrid()[wpos + off] = sd;
             }
             w.sync();
             wpos += tot;
@@ -1427,7 +1554,7 @@ struct Replica {
                 fail(E_CAPACITY);
                 return;
             }
-            d.gq[(h.gqHead + h.gqN) % d.caps.gcap] = gid;
+            d.gq()[(h.gqHead + h.gqN) % d.caps.gcap] = gid;
             h.gqN++;
             *created = true;
         }
@@ -1602,20 +1729,20 @@ struct Replica {
 
     /* ---- properties (segmentPropertiesManager.ts:35-111) ---------------------------- */
     MT_HD int32_t key_slot(uint16_t key) {
-        for (int32_t i = 0; i < h.nkeys; i++)
+        for (int32_t i = 0; i < z.h.nkeys; i++)
             if (z.keys[i] == key) return i;
-        if (h.nkeys >= NKEYS) {
+        if (z.h.nkeys >= HT::K) {
             fail(E_UNSUPPORTED);
             return -1;
         }
-        z.keys[h.nkeys] = key;
-        return h.nkeys++;
+        z.keys[z.h.nkeys] = key;
+        return z.h.nkeys++;
     }
     MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
         if (!(z.flags(s) & RF_PROPS)) {
             cold(s).prw = 0;
             z.flags(s) |= RF_PROPS;
-            for (int k = 0; k < NKEYS; k++) {
+            for (int k = 0; k < HT::K; k++) {
                 cold(s).pv[k] = 0;
                 cold(s).pk[k] = 0;
             }
@@ -1623,7 +1750,7 @@ struct Replica {
         if (cold(s).prw > 0 && seq != UNASSIGNED_SEQ && collaborating) return;
         if (rewrite) {
             if (collaborating && seq == UNASSIGNED_SEQ) cold(s).prw++;
-            for (int32_t k = 0; k < h.nkeys; k++) {
+            for (int32_t k = 0; k < z.h.nkeys; k++) {
                 if (cold(s).pv[k] == 0) continue;
                 bool inNew = false;
                 for (int32_t j = 0; j < nkv; j++)
@@ -1663,7 +1790,7 @@ struct Replica {
         bool pa = z.flags(a) & RF_PROPS, pb = z.flags(b) & RF_PROPS;
         if (pa != pb) return false;
         if (!pa) return true;
-        for (int k = 0; k < NKEYS; k++)
+        for (int k = 0; k < HT::K; k++)
             if (cold(a).pv[k] != cold(b).pv[k]) return false;
         return true;
     }
@@ -1868,7 +1995,7 @@ struct Replica {
         if ((drop >> q) & 1) {
             int32_t pos = h.nfreeRid + __builtin_popcountll(drop & below);
             z.rgen[r.rid]++;
-            d.frid[pos] = (IX)r.rid;
+            d.frid()[pos] = (IX)r.rid;
         }
         int32_t ndrop = __builtin_popcountll(drop);
         h.nfreeRid += ndrop;
@@ -1997,6 +2124,7 @@ struct Replica {
                 }
             }
             h.nleaf = nl + delta;
+            if (delta > 0) note_leaves();
             for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (IX)newk[i];
             nch[parent] = (int8_t)cc;
         } else {
@@ -2252,6 +2380,7 @@ struct Replica {
             z.ng(s) = 0;
             cold(s).prw = 0;
             cold(s).ovl = 0;
+            cold(s).ovx = 0;
             z.rleaf[z.rid[s]] = (IX)(s / MAXN);
             h.nrows++;
             h.sumW++;
@@ -2273,7 +2402,7 @@ struct Replica {
             }
             z.flags(s) = (uint8_t)fl;
             if constexpr (TILED) row_enter(s);
-            for (int k = 0; k < NKEYS; k++) {
+            for (int k = 0; k < HT::K; k++) {
                 cold(s).pv[k] = 0;
                 cold(s).pk[k] = 0;
             }
@@ -2483,15 +2612,8 @@ struct Replica {
                     z.rseq(s) = seq;
                     z.flags(s) &= (uint8_t)~RF_LRSEQ;
                 } else {
-                    uint64_t ov = cold(s).ovl;
-                    int k = 0;
-                    while (k < NOVL && ((ov >> (8 * k)) & 0xFF)) k++;
-                    if (k >= NOVL) {
-                        fail(E_UNSUPPORTED);
-                    } else {
-                        cold(s).ovl = ov | ((uint64_t)(client + 1) << (8 * k));
-                        z.flags(s) |= RF_OVL;
-                    }
+                    ovl_push(s, client);
+                    z.flags(s) |= RF_OVL;
                 }
             } else {
                 h.localLen -= z.len(s); /* the row leaves the local view */
@@ -2535,14 +2657,14 @@ struct Replica {
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
         if (h.gqN > 0) {
             MT_PROF_SCOPE(PH_ACK);
-            int32_t gid = d.gq[h.gqHead % d.caps.gcap];
+            int32_t gid = d.gq()[h.gqHead % d.caps.gcap];
             h.gqHead = (h.gqHead + 1) % d.caps.gcap;
             h.gqN--;
             int32_t mn = h.memN;
             for (int32_t b = 0; b < mn; b += W::N) {
                 int32_t i = b + w.lane();
-                int32_t rd = i < mn ? d.mrid[i] : 0;
-                uint64_t msk = w.ballot(i < mn && d.mgid[i] == gid);
+                int32_t rd = i < mn ? d.mrid()[i] : 0;
+                uint64_t msk = w.ballot(i < mn && d.mgid()[i] == gid);
                 while (msk) {
                     int32_t l = W::ffs(msk);
                     msk &= msk - 1;
@@ -2655,8 +2777,10 @@ struct Replica {
         if (!(op.min_seq <= op.seq)) fail(E_ASSERT);
         set_min_seq(op.min_seq);
         h.opsDone++;
-        int32_t slots = h.nleaf * MAXN;
-        if (slots > h.hwSlots) h.hwSlots = slots;
+    }
+    /* high-water mark of row slots in use (stats), noted whenever the leaf count grows */
+    MT_HD void note_leaves() {
+        if (h.nleaf * MAXN > z.h.hwSlots) z.h.hwSlots = h.nleaf * MAXN;
     }
     /* ---- snapshot load (SnapshotLoader, snapshotLoader.ts:86-228; records in mt_oplog.h) ------- */
     /* the fields of a loaded segment (SnapshotLoader.specToSegment, snapshotLoader.ts:96-126) on an
@@ -2746,6 +2870,7 @@ struct Replica {
         cold(s).lrseq = 0;
         cold(s).prw = 0;
         cold(s).ovl = 0;
+        cold(s).ovx = 0;
         z.rleaf[z.rid[s]] = (IX)(s / MAXN);
         int32_t fl = (marker ? RF_MARKER : 0) | (perm ? RF_PERM : 0);
         if (marker) {
@@ -2758,7 +2883,7 @@ struct Replica {
             fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
         }
         z.flags(s) = (uint8_t)fl;
-        for (int k = 0; k < NKEYS; k++) {
+        for (int k = 0; k < HT::K; k++) {
             cold(s).pv[k] = 0;
             cold(s).pk[k] = 0;
         }
@@ -2783,8 +2908,8 @@ struct Replica {
              * length; its later members (GROUPED) go at the previous position + the previous
              * segment's whole length, removed or not */
             mt_op_rec ins = op;
-            ins.pos1 = (op.kind & MT_OPF_GROUPED) ? h.loadPos : h.localLen;
-            h.loadPos = ins.pos1 + seg_len(op);
+            ins.pos1 = (op.kind & MT_OPF_GROUPED) ? z.h.loadPos : h.localLen;
+            z.h.loadPos = ins.pos1 + seg_len(op);
             int32_t cl = loader_client(op.client);
             int32_t rc = op.ref_seq > 0 ? loader_client((uint16_t)op.min_seq) : 0;
             if (h.err) return;
@@ -2913,11 +3038,10 @@ struct Replica {
             int32_t s = lfn * MAXN + jj;
             uint8_t fl = z.flags(s);
             bool rem = z.rseq(s) != NOREM;
-            int nov = 0;
-            while (nov < NOVL && ((cold(s).ovl >> (8 * nov)) & 0xFF)) nov++;
+            int nov = ovl_count(s);
             int np = 0;
             if (fl & RF_PROPS)
-                for (int k = 0; k < NKEYS; k++)
+                for (int k = 0; k < HT::K; k++)
                     if (cold(s).pv[k]) np++;
             uint8_t b4[4] = {(uint8_t)((fl & RF_MARKER) ? MT_SEG_MARKER : (fl & RF_PERM) ? MT_SEG_PERM : MT_SEG_TEXT),
                              (uint8_t)(((fl & RF_PROPS) ? MT_DF_HAS_PROPS : 0) | (rem ? MT_DF_REMOVED : 0) |
@@ -2934,7 +3058,7 @@ struct Replica {
                             ordinal};
             put_bytes(o, f, sizeof(f));
             for (int k = 0; k < nov; k++) {
-                int32_t lo = long_of((uint8_t)(((cold(s).ovl >> (8 * k)) & 0xFF) - 1));
+                int32_t lo = long_of((uint8_t)ovl_at(s, k));
                 put_bytes(o, &lo, 4);
             }
             uint16_t h2[2] = {(uint16_t)np, (uint16_t)((fl & RF_MARKER) ? cold(s).toff : 0)};
@@ -2943,7 +3067,7 @@ struct Replica {
             int32_t last = -1;
             for (int q = 0; q < np; q++) {
                 int32_t best = -1, bk = 0x7fffffff;
-                for (int k = 0; k < NKEYS; k++) {
+                for (int k = 0; k < HT::K; k++) {
                     int32_t key = z.keys[k];
                     if (cold(s).pv[k] && key > last && key < bk) {
                         bk = key;

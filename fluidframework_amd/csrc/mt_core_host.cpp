@@ -116,7 +116,7 @@ int32_t mth_error(mth_store* s, int64_t doc) {
     return with_replica(s, doc, [](auto& r) { return r.h.err; });
 }
 int32_t mth_error_op(mth_store* s, int64_t doc) {
-    return with_replica(s, doc, [](auto& r) { return r.h.errOp; });
+    return with_replica(s, doc, [](auto& r) { return r.z.h.errOp; });
 }
 
 int32_t mth_length(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client) {
@@ -179,7 +179,7 @@ void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {
     with_replica(s, doc, [&](auto& r) {
         DocHdr* h = &r.h;
         out8[0] = h->nleaf;
-        out8[1] = h->hwSlots;
+        out8[1] = r.z.h.hwSlots;
         out8[2] = h->hwHeap;
         out8[3] = h->heapN;
         out8[4] = h->memN;

@@ -358,6 +358,9 @@ struct mt_engine {
 /* call f(store) for the engine's profile */
 template <class F>
 static int32_t with_store(mt_engine* e, F&& f) {
+#ifdef MT_ISA_SMALL /* analysis builds (tools/isa_small.sh): the config-3 profile's kernels only */
+    return f(e->s0);
+#endif
     if (e->profile == 0) return f(e->s0);
     if (e->profile == 1) return f(e->s1);
     if (e->profile == 3) return f(e->s3);
@@ -591,6 +594,9 @@ int32_t mt_engine_run(mt_engine* e) {
              * hides more of it than full LDS residency (4 documents per CU) saves. With the leaf-line
              * layout 7 beats 6 and 8 (174 / 161 / 168 Mops/s at 32k docs; 8 spills registers;
              * tools/gpu_occupancy.sh). MT_REPLAY_LDS=1 selects the fully LDS-staged form. */
+#ifdef MT_ISA_SMALL
+            launch(k_replay<HT, false, 7>);
+#else
             if (e->lds)
                 launch(k_replay<HT, true>);
             else if (e->waves == 8)
@@ -599,6 +605,7 @@ int32_t mt_engine_run(mt_engine* e) {
                 launch(k_replay<HT, false, 6>);
             else
                 launch(k_replay<HT, false, 7>);
+#endif
         } else if constexpr (std::is_same_v<HT, HotMat>) {
             /* Default (MT_REPLAY_MAT_SKEL=2): only SkelLite (4.5 KB) in LDS, 7 waves per SIMD
              * (116 Mops/s at 16k replicas). =1 stages the whole Skel (10.7 KB), which caps residency

@@ -19,20 +19,13 @@ template <class HT>
 struct Store {
     typedef HT Hot;
     uint8_t* base;
-    int64_t stride; /* bytes per document */
-    int64_t offCold, offFrid, offArena, offMgid, offMrid, offGq;
+    int64_t stride; /* bytes per document (Doc<HT>::stride) */
     Caps caps;
 
     MT_HD Doc<HT> doc(int64_t d) const {
-        uint8_t* b = base + d * stride;
         Doc<HT> v;
-        v.t = (HT*)b;
-        v.cold = (ColdRow*)(b + offCold);
-        v.frid = (typename HT::IX*)(b + offFrid);
-        v.arena = (uint16_t*)(b + offArena);
-        v.mgid = (int32_t*)(b + offMgid);
-        v.mrid = (int32_t*)(b + offMrid);
-        v.gq = (int32_t*)(b + offGq);
+        v.b = base + d * stride;
+        v.t = (HT*)v.b;
         v.caps = caps;
         return v;
     }
@@ -47,26 +40,14 @@ inline uint8_t* host_store_alloc(int64_t bytes) {
     return (uint8_t*)p;
 }
 
-/* Fill offsets/stride for capacities `caps`; returns bytes for `ndocs` documents. */
+/* Fill the stride for capacities `caps` (the block layout is Doc<HT>'s); returns bytes for `ndocs`
+ * documents. */
 template <class HT>
 inline int64_t store_layout(Store<HT>& st, const Caps& caps, int64_t ndocs) {
-    int64_t o = align256((int64_t)sizeof(HT));
-    st.offCold = o;
-    o = align256(o + (int64_t)sizeof(ColdRow) * HT::S);
-    st.offFrid = o;
-    o = align256(o + (int64_t)sizeof(typename HT::IX) * HT::S);
-    st.offArena = o;
-    o = align256(o + 2 * 2 * (int64_t)caps.acap);
-    st.offMgid = o;
-    o = align256(o + 4 * (int64_t)caps.mcap);
-    st.offMrid = o;
-    o = align256(o + 4 * (int64_t)caps.mcap);
-    st.offGq = o;
-    o = align256(o + 4 * (int64_t)caps.gcap);
-    st.stride = o;
+    st.stride = Doc<HT>::stride(caps);
     st.caps = caps;
     st.base = nullptr;
-    return o * ndocs;
+    return st.stride * ndocs;
 }
 
 inline bool caps_valid(const Caps& k) { return k.acap >= 16 && k.mcap >= 4 && k.gcap >= 1; }
