@@ -227,12 +227,12 @@ struct alignas(4) B4 {
 /* 16-byte / 4-byte column reads. memcpy, not a pointer cast: the columns are members of the leaf
  * line struct, and an I4/B4-typed load of them would be "no alias" for type-based alias analysis,
  * letting the compiler move it above a store to the same slot. */
-MT_HD I4 ld4(const int32_t* p) { /* p 16-byte aligned */
+MT_HD inline I4 ld4(const int32_t* p) { /* p 16-byte aligned */
     I4 v;
     __builtin_memcpy(&v, __builtin_assume_aligned(p, 16), sizeof v);
     return v;
 }
-MT_HD B4 ldb4(const uint8_t* p) { /* p 4-byte aligned */
+MT_HD inline B4 ldb4(const uint8_t* p) { /* p 4-byte aligned */
     B4 v;
     __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), sizeof v);
     return v;

@@ -51,15 +51,38 @@ def hipcc() -> str:
     return os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
-def build_replay(force: bool = False) -> str:
-    """The product library: HIP kernels for gfx950 + the C ABI of include/mt_engine.h."""
-    out = lib_path("libmtreplay.so")
-    srcs = [os.path.join(CSRC, "mt_replay.hip")] + [os.path.join(CSRC, f) for f in CORE_HDRS] + [
+def replay_units() -> list:
+    """The library's translation units: the C ABI (mt_replay.hip) and one per profile / k_replay
+    variant, so they compile in parallel."""
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+
+
+def build_replay(force: bool = False, defines: tuple = (), name: str = "libmtreplay.so", jobs: int = 0) -> str:
+    """The product library: HIP kernels for gfx950 + the C ABI of include/mt_engine.h. Each unit
+    compiles to its own object (build/obj-<name>/), up to `jobs` at once, then one link."""
+    out = lib_path(name)
+    units = replay_units()
+    hdrs = [os.path.join(CSRC, f) for f in CORE_HDRS + ("mt_kernels.h",)] + [
         os.path.join(ROOT, "include", "mt_engine.h"), os.path.join(ROOT, "include", "mt_oplog.h")]
-    if force or _stale(out, srcs):
-        os.makedirs(BUILD, exist_ok=True)
-        subprocess.run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", out,
-                        srcs[0]], check=True)
+    objdir = os.path.join(BUILD, "obj-" + name.replace(".so", ""))
+    os.makedirs(objdir, exist_ok=True)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"] + ["-D" + d for d in defines]
+    todo = []
+    objs = []
+    for u in units:
+        o = os.path.join(objdir, os.path.basename(u).replace(".hip", ".o"))
+        objs.append(o)
+        if force or _stale(o, [u] + hdrs):
+            todo.append((u, o))
+    if todo:
+        import concurrent.futures as cf
+        n = jobs or max(1, min(len(todo), os.cpu_count() or 1, 16))
+        with cf.ThreadPoolExecutor(n) as ex:
+            futs = [ex.submit(subprocess.run, [hipcc()] + flags + ["-c", "-o", o, u], check=True) for u, o in todo]
+            for f in futs:
+                f.result()
+    if todo or _stale(out, objs):
+        subprocess.run([hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out] + objs, check=True)
     return out
 
 

@@ -14,9 +14,7 @@ LIB = native.lib_path("libmtreplay_prof.so")
 
 
 def build():
-    src = os.path.join(native.CSRC, "mt_replay.hip")
-    subprocess.run([native.hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMT_PROF",
-                    "-o", LIB, src], check=True)
+    native.build_replay(defines=("MT_PROF",), name="libmtreplay_prof.so")
 
 
 def main():
