@@ -27,7 +27,11 @@
 #include "../../include/mt_oplog.h"
 
 #ifdef __HIPCC__
+#ifdef MT_NO_FORCE_INLINE /* analysis builds: let the compiler choose what to inline */
+#define MT_HD __host__ __device__
+#else
 #define MT_HD __host__ __device__ __attribute__((always_inline))
+#endif
 #define MT_DEV __device__
 #else
 #define MT_HD

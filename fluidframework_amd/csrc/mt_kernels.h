@@ -111,7 +111,9 @@ __device__ inline void skel_lite_move(SkelLite<HT>& k, HT& z, bool in) {
 /* K1-K4 fused: the whole event stream of a document, one wave per document. LDS = true stages the
  * whole small-profile hot image in LDS; otherwise the image stays in HBM and only the skeleton and
  * the heap (Skel, 3.5 KB for the small profile) are staged. */
-template <class HT, bool LDS, int MINW = 1, int SKM = 1> /* SKM: 1 Skel, 2 SkelLite, 0 none */
+/* VAR tags a build variant compiled with other flags in its own translation unit (1: compiler-chosen
+ * inlining): the kernel's name must differ, since a host launch resolves the kernel by name. */
+template <class HT, bool LDS, int MINW = 1, int SKM = 1, int VAR = 0> /* SKM: 1 Skel, 2 SkelLite, 0 none */
 __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
@@ -345,6 +347,7 @@ struct mt_engine {
     int64_t ndocs;
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
+    bool noinline = false; /* small profile: compiler-chosen inlining (MT_REPLAY_NOINLINE=1) */
     int waves = 7;    /* occupancy target of the HBM-resident kernel (MT_REPLAY_WAVES=6|7|8) */
     int mat_skel = 2; /* config-5 profile: 2 SkelLite in LDS, 1 Skel, 0 none (MT_REPLAY_MAT_SKEL) */
     Store<HotSmall> s0;

@@ -39,6 +39,8 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
      * better served by 8, which runs it in 1 or 2 full rounds instead of a last partial one. */
     const char* wv = getenv("MT_REPLAY_WAVES");
     e->waves = wv ? atoi(wv) : (ndocs <= 16384 ? 8 : 7);
+    const char* ni = getenv("MT_REPLAY_NOINLINE");
+    e->noinline = ni && ni[0] == '1';
     const char* ms = getenv("MT_REPLAY_MAT_SKEL");
     e->mat_skel = ms ? atoi(ms) : 2;
     e->profile = prof;
