@@ -111,16 +111,20 @@ struct DocHdr {
 /* Cold per-row data, indexed by a row id that does not move when the row's slot moves. K = the
  * profile's property key slots per document. */
 template <int K>
-struct ColdRowT {
+struct alignas(16) ColdRowT {
     int32_t lseq, lrseq;
     uint32_t toff; /* text offset in the arena; a marker's refType */
     uint8_t prw;   /* pendingRewriteCount */
     uint8_t gc;    /* arena-GC epoch that last moved this row's text (0 = never) */
     uint16_t ovx;  /* first overflow block of removedClientOverlap past the inline 8 (0 = none) */
+    uint16_t pv[K]; /* property values per doc key slot (0 = absent); 16-byte aligned: compared and
+                       cleared 16 bytes at a time. pv, pk and prw are meaningful only while the row's
+                       RF_PROPS flag is set (add_props clears them when it sets the flag). */
     uint64_t ovl;  /* removedClientOverlap: the first 8 short ids (+1), push order */
-    uint16_t pv[K]; /* property values per doc key slot (0 = absent) */
     uint8_t pk[K];  /* pendingKeyUpdateCount per key slot */
 };
+static_assert(sizeof(ColdRowT<8>) % 16 == 0 && sizeof(ColdRowT<24>) % 16 == 0, "cold rows are 16-byte granular");
+static_assert((2 * 8) % 16 == 0 && (2 * 24) % 16 == 0, "pv spans whole 16-byte units");
 
 /* Position index of the large-document profile ("tiled", config 4: >100k live rows).
  *
@@ -235,6 +239,12 @@ MT_HD inline I4 ld4(const int32_t* p) { /* p 16-byte aligned */
     I4 v;
     __builtin_memcpy(&v, __builtin_assume_aligned(p, 16), sizeof v);
     return v;
+}
+MT_HD inline void st4(void* p, const I4& v) { /* p 16-byte aligned */
+    __builtin_memcpy(__builtin_assume_aligned(p, 16), &v, sizeof v);
+}
+MT_HD inline bool eq4(const I4& a, const I4& b) {
+    return a.x[0] == b.x[0] && a.x[1] == b.x[1] && a.x[2] == b.x[2] && a.x[3] == b.x[3];
 }
 MT_HD inline B4 ldb4(const uint8_t* p) { /* p 4-byte aligned */
     B4 v;
@@ -362,6 +372,14 @@ struct Replica {
     }
 
     MT_HD typename HT::Cold& cold(int32_t s) const { return d.cold()[z.rid[s]]; }
+    /* cold row of slot a into slot b's row, 16 bytes per load / store */
+    MT_HD void copy_cold(int32_t b, int32_t a) {
+        const int32_t* src = (const int32_t*)&cold(a);
+        int32_t* dst = (int32_t*)&cold(b);
+        I4 v[sizeof(typename HT::Cold) / 16];
+        for (int i = 0; i < (int)(sizeof(typename HT::Cold) / 16); i++) v[i] = ld4(src + 4 * i);
+        for (int i = 0; i < (int)(sizeof(typename HT::Cold) / 16); i++) st4(dst + 4 * i, v[i]);
+    }
 
     MT_HD void fail(int32_t e) {
         if (h.err == E_OK) {
@@ -517,20 +535,34 @@ struct Replica {
         return !h.collaborating || client == h.localShort;
     }
     /* nodeLength of a leaf (mergeTree.ts:1692-1732); local perspective -> localNetLength */
-    MT_HD int32_t vis(int32_t s, int32_t refSeq, int32_t client) const {
-        int32_t L = z.len(s);
-        if (is_local(client)) return z.rseq(s) == NOREM ? L : 0;
-        int32_t c = z.cli(s) == LOCAL_CLIENT ? -1 : z.cli(s);
-        int32_t sq = z.seq(s);
-        if (!(c == client || (sq != UNASSIGNED_SEQ && sq <= refSeq))) return 0;
-        int32_t rs = z.rseq(s);
-        if (rs != NOREM) {
-            int32_t rc = z.rcli(s) == LOCAL_CLIENT ? -1 : z.rcli(s);
+    /* the scan columns of one slot, read together (four independent loads, one round trip) */
+    struct RowView {
+        int32_t len, seq, rseq;
+        uint32_t b4; /* {cli, rcli, flags, ng} */
+    };
+    MT_HD RowView row_view(int32_t s) const {
+        RowView r;
+        r.len = z.len(s);
+        r.seq = z.seq(s);
+        r.rseq = z.rseq(s);
+        r.b4 = ld_bytes4(s);
+        return r;
+    }
+    MT_HD int32_t vis_of(int32_t s, const RowView& r, int32_t refSeq, int32_t client) const {
+        if (is_local(client)) return r.rseq == NOREM ? r.len : 0;
+        uint8_t cq = (uint8_t)r.b4, rcq = (uint8_t)(r.b4 >> 8), fq = (uint8_t)(r.b4 >> 16);
+        int32_t c = cq == LOCAL_CLIENT ? -1 : cq;
+        if (!(c == client || (r.seq != UNASSIGNED_SEQ && r.seq <= refSeq))) return 0;
+        if (r.rseq != NOREM) {
+            int32_t rc = rcq == LOCAL_CLIENT ? -1 : rcq;
             if (rc == client) return 0;
-            if ((z.flags(s) & RF_OVL) && ovl_has(s, client)) return 0; /* cold read: rare */
-            if (rs != UNASSIGNED_SEQ && rs <= refSeq) return 0;
+            if ((fq & RF_OVL) && ovl_has(s, client)) return 0; /* cold read: rare */
+            if (r.rseq != UNASSIGNED_SEQ && r.rseq <= refSeq) return 0;
         }
-        return L;
+        return r.len;
+    }
+    MT_HD int32_t vis(int32_t s, int32_t refSeq, int32_t client) const {
+        return vis_of(s, row_view(s), refSeq, client);
     }
     /* localNetLength (mergeTree.ts:1195-1206) */
     MT_HD int32_t local_len(int32_t s) const { return z.rseq(s) == NOREM ? z.len(s) : 0; }
@@ -578,11 +610,15 @@ struct Replica {
         z.seq(b) = z.seq(a);
         z.rseq(b) = z.rseq(a);
         z.rid[b] = z.rid[a];
-        z.cli(b) = z.cli(a);
-        z.rcli(b) = z.rcli(a);
-        z.flags(b) = z.flags(a);
-        z.ng(b) = z.ng(a);
+        st_bytes4(b, ld_bytes4(a));
     }
+    /* a slot's {cli, rcli, flags, ng} bytes as one dword (one memory access instead of four) */
+    MT_HD uint32_t ld_bytes4(int32_t a) const {
+        uint32_t v;
+        __builtin_memcpy(&v, __builtin_assume_aligned(&z.cli(a), 4), 4);
+        return v;
+    }
+    MT_HD void st_bytes4(int32_t b, uint32_t v) { __builtin_memcpy(__builtin_assume_aligned(&z.cli(b), 4), &v, 4); }
     /* a row's slot contents held in registers */
     struct HotRow {
         int32_t len, seq, rseq;
@@ -596,10 +632,11 @@ struct Replica {
         r.seq = z.seq(a);
         r.rseq = z.rseq(a);
         r.rid = z.rid[a];
-        r.cli = z.cli(a);
-        r.rcli = z.rcli(a);
-        r.flags = z.flags(a);
-        r.ng = z.ng(a);
+        uint32_t b4 = ld_bytes4(a);
+        r.cli = (uint8_t)b4;
+        r.rcli = (uint8_t)(b4 >> 8);
+        r.flags = (uint8_t)(b4 >> 16);
+        r.ng = (uint8_t)(b4 >> 24);
         r.xf = 0;
         if constexpr (TILED) r.xf = z.tl.xf[a];
         return r;
@@ -609,10 +646,7 @@ struct Replica {
         z.seq(b) = r.seq;
         z.rseq(b) = r.rseq;
         z.rid[b] = r.rid;
-        z.cli(b) = r.cli;
-        z.rcli(b) = r.rcli;
-        z.flags(b) = r.flags;
-        z.ng(b) = r.ng;
+        st_bytes4(b, (uint32_t)r.cli | ((uint32_t)r.rcli << 8) | ((uint32_t)r.flags << 16) | ((uint32_t)r.ng << 24));
         if constexpr (TILED) z.tl.xf[b] = r.xf;
     }
     /* shift slab rows [j, c) of leaf n right by one slot (wave-parallel: read all, then write) */
@@ -681,8 +715,8 @@ struct Replica {
     }
     /* slot of a live row id (its leaf is rleaf[rid]); -1 if the id was freed since `gen` */
     MT_HD int32_t slot_of(int32_t rid, int32_t gen) {
-        if (gen >= 0 && z.rgen[rid] != (uint8_t)gen) return -1;
-        int32_t leaf = z.rleaf[rid];
+        int32_t g = z.rgen[rid], leaf = z.rleaf[rid]; /* both reads in one round trip */
+        if (gen >= 0 && g != (uint8_t)gen) return -1;
         int32_t c = nch[leaf];
         if (W::N == 1) {
             for (int32_t j = 0; j < c; j++)
@@ -1379,12 +1413,15 @@ struct Replica {
         }
     }
     /* Make room at child index j of leaf n; returns slot for the new row (after any split). */
-    MT_HD int32_t leaf_insert_slot(int32_t n, int32_t j) {
+    /* dup: the new slot starts as a copy of the row before it (j >= 1; a split's right part), made
+     * by the same parallel shift instead of a separate row copy */
+    MT_HD int32_t leaf_insert_slot(int32_t n, int32_t j, bool dup = false) {
         MT_PROF_SCOPE(PH_LEAFINS);
         int32_t c = nch[n];
-        slab_shift_right(n, j, c);
-        z.rid[n * MAXN + j] = -1; /* not a row yet: the caller assigns one */
-        if constexpr (TILED) z.tl.xf[n * MAXN + j] = 0;
+        slab_shift_right(n, dup ? j - 1 : j, c);
+        z.rid[n * MAXN + j] = -1; /* not a row yet (a leaf split must not re-home it): the caller assigns one */
+        if constexpr (TILED)
+            if (!dup) z.tl.xf[n * MAXN + j] = 0;
         nch[n] = (int8_t)(c + 1);
         if (c + 1 >= MAXN) {
             int32_t nn = split_node(n);
@@ -1457,19 +1494,22 @@ struct Replica {
         int32_t s0 = n * MAXN + j;
         if (z.flags(s0) & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
         bool willSplit = nch[n] + 1 >= MAXN;
-        int32_t rs = leaf_insert_slot(n, j + 1);
+        int32_t rs = leaf_insert_slot(n, j + 1, true); /* rs starts as a copy of the row */
         if (rs < 0) return -1;
         /* the left part stays at n*8+j unless the leaf split moved children 4..7 (then it sits just
          * before the new slot, in the new leaf) */
         int32_t ls = n * MAXN + j;
         if (willSplit && j >= 4) ls = rs - 1;
-        copy_row(rs, ls);
-        z.rid[rs] = (IX)alloc_rid();
-        z.rleaf[z.rid[rs]] = (IX)(rs / MAXN);
-        cold(rs) = cold(ls); /* splitAt copies every field (mergeTree.ts:523-567) */
-        if (cold(ls).ovx) ovl_clone(rs, ls);
-        z.len(rs) = z.len(ls) - off;
-        cold(rs).toff = cold(ls).toff + (uint32_t)off;
+        int32_t rrid = alloc_rid();
+        z.rid[rs] = (IX)rrid;
+        z.rleaf[rrid] = (IX)(rs / MAXN);
+        typename HT::Cold& cl = cold(ls);
+        typename HT::Cold& cr = d.cold()[rrid];
+        copy_cold(rs, ls); /* splitAt copies every field (mergeTree.ts:523-567) */
+        if (cl.ovx) ovl_clone(rs, ls);
+        int32_t lenL = z.len(ls);
+        z.len(rs) = lenL - off;
+        cr.toff = cl.toff + (uint32_t)off;
         z.len(ls) = off;
         z.flags(ls) &= (uint8_t)~RF_NLK; /* the left part's last unit is not known any more */
         h.nrows++;
@@ -1743,24 +1783,22 @@ struct Replica {
         return z.h.nkeys++;
     }
     MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
+        typename HT::Cold& c = cold(s); /* the row id is read once, not after every store */
         if (!(z.flags(s) & RF_PROPS)) {
-            cold(s).prw = 0;
+            c.prw = 0;
             z.flags(s) |= RF_PROPS;
-            for (int k = 0; k < HT::K; k++) {
-                cold(s).pv[k] = 0;
-                cold(s).pk[k] = 0;
-            }
+            clear_props(s);
         }
-        if (cold(s).prw > 0 && seq != UNASSIGNED_SEQ && collaborating) return;
+        if (c.prw > 0 && seq != UNASSIGNED_SEQ && collaborating) return;
         if (rewrite) {
-            if (collaborating && seq == UNASSIGNED_SEQ) cold(s).prw++;
+            if (collaborating && seq == UNASSIGNED_SEQ) c.prw++;
             for (int32_t k = 0; k < z.h.nkeys; k++) {
-                if (cold(s).pv[k] == 0) continue;
+                if (c.pv[k] == 0) continue;
                 bool inNew = false;
                 for (int32_t j = 0; j < nkv; j++)
                     if (kv[j].key == z.keys[k] && kv[j].value != 0 && !(kv[j].value & MT_VALUE_FALSY)) inNew = true;
-                bool modify = seq == UNASSIGNED_SEQ || cold(s).pk[k] == 0;
-                if (!inNew && modify) cold(s).pv[k] = 0;
+                bool modify = seq == UNASSIGNED_SEQ || c.pk[k] == 0;
+                if (!inNew && modify) c.pv[k] = 0;
             }
         }
         for (int32_t j = 0; j < nkv; j++) {
@@ -1768,25 +1806,36 @@ struct Replica {
             if (k < 0) return;
             if (collaborating) {
                 if (seq == UNASSIGNED_SEQ) {
-                    if (cold(s).pk[k] == 0xFF) {
+                    if (c.pk[k] == 0xFF) {
                         fail(E_CAPACITY);
                         return;
                     }
-                    cold(s).pk[k]++;
-                } else if (!(cold(s).pk[k] == 0)) {
+                    c.pk[k]++;
+                } else if (!(c.pk[k] == 0)) {
                     continue;
                 }
             }
-            cold(s).pv[k] = kv[j].value;
+            c.pv[k] = kv[j].value;
         }
     }
     /* ackPendingProperties (segmentPropertiesManager.ts:19-33) */
     MT_HD void ack_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite) {
-        if (rewrite) cold(s).prw--;
+        typename HT::Cold& c = cold(s);
+        if (rewrite) c.prw--;
         for (int32_t j = 0; j < nkv; j++) {
             int32_t k = key_slot(kv[j].key);
             if (k < 0) return;
-            if (cold(s).pk[k]) cold(s).pk[k]--;
+            if (c.pk[k]) c.pk[k]--;
+        }
+    }
+    /* property values and pending-key counters of row s to "absent" (16 / 8 bytes per store) */
+    MT_HD void clear_props(int32_t s) {
+        typename HT::Cold& c = cold(s);
+        I4 zero = {{0, 0, 0, 0}};
+        for (int i = 0; i < HT::K / 8; i++) st4(&c.pv[8 * i], zero);
+        for (int i = 0; i < HT::K / 8; i++) {
+            uint64_t z8 = 0;
+            __builtin_memcpy(__builtin_assume_aligned(&c.pk[8 * i], 8), &z8, 8);
         }
     }
     MT_HD bool match_props(int32_t a, int32_t b) { /* matchProperties (properties.ts:61-92) */
@@ -1794,8 +1843,10 @@ struct Replica {
         bool pa = z.flags(a) & RF_PROPS, pb = z.flags(b) & RF_PROPS;
         if (pa != pb) return false;
         if (!pa) return true;
-        for (int k = 0; k < HT::K; k++)
-            if (cold(a).pv[k] != cold(b).pv[k]) return false;
+        const typename HT::Cold& ca = cold(a);
+        const typename HT::Cold& cb = cold(b);
+        for (int i = 0; i < HT::K / 8; i++) /* 8 key slots per 16-byte compare */
+            if (!eq4(ld4((const int32_t*)&ca.pv[8 * i]), ld4((const int32_t*)&cb.pv[8 * i]))) return false;
         return true;
     }
 
@@ -1833,15 +1884,16 @@ struct Replica {
             return;
         }
         uint16_t* base = arena_base(h.arenaSide);
-        if ((int32_t)cold(a).toff + La == h.arenaTop && h.arenaTop + Lb <= d.caps.acap) {
+        int32_t ta = (int32_t)cold(a).toff, tb = (int32_t)cold(b).toff; /* both reads in one round trip */
+        if (ta + La == h.arenaTop && h.arenaTop + Lb <= d.caps.acap) {
             int32_t off = arena_alloc(Lb);
-            arena_copy(base + off, base + cold(b).toff, Lb);
-        } else if ((int32_t)cold(a).toff + La == (int32_t)cold(b).toff) {
+            arena_copy(base + off, base + tb, Lb);
+        } else if (ta + La == tb) {
             /* already contiguous */
         } else {
             int32_t off = arena_alloc(La + Lb);
             if (off < 0) return;
-            base = arena_base(h.arenaSide); /* a GC may have switched halves */
+            base = arena_base(h.arenaSide); /* a GC may have switched halves (and moved both texts) */
             arena_copy(base + off, base + cold(a).toff, La);
             arena_copy(base + off + La, base + cold(b).toff, Lb);
             cold(a).toff = (uint32_t)off;
@@ -2246,11 +2298,14 @@ struct Replica {
 
     /* ---- insert (insertSegments 2001-2031, blockInsert 2174-2257) -------------------- */
     /* breakTie for a zero-length row (2281-2310) */
-    MT_HD bool break_tie(int32_t s, int32_t refSeq, int32_t client) const {
-        int32_t rs = z.rseq(s);
+    MT_HD bool break_tie_of(const RowView& r, int32_t refSeq, int32_t client) const {
+        int32_t rs = r.rseq;
         if (rs != NOREM && rs != 0 && rs <= refSeq && rs != UNASSIGNED_SEQ) return false;
         if (client == h.localShort) return true;
-        return z.seq(s) != UNASSIGNED_SEQ;
+        return r.seq != UNASSIGNED_SEQ;
+    }
+    MT_HD bool break_tie(int32_t s, int32_t refSeq, int32_t client) const {
+        return break_tie_of(row_view(s), refSeq, client);
     }
     /* continueFrom (2187-2194): first row after leaf lorder[k] with localNetLength > 0 is a
      * local-pending insert */
@@ -2333,7 +2388,8 @@ struct Replica {
             int32_t c = nch[n];
             for (; j < c; j++) {
                 int32_t s = n * MAXN + j;
-                if (vis(s, refSeq, client) > 0 || break_tie(s, refSeq, client)) return leaf_insert_slot(n, j);
+                RowView r = row_view(s);
+                if (vis_of(s, r, refSeq, client) > 0 || break_tie_of(r, refSeq, client)) return leaf_insert_slot(n, j);
             }
             if (seq != UNASSIGNED_SEQ && kvalid(knext(k)) && continue_from(k)) {
                 k = knext(k);
@@ -2371,45 +2427,36 @@ struct Replica {
                 fail(E_INSERT_FAILED);
                 return;
             }
-            z.rid[s] = (IX)alloc_rid();
-            cold(s).gc = 0;
+            int32_t rid = alloc_rid();
+            z.rid[s] = (IX)rid;
+            typename HT::Cold& c = d.cold()[rid]; /* row id kept in a register, not re-read per field */
+            c.gc = 0;
             z.len(s) = L;
             z.seq(s) = seq;
-            z.rseq(s) = NOREM;
-            cold(s).lseq = localSeq;
-            cold(s).lrseq = 0;
-            z.cli(s) = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-            z.rcli(s) = 0;
+            z.rseq(s) = preRseq > 0 ? preRseq : NOREM;
+            c.lseq = localSeq;
+            c.lrseq = 0;
             int32_t fl = (marker ? RF_MARKER : 0) | (perm ? RF_PERM : 0) | (hasL ? RF_LSEQ : 0);
-            z.ng(s) = 0;
-            cold(s).prw = 0;
-            cold(s).ovl = 0;
-            cold(s).ovx = 0;
-            z.rleaf[z.rid[s]] = (IX)(s / MAXN);
+            c.ovl = 0; /* pv / pk / prw: set up by add_props with RF_PROPS */
+            c.ovx = 0;
+            z.rleaf[rid] = (IX)(s / MAXN);
             h.nrows++;
             h.sumW++;
-            if (preRseq > 0) {
-                z.rseq(s) = preRseq;
-                z.rcli(s) = preRcli;
-            } else {
-                h.localLen += L;
-            }
+            if (preRseq <= 0) h.localLen += L;
             if (marker) {
-                cold(s).toff = (uint32_t)op.pos2;
+                c.toff = (uint32_t)op.pos2;
             } else if (perm) {
-                cold(s).toff = 0;
+                c.toff = 0;
             } else {
                 MT_PROF_SCOPE(PH_TEXT);
-                cold(s).toff = (uint32_t)off;
+                c.toff = (uint32_t)off;
                 int32_t last = arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
                 fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
             }
-            z.flags(s) = (uint8_t)fl;
+            /* {cli, rcli, flags, ng = 0} in one store */
+            st_bytes4(s, (uint32_t)(uint8_t)(client < 0 ? LOCAL_CLIENT : client) |
+                             ((uint32_t)(preRseq > 0 ? preRcli : 0) << 8) | ((uint32_t)(uint8_t)fl << 16));
             if constexpr (TILED) row_enter(s);
-            for (int k = 0; k < HT::K; k++) {
-                cold(s).pv[k] = 0;
-                cold(s).pk[k] = 0;
-            }
             if (op.props) { /* TextSegment.make(text, props): addProperties without collab */
                 const mt_props_rec& pr = p.props[op.props - 1];
                 add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE, 0, false);
@@ -2608,30 +2655,30 @@ struct Replica {
         bool hasL = seq == UNASSIGNED_SEQ;
         int32_t localSeq = hasL ? ++h.localSeq : 0;
         bool created = false;
+        const uint32_t rcl = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
         range_op(start, end, refSeq, client, [&](int32_t s) {
             h.sumW++;
-            if (z.rseq(s) != NOREM) {
-                if (z.rseq(s) == UNASSIGNED_SEQ) {
-                    z.rcli(s) = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-                    z.rseq(s) = seq;
-                    z.flags(s) &= (uint8_t)~RF_LRSEQ;
+            int32_t rs = z.rseq(s), L = z.len(s);
+            uint32_t b4 = ld_bytes4(s); /* {cli, rcli, flags, ng}: one read, one write */
+            uint32_t fl = (b4 >> 16) & 0xFF;
+            if (rs != NOREM) {
+                if (rs == UNASSIGNED_SEQ) {
+                    z.rseq(s) = rs = seq;
+                    st_bytes4(s, (b4 & 0xFF0000FFu) | (rcl << 8) | ((fl & ~(uint32_t)RF_LRSEQ) << 16));
                 } else {
                     ovl_push(s, client);
-                    z.flags(s) |= RF_OVL;
+                    st_bytes4(s, (b4 & 0xFF00FFFFu) | ((fl | RF_OVL) << 16));
                 }
             } else {
-                h.localLen -= z.len(s); /* the row leaves the local view */
-                z.rcli(s) = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-                z.rseq(s) = seq;
+                h.localLen -= L; /* the row leaves the local view */
+                z.rseq(s) = rs = seq;
                 cold(s).lrseq = localSeq;
-                if (hasL)
-                    z.flags(s) |= RF_LRSEQ;
-                else
-                    z.flags(s) &= (uint8_t)~RF_LRSEQ;
+                fl = hasL ? (fl | RF_LRSEQ) : (fl & ~(uint32_t)RF_LRSEQ);
+                st_bytes4(s, (b4 & 0xFF0000FFu) | (rcl << 8) | (fl << 16));
             }
             if constexpr (TILED) row_removed(s);
             if (h.collaborating) {
-                if (z.rseq(s) == UNASSIGNED_SEQ && client == h.localShort)
+                if (rs == UNASSIGNED_SEQ && client == h.localShort)
                     pending_add(s, localSeq, &created);
                 else
                     add_lru(s, seq);
@@ -2872,7 +2919,6 @@ struct Replica {
         z.ng(s) = 0;
         cold(s).lseq = 0;
         cold(s).lrseq = 0;
-        cold(s).prw = 0;
         cold(s).ovl = 0;
         cold(s).ovx = 0;
         z.rleaf[z.rid[s]] = (IX)(s / MAXN);
@@ -2887,10 +2933,6 @@ struct Replica {
             fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
         }
         z.flags(s) = (uint8_t)fl;
-        for (int k = 0; k < HT::K; k++) {
-            cold(s).pv[k] = 0;
-            cold(s).pk[k] = 0;
-        }
         if (op.props) {
             const mt_props_rec& pr = p.props[op.props - 1];
             add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE, 0, false);

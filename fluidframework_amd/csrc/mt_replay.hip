@@ -34,11 +34,11 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->lds = g && g[0] == '1';
     /* Occupancy of the HBM-resident small-profile kernel: documents are replayed one per wave and
      * a document's events are sequential, so a batch runs in "rounds" of 1,024 x waves documents
-     * (256 CUs x 4 SIMDs). 7 waves/SIMD is fastest per wave (8 spills registers: 168 vs 174 Mops/s
-     * at 32k docs), but a small batch (a strong-scaled shard: 8,192 or 16,384 docs per GPU) is
-     * better served by 8, which runs it in 1 or 2 full rounds instead of a last partial one. */
+     * (256 CUs x 4 SIMDs). Round-2 sweep at 65,536 documents (profiles/r02_occupancy.txt): 2 / 4 /
+     * 5 / 6 / 7 / 8 waves per SIMD give 122 / 142 / 137 / 144 / 144 / 149 Mops/s: the memory
+     * system, not the wave count, sets the rate, and 8 is best at every batch size. */
     const char* wv = getenv("MT_REPLAY_WAVES");
-    e->waves = wv ? atoi(wv) : (ndocs <= 16384 ? 8 : 7);
+    e->waves = wv ? atoi(wv) : 8;
     const char* ni = getenv("MT_REPLAY_NOINLINE");
     e->noinline = ni && ni[0] == '1';
     const char* ms = getenv("MT_REPLAY_MAT_SKEL");

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Memory-pipeline counters of the config-3 kernel (L1 TLB, L1->L2 latency, TA busy, L2 hits,
-# vector-memory latency), one counter group per bounded run, then a PC-sampling attempt.
+# vector-memory latency), one counter group per bounded run.
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-mem}
@@ -17,5 +17,3 @@ for CTRS in "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum TCP_TCC_READ_R
   timeout -s KILL 300 rocprofv3 --pmc $CTRS -d "$OUT/pmc$P" -o run --output-format csv -- python3 bench.py --docs $D --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc$P.json" 2> "$OUT/pmc$P.err" || { echo "pmc pass $P rc=$?"; tail -5 "$OUT/pmc$P.err"; exit 1; }
   echo "pass $P ok"
 done
-[ -n "$NOPC" ] && exit 0
-DOCS=8192 bash tools/gpu_pcsamp.sh $TAG/pcs

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Forced vs compiler-chosen inlining (distinct kernels now) at 65,536 docs, 8 waves; then the
-# memory-pipeline counters and a PC-sampling attempt (tools/gpu_mem.sh).
+# memory-pipeline counters (tools/gpu_mem.sh).
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-r2h}
