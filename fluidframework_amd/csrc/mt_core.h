@@ -80,6 +80,16 @@ struct Caps {
     int32_t acap; /* text arena half-size (UTF-16 units); arena holds 2 halves */
     int32_t mcap; /* segment-group membership log entries */
     int32_t gcap; /* pending segment groups (local ops in flight) */
+    int32_t dcap; /* delta event log words (0 = delta events off; mt_oplog.h MT_DELTA_*) */
+};
+
+/* delta event stream state at the head of a document's delta region (mt_oplog.h) */
+struct alignas(16) DState {
+    int64_t n;   /* words emitted (may exceed dcap: later words are hashed, not stored) */
+    uint64_t h;  /* FNV-1a-64 of every emitted word */
+    int32_t seq; /* seq of the record being applied (-1: local edit) */
+    int32_t on;  /* 0 while a snapshot-load record applies */
+    int32_t _p[2];
 };
 
 /* per-document scalar header */
@@ -270,7 +280,13 @@ struct Doc {
     MT_HD static int64_t off_mgid(const Caps& c) { return OFF_ARENA + align256c(4 * (int64_t)c.acap); }
     MT_HD static int64_t off_mrid(const Caps& c) { return off_mgid(c) + align256c(4 * (int64_t)c.mcap); }
     MT_HD static int64_t off_gq(const Caps& c) { return off_mrid(c) + align256c(4 * (int64_t)c.mcap); }
-    MT_HD static int64_t stride(const Caps& c) { return off_gq(c) + align256c(4 * (int64_t)c.gcap); }
+    /* delta region (only when c.dcap > 0): DState, then dcap words */
+    MT_HD static int64_t off_dl(const Caps& c) { return off_gq(c) + align256c(4 * (int64_t)c.gcap); }
+    MT_HD static int64_t stride(const Caps& c) {
+        return off_dl(c) + (c.dcap > 0 ? align256c((int64_t)sizeof(DState) + 4 * (int64_t)c.dcap) : 0);
+    }
+    MT_HD DState* dstate() const { return (DState*)(b + off_dl(caps)); }
+    MT_HD int32_t* dlog() const { return (int32_t*)(b + off_dl(caps) + (int64_t)sizeof(DState)); }
     MT_HD typename HT::Cold* cold() const { return (typename HT::Cold*)(b + OFF_COLD); } /* HT::S records */
     MT_HD typename HT::IX* frid() const { return (typename HT::IX*)(b + OFF_FRID); } /* free row-id stack */
     MT_HD uint16_t* arena() const { return (uint16_t*)(b + OFF_ARENA); } /* 2 * acap */
@@ -307,7 +323,9 @@ struct ProfScope {
 /* ------------------------------------------------------------------------------------------
  * Replica: all operations of one document replica, executed by one wave.
  * ---------------------------------------------------------------------------------------- */
-template <class W, class HT>
+/* DL: this build emits delta events (mt_oplog.h) when the engine has a delta log; the hot replay
+ * kernels are built without (DL = false), so the emission costs them no registers or code */
+template <class W, class HT, bool DL = false>
 struct Replica {
     typedef typename HT::IX IX;
     static constexpr bool TILED = HT::TILED;
@@ -494,7 +512,103 @@ struct Replica {
             int32_t i = b + w.lane();
             if (i < HT::C) z.l2s[i] = 0xFF;
         }
+        if (d.caps.dcap > 0) {
+            DState* st = d.dstate();
+            st->n = 0;
+            st->h = MT_FNV_OFFSET;
+            st->seq = 0;
+            st->on = 1;
+        }
         w.sync();
+    }
+
+    /* ---- delta events (§8 f3; stream format in mt_oplog.h): the reference's
+     * mergeTreeDeltaCallback / mergeTreeMaintenanceCallback, in firing order. Only engines created
+     * with caps.dcap > 0 emit; the state lives in the document's delta region, not in registers. */
+    MT_HD bool dl_on() const {
+        if constexpr (!DL)
+            return false;
+        else
+            return d.caps.dcap > 0 && d.dstate()->on;
+    }
+    MT_HD void dput(int32_t v) {
+        DState* st = d.dstate();
+        int64_t n = st->n;
+        uint64_t hh = st->h;
+        for (int i = 0; i < 4; i++) {
+            hh ^= (uint8_t)((uint32_t)v >> (8 * i));
+            hh *= MT_FNV_PRIME;
+        }
+        if (n < d.caps.dcap) d.dlog()[n] = v;
+        st->n = n + 1;
+        st->h = hh;
+    }
+    MT_HD void dhead(int32_t op) {
+        dput(op);
+        dput(d.dstate()->seq);
+    }
+    MT_HD void dtail(int32_t nseg) { /* end of the segment list, then its count */
+        dput(MT_DELTA_END);
+        dput(nseg);
+    }
+    MT_HD void dseg(int32_t pos, int32_t len) {
+        dput(pos);
+        dput(len);
+        dput(0);
+    }
+    /* Client.getPosition(segment) (client.ts:291): the local view */
+    MT_HD int32_t local_pos(int32_t s) { return position_of(s, h.currentSeq, h.localShort); }
+    /* the propertyDeltas addProperties (segmentPropertiesManager.ts:35-111) returns for row s and this
+     * annotate, read before the row changes: nd, then (key << 16 | previous value) by key id */
+    MT_HD bool prop_delta(int32_t s, int32_t kid, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collab,
+                          int32_t* val) {
+        bool has = z.flags(s) & RF_PROPS;
+        int32_t cv = 0, pd = 0;
+        if (has)
+            for (int32_t k = 0; k < z.h.nkeys; k++)
+                if (z.keys[k] == kid) {
+                    cv = cold(s).pv[k];
+                    pd = cold(s).pk[k];
+                }
+        bool inNew = false, truthy = false;
+        for (int32_t j = 0; j < nkv; j++)
+            if (kv[j].key == kid) {
+                inNew = true;
+                truthy = kv[j].value != 0 && !(kv[j].value & MT_VALUE_FALSY);
+            }
+        bool in = false, del = false;
+        if (rewrite && cv != 0 && !truthy && (seq == UNASSIGNED_SEQ || pd == 0)) { /* rewrite deletes it */
+            in = del = true;
+            *val = cv;
+        }
+        if (inNew && !(collab && seq != UNASSIGNED_SEQ && pd != 0)) { /* deltas[key] = previous ?? null */
+            in = true;
+            *val = del ? 0 : cv;
+        }
+        return in;
+    }
+    MT_HD void prop_deltas(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collab) {
+        if ((z.flags(s) & RF_PROPS) && cold(s).prw > 0 && seq != UNASSIGNED_SEQ && collab) {
+            dput(-1); /* outstanding local rewrites: addProperties returns undefined */
+            return;
+        }
+        for (int pass = 0; pass < 2; pass++) {
+            int32_t last = -1, nd = 0;
+            for (;;) { /* candidate keys (the doc's key slots and the op's keys) in id order */
+                int32_t best = 0x7fffffff;
+                for (int32_t k = 0; k < z.h.nkeys; k++)
+                    if (z.keys[k] > last && z.keys[k] < best) best = z.keys[k];
+                for (int32_t j = 0; j < nkv; j++)
+                    if (kv[j].key > last && kv[j].key < best) best = kv[j].key;
+                if (best == 0x7fffffff) break;
+                last = best;
+                int32_t v = 0;
+                if (!prop_delta(s, best, kv, nkv, rewrite, seq, collab, &v)) continue;
+                nd++;
+                if (pass) dput((int32_t)(((uint32_t)best << 16) | ((uint32_t)v & 0xFFFF)));
+            }
+            if (!pass) dput(nd);
+        }
     }
 
     /* ---- clients (client.ts:637-661) --------------------------------------------------- */
@@ -1541,6 +1655,12 @@ struct Replica {
                 }
             }
         }
+        if (dl_on()) { /* MergeTreeMaintenanceType.SPLIT (mergeTree.ts:2264-2269): [segment, next] */
+            dhead(MT_DELTA_SPLIT);
+            dseg(-1, z.len(ls));
+            dseg(-1, z.len(rs));
+            dtail(2);
+        }
         if (rsOut) *rsOut = rs;
         return ls;
     }
@@ -1918,6 +2038,11 @@ struct Replica {
                         if (wpos != k) copy_row(n * MAXN + wpos, s);
                         wpos++;
                     } else {
+                        if (dl_on()) { /* MergeTreeMaintenanceType.UNLINK (mergeTree.ts:1343-1348) */
+                            dhead(MT_DELTA_UNLINK);
+                            dseg(-1, z.len(s));
+                            dtail(1);
+                        }
                         free_rid(z.rid[s]); /* unlinked */
                     }
                     prev = -1;
@@ -1933,6 +2058,12 @@ struct Replica {
                                   can_append(prev, s);
                         if (ok) {
                             append_text(prev, s);
+                            if (dl_on()) { /* APPEND (mergeTree.ts:1368-1373): [prevSegment, segment] */
+                                dhead(MT_DELTA_APPEND);
+                                dseg(-1, z.len(prev));
+                                dseg(-1, z.len(s));
+                                dtail(2);
+                            }
                             free_rid(z.rid[s]);
                         } else {
                             int32_t dst = n * MAXN + wpos;
@@ -2003,6 +2134,7 @@ struct Replica {
         uint64_t keep = w.ballot(code == 1) | (cand & ~pairs);
         int32_t fl = r.flags;
         int32_t prev = -1, prevLen = 0, prevFl = 0;
+        int32_t alen = 0; /* an appended row's lane: its prevSegment's length right after the append */
         uint64_t m = pairs;
         while (m) {
             int32_t k = W::ffs(m);
@@ -2031,6 +2163,7 @@ struct Replica {
                     prevLen += lk;
                     prevFl = (prevFl & ~(RF_NLK | RF_NL)) | (fk & (RF_NLK | RF_NL));
                     nlen = w.writelane(prevLen, prev, nlen);
+                    alen = w.writelane(prevLen, k, alen);
                 }
                 fl = w.writelane(prevFl, prev, fl);
             }
@@ -2047,6 +2180,24 @@ struct Replica {
 #endif
         /* frees: every valid row not kept (unlinked or appended) */
         uint64_t drop = vmask & ~keep;
+        if (dl_on()) { /* UNLINK / APPEND maintenance events in the reference's walk order (lane order) */
+            uint64_t em = drop;
+            while (em) {
+                int32_t l = W::ffs(em);
+                em &= em - 1;
+                int32_t ln = w.bcast(r.len, l);
+                if (w.bcast(code, l) == 2) {
+                    dhead(MT_DELTA_UNLINK);
+                    dseg(-1, ln);
+                    dtail(1);
+                } else {
+                    dhead(MT_DELTA_APPEND);
+                    dseg(-1, w.bcast(alen, l));
+                    dseg(-1, ln);
+                    dtail(2);
+                }
+            }
+        }
         uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
         if ((drop >> q) & 1) {
             int32_t pos = h.nfreeRid + __builtin_popcountll(drop & below);
@@ -2469,6 +2620,12 @@ struct Replica {
                     add_lru(s, seq);
                 }
             }
+            if (dl_on()) { /* INSERT delta (mergeTree.ts:2014-2021), after blockInsert */
+                int32_t pp = local_pos(s);
+                dhead(MT_DELTA_INSERT);
+                dseg(pp, L);
+                dtail(1);
+            }
         }
         if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
@@ -2481,11 +2638,30 @@ struct Replica {
      * the first replaced by its right part if start falls inside it and the last cut at end. So one
      * scan finds the first and the last overlapping row, the two splits are made in the reference's
      * order, and the visit walks document order from the first row to the last. */
+    /* Visit, in document order, the rows with vis > 0 from slot sa to slot sb: leaf(s, pos). With dl,
+     * pos is the row's local-view position once the visit is done (Client.getPosition at the delta
+     * callback, client.ts:291): the local length before sa plus, for each row passed, its local length
+     * after its own visit (a REMOVE drops a visited row's; an ANNOTATE changes none). */
     template <class F>
-    MT_HD void range_op(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
+    MT_HD void visit_run(int32_t sa, int32_t sb, int32_t refSeq, int32_t client, F& leaf, bool dl) {
+        int32_t run = dl ? local_pos(sa) : 0;
+        int32_t ka = kpos(sa / MAXN), kb = kpos(sb / MAXN);
+        for (int32_t k = ka;; k = knext(k)) {
+            int32_t n = leaf_at(k), c = nch[n];
+            int32_t j0 = k == ka ? (sa & (MAXN - 1)) : 0;
+            int32_t j1 = k == kb ? (sb & (MAXN - 1)) : c - 1;
+            for (int32_t j = j0; j <= j1; j++) {
+                if (vis(n * MAXN + j, refSeq, client) > 0) leaf(n * MAXN + j, run);
+                if (dl) run += local_len(n * MAXN + j);
+            }
+            if (k == kb || !kvalid(knext(k))) break;
+        }
+    }
+    template <class F>
+    MT_HD void range_op(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf, bool dl = false) {
         MT_PROF_SCOPE(PH_MAP);
         if constexpr (TILED) {
-            range_op_tiled(start, end, refSeq, client, leaf);
+            range_op_tiled(start, end, refSeq, client, leaf, dl);
             return;
         }
         int32_t run = 0;
@@ -2555,6 +2731,10 @@ struct Replica {
             fail(E_ASSERT);
             return;
         }
+        if (dl) { /* delta events need each visited row's position: the serial visit */
+            visit_run(sa, sb, refSeq, client, leaf, true);
+            return;
+        }
         int32_t ta = kpos(sa / MAXN) * MAXN + (sa & (MAXN - 1));
         int32_t tb = kpos(sb / MAXN) * MAXN + (sb & (MAXN - 1));
         for (int32_t b = ta & ~3; b <= tb; b += 4 * W::N) {
@@ -2574,7 +2754,7 @@ struct Replica {
                 while (bits) {
                     int32_t q = __builtin_ctz((unsigned)bits);
                     bits &= bits - 1;
-                    leaf(sbase + q);
+                    leaf(sbase + q, 0);
                 }
             }
         }
@@ -2583,7 +2763,7 @@ struct Replica {
      * reaching start + 1 and min(end, length) (one window pass, two summary searches); the same
      * two splits; then the rows with length > 0 between them are visited leaf by leaf. */
     template <class F>
-    MT_HD void range_op_tiled(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf) {
+    MT_HD void range_op_tiled(int32_t start, int32_t end, int32_t refSeq, int32_t client, F& leaf, bool dl) {
         int32_t tf, Pf, tg, Pg;
         if (tiles_cover(refSeq, client)) {
             int32_t total = win_pass(refSeq, client);
@@ -2640,15 +2820,7 @@ struct Replica {
             fail(E_ASSERT);
             return;
         }
-        int32_t ka = kpos(sa / MAXN), kb = kpos(sb / MAXN);
-        for (int32_t k = ka;; k = knext(k)) {
-            int32_t n = leaf_at(k), c = nch[n];
-            int32_t j0 = k == ka ? (sa & (MAXN - 1)) : 0;
-            int32_t j1 = k == kb ? (sb & (MAXN - 1)) : c - 1;
-            for (int32_t j = j0; j <= j1; j++)
-                if (vis(n * MAXN + j, refSeq, client) > 0) leaf(n * MAXN + j);
-            if (k == kb || !kvalid(knext(k))) break;
-        }
+        visit_run(sa, sb, refSeq, client, leaf, dl);
     }
 
     MT_HD void mark_range_removed(int32_t start, int32_t end, int32_t refSeq, int32_t client, int32_t seq) {
@@ -2656,7 +2828,14 @@ struct Replica {
         int32_t localSeq = hasL ? ++h.localSeq : 0;
         bool created = false;
         const uint32_t rcl = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
-        range_op(start, end, refSeq, client, [&](int32_t s) {
+        const bool dl = dl_on();
+        bool dh = false; /* the REMOVE event's head goes out after the boundary splits' SPLIT events */
+        int32_t dn = 0;
+        range_op(start, end, refSeq, client, [&](int32_t s, int32_t dpos) {
+            if (dl && !dh) {
+                dhead(MT_DELTA_REMOVE);
+                dh = true;
+            }
             h.sumW++;
             int32_t rs = z.rseq(s), L = z.len(s);
             uint32_t b4 = ld_bytes4(s); /* {cli, rcli, flags, ng}: one read, one write */
@@ -2675,6 +2854,10 @@ struct Replica {
                 cold(s).lrseq = localSeq;
                 fl = hasL ? (fl | RF_LRSEQ) : (fl & ~(uint32_t)RF_LRSEQ);
                 st_bytes4(s, (b4 & 0xFF0000FFu) | (rcl << 8) | (fl << 16));
+                if (dl) { /* removedSegments: only rows this op removes (mergeTree.ts:2669-2672) */
+                    dseg(dpos, L);
+                    dn++;
+                }
             }
             if constexpr (TILED) row_removed(s);
             if (h.collaborating) {
@@ -2683,7 +2866,11 @@ struct Replica {
                 else
                     add_lru(s, seq);
             }
-        });
+        }, dl);
+        if (dl) {
+            if (!dh) dhead(MT_DELTA_REMOVE);
+            dtail(dn);
+        }
         if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
     MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t refSeq,
@@ -2691,8 +2878,21 @@ struct Replica {
         int32_t localSeq = seq == UNASSIGNED_SEQ ? ++h.localSeq : 0;
         bool created = false;
         bool collab = h.collaborating;
-        range_op(start, end, refSeq, client, [&](int32_t s) {
+        const bool dl = dl_on();
+        bool dh = false;
+        int32_t dn = 0;
+        range_op(start, end, refSeq, client, [&](int32_t s, int32_t dpos) {
             h.sumW++;
+            if (dl) { /* deltaSegments.push({segment, propertyDeltas}) (mergeTree.ts:2608-2609) */
+                if (!dh) {
+                    dhead(MT_DELTA_ANNOTATE);
+                    dh = true;
+                }
+                dput(dpos);
+                dput(z.len(s));
+                prop_deltas(s, kv, nkv, rewrite, seq, collab);
+                dn++;
+            }
             add_props(s, kv, nkv, rewrite, seq, collab);
             if (collab) {
                 if (seq == UNASSIGNED_SEQ)
@@ -2700,7 +2900,11 @@ struct Replica {
                 else
                     add_lru(s, seq);
             }
-        });
+        }, dl);
+        if (dl) {
+            if (!dh) dhead(MT_DELTA_ANNOTATE);
+            dtail(dn);
+        }
         if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
 
@@ -2756,6 +2960,13 @@ struct Replica {
         MT_PROF_SCOPE(PH_APPLY);
         if (h.err) return;
         int32_t kind = op.kind & MT_OP_KIND_MASK;
+        if constexpr (DL) {
+            if (d.caps.dcap > 0) { /* delta events: this record's seq; none while a snapshot loads */
+                DState* st = d.dstate();
+                st->seq = (op.kind & MT_OPF_LOCAL) ? UNASSIGNED_SEQ : op.seq;
+                st->on = (op.kind & MT_OPF_LOCAL) || kind < MT_OP_RELOAD;
+            }
+        }
         const mt_kv* kv = 0;
         int32_t nkv = 0;
         bool rw = false;
@@ -3029,12 +3240,26 @@ struct Replica {
                 return total;
             }
         }
-        for (int32_t k = 0; kvalid(k); k = knext(k)) {
-            int32_t n = leaf_at(k), c = nch[n];
-            for (int32_t j = 0; j < c; j++) {
-                if (k == k0 && j == j0) return total;
-                total += vis(n * MAXN + j, refSeq, client);
+        if constexpr (TILED) { /* a remote perspective below minSeq: walk every leaf */
+            for (int32_t k = 0; kvalid(k); k = knext(k)) {
+                int32_t n = leaf_at(k), c = nch[n];
+                for (int32_t j = 0; j < c; j++) {
+                    if (k == k0 && j == j0) return total;
+                    total += vis(n * MAXN + j, refSeq, client);
+                }
             }
+            return total;
+        }
+        /* flat profiles: the perspective scan over the slots before s (a quad per lane) */
+        int32_t t0 = k0 * MAXN + j0;
+        for (int32_t b = 0; b < t0; b += 4 * W::N) {
+            int32_t tq = b + 4 * w.lane();
+            int32_t v[4];
+            quad_vis(quad_slot(tq), refSeq, client, v);
+            int32_t x = 0;
+            for (int q = 0; q < 4; q++)
+                if (tq + q < t0) x += v[q];
+            total += w.sum(x);
         }
         return total;
     }

@@ -28,32 +28,32 @@ struct mth_store {
     uint8_t* mem;
 };
 
-/* call F with a Replica<WaveHost, HT> for doc d of the store's profile */
+/* call F with a Replica<WaveHost, HT, true> (delta events on) for doc d of the store's profile */
 template <class F>
 static auto with_replica(mth_store* s, int64_t d, F&& f) {
     /* every call ends with commit(): the replica's register header goes back to the image */
     if (s->profile == 0) {
-        Replica<WaveHost, HotSmall> r(s->s0.doc(d), WaveHost());
+        Replica<WaveHost, HotSmall, true> r(s->s0.doc(d), WaveHost());
         auto res = f(r);
         r.commit();
         return res;
     } else if (s->profile == 3) {
-        Replica<WaveHost, HotMat> r(s->s3.doc(d), WaveHost());
+        Replica<WaveHost, HotMat, true> r(s->s3.doc(d), WaveHost());
         auto res = f(r);
         r.commit();
         return res;
     } else if (s->profile == 1) {
-        Replica<WaveHost, HotMid> r(s->s1.doc(d), WaveHost());
+        Replica<WaveHost, HotMid, true> r(s->s1.doc(d), WaveHost());
         auto res = f(r);
         r.commit();
         return res;
     } else if (s->profile == 4) {
-        Replica<WaveHost, HotHuge> r(s->s4.doc(d), WaveHost());
+        Replica<WaveHost, HotHuge, true> r(s->s4.doc(d), WaveHost());
         auto res = f(r);
         r.commit();
         return res;
     }
-    Replica<WaveHost, HotBig> r(s->s2.doc(d), WaveHost());
+    Replica<WaveHost, HotBig, true> r(s->s2.doc(d), WaveHost());
     auto res = f(r);
     r.commit();
     return res;
@@ -61,9 +61,12 @@ static auto with_replica(mth_store* s, int64_t d, F&& f) {
 
 extern "C" {
 
-mth_store* mth_create(int64_t ndocs, const int32_t* caps6) {
-    /* caps6 = (ncap, hcap[ignored: 2*ncap], acap, mcap, gcap, ccap[ignored: 64]) */
-    Caps k = {caps6[2], caps6[3], caps6[4]};
+mth_store* mth_create(int64_t ndocs, const int32_t* caps6) { return mth_create_dl(ndocs, caps6, 0); }
+
+mth_store* mth_create_dl(int64_t ndocs, const int32_t* caps6, int32_t dcap) {
+    /* caps6 = (ncap, hcap[ignored: 2*ncap], acap, mcap, gcap, ccap[ignored: 64]); dcap: delta event
+     * log words per doc (mt_caps.dcap) */
+    Caps k = {caps6[2], caps6[3], caps6[4], dcap < 0 ? 0 : dcap};
     int prof = profile_for(caps6[0]);
     if (!caps_valid(k) || ndocs < 1 || prof < 0) return nullptr;
     mth_store* s = (mth_store*)calloc(1, sizeof(mth_store));
@@ -173,6 +176,23 @@ int64_t mth_dump(mth_store* s, int64_t doc, uint8_t* out, int64_t cap) {
 
 uint64_t mth_digest(mth_store* s, int64_t doc) {
     return with_replica(s, doc, [](auto& r) { return r.digest(); });
+}
+
+/* delta events of one doc (mt_oplog.h): words emitted (returned), their FNV-1a-64, and the logged
+ * words (at most min(n, dcap, cap)) */
+int64_t mth_deltas(mth_store* s, int64_t doc, int32_t* out, int64_t cap, uint64_t* hash) {
+    return with_replica(s, doc, [&](auto& r) -> int64_t {
+        if (r.d.caps.dcap <= 0) {
+            if (hash) *hash = 0;
+            return 0;
+        }
+        const DState* st = r.d.dstate();
+        int64_t m = st->n < r.d.caps.dcap ? st->n : r.d.caps.dcap;
+        if (m > cap) m = cap;
+        for (int64_t i = 0; out && i < m; i++) out[i] = r.d.dlog()[i];
+        if (hash) *hash = st->h;
+        return st->n;
+    });
 }
 
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {

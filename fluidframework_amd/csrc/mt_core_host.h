@@ -7,6 +7,8 @@ extern "C" {
 #endif
 typedef struct mth_store mth_store;
 mth_store* mth_create(int64_t ndocs, const int32_t* caps6);
+mth_store* mth_create_dl(int64_t ndocs, const int32_t* caps6, int32_t dcap);
+int64_t mth_deltas(mth_store* s, int64_t doc, int32_t* out, int64_t cap, uint64_t* hash);
 void mth_destroy(mth_store* s);
 void mth_start_collab(mth_store* s, int64_t doc, int32_t long_id, int32_t min_seq, int32_t cur_seq);
 int32_t mth_apply(mth_store* s, int64_t doc, const mt_op_rec* op, const uint16_t* text, const mt_props_rec* props,

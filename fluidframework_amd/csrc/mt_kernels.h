@@ -113,7 +113,8 @@ __device__ inline void skel_lite_move(SkelLite<HT>& k, HT& z, bool in) {
  * the heap (Skel, 3.5 KB for the small profile) are staged. */
 /* VAR tags a build variant compiled with other flags in its own translation unit (1: compiler-chosen
  * inlining): the kernel's name must differ, since a host launch resolves the kernel by name. */
-template <class HT, bool LDS, int MINW = 1, int SKM = 1, int VAR = 0> /* SKM: 1 Skel, 2 SkelLite, 0 none */
+/* DL: the delta-event build (engines created with caps.dcap > 0) */
+template <class HT, bool LDS, int MINW = 1, int SKM = 1, int VAR = 0, bool DL = false> /* SKM: 1 Skel, 2 SkelLite, 0 none */
 __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
         copy_image(&hot, g);
         __syncthreads();
         v.t = &hot;
-        Replica<WaveGPU, HT> r(v, WaveGPU());
+        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
         r.replay(p);
         r.commit();
 #ifdef MT_PROF
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
         __shared__ __attribute__((aligned(16))) SkelLite<HT> sk;
         skel_lite_move(sk, *v.t, true);
         __syncthreads();
-        Replica<WaveGPU, HT> r(v, WaveGPU());
+        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild;
         r.replay(p);
         r.commit();
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
         __shared__ __attribute__((aligned(16))) Skel<HT> sk;
         skel_move(sk, *v.t, true);
         __syncthreads();
-        Replica<WaveGPU, HT> r(v, WaveGPU());
+        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild, r.nlev = sk.nlevel;
         r.nsc = sk.nscour, r.hsq = sk.hseq, r.hrd = sk.hrid, r.hgn = sk.hgen;
         r.replay(p);
@@ -172,7 +173,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
             for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
 #endif
     } else {
-        Replica<WaveGPU, HT> r(v, WaveGPU());
+        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
         r.replay(p);
         r.commit();
 #ifdef MT_PROF
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
  * itself for the position-search scratch: per-chunk window deltas (NCH counters, all zero between
  * searches) and each window row's chunk position / leaf index / perspective length. The image, the
  * rope and the summaries stay in HBM (~0.2 GB per 1M-op document). */
-template <class HT>
+template <class HT, bool DL = false>
 __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                                      const int64_t* op_off, const uint16_t* text,
                                                      const int64_t* text_off, const mt_props_rec* props,
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     p.text = text + text_off[d];
     p.props = props + props_off[d];
     p.kv = kv + kv_off[d];
-    Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
+    Replica<WaveGPU, HT, DL> r(st.doc(d), WaveGPU());
     r.cdel = cdel;
     r.wcp = wcp;
     r.wvs = wvs;
@@ -345,6 +346,7 @@ struct mt_engine {
     const ProfOps* ops = nullptr; /* the profile's launchers (one translation unit per profile) */
     int device;
     int64_t ndocs;
+    int32_t dcap = 0; /* delta event log words per document (0: off) */
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
     bool noinline = false; /* small profile: compiler-chosen inlining (MT_REPLAY_NOINLINE=1) */

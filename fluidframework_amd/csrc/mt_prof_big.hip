@@ -1,7 +1,10 @@
 /* HotBig profile (16,384 nodes, HBM-resident, one wave per document) */
 #include "mt_kernels.h"
 
-static int32_t replay_big(mt_engine* e) { return launch_replay<HotBig>(e, k_replay<HotBig, false>); }
+static int32_t replay_big(mt_engine* e) {
+    if (e->dcap > 0) return launch_replay<HotBig>(e, k_replay<HotBig, false, 1, 1, 0, true>); /* delta events */
+    return launch_replay<HotBig>(e, k_replay<HotBig, false>);
+}
 
 const ProfOps* ops_big() {
     static const ProfOps t = Launch<HotBig>::table(replay_big);

@@ -1,7 +1,10 @@
 /* HotMid profile (2,048 nodes, HBM-resident, one wave per document) */
 #include "mt_kernels.h"
 
-static int32_t replay_mid(mt_engine* e) { return launch_replay<HotMid>(e, k_replay<HotMid, false>); }
+static int32_t replay_mid(mt_engine* e) {
+    if (e->dcap > 0) return launch_replay<HotMid>(e, k_replay<HotMid, false, 1, 1, 0, true>); /* delta events */
+    return launch_replay<HotMid>(e, k_replay<HotMid, false>);
+}
 
 const ProfOps* ops_mid() {
     static const ProfOps t = Launch<HotMid>::table(replay_mid);

@@ -24,12 +24,14 @@ extern "C" {
 int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_engine** out) {
     if (!out || !caps || ndocs < 1 || ndocs > (int64_t)0x7fffffff) return MT_E_ARG;
     *out = nullptr;
-    Caps k = {caps->acap, caps->mcap, caps->gcap};
+    Caps k = {caps->acap, caps->mcap, caps->gcap, caps->dcap};
     int prof = profile_for(caps->ncap);
-    if (!caps_valid(k) || prof < 0 || caps->ccap > 254) return MT_E_ARG; /* short ids are bytes; 0xFF = LocalClientId */
+    if (!caps_valid(k) || prof < 0 || caps->ccap > 254 || caps->dcap < 0)
+        return MT_E_ARG; /* short ids are bytes; 0xFF = LocalClientId */
     mt_engine* e = new mt_engine();
     e->device = device;
     e->ndocs = ndocs;
+    e->dcap = caps->dcap;
     const char* g = getenv("MT_REPLAY_LDS");
     e->lds = g && g[0] == '1';
     /* Occupancy of the HBM-resident small-profile kernel: documents are replayed one per wave and
@@ -331,6 +333,53 @@ int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t g
     if (!r[0]) return MT_E_ARG;
     *out = r[1];
     return MT_OK;
+}
+
+/* the delta region of every document: offset inside a document's block, and the block stride */
+static void delta_geometry(const mt_engine* e, int64_t* off, int64_t* stride) {
+    switch (e->profile) {
+    case 0: *off = Doc<HotSmall>::off_dl(e->s0.caps), *stride = e->s0.stride; break;
+    case 1: *off = Doc<HotMid>::off_dl(e->s1.caps), *stride = e->s1.stride; break;
+    case 3: *off = Doc<HotMat>::off_dl(e->s3.caps), *stride = e->s3.stride; break;
+    case 4: *off = Doc<HotHuge>::off_dl(e->s4.caps), *stride = e->s4.stride; break;
+    default: *off = Doc<HotBig>::off_dl(e->s2.caps), *stride = e->s2.stride; break;
+    }
+}
+
+int32_t mt_engine_delta_state(mt_engine* e, int64_t* n_out, uint64_t* hash_out) {
+    if (!e || e->dcap <= 0) return MT_E_ARG;
+    HIPCHK(e, hipSetDevice(e->device));
+    int64_t off, stride;
+    delta_geometry(e, &off, &stride);
+    std::vector<DState> st((size_t)e->ndocs);
+    /* one strided copy: the DState at the head of each document's delta region */
+    HIPCHK(e, hipMemcpy2DAsync(st.data(), sizeof(DState), (const uint8_t*)e->mem + off, (size_t)stride, sizeof(DState),
+                               (size_t)e->ndocs, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    for (int64_t d = 0; d < e->ndocs; d++) {
+        if (n_out) n_out[d] = st[d].n;
+        if (hash_out) hash_out[d] = st[d].h;
+    }
+    return MT_OK;
+}
+
+int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap) {
+    if (!e || e->dcap <= 0 || doc < 0 || doc >= e->ndocs || cap < 0) return -MT_E_ARG;
+    if (hipSetDevice(e->device) != hipSuccess) return -MT_E_HIP;
+    int64_t off, stride;
+    delta_geometry(e, &off, &stride);
+    const uint8_t* base = (const uint8_t*)e->mem + doc * stride + off;
+    DState st;
+    if (hipMemcpyAsync(&st, base, sizeof st, hipMemcpyDeviceToHost, e->stream) != hipSuccess) return -MT_E_HIP;
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
+    int64_t logged = st.n < e->dcap ? st.n : e->dcap;
+    int64_t m = logged < cap ? logged : cap;
+    if (out && m > 0) {
+        if (hipMemcpyAsync(out, base + sizeof(DState), 4 * (size_t)m, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+            return -MT_E_HIP;
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
+    }
+    return logged;
 }
 
 #ifdef MT_PROF

@@ -31,7 +31,7 @@ class SegRef(ctypes.Structure):
 
 
 class _Caps(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_int32) for n in ("ncap", "hcap", "acap", "mcap", "gcap", "ccap")]
+    _fields_ = [(n, ctypes.c_int32) for n in ("ncap", "hcap", "acap", "mcap", "gcap", "ccap", "dcap")]
 
 
 _LIB = None
@@ -69,6 +69,9 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_stats.argtypes = [vp, vp]
         L.mt_engine_get_containing_segment.argtypes = [vp, i64, i32, i32, i32, ctypes.POINTER(SegRef)]
         L.mt_engine_get_position.argtypes = [vp, i64, i32, i32, i32, i32, ctypes.POINTER(i32)]
+        L.mt_engine_delta_state.argtypes = [vp, vp, vp]
+        L.mt_engine_deltas.argtypes = [vp, i64, vp, i64]
+        L.mt_engine_deltas.restype = i64
         L.mt_engine_ndocs.argtypes = [vp]
         L.mt_engine_ndocs.restype = i64
         _LIB = L
@@ -97,7 +100,9 @@ def default_caps(ops_per_doc: int, config: int = 3) -> dict:
 
 
 class Engine:
-    """A batch of `ndocs` replicas on HIP device `device`."""
+    """A batch of `ndocs` replicas on HIP device `device`. caps["dcap"] > 0 turns on the delta event
+    stream (include/mt_oplog.h MT_DELTA_*: what SharedString "sequenceDelta" / "maintenance"
+    listeners see), logging up to dcap words per document."""
 
     def __init__(self, ndocs: int, device: int = 0, **caps):
         c = default_caps(0)
@@ -212,6 +217,22 @@ class Engine:
         self._check(self.L.mt_engine_get_position(self.h, doc, seg.rid, seg.gen, ref_seq, long_client, ctypes.byref(v)),
                     "get_position")
         return v.value
+
+    def delta_state(self):
+        """Per doc (words emitted since create/reset, FNV-1a-64 of them) of the delta stream."""
+        n = np.zeros(self.ndocs, np.int64)
+        h = np.zeros(self.ndocs, np.uint64)
+        self._check(self.L.mt_engine_delta_state(self.h, _p(n), _p(h)), "delta_state")
+        return n, h
+
+    def deltas(self, doc: int) -> np.ndarray:
+        """The logged delta-stream words of one document (at most dcap)."""
+        n = self.L.mt_engine_deltas(self.h, doc, None, 0)
+        if n < 0:
+            raise EngineError(f"deltas failed {n}")
+        buf = np.zeros(max(n, 1), np.int32)
+        self.L.mt_engine_deltas(self.h, doc, _p(buf), n)
+        return buf[:n]
 
     def stats(self) -> np.ndarray:
         out = np.zeros((self.ndocs, 4), np.int32)

@@ -52,6 +52,48 @@ class Interner {
     }
 }
 
+/* MergeTreeDeltaType / MergeTreeMaintenanceType names of the delta stream's op words (include/mt_oplog.h) */
+const DELTA_OPS = { 0: "INSERT", 1: "REMOVE", 2: "ANNOTATE", "-1": "APPEND", "-2": "SPLIT", "-3": "UNLINK" };
+
+/* Decode a document's delta-stream words (include/mt_oplog.h MT_DELTA_*) into the events a SharedString
+ * "sequenceDelta" (INSERT / REMOVE / ANNOTATE) or "maintenance" (APPEND / SPLIT / UNLINK) listener
+ * receives (sequence.ts:136-150; SequenceDeltaEvent.ranges, sequenceDeltaEvent.ts:40-50): per event the
+ * operation, the seq of the message (-1: local edit) and per delta segment its position (delta events),
+ * length and propertyDeltas (annotate). */
+function decodeDeltas(words, interner) {
+    const END = -0x80000000; // MT_DELTA_END: no position or length takes this value
+    const keyName = new Map([...interner.keys].map(([k, i]) => [i, k]));
+    const valueOf = new Map([...interner.values].map(([v, i]) => [i, JSON.parse(v)]));
+    const events = [];
+    let i = 0;
+    while (i < words.length) {
+        const op = words[i], seq = words[i + 1];
+        i += 2;
+        const deltaSegments = [];
+        while (words[i] !== END) {
+            const pos = words[i], length = words[i + 1], nd = words[i + 2];
+            i += 3;
+            const seg = { position: pos < 0 ? undefined : pos, length };
+            if (op === 2) {
+                if (nd < 0) {
+                    seg.propertyDeltas = undefined; // addProperties was blocked by pending local rewrites
+                } else {
+                    seg.propertyDeltas = {};
+                    for (let k = 0; k < nd; k++, i++) {
+                        const w = words[i] >>> 0, v = w & 0xffff;
+                        seg.propertyDeltas[keyName.get(w >>> 16)] = v === 0 ? null : valueOf.get(v & ~VALUE_FALSY);
+                    }
+                }
+            }
+            deltaSegments.push(seg);
+        }
+        if (words[i + 1] !== deltaSegments.length) throw new Error(`malformed delta stream at word ${i}`);
+        i += 2;
+        events.push({ operation: DELTA_OPS[op], seq, deltaSegments });
+    }
+    return events;
+}
+
 class DocQueue {
     constructor() { this.recs = []; this.text = []; this.props = []; this.kv = []; }
 }
@@ -244,6 +286,10 @@ class GpuClient {
 
     /* Client.getPosition (client.ts:291) of a handle from getContainingSegment */
     getPosition(segment) { return addon.getPosition(this.read(), this.doc, segment.rid, segment.gen, 0, -1); }
+
+    /* Every "sequenceDelta" / "maintenance" event this replica has fired since the engine was created
+     * (engines created with caps.dcap > 0), decoded (decodeDeltas) */
+    deltaEvents() { return decodeDeltas(addon.deltas(this.read(), this.doc), this.engine.interner); }
 }
 
-module.exports = { ReplayEngine, GpuClient, Interner, addon, OP, DEFAULT_CAPS };
+module.exports = { ReplayEngine, GpuClient, Interner, addon, OP, DEFAULT_CAPS, decodeDeltas };

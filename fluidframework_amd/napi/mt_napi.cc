@@ -99,13 +99,20 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
     int32_t device;
     int64_t ndocs;
     if (!i32_of(env, argv[0], &device) || !i64_of(env, argv[1], &ndocs)) return nullptr;
-    mt_caps caps;
+    mt_caps caps = {};
     const char* names[6] = {"ncap", "hcap", "acap", "mcap", "gcap", "ccap"};
     int32_t* fields[6] = {&caps.ncap, &caps.hcap, &caps.acap, &caps.mcap, &caps.gcap, &caps.ccap};
     for (int i = 0; i < 6; i++) {
         napi_value f;
         NAPI_OK(napi_get_named_property(env, argv[2], names[i], &f));
         if (!i32_of(env, f, fields[i])) return nullptr;
+    }
+    bool has_dcap = false; /* optional: delta event log words per doc (mt_caps.dcap) */
+    NAPI_OK(napi_has_named_property(env, argv[2], "dcap", &has_dcap));
+    if (has_dcap) {
+        napi_value f;
+        NAPI_OK(napi_get_named_property(env, argv[2], "dcap", &f));
+        if (!i32_of(env, f, &caps.dcap)) return nullptr;
     }
     mt_engine* e = nullptr;
     int32_t rc = mt_engine_create(device, ndocs, &caps, &e);
@@ -214,6 +221,26 @@ static napi_value js_digests(napi_env env, napi_callback_info info) {
     return ta;
 }
 
+/* deltas(h, doc) -> Int32Array: the doc's logged delta-stream words (include/mt_oplog.h MT_DELTA_*) */
+static napi_value js_deltas(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    if (!e || !i64_of(env, argv[1], &doc)) return nullptr;
+    int64_t n = mt_engine_deltas(e, doc, nullptr, 0);
+    if (n < 0) return throw_status(env, e, (int32_t)-n, "mt_engine_deltas");
+    std::vector<int32_t> tmp((size_t)(n > 0 ? n : 1));
+    int64_t m = mt_engine_deltas(e, doc, tmp.data(), n);
+    if (m < 0) return throw_status(env, e, (int32_t)-m, "mt_engine_deltas");
+    napi_value ab, ta;
+    void* p;
+    NAPI_OK(napi_create_arraybuffer(env, 4 * (size_t)m, &p, &ab));
+    memcpy(p, tmp.data(), 4 * (size_t)m);
+    NAPI_OK(napi_create_typedarray(env, napi_int32_array, (size_t)m, ab, 0, &ta));
+    return ta;
+}
+
 /* getLength(h, doc, refSeq, longClient) -> number (longClient < 0: Client.getLength) */
 static napi_value js_get_length(napi_env env, napi_callback_info info) {
     napi_value argv[4];
@@ -309,7 +336,8 @@ static napi_value init(napi_env env, napi_value exports) {
                {"run", js_run},             {"sync", js_sync},                {"reset", js_reset},
                {"errors", js_errors},       {"digests", js_digests},          {"getLength", js_get_length},
                {"getText", js_get_text},    {"getContainingSegment", js_get_containing},
-               {"getPosition", js_get_position}, {"ndocs", js_ndocs},        {"lastRunMs", js_last_run_ms}};
+               {"getPosition", js_get_position}, {"ndocs", js_ndocs},        {"lastRunMs", js_last_run_ms},
+               {"deltas", js_deltas}};
     for (auto& f : fns) {
         napi_value fn;
         NAPI_OK(napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn));

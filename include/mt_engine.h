@@ -31,6 +31,7 @@ typedef struct mt_caps {
     int32_t mcap; /* pending segment-group membership log entries                       */
     int32_t gcap; /* pending local ops (segment groups) in flight                       */
     int32_t ccap; /* distinct clients per doc (<= 254)                                  */
+    int32_t dcap; /* delta event log words per doc; 0 = no delta events (mt_oplog.h)   */
 } mt_caps;
 
 /* status codes */
@@ -112,6 +113,13 @@ int32_t mt_engine_get_containing_segment(mt_engine* e, int64_t doc, int32_t pos,
  * MT_E_ARG if the handle no longer resolves. long_client < 0 = Client.getPosition (client.ts:291). */
 int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t gen, int32_t ref_seq,
                                int32_t long_client, int32_t* out);
+/* Delta events (mt_oplog.h MT_DELTA_*; engines created with caps.dcap > 0): the stream a
+ * SharedString "sequenceDelta" + "maintenance" listener would see (sequence.ts:136-150), batched.
+ * mt_engine_delta_state: per doc the words emitted since create/reset (n_out, may exceed dcap) and
+ * their FNV-1a-64 (hash_out). mt_engine_deltas: one doc's logged words, the first min(n, dcap); writes
+ * at most cap of them and returns how many are logged (<0 on error). */
+int32_t mt_engine_delta_state(mt_engine* e, int64_t* n_out, uint64_t* hash_out);
+int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap);
 /* Per-doc counters: nleaf, high-water row slots, high-water heap, events applied. */
 int32_t mt_engine_stats(mt_engine* e, int32_t* out4_per_doc);
 int64_t mt_engine_ndocs(const mt_engine* e);

@@ -132,6 +132,35 @@ enum {
 #define MT_FNV_OFFSET 0xcbf29ce484222325ULL
 #define MT_FNV_PRIME 0x100000001b3ULL
 
+/* ---- delta event stream (per document, int32 words; enabled by mt_caps.dcap > 0) ---------------
+ * One event per reference callback, in the order the reference fires them while a replica applies
+ * its event stream: mergeTreeDeltaCallback (INSERT mergeTree.ts:2014-2021, ANNOTATE 2625-2631,
+ * REMOVE 2738-2744; what SharedString turns into "sequenceDelta", sequence.ts:136-143) and
+ * mergeTreeMaintenanceCallback (SPLIT 2264-2269, APPEND 1368-1373, UNLINK 1343-1348; SharedString
+ * "maintenance", sequence.ts:144-150). Snapshot-load records emit nothing (the reference loads with
+ * opArgs undefined).
+ *   event:   int32 op (MT_DELTA_*), int32 seq (of the record being applied; -1 for a local edit),
+ *            then per delta segment: int32 pos, int32 len, int32 nd, nd x int32 (key << 16 | value),
+ *            then int32 MT_DELTA_END (no position or length takes that value), int32 nseg.
+ *   pos:     Client.getPosition(segment) (client.ts:291, the local view) at callback time for
+ *            INSERT / REMOVE / ANNOTATE (what SequenceDeltaEvent.ranges reports,
+ *            sequenceDeltaEvent.ts:40-50); -1 for maintenance events.
+ *   len:     segment.cachedLength at callback time.
+ *   nd:      ANNOTATE: the number of propertyDeltas entries (segmentPropertiesManager.ts:35-111),
+ *            -1 when addProperties returned undefined; 0 otherwise. Entries sorted by key id; value
+ *            0 = null (the key was absent), else the value id as in the canonical dump.
+ * The engine folds every word (little-endian bytes) into a per-document FNV-1a-64, also past the
+ * log's capacity, so a full-size run is verified by digest alone. */
+enum {
+    MT_DELTA_INSERT = 0,
+    MT_DELTA_REMOVE = 1,
+    MT_DELTA_ANNOTATE = 2,
+    MT_DELTA_APPEND = -1, /* MergeTreeMaintenanceType (mergeTreeDeltaCallback.ts:16-30) */
+    MT_DELTA_SPLIT = -2,
+    MT_DELTA_UNLINK = -3,
+};
+#define MT_DELTA_END ((int32_t)0x80000000) /* ends an event's segment list */
+
 #ifdef __cplusplus
 }
 #endif

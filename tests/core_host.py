@@ -22,6 +22,10 @@ def lib():
         vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
         L.mth_create.restype = vp
         L.mth_create.argtypes = [i64, vp]
+        L.mth_create_dl.restype = vp
+        L.mth_create_dl.argtypes = [i64, vp, i32]
+        L.mth_deltas.argtypes = [vp, i64, vp, i64, vp]
+        L.mth_deltas.restype = i64
         L.mth_destroy.argtypes = [vp]
         L.mth_start_collab.argtypes = [vp, i64, i32, i32, i32]
         L.mth_apply.argtypes = [vp, i64, vp, vp, vp, vp]
@@ -50,10 +54,10 @@ DEFAULT_CAPS = (192, 256, 1 << 16, 4096, 1024, 64)
 
 
 class HostStore:
-    def __init__(self, ndocs: int, caps=DEFAULT_CAPS):
+    def __init__(self, ndocs: int, caps=DEFAULT_CAPS, dcap: int = 0):
         self.L = lib()
         self.caps = np.asarray(caps, np.int32)
-        self.h = self.L.mth_create(ndocs, _p(self.caps))
+        self.h = self.L.mth_create_dl(ndocs, _p(self.caps), dcap)
         if not self.h:
             raise RuntimeError("mth_create failed")
         self.ndocs = ndocs
@@ -98,15 +102,23 @@ class HostStore:
         self.L.mth_containing(self.h, doc, pos, ref_seq, long_client, _p(out))
         return tuple(int(x) for x in out)
 
+    def deltas(self, doc):
+        """(words emitted, FNV-1a-64 of them, the logged words) of the doc's delta stream"""
+        h = np.zeros(1, np.uint64)
+        n = self.L.mth_deltas(self.h, doc, None, 0, _p(h))
+        buf = np.zeros(max(n, 1), np.int32)
+        self.L.mth_deltas(self.h, doc, _p(buf), n, _p(h))
+        return int(n), int(h[0]), buf[:n]
+
     def stats(self, doc):
         out = np.zeros(8, np.int32)
         self.L.mth_stats(self.h, doc, _p(out))
         return dict(zip(("nleaf", "hw_slots", "hw_heap", "heap", "mem", "arena_top", "nodes", "ops"), out.tolist()))
 
 
-def replay_batch(batch: ol.Batch, caps=DEFAULT_CAPS):
+def replay_batch(batch: ol.Batch, caps=DEFAULT_CAPS, dcap: int = 0):
     """Replay every document of a batch on the host core; returns (digests, errors, store)."""
-    st = HostStore(batch.ndocs, caps)
+    st = HostStore(batch.ndocs, caps, dcap)
     dig = np.zeros(batch.ndocs, np.uint64)
     err = np.zeros(batch.ndocs, np.int32)
     for d in range(batch.ndocs):

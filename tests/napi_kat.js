@@ -4,7 +4,7 @@
 // the GPU. Run by tests/test_napi.py (GPU tier); prints one JSON line of results.
 //   client.applyMsg.spec.ts:17-21 (setup), 88-98 (insert ack), 100-110 (remove ack),
 //   261-290 (intersecting insert after local delete), mergeTree.markRangeRemoved.spec.ts:25-44.
-const { ReplayEngine } = require("../fluidframework_amd/js/mergetree_gpu.js");
+const { ReplayEngine, DEFAULT_CAPS } = require("../fluidframework_amd/js/mergetree_gpu.js");
 
 const out = {};
 const eng = new ReplayEngine(4);
@@ -52,4 +52,16 @@ out.groupReplace = c[3].getText();
 out.groupLength = c[3].getLength();
 
 out.digests = Array.from(eng.digests(), (x) => x.toString(16));
+
+// delta events (include/mt_oplog.h), as a SharedString "sequenceDelta" / "maintenance" listener sees them
+const deng = new ReplayEngine(1, { ...DEFAULT_CAPS, dcap: 4096 });
+const dc = deng.client(0);
+deng.startCollaboration(["me"]);
+dc.applyMsg({ clientId: "B", sequenceNumber: 1, referenceSequenceNumber: 0, minimumSequenceNumber: 0,
+    type: "op", contents: { type: 0, pos1: 0, seg: "hello world" } });
+dc.applyMsg({ clientId: "B", sequenceNumber: 2, referenceSequenceNumber: 1, minimumSequenceNumber: 0,
+    type: "op", contents: { type: 2, pos1: 0, pos2: 5, props: { bold: true } } });
+dc.applyMsg({ clientId: "B", sequenceNumber: 3, referenceSequenceNumber: 2, minimumSequenceNumber: 0,
+    type: "op", contents: { type: 1, pos1: 5, pos2: 6 } });
+out.deltas = dc.deltaEvents();
 console.log(JSON.stringify(out));

@@ -232,12 +232,51 @@ def sn_blobs(tree):
     return sn._blobs(tree)
 
 
+def words_fnv(w: np.ndarray) -> int:
+    return fnv1a64(np.ascontiguousarray(w, "<i4").tobytes())
+
+
+def make_deltas(names, node: str) -> None:
+    """tests/golden/refdelta_<set>.npz: the reference's delta / maintenance callback stream
+    (include/mt_oplog.h MT_DELTA_*, recorded by ref_replay.mjs --deltas) for every document of the set:
+    per-document word counts and FNV-1a-64 of the words, and the full streams of the first documents."""
+    for name in names:
+        w, ids = SETS[name]
+        b = gen.generate(w, ids=ids, threads=8)
+        d = os.path.join(SCRATCH, name + "_deltas")
+        write_batch(b, gen.generator_interner(), d)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d, "--deltas"],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+        errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
+        if errs:
+            raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
+        words = np.fromfile(os.path.join(d, "ref_deltas.bin"), "<i4")
+        off = np.fromfile(os.path.join(d, "ref_delta_off.bin"), "<i8")
+        per = [words[off[i]: off[i + 1]] for i in range(b.ndocs)]
+        keep = min(2, b.ndocs)  # full streams of the first two documents
+        np.savez_compressed(
+            os.path.join(GOLDEN, f"refdelta_{name}.npz"),
+            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(b),
+            nwords=np.diff(off).astype(np.int64), hashes=np.asarray([words_fnv(x) for x in per], np.uint64),
+            keep_words=np.concatenate(per[:keep]).astype(np.int32), keep_off=off[: keep + 1].astype(np.int64),
+            source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                    "tools/ref_replay.mjs --deltas: mergeTreeDeltaCallback / mergeTreeMaintenanceCallback"),
+        )
+        print(f"refdelta_{name}: {b.ndocs} docs, {int(off[-1])} words", flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default=",".join(SETS))
     ap.add_argument("--node", default="node")
+    ap.add_argument("--deltas", action="store_true", help="write the delta-stream fixtures (refdelta_*.npz) only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
+    if args.deltas:
+        make_deltas([n for n in args.sets.split(",") if n in SETS], args.node)
+        return
     import oracle_client as oc
     if "snap_body" in args.sets.split(","):
         make_snap_body(args.node)

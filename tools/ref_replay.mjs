@@ -15,6 +15,10 @@ import path from "path";
 
 const [erased, dir] = process.argv.slice(2);
 const timeOnly = process.argv.includes("--time");
+// --deltas: also record every mergeTreeDeltaCallback / mergeTreeMaintenanceCallback the replica fires
+// (the stream SharedString's "sequenceDelta" / "maintenance" listeners see, sequence.ts:136-150) in the
+// word format of include/mt_oplog.h (MT_DELTA_*) -> batch-dir/ref_deltas.bin + ref_delta_off.bin
+const withDeltas = process.argv.includes("--deltas");
 let Client, TextSegment, Marker, PermutationSegment, SnapshotV1; // bound in main() (Node 12 has no top-level await)
 
 const rd = (f) => fs.readFileSync(path.join(dir, f));
@@ -92,12 +96,14 @@ const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPe
 
 // apply records [from, to) of `doc` to `client` (applyMsg / the local-edit entry points)
 let applying = -1; // the record being applied (for error reports)
+let curSeq = 0; // seq of the record being applied (-1: a local edit), the delta stream's event seq
 function applyRange(client, doc, from, to) {
     let members = []; // members of a group message so far (records flagged GROUPED, mt_oplog.h)
     for (let i = from; i < to; i++) {
         applying = i;
         const rec = record(i);
         const kind = rec.kind & 7;
+        curSeq = rec.kind & 0x80 ? -1 : rec.seq;
         if (rec.kind & 0x80) { // local edit: insertSegmentLocal / removeRangeLocal / annotateRangeLocal
             if (kind === 0) {
                 const ps = propSet(doc, rec.props);
@@ -123,8 +129,44 @@ function applyRange(client, doc, from, to) {
     }
 }
 
-function replayDoc(doc, to = opOff[doc + 1]) {
+// the delta stream (include/mt_oplog.h): per callback op, seq, per delta segment (position in the
+// local view for delta events, -1 for maintenance; cachedLength; property deltas by key id), count
+function valueWord(v) {
+    if (v === null || v === undefined) return 0;
+    const id = valueId.get(canonical(v));
+    if (id === undefined) throw new Error(`property value not in the interner: ${canonical(v)}`);
+    return id | (v !== null && typeof v !== "object" && !v ? FALSY : 0);
+}
+const END = -0x80000000; // MT_DELTA_END
+function hookDeltas(client, words) {
+    client.mergeTreeDeltaCallback = (opArgs, args) => {
+        words.push(args.operation, curSeq);
+        for (const d of args.deltaSegments) {
+            words.push(client.getPosition(d.segment), d.segment.cachedLength);
+            if (args.operation !== 2) { words.push(0); continue; }
+            if (d.propertyDeltas === undefined) { words.push(-1); continue; }
+            const pd = Object.keys(d.propertyDeltas).map((k) => [keyId.get(k), valueWord(d.propertyDeltas[k])])
+                .sort((a, b) => a[0] - b[0]);
+            words.push(pd.length);
+            for (const [k, v] of pd) words.push(((k << 16) | v) | 0);
+        }
+        words.push(END, args.deltaSegments.length);
+    };
+    client.mergeTreeMaintenanceCallback = (args) => {
+        words.push(args.operation, curSeq);
+        for (const d of args.deltaSegments) words.push(-1, d.segment.cachedLength, 0);
+        words.push(END, args.deltaSegments.length);
+    };
+}
+const deltaWords = [];
+
+function replayDoc(doc, to = opOff[doc + 1], deltas = false) {
     const client = new Client(specToSegment, logger);
+    if (deltas) {
+        const words = [];
+        deltaWords[doc] = words;
+        hookDeltas(client, words);
+    }
     const local = localIds.readInt32LE(4 * doc);
     if (local >= 0) client.startOrUpdateCollaboration(name(local));
     applyRange(client, doc, opOff[doc], to);
@@ -240,7 +282,7 @@ const t0 = process.hrtime.bigint();
 const dumps = [], errs = {};
 for (let d = 0; d < ndocs; d++) {
     try {
-        const c = replayDoc(d);
+        const c = replayDoc(d, opOff[d + 1], withDeltas);
         for (const [qd, pos, ref, cl] of queries) {
             if (qd !== d) continue;
             const mt = c.mergeTree;
@@ -288,6 +330,22 @@ if (!timeOnly) {
     off.writeBigInt64LE(BigInt(acc), 8 * ndocs);
     fs.writeFileSync(path.join(dir, "ref_dumps.bin"), Buffer.concat(dumps));
     fs.writeFileSync(path.join(dir, "ref_dump_off.bin"), off);
+}
+if (withDeltas) {
+    const off = Buffer.alloc(8 * (ndocs + 1));
+    const parts = [];
+    let acc = 0;
+    for (let d = 0; d < ndocs; d++) {
+        const w = deltaWords[d] || [];
+        const b = Buffer.alloc(4 * w.length);
+        w.forEach((x, i) => b.writeInt32LE(x, 4 * i));
+        parts.push(b);
+        off.writeBigInt64LE(BigInt(acc), 8 * d);
+        acc += w.length;
+    }
+    off.writeBigInt64LE(BigInt(acc), 8 * ndocs);
+    fs.writeFileSync(path.join(dir, "ref_deltas.bin"), Buffer.concat(parts));
+    fs.writeFileSync(path.join(dir, "ref_delta_off.bin"), off);
 }
 fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
 if (queries.length) fs.writeFileSync(path.join(dir, "ref_answers.json"), JSON.stringify(answers));
