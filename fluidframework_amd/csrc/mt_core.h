@@ -81,6 +81,7 @@ struct Caps {
     int32_t mcap; /* segment-group membership log entries */
     int32_t gcap; /* pending segment groups (local ops in flight) */
     int32_t dcap; /* delta event log words (0 = delta events off; mt_oplog.h MT_DELTA_*) */
+    int32_t rcap; /* local references (0 = none; mt_oplog.h MT_OP_REF) */
 };
 
 /* delta event stream state at the head of a document's delta region (mt_oplog.h) */
@@ -89,7 +90,21 @@ struct alignas(16) DState {
     uint64_t h;  /* FNV-1a-64 of every emitted word */
     int32_t seq; /* seq of the record being applied (-1: local edit) */
     int32_t on;  /* 0 while a snapshot-load record applies */
-    int32_t _p[2];
+    int32_t nref;  /* local references created */
+    int32_t ncoll; /* segments holding a LocalReferenceCollection (LColl) */
+};
+/* a local reference (localReference.ts:20-117): the row id of its segment (-1: detached), its offset
+ * in the segment and its ReferenceType */
+struct alignas(16) LRef {
+    int32_t rid, off, type, _p;
+};
+enum : int32_t { REF_DETACHED = -1, REF_SAVED = -2 /* on a row the current remove took (mergeTree.ts:2673-2676) */ };
+/* a segment's LocalReferenceCollection: its row id and refsByOffset.length, which is what an append adds
+ * to the offsets of the references it takes over (localReference.ts:211-223). That length follows the
+ * JavaScript array, not the segment: set at creation, cut by a split, extended by appends and by
+ * assignments past its end, and left alone when the segment grows by a reference-free append. */
+struct LColl {
+    int32_t rid, len;
 };
 
 /* per-document scalar header */
@@ -280,13 +295,22 @@ struct Doc {
     MT_HD static int64_t off_mgid(const Caps& c) { return OFF_ARENA + align256c(4 * (int64_t)c.acap); }
     MT_HD static int64_t off_mrid(const Caps& c) { return off_mgid(c) + align256c(4 * (int64_t)c.mcap); }
     MT_HD static int64_t off_gq(const Caps& c) { return off_mrid(c) + align256c(4 * (int64_t)c.mcap); }
-    /* delta region (only when c.dcap > 0): DState, then dcap words */
+    /* client-feature region (only when c.dcap > 0 or c.rcap > 0): DState, dcap delta-log words, rcap
+     * local references */
+    MT_HD static bool has_fx(const Caps& c) { return c.dcap > 0 || c.rcap > 0; }
     MT_HD static int64_t off_dl(const Caps& c) { return off_gq(c) + align256c(4 * (int64_t)c.gcap); }
+    MT_HD static int64_t off_refs(const Caps& c) {
+        return off_dl(c) + (int64_t)sizeof(DState) + ((4 * (int64_t)c.dcap + 15) & ~(int64_t)15);
+    }
+    MT_HD static int64_t off_coll(const Caps& c) { return off_refs(c) + (int64_t)sizeof(LRef) * c.rcap; }
+    MT_HD static int32_t coll_cap(const Caps& c) { return 4 * c.rcap; }
     MT_HD static int64_t stride(const Caps& c) {
-        return off_dl(c) + (c.dcap > 0 ? align256c((int64_t)sizeof(DState) + 4 * (int64_t)c.dcap) : 0);
+        return has_fx(c) ? align256c(off_coll(c) + (int64_t)sizeof(LColl) * coll_cap(c)) : off_dl(c);
     }
     MT_HD DState* dstate() const { return (DState*)(b + off_dl(caps)); }
     MT_HD int32_t* dlog() const { return (int32_t*)(b + off_dl(caps) + (int64_t)sizeof(DState)); }
+    MT_HD LRef* refs() const { return (LRef*)(b + off_refs(caps)); }
+    MT_HD LColl* colls() const { return (LColl*)(b + off_coll(caps)); }
     MT_HD typename HT::Cold* cold() const { return (typename HT::Cold*)(b + OFF_COLD); } /* HT::S records */
     MT_HD typename HT::IX* frid() const { return (typename HT::IX*)(b + OFF_FRID); } /* free row-id stack */
     MT_HD uint16_t* arena() const { return (uint16_t*)(b + OFF_ARENA); } /* 2 * acap */
@@ -307,7 +331,8 @@ struct Pools {
 /* Phase clock for the profiling build only (-DMT_PROF, tools/phase_profile.py): shader-clock
  * cycles accumulated per phase in registers and written out per document. */
 enum { PH_APPLY, PH_ZAMBONI, PH_FIND, PH_MAP, PH_SPLIT, PH_ACK, PH_TEXT, PH_HEAP, PH_SCOUR, PH_PACK, PH_APPEND,
-       PH_CAND, PH_S1, PH_S2, PH_S3, PH_P1, PH_P2, PH_INSROW, PH_LEAFINS, PH_N };
+       PH_CAND, PH_S1, PH_S2, PH_S3, PH_P1, PH_P2, PH_INSROW, PH_LEAFINS,
+       PH_WIN, PH_TFIND, PH_LFIND, PH_ROPE, PH_RESTAT, PH_N }; /* the last five: tiled profile */
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {
     uint64_t* acc;
@@ -512,12 +537,14 @@ struct Replica {
             int32_t i = b + w.lane();
             if (i < HT::C) z.l2s[i] = 0xFF;
         }
-        if (d.caps.dcap > 0) {
+        if (Doc<HT>::has_fx(d.caps)) {
             DState* st = d.dstate();
             st->n = 0;
             st->h = MT_FNV_OFFSET;
             st->seq = 0;
             st->on = 1;
+            st->nref = 0;
+            st->ncoll = 0;
         }
         w.sync();
     }
@@ -556,6 +583,169 @@ struct Replica {
         dput(len);
         dput(0);
     }
+    /* ---- local references (§8 f4; mt_oplog.h MT_OP_REF, localReference.ts) ------------------- */
+    MT_HD bool refs_on() const {
+        if constexpr (!DL)
+            return false;
+        else
+            return d.caps.rcap > 0 && d.dstate()->nref > 0;
+    }
+    /* the references on row id `from` at offset >= o0 move to row id `to`, offset + delta (split:
+     * LocalReferenceCollection.split, localReference.ts:225-241; append: 211-223; to < 0 marks them) */
+    MT_HD int32_t refs_move(int32_t from, int32_t o0, int32_t to, int32_t delta) {
+        LRef* R = d.refs();
+        int32_t n = d.dstate()->nref, moved = 0;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            bool mv = i < n && R[i].rid == from && R[i].off >= o0;
+            if (mv) {
+                R[i].rid = to;
+                R[i].off += delta;
+            }
+            moved += w.sum(mv ? 1 : 0);
+        }
+        w.sync();
+        return moved;
+    }
+    /* the LocalReferenceCollection of row id `rid`: its index in the table, or -1 */
+    MT_HD int32_t coll_find(int32_t rid) {
+        LColl* C = d.colls();
+        int32_t n = d.dstate()->ncoll;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            uint64_t m = w.ballot(i < n && C[i].rid == rid);
+            if (m) return b + W::ffs(m);
+        }
+        return -1;
+    }
+    /* `new LocalReferenceCollection(segment)` unless it has one: refsByOffset.length = its length now */
+    MT_HD int32_t coll_get(int32_t rid, int32_t len) {
+        int32_t i = coll_find(rid);
+        if (i >= 0) return i;
+        DState* st = d.dstate();
+        i = st->ncoll;
+        if (i >= Doc<HT>::coll_cap(d.caps)) {
+            fail(E_CAPACITY);
+            return -1;
+        }
+        LColl c = {rid, len};
+        d.colls()[i] = c;
+        st->ncoll = i + 1;
+        return i;
+    }
+    MT_HD void coll_drop(int32_t rid) { /* segment.localRefs = undefined, or the segment left the tree */
+        int32_t i = coll_find(rid);
+        if (i < 0) return;
+        DState* st = d.dstate();
+        int32_t n = st->ncoll - 1;
+        d.colls()[i] = d.colls()[n];
+        st->ncoll = n;
+    }
+    MT_HD int32_t refs_on_row(int32_t rid) { /* LocalReferenceCollection.refCount of the row's collection */
+        LRef* R = d.refs();
+        int32_t n = d.dstate()->nref, c = 0;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            c += w.sum(i < n && R[i].rid == rid ? 1 : 0);
+        }
+        return c;
+    }
+    /* splitAt -> localRefs.split(pos, next) (mergeTree.ts:561-563, localReference.ts:225-241): a
+     * non-empty collection hands its references at offsets >= pos, and refsByOffset.splice(pos) of its
+     * array, to a new collection of the right part */
+    MT_HD void refs_split(int32_t lrid, int32_t rrid, int32_t pos) {
+        int32_t i = coll_find(lrid);
+        if (i < 0 || refs_on_row(lrid) == 0) return;
+        int32_t cl = d.colls()[i].len;
+        refs_move(lrid, pos, rrid, -pos);
+        int32_t j = coll_get(rrid, 0);
+        if (j < 0) return;
+        d.colls()[j].len = cl > pos ? cl - pos : 0;
+        if (cl > pos) d.colls()[i].len = pos;
+    }
+    /* TextSegment / PermutationSegment.append -> LocalReferenceCollection.append(seg1, seg2)
+     * (textSegment.ts:78, permutationvector.ts:98, localReference.ts:126-133, 211-223), before seg1's
+     * length (len1) changes; seg2 leaves the tree */
+    MT_HD void refs_append(int32_t rid1, int32_t rid2, int32_t len1) {
+        int32_t j = coll_find(rid2);
+        if (j >= 0 && refs_on_row(rid2) > 0) {
+            int32_t cl2 = d.colls()[j].len;
+            int32_t i = coll_get(rid1, len1);
+            if (i < 0) return;
+            j = coll_find(rid2); /* the table may have moved */
+            int32_t cl1 = d.colls()[i].len;
+            refs_move(rid2, INT32_MIN, rid1, cl1);
+            d.colls()[i].len = cl1 + cl2;
+        }
+        coll_drop(rid2);
+    }
+    /* new LocalReference(segment, offset) + addLocalReference for getContainingSegment(pos) (local view) */
+    MT_HD void add_ref(int32_t pos, int32_t type) {
+        DState* st = d.dstate();
+        int32_t n = st->nref;
+        if (n >= d.caps.rcap) {
+            fail(E_CAPACITY);
+            return;
+        }
+        int32_t off = 0;
+        int32_t s = containing(pos, h.currentSeq, h.localShort, &off);
+        LRef r = {s >= 0 ? (int32_t)z.rid[s] : REF_DETACHED, s >= 0 ? off : 0, type, 0};
+        if (s >= 0) { /* addLocalRef: refsByOffset[offset] = ... (localReference.ts:190-202) */
+            int32_t i = coll_get(r.rid, z.len(s));
+            if (i < 0) return;
+            if (d.colls()[i].len < off + 1) d.colls()[i].len = off + 1;
+        }
+        d.refs()[n] = r;
+        st->nref = n + 1;
+    }
+    /* after a remove took rows holding references (markRangeRemoved, mergeTree.ts:2703-2732): under the
+     * op's perspective, SlideOnRemove references go to offset 0 of the segment at `start`
+     * (addBeforeTombstones) or, past the end, to the last offset of the last segment (addAfterTombstones);
+     * the others, or all of them in an empty document, detach */
+    MT_HD void refs_slide(int32_t start, int32_t refSeq, int32_t client) {
+        int32_t L = length(refSeq, client), tgt = REF_DETACHED, toff = 0, off = 0, ci = -1, need = 0;
+        if (start < L) {
+            int32_t s = containing(start, refSeq, client, &off);
+            if (s >= 0) {
+                tgt = z.rid[s];
+                ci = coll_get(tgt, z.len(s));
+                need = 1; /* refsByOffset[0] */
+            }
+        } else if (L > 0) {
+            int32_t s = containing(L - 1, refSeq, client, &off);
+            if (s >= 0) {
+                tgt = z.rid[s];
+                toff = z.len(s) - 1;
+                ci = coll_get(tgt, z.len(s));
+                need = z.len(s); /* refsByOffset[cachedLength - 1] */
+            }
+        }
+        LRef* R = d.refs();
+        int32_t n = d.dstate()->nref, nslide = 0;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            bool slide = false;
+            if (i < n && R[i].rid == REF_SAVED) {
+                slide = (R[i].type & MT_REF_SLIDE_ON_REMOVE) && tgt >= 0;
+                R[i].rid = slide ? tgt : REF_DETACHED;
+                R[i].off = slide ? toff : 0;
+            }
+            nslide += w.sum(slide ? 1 : 0);
+        }
+        w.sync();
+        if (nslide > 0 && ci >= 0 && d.colls()[ci].len < need) d.colls()[ci].len = need;
+    }
+    /* LocalReference.toPosition (localReference.ts:62-68): getPosition(segment) + getOffset() (0 on a
+     * removed segment: `removedSeq` truthy), -1 when detached */
+    MT_HD int32_t ref_position(int32_t i) {
+        LRef r = d.refs()[i];
+        if (r.rid < 0) return -1;
+        int32_t s = slot_of(r.rid, -1);
+        if (s < 0) return -1;
+        int32_t rs = z.rseq(s);
+        return local_pos(s) + (rs != NOREM && rs != 0 ? 0 : r.off);
+    }
+
     /* Client.getPosition(segment) (client.ts:291): the local view */
     MT_HD int32_t local_pos(int32_t s) { return position_of(s, h.currentSeq, h.localShort); }
     /* the propertyDeltas addProperties (segmentPropertiesManager.ts:35-111) returns for row s and this
@@ -932,6 +1122,7 @@ struct Replica {
     }
     /* leaf b goes right after leaf a in document order (a full chunk splits 32 + 32) */
     MT_HD void rope_insert_after(int32_t a, int32_t b) {
+        MT_PROF_SCOPE(PH_ROPE);
         auto& t = z.tl;
         constexpr int32_t CH = HT::TL::CH, HALF = CH / 2;
         int32_t c = t.lch[a], i = t.lix[a] + 1;
@@ -977,6 +1168,7 @@ struct Replica {
     }
     /* leaf b leaves the document order (its STABLE length leaves its chunk's summary) */
     MT_HD void rope_remove(int32_t b) {
+        MT_PROF_SCOPE(PH_ROPE);
         auto& t = z.tl;
         int32_t c = t.lch[b], i = t.lix[b], p = t.cpos[c];
         t.cst[p] -= t.lst[b];
@@ -998,6 +1190,7 @@ struct Replica {
     }
     /* recompute leaf n's STABLE length from its rows */
     MT_HD void leaf_restat(int32_t n) {
+        MT_PROF_SCOPE(PH_RESTAT);
         int32_t c = nch[n];
         int32_t v = 0;
         for (int32_t b = 0; b < c; b += W::N) {
@@ -1052,55 +1245,80 @@ struct Replica {
      * position, leaf index and perspective length go to the scratch, its length scattered onto
      * cdel[chunk position]. Returns the sum of those lengths. */
     MT_HD int32_t win_pass(int32_t refSeq, int32_t client) {
+        MT_PROF_SCOPE(PH_WIN);
         auto& t = z.tl;
+        /* NB passes of the wave at a time, stage by stage: every entry's loads of one stage are issued
+         * together (one round trip per stage, not one per stage per pass); the settling and the
+         * compaction then run pass by pass, in entry order. Every read of a block precedes its writes,
+         * and the compaction only writes entries at or before the ones read. */
+        constexpr int NB = W::N >= 64 ? 8 : 1;
         int32_t n = t.wN, wpos = 0, total = 0;
-        for (int32_t b = 0; b < n; b += W::N) {
-            int32_t i = b + w.lane();
-            bool ok = i < n;
-            int32_t rd = ok ? t.wrid[i] : 0;
-            int32_t g = ok ? t.wgen[i] : 0;
-            int32_t s = -1;
-            if (ok && z.rgen[rd] == (uint8_t)g) {
-                int32_t lf = z.rleaf[rd], c = nch[lf];
-                for (int32_t j = 0; j < MAXN; j++)
-                    if (j < c && z.rid[lf * MAXN + j] == rd) s = lf * MAXN + j;
+        for (int32_t b0 = 0; b0 < n; b0 += NB * W::N) {
+            int32_t rd[NB], g[NB], lf[NB], s[NB], v[NB], cp[NB], lx[NB];
+            bool settle[NB], keep[NB];
+#pragma unroll
+            for (int q = 0; q < NB; q++) { /* the entries */
+                int32_t i = b0 + q * W::N + w.lane();
+                bool ok = i < n;
+                rd[q] = ok ? t.wrid[i] : 0;
+                g[q] = ok ? t.wgen[i] : -1;
             }
-            bool settle = s >= 0 && settled(s);
-            bool keep = s >= 0 && !settle;
-            int32_t v = 0, cp = 0, lx = 0;
-            if (keep) {
-                v = vis(s, refSeq, client);
-                int32_t lf = s / MAXN;
-                cp = t.cpos[t.lch[lf]];
-                lx = t.lix[lf];
+#pragma unroll
+            for (int q = 0; q < NB; q++) { /* the row is still the one added: its leaf */
+                lf[q] = -1;
+                if (g[q] >= 0 && z.rgen[rd[q]] == (uint8_t)g[q]) lf[q] = z.rleaf[rd[q]];
             }
-            uint64_t m = w.ballot(settle);
-            while (m) { /* a few rows per op: serial */
-                int32_t l = W::ffs(m);
-                m &= m - 1;
-                int32_t ss = w.bcast(s, l);
-                if (z.rseq(ss) == NOREM) {
-                    t.xf[ss] = XF_STABLE;
-                    lst_add(ss / MAXN, z.len(ss));
-                } else {
-                    t.xf[ss] = 0;
+#pragma unroll
+            for (int q = 0; q < NB; q++) { /* its slot in the leaf */
+                s[q] = -1;
+                if (lf[q] >= 0) {
+                    int32_t c = nch[lf[q]];
+                    for (int32_t j = 0; j < MAXN; j++)
+                        if (j < c && z.rid[lf[q] * MAXN + j] == rd[q]) s[q] = lf[q] * MAXN + j;
                 }
             }
-            int32_t tot;
-            int32_t off = w.excl_scan(keep ? 1 : 0, &tot);
-            w.sync();
-            if (keep) {
-                int32_t o = wpos + off;
-                t.wrid[o] = rd;
-                t.wgen[o] = (uint8_t)g;
-                wcp[o] = cp;
-                wlx[o] = (uint8_t)lx;
-                wvs[o] = v;
-                if (v) W::atomic_add(&cdel[cp], v);
+#pragma unroll
+            for (int q = 0; q < NB; q++) { /* settled, or its perspective length and chunk position */
+                settle[q] = s[q] >= 0 && settled(s[q]);
+                keep[q] = s[q] >= 0 && !settle[q];
+                v[q] = cp[q] = lx[q] = 0;
+                if (keep[q]) {
+                    v[q] = vis(s[q], refSeq, client);
+                    int32_t l = s[q] / MAXN;
+                    cp[q] = t.cpos[t.lch[l]];
+                    lx[q] = t.lix[l];
+                }
             }
-            w.sync();
-            wpos += tot;
-            total += w.sum(v);
+            for (int q = 0; q < NB; q++) {
+                if (b0 + q * W::N >= n) break;
+                uint64_t m = w.ballot(settle[q]);
+                while (m) { /* a few rows per op: serial */
+                    int32_t l = W::ffs(m);
+                    m &= m - 1;
+                    int32_t ss = w.bcast(s[q], l);
+                    if (z.rseq(ss) == NOREM) {
+                        t.xf[ss] = XF_STABLE;
+                        lst_add(ss / MAXN, z.len(ss));
+                    } else {
+                        t.xf[ss] = 0;
+                    }
+                }
+                int32_t tot;
+                int32_t off = w.excl_scan(keep[q] ? 1 : 0, &tot);
+                w.sync();
+                if (keep[q]) {
+                    int32_t o = wpos + off;
+                    t.wrid[o] = rd[q];
+                    t.wgen[o] = (uint8_t)g[q];
+                    wcp[o] = cp[q];
+                    wlx[o] = (uint8_t)lx[q];
+                    wvs[o] = v[q];
+                    if (v[q]) W::atomic_add(&cdel[cp[q]], v[q]);
+                }
+                w.sync();
+                wpos += tot;
+                total += w.sum(v[q]);
+            }
         }
         t.wN = wpos;
         return total;
@@ -1118,6 +1336,7 @@ struct Replica {
      * P < pos <= P + vis, from the chunk and leaf summaries plus the window scratch of the last
      * win_pass (same perspective). -1 if pos is beyond the length. */
     MT_HD int32_t tile_find(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+        MT_PROF_SCOPE(PH_TFIND);
         auto& t = z.tl;
         int32_t nc = t.nchunk;
         int32_t run = 0, cpf = -1;
@@ -1183,7 +1402,22 @@ struct Replica {
     }
     /* within leaf position k (start offset P): the row t = k*8+j with P < pos <= P + vis */
     MT_HD int32_t leaf_find(int32_t k, int32_t P, int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+        MT_PROF_SCOPE(PH_LFIND);
         int32_t n = leaf_at(k), c = nch[n];
+        if constexpr (W::N >= MAXN) { /* lane j: child j; one prefix scan */
+            int32_t j = w.lane();
+            int32_t v = j < c ? vis(n * MAXN + (j & (MAXN - 1)), refSeq, client) : 0;
+            int32_t tot;
+            int32_t p = P + w.excl_scan(v, &tot);
+            uint64_t m = w.ballot(j < c && p < pos && pos <= p + v);
+            if (m) {
+                int32_t l = W::ffs(m);
+                *Pout = w.bcast(p, l);
+                return k * MAXN + l;
+            }
+            fail(E_ASSERT);
+            return -1;
+        }
         int32_t run = P;
         for (int32_t j = 0; j < c; j++) {
             int32_t v = vis(n * MAXN + j, refSeq, client);
@@ -1621,6 +1855,7 @@ struct Replica {
         typename HT::Cold& cr = d.cold()[rrid];
         copy_cold(rs, ls); /* splitAt copies every field (mergeTree.ts:523-567) */
         if (cl.ovx) ovl_clone(rs, ls);
+        if (refs_on()) refs_split(z.rid[ls], rrid, off);
         int32_t lenL = z.len(ls);
         z.len(rs) = lenL - off;
         cr.toff = cl.toff + (uint32_t)off;
@@ -1862,6 +2097,85 @@ struct Replica {
             }
             w.sync();
             h.heapTop = d > 0 ? w.bcast(ms, 0) : xs;
+        } else if constexpr (W::N == 64) {
+            /* Larger heaps: the sift-down looks 5 levels ahead at a time. The 62 nodes of the 5-level
+             * subtree below the current node are read in one pass (lane l: depth dd, offset off), the
+             * descent through them is taken on scalars (lane broadcasts), then the next subtree; the
+             * entries on the path move up one level in one parallel pass, as above. */
+            int32_t l = w.lane();
+            *rid = hrd[0];
+            *gen = hgn[0];
+            *seq = hsq[0];
+            int32_t last = cnt - 1;
+            IX xr = hrd[last];
+            uint8_t xg = hgn[last];
+            int32_t xs = hsq[last];
+            cnt--;
+            h.heapN = cnt;
+            if (cnt == 0) return;
+            int32_t dd = l < 2 ? 1 : l < 6 ? 2 : l < 14 ? 3 : l < 30 ? 4 : l < 62 ? 5 : 0;
+            int32_t off = dd ? l - ((1 << dd) - 2) : 0;
+            int32_t path[24];
+            int32_t d = 0, k = 1;
+            bool done = false;
+            while (!done) {
+                int32_t node = dd ? (k << dd) + off : 0;
+                int32_t sv = (dd && node <= cnt) ? hsq[node - 1] : 0;
+                int32_t cur = 0; /* the current node is (k << t) + cur */
+                for (int32_t t = 0; t < 5; t++) {
+                    int32_t j = (k << (t + 1)) + 2 * cur; /* its left child (1-based) */
+                    if (j > cnt) {
+                        done = true;
+                        break;
+                    }
+                    int32_t lj = (1 << (t + 1)) - 2 + 2 * cur; /* the lane holding it */
+                    int32_t sj = w.bcast(sv, lj);
+                    int32_t c2 = 2 * cur;
+                    if (j < cnt) {
+                        int32_t s2 = w.bcast(sv, lj + 1);
+                        if (sj - s2 > 0) {
+                            j++;
+                            sj = s2;
+                            c2++;
+                        }
+                    }
+                    if (xs - sj <= 0) {
+                        done = true;
+                        break;
+                    }
+                    path[d++] = j;
+                    cur = c2;
+                }
+                if (!done) k = path[d - 1];
+            }
+            int32_t fin = d > 0 ? path[d - 1] : 1;
+            int32_t src = 0, dst = 0;
+            for (int32_t t = 0; t < 24; t++)
+                if (t == l && t < d) {
+                    src = path[t];
+                    dst = t == 0 ? 1 : path[t - 1];
+                }
+            IX mr = 0;
+            uint8_t mg = 0;
+            int32_t ms = 0;
+            if (l < d) {
+                mr = hrd[src - 1];
+                mg = hgn[src - 1];
+                ms = hsq[src - 1];
+            }
+            w.sync();
+            if (l < d) {
+                hrd[dst - 1] = mr;
+                hsq[dst - 1] = ms;
+                hgn[dst - 1] = mg;
+            }
+            if (l == 0) {
+                hrd[fin - 1] = xr;
+                hsq[fin - 1] = xs;
+                hgn[fin - 1] = xg;
+            }
+            w.sync();
+            h.heapTop = d > 0 ? w.bcast(ms, 0) : xs;
         } else {
             *rid = hrd[0];
             *seq = hsq[0];
@@ -2043,6 +2357,10 @@ struct Replica {
                             dseg(-1, z.len(s));
                             dtail(1);
                         }
+                        if (refs_on()) { /* the segment loses its parent: its references detach */
+                            refs_move(z.rid[s], INT32_MIN, REF_DETACHED, 0);
+                            coll_drop(z.rid[s]);
+                        }
                         free_rid(z.rid[s]); /* unlinked */
                     }
                     prev = -1;
@@ -2057,6 +2375,7 @@ struct Replica {
                                   ((z.flags(prev) ^ z.flags(s)) & RF_PROPS) == 0 && match_props(prev, s) &&
                                   can_append(prev, s);
                         if (ok) {
+                            if (refs_on()) refs_append(z.rid[prev], z.rid[s], z.len(prev));
                             append_text(prev, s);
                             if (dl_on()) { /* APPEND (mergeTree.ts:1368-1373): [prevSegment, segment] */
                                 dhead(MT_DELTA_APPEND);
@@ -2159,6 +2478,7 @@ struct Replica {
                     ok = !nl;
                 }
                 if (ok) {
+                    if (refs_on()) refs_append(z.rid[sp], z.rid[sk], prevLen);
                     append_text(sp, sk); /* updates z.len(sp) (read by a GC inside it) and its NL bits */
                     prevLen += lk;
                     prevFl = (prevFl & ~(RF_NLK | RF_NL)) | (fk & (RF_NLK | RF_NL));
@@ -2180,6 +2500,16 @@ struct Replica {
 #endif
         /* frees: every valid row not kept (unlinked or appended) */
         uint64_t drop = vmask & ~keep;
+        if (refs_on()) { /* references on unlinked rows detach (their segment loses its parent) */
+            uint64_t um = drop & w.ballot(code == 2);
+            while (um) {
+                int32_t l = W::ffs(um);
+                um &= um - 1;
+                int32_t ur = w.bcast((int32_t)r.rid, l);
+                refs_move(ur, INT32_MIN, REF_DETACHED, 0);
+                coll_drop(ur);
+            }
+        }
         if (dl_on()) { /* UNLINK / APPEND maintenance events in the reference's walk order (lane order) */
             uint64_t em = drop;
             while (em) {
@@ -2831,6 +3161,8 @@ struct Replica {
         const bool dl = dl_on();
         bool dh = false; /* the REMOVE event's head goes out after the boundary splits' SPLIT events */
         int32_t dn = 0;
+        const bool rf = refs_on();
+        bool saved = false;
         range_op(start, end, refSeq, client, [&](int32_t s, int32_t dpos) {
             if (dl && !dh) {
                 dhead(MT_DELTA_REMOVE);
@@ -2858,6 +3190,10 @@ struct Replica {
                     dseg(dpos, L);
                     dn++;
                 }
+                if (rf) { /* savedLocalRefs; segment.localRefs = undefined (mergeTree.ts:2673-2676) */
+                    if (refs_move(z.rid[s], INT32_MIN, REF_SAVED, 0)) saved = true;
+                    coll_drop(z.rid[s]);
+                }
             }
             if constexpr (TILED) row_removed(s);
             if (h.collaborating) {
@@ -2867,6 +3203,7 @@ struct Replica {
                     add_lru(s, seq);
             }
         }, dl);
+        if (saved) refs_slide(start, refSeq, client);
         if (dl) {
             if (!dh) dhead(MT_DELTA_REMOVE);
             dtail(dn);
@@ -2961,7 +3298,7 @@ struct Replica {
         if (h.err) return;
         int32_t kind = op.kind & MT_OP_KIND_MASK;
         if constexpr (DL) {
-            if (d.caps.dcap > 0) { /* delta events: this record's seq; none while a snapshot loads */
+            if (Doc<HT>::has_fx(d.caps)) { /* delta events: this record's seq; none while a snapshot loads */
                 DState* st = d.dstate();
                 st->seq = (op.kind & MT_OPF_LOCAL) ? UNASSIGNED_SEQ : op.seq;
                 st->on = (op.kind & MT_OPF_LOCAL) || kind < MT_OP_RELOAD;
@@ -2978,6 +3315,12 @@ struct Replica {
         }
         if (kind >= MT_OP_RELOAD && !(op.kind & MT_OPF_LOCAL)) {
             apply_load(op, p);
+            h.opsDone++;
+            return;
+        }
+        if (kind == MT_OP_REF) { /* a local reference (mt_oplog.h): the client-feature build keeps them */
+            if constexpr (DL)
+                if (op.kind & MT_OPF_LOCAL) add_ref(op.pos1, op.pos2);
             h.opsDone++;
             return;
         }

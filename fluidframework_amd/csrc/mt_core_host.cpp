@@ -64,9 +64,13 @@ extern "C" {
 mth_store* mth_create(int64_t ndocs, const int32_t* caps6) { return mth_create_dl(ndocs, caps6, 0); }
 
 mth_store* mth_create_dl(int64_t ndocs, const int32_t* caps6, int32_t dcap) {
+    return mth_create_fx(ndocs, caps6, dcap, 0);
+}
+
+mth_store* mth_create_fx(int64_t ndocs, const int32_t* caps6, int32_t dcap, int32_t rcap) {
     /* caps6 = (ncap, hcap[ignored: 2*ncap], acap, mcap, gcap, ccap[ignored: 64]); dcap: delta event
-     * log words per doc (mt_caps.dcap) */
-    Caps k = {caps6[2], caps6[3], caps6[4], dcap < 0 ? 0 : dcap};
+     * log words per doc (mt_caps.dcap); rcap: local references per doc (mt_caps.rcap) */
+    Caps k = {caps6[2], caps6[3], caps6[4], dcap < 0 ? 0 : dcap, rcap < 0 ? 0 : rcap};
     int prof = profile_for(caps6[0]);
     if (!caps_valid(k) || ndocs < 1 || prof < 0) return nullptr;
     mth_store* s = (mth_store*)calloc(1, sizeof(mth_store));
@@ -192,6 +196,16 @@ int64_t mth_deltas(mth_store* s, int64_t doc, int32_t* out, int64_t cap, uint64_
         for (int64_t i = 0; out && i < m; i++) out[i] = r.d.dlog()[i];
         if (hash) *hash = st->h;
         return st->n;
+    });
+}
+
+/* local references of one doc: their count (returned) and LocalReference.toPosition() of each */
+int32_t mth_ref_positions(mth_store* s, int64_t doc, int32_t* out, int32_t cap) {
+    return with_replica(s, doc, [&](auto& r) -> int32_t {
+        if (r.d.caps.rcap <= 0) return 0;
+        int32_t n = r.d.dstate()->nref;
+        for (int32_t i = 0; i < n && i < cap; i++) out[i] = r.ref_position(i);
+        return n;
     });
 }
 

@@ -311,6 +311,20 @@ __global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t m
         for (int i = 0; i < 7; i++) out[i] = res[i];
 }
 
+/* local references: per doc their count and LocalReference.toPosition() of each (-1 detached) */
+template <class HT>
+__global__ __launch_bounds__(WG) void k_refpos(Store<HT> st, int64_t ndocs, int32_t rcap, int32_t* nref, int32_t* pos) {
+    int64_t d = blockIdx.x;
+    if (d >= ndocs) return;
+    Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
+    int32_t n = r.d.dstate()->nref;
+    for (int32_t i = 0; i < n; i++) {
+        int32_t p = r.ref_position(i);
+        if (threadIdx.x == 0) pos[d * rcap + i] = p;
+    }
+    if (threadIdx.x == 0) nref[d] = n;
+}
+
 /* per-doc header fields: errors, stats, roofline work counters */
 template <class HT>
 __global__ void k_hdr(Store<HT> st, int64_t ndocs, int32_t* err, int32_t* err_op, int32_t* stats4, int64_t* work3) {
@@ -347,6 +361,8 @@ struct mt_engine {
     int device;
     int64_t ndocs;
     int32_t dcap = 0; /* delta event log words per document (0: off) */
+    int32_t rcap = 0; /* local references per document (0: none) */
+    bool fx = false;  /* delta events or local references: the client-feature replay build */
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
     bool noinline = false; /* small profile: compiler-chosen inlining (MT_REPLAY_NOINLINE=1) */
@@ -400,6 +416,7 @@ struct ProfOps {
                     int64_t* dn);
     int32_t (*seg)(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,
                    int32_t long_client, int32_t* dout);
+    int32_t (*refpos)(mt_engine* e, int32_t* dn, int32_t* dpos);
 };
 /* each profile's table (host functions, defined in its mt_prof_*.hip) */
 const ProfOps* ops_small();
@@ -475,7 +492,12 @@ struct Launch {
                            long_client, dout);
         return launch_check(e, "k_seg");
     }
+    static int32_t refpos(mt_engine* e, int32_t* dn, int32_t* dpos) {
+        hipLaunchKernelGGL((k_refpos<HT>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, store_of<HT>(e), e->ndocs,
+                           e->rcap, dn, dpos);
+        return launch_check(e, "k_refpos");
+    }
     static ProfOps table(int32_t (*replay)(mt_engine*)) {
-        return ProfOps{init, start_collab, replay, hdr, digest, dump, length, text, seg};
+        return ProfOps{init, start_collab, replay, hdr, digest, dump, length, text, seg, refpos};
     }
 };

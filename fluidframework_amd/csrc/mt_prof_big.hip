@@ -2,7 +2,7 @@
 #include "mt_kernels.h"
 
 static int32_t replay_big(mt_engine* e) {
-    if (e->dcap > 0) return launch_replay<HotBig>(e, k_replay<HotBig, false, 1, 1, 0, true>); /* delta events */
+    if (e->fx) return launch_replay<HotBig>(e, k_replay<HotBig, false, 1, 1, 0, true>); /* delta events */
     return launch_replay<HotBig>(e, k_replay<HotBig, false>);
 }
 

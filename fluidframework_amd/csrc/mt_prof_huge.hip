@@ -2,7 +2,7 @@
 #include "mt_kernels.h"
 
 static int32_t replay_huge(mt_engine* e) {
-    if (e->dcap > 0) return launch_replay<HotHuge>(e, k_replay_tiled<HotHuge, true>); /* delta events */
+    if (e->fx) return launch_replay<HotHuge>(e, k_replay_tiled<HotHuge, true>); /* delta events */
     return launch_replay<HotHuge>(e, k_replay_tiled<HotHuge>);
 }
 

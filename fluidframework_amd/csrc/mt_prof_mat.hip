@@ -10,7 +10,7 @@ int32_t replay_mat_dl(mt_engine* e);
  * replicas). =1 stages the whole Skel (10.7 KB), which caps residency at 14 documents per CU through
  * LDS (103 Mops/s); =0 stages nothing (104 Mops/s). */
 static int32_t replay_mat(mt_engine* e) {
-    if (e->dcap > 0) return replay_mat_dl(e); /* the delta-event build */
+    if (e->fx) return replay_mat_dl(e); /* the delta-event build */
     if (e->mat_skel == 1) return replay_mat_skel(e);
     if (e->mat_skel == 2) return replay_mat_lite(e);
     return replay_mat_none(e);

@@ -22,7 +22,7 @@ int32_t replay_small_dl(mt_engine* e);
  * MT_REPLAY_LDS=1 selects the fully LDS-staged form, MT_REPLAY_WAVES=2|4|5|6|7|8 the occupancy,
  * MT_REPLAY_NOINLINE=1 the build with compiler-chosen inlining. */
 static int32_t replay_small(mt_engine* e) {
-    if (e->dcap > 0) return replay_small_dl(e); /* the delta-event build */
+    if (e->fx) return replay_small_dl(e); /* the delta-event build */
     if (e->lds) return replay_small_lds(e);
     if (e->noinline) return e->waves == 8 ? replay_small_w8ni(e) : e->waves == 6 ? replay_small_w6ni(e) : replay_small_w7ni(e);
     if (e->waves == 8) return replay_small_w8(e);

@@ -24,14 +24,16 @@ extern "C" {
 int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_engine** out) {
     if (!out || !caps || ndocs < 1 || ndocs > (int64_t)0x7fffffff) return MT_E_ARG;
     *out = nullptr;
-    Caps k = {caps->acap, caps->mcap, caps->gcap, caps->dcap};
+    Caps k = {caps->acap, caps->mcap, caps->gcap, caps->dcap, caps->rcap};
     int prof = profile_for(caps->ncap);
-    if (!caps_valid(k) || prof < 0 || caps->ccap > 254 || caps->dcap < 0)
+    if (!caps_valid(k) || prof < 0 || caps->ccap > 254 || caps->dcap < 0 || caps->rcap < 0)
         return MT_E_ARG; /* short ids are bytes; 0xFF = LocalClientId */
     mt_engine* e = new mt_engine();
     e->device = device;
     e->ndocs = ndocs;
     e->dcap = caps->dcap;
+    e->rcap = caps->rcap;
+    e->fx = caps->dcap > 0 || caps->rcap > 0;
     const char* g = getenv("MT_REPLAY_LDS");
     e->lds = g && g[0] == '1';
     /* Occupancy of the HBM-resident small-profile kernel: documents are replayed one per wave and
@@ -380,6 +382,23 @@ int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap) {
         if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
     }
     return logged;
+}
+
+int32_t mt_engine_ref_positions(mt_engine* e, int32_t* nref_out, int32_t* pos_out) {
+    if (!e || e->rcap <= 0) return MT_E_ARG;
+    HIPCHK(e, hipSetDevice(e->device));
+    int64_t n = e->ndocs;
+    int32_t rc = ensure(e, e->tmp, 4 * (size_t)n * (1 + (size_t)e->rcap));
+    if (rc) return rc;
+    int32_t* dn = (int32_t*)e->tmp.p;
+    int32_t* dpos = dn + n;
+    rc = e->ops->refpos(e, dn, dpos);
+    if (rc) return rc;
+    if (nref_out) HIPCHK(e, hipMemcpyAsync(nref_out, dn, 4 * (size_t)n, hipMemcpyDeviceToHost, e->stream));
+    if (pos_out)
+        HIPCHK(e, hipMemcpyAsync(pos_out, dpos, 4 * (size_t)n * e->rcap, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return MT_OK;
 }
 
 #ifdef MT_PROF

@@ -31,7 +31,7 @@ class SegRef(ctypes.Structure):
 
 
 class _Caps(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_int32) for n in ("ncap", "hcap", "acap", "mcap", "gcap", "ccap", "dcap")]
+    _fields_ = [(n, ctypes.c_int32) for n in ("ncap", "hcap", "acap", "mcap", "gcap", "ccap", "dcap", "rcap")]
 
 
 _LIB = None
@@ -70,6 +70,7 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_get_containing_segment.argtypes = [vp, i64, i32, i32, i32, ctypes.POINTER(SegRef)]
         L.mt_engine_get_position.argtypes = [vp, i64, i32, i32, i32, i32, ctypes.POINTER(i32)]
         L.mt_engine_delta_state.argtypes = [vp, vp, vp]
+        L.mt_engine_ref_positions.argtypes = [vp, vp, vp]
         L.mt_engine_deltas.argtypes = [vp, i64, vp, i64]
         L.mt_engine_deltas.restype = i64
         L.mt_engine_ndocs.argtypes = [vp]
@@ -102,7 +103,8 @@ def default_caps(ops_per_doc: int, config: int = 3) -> dict:
 class Engine:
     """A batch of `ndocs` replicas on HIP device `device`. caps["dcap"] > 0 turns on the delta event
     stream (include/mt_oplog.h MT_DELTA_*: what SharedString "sequenceDelta" / "maintenance"
-    listeners see), logging up to dcap words per document."""
+    listeners see), logging up to dcap words per document; caps["rcap"] > 0 keeps up to rcap local
+    references per document (MT_OP_REF records)."""
 
     def __init__(self, ndocs: int, device: int = 0, **caps):
         c = default_caps(0)
@@ -233,6 +235,14 @@ class Engine:
         buf = np.zeros(max(n, 1), np.int32)
         self.L.mt_engine_deltas(self.h, doc, _p(buf), n)
         return buf[:n]
+
+    def ref_positions(self):
+        """Per doc the number of local references, and (ndocs, rcap) LocalReference.toPosition() of each
+        (-1: detached)."""
+        n = np.zeros(self.ndocs, np.int32)
+        pos = np.full((self.ndocs, max(self.caps.rcap, 1)), -1, np.int32)
+        self._check(self.L.mt_engine_ref_positions(self.h, _p(n), _p(pos)), "ref_positions")
+        return n, pos
 
     def stats(self) -> np.ndarray:
         out = np.zeros((self.ndocs, 4), np.int32)

@@ -16,6 +16,7 @@ from typing import Any, Dict, List, Optional, Sequence
 import numpy as np
 
 OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 4
+OP_REF = 3  # local reference (mt_oplog.h MT_OP_REF; always with OPF_LOCAL)
 OP_RELOAD, OP_COLLAB, OP_APPEND = 5, 6, 7  # snapshot load records (mt_oplog.h)
 OPF_LOCAL = 0x80
 OPF_GROUPED = 0x40

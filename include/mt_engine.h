@@ -32,6 +32,7 @@ typedef struct mt_caps {
     int32_t gcap; /* pending local ops (segment groups) in flight                       */
     int32_t ccap; /* distinct clients per doc (<= 254)                                  */
     int32_t dcap; /* delta event log words per doc; 0 = no delta events (mt_oplog.h)   */
+    int32_t rcap; /* local references per doc (MT_OP_REF records); 0 = none           */
 } mt_caps;
 
 /* status codes */
@@ -120,6 +121,13 @@ int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t g
  * at most cap of them and returns how many are logged (<0 on error). */
 int32_t mt_engine_delta_state(mt_engine* e, int64_t* n_out, uint64_t* hash_out);
 int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap);
+/* Local references (MT_OP_REF records; engines created with caps.rcap > 0): per doc the number of
+ * references (nref_out[d]) and, for reference i, LocalReference.toPosition() (localReference.ts:62-68:
+ * Client.getPosition(segment) + getOffset(), -1 when detached) at pos_out[d * rcap + i]. References
+ * follow their segment through splits and zamboni appends, and a remove slides SlideOnRemove ones to
+ * the next (or last) segment and detaches the rest (mergeTree.ts:2703-2732, localReference.ts:
+ * 251-342). */
+int32_t mt_engine_ref_positions(mt_engine* e, int32_t* nref_out, int32_t* pos_out);
 /* Per-doc counters: nleaf, high-water row slots, high-water heap, events applied. */
 int32_t mt_engine_stats(mt_engine* e, int32_t* out4_per_doc);
 int64_t mt_engine_ndocs(const mt_engine* e);

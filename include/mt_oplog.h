@@ -34,6 +34,12 @@ enum {
     MT_OP_INSERT = 0,
     MT_OP_REMOVE = 1,
     MT_OP_ANNOTATE = 2,
+    /* Local reference (with MT_OPF_LOCAL; localReference.ts:20-117): what `new LocalReference(client,
+     * segment, offset, refType)` + Client.addLocalReference (client.ts:295) does for the segment and
+     * offset Client.getContainingSegment(pos1) returns in the local view (client.ts:1006); pos2 =
+     * refType (ReferenceType, ops.ts; SlideOnRemove = 0x40). The document's references are numbered in
+     * creation order; a position past the end makes a detached reference. */
+    MT_OP_REF = 3,
     MT_OP_NOOP = 4, /* sequenced message that is not a merge-tree op: advances currentSeq/MSN only */
     /* Snapshot load (SnapshotLoader, snapshotLoader.ts:86-228), on an empty non-collaborating replica:
      *   RELOAD: one header segment; pos1 counts down n..1 over the header's n records, and the whole
@@ -160,6 +166,7 @@ enum {
     MT_DELTA_UNLINK = -3,
 };
 #define MT_DELTA_END ((int32_t)0x80000000) /* ends an event's segment list */
+#define MT_REF_SLIDE_ON_REMOVE 0x40 /* ReferenceType.SlideOnRemove (ops.ts) */
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,9 @@ def lib():
         L.mth_create.argtypes = [i64, vp]
         L.mth_create_dl.restype = vp
         L.mth_create_dl.argtypes = [i64, vp, i32]
+        L.mth_create_fx.restype = vp
+        L.mth_create_fx.argtypes = [i64, vp, i32, i32]
+        L.mth_ref_positions.argtypes = [vp, i64, vp, i32]
         L.mth_deltas.argtypes = [vp, i64, vp, i64, vp]
         L.mth_deltas.restype = i64
         L.mth_destroy.argtypes = [vp]
@@ -54,10 +57,11 @@ DEFAULT_CAPS = (192, 256, 1 << 16, 4096, 1024, 64)
 
 
 class HostStore:
-    def __init__(self, ndocs: int, caps=DEFAULT_CAPS, dcap: int = 0):
+    def __init__(self, ndocs: int, caps=DEFAULT_CAPS, dcap: int = 0, rcap: int = 0):
         self.L = lib()
         self.caps = np.asarray(caps, np.int32)
-        self.h = self.L.mth_create_dl(ndocs, _p(self.caps), dcap)
+        self.rcap = rcap
+        self.h = self.L.mth_create_fx(ndocs, _p(self.caps), dcap, rcap)
         if not self.h:
             raise RuntimeError("mth_create failed")
         self.ndocs = ndocs
@@ -110,15 +114,21 @@ class HostStore:
         self.L.mth_deltas(self.h, doc, _p(buf), n, _p(h))
         return int(n), int(h[0]), buf[:n]
 
+    def ref_positions(self, doc) -> np.ndarray:
+        """LocalReference.toPosition() of each of the doc's local references (-1: detached)"""
+        out = np.zeros(max(self.rcap, 1), np.int32)
+        n = self.L.mth_ref_positions(self.h, doc, _p(out), self.rcap)
+        return out[:n]
+
     def stats(self, doc):
         out = np.zeros(8, np.int32)
         self.L.mth_stats(self.h, doc, _p(out))
         return dict(zip(("nleaf", "hw_slots", "hw_heap", "heap", "mem", "arena_top", "nodes", "ops"), out.tolist()))
 
 
-def replay_batch(batch: ol.Batch, caps=DEFAULT_CAPS, dcap: int = 0):
+def replay_batch(batch: ol.Batch, caps=DEFAULT_CAPS, dcap: int = 0, rcap: int = 0):
     """Replay every document of a batch on the host core; returns (digests, errors, store)."""
-    st = HostStore(batch.ndocs, caps, dcap)
+    st = HostStore(batch.ndocs, caps, dcap, rcap)
     dig = np.zeros(batch.ndocs, np.uint64)
     err = np.zeros(batch.ndocs, np.int32)
     for d in range(batch.ndocs):

@@ -1,0 +1,48 @@
+"""Local-reference records (mt_oplog.h MT_OP_REF) injected into generator logs — test infrastructure for
+the §8(f) f4 fixtures (tools/make_ref_goldens.py --refs, tests/test_ref_refs.py).
+
+A reference is a local, unsequenced record, so adding one changes nothing else the replica does. Each
+document gets `nref` of them at seeded points of its stream (never inside a group message, whose members
+the reference applies together), at a position drawn from the replica's local length at that point
+(measured with the host build of the engine core), including a few just past the end (detached
+references); 60 % are SlideOnRemove."""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+from fluidframework_amd import oplog as ol
+import core_host
+
+SLIDE = 0x40  # ReferenceType.SlideOnRemove (ops.ts)
+
+
+def inject(b: ol.Batch, caps, nref: int = 24, seed: int = 4242) -> ol.Batch:
+    st = core_host.HostStore(b.ndocs, caps)
+    out, off = [], [0]
+    for d in range(b.ndocs):
+        ops, text, props, kv = b.doc(d)
+        st.start_collab(d, int(b.local_long_id[d]))
+        rng = np.random.default_rng(seed + d)
+        grouped = (ops["kind"] & ol.OPF_GROUPED) != 0
+        ok = np.ones(len(ops) + 1, bool)
+        ok[1:] = ~grouped  # not right after a group member
+        cand = np.nonzero(ok)[0]
+        at = np.sort(rng.choice(cand, size=min(nref, len(cand)), replace=False))
+        pieces, prev = [], 0
+        for i in at:
+            if i > prev:
+                assert st.replay(d, ops[prev:i], text, props, kv) == 0
+            L = st.L.mth_length_local(st.h, d)
+            r = np.zeros(1, ol.OP_DTYPE)
+            r["kind"] = ol.OP_REF | ol.OPF_LOCAL
+            r["pos1"] = int(rng.integers(0, L + 2)) if L > 0 else 0
+            r["pos2"] = SLIDE if rng.random() < 0.6 else 0
+            pieces += [ops[prev:i], r]
+            prev = i
+        pieces.append(ops[prev:])
+        merged = np.concatenate(pieces)
+        out.append(merged)
+        off.append(off[-1] + len(merged))
+    return dataclasses.replace(b, ops=np.concatenate(out), op_off=np.asarray(off, np.int64))

@@ -267,13 +267,63 @@ def make_deltas(names, node: str) -> None:
         print(f"refdelta_{name}: {b.ndocs} docs, {int(off[-1])} words", flush=True)
 
 
+REF_SETS = ("c1_farm", "c2_observer", "c3_lagged", "c4_scaled", "c5_perm")
+
+
+def make_refs(names, node: str) -> None:
+    """tests/golden/refrefs_<set>.npz: local references (MT_OP_REF records injected by tests/refs_inject.py)
+    replayed by the reference: LocalReference.toPosition() of every reference at the end of each document's
+    stream (-2: Client.addLocalReference threw, a reference defect: localReference.ts:195-201 pushes onto the
+    missing `at` list of an offset that holds only slid references), and the reference's digests of the
+    same replicas (references change nothing else)."""
+    import refs_inject
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_ref_goldens import caps_for
+    for name in names:
+        w, ids = SETS[name]
+        b = gen.generate(w, ids=ids, threads=8)
+        c = caps_for(w)
+        rb = refs_inject.inject(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
+        d = os.path.join(SCRATCH, name + "_refs")
+        write_batch(rb, gen.generator_interner(), d)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d], capture_output=True,
+                           text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+        errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
+        if errs:
+            raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
+        rp = json.load(open(os.path.join(d, "ref_refpos.json")))
+        nref = np.asarray([len(rp.get(str(i), [])) for i in range(rb.ndocs)], np.int32)
+        pos = np.full((rb.ndocs, max(nref.max(), 1)), -1, np.int32)
+        for i in range(rb.ndocs):
+            pos[i, : nref[i]] = rp.get(str(i), [])
+        blob = np.fromfile(os.path.join(d, "ref_dumps.bin"), np.uint8)
+        off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
+        digests = np.asarray([fnv1a64(blob[off[i]: off[i + 1]].tobytes()) for i in range(rb.ndocs)], np.uint64)
+        np.savez_compressed(
+            os.path.join(GOLDEN, f"refrefs_{name}.npz"),
+            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(rb),
+            nref=nref, positions=pos, digests=digests,
+            source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                    "tools/ref_replay.mjs: LocalReference + Client.addLocalReference, toPosition() at the end"),
+        )
+        print(f"refrefs_{name}: {rb.ndocs} docs, {int(nref.sum())} references: {int((pos >= 0).sum())} attached, "
+              f"{int((pos == -1).sum() - (pos.shape[1] * rb.ndocs - nref.sum()))} detached, "
+              f"{int((pos == -2).sum())} the reference could not add", flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default=",".join(SETS))
     ap.add_argument("--node", default="node")
     ap.add_argument("--deltas", action="store_true", help="write the delta-stream fixtures (refdelta_*.npz) only")
+    ap.add_argument("--refs", action="store_true", help="write the local-reference fixtures (refrefs_*.npz) only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
+    if args.refs:
+        make_refs([n for n in args.sets.split(",") if n in REF_SETS], args.node)
+        return
     if args.deltas:
         make_deltas([n for n in args.sets.split(",") if n in SETS], args.node)
         return

@@ -9,7 +9,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from fluidframework_amd import native
 
-PHASES = ["APPLY", "ZAMBONI", "FIND", "MAP", "SPLIT", "ACK", "TEXT", "HEAP", "SCOUR", "PACK", "APPEND", "CAND", "S1load", "S2walk", "S3compact", "P1leaf", "P2interior", "INSROW", "LEAFINS"]
+PHASES = ["APPLY", "ZAMBONI", "FIND", "MAP", "SPLIT", "ACK", "TEXT", "HEAP", "SCOUR", "PACK", "APPEND", "CAND", "S1load", "S2walk", "S3compact", "P1leaf", "P2interior", "INSROW", "LEAFINS",
+          "WIN", "TFIND", "LFIND", "ROPE", "RESTAT"]
 LIB = native.lib_path("libmtreplay_prof.so")
 
 
@@ -22,6 +23,7 @@ def main():
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--docs", type=int, default=2048)
     ap.add_argument("--ops", type=int, default=4096)
+    ap.add_argument("--config", type=int, default=3)
     a = ap.parse_args()
     if a.build_only:
         build()
@@ -30,8 +32,9 @@ def main():
     os.environ["MT_REPLAY_LIB"] = LIB
     from fluidframework_amd import gen
     from fluidframework_amd.engine import Engine, default_caps, lib
-    b = gen.generate(gen.config3(a.ops), a.docs)
-    eng = Engine(b.ndocs, **default_caps(a.ops))
+    w = {3: gen.config3, 4: gen.config4, 5: gen.config5, 2: gen.config2}[a.config](a.ops)
+    b = gen.generate(w, a.docs)
+    eng = Engine(b.ndocs, **default_caps(a.ops, config=a.config))
     eng.start_collab(b.local_long_id)
     eng.replay(b)
     L = lib()
@@ -40,7 +43,7 @@ def main():
     assert L.mt_engine_profile(eng.h, out.ctypes.data) == 0
     tot = out.sum(0).astype(np.float64)
     ev = b.nops
-    print(f"docs {b.ndocs} events {ev} kernel {eng.last_run_ms:.1f} ms")
+    print(f"config {a.config} docs {b.ndocs} events {ev} kernel {eng.last_run_ms:.1f} ms")
     for i, n in enumerate(PHASES):
         print(f"{n:8s} {tot[i] / ev:10.0f} cycles/event  {100 * tot[i] / tot[0]:5.1f}% of APPLY")
 

@@ -19,7 +19,7 @@ const timeOnly = process.argv.includes("--time");
 // (the stream SharedString's "sequenceDelta" / "maintenance" listeners see, sequence.ts:136-150) in the
 // word format of include/mt_oplog.h (MT_DELTA_*) -> batch-dir/ref_deltas.bin + ref_delta_off.bin
 const withDeltas = process.argv.includes("--deltas");
-let Client, TextSegment, Marker, PermutationSegment, SnapshotV1; // bound in main() (Node 12 has no top-level await)
+let Client, TextSegment, Marker, PermutationSegment, SnapshotV1, LocalReference; // bound in main() (Node 12 has no top-level await)
 
 const rd = (f) => fs.readFileSync(path.join(dir, f));
 const meta = JSON.parse(rd("meta.json"));
@@ -116,6 +116,18 @@ function applyRange(client, doc, from, to) {
             } else if (kind === 2) {
                 const ps = propSet(doc, rec.props);
                 client.annotateRangeLocal(rec.pos1, rec.pos2, ps ? ps.set : {}, ps ? ps.combiningOp : undefined);
+            } else if (kind === 3) { // a local reference (mt_oplog.h MT_OP_REF) at getContainingSegment(pos1)
+                const { segment, offset } = client.getContainingSegment(rec.pos1);
+                let lref = null;
+                if (segment) {
+                    lref = new LocalReference(client, segment, offset, rec.pos2);
+                    try {
+                        client.addLocalReference(lref);
+                    } catch (e) { // addLocalRef at an offset holding only slid refs: refsByOffset[o].at is
+                        lref = "threw"; // undefined (localReference.ts:195-201); the tree is untouched
+                    }
+                }
+                curRefs.push(lref);
             }
             continue;
         }
@@ -159,9 +171,12 @@ function hookDeltas(client, words) {
     };
 }
 const deltaWords = [];
+let curRefs = []; // the local references of the document being replayed, in creation order
+const refPositions = {};
 
 function replayDoc(doc, to = opOff[doc + 1], deltas = false) {
     const client = new Client(specToSegment, logger);
+    curRefs = [];
     if (deltas) {
         const words = [];
         deltaWords[doc] = words;
@@ -269,7 +284,7 @@ function dump(client) {
 
 async function main() {
 const MT = await import(path.join(erased, "index.mjs"));
-({ Client, TextSegment, Marker } = MT);
+({ Client, TextSegment, Marker, LocalReference } = MT);
 ({ PermutationSegment } = await import(path.join(erased, "permutationSegment.mjs")));
 ({ SnapshotV1 } = await import(path.join(erased, "snapshotV1.mjs")));
 const ndocs = opOff.length - 1;
@@ -283,6 +298,8 @@ const dumps = [], errs = {};
 for (let d = 0; d < ndocs; d++) {
     try {
         const c = replayDoc(d, opOff[d + 1], withDeltas);
+        // LocalReference.toPosition (localReference.ts:62-68) of every reference, -1 when detached
+        if (curRefs.length) refPositions[d] = curRefs.map((r) => (r === "threw" ? -2 : r ? r.toPosition() : -1));
         for (const [qd, pos, ref, cl] of queries) {
             if (qd !== d) continue;
             const mt = c.mergeTree;
@@ -347,6 +364,7 @@ if (withDeltas) {
     fs.writeFileSync(path.join(dir, "ref_deltas.bin"), Buffer.concat(parts));
     fs.writeFileSync(path.join(dir, "ref_delta_off.bin"), off);
 }
+if (Object.keys(refPositions).length) fs.writeFileSync(path.join(dir, "ref_refpos.json"), JSON.stringify(refPositions));
 fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
 if (queries.length) fs.writeFileSync(path.join(dir, "ref_answers.json"), JSON.stringify(answers));
 console.log(JSON.stringify({ ndocs, errors: Object.keys(errs).length, seconds: secs }));
