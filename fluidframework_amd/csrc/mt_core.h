@@ -96,9 +96,15 @@ struct alignas(16) DState {
 /* a local reference (localReference.ts:20-117): the row id of its segment (-1: detached), its offset
  * in the segment and its ReferenceType */
 struct alignas(16) LRef {
-    int32_t rid, off, type, _p;
+    int32_t rid, off, type;
+    int32_t ek; /* the refsByOffset entry it sits in was created by addLocalRef (0: has an `at` list) or by
+                   a tombstone slide (1: `before` / `after` only) */
 };
-enum : int32_t { REF_DETACHED = -1, REF_SAVED = -2 /* on a row the current remove took (mergeTree.ts:2673-2676) */ };
+enum : int32_t {
+    REF_DETACHED = -1,
+    REF_SAVED = -2, /* on a row the current remove took (mergeTree.ts:2673-2676) */
+    REF_GHOST = -3, /* addLocalReference threw: refsByOffset[offset].at is undefined (localReference.ts:195-201) */
+};
 /* a segment's LocalReferenceCollection: its row id and refsByOffset.length, which is what an append adds
  * to the offsets of the references it takes over (localReference.ts:211-223). That length follows the
  * JavaScript array, not the segment: set at creation, cut by a split, extended by appends and by
@@ -679,6 +685,17 @@ struct Replica {
         }
         coll_drop(rid2);
     }
+    /* the kind (LRef.ek) of the refsByOffset entry at `off` of row `rid`'s collection, -1 if none */
+    MT_HD int32_t entry_kind(int32_t rid, int32_t off) {
+        LRef* R = d.refs();
+        int32_t n = d.dstate()->nref, k = -1;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            uint64_t m = w.ballot(i < n && R[i].rid == rid && R[i].off == off);
+            if (m && k < 0) k = R[b + W::ffs(m)].ek;
+        }
+        return k;
+    }
     /* new LocalReference(segment, offset) + addLocalReference for getContainingSegment(pos) (local view) */
     MT_HD void add_ref(int32_t pos, int32_t type) {
         DState* st = d.dstate();
@@ -690,6 +707,12 @@ struct Replica {
         int32_t off = 0;
         int32_t s = containing(pos, h.currentSeq, h.localShort, &off);
         LRef r = {s >= 0 ? (int32_t)z.rid[s] : REF_DETACHED, s >= 0 ? off : 0, type, 0};
+        if (s >= 0 && entry_kind(r.rid, off) == 1) { /* the reference's addLocalRef throws here: the tree */
+            r.rid = REF_GHOST;                            /* is untouched and the reference is not kept */
+            d.refs()[n] = r;
+            st->nref = n + 1;
+            return;
+        }
         if (s >= 0) { /* addLocalRef: refsByOffset[offset] = ... (localReference.ts:190-202) */
             int32_t i = coll_get(r.rid, z.len(s));
             if (i < 0) return;
@@ -722,6 +745,8 @@ struct Replica {
         }
         LRef* R = d.refs();
         int32_t n = d.dstate()->nref, nslide = 0;
+        int32_t ek = tgt >= 0 ? entry_kind(tgt, toff) : -1; /* sliding into an existing entry keeps its kind */
+        if (ek < 0) ek = 1;
         for (int32_t b = 0; b < n; b += W::N) {
             int32_t i = b + w.lane();
             bool slide = false;
@@ -729,16 +754,60 @@ struct Replica {
                 slide = (R[i].type & MT_REF_SLIDE_ON_REMOVE) && tgt >= 0;
                 R[i].rid = slide ? tgt : REF_DETACHED;
                 R[i].off = slide ? toff : 0;
+                if (slide) R[i].ek = ek;
             }
             nslide += w.sum(slide ? 1 : 0);
         }
         w.sync();
         if (nslide > 0 && ci >= 0 && d.colls()[ci].len < need) d.colls()[ci].len = need;
     }
+    MT_HD int32_t kprev(int32_t k) const { /* the leaf position before k (k > 0) */
+        if constexpr (TILED)
+            return (k & 63) ? k - 1 : ((((k >> 6) - 1) << 6) | (z.tl.ccnt[z.tl.cord[(k >> 6) - 1]] - 1));
+        else
+            return k - 1;
+    }
+    /* Client.insertAtReferencePositionLocal (client.ts:217-245) -> MergeTree.insertAtReferencePosition
+     * (mergeTree.ts:2033-2130): split the reference's segment at its offset unless the offset or the
+     * segment's local length is 0, walk left over zero-length rows (leftExcursion, 2313-2344) taking
+     * every one breakTie(0, 0, ...) accepts, and insert the new local segment right before that row. */
+    MT_HD void insert_at_ref(const mt_op_rec& op, const Pools& p) {
+        if (op.pos1 < 0 || op.pos1 >= d.dstate()->nref) {
+            fail(E_ASSERT);
+            return;
+        }
+        LRef r = d.refs()[op.pos1];
+        if (r.rid < 0 || seg_len(op) <= 0) return; /* DetachedPosition / a zero-length segment: no-op */
+        int32_t s = slot_of(r.rid, -1);
+        if (s < 0) return;
+        int32_t rs0 = z.rseq(s);
+        int32_t off = (rs0 != NOREM && rs0 != 0) ? 0 : r.off; /* getOffset() */
+        if (off != 0 && local_len(s) != 0) {
+            int32_t rs = -1;
+            if (split_row(kpos(s / MAXN) * MAXN + (s & (MAXN - 1)), off, &rs) < 0 || rs < 0) return;
+            s = rs;
+        }
+        int32_t st = s, k = kpos(s / MAXN), j = s & (MAXN - 1);
+        for (;;) {
+            if (j == 0) {
+                if (k == 0) break;
+                k = kprev(k);
+                j = nch[leaf_at(k)];
+                continue;
+            }
+            j--;
+            int32_t q = leaf_at(k) * MAXN + j;
+            if (local_len(q) != 0) break;
+            if (break_tie(q, h.currentSeq, h.localShort)) st = q;
+        }
+        insert_segments(op, p, h.currentSeq, h.localShort, UNASSIGNED_SEQ, 0, 0,
+                        kpos(st / MAXN) * MAXN + (st & (MAXN - 1)));
+    }
     /* LocalReference.toPosition (localReference.ts:62-68): getPosition(segment) + getOffset() (0 on a
      * removed segment: `removedSeq` truthy), -1 when detached */
     MT_HD int32_t ref_position(int32_t i) {
         LRef r = d.refs()[i];
+        if (r.rid == REF_GHOST) return -2;
         if (r.rid < 0) return -1;
         int32_t s = slot_of(r.rid, -1);
         if (s < 0) return -1;
@@ -2888,7 +2957,7 @@ struct Replica {
     /* insertSegments (mergeTree.ts:2001-2040) of one segment; preRseq > 0: the segment arrives
      * already removed (a loaded segment's merge info, snapshotLoader.ts:101-106) */
     MT_HD void insert_segments(const mt_op_rec& op, const Pools& p, int32_t refSeq, int32_t client, int32_t seq,
-                               int32_t preRseq = 0, uint8_t preRcli = 0) {
+                               int32_t preRseq = 0, uint8_t preRcli = 0, int32_t atT = -1) {
         int32_t pos = op.pos1;
         bool hasL = seq == UNASSIGNED_SEQ;
         int32_t localSeq = hasL ? ++h.localSeq : 0;
@@ -2903,7 +2972,8 @@ struct Replica {
                 off = arena_alloc(L);
                 if (off < 0) return;
             }
-            int32_t s = insert_row(pos, refSeq, client, seq);
+            /* atT >= 0: right before the row at document coordinate atT (insertAtReferencePosition) */
+            int32_t s = atT >= 0 ? leaf_insert_slot(leaf_at(atT >> 3), atT & (MAXN - 1)) : insert_row(pos, refSeq, client, seq);
             if (s < 0) {
                 fail(E_INSERT_FAILED);
                 return;
@@ -3333,6 +3403,11 @@ struct Replica {
             int32_t start = op.pos1, end = op.pos2;
             bool bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
             if (kind != MT_OP_INSERT && end <= start) bad = true;
+            if (kind == MT_OP_INSERT && (op.kind & MT_OPF_ATREF)) { /* pos1 is a reference, not a position */
+                if constexpr (DL) insert_at_ref(op, p);
+                h.opsDone++;
+                return;
+            }
             if (bad) { /* rejected: no effect (the reference logs InvalidOpRange and returns undefined) */
                 h.opsDone++;
                 return;

@@ -68,6 +68,10 @@ enum {
  * flagged MT_OPF_GROUPED. Members apply (or, for this replica's own message, ack) one after another
  * under the one seq (client.ts:782-790, 615-622); the message's updateSeqNumbers runs after the last. */
 #define MT_OPF_GROUPED 0x40
+/* A local insert (MT_OP_INSERT | MT_OPF_LOCAL) with MT_OPF_ATREF is Client.insertAtReferencePositionLocal
+ * (client.ts:217-245, MergeTree.insertAtReferencePosition mergeTree.ts:2033-2130): pos1 is the index of
+ * one of the document's local references (MT_OP_REF); nothing happens if it is detached. */
+#define MT_OPF_ATREF 0x08
 
 /* segment kinds */
 enum {

@@ -16,6 +16,33 @@ from fluidframework_amd import oplog as ol
 import core_host
 
 SLIDE = 0x40  # ReferenceType.SlideOnRemove (ops.ts)
+OPF_ATREF = 0x08  # mt_oplog.h: a local insert at a local reference (insertAtReferencePositionLocal)
+
+
+def add_atref_inserts(b: ol.Batch, targets, texts=("@", "ref", "<at>")) -> ol.Batch:
+    """Append, after each document's whole stream, one insertAtReferencePositionLocal record per entry of
+    targets[d] (reference indices), with short texts appended to the batch's text pool."""
+    text = [b.text]
+    base = len(b.text)
+    out, off = [], [0]
+    extra = 0
+    for d in range(b.ndocs):
+        ops = b.ops[b.op_off[d]: b.op_off[d + 1]]
+        recs = np.zeros(len(targets[d]), ol.OP_DTYPE)
+        for k, ri in enumerate(targets[d]):
+            t = texts[k % len(texts)] + str(k)
+            arr = np.frombuffer(t.encode("utf-16-le"), "<u2")
+            recs[k]["kind"] = ol.OP_INSERT | ol.OPF_LOCAL | OPF_ATREF
+            recs[k]["pos1"] = int(ri)
+            recs[k]["text_off"] = base + extra - int(b.text_off[d])
+            recs[k]["text_len"] = len(arr)
+            text.append(arr)
+            extra += len(arr)
+        merged = np.concatenate([ops, recs])
+        out.append(merged)
+        off.append(off[-1] + len(merged))
+    return dataclasses.replace(b, ops=np.concatenate(out), op_off=np.asarray(off, np.int64),
+                               text=np.concatenate(text).astype(b.text.dtype))
 
 
 def inject(b: ol.Batch, caps, nref: int = 24, seed: int = 4242) -> ol.Batch:

@@ -270,12 +270,37 @@ def make_deltas(names, node: str) -> None:
 REF_SETS = ("c1_farm", "c2_observer", "c3_lagged", "c4_scaled", "c5_perm")
 
 
+def run_refs(rb, d: str, node: str):
+    write_batch(rb, gen.generator_interner(), d)
+    r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d], capture_output=True,
+                       text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+    errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
+    if errs:
+        raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
+    rp = json.load(open(os.path.join(d, "ref_refpos.json")))
+    nref = np.asarray([len(rp.get(str(i), [])) for i in range(rb.ndocs)], np.int32)
+    pos = np.full((rb.ndocs, max(nref.max(), 1)), -1, np.int32)
+    for i in range(rb.ndocs):
+        pos[i, : nref[i]] = rp.get(str(i), [])
+    blob = np.fromfile(os.path.join(d, "ref_dumps.bin"), np.uint8)
+    off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
+    digests = np.asarray([fnv1a64(blob[off[i]: off[i + 1]].tobytes()) for i in range(rb.ndocs)], np.uint64)
+    ins = json.load(open(os.path.join(d, "ref_refinside.json")))
+    inside = np.zeros(pos.shape, bool)
+    for i in range(rb.ndocs):
+        inside[i, : nref[i]] = ins.get(str(i), [])
+    return nref, pos, digests, inside
+
+
 def make_refs(names, node: str) -> None:
     """tests/golden/refrefs_<set>.npz: local references (MT_OP_REF records injected by tests/refs_inject.py)
-    replayed by the reference: LocalReference.toPosition() of every reference at the end of each document's
-    stream (-2: Client.addLocalReference threw, a reference defect: localReference.ts:195-201 pushes onto the
-    missing `at` list of an offset that holds only slid references), and the reference's digests of the
-    same replicas (references change nothing else)."""
+    replayed by the reference, then up to 4 insertAtReferencePositionLocal records per document appended
+    at the end of its stream on references the first pass left attached. Stored: the targets, and after
+    the whole stream LocalReference.toPosition() of every reference (-2: Client.addLocalReference threw, a
+    reference defect: localReference.ts:195-201 pushes onto the missing `at` list of an offset that holds
+    only slid references) and the reference's digests of the replicas."""
     import refs_inject
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from test_ref_goldens import caps_for
@@ -284,33 +309,28 @@ def make_refs(names, node: str) -> None:
         b = gen.generate(w, ids=ids, threads=8)
         c = caps_for(w)
         rb = refs_inject.inject(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
-        d = os.path.join(SCRATCH, name + "_refs")
-        write_batch(rb, gen.generator_interner(), d)
-        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d], capture_output=True,
-                           text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
-        errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
-        if errs:
-            raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
-        rp = json.load(open(os.path.join(d, "ref_refpos.json")))
-        nref = np.asarray([len(rp.get(str(i), [])) for i in range(rb.ndocs)], np.int32)
-        pos = np.full((rb.ndocs, max(nref.max(), 1)), -1, np.int32)
+        _, pos1, _, inside = run_refs(rb, os.path.join(SCRATCH, name + "_refs"), node)
+        targets = np.full((rb.ndocs, 4), -1, np.int32)
         for i in range(rb.ndocs):
-            pos[i, : nref[i]] = rp.get(str(i), [])
-        blob = np.fromfile(os.path.join(d, "ref_dumps.bin"), np.uint8)
-        off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
-        digests = np.asarray([fnv1a64(blob[off[i]: off[i + 1]].tobytes()) for i in range(rb.ndocs)], np.uint64)
+            # attached references whose offset lies inside their segment: past the end, the reference's
+            # splitAt makes a zero-length segment, which the engine does not model
+            att = np.nonzero((pos1[i] >= 0) & inside[i])[0]
+            if len(att):
+                pick = np.random.default_rng(777 + i).choice(att, size=min(4, len(att)), replace=False)
+                targets[i, : len(pick)] = pick
+        rb2 = refs_inject.add_atref_inserts(rb, [t[t >= 0] for t in targets])
+        nref, pos, digests, _ = run_refs(rb2, os.path.join(SCRATCH, name + "_refs2"), node)
         np.savez_compressed(
             os.path.join(GOLDEN, f"refrefs_{name}.npz"),
-            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(rb),
-            nref=nref, positions=pos, digests=digests,
+            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(rb2),
+            nref=nref, positions=pos, digests=digests, atref_targets=targets,
             source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
-                    "tools/ref_replay.mjs: LocalReference + Client.addLocalReference, toPosition() at the end"),
+                    "tools/ref_replay.mjs: LocalReference + Client.addLocalReference, "
+                    "insertAtReferencePositionLocal, toPosition() at the end"),
         )
-        print(f"refrefs_{name}: {rb.ndocs} docs, {int(nref.sum())} references: {int((pos >= 0).sum())} attached, "
-              f"{int((pos == -1).sum() - (pos.shape[1] * rb.ndocs - nref.sum()))} detached, "
-              f"{int((pos == -2).sum())} the reference could not add", flush=True)
+        print(f"refrefs_{name}: {rb2.ndocs} docs, {int(nref.sum())} references: {int((pos >= 0).sum())} attached, "
+              f"{int((pos == -2).sum())} the reference could not add; {int((targets >= 0).sum())} inserts at "
+              "references", flush=True)
 
 
 def main() -> None:

@@ -19,6 +19,7 @@ const timeOnly = process.argv.includes("--time");
 // (the stream SharedString's "sequenceDelta" / "maintenance" listeners see, sequence.ts:136-150) in the
 // word format of include/mt_oplog.h (MT_DELTA_*) -> batch-dir/ref_deltas.bin + ref_delta_off.bin
 const withDeltas = process.argv.includes("--deltas");
+const traceDoc = process.argv.includes("--trace-refs") ? Number(process.argv[process.argv.indexOf("--trace-refs") + 1]) : -1;
 let Client, TextSegment, Marker, PermutationSegment, SnapshotV1, LocalReference; // bound in main() (Node 12 has no top-level await)
 
 const rd = (f) => fs.readFileSync(path.join(dir, f));
@@ -110,7 +111,17 @@ function applyRange(client, doc, from, to) {
                 const seg = rec.seg_kind === 2 ? new PermutationSegment(rec.text_len)
                     : rec.seg_kind === 1 ? Marker.make(rec.pos2, ps && ps.set) : TextSegment.make(textOf(doc, rec), ps && ps.set);
                 if (rec.seg_kind === 2 && ps) seg.addProperties(ps.set);
-                client.insertSegmentLocal(rec.pos1, seg);
+                if (rec.kind & 0x08) { // MT_OPF_ATREF: insertAtReferencePositionLocal at reference pos1
+                    const r = curRefs[rec.pos1];
+                    if (traceDoc === doc) { // debugging aid (--trace-refs DOC): where every reference sits
+                        console.error(JSON.stringify(curRefs.map((x, k) => x && x.segment && {
+                            k, len: x.segment.cachedLength, off: x.offset, rm: x.segment.removedSeq, seq: x.segment.seq,
+                            pos: x.toPosition(), text: x.segment.text })));
+                    }
+                    if (r) client.insertAtReferencePositionLocal(r, seg);
+                } else {
+                    client.insertSegmentLocal(rec.pos1, seg);
+                }
             } else if (kind === 1) {
                 client.removeRangeLocal(rec.pos1, rec.pos2);
             } else if (kind === 2) {
@@ -124,7 +135,7 @@ function applyRange(client, doc, from, to) {
                     try {
                         client.addLocalReference(lref);
                     } catch (e) { // addLocalRef at an offset holding only slid refs: refsByOffset[o].at is
-                        lref = "threw"; // undefined (localReference.ts:195-201); the tree is untouched
+                        threwRefs.add(lref); // undefined (localReference.ts:195-201); the tree is untouched
                     }
                 }
                 curRefs.push(lref);
@@ -172,7 +183,9 @@ function hookDeltas(client, words) {
 }
 const deltaWords = [];
 let curRefs = []; // the local references of the document being replayed, in creation order
+const threwRefs = new Set(); // references whose addLocalReference threw
 const refPositions = {};
+const refInside = {};
 
 function replayDoc(doc, to = opOff[doc + 1], deltas = false) {
     const client = new Client(specToSegment, logger);
@@ -299,7 +312,12 @@ for (let d = 0; d < ndocs; d++) {
     try {
         const c = replayDoc(d, opOff[d + 1], withDeltas);
         // LocalReference.toPosition (localReference.ts:62-68) of every reference, -1 when detached
-        if (curRefs.length) refPositions[d] = curRefs.map((r) => (r === "threw" ? -2 : r ? r.toPosition() : -1));
+        if (curRefs.length) {
+            refPositions[d] = curRefs.map((r) => (threwRefs.has(r) ? -2 : r ? r.toPosition() : -1));
+            // an offset inside its segment (an append can leave one past the end: refsByOffset.length is not
+            // the segment's length, localReference.ts:211-223; inserting there splits off an empty segment)
+            refInside[d] = curRefs.map((r) => !!(r && r.segment && r.offset < r.segment.cachedLength));
+        }
         for (const [qd, pos, ref, cl] of queries) {
             if (qd !== d) continue;
             const mt = c.mergeTree;
@@ -364,7 +382,10 @@ if (withDeltas) {
     fs.writeFileSync(path.join(dir, "ref_deltas.bin"), Buffer.concat(parts));
     fs.writeFileSync(path.join(dir, "ref_delta_off.bin"), off);
 }
-if (Object.keys(refPositions).length) fs.writeFileSync(path.join(dir, "ref_refpos.json"), JSON.stringify(refPositions));
+if (Object.keys(refPositions).length) {
+    fs.writeFileSync(path.join(dir, "ref_refpos.json"), JSON.stringify(refPositions));
+    fs.writeFileSync(path.join(dir, "ref_refinside.json"), JSON.stringify(refInside));
+}
 fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
 if (queries.length) fs.writeFileSync(path.join(dir, "ref_answers.json"), JSON.stringify(answers));
 console.log(JSON.stringify({ ndocs, errors: Object.keys(errs).length, seconds: secs }));
