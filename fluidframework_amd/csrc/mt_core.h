@@ -2015,8 +2015,11 @@ struct Replica {
         z.ng(s) = (uint8_t)(ng + 1);
         mem_append(gid, z.rid[s]);
     }
-    /* addToPendingList (mergeTree.ts:1955-1962); the group id is the op's localSeq */
-    MT_HD void pending_add(int32_t s, int32_t gid, bool* created) {
+    /* addToPendingList (mergeTree.ts:1955-1962). Group ids increase along the pending queue: an op's
+     * group is its localSeq << 8; a group regeneratePendingOp appends takes the next id after the queue's
+     * tail (below the next op's), so acks and compaction can keep comparing ids. */
+    MT_HD void pending_add(int32_t s, int32_t localSeq, bool* created) {
+        int32_t gid = localSeq << 8;
         if (!*created) {
             if (h.gqN >= d.caps.gcap) {
                 fail(E_CAPACITY);
@@ -3315,6 +3318,123 @@ struct Replica {
         if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
     }
 
+    /* ---- reconnect: Client.regeneratePendingOp (client.ts:706-762, 855-893) -------------- */
+    MT_HD int32_t regen_gid() {
+        int32_t base = h.localSeq << 8;
+        int32_t tail = h.gqN ? d.gq()[(h.gqHead + h.gqN - 1) % d.caps.gcap] : -1;
+        return tail >= base ? tail + 1 : base + 1;
+    }
+    /* findReconnectionPostition (client.ts:675-705): the lengths of the rows before slot s that are
+     * inserted (no pending localSeq, or one <= lseq) and not removed (or removed by a local op after lseq) */
+    MT_HD int32_t recon_pos(int32_t s, int32_t lseq) {
+        int32_t ks = kpos(s / MAXN), js = s & (MAXN - 1), total = 0;
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+            int32_t n = leaf_at(k), c = k == ks ? js : nch[n];
+            int32_t v = 0;
+            int32_t j = w.lane();
+            if (j < c && j < MAXN) {
+                int32_t q = n * MAXN + j;
+                uint8_t fl = z.flags(q);
+                bool ins = !(fl & RF_LSEQ) || cold(q).lseq <= lseq;
+                bool live = z.rseq(q) == NOREM || ((fl & RF_LRSEQ) && cold(q).lrseq > lseq);
+                if (ins && live) v = z.len(q);
+            }
+            if constexpr (W::N < MAXN) {
+                for (int32_t jj = 1; jj < c; jj++) {
+                    int32_t q = n * MAXN + jj;
+                    uint8_t fl = z.flags(q);
+                    bool ins = !(fl & RF_LSEQ) || cold(q).lseq <= lseq;
+                    bool live = z.rseq(q) == NOREM || ((fl & RF_LRSEQ) && cold(q).lrseq > lseq);
+                    if (ins && live) v += z.len(q);
+                }
+            }
+            total += w.sum(v);
+            if (k == ks) break;
+        }
+        return total;
+    }
+    /* resetPendingDeltaToOps for the head pending group (an op of `kind`): its segments in document
+     * order each get a fresh single-segment group at the tail of the queue and a regenerated op at
+     * findReconnectionPostition — except a remove whose removal a remote remove has taken over
+     * (localRemovedSeq undefined). With delta events on, the regenerated ops are logged as one
+     * MT_DELTA_REGEN event. */
+    MT_HD void regen(int32_t kind) {
+        if (h.gqN <= 0) {
+            fail(E_ASSERT); /* "Segment group not at head of merge tree pending queue" */
+            return;
+        }
+        int32_t g0 = d.gq()[h.gqHead % d.caps.gcap];
+        h.gqHead = (h.gqHead + 1) % d.caps.gcap;
+        h.gqN--;
+        int32_t lseq0 = g0 >> 8;
+        /* the group's rows (<= 64) and their document coordinates, sorted: segments by ordinal */
+        constexpr int32_t MAXM = 64;
+        int32_t mrd[MAXM], mt[MAXM];
+        int32_t mn = h.memN, cnt = 0;
+        for (int32_t b = 0; b < mn; b += W::N) {
+            int32_t i = b + w.lane();
+            bool hit = i < mn && d.mgid()[i] == g0;
+            int32_t rd = hit ? d.mrid()[i] : -1;
+            uint64_t m = w.ballot(hit);
+            while (m) {
+                int32_t l = W::ffs(m);
+                m &= m - 1;
+                if (cnt >= MAXM) {
+                    fail(E_CAPACITY);
+                    return;
+                }
+                mrd[cnt++] = w.bcast(rd, l);
+            }
+        }
+        for (int32_t q = 0; q < cnt; q++) {
+            int32_t sq = slot_of(mrd[q], -1);
+            if (sq < 0) {
+                fail(E_ASSERT);
+                return;
+            }
+            mt[q] = kpos(sq / MAXN) * MAXN + (sq & (MAXN - 1));
+            for (int32_t u = q; u > 0 && mt[u - 1] > mt[u]; u--) { /* insertion sort by coordinate */
+                int32_t t0 = mt[u], r0 = mrd[u];
+                mt[u] = mt[u - 1], mrd[u] = mrd[u - 1];
+                mt[u - 1] = t0, mrd[u - 1] = r0;
+            }
+        }
+        const bool dl = dl_on();
+        int32_t nops = 0;
+        if (dl) dhead(MT_DELTA_REGEN);
+        for (int32_t r = 0; r < cnt; r++) {
+            int32_t s = slot_of(mrd[r], -1);
+            if (s < 0) {
+                fail(E_ASSERT);
+                return;
+            }
+            int32_t ng = z.ng(s); /* segment.segmentGroups.dequeue() */
+            if (ng < 1) fail(E_ASSERT);
+            if (ng > 0) z.ng(s) = (uint8_t)(ng - 1);
+            bool op = true;
+            if (kind == MT_OP_REMOVE) op = (z.flags(s) & RF_LRSEQ) != 0;
+            else if (kind == MT_OP_INSERT && z.seq(s) != UNASSIGNED_SEQ) fail(E_ASSERT);
+            else if (kind == MT_OP_ANNOTATE && !(z.flags(s) & RF_PROPS)) fail(E_ASSERT);
+            if (!op) continue;
+            int32_t pos = recon_pos(s, lseq0);
+            int32_t gN = regen_gid();
+            if (h.gqN >= d.caps.gcap) {
+                fail(E_CAPACITY);
+                return;
+            }
+            d.gq()[(h.gqHead + h.gqN) % d.caps.gcap] = gN;
+            h.gqN++;
+            row_enqueue_group(s, gN);
+            if (dl) {
+                dput(pos);
+                dput(z.len(s));
+                dput(kind);
+            }
+            nops++;
+        }
+        if (dl) dtail(nops);
+    }
+
     /* ---- ack (mergeTree.ts:1926-1953, BaseSegment.ack 486-521) ------------------------ */
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
         if (h.gqN > 0) {
@@ -3389,8 +3509,11 @@ struct Replica {
             return;
         }
         if (kind == MT_OP_REF) { /* a local reference (mt_oplog.h): the client-feature build keeps them */
-            if constexpr (DL)
+            if constexpr (DL) {
                 if (op.kind & MT_OPF_LOCAL) add_ref(op.pos1, op.pos2);
+            } else {
+                fail(E_UNSUPPORTED);
+            }
             h.opsDone++;
             return;
         }
@@ -3404,7 +3527,18 @@ struct Replica {
             bool bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
             if (kind != MT_OP_INSERT && end <= start) bad = true;
             if (kind == MT_OP_INSERT && (op.kind & MT_OPF_ATREF)) { /* pos1 is a reference, not a position */
-                if constexpr (DL) insert_at_ref(op, p);
+                if constexpr (DL)
+                    insert_at_ref(op, p);
+                else
+                    fail(E_UNSUPPORTED); /* the client-feature build (caps.rcap > 0) replays these */
+                h.opsDone++;
+                return;
+            }
+            if (op.kind & MT_OPF_REGEN) { /* regeneratePendingOp of the head pending op (mt_oplog.h) */
+                if constexpr (DL)
+                    regen(kind);
+                else
+                    fail(E_UNSUPPORTED);
                 h.opsDone++;
                 return;
             }

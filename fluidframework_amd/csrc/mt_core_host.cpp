@@ -209,6 +209,11 @@ int32_t mth_ref_positions(mth_store* s, int64_t doc, int32_t* out, int32_t cap) 
     });
 }
 
+/* pending segment groups (local ops in flight) of one doc */
+int32_t mth_pending(mth_store* s, int64_t doc) {
+    return with_replica(s, doc, [](auto& r) { return r.h.gqN; });
+}
+
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {
     with_replica(s, doc, [&](auto& r) {
         DocHdr* h = &r.h;

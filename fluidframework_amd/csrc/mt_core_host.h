@@ -10,6 +10,7 @@ mth_store* mth_create(int64_t ndocs, const int32_t* caps6);
 mth_store* mth_create_dl(int64_t ndocs, const int32_t* caps6, int32_t dcap);
 mth_store* mth_create_fx(int64_t ndocs, const int32_t* caps6, int32_t dcap, int32_t rcap);
 int32_t mth_ref_positions(mth_store* s, int64_t doc, int32_t* out, int32_t cap);
+int32_t mth_pending(mth_store* s, int64_t doc);
 int64_t mth_deltas(mth_store* s, int64_t doc, int32_t* out, int64_t cap, uint64_t* hash);
 void mth_destroy(mth_store* s);
 void mth_start_collab(mth_store* s, int64_t doc, int32_t long_id, int32_t min_seq, int32_t cur_seq);

@@ -72,6 +72,13 @@ enum {
  * (client.ts:217-245, MergeTree.insertAtReferencePosition mergeTree.ts:2033-2130): pos1 is the index of
  * one of the document's local references (MT_OP_REF); nothing happens if it is detached. */
 #define MT_OPF_ATREF 0x08
+/* A local record with MT_OPF_REGEN (kind = the pending op's kind) is Client.regeneratePendingOp for the
+ * head pending op (client.ts:706-762, 855-893; SharedSegmentSequence.reSubmitCore on reconnect): each of
+ * its segments, in document order, gets a new single-segment pending group at the tail of the queue and a
+ * regenerated op at findReconnectionPostition (675-705). The ack of the resubmitted message is then one
+ * member record per regenerated op (a NOOP if there are none). REF, ATREF and REGEN records need the
+ * client-feature build (caps.rcap or caps.dcap > 0); other engines latch MT_E_UNSUPPORTED. */
+#define MT_OPF_REGEN 0x10
 
 /* segment kinds */
 enum {
@@ -168,6 +175,8 @@ enum {
     MT_DELTA_APPEND = -1, /* MergeTreeMaintenanceType (mergeTreeDeltaCallback.ts:16-30) */
     MT_DELTA_SPLIT = -2,
     MT_DELTA_UNLINK = -3,
+    MT_DELTA_REGEN = 3, /* not a callback: the ops regeneratePendingOp returned (pos = pos1, len = the
+                           segment's length, nd = the op type; seq -1) */
 };
 #define MT_DELTA_END ((int32_t)0x80000000) /* ends an event's segment list */
 #define MT_REF_SLIDE_ON_REMOVE 0x40 /* ReferenceType.SlideOnRemove (ops.ts) */

@@ -27,6 +27,7 @@ def lib():
         L.mth_create_fx.restype = vp
         L.mth_create_fx.argtypes = [i64, vp, i32, i32]
         L.mth_ref_positions.argtypes = [vp, i64, vp, i32]
+        L.mth_pending.argtypes = [vp, i64]
         L.mth_deltas.argtypes = [vp, i64, vp, i64, vp]
         L.mth_deltas.restype = i64
         L.mth_destroy.argtypes = [vp]
@@ -113,6 +114,10 @@ class HostStore:
         buf = np.zeros(max(n, 1), np.int32)
         self.L.mth_deltas(self.h, doc, _p(buf), n, _p(h))
         return int(n), int(h[0]), buf[:n]
+
+    def pending(self, doc) -> int:
+        """segment groups in flight (local ops not yet acked)"""
+        return int(self.L.mth_pending(self.h, doc))
 
     def ref_positions(self, doc) -> np.ndarray:
         """LocalReference.toPosition() of each of the doc's local references (-1: detached)"""

@@ -333,14 +333,62 @@ def make_refs(names, node: str) -> None:
               "references", flush=True)
 
 
+REGEN_SETS = ("c1_farm", "c3_lagged", "c3_lagged_long", "c5_perm")
+
+
+def make_regen(names, node: str) -> None:
+    """tests/golden/refregen_<set>.npz: one reconnect per document (tests/regen_inject.py: REGEN records
+    for every op in flight at a seeded point; the acks of the resubmitted messages rewritten member by
+    member) replayed by the reference with Client.regeneratePendingOp (tools/ref_replay.mjs --deltas):
+    the digests of the replicas and their delta streams, which carry the regenerated ops
+    (MT_DELTA_REGEN events) between the callbacks."""
+    import regen_inject
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_ref_goldens import caps_for
+    for name in names:
+        w, ids = SETS[name]
+        b = gen.generate(w, ids=ids, threads=8)
+        c = caps_for(w)
+        rb = regen_inject.inject(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
+        d = os.path.join(SCRATCH, name + "_regen")
+        write_batch(rb, gen.generator_interner(), d)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d, "--deltas"],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+        errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
+        if errs:
+            raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
+        blob = np.fromfile(os.path.join(d, "ref_dumps.bin"), np.uint8)
+        off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
+        digests = np.asarray([fnv1a64(blob[off[i]: off[i + 1]].tobytes()) for i in range(rb.ndocs)], np.uint64)
+        words = np.fromfile(os.path.join(d, "ref_deltas.bin"), "<i4")
+        woff = np.fromfile(os.path.join(d, "ref_delta_off.bin"), "<i8")
+        per = [words[woff[i]: woff[i + 1]] for i in range(rb.ndocs)]
+        nregen = np.asarray([int(((rb.doc(i)[0]["kind"] & 0x90) == 0x90).sum()) for i in range(rb.ndocs)], np.int32)
+        np.savez_compressed(
+            os.path.join(GOLDEN, f"refregen_{name}.npz"),
+            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(rb),
+            digests=digests, nwords=np.diff(woff).astype(np.int64),
+            hashes=np.asarray([words_fnv(x) for x in per], np.uint64), nregen=nregen,
+            source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                    "tools/ref_replay.mjs --deltas: Client.regeneratePendingOp on reconnect"),
+        )
+        print(f"refregen_{name}: {rb.ndocs} docs, {int(nregen.sum())} regenerated groups", flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default=",".join(SETS))
     ap.add_argument("--node", default="node")
     ap.add_argument("--deltas", action="store_true", help="write the delta-stream fixtures (refdelta_*.npz) only")
     ap.add_argument("--refs", action="store_true", help="write the local-reference fixtures (refrefs_*.npz) only")
+    ap.add_argument("--regen", action="store_true", help="write the reconnect fixtures (refregen_*.npz) only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
+    if args.regen:
+        make_regen([n for n in args.sets.split(",") if n in REGEN_SETS], args.node)
+        return
     if args.refs:
         make_refs([n for n in args.sets.split(",") if n in REF_SETS], args.node)
         return

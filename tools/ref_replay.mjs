@@ -105,12 +105,33 @@ function applyRange(client, doc, from, to) {
         const rec = record(i);
         const kind = rec.kind & 7;
         curSeq = rec.kind & 0x80 ? -1 : rec.seq;
+        if ((rec.kind & 0x90) === 0x90) { // MT_OPF_REGEN: Client.regeneratePendingOp for the head pending op
+            const e = pendingOps.shift();
+            const newOp = client.regeneratePendingOp(e.op, e.group);
+            const ops = newOp.type === 3 ? newOp.ops : [newOp];
+            const w = [3, -1]; // MT_DELTA_REGEN
+            for (const o of ops) {
+                const len = o.type === 0 ? (typeof o.seg === "string" ? o.seg.length : o.seg.text !== undefined
+                    ? o.seg.text.length : Array.isArray(o.seg) ? o.seg[0] : 1) : o.pos2 - o.pos1;
+                w.push(o.pos1, len, o.type);
+            }
+            w.push(END, ops.length);
+            if (deltaWords[curDoc]) deltaWords[curDoc].push(...w);
+            (regenWords[curDoc] = regenWords[curDoc] || []).push(...w);
+            if (ops.length) {
+                const groups = client.peekPendingSegmentGroups(ops.length);
+                const gs = ops.length === 1 ? [groups] : groups;
+                ops.forEach((o, i) => pendingOps.push({ op: o, group: gs[i] }));
+            }
+            continue;
+        }
         if (rec.kind & 0x80) { // local edit: insertSegmentLocal / removeRangeLocal / annotateRangeLocal
             if (kind === 0) {
                 const ps = propSet(doc, rec.props);
                 const seg = rec.seg_kind === 2 ? new PermutationSegment(rec.text_len)
                     : rec.seg_kind === 1 ? Marker.make(rec.pos2, ps && ps.set) : TextSegment.make(textOf(doc, rec), ps && ps.set);
                 if (rec.seg_kind === 2 && ps) seg.addProperties(ps.set);
+                let sent;
                 if (rec.kind & 0x08) { // MT_OPF_ATREF: insertAtReferencePositionLocal at reference pos1
                     const r = curRefs[rec.pos1];
                     if (traceDoc === doc) { // debugging aid (--trace-refs DOC): where every reference sits
@@ -118,15 +139,22 @@ function applyRange(client, doc, from, to) {
                             k, len: x.segment.cachedLength, off: x.offset, rm: x.segment.removedSeq, seq: x.segment.seq,
                             pos: x.toPosition(), text: x.segment.text })));
                     }
-                    if (r) client.insertAtReferencePositionLocal(r, seg);
+                    if (r) {
+                        const before = client.peekPendingSegmentGroups();
+                        client.insertAtReferencePositionLocal(r, seg);
+                        if (client.peekPendingSegmentGroups() !== before) sent = { type: 0, pos1: 0, seg: seg.toJSONObject() };
+                    }
                 } else {
-                    client.insertSegmentLocal(rec.pos1, seg);
+                    sent = client.insertSegmentLocal(rec.pos1, seg);
                 }
+                if (sent && client.getCollabWindow().collaborating) pendingOps.push({ op: sent, group: client.peekPendingSegmentGroups() });
             } else if (kind === 1) {
-                client.removeRangeLocal(rec.pos1, rec.pos2);
+                const sent = client.removeRangeLocal(rec.pos1, rec.pos2);
+                if (sent && client.getCollabWindow().collaborating) pendingOps.push({ op: sent, group: client.peekPendingSegmentGroups() });
             } else if (kind === 2) {
                 const ps = propSet(doc, rec.props);
-                client.annotateRangeLocal(rec.pos1, rec.pos2, ps ? ps.set : {}, ps ? ps.combiningOp : undefined);
+                const sent = client.annotateRangeLocal(rec.pos1, rec.pos2, ps ? ps.set : {}, ps ? ps.combiningOp : undefined);
+                if (sent && client.getCollabWindow().collaborating) pendingOps.push({ op: sent, group: client.peekPendingSegmentGroups() });
             } else if (kind === 3) { // a local reference (mt_oplog.h MT_OP_REF) at getContainingSegment(pos1)
                 const { segment, offset } = client.getContainingSegment(rec.pos1);
                 let lref = null;
@@ -149,6 +177,9 @@ function applyRange(client, doc, from, to) {
             clientId: name(rec.client), sequenceNumber: rec.seq, referenceSequenceNumber: rec.ref_seq,
             minimumSequenceNumber: rec.min_seq, type: kind === 4 ? "noop" : "op", contents,
         });
+        if (kind !== 4 && name(rec.client) === client.longClientId) { // an ack: its groups leave the queue
+            pendingOps.splice(0, contents.type === 3 ? contents.ops.length : 1);
+        }
     }
 }
 
@@ -182,7 +213,12 @@ function hookDeltas(client, words) {
     };
 }
 const deltaWords = [];
+let curDoc = -1;
 let curRefs = []; // the local references of the document being replayed, in creation order
+// the replica's pending ops, one entry per pending segment group: {op, group} — what the runtime keeps
+// as the message contents and localOpMetadata it hands to regeneratePendingOp on reconnect
+let pendingOps = [];
+const regenWords = [];
 const threwRefs = new Set(); // references whose addLocalReference threw
 const refPositions = {};
 const refInside = {};
@@ -190,6 +226,8 @@ const refInside = {};
 function replayDoc(doc, to = opOff[doc + 1], deltas = false) {
     const client = new Client(specToSegment, logger);
     curRefs = [];
+    pendingOps = [];
+    curDoc = doc;
     if (deltas) {
         const words = [];
         deltaWords[doc] = words;
@@ -381,6 +419,11 @@ if (withDeltas) {
     off.writeBigInt64LE(BigInt(acc), 8 * ndocs);
     fs.writeFileSync(path.join(dir, "ref_deltas.bin"), Buffer.concat(parts));
     fs.writeFileSync(path.join(dir, "ref_delta_off.bin"), off);
+}
+if (regenWords.some((x) => x)) {
+    const out = {};
+    regenWords.forEach((w, d) => { if (w) out[d] = w; });
+    fs.writeFileSync(path.join(dir, "ref_regen.json"), JSON.stringify(out));
 }
 if (Object.keys(refPositions).length) {
     fs.writeFileSync(path.join(dir, "ref_refpos.json"), JSON.stringify(refPositions));
