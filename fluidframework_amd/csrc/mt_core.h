@@ -3735,6 +3735,36 @@ struct Replica {
     MT_HD int64_t get_text(int32_t refSeq, int32_t client, uint16_t* out, int64_t cap) {
         int64_t n = 0;
         const uint16_t* base = arena_base(h.arenaSide);
+        if constexpr (W::N >= MAXN * MAXN) {
+            /* 8 leaves x 8 slots per pass of the wave: each lane's row length under the perspective, one
+             * exclusive scan for the output offsets, and every lane copies its own row's text */
+            int32_t k = 0;
+            bool more = kvalid(0);
+            while (more) {
+                int32_t q = w.lane(), li = q >> 3, j = q & (MAXN - 1), leaf = -1;
+                for (int32_t i = 0; i < MAXN && more; i++) {
+                    int32_t lf = leaf_at(k);
+                    if (i == li) leaf = lf;
+                    k = knext(k);
+                    more = kvalid(k);
+                }
+                int32_t v = 0, s = -1;
+                if (leaf >= 0 && j < nch[leaf]) {
+                    s = leaf * MAXN + j;
+                    if (!(z.flags(s) & RF_NOTEXT)) v = vis(s, refSeq, client);
+                }
+                int32_t tot;
+                int64_t o = n + w.excl_scan(v, &tot);
+                if (out && v > 0 && o < cap) {
+                    const uint16_t* src = base + cold(s).toff;
+                    int64_t m = v < cap - o ? v : cap - o;
+                    for (int64_t u = 0; u < m; u++) out[o + u] = src[u];
+                }
+                n += tot;
+            }
+            w.sync();
+            return n;
+        }
         for (int32_t k = 0; kvalid(k); k = knext(k)) {
             int32_t lf = leaf_at(k), c = nch[lf];
             for (int32_t j = 0; j < c; j++) {
