@@ -384,6 +384,8 @@ int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap) {
     return logged;
 }
 
+int32_t mt_engine_ref_capacity(const mt_engine* e) { return e ? e->rcap : 0; }
+
 int32_t mt_engine_ref_positions(mt_engine* e, int32_t* nref_out, int32_t* pos_out) {
     if (!e || e->rcap <= 0) return MT_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));

@@ -19,8 +19,12 @@ const path = require("path");
 const addon = require(process.env.MT_NAPI_ADDON || path.join(__dirname, "..", "build", "mt_napi.node"));
 
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, GROUP: 3, NOOP: 4 };
+const OP_REF = 3; // record kind of a local reference (include/mt_oplog.h MT_OP_REF)
 const OPF_LOCAL = 0x80;
 const OPF_GROUPED = 0x40;
+const OPF_ATREF = 0x08; // insertAtReferencePositionLocal
+const OPF_REGEN = 0x10; // regeneratePendingOp
+const ReferenceType = { Simple: 0x0, SlideOnRemove: 0x40 }; // ops.ts
 const SEG = { TEXT: 0, MARKER: 1 };
 const VALUE_FALSY = 0x8000;
 const ERRORS = { 1: "MergeTree insert failed", 2: "assertion", 3: "invalid op range", 4: "unsupported",
@@ -53,7 +57,7 @@ class Interner {
 }
 
 /* MergeTreeDeltaType / MergeTreeMaintenanceType names of the delta stream's op words (include/mt_oplog.h) */
-const DELTA_OPS = { 0: "INSERT", 1: "REMOVE", 2: "ANNOTATE", "-1": "APPEND", "-2": "SPLIT", "-3": "UNLINK" };
+const DELTA_OPS = { 0: "INSERT", 1: "REMOVE", 2: "ANNOTATE", 3: "REGEN", "-1": "APPEND", "-2": "SPLIT", "-3": "UNLINK" };
 
 /* Decode a document's delta-stream words (include/mt_oplog.h MT_DELTA_*) into the events a SharedString
  * "sequenceDelta" (INSERT / REMOVE / ANNOTATE) or "maintenance" (APPEND / SPLIT / UNLINK) listener
@@ -74,6 +78,7 @@ function decodeDeltas(words, interner) {
             const pos = words[i], length = words[i + 1], nd = words[i + 2];
             i += 3;
             const seg = { position: pos < 0 ? undefined : pos, length };
+            if (op === 3) seg.opType = nd; // REGEN: the regenerated op's type
             if (op === 2) {
                 if (nd < 0) {
                     seg.propertyDeltas = undefined; // addProperties was blocked by pending local rewrites
@@ -108,6 +113,8 @@ class ReplayEngine {
         this.localNames = new Array(ndocs).fill(undefined);
         this.collab = false;
         this.currentSeq = new Array(ndocs).fill(0);
+        this.nrefs = new Array(ndocs).fill(0);   // local references created per document
+        this.pending = Array.from({ length: ndocs }, () => []); // op types in flight, per pending group
     }
 
     longIndex(name) {
@@ -236,26 +243,37 @@ class GpuClient {
                 } else throw new Error(`op type ${m.type} unsupported`);
             });
         }
+        if (msg.type === "op" && msg.clientId === this.longClientId) { // an ack: its groups leave the queue
+            const n = msg.contents.type === OP.GROUP ? msg.contents.ops.length : 1;
+            e.pending[this.doc].splice(0, n);
+        }
         e.currentSeq[this.doc] = msg.sequenceNumber;
     }
 
-    /* local edits (client.ts:164-211): return the op to submit, as the reference does */
+    /* local edits (client.ts:164-211): return the op to submit, as the reference does. The facade keeps
+     * the type of each op in flight (one per segment group) for regeneratePendingOp; the engine rejects
+     * an invalid local range as the reference does, so callers submit only ops of valid ranges. */
     insertTextLocal(pos, text, props) {
         if (text.length === 0) return undefined;
         const seg = props ? { text, props } : text;
         this.engine.enqueue(this.doc, OP.INSERT | OPF_LOCAL, { pos1: pos }, seg);
+        this.sent(OP.INSERT);
         return { type: OP.INSERT, pos1: pos, seg };
     }
+
+    sent(type) { if (this.engine.collab) this.engine.pending[this.doc].push(type); }
 
     insertMarkerLocal(pos, refType, props) {
         const seg = { marker: { refType } };
         if (props) seg.props = props;
         this.engine.enqueue(this.doc, OP.INSERT | OPF_LOCAL, { pos1: pos }, seg);
+        this.sent(OP.INSERT);
         return { type: OP.INSERT, pos1: pos, seg };
     }
 
     removeRangeLocal(start, end) {
         this.engine.enqueue(this.doc, OP.REMOVE | OPF_LOCAL, { pos1: start, pos2: end });
+        this.sent(OP.REMOVE);
         return { type: OP.REMOVE, pos1: start, pos2: end };
     }
 
@@ -263,7 +281,44 @@ class GpuClient {
         const op = { type: OP.ANNOTATE, pos1: start, pos2: end, props };
         if (combiningOp) op.combiningOp = combiningOp;
         this.engine.enqueue(this.doc, OP.ANNOTATE | OPF_LOCAL, { pos1: start, pos2: end }, op);
+        this.sent(OP.ANNOTATE);
         return op;
+    }
+
+    /* new LocalReference + Client.addLocalReference at getContainingSegment(pos) (client.ts:295,
+     * localReference.ts:20-117); engines need caps.rcap > 0. Returns the reference's handle. */
+    createLocalReference(pos, refType = ReferenceType.SlideOnRemove) {
+        this.engine.enqueue(this.doc, OP_REF | OPF_LOCAL, { pos1: pos, pos2: refType });
+        return { doc: this.doc, index: this.engine.nrefs[this.doc]++ };
+    }
+
+    /* LocalReference.toPosition() (localReference.ts:62-68): -1 detached */
+    localReferencePosition(ref) {
+        const [n, pos] = addon.refPositions(this.read());
+        const rcap = pos.length / this.engine.ndocs;
+        return ref.index < n[this.doc] ? pos[this.doc * rcap + ref.index] : -1;
+    }
+
+    /* Client.insertAtReferencePositionLocal (client.ts:217-245) */
+    insertAtReferencePositionLocal(ref, text) {
+        this.engine.enqueue(this.doc, OP.INSERT | OPF_LOCAL | OPF_ATREF, { pos1: ref.index }, text);
+        this.sent(OP.INSERT);
+    }
+
+    /* Client.regeneratePendingOp for every op in flight, in order (client.ts:855-893; what a
+     * SharedSegmentSequence does on reconnect). The regenerated ops come back in deltaEvents() as
+     * "REGEN" events; the acks of the resubmitted messages carry one member per regenerated op. */
+    regeneratePendingOps() {
+        const e = this.engine;
+        const q = e.pending[this.doc];
+        if (q.length === 0) return [];
+        for (const type of q) e.enqueue(this.doc, type | OPF_LOCAL | OPF_REGEN, {});
+        const regen = this.deltaEvents().filter((ev) => ev.operation === "REGEN").slice(-q.length);
+        if (regen.length !== q.length) throw new Error("regeneratePendingOps needs an engine with caps.dcap > 0");
+        const ops = [];
+        for (const ev of regen) for (const sg of ev.deltaSegments) ops.push({ type: sg.opType, pos1: sg.position, length: sg.length });
+        e.pending[this.doc] = ops.map((o) => o.type);
+        return ops; // per regenerated op: type, findReconnectionPostition, the segment's length
     }
 
     /* reads flush the queued events first */
@@ -292,4 +347,4 @@ class GpuClient {
     deltaEvents() { return decodeDeltas(addon.deltas(this.read(), this.doc), this.engine.interner); }
 }
 
-module.exports = { ReplayEngine, GpuClient, Interner, addon, OP, DEFAULT_CAPS, decodeDeltas };
+module.exports = { ReplayEngine, GpuClient, Interner, addon, OP, DEFAULT_CAPS, decodeDeltas, ReferenceType };

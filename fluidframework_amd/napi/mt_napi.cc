@@ -221,6 +221,31 @@ static napi_value js_digests(napi_env env, napi_callback_info info) {
     return ta;
 }
 
+/* refPositions(h) -> [Int32Array nref (per doc), Int32Array positions (ndocs x rcap)]:
+ * LocalReference.toPosition() of every local reference (mt_engine_ref_positions) */
+static napi_value js_ref_positions(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    int64_t nd = mt_engine_ndocs(e);
+    int32_t rcap = mt_engine_ref_capacity(e);
+    if (rcap <= 0) return throw_status(env, e, MT_E_ARG, "refPositions (engine created without caps.rcap)");
+    napi_value out, ab[2], ta[2];
+    void* p[2];
+    size_t len[2] = {(size_t)nd, (size_t)nd * (size_t)rcap};
+    for (int i = 0; i < 2; i++) {
+        NAPI_OK(napi_create_arraybuffer(env, 4 * len[i], &p[i], &ab[i]));
+        NAPI_OK(napi_create_typedarray(env, napi_int32_array, len[i], ab[i], 0, &ta[i]));
+    }
+    int32_t rc = mt_engine_ref_positions(e, (int32_t*)p[0], (int32_t*)p[1]);
+    if (rc) return throw_status(env, e, rc, "mt_engine_ref_positions");
+    NAPI_OK(napi_create_array_with_length(env, 2, &out));
+    NAPI_OK(napi_set_element(env, out, 0, ta[0]));
+    NAPI_OK(napi_set_element(env, out, 1, ta[1]));
+    return out;
+}
+
 /* deltas(h, doc) -> Int32Array: the doc's logged delta-stream words (include/mt_oplog.h MT_DELTA_*) */
 static napi_value js_deltas(napi_env env, napi_callback_info info) {
     napi_value argv[2];
@@ -337,7 +362,7 @@ static napi_value init(napi_env env, napi_value exports) {
                {"errors", js_errors},       {"digests", js_digests},          {"getLength", js_get_length},
                {"getText", js_get_text},    {"getContainingSegment", js_get_containing},
                {"getPosition", js_get_position}, {"ndocs", js_ndocs},        {"lastRunMs", js_last_run_ms},
-               {"deltas", js_deltas}};
+               {"deltas", js_deltas},       {"refPositions", js_ref_positions}};
     for (auto& f : fns) {
         napi_value fn;
         NAPI_OK(napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn));

@@ -128,6 +128,8 @@ int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap);
  * the next (or last) segment and detaches the rest (mergeTree.ts:2703-2732, localReference.ts:
  * 251-342). */
 int32_t mt_engine_ref_positions(mt_engine* e, int32_t* nref_out, int32_t* pos_out);
+/* caps.rcap of the engine (the row length of mt_engine_ref_positions' pos_out) */
+int32_t mt_engine_ref_capacity(const mt_engine* e);
 /* Per-doc counters: nleaf, high-water row slots, high-water heap, events applied. */
 int32_t mt_engine_stats(mt_engine* e, int32_t* out4_per_doc);
 int64_t mt_engine_ndocs(const mt_engine* e);

@@ -64,4 +64,20 @@ dc.applyMsg({ clientId: "B", sequenceNumber: 2, referenceSequenceNumber: 1, mini
 dc.applyMsg({ clientId: "B", sequenceNumber: 3, referenceSequenceNumber: 2, minimumSequenceNumber: 0,
     type: "op", contents: { type: 1, pos1: 5, pos2: 6 } });
 out.deltas = dc.deltaEvents();
+
+// a local reference, a remove that slides it, an insert at it, then a reconnect (regeneratePendingOp)
+const reng = new ReplayEngine(1, { ...DEFAULT_CAPS, dcap: 4096, rcap: 8 });
+const rc = reng.client(0);
+reng.startCollaboration(["me"]);
+rc.applyMsg({ clientId: "B", sequenceNumber: 1, referenceSequenceNumber: 0, minimumSequenceNumber: 0,
+    type: "op", contents: { type: 0, pos1: 0, seg: "hello world" } });
+const ref = rc.createLocalReference(6);
+out.refBefore = rc.localReferencePosition(ref);
+rc.applyMsg({ clientId: "B", sequenceNumber: 2, referenceSequenceNumber: 1, minimumSequenceNumber: 0,
+    type: "op", contents: { type: 1, pos1: 5, pos2: 8 } });
+out.refSlid = rc.localReferencePosition(ref);
+rc.insertAtReferencePositionLocal(ref, "X");
+out.refText = rc.getText();
+out.refAfterInsert = rc.localReferencePosition(ref);
+out.regen = rc.regeneratePendingOps();
 console.log(JSON.stringify(out));

@@ -21,7 +21,7 @@ NODE = shutil.which("node")
 pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
 EXPORTS = ["create", "startCollab", "submit", "run", "sync", "reset", "errors", "digests", "getLength", "getText",
-           "getContainingSegment", "getPosition", "ndocs", "lastRunMs", "deltas"]
+           "getContainingSegment", "getPosition", "ndocs", "lastRunMs", "deltas", "refPositions"]
 
 
 def _node(script: str) -> str:
@@ -98,3 +98,8 @@ def test_known_answers_through_node():
                   ("ANNOTATE", 2, [(0, 5, {"bold": None})]),
                   ("SPLIT", 3, [(None, 1, None), (None, 5, None)]),
                   ("REMOVE", 3, [(5, 1, None)])]
+    # local reference at "w"; the remove of " wo" slides it to "rld" (position 5); an insert at it goes
+    # before "rld" and after the tombstone; reconnect regenerates that insert at 5
+    # (localReference.ts, mergeTree.ts:2033-2130, client.ts:675-762)
+    assert (out["refBefore"], out["refSlid"], out["refText"], out["refAfterInsert"]) == (6, 5, "helloXrld", 6)
+    assert out["regen"] == [{"type": 0, "pos1": 5, "length": 1}]
