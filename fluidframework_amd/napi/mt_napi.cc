@@ -107,12 +107,16 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
         NAPI_OK(napi_get_named_property(env, argv[2], names[i], &f));
         if (!i32_of(env, f, fields[i])) return nullptr;
     }
-    bool has_dcap = false; /* optional: delta event log words per doc (mt_caps.dcap) */
-    NAPI_OK(napi_has_named_property(env, argv[2], "dcap", &has_dcap));
-    if (has_dcap) {
+    /* optional: delta event log words (mt_caps.dcap) and local references (mt_caps.rcap) per doc */
+    const char* opt[2] = {"dcap", "rcap"};
+    int32_t* ofield[2] = {&caps.dcap, &caps.rcap};
+    for (int i = 0; i < 2; i++) {
+        bool has = false;
+        NAPI_OK(napi_has_named_property(env, argv[2], opt[i], &has));
+        if (!has) continue;
         napi_value f;
-        NAPI_OK(napi_get_named_property(env, argv[2], "dcap", &f));
-        if (!i32_of(env, f, &caps.dcap)) return nullptr;
+        NAPI_OK(napi_get_named_property(env, argv[2], opt[i], &f));
+        if (!i32_of(env, f, ofield[i])) return nullptr;
     }
     mt_engine* e = nullptr;
     int32_t rc = mt_engine_create(device, ndocs, &caps, &e);
