@@ -143,7 +143,9 @@ class ReplayEngine {
         const r = { kind, seg_kind: 0, client: 0, seq: 0, ref_seq: 0, min_seq: 0, pos1: 0, pos2: 0, text_off: 0,
             text_len: 0, props: 0, ...fields };
         const k = kind & 7;
-        if (k === OP.INSERT) {
+        if (kind & OPF_REGEN) {
+            // regeneratePendingOp: the record names only the pending op's type
+        } else if (k === OP.INSERT) {
             const seg = segOrProps;
             let props;
             if (typeof seg === "string") {
