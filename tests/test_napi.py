@@ -100,6 +100,7 @@ def test_known_answers_through_node():
                   ("REMOVE", 3, [(5, 1, None)])]
     # local reference at "w"; the remove of " wo" slides it to "rld" (position 5); an insert at it goes
     # before "rld" and after the tombstone; reconnect regenerates that insert at 5
-    # (localReference.ts, mergeTree.ts:2033-2130, client.ts:675-762)
+    # (localReference.ts, mergeTree.ts:2033-2130, client.ts:675-762); the same scenario on the
+    # type-erased reference gives these values
     assert (out["refBefore"], out["refSlid"], out["refText"], out["refAfterInsert"]) == (6, 5, "helloXrld", 6)
     assert out["regen"] == [{"type": 0, "pos1": 5, "length": 1}]
