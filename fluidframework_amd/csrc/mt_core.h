@@ -131,13 +131,15 @@ struct DocHdr {
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
 };
 /* the int32 fields of DocHdr the replica keeps in registers while it runs; the rarely used ones
- * (nclients, nextSid, errOp, nkeys, hwSlots, gcEpoch, loadPos, ovTop, ovFree) stay in the image
- * and are read and written there (z.h), which keeps the replay loop's scalar registers for the
- * fields every event touches */
+ * (nclients, nextSid, errOp, nkeys, hwSlots, gcEpoch, loadPos, ovTop, ovFree, and since round 2 root,
+ * nfree, freeHead, nfreeRid, hwHeap, seqOps) stay in the image and are read and written there (z.h),
+ * which keeps the replay loop's scalar registers for the fields every event touches. The last six
+ * took the config-3 kernel from 227 to 79 VGPR spills and from 164.8M to 184.7M ops/s
+ * (profiles/r02_spill_variants.txt). */
 #define MT_HDR_FIELDS(X)                                                                          \
-    X(root) X(nleaf) X(freeHead) X(nfree) X(currentSeq) X(minSeq) X(localSeq) X(collaborating)   \
+    X(nleaf) X(currentSeq) X(minSeq) X(localSeq) X(collaborating)   \
     X(localShort) X(localLong) X(heapN) X(memN) X(gqHead) X(gqN) X(arenaTop) X(arenaSide) X(err) \
-    X(opsDone) X(hwHeap) X(nrows) X(seqOps) X(nfreeRid) X(localLen) X(heapTop)
+    X(opsDone) X(nrows) X(localLen) X(heapTop)
 
 /* Cold per-row data, indexed by a row id that does not move when the row's slot moves. K = the
  * profile's property key slots per document. */
@@ -439,13 +441,13 @@ struct Replica {
 
     /* ---- node allocation ------------------------------------------------------------- */
     MT_HD int32_t alloc_node(int8_t level) {
-        int32_t n = h.freeHead;
+        int32_t n = z.h.freeHead;
         if (n < 0) {
             fail(E_CAPACITY);
             return -1;
         }
-        h.freeHead = npar[n];
-        h.nfree--;
+        z.h.freeHead = npar[n];
+        z.h.nfree--;
         npar[n] = -1;
         nch[n] = 0;
         nlev[n] = level;
@@ -464,10 +466,10 @@ struct Replica {
         w.sync();
     }
     MT_HD void free_node(int32_t n) {
-        npar[n] = (IX)h.freeHead;
+        npar[n] = (IX)z.h.freeHead;
         nch[n] = 0;
-        h.freeHead = n;
-        h.nfree++;
+        z.h.freeHead = n;
+        z.h.nfree++;
     }
 
     /* ---- init -------------------------------------------------------------------------- */
@@ -501,11 +503,11 @@ struct Replica {
         }
         w.sync();
         if constexpr (TILED) rope_init();
-        h.nfreeRid = HT::S;
+        z.h.nfreeRid = HT::S;
         z.h.gcEpoch = 0;
-        h.freeHead = 1;
-        h.nfree = ncap - 1;
-        h.root = 0;
+        z.h.freeHead = 1;
+        z.h.nfree = ncap - 1;
+        z.h.root = 0;
         npar[0] = -1;
         lo[0] = 0;
         lp[0] = 0;
@@ -529,9 +531,9 @@ struct Replica {
         z.h.nkeys = 0;
         h.opsDone = 0;
         z.h.hwSlots = 0;
-        h.hwHeap = 0;
+        z.h.hwHeap = 0;
         h.nrows = 0;
-        h.seqOps = 0;
+        z.h.seqOps = 0;
         h.sumR = 0;
         h.sumW = 0;
         h.localLen = 0;
@@ -1065,17 +1067,17 @@ struct Replica {
     }
     /* cold row ids */
     MT_HD int32_t alloc_rid() {
-        int32_t n = h.nfreeRid;
+        int32_t n = z.h.nfreeRid;
         if (n <= 0) {
             fail(E_CAPACITY);
             return 0;
         }
-        h.nfreeRid = n - 1;
+        z.h.nfreeRid = n - 1;
         return d.frid()[n - 1];
     }
     MT_HD void free_rid(int32_t r) {
         z.rgen[r]++;
-        d.frid()[h.nfreeRid++] = (IX)r;
+        d.frid()[z.h.nfreeRid++] = (IX)r;
     }
     /* record leaf n as the holder of its first `cnt` rows */
     MT_HD void set_leaf_of_rows(int32_t n, int32_t cnt) {
@@ -1821,7 +1823,7 @@ struct Replica {
                 nch[r] = 2;
                 npar[n] = (IX)r;
                 npar[nn] = (IX)r;
-                h.root = r;
+                z.h.root = r;
                 return first;
             }
             node_insert_child(p, child_index(p, n) + 1, nn);
@@ -2057,7 +2059,7 @@ struct Replica {
         }
         int32_t k = n + 1; /* L[k] (1-based) lives at index k-1 */
         h.heapN = n + 1;
-        if (n + 1 > h.hwHeap) h.hwHeap = n + 1;
+        if (n + 1 > z.h.hwHeap) z.h.hwHeap = n + 1;
         uint8_t gen = z.rgen[rid];
         if constexpr (W::N >= 32) {
             int32_t l = w.lane();
@@ -2602,12 +2604,12 @@ struct Replica {
         }
         uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
         if ((drop >> q) & 1) {
-            int32_t pos = h.nfreeRid + __builtin_popcountll(drop & below);
+            int32_t pos = z.h.nfreeRid + __builtin_popcountll(drop & below);
             z.rgen[r.rid]++;
             d.frid()[pos] = (IX)r.rid;
         }
         int32_t ndrop = __builtin_popcountll(drop);
-        h.nfreeRid += ndrop;
+        z.h.nfreeRid += ndrop;
         h.nrows -= ndrop;
         /* compaction: kept rows move down within their leaf; vacated slots get length 0 */
         uint64_t lmask = n >= 0 ? (0xFFull << (8 * li)) : 0ull;
@@ -3559,7 +3561,7 @@ struct Replica {
         }
         get_or_add_short(op.client);
         bool grouped = (op.kind & MT_OPF_GROUPED) != 0; /* a group member before the last (mt_oplog.h) */
-        if (!grouped) h.seqOps++; /* one sequenced message per group */
+        if (!grouped) z.h.seqOps++; /* one sequenced message per group */
         if (grouped) {
         } else if constexpr (TILED) /* BASELINE.md tile formula, in 16-byte units: 4 B per chunk summary,
                                 64 B per window row, 640 B for the target chunk's leaves + leaf line */
@@ -3650,8 +3652,8 @@ struct Replica {
             cnt = m;
             lvl++;
         }
-        h.root = hrd[0];
-        npar[h.root] = -1;
+        z.h.root = hrd[0];
+        npar[z.h.root] = -1;
     }
     /* one loaded segment into slot s (a fresh row): text / marker / permutation, props, merge info */
     MT_HD bool place_loaded(const mt_op_rec& op, const Pools& p, int32_t s) {
