@@ -126,7 +126,7 @@ struct DocHdr {
     int32_t heapTop;       /* maxSeq of the heap's root (valid when heapN > 0) */
     int32_t loadPos;       /* snapshot load: the next position of the open loadBody batch (mt_oplog.h) */
     int32_t ovTop, ovFree; /* overlap overflow pool: next never-used block, free-list head (0 = none) */
-    int32_t _r2;
+    int32_t gidNext;       /* id of the next pending segment group (ids increase along the queue) */
     int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
 };
@@ -306,7 +306,8 @@ struct Doc {
     /* client-feature region (only when c.dcap > 0 or c.rcap > 0): DState, dcap delta-log words, rcap
      * local references */
     MT_HD static bool has_fx(const Caps& c) { return c.dcap > 0 || c.rcap > 0; }
-    MT_HD static int64_t off_dl(const Caps& c) { return off_gq(c) + align256c(4 * (int64_t)c.gcap); }
+    MT_HD static int64_t off_gql(const Caps& c) { return off_gq(c) + align256c(4 * (int64_t)c.gcap); }
+    MT_HD static int64_t off_dl(const Caps& c) { return off_gql(c) + align256c(4 * (int64_t)c.gcap); }
     MT_HD static int64_t off_refs(const Caps& c) {
         return off_dl(c) + (int64_t)sizeof(DState) + ((4 * (int64_t)c.dcap + 15) & ~(int64_t)15);
     }
@@ -325,6 +326,7 @@ struct Doc {
     MT_HD int32_t* mgid() const { return (int32_t*)(b + off_mgid(caps)); }
     MT_HD int32_t* mrid() const { return (int32_t*)(b + off_mrid(caps)); } /* row id of each membership entry */
     MT_HD int32_t* gq() const { return (int32_t*)(b + off_gq(caps)); }
+    MT_HD int32_t* gql() const { return (int32_t*)(b + off_gql(caps)); } /* each queued group's SegmentGroup.localSeq */
 };
 
 /* Op pools of one document. */
@@ -538,7 +540,8 @@ struct Replica {
         h.sumW = 0;
         h.localLen = 0;
         h.heapTop = 0;
-        z.h.loadPos = h._r2 = 0;
+        z.h.loadPos = 0;
+        z.h.gidNext = 0;
         z.h.ovTop = 1; /* block 0 is the null link */
         z.h.ovFree = 0;
         for (int32_t b = 0; b < HT::C; b += W::N) {
@@ -785,6 +788,15 @@ struct Replica {
         int32_t rs0 = z.rseq(s);
         int32_t off = (rs0 != NOREM && rs0 != 0) ? 0 : r.off; /* getOffset() */
         if (off != 0 && local_len(s) != 0) {
+            /* Past the segment's end (an append adds refsByOffset.length, not the length, to the offsets
+             * it takes over, localReference.ts:211-223) a text segment splits off an empty segment, which
+             * split_row models. A PermutationSegment would take a negative length and grow its left part
+             * (permutationvector.ts:103-114), and a Marker does not split, so the reference's
+             * assert(splitSeg.next) throws (mergeTree.ts:2082-2083): neither is modelled. */
+            if (off >= z.len(s) && (z.flags(s) & RF_NOTEXT)) {
+                fail(E_UNSUPPORTED);
+                return;
+            }
             int32_t rs = -1;
             if (split_row(kpos(s / MAXN) * MAXN + (s & (MAXN - 1)), off, &rs) < 0 || rs < 0) return;
             s = rs;
@@ -1928,10 +1940,18 @@ struct Replica {
         if (cl.ovx) ovl_clone(rs, ls);
         if (refs_on()) refs_split(z.rid[ls], rrid, off);
         int32_t lenL = z.len(ls);
-        z.len(rs) = lenL - off;
-        cr.toff = cl.toff + (uint32_t)off;
-        z.len(ls) = off;
-        z.flags(ls) &= (uint8_t)~RF_NLK; /* the left part's last unit is not known any more */
+        if (off < lenL) {
+            z.len(rs) = lenL - off;
+            cr.toff = cl.toff + (uint32_t)off;
+            z.len(ls) = off;
+            z.flags(ls) &= (uint8_t)~RF_NLK; /* the left part's last unit is not known any more */
+        } else { /* a split at or past the end (a local reference past its segment's end): text.substring(off)
+                    is "", so the right part is an empty segment and the left keeps its text
+                    (textSegment.ts:103-111); insert_at_ref admits text rows only */
+            z.len(rs) = 0;
+            cr.toff = cl.toff + (uint32_t)lenL;
+            z.flags(rs) = (uint8_t)((z.flags(rs) & ~RF_NL) | RF_NLK);
+        }
         h.nrows++;
         h.sumW += 2;
         if constexpr (TILED) {
@@ -2017,21 +2037,28 @@ struct Replica {
         z.ng(s) = (uint8_t)(ng + 1);
         mem_append(gid, z.rid[s]);
     }
-    /* addToPendingList (mergeTree.ts:1955-1962). Group ids increase along the pending queue: an op's
-     * group is its localSeq << 8; a group regeneratePendingOp appends takes the next id after the queue's
-     * tail (below the next op's), so acks and compaction can keep comparing ids. */
+    /* addToPendingList (mergeTree.ts:1955-1962). Group ids come from a per-document counter, so they
+     * increase along the pending queue (acks and compaction compare them with the head's); the ring
+     * beside the queue keeps each group's SegmentGroup.localSeq (findReconnectionPostition uses it). */
     MT_HD void pending_add(int32_t s, int32_t localSeq, bool* created) {
-        int32_t gid = localSeq << 8;
         if (!*created) {
             if (h.gqN >= d.caps.gcap) {
                 fail(E_CAPACITY);
                 return;
             }
-            d.gq()[(h.gqHead + h.gqN) % d.caps.gcap] = gid;
-            h.gqN++;
+            group_push(localSeq);
             *created = true;
         }
-        row_enqueue_group(s, gid);
+        row_enqueue_group(s, d.gq()[(h.gqHead + h.gqN - 1) % d.caps.gcap]);
+    }
+    /* pendingSegments.enqueue of a new group (the caller checked the ring's room) */
+    MT_HD void group_push(int32_t localSeq) {
+        int32_t gid = z.h.gidNext;
+        z.h.gidNext = gid + 1;
+        int32_t q = (h.gqHead + h.gqN) % d.caps.gcap;
+        d.gq()[q] = gid;
+        d.gql()[q] = localSeq;
+        h.gqN++;
     }
 
     /* ---- zamboni heap (collections.ts:212-264, LRUSegmentComparer mergeTree.ts:957-960) ---- */
@@ -2541,7 +2568,10 @@ struct Replica {
             int32_t fk = w.bcast(fl, k);
             bool ok = false;
             bool permPair = (prevFl & fk & RF_PERM) != 0;
-            if ((permPair || (!((prevFl | fk) & RF_NOTEXT) && (prevLen <= GRANULARITY || lk <= GRANULARITY))) &&
+            /* localNetLength > 0 on both sides: a zero-length row (the empty right part of a split past a
+             * segment's end) is held and leaves no prevSegment (mergeTree.ts:1355-1383) */
+            if (prevLen > 0 && lk > 0 &&
+                (permPair || (!((prevFl | fk) & RF_NOTEXT) && (prevLen <= GRANULARITY || lk <= GRANULARITY))) &&
                 ((prevFl ^ fk) & RF_PROPS) == 0) {
                 int32_t sp = w.bcast(n, prev) * MAXN + (prev & (MAXN - 1));
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
@@ -2563,7 +2593,7 @@ struct Replica {
             }
             if (!ok) {
                 keep |= 1ull << k;
-                prev = k; /* a non-removed row always has localNetLength > 0 */
+                prev = k; /* prevLen 0 (a zero-length row) stands for "no prevSegment" */
                 prevLen = lk;
                 prevFl = fk;
             }
@@ -3321,11 +3351,6 @@ struct Replica {
     }
 
     /* ---- reconnect: Client.regeneratePendingOp (client.ts:706-762, 855-893) -------------- */
-    MT_HD int32_t regen_gid() {
-        int32_t base = h.localSeq << 8;
-        int32_t tail = h.gqN ? d.gq()[(h.gqHead + h.gqN - 1) % d.caps.gcap] : -1;
-        return tail >= base ? tail + 1 : base + 1;
-    }
     /* findReconnectionPostition (client.ts:675-705): the lengths of the rows before slot s that are
      * inserted (no pending localSeq, or one <= lseq) and not removed (or removed by a local op after lseq) */
     MT_HD int32_t recon_pos(int32_t s, int32_t lseq) {
@@ -3355,60 +3380,72 @@ struct Replica {
         }
         return total;
     }
-    /* resetPendingDeltaToOps for the head pending group (an op of `kind`): its segments in document
-     * order each get a fresh single-segment group at the tail of the queue and a regenerated op at
-     * findReconnectionPostition — except a remove whose removal a remote remove has taken over
-     * (localRemovedSeq undefined). With delta events on, the regenerated ops are logged as one
-     * MT_DELTA_REGEN event. */
+    /* resetPendingDeltaToOps (client.ts:708-762) for the head pending group (an op of `kind`): its segments in
+     * document order (sorted by ordinal) each get a fresh single-segment group at the tail of the queue with
+     * the op's localSeq, and a regenerated op at findReconnectionPostition — except a remove whose removal a
+     * remote remove has taken over (localRemovedSeq undefined). With delta events on, the regenerated ops are
+     * logged as one MT_DELTA_REGEN event.
+     * The group's membership entries are marked in place with their row's document coordinate t
+     * (mgid = -(t + 2)) and taken smallest first; a processed entry becomes -1, which the closing compaction
+     * drops. Any number of segments; room for their new entries is made before the group leaves the head
+     * (a compaction after that would drop its entries). */
     MT_HD void regen(int32_t kind) {
         if (h.gqN <= 0) {
             fail(E_ASSERT); /* "Segment group not at head of merge tree pending queue" */
             return;
         }
-        int32_t g0 = d.gq()[h.gqHead % d.caps.gcap];
-        h.gqHead = (h.gqHead + 1) % d.caps.gcap;
-        h.gqN--;
-        int32_t lseq0 = g0 >> 8;
-        /* the group's rows (<= 64) and their document coordinates, sorted: segments by ordinal */
-        constexpr int32_t MAXM = 64;
-        int32_t mrd[MAXM], mt[MAXM];
+        int32_t hq = h.gqHead % d.caps.gcap;
+        int32_t g0 = d.gq()[hq], lseq0 = d.gql()[hq];
         int32_t mn = h.memN, cnt = 0;
         for (int32_t b = 0; b < mn; b += W::N) {
             int32_t i = b + w.lane();
-            bool hit = i < mn && d.mgid()[i] == g0;
-            int32_t rd = hit ? d.mrid()[i] : -1;
-            uint64_t m = w.ballot(hit);
-            while (m) {
-                int32_t l = W::ffs(m);
-                m &= m - 1;
-                if (cnt >= MAXM) {
-                    fail(E_CAPACITY);
-                    return;
-                }
-                mrd[cnt++] = w.bcast(rd, l);
-            }
+            cnt += w.sum(i < mn && d.mgid()[i] == g0 ? 1 : 0);
         }
-        for (int32_t q = 0; q < cnt; q++) {
-            int32_t sq = slot_of(mrd[q], -1);
-            if (sq < 0) {
-                fail(E_ASSERT);
+        if (h.memN + cnt > d.caps.mcap) {
+            mem_compact();
+            if (h.memN + cnt > d.caps.mcap) {
+                fail(E_CAPACITY);
                 return;
             }
-            mt[q] = kpos(sq / MAXN) * MAXN + (sq & (MAXN - 1));
-            for (int32_t u = q; u > 0 && mt[u - 1] > mt[u]; u--) { /* insertion sort by coordinate */
-                int32_t t0 = mt[u], r0 = mrd[u];
-                mt[u] = mt[u - 1], mrd[u] = mrd[u - 1];
-                mt[u - 1] = t0, mrd[u - 1] = r0;
+        }
+        h.gqHead = (h.gqHead + 1) % d.caps.gcap;
+        h.gqN--;
+        mn = h.memN;
+        for (int32_t b = 0; b < mn; b += W::N) { /* mark: each member's coordinate (per lane: its leaf's 8 slots) */
+            int32_t i = b + w.lane();
+            if (i < mn && d.mgid()[i] == g0) {
+                int32_t rd = d.mrid()[i], lf = z.rleaf[rd], t = -1;
+                for (int32_t j = 0; j < MAXN; j++)
+                    if (j < nch[lf] && z.rid[lf * MAXN + j] == rd) t = kpos(lf) * MAXN + j;
+                d.mgid()[i] = t >= 0 ? -(t + 2) : -1;
+                if (t < 0) fail(E_ASSERT);
             }
         }
+        w.sync();
         const bool dl = dl_on();
         int32_t nops = 0;
         if (dl) dhead(MT_DELTA_REGEN);
-        for (int32_t r = 0; r < cnt; r++) {
-            int32_t s = slot_of(mrd[r], -1);
+        for (int32_t r = 0; r < cnt && !h.err; r++) {
+            int32_t best = -1, bi = -1; /* the marked entry with the smallest coordinate (largest mark) */
+            for (int32_t b = 0; b < mn; b += W::N) {
+                int32_t i = b + w.lane();
+                int32_t v = i < mn ? d.mgid()[i] : 0;
+                int32_t m = w.max(v <= -2 ? v : INT32_MIN);
+                if (m != INT32_MIN && (bi < 0 || m > best)) {
+                    best = m;
+                    bi = b + W::ffs(w.ballot(v == m));
+                }
+            }
+            if (bi < 0) {
+                fail(E_ASSERT);
+                break;
+            }
+            d.mgid()[bi] = -1;
+            w.sync();
+            int32_t s = slot_at(-(best + 2));
             if (s < 0) {
                 fail(E_ASSERT);
-                return;
+                break;
             }
             int32_t ng = z.ng(s); /* segment.segmentGroups.dequeue() */
             if (ng < 1) fail(E_ASSERT);
@@ -3419,14 +3456,12 @@ struct Replica {
             else if (kind == MT_OP_ANNOTATE && !(z.flags(s) & RF_PROPS)) fail(E_ASSERT);
             if (!op) continue;
             int32_t pos = recon_pos(s, lseq0);
-            int32_t gN = regen_gid();
             if (h.gqN >= d.caps.gcap) {
                 fail(E_CAPACITY);
-                return;
+                break;
             }
-            d.gq()[(h.gqHead + h.gqN) % d.caps.gcap] = gN;
-            h.gqN++;
-            row_enqueue_group(s, gN);
+            group_push(lseq0); /* { segments: [], localSeq: segmentGroup.localSeq } (client.ts:755-758) */
+            row_enqueue_group(s, d.gq()[(h.gqHead + h.gqN - 1) % d.caps.gcap]);
             if (dl) {
                 dput(pos);
                 dput(z.len(s));
@@ -3435,6 +3470,7 @@ struct Replica {
             nops++;
         }
         if (dl) dtail(nops);
+        mem_compact();
     }
 
     /* ---- ack (mergeTree.ts:1926-1953, BaseSegment.ack 486-521) ------------------------ */

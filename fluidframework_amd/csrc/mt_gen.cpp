@@ -141,7 +141,16 @@ static const char ALNUM[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxy
 #define ANN_RECORDS 20
 #define INS_RECORDS 4096
 #define CLIENT_RECORDS 32 /* {client: "<name>"} for the farm's annotateRange (mergeTreeOperationRunner.ts:22-24) */
+#define REW1_RECORDS 20   /* the annotate records again, with combiningOp "rewrite" */
+#define REW2_RECORDS 8    /* two-key rewrites {k1: v1, k2: v2} */
+#define REW_BASE (1 + ANN_RECORDS + INS_RECORDS + CLIENT_RECORDS)
 static int ann_props(rng_t* r) { return 1 + uni(r, 0, ANN_RECORDS - 1); }
+/* an annotate's props record: a rewrite one for rewrite_pct % of them (no draw when rewrite_pct == 0,
+ * so the other workloads' streams are unchanged) */
+static int ann_props_mix(const mtg_params* P, rng_t* r) {
+    if (P->rewrite_pct > 0 && uni(r, 0, 99) < P->rewrite_pct) return REW_BASE + uni(r, 0, REW1_RECORDS + REW2_RECORDS - 1);
+    return ann_props(r);
+}
 
 /* Draw an op valid for perspective (refSeq, client); kind forced to insert on an empty view. */
 template <class HT>
@@ -179,7 +188,7 @@ static void gen_op(const mtg_params* P, rng_t* r, Model<HT>* m, int32_t refSeq, 
         e->pos1 = uni(r, 0, len - 1);
         int span = uni(r, 1, P->max_rem_len);
         e->pos2 = e->pos1 + span > len ? len : e->pos1 + span;
-        if (kind == MT_OP_ANNOTATE) e->props = (uint16_t)ann_props(r);
+        if (kind == MT_OP_ANNOTATE) e->props = (uint16_t)ann_props_mix(P, r);
     }
 }
 
@@ -634,8 +643,8 @@ static int generate(const mtg_params* P, const int64_t* ids, int64_t doc_base, i
                     int64_t text_stride, mt_op_rec* ops, int64_t* nops, uint16_t* text, int64_t* ntext, int threads) {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
-    static mt_props_rec props[ANN_RECORDS + INS_RECORDS + CLIENT_RECORDS];
-    static mt_kv kv[ANN_RECORDS + INS_RECORDS + CLIENT_RECORDS];
+    static mt_props_rec props[REW_BASE - 1 + REW1_RECORDS + REW2_RECORDS];
+    static mt_kv kv[REW_BASE - 1 + REW1_RECORDS + 3 * REW2_RECORDS];
     mtg_props_table(props, kv);
     pthread_t th[256];
     Job jobs[256];
@@ -663,7 +672,9 @@ extern "C" int mtg_generate_ids(const mtg_params* P, const int64_t* ids, int64_t
 /* The fixed props table every generated doc shares: records 1..20 annotate one key of
  * {b,i,u,c} (key ids 1..4) with value ids for JSON 0,1,2,3 (value id = v + 1; "0" is falsy)
  * or null; records 21..4116 are insert props {s: v}, key id 5, v in 0..4095; records
- * 4117..4148 are the farm's {client: "<name of client k>"}, key id 6, value id 4097 + k. */
+ * 4117..4148 are the farm's {client: "<name of client k>"}, key id 6, value id 4097 + k;
+ * records 4149..4168 are records 1..20 with combiningOp "rewrite", and 4169..4176 two-key rewrites
+ * {k1: v1, k2: v2} over {b,i,u,c} (their key/value entries follow the single-entry ones). */
 extern "C" int mtg_props_table(mt_props_rec* props, mt_kv* kv) {
     int n = 0;
     for (int k = 0; k < 4; k++)
@@ -692,6 +703,33 @@ extern "C" int mtg_props_table(mt_props_rec* props, mt_kv* kv) {
         props[n]._pad = 0;
         kv[n].key = 6;
         kv[n].value = (uint16_t)(INS_RECORDS + 1 + k);
+        n++;
+    }
+    for (int k = 0; k < 4; k++)
+        for (int v = 0; v < 5; v++) {
+            props[n].kv_off = (uint32_t)n;
+            props[n].nkv = 1;
+            props[n].combining = MT_COMBINE_REWRITE;
+            props[n]._pad = 0;
+            kv[n].key = (uint16_t)(k + 1);
+            kv[n].value = v == 4 ? 0 : (uint16_t)((v + 1) | (v == 0 ? MT_VALUE_FALSY : 0));
+            n++;
+        }
+    int nkv = n + REW2_RECORDS; /* the single-entry records' kv slots end at n + REW2_RECORDS */
+    for (int i = 0; i < REW2_RECORDS; i++) {
+        int k1 = i % 4, k2 = (i + 1 + i / 4) % 4; /* two distinct keys */
+        int v1 = (i % 3) + 1, v2 = (i % 2) ? 0 : 3; /* v2 = null on odd records: "delete k2" */
+        props[n].kv_off = (uint32_t)nkv;
+        props[n].nkv = 2;
+        props[n].combining = MT_COMBINE_REWRITE;
+        props[n]._pad = 0;
+        kv[n].key = 0; /* unused slot (keeps kv index == record index for the single-entry records) */
+        kv[n].value = 0;
+        kv[nkv].key = (uint16_t)(k1 + 1);
+        kv[nkv].value = (uint16_t)(v1 + 1);
+        kv[nkv + 1].key = (uint16_t)(k2 + 1);
+        kv[nkv + 1].value = v2 == 0 ? 0 : (uint16_t)(v2 + 1);
+        nkv += 2;
         n++;
     }
     return n;

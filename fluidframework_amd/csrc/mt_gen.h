@@ -26,6 +26,10 @@ typedef struct mtg_params {
     int32_t min_length;    /* MTG_FARM: below this local length a client only inserts      */
     int32_t group_pct;     /* MTG_LAGGED: % of edits that are replaceRange groups (insert + remove,
                               one sequenced GROUP message; sequence.ts:455-469)             */
+    int32_t rewrite_pct;   /* % of annotates that carry combiningOp {name: "rewrite"}
+                              (segmentPropertiesManager.ts:49-79): 1-2 keys, every other key of
+                              the segment deleted unless a local update of it is pending       */
+    int32_t _pad0;
     uint64_t seed_base;    /* doc d uses splitmix64 seed seed_base + d                     */
 } mtg_params;
 int mtg_generate(const mtg_params* P, int64_t doc_base, int64_t ndocs, int64_t op_stride, int64_t text_stride,

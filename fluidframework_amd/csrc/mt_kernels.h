@@ -365,9 +365,7 @@ struct mt_engine {
     bool fx = false;  /* delta events or local references: the client-feature replay build */
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
-    bool noinline = false; /* small profile: compiler-chosen inlining (MT_REPLAY_NOINLINE=1) */
-    int waves = 7;    /* occupancy target of the HBM-resident kernel (MT_REPLAY_WAVES=6|7|8) */
-    int mat_skel = 2; /* config-5 profile: 2 SkelLite in LDS, 1 Skel, 0 none (MT_REPLAY_MAT_SKEL) */
+    int waves = 8;    /* occupancy target of the HBM-resident small-profile kernel */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;

@@ -5,6 +5,9 @@
  */
 #include "mt_kernels.h"
 
+#include <algorithm>
+#include <thread>
+
 static int32_t ensure(mt_engine* e, DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return MT_OK;
@@ -36,17 +39,7 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->fx = caps->dcap > 0 || caps->rcap > 0;
     const char* g = getenv("MT_REPLAY_LDS");
     e->lds = g && g[0] == '1';
-    /* Occupancy of the HBM-resident small-profile kernel: documents are replayed one per wave and
-     * a document's events are sequential, so a batch runs in "rounds" of 1,024 x waves documents
-     * (256 CUs x 4 SIMDs). Round-2 sweep at 65,536 documents (profiles/r02_occupancy.txt): 2 / 4 /
-     * 5 / 6 / 7 / 8 waves per SIMD give 122 / 142 / 137 / 144 / 144 / 149 Mops/s: the memory
-     * system, not the wave count, sets the rate, and 8 is best at every batch size. */
-    const char* wv = getenv("MT_REPLAY_WAVES");
-    e->waves = wv ? atoi(wv) : 8;
-    const char* ni = getenv("MT_REPLAY_NOINLINE");
-    e->noinline = ni && ni[0] == '1';
-    const char* ms = getenv("MT_REPLAY_MAT_SKEL");
-    e->mat_skel = ms ? atoi(ms) : 2;
+    e->waves = 8; /* occupancy of the HBM-resident small-profile kernel (mt_prof_small.hip) */
     e->profile = prof;
     e->ops = prof == 0 ? ops_small() : prof == 1 ? ops_mid() : prof == 3 ? ops_mat() : prof == 4 ? ops_huge() : ops_big();
     if (hipSetDevice(device) != hipSuccess) {
@@ -132,24 +125,40 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
             props_off[d] < 0 || props_off[d] > nprops || kv_off[d] < 0 || kv_off[d] > nkv)
             return MT_E_ARG;
     }
-    /* every pool reference of every event must be in bounds before the kernel dereferences it */
-    for (int64_t d = 0; d < nd; d++) {
-        for (int64_t i = op_off[d]; i < op_off[d + 1]; i++) {
-            const mt_op_rec& o = ops[i];
-            int kind = o.kind & MT_OP_KIND_MASK;
-            if (kind == MT_OP_INSERT && o.seg_kind == MT_SEG_TEXT &&
-                text_off[d] + (int64_t)o.text_off + o.text_len > text_units)
-                return MT_E_ARG;
-            /* snapshot-load records carry the segment length in pos2 (mt_oplog.h) */
-            if ((kind == MT_OP_RELOAD || kind == MT_OP_APPEND) && o.seg_kind == MT_SEG_TEXT &&
-                (o.pos2 < 0 || text_off[d] + (int64_t)o.text_off + o.pos2 > text_units))
-                return MT_E_ARG;
-            if (o.props) {
-                if (props_off[d] + (int64_t)o.props > nprops) return MT_E_ARG;
-                const mt_props_rec& pr = props[props_off[d] + o.props - 1];
-                if (kv_off[d] + (int64_t)pr.kv_off + pr.nkv > nkv) return MT_E_ARG;
+    /* every pool reference of every event must be in bounds before the kernel dereferences it: the
+     * documents are checked in parallel on the host (up to 16 threads, one contiguous range each) */
+    auto check = [&](int64_t d0, int64_t d1) -> bool {
+        for (int64_t d = d0; d < d1; d++) {
+            for (int64_t i = op_off[d]; i < op_off[d + 1]; i++) {
+                const mt_op_rec& o = ops[i];
+                int kind = o.kind & MT_OP_KIND_MASK;
+                if (kind == MT_OP_INSERT && o.seg_kind == MT_SEG_TEXT &&
+                    text_off[d] + (int64_t)o.text_off + o.text_len > text_units)
+                    return false;
+                /* snapshot-load records carry the segment length in pos2 (mt_oplog.h) */
+                if ((kind == MT_OP_RELOAD || kind == MT_OP_APPEND) && o.seg_kind == MT_SEG_TEXT &&
+                    (o.pos2 < 0 || text_off[d] + (int64_t)o.text_off + o.pos2 > text_units))
+                    return false;
+                if (o.props) {
+                    if (props_off[d] + (int64_t)o.props > nprops) return false;
+                    const mt_props_rec& pr = props[props_off[d] + o.props - 1];
+                    if (kv_off[d] + (int64_t)pr.kv_off + pr.nkv > nkv) return false;
+                }
             }
         }
+        return true;
+    };
+    int nth = nops > (1 << 20) ? (int)std::min<int64_t>(16, std::max<unsigned>(1, std::thread::hardware_concurrency())) : 1;
+    if (nth <= 1) {
+        if (!check(0, nd)) return MT_E_ARG;
+    } else {
+        std::vector<std::thread> th;
+        std::vector<char> ok((size_t)nth, 1);
+        for (int t = 0; t < nth; t++)
+            th.emplace_back([&, t] { ok[(size_t)t] = check(nd * t / nth, nd * (t + 1) / nth); });
+        for (auto& x : th) x.join();
+        for (char c : ok)
+            if (!c) return MT_E_ARG;
     }
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc;

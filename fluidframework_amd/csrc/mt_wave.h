@@ -16,6 +16,7 @@ struct WaveHost {
         return 0;
     }
     int32_t sum(int32_t v) const { return v; }
+    int32_t max(int32_t v) const { return v; }
     uint64_t ballot(bool p) const { return p ? 1ull : 0ull; }
     int32_t bcast(int32_t v, int) const { return v; }
     static int32_t uniform(int32_t v) { return v; }
@@ -54,6 +55,14 @@ struct WaveGPU {
     }
     __device__ __attribute__((always_inline)) int32_t sum(int32_t v) const {
         return __builtin_amdgcn_readlane(incl_scan(v), 63);
+    }
+    /* maximum over the 64 lanes (butterfly over ds_bpermute; off the per-event path) */
+    __device__ __attribute__((always_inline)) int32_t max(int32_t v) const {
+        for (int o = 32; o > 0; o >>= 1) {
+            int32_t u = __shfl_xor(v, o);
+            v = u > v ? u : v;
+        }
+        return __builtin_amdgcn_readfirstlane(v);
     }
     __device__ __attribute__((always_inline)) uint64_t ballot(bool p) const { return __ballot(p); }
     /* a value every lane holds equally, moved to an SGPR */

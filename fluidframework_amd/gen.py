@@ -12,14 +12,15 @@ from . import oplog as ol
 
 MTG_FARM, MTG_OBSERVER, MTG_LAGGED, MTG_MATRIX = 1, 2, 3, 5
 ALNUM = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789"
-N_PROPS = 20 + 4096 + 32  # mtg_props_table records
+N_PROPS = 20 + 4096 + 32 + 20 + 8  # mtg_props_table records
+N_KV = N_PROPS + 16  # their key/value entries (the last 8 records hold two each, after the others)
 
 
 class _Params(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "mode", "ops_per_doc", "nclients", "max_lag", "local_pct", "ack_lag", "pct_insert",
         "pct_remove", "max_ins_len", "max_rem_len", "distinct_props", "newline_pct", "model_ncap",
-        "model_acap", "perm", "round_ops", "min_length", "group_pct")] + [
+        "model_acap", "perm", "round_ops", "min_length", "group_pct", "rewrite_pct", "_pad0")] + [
         ("seed_base", ctypes.c_uint64)]
 
 
@@ -43,6 +44,8 @@ class Workload:
     round_ops: int = 0
     min_length: int = 0
     group_pct: int = 0
+    rewrite_pct: int = 0
+    _pad0: int = 0
     seed_base: int = 0x5EED0000
 
 
@@ -62,8 +65,9 @@ def config2(ops_per_doc: int = 10_000) -> Workload:
 
 def config3(ops_per_doc: int = 4_096) -> Workload:
     """65,536 docs, 8 clients, lag <= 64, local-pending replica (~1/8 local edits); 4% of the edits
-    (local and remote) are SharedString.replaceRange groups (insert + remove in one message)."""
-    return Workload(MTG_LAGGED, ops_per_doc, max_lag=64, local_pct=12, ack_lag=64, group_pct=4)
+    (local and remote) are SharedString.replaceRange groups (insert + remove in one message); a
+    quarter of the annotates (local and remote) carry combiningOp "rewrite"."""
+    return Workload(MTG_LAGGED, ops_per_doc, max_lag=64, local_pct=12, ack_lag=64, group_pct=4, rewrite_pct=25)
 
 
 def config4(ops_per_doc: int = 1_000_000) -> Workload:
@@ -75,9 +79,9 @@ def config4(ops_per_doc: int = 1_000_000) -> Workload:
 def config5(ops_per_doc: int = 4_096) -> Workload:
     """SharedMatrix PermutationVector replay: docs 2m / 2m+1 = rows / cols vectors of matrix m,
     one sequenced stream per matrix, PermutationSegment inserts of U{1..8} rows, removes of
-    U{1..4}, 50% annotate; 8 clients, lag <= 64, local-pending replica."""
+    U{1..4}, 50% annotate (a quarter of them "rewrite"); 8 clients, lag <= 64, local-pending replica."""
     return Workload(MTG_MATRIX, ops_per_doc, max_lag=64, local_pct=12, ack_lag=64, pct_insert=32,
-                    pct_remove=18, max_ins_len=8, max_rem_len=4, perm=1)
+                    pct_remove=18, max_ins_len=8, max_rem_len=4, perm=1, rewrite_pct=25)
 
 
 _LIB = None
@@ -110,7 +114,7 @@ def generator_interner() -> ol.Interner:
 
 def props_table():
     props = np.zeros(N_PROPS, ol.PROPS_DTYPE)
-    kv = np.zeros(N_PROPS, ol.KV_DTYPE)
+    kv = np.zeros(N_KV, ol.KV_DTYPE)
     n = _lib().mtg_props_table(props.ctypes.data, kv.ctypes.data)
     assert n == len(props)
     return props, kv

@@ -69,12 +69,18 @@ function decodeDeltas(words, interner) {
     const keyName = new Map([...interner.keys].map(([k, i]) => [i, k]));
     const valueOf = new Map([...interner.values].map(([v, i]) => [i, JSON.parse(v)]));
     const events = [];
+    const n = words.length;
+    const need = (k) => { if (i + k > n) throw new Error(`truncated delta stream at word ${i} of ${n}`); };
     let i = 0;
-    while (i < words.length) {
+    while (i < n) {
+        need(2);
         const op = words[i], seq = words[i + 1];
         i += 2;
         const deltaSegments = [];
-        while (words[i] !== END) {
+        for (;;) {
+            need(1);
+            if (words[i] === END) break;
+            need(3);
             const pos = words[i], length = words[i + 1], nd = words[i + 2];
             i += 3;
             const seg = { position: pos < 0 ? undefined : pos, length };
@@ -84,6 +90,7 @@ function decodeDeltas(words, interner) {
                     seg.propertyDeltas = undefined; // addProperties was blocked by pending local rewrites
                 } else {
                     seg.propertyDeltas = {};
+                    need(nd);
                     for (let k = 0; k < nd; k++, i++) {
                         const w = words[i] >>> 0, v = w & 0xffff;
                         seg.propertyDeltas[keyName.get(w >>> 16)] = v === 0 ? null : valueOf.get(v & ~VALUE_FALSY);
@@ -92,6 +99,7 @@ function decodeDeltas(words, interner) {
             }
             deltaSegments.push(seg);
         }
+        need(2);
         if (words[i + 1] !== deltaSegments.length) throw new Error(`malformed delta stream at word ${i}`);
         i += 2;
         events.push({ operation: DELTA_OPS[op], seq, deltaSegments });
@@ -294,11 +302,15 @@ class GpuClient {
         return { doc: this.doc, index: this.engine.nrefs[this.doc]++ };
     }
 
-    /* LocalReference.toPosition() (localReference.ts:62-68): -1 detached */
+    /* LocalReference.toPosition() (localReference.ts:62-68): -1 detached. A reference whose creation the
+     * reference's Client.addLocalReference would have thrown on (its offset holds only slid references,
+     * localReference.ts:195-201) throws here, at its first read, as the reference throws at creation. */
     localReferencePosition(ref) {
         const [n, pos] = addon.refPositions(this.read());
         const rcap = pos.length / this.engine.ndocs;
-        return ref.index < n[this.doc] ? pos[this.doc * rcap + ref.index] : -1;
+        const p = ref.index < n[this.doc] ? pos[this.doc * rcap + ref.index] : -1;
+        if (p === -2) throw new Error("addLocalReference: the offset's reference list is undefined");
+        return p;
     }
 
     /* Client.insertAtReferencePositionLocal (client.ts:217-245) */
@@ -314,8 +326,10 @@ class GpuClient {
         const e = this.engine;
         const q = e.pending[this.doc];
         if (q.length === 0) return [];
+        const before = addon.deltas(this.read(), this.doc).length; // the events logged before these records
         for (const type of q) e.enqueue(this.doc, type | OPF_LOCAL | OPF_REGEN, {});
-        const regen = this.deltaEvents().filter((ev) => ev.operation === "REGEN").slice(-q.length);
+        const words = addon.deltas(this.read(), this.doc);
+        const regen = decodeDeltas(words.subarray(before), e.interner).filter((ev) => ev.operation === "REGEN");
         if (regen.length !== q.length) throw new Error("regeneratePendingOps needs an engine with caps.dcap > 0");
         const ops = [];
         for (const ev of regen) for (const sg of ev.deltaSegments) ops.push({ type: sg.opType, pos1: sg.position, length: sg.length });

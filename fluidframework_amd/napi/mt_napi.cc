@@ -259,6 +259,14 @@ static napi_value js_deltas(napi_env env, napi_callback_info info) {
     if (!e || !i64_of(env, argv[1], &doc)) return nullptr;
     int64_t n = mt_engine_deltas(e, doc, nullptr, 0);
     if (n < 0) return throw_status(env, e, (int32_t)-n, "mt_engine_deltas");
+    /* a full log holds only the first dcap words (cut mid-event): the stream is not decodable */
+    std::vector<int64_t> emitted((size_t)mt_engine_ndocs(e));
+    int32_t rc = mt_engine_delta_state(e, emitted.data(), nullptr);
+    if (rc) return throw_status(env, e, rc, "mt_engine_delta_state");
+    if (emitted[(size_t)doc] > n) {
+        napi_throw_error(env, nullptr, "delta log full: the engine's caps.dcap is too small for this document's events");
+        return nullptr;
+    }
     std::vector<int32_t> tmp((size_t)(n > 0 ? n : 1));
     int64_t m = mt_engine_deltas(e, doc, tmp.data(), n);
     if (m < 0) return throw_status(env, e, (int32_t)-m, "mt_engine_deltas");

@@ -110,6 +110,10 @@ def concat_records(a, b):
             np.concatenate([akv, bkv]))
 
 
+# canonical-dump segment flag bits (include/mt_oplog.h MT_DF_*)
+DF_HAS_PROPS, DF_REMOVED, DF_LSEQ, DF_LRSEQ = 1, 2, 4, 8
+
+
 def parse_dump(b: bytes):
     """Decode the canonical dump (include/mt_oplog.h) into (header dict, [segment dicts])."""
     hdr = struct.unpack_from("<6i", b, 0)
@@ -149,14 +153,23 @@ class DocLog:
     text: List[int] = field(default_factory=list)
     props: List[tuple] = field(default_factory=list)
     kv: List[tuple] = field(default_factory=list)
+    _pindex: Dict[tuple, int] = field(default_factory=dict, repr=False)
 
     def _props(self, props: Optional[Dict[str, Any]], combining: int = COMBINE_NONE) -> int:
+        """The record index (1-based; a record's `props` field is 16 bits) of a property set: equal sets
+        (same keys in the same order, same values, same combining op) share one record."""
         if props is None:
             return 0
+        kvs = tuple((self.interner.key(k), self.interner.value(v)) for k, v in props.items())
+        i = self._pindex.get((kvs, combining))
+        if i is not None:
+            return i
+        if len(self.props) >= 0xFFFF:
+            raise ValueError("more than 65,535 distinct property sets in one document's log")
         off = len(self.kv)
-        for k, v in props.items():
-            self.kv.append((self.interner.key(k), self.interner.value(v)))
+        self.kv.extend(kvs)
         self.props.append((off, len(props), combining, 0))
+        self._pindex[(kvs, combining)] = len(self.props)
         return len(self.props)
 
     def _text(self, text: str) -> tuple:

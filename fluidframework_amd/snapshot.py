@@ -136,6 +136,80 @@ def _blob(path: str, chunk: dict) -> dict:
     return {"mode": "100644", "path": path, "type": "Blob", "value": {"contents": _js(chunk), "encoding": "utf-8"}}
 
 
+# ---- emit, legacy format (SharedString's default summary) -------------------------------------
+CATCHUP = "catchupOps"      # SnapshotLegacy.catchupOps (snapshotlegacy.ts:56); options.catchUpBlobName
+
+
+def extract_segments_legacy(hdr, segs, interner: ol.Interner) -> List[tuple]:
+    """SnapshotLegacy.extractSync (snapshotlegacy.ts:179-242) over a parsed canonical dump: a list of
+    (json spec, length). mergeTree.map(..., minSeq, NonCollabClient) visits the segments of nonzero
+    length in that perspective (nodeMap, mergeTree.ts:2936-2998), and extractSegment keeps those
+    sequenced at or below the MSN and not removed at or below it (a pending removal, -1, is kept);
+    consecutive ones merge while prev.canAppend(segment) and their properties match (prev grows)."""
+    min_seq = hdr["minSeq"]
+    out: List[tuple] = []
+    prev = None
+    for s in segs:
+        if s["len"] <= 0 or s["seq"] == -1 or s["seq"] > min_seq:
+            continue
+        rs = s["removedSeq"]
+        if rs is not None and rs != -1 and rs <= min_seq:
+            continue
+        cur = dict(s, _props=_props(s, interner))
+        if prev is not None and _can_append(prev, cur) and prev["_props"] == cur["_props"]:
+            prev = dict(prev, len=prev["len"] + cur["len"],
+                        text=(prev["text"] + cur["text"]) if prev["kind"] == ol.SEG_TEXT else None)
+        else:
+            if prev is not None:
+                out.append((_json_spec(prev, prev["_props"]), prev["len"]))
+            prev = cur
+    if prev is not None:
+        out.append((_json_spec(prev, prev["_props"]), prev["len"]))
+    return out
+
+
+def emit_legacy(hdr, segs, interner: ol.Interner, catchup: Optional[List[dict]] = None,
+                chunk_size: int = CHUNK_SIZE, catchup_blob: str = CATCHUP) -> dict:
+    """SnapshotLegacy.extractSync + emit (snapshotlegacy.ts:104-242), what Client.snapshot writes unless
+    newMergeTreeSnapshotFormat is set (client.ts:895-935): a header chunk of the first segments up to
+    ~chunk_size characters, one body chunk with the rest, and the caller's catch-up messages
+    (SharedString's messagesSinceMSNChange: see catchup_messages) as JSON. The chunks are the legacy
+    chunk object serialized by serializeAsMinSupportedVersion (snapshotChunks.ts:76-122), key order
+    included (`version` is undefined and JSON.stringify drops it)."""
+    specs = extract_segments_legacy(hdr, segs, interner)
+    total = sum(n for _, n in specs)  # segmentsTotalLength (the extracted total wins a mismatch, 232-240)
+    seq = hdr["minSeq"]
+
+    def chunk(approx, start):  # getSeqLengthSegs (75-100)
+        seg_list, length, count = [], 0, 0
+        while length < approx and start + count < len(specs):
+            seg_list.append(specs[start + count][0])
+            length += specs[start + count][1]
+            count += 1
+        return {"chunkStartSegmentIndex": start, "chunkSegmentCount": count, "chunkLengthChars": length,
+                "totalLengthChars": total, "totalSegmentCount": len(specs), "chunkSequenceNumber": seq,
+                "segmentTexts": seg_list}
+
+    c1 = chunk(chunk_size, 0)
+    ids = [{"id": HEADER}] + ([{"id": BODY}] if c1["chunkLengthChars"] < total else [])
+    # buildHeaderMetadataForLegecyChunk (snapshotChunks.ts:165-185): minSequenceNumber is undefined
+    c1["headerMetadata"] = {"orderedChunkMetadata": ids, "sequenceNumber": seq, "totalLength": total,
+                            "totalSegmentCount": len(specs)}
+    entries = [_blob(HEADER, c1)]
+    if c1["chunkSegmentCount"] < len(specs):
+        entries.append(_blob(BODY, chunk(total, c1["chunkSegmentCount"])))
+    entries.append({"mode": "100644", "path": catchup_blob, "type": "Blob",
+                    "value": {"contents": _js(catchup or []), "encoding": "utf-8"}})
+    return {"entries": entries, "id": None}
+
+
+def emit_legacy_from_dump(dump: bytes, interner: ol.Interner, catchup: Optional[List[dict]] = None,
+                          chunk_size: int = CHUNK_SIZE, catchup_blob: str = CATCHUP) -> dict:
+    """emit_legacy over an engine / oracle canonical dump (bytes)."""
+    hdr, segs = ol.parse_dump(dump)
+    return emit_legacy(hdr, segs, interner, catchup, chunk_size, catchup_blob)
+
+
 def emit_from_dump(dump: bytes, interner: ol.Interner, long_name, chunk_size: int = CHUNK_SIZE) -> dict:
     """emit_v1 over an engine / oracle canonical dump (bytes)."""
     hdr, segs = ol.parse_dump(dump)
@@ -199,19 +273,34 @@ def load_records(tree: dict, log: ol.DocLog, client_index, local_client: Optiona
     md = head["headerMetadata"]
     body = [spec for c in chunks for spec in c["segments"]]
 
-    batch = [False]  # an open loadBody batch (snapshotLoader.ts:215-226)
+    batch = [False, False]  # an open loadBody batch; a batchable segment seen (snapshotLoader.ts:207-226)
 
     def add(kind, spec, countdown=0):
         info = {}
         if isinstance(spec, dict) and "json" in spec:  # IJSONSegmentWithMergeInfo (snapshotChunks.ts:60-73)
             info, spec = spec, spec["json"]
         if kind == ol.OP_APPEND:
-            # segments without seq and client batch into one insertSegments call: members after the
-            # first continue at the previous member's position (MT_OPF_GROUPED, mt_oplog.h)
-            batchable = info.get("seq") is None and info.get("client") is None
+            # loadBody batches a segment whose clientId is NonCollabClient and seq UniversalSequenceNumber
+            # (specToSegment: no `client`, and `seq` absent or 0; snapshotLoader.ts:93-100, 219) into one
+            # insertSegments call: members after the first continue at the previous member's position
+            # (MT_OPF_GROUPED, mt_oplog.h)
+            seq0 = "seq" not in info or (type(info["seq"]) is int and info["seq"] == 0)
+            batchable = "client" not in info and seq0
+            # The reference's flushBatch never empties `batch` (208-211): every later flush and the final
+            # one pass the already inserted segments to insertSegments again. Each such re-insert is a
+            # no-op (the walk cannot reach root.cachedLength: the segment that forced the earlier flush
+            # has seq > 0 and another client, so it is invisible under (UniversalSequenceNumber,
+            # NonCollabClient), and the segment keeps its parent, so blockInsert does not throw,
+            # mergeTree.ts:2236-2249); a segment batched after such a flush is placed past that point and
+            # throws "MergeTree insert failed", as the engine's insert of it does. A segment with a
+            # client but seq 0 would be visible there, and the re-insert would duplicate the batch.
+            if not batchable and batch[1] and seq0:
+                raise ValueError("snapshot body: a segment with a client and seq 0 after batched segments; the "
+                                 "reference's loadBody inserts the batch twice (snapshotLoader.ts:208-226)")
             if batchable and batch[0]:
                 kind |= ol.OPF_GROUPED
             batch[0] = batchable
+            batch[1] = batch[1] or batchable
         seq = info.get("seq", 0)
         client = client_index(info["client"]) if info.get("client") is not None else ol.CLIENT_NONCOLLAB
         rseq = info.get("removedSeq", 0) or 0

@@ -126,7 +126,9 @@ int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap);
  * Client.getPosition(segment) + getOffset(), -1 when detached) at pos_out[d * rcap + i]. References
  * follow their segment through splits and zamboni appends, and a remove slides SlideOnRemove ones to
  * the next (or last) segment and detaches the rest (mergeTree.ts:2703-2732, localReference.ts:
- * 251-342). */
+ * 251-342). -2: the reference's Client.addLocalReference threw for this reference (its offset holds
+ * only slid references, so refsByOffset[offset].at is undefined, localReference.ts:195-201); the
+ * reference keeps no such reference, and the engine leaves the tree untouched for it. */
 int32_t mt_engine_ref_positions(mt_engine* e, int32_t* nref_out, int32_t* pos_out);
 /* caps.rcap of the engine (the row length of mt_engine_ref_positions' pos_out) */
 int32_t mt_engine_ref_capacity(const mt_engine* e);

@@ -946,9 +946,15 @@ static Seg* splitAt(mto_client* c, Seg* s, int pos) {
     int len = s->hdr.cachedLength;
     /* PermutationSegment.createSplitSegmentAt (permutationvector.ts:103-114): unallocated stays
      * unallocated */
-    Seg* r = s->kind == MT_SEG_PERM ? newSeg(c, MT_SEG_PERM, NULL, len - pos, 0)
-                                    : newSeg(c, MT_SEG_TEXT, s->text + pos, len - pos, 0);
-    s->hdr.cachedLength = pos;
+    Seg* r;
+    if (s->kind == MT_SEG_PERM) { /* new PermutationSegment(cachedLength - pos); cachedLength = pos */
+        r = newSeg(c, MT_SEG_PERM, NULL, len - pos, 0);
+        s->hdr.cachedLength = pos;
+    } else { /* text.substring(pos) / substring(0, pos): past the end, an empty right part */
+        int cut = pos < len ? pos : len;
+        r = newSeg(c, MT_SEG_TEXT, s->text + cut, len - cut, 0);
+        s->hdr.cachedLength = cut;
+    }
     /* propertyManager.copyTo (segmentPropertiesManager.ts:113-128) */
     if (s->hasProps) {
         r->hasProps = 1;

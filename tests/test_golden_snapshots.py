@@ -183,3 +183,25 @@ def test_legacy_snapshot_loads(name, fmt, kind):
     dump = _replay_arrays(kind, it, log.arrays(), -1)
     v1 = json.load(open(os.path.join(GOLD, name + ".json")))
     assert _contents(sn.emit_from_dump(dump, it, lambda i: "snapshot")) == _contents(v1)
+
+
+@pytest.mark.parametrize("kind", ["oracle", "host", pytest.param("gpu", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("fmt", sorted(LEGACY))
+@pytest.mark.parametrize("name", NAMES)
+def test_legacy_snapshot_emit_roundtrip(name, fmt, kind):
+    """SnapshotLegacy emit (snapshotlegacy.ts:104-242, SharedString's default summary): the legacy
+    fixture loaded into a replica is summarized again in the legacy format, with the fixture's
+    catch-up blob name (options.catchUpBlobName) and its (empty) catch-up messages; every blob is the
+    fixture's byte for byte. The same holds for the document built by the generator script."""
+    tree = json.load(open(os.path.join(LEGACY[fmt], name + ".json")))
+    want = _contents(tree)
+    blob = [p for p in want if p not in (sn.HEADER, sn.BODY)]
+    assert len(blob) == 1
+    it = ol.Interner()
+    log = ol.DocLog(it)
+    sn.load_records(tree, log, lambda n: {"snapshot": 0}[n], "snapshot")
+    dump = _replay_arrays(kind, it, log.arrays(), -1)
+    assert _contents(sn.emit_legacy_from_dump(dump, it, [], catchup_blob=blob[0])) == want
+    d = _script(name)
+    dump = _replay(kind, d, local=-1)
+    assert _contents(sn.emit_legacy_from_dump(dump, d.it, [], catchup_blob=blob[0])) == want

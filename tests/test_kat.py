@@ -61,7 +61,19 @@ def test_interleaved_inserts_annotates_deletes(client):
         assert op is not None
         changes[i] = client.make_op_message(op, i + 1)
     for i in range(100):
+        # the segments of op i's SegmentGroup: op i is local op i + 1 (getLocalSequenceNumber), so they are
+        # the rows with that localSeq (insert) / localRemovedSeq (remove). The ack neither splits nor (MSN
+        # 0) scours, so the rows keep their order across it.
+        _, pre = parse_dump(client.dump())
         assert client.apply_msg(changes[i]) == 0
+        _, post = parse_dump(client.dump())
+        assert len(pre) == len(post)
+        m6 = i % 6
+        for a, b in zip(pre, post):
+            if m6 in (0, 5) and a["flags"] & ol.DF_LRSEQ and a["localRemovedSeq"] == i + 1:
+                assert b["removedSeq"] == i + 1, "removed segment has unexpected id"  # applyMsg.spec.ts:74-76
+            if m6 in (1, 4) and a["flags"] & ol.DF_LSEQ and a["localSeq"] == i + 1:
+                assert b["seq"] == i + 1, "inserted segment has unexpected id"  # applyMsg.spec.ts:78-81
     _, segs = parse_dump(client.dump())
     for s in segs:
         assert s["seq"] != -1 and s["ngroups"] == 0

@@ -48,6 +48,8 @@ def caps_for(w: gen.Workload) -> dict:
     from fluidframework_amd.engine import default_caps
     if w.mode == gen.MTG_MATRIX:
         return default_caps(w.ops_per_doc, config=5)
+    if w.distinct_props and w.ops_per_doc > 50_000:  # config 4 at scale: the tiled profile
+        return default_caps(w.ops_per_doc, config=4)
     if w.distinct_props:  # config-4 shape: coalescing defeated, thousands of rows
         return dict(ncap=4096, hcap=8192, acap=1 << 17, mcap=4096, gcap=1024, ccap=64)
     return default_caps(w.ops_per_doc)

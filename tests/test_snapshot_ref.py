@@ -191,10 +191,11 @@ def test_body_window_set_shape():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", SETS)
+@pytest.mark.parametrize("name", [n for n in SETS if n != "c4_large"])
 def test_gpu_snapshot_emit_and_load_match_reference(name):
     """Both halves on the HIP engine: the prefix replays on the GPU and its dumps are emitted; the
-    loaded replicas (load records + tail) replay on the GPU as one batch."""
+    loaded replicas (load records + tail) replay on the GPU as one batch. (c4_large, two 300k-message
+    documents, runs on the CPU tier only: its load records alone are minutes of one wave's work.)"""
     from fluidframework_amd.engine import Engine
     z, b, it, caps = fixture(name)
     if not has_snapshots(z):

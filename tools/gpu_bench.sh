@@ -4,6 +4,10 @@
 TAG=${1:-bench}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
+# a heartbeat under gpurun_out/ while long steps run (each step has its own time limit)
+( while sleep 60; do date >> "$OUT/heartbeat"; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 export TMPDIR=/tmp
 ARGS=${ARGS:-}
 timeout -k 10 600 python -u bench.py $ARGS > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench rc=$?"; tail -20 "$OUT/bench.err"; exit 1; }

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Analysis build of one config-3 replay kernel variant alone (VARIANT=w7|w6|w8|lds): resource usage (register and
+# Analysis build of one config-3 replay kernel variant alone (VARIANT=w8|lds|dl): resource usage (register and
 # spill counts) and the gfx950 assembly, in a minute instead of the full library's several.
 # usage: tools/isa_small.sh OUTDIR [extra hipcc flags]
 set -e
-SRC=$(cd "$(dirname "$0")/.." && pwd)/fluidframework_amd/csrc/mt_small_${VARIANT:-w7}.hip
+SRC=$(cd "$(dirname "$0")/.." && pwd)/fluidframework_amd/csrc/mt_small_${VARIANT:-w8}.hip
 OUT=${1:-/tmp/isa}; shift || true
 mkdir -p "$OUT"
 cd "$OUT"

@@ -49,7 +49,10 @@ SETS = {
     "c3_lagged_long": (gen.config3(4096), list(range(1000, 1032))),         # the bench's doc length
     "c4_scaled": (gen.config4(20000), list(range(4))),                      # coalescing defeated, MSN advancing
     "c5_perm": (gen.config5(1500), list(range(64))),                        # PermutationSegment rows
+    "c2_full": (gen.config2(10_000), list(range(16))),                      # config 2 at its full 10k msgs
+    "c4_large": (gen.config4(300_000), [0, 1]),                             # >100k live rows: the tiled profile
 }
+KEEP = {"c4_large": 0, "c2_full": 1}  # stored full logs per set (default KEEP_LOGS): fixtures stay small
 
 
 def write_batch(b: ol.Batch, interner: ol.Interner, d: str) -> None:
@@ -288,10 +291,13 @@ def run_refs(rb, d: str, node: str):
     off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
     digests = np.asarray([fnv1a64(blob[off[i]: off[i + 1]].tobytes()) for i in range(rb.ndocs)], np.uint64)
     ins = json.load(open(os.path.join(d, "ref_refinside.json")))
+    pe = json.load(open(os.path.join(d, "ref_refpastend.json")))
     inside = np.zeros(pos.shape, bool)
+    past = np.zeros(pos.shape, bool)
     for i in range(rb.ndocs):
         inside[i, : nref[i]] = ins.get(str(i), [])
-    return nref, pos, digests, inside
+        past[i, : nref[i]] = pe.get(str(i), [])
+    return nref, pos, digests, inside, past
 
 
 def make_refs(names, node: str) -> None:
@@ -309,28 +315,30 @@ def make_refs(names, node: str) -> None:
         b = gen.generate(w, ids=ids, threads=8)
         c = caps_for(w)
         rb = refs_inject.inject(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
-        _, pos1, _, inside = run_refs(rb, os.path.join(SCRATCH, name + "_refs"), node)
+        _, pos1, _, inside, past = run_refs(rb, os.path.join(SCRATCH, name + "_refs"), node)
         targets = np.full((rb.ndocs, 4), -1, np.int32)
         for i in range(rb.ndocs):
-            # attached references whose offset lies inside their segment: past the end, the reference's
-            # splitAt makes a zero-length segment, which the engine does not model
+            # attached references an insert can target: inside their segment, or past the end of a text
+            # segment (the reference's splitAt makes an empty segment there, which the engine models); past
+            # the end of a PermutationSegment or a Marker the reference corrupts or throws
             att = np.nonzero((pos1[i] >= 0) & inside[i])[0]
             if len(att):
                 pick = np.random.default_rng(777 + i).choice(att, size=min(4, len(att)), replace=False)
                 targets[i, : len(pick)] = pick
         rb2 = refs_inject.add_atref_inserts(rb, [t[t >= 0] for t in targets])
-        nref, pos, digests, _ = run_refs(rb2, os.path.join(SCRATCH, name + "_refs2"), node)
+        nref, pos, digests, _, _ = run_refs(rb2, os.path.join(SCRATCH, name + "_refs2"), node)
+        npast = int(sum(past[i, t[t >= 0]].sum() for i, t in enumerate(targets)))
         np.savez_compressed(
             os.path.join(GOLDEN, f"refrefs_{name}.npz"),
             workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(rb2),
-            nref=nref, positions=pos, digests=digests, atref_targets=targets,
+            nref=nref, positions=pos, digests=digests, atref_targets=targets, atref_past_end=npast,
             source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
                     "tools/ref_replay.mjs: LocalReference + Client.addLocalReference, "
                     "insertAtReferencePositionLocal, toPosition() at the end"),
         )
         print(f"refrefs_{name}: {rb2.ndocs} docs, {int(nref.sum())} references: {int((pos >= 0).sum())} attached, "
               f"{int((pos == -2).sum())} the reference could not add; {int((targets >= 0).sum())} inserts at "
-              "references", flush=True)
+              f"references, {npast} of them past their segment's end", flush=True)
 
 
 REGEN_SETS = ("c1_farm", "c3_lagged", "c3_lagged_long", "c5_perm")
@@ -419,7 +427,7 @@ def main() -> None:
         agree = int((odig == digests).sum())
         print(f"{name}: {b.ndocs} docs, {b.nops} events, reference {info['seconds']:.2f}s; "
               f"oracle agrees on {agree}/{b.ndocs} digests", flush=True)
-        keep = b.subset(range(min(KEEP_LOGS, b.ndocs)))
+        keep = b.subset(range(min(KEEP.get(name, KEEP_LOGS), b.ndocs)))
         np.savez_compressed(
             os.path.join(GOLDEN, f"ref_{name}.npz"),
             workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(b),

@@ -222,6 +222,7 @@ const regenWords = [];
 const threwRefs = new Set(); // references whose addLocalReference threw
 const refPositions = {};
 const refInside = {};
+const refPastEnd = {};
 
 function replayDoc(doc, to = opOff[doc + 1], deltas = false) {
     const client = new Client(specToSegment, logger);
@@ -352,9 +353,14 @@ for (let d = 0; d < ndocs; d++) {
         // LocalReference.toPosition (localReference.ts:62-68) of every reference, -1 when detached
         if (curRefs.length) {
             refPositions[d] = curRefs.map((r) => (threwRefs.has(r) ? -2 : r ? r.toPosition() : -1));
-            // an offset inside its segment (an append can leave one past the end: refsByOffset.length is not
-            // the segment's length, localReference.ts:211-223; inserting there splits off an empty segment)
-            refInside[d] = curRefs.map((r) => !!(r && r.segment && r.offset < r.segment.cachedLength));
+            // a reference an insert can target: an offset inside its segment, or past the end of a text
+            // segment (an append can leave one there: refsByOffset.length is not the segment's length,
+            // localReference.ts:211-223; inserting there splits off an empty segment). Past the end of a
+            // PermutationSegment the split makes a negative length, and a Marker does not split (the
+            // insert throws, mergeTree.ts:2082-2083).
+            refInside[d] = curRefs.map((r) => !!(r && r.segment && (r.offset < r.segment.cachedLength ||
+                TextSegment.is(r.segment))));
+            refPastEnd[d] = curRefs.map((r) => !!(r && r.segment && r.offset >= r.segment.cachedLength));
         }
         for (const [qd, pos, ref, cl] of queries) {
             if (qd !== d) continue;
@@ -428,6 +434,7 @@ if (regenWords.some((x) => x)) {
 if (Object.keys(refPositions).length) {
     fs.writeFileSync(path.join(dir, "ref_refpos.json"), JSON.stringify(refPositions));
     fs.writeFileSync(path.join(dir, "ref_refinside.json"), JSON.stringify(refInside));
+    fs.writeFileSync(path.join(dir, "ref_refpastend.json"), JSON.stringify(refPastEnd));
 }
 fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
 if (queries.length) fs.writeFileSync(path.join(dir, "ref_answers.json"), JSON.stringify(answers));
