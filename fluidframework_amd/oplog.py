@@ -110,6 +110,46 @@ def concat_records(a, b):
             np.concatenate([akv, bkv]))
 
 
+DELTA_END = -0x80000000  # MT_DELTA_END (include/mt_oplog.h)
+
+
+def decode_deltas(words):
+    """A document's delta-stream words (include/mt_oplog.h MT_DELTA_*) -> [(op, seq, segments)], a segment
+    being (pos, len, nd or word) and for ANNOTATE events its property deltas [(key id, value id)] or None
+    (addProperties was blocked by a pending local rewrite). Raises on a truncated stream."""
+    w = [int(x) for x in words]
+    n, i, out = len(w), 0, []
+
+    def need(k):
+        if i + k > n:
+            raise ValueError(f"truncated delta stream at word {i} of {n}")
+
+    while i < n:
+        need(2)
+        op, seq = w[i], w[i + 1]
+        i += 2
+        segs = []
+        while True:
+            need(1)
+            if w[i] == DELTA_END:
+                break
+            need(3)
+            pos, ln, nd = w[i], w[i + 1], w[i + 2]
+            i += 3
+            pd = None
+            if op == 2 and nd >= 0:
+                need(nd)
+                pd = [((x & 0xFFFFFFFF) >> 16, x & 0xFFFF) for x in w[i: i + nd]]
+                i += nd
+            segs.append((pos, ln, nd, pd))
+        need(2)
+        if w[i + 1] != len(segs):
+            raise ValueError(f"malformed delta stream at word {i}")
+        i += 2
+        out.append((op, seq, segs))
+    return out
+
+
 # canonical-dump segment flag bits (include/mt_oplog.h MT_DF_*)
 DF_HAS_PROPS, DF_REMOVED, DF_LSEQ, DF_LRSEQ = 1, 2, 4, 8
 

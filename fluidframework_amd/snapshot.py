@@ -203,6 +203,94 @@ def emit_legacy(hdr, segs, interner: ol.Interner, catchup: Optional[List[dict]] 
     return {"entries": entries, "id": None}
 
 
+def _insert_spec(op: Dict[str, Any]):
+    """TextSegment / Marker .toJSONObject() of the segment an insert op made, as a delta callback sees it:
+    its properties are the op's with the null-valued keys deleted (addProperties, segmentPropertiesManager.ts
+    100-106), present (possibly empty) whenever the op carried props."""
+    seg = op["seg"]
+    if isinstance(seg, dict) and "props" in seg:
+        seg = dict(seg, props={k: v for k, v in seg["props"].items() if v is not None})
+    return seg
+
+
+def _same_props(a, b) -> bool:
+    """matchProperties (properties.ts:61-92) of two JSON property sets (None: undefined)."""
+    if a is None or b is None:
+        return a is None and b is None
+    return a == b
+
+
+def ops_from_deltas(msg: Dict[str, Any], events, interner: ol.Interner) -> List[Dict[str, Any]]:
+    """SharedSegmentSequence.createOpsFromDelta (sequence.ts:62-110) over the sequenceDelta events one
+    message fired (delta words decoded by oplog.decode_deltas), ops accumulating across the events of a
+    group: insert ranges become insert ops of the segment's JSON; remove ranges extend the last op when it
+    starts at the range's position (its pos2 becomes NaN, JSON null, when it has none) or add
+    [pos, pos + length); annotate ranges carry the segment's value (null if absent) of each changed key and
+    extend the last op when it ends at the range and has the same props. A remote annotate that pending local
+    rewrites blocked has no property deltas, and the reference's Object.keys(undefined) throws there."""
+    members = msg["contents"]["ops"] if msg["contents"]["type"] == 3 else [msg["contents"]]
+    inserts = [m for m in members if m["type"] == ol.OP_INSERT]
+    annot = [m for m in members if m["type"] == ol.OP_ANNOTATE]
+    out: List[Dict[str, Any]] = []
+    nan = float("nan")
+    for op, _seq, segs in events:
+        if op == ol.OP_INSERT:
+            ins = inserts.pop(0)
+            for pos, _ln, _nd, _pd in segs:
+                out.append({"pos1": pos, "seg": _insert_spec(ins), "type": ol.OP_INSERT})
+        elif op == ol.OP_REMOVE:
+            for pos, ln, _nd, _pd in segs:
+                last = out[-1] if out else None
+                if last is not None and last.get("pos1") == pos:
+                    p2 = last.get("pos2", nan)
+                    last["pos2"] = nan if p2 is None or p2 != p2 else p2 + ln
+                else:
+                    out.append({"pos1": pos, "pos2": pos + ln, "type": ol.OP_REMOVE})
+        elif op == ol.OP_ANNOTATE:
+            new = annot.pop(0)["props"]
+            for pos, ln, nd, pd in segs:
+                if pd is None:
+                    raise ValueError("createOpsFromDelta: an annotate range without property deltas (its "
+                                     "addProperties was blocked by pending local rewrites); the reference throws")
+                props = {}
+                for k, _v in pd:
+                    key = interner.key_str(k)
+                    props[key] = new.get(key)  # the key's value after the op: written from the op, or deleted
+                last = out[-1] if out else None
+                if last is not None and last.get("pos2") == pos and _same_props(last.get("props"), props):
+                    last["pos2"] += ln
+                else:
+                    out.append({"pos1": pos, "pos2": pos + ln, "props": props, "type": ol.OP_ANNOTATE})
+    for o in out:  # JSON.stringify(NaN) is null
+        if "pos2" in o and o["pos2"] is not None and o["pos2"] != o["pos2"]:
+            o["pos2"] = None
+    return out
+
+
+def catchup_messages(ops, text, props, kv, deltas, interner: ol.Interner, long_name, min_seq: int):
+    """SharedString's messagesSinceMSNChange when it summarizes (sequence.ts:566-616): every sequenced op
+    message the replica applied, those with referenceSequenceNumber != sequenceNumber - 1 rebased
+    (refSeq = seq - 1, contents = createOpsFromDelta of the sequenceDelta events the message fired; one op,
+    else a group of them: an ack fires none), then those above the MSN, with the MSN as their
+    minimumSequenceNumber. `ops/text/props/kv`: the replica's records so far; `deltas`: its delta-stream
+    words over the same records (an engine created with caps.dcap > 0)."""
+    from . import wire
+    by_seq: Dict[int, list] = {}
+    for ev in ol.decode_deltas(deltas):
+        if ev[0] in (ol.OP_INSERT, ol.OP_REMOVE, ol.OP_ANNOTATE) and ev[1] >= 0:
+            by_seq.setdefault(ev[1], []).append(ev)
+    stash = []
+    for msg, _last in wire.record_messages(ops, text, props, kv, interner, long_name):
+        if msg["type"] != wire.MSG_OP:
+            continue
+        if msg["referenceSequenceNumber"] != msg["sequenceNumber"] - 1:
+            got = ops_from_deltas(msg, by_seq.get(msg["sequenceNumber"], []), interner)
+            msg = dict(msg, referenceSequenceNumber=msg["sequenceNumber"] - 1,
+                       contents=got[0] if len(got) == 1 else {"ops": got, "type": 3})
+        stash.append(msg)
+    return [dict(m, minimumSequenceNumber=min_seq) for m in stash if m["sequenceNumber"] > min_seq]
+
+
 def emit_legacy_from_dump(dump: bytes, interner: ol.Interner, catchup: Optional[List[dict]] = None,
                           chunk_size: int = CHUNK_SIZE, catchup_blob: str = CATCHUP) -> dict:
     """emit_legacy over an engine / oracle canonical dump (bytes)."""

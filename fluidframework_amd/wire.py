@@ -63,6 +63,9 @@ def add_message(log: ol.DocLog, msg: Dict[str, Any], client_index: Callable[[str
     if isinstance(op, str):
         op = json.loads(op)
     members = op["ops"] if op["type"] == 3 else [op]  # MergeTreeDeltaType.GROUP (ops.ts:33)
+    if not members:  # an empty group applies nothing; applyMsg still runs updateSeqNumbers
+        log.add(ol.OP_NOOP, **common)
+        return
     for i, m in enumerate(members):
         _op_record(log, m["type"] | (ol.OPF_GROUPED if i + 1 < len(members) else 0), m, common)
 
@@ -71,6 +74,73 @@ def add_messages(log: ol.DocLog, msgs: Iterable[Union[Dict[str, Any], str]],
                  client_index: Callable[[str], int]) -> None:
     for m in msgs:
         add_message(log, json.loads(m) if isinstance(m, str) else m, client_index)
+
+
+UNALLOCATED = -0x80000000  # Handle.unallocated (matrix handletable.ts:11)
+
+
+def _props_of(props, kv, pidx: int, interner: ol.Interner):
+    """(property set with JSON nulls, combining op) of a record's props index (0: none)."""
+    if not pidx:
+        return None, None
+    pr = props[pidx - 1]
+    ps = {}
+    for j in range(int(pr["nkv"])):
+        e = kv[int(pr["kv_off"]) + j]
+        v = int(e["value"])
+        ps[interner.key_str(int(e["key"]))] = None if v == 0 else interner.value_obj(v)
+    return ps, ({"name": "rewrite"} if int(pr["combining"]) == ol.COMBINE_REWRITE else None)
+
+
+def record_op(rec, text, props, kv, interner: ol.Interner) -> Dict[str, Any]:
+    """The IMergeTreeOp (ops.ts:63-102) a (non-load) record stands for: the inverse of _op_record."""
+    kind = int(rec["kind"]) & 7
+    ps, comb = _props_of(props, kv, int(rec["props"]), interner)
+    if kind == ol.OP_INSERT:
+        if int(rec["seg_kind"]) == ol.SEG_PERM:
+            seg = [int(rec["text_len"]), UNALLOCATED]
+        elif int(rec["seg_kind"]) == ol.SEG_MARKER:
+            seg = {"marker": {"refType": int(rec["pos2"])}}
+            if ps is not None:
+                seg["props"] = ps
+        else:
+            t = text[int(rec["text_off"]): int(rec["text_off"]) + int(rec["text_len"])].tobytes().decode("utf-16-le")
+            seg = {"text": t, "props": ps} if ps is not None else t
+        return {"pos1": int(rec["pos1"]), "seg": seg, "type": ol.OP_INSERT}
+    if kind == ol.OP_REMOVE:
+        return {"pos1": int(rec["pos1"]), "pos2": int(rec["pos2"]), "type": ol.OP_REMOVE}
+    if kind == ol.OP_ANNOTATE:
+        op = {"pos1": int(rec["pos1"]), "pos2": int(rec["pos2"]), "props": ps if ps is not None else {},
+              "type": ol.OP_ANNOTATE}
+        if comb is not None:
+            op["combiningOp"] = comb
+        return op
+    raise ValueError(f"record kind {kind} is not a merge-tree op")
+
+
+def record_messages(ops, text, props, kv, interner: ol.Interner, long_name: Callable[[int], str]):
+    """The sequenced messages (ISequencedDocumentMessage, protocol.ts:132-172) of a record stream, in
+    order: one per non-local record, a group's members combined into a GROUP op (createGroupOp,
+    opBuilder.ts:128-134). Returns [(message, index of its last record)]."""
+    out, members = [], []
+    for i, rec in enumerate(ops):
+        k = int(rec["kind"])
+        if k & ol.OPF_LOCAL or (k & 7) >= ol.OP_RELOAD:
+            continue
+        if k & ol.OPF_GROUPED:
+            members.append(record_op(rec, text, props, kv, interner))
+            continue
+        msg = {"clientId": long_name(int(rec["client"])), "sequenceNumber": int(rec["seq"]),
+               "referenceSequenceNumber": int(rec["ref_seq"]), "minimumSequenceNumber": int(rec["min_seq"])}
+        if (k & 7) == ol.OP_NOOP:
+            msg["type"] = "noop"
+        else:
+            msg["type"] = MSG_OP
+            op = record_op(rec, text, props, kv, interner)
+            msg["contents"] = {"ops": members + [op], "type": 3} if members else op
+        members = []
+        out.append((msg, i))
+    return out
 
 
 class ClientNames:

@@ -385,6 +385,54 @@ def make_regen(names, node: str) -> None:
         print(f"refregen_{name}: {rb.ndocs} docs, {int(nregen.sum())} regenerated groups", flush=True)
 
 
+LEGACY_SETS = ("c1_farm", "c2_observer", "c3_lagged", "c3_lagged_long", "c4_scaled", "c2_full")
+LEGACY_LOADER = 250  # the long id of the client that loads a legacy summary (a fresh one: catch-up ops are remote)
+
+
+def make_legacy(names, node: str) -> None:
+    """tests/golden/reflegacy_<set>.npz: SharedString's default (legacy) summary of every document after
+    records [0, cut) (cut as for the v1 snapshots): the reference's SnapshotLegacy over its
+    messagesSinceMSNChange (tools/ref_replay.mjs snapshotLegacyDoc), the tree's canonical SHA-256, and the
+    digest of a fresh client (long id LEGACY_LOADER) that loaded it and applied its catch-up messages;
+    documents whose summarizing SharedString throws (createOpsFromDelta on an annotate blocked by pending
+    local rewrites) or whose tree does not load are flagged."""
+    for name in names:
+        w, ids = SETS[name]
+        b = gen.generate(w, ids=ids, threads=8)
+        cuts = [snapshot_cut(b.doc(i)[0], int(b.local_long_id[i])) for i in range(b.ndocs)]
+        d = os.path.join(SCRATCH, name + "_legacy")
+        write_batch(b, gen.generator_interner(), d)
+        with open(os.path.join(d, "snapshots_legacy.json"), "w") as f:
+            json.dump([[i, int(c), LEGACY_LOADER] for i, c in enumerate(cuts)], f)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d], capture_output=True,
+                           text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+        sj = json.load(open(os.path.join(d, "ref_snapshots_legacy.json")))
+        lb = np.fromfile(os.path.join(d, "ref_legacy_loaded_dumps.bin"), np.uint8)
+        lo = np.fromfile(os.path.join(d, "ref_legacy_loaded_off.bin"), "<i8")
+        emit_err = np.zeros(b.ndocs, bool)
+        for k in sj["errors"]:
+            emit_err[int(k)] = True
+        load_err = np.zeros(b.ndocs, bool)
+        for k in sj["loadErrors"]:
+            load_err[int(k)] = True
+        trees = [sj["trees"].get(str(i)) for i in range(b.ndocs)]
+        np.savez_compressed(
+            os.path.join(GOLDEN, f"reflegacy_{name}.npz"),
+            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(b),
+            cut=np.asarray(cuts, np.int64), loader=LEGACY_LOADER,
+            sha256=np.asarray([hashlib.sha256(canonical_tree(t).encode()).hexdigest() if t else "" for t in trees]),
+            loaded_digests=np.asarray([fnv1a64(lb[lo[i]: lo[i + 1]].tobytes()) for i in range(b.ndocs)], np.uint64),
+            emit_error=emit_err, load_error=load_err, keep_trees=json.dumps(trees[:2]),
+            source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                    "tools/ref_replay.mjs: SnapshotLegacy over SharedString's messagesSinceMSNChange, Client.load"),
+        )
+        print(f"reflegacy_{name}: {b.ndocs} docs; summarize throws on {int(emit_err.sum())}, load fails on "
+              f"{int(load_err.sum())}; catch-up messages per doc "
+              f"{[len(json.loads(sn_blobs(t)['catchupOps'])) if t else -1 for t in trees[:8]]}", flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default=",".join(SETS))
@@ -392,8 +440,12 @@ def main() -> None:
     ap.add_argument("--deltas", action="store_true", help="write the delta-stream fixtures (refdelta_*.npz) only")
     ap.add_argument("--refs", action="store_true", help="write the local-reference fixtures (refrefs_*.npz) only")
     ap.add_argument("--regen", action="store_true", help="write the reconnect fixtures (refregen_*.npz) only")
+    ap.add_argument("--legacy", action="store_true", help="write the legacy-summary fixtures (reflegacy_*.npz) only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
+    if args.legacy:
+        make_legacy([n for n in args.sets.split(",") if n in LEGACY_SETS], args.node)
+        return
     if args.regen:
         make_regen([n for n in args.sets.split(",") if n in REGEN_SETS], args.node)
         return

@@ -20,7 +20,7 @@ const timeOnly = process.argv.includes("--time");
 // word format of include/mt_oplog.h (MT_DELTA_*) -> batch-dir/ref_deltas.bin + ref_delta_off.bin
 const withDeltas = process.argv.includes("--deltas");
 const traceDoc = process.argv.includes("--trace-refs") ? Number(process.argv[process.argv.indexOf("--trace-refs") + 1]) : -1;
-let Client, TextSegment, Marker, PermutationSegment, SnapshotV1, LocalReference; // bound in main() (Node 12 has no top-level await)
+let Client, TextSegment, Marker, PermutationSegment, SnapshotV1, SnapshotLegacy, LocalReference; // bound in main() (Node 12 has no top-level await)
 
 const rd = (f) => fs.readFileSync(path.join(dir, f));
 const meta = JSON.parse(rd("meta.json"));
@@ -173,10 +173,25 @@ function applyRange(client, doc, from, to) {
         if (rec.kind & 0x40) { members.push(wireOp(doc, rec)); continue; }
         let contents = kind === 4 ? undefined : wireOp(doc, rec);
         if (members.length) { contents = { type: 3, ops: [...members, contents] }; members = []; } // createGroupOp (opBuilder.ts:128-134)
-        client.applyMsg({
+        const msg = {
             clientId: name(rec.client), sequenceNumber: rec.seq, referenceSequenceNumber: rec.ref_seq,
             minimumSequenceNumber: rec.min_seq, type: kind === 4 ? "noop" : "op", contents,
-        });
+        };
+        // SharedString.processMergeTreeMsg (sequence.ts:579-616) when summaries are legacy: a message whose
+        // refSeq is not seq - 1 is stashed rebased, its contents the ops of the sequenceDelta events it fires
+        const rebase = stash !== null && kind !== 4 && msg.referenceSequenceNumber !== msg.sequenceNumber - 1;
+        if (rebase) rebaseSink = [];
+        client.applyMsg(msg);
+        if (stash !== null && kind !== 4) {
+            let st = msg;
+            if (rebase) {
+                st = JSON.parse(JSON.stringify(msg));
+                st.referenceSequenceNumber = msg.sequenceNumber - 1;
+                st.contents = rebaseSink.length !== 1 ? { ops: rebaseSink, type: 3 } : rebaseSink[0];
+                rebaseSink = null;
+            }
+            stash.push(st);
+        }
         if (kind !== 4 && name(rec.client) === client.longClientId) { // an ack: its groups leave the queue
             pendingOps.splice(0, contents.type === 3 ? contents.ops.length : 1);
         }
@@ -213,6 +228,39 @@ function hookDeltas(client, words) {
     };
 }
 const deltaWords = [];
+// legacy summaries: SharedString's messagesSinceMSNChange of the replica being replayed (null: not kept),
+// and the ops createOpsFromDelta makes of the sequenceDelta events of the message being rebased
+let stash = null;
+let rebaseSink = null;
+// SharedSegmentSequence.createOpsFromDelta (sequence.ts:62-110), restated over one callback's delta
+// segments: ranges in document order at their current position (SequenceDeltaEvent.ranges); insert ranges
+// give insert ops of the segment's JSON; remove ranges extend the last op when it starts at the range's
+// position, else add one; annotate ranges carry each changed key's current value (null if absent) and
+// extend the last op when it ends at the range with the same props
+function opsFromDelta(client, args, out) {
+    const ranges = args.deltaSegments.map((d) => ({ position: client.getPosition(d.segment), segment: d.segment,
+        propertyDeltas: d.propertyDeltas })).sort((a, b) => (a.segment.ordinal < b.segment.ordinal ? -1 : 1));
+    for (const r of ranges) {
+        const last = out[out.length - 1];
+        if (args.operation === 0) {
+            out.push({ pos1: r.position, seg: JSON.parse(JSON.stringify(r.segment.toJSONObject())), type: 0 });
+        } else if (args.operation === 1) {
+            if (last !== undefined && last.pos1 === r.position) last.pos2 += r.segment.cachedLength;
+            else out.push({ pos1: r.position, pos2: r.position + r.segment.cachedLength, type: 1 });
+        } else if (args.operation === 2) {
+            const p = {};
+            for (const k of Object.keys(r.propertyDeltas)) {
+                p[k] = r.segment.properties[k] === undefined ? null : r.segment.properties[k];
+            }
+            if (last !== undefined && last.pos2 === r.position && MT.matchProperties(last.props, p)) {
+                last.pos2 += r.segment.cachedLength;
+            } else {
+                out.push({ pos1: r.position, pos2: r.position + r.segment.cachedLength, props: p, type: 2 });
+            }
+        }
+    }
+}
+let MT;
 let curDoc = -1;
 let curRefs = []; // the local references of the document being replayed, in creation order
 // the replica's pending ops, one entry per pending segment group: {op, group} — what the runtime keeps
@@ -234,10 +282,44 @@ function replayDoc(doc, to = opOff[doc + 1], deltas = false) {
         deltaWords[doc] = words;
         hookDeltas(client, words);
     }
+    if (stash !== null) {
+        client.mergeTreeDeltaCallback = (opArgs, args) => { if (rebaseSink !== null) opsFromDelta(client, args, rebaseSink); };
+    }
     const local = localIds.readInt32LE(4 * doc);
     if (local >= 0) client.startOrUpdateCollaboration(name(local));
     applyRange(client, doc, opOff[doc], to);
     return client;
+}
+
+// ---- legacy summaries (snapshots_legacy.json: [[doc, cut, loadLong], ...]) -------------------------
+// SharedString's default summary: after records [0, cut) Client.snapshot with its messagesSinceMSNChange
+// (sequence.ts:566-577): the messages above the MSN, minimumSequenceNumber set to the MSN; SnapshotLegacy
+// extractSync + emit (snapshotlegacy.ts:104-242). A fresh Client name(loadLong) loads the tree and applies
+// the catch-up messages as SharedString's load does (sequence.ts:501-515); its dump is the "loaded" dump.
+async function snapshotLegacyDoc(doc, cut, loadLong) {
+    stash = [];
+    let a;
+    try {
+        a = replayDoc(doc, opOff[doc] + cut);
+    } finally {
+        rebaseSink = null;
+    }
+    const msgs = stash;
+    stash = null;
+    const minSeq = a.getCollabWindow().minSeq;
+    const catchUp = msgs.filter((m) => m.sequenceNumber > minSeq);
+    catchUp.forEach((m) => { m.minimumSequenceNumber = minSeq; });
+    const snap = new SnapshotLegacy(a.mergeTree, runtimeOf(name(loadLong)).logger);
+    snap.extractSync();
+    const tree = snap.emit(catchUp);
+    const b = new Client(specToSegment, logger);
+    try {
+        const { catchupOpsP } = await b.load(runtimeOf(name(loadLong)), storageOf(tree));
+        for (const m of await catchupOpsP) b.applyMsg(m);
+    } catch (e) {
+        return { tree, loaded: Buffer.alloc(0), loadError: String(e && e.message || e) };
+    }
+    return { tree, loaded: dump(b) };
 }
 
 // ---- snapshots (snapshots.json: [[doc, cut, loadLong], ...]) --------------------------------------
@@ -335,10 +417,11 @@ function dump(client) {
 }
 
 async function main() {
-const MT = await import(path.join(erased, "index.mjs"));
+MT = await import(path.join(erased, "index.mjs"));
 ({ Client, TextSegment, Marker, LocalReference } = MT);
 ({ PermutationSegment } = await import(path.join(erased, "permutationSegment.mjs")));
 ({ SnapshotV1 } = await import(path.join(erased, "snapshotV1.mjs")));
+({ SnapshotLegacy } = await import(path.join(erased, "snapshotlegacy.mjs")));
 const ndocs = opOff.length - 1;
 // optional read queries (queries.json: [[doc, pos, refSeq, longClient | -1 = local view], ...]):
 // getContainingSegment + getPosition (mergeTree.ts:1656-1667, 1619-1636) after the doc's replay
@@ -401,6 +484,28 @@ if (fs.existsSync(spath)) {
     fs.writeFileSync(path.join(dir, "ref_loaded_dumps.bin"), Buffer.concat(loaded));
     fs.writeFileSync(path.join(dir, "ref_loaded_off.bin"), off);
     fs.writeFileSync(path.join(dir, "ref_snapshots.json"), JSON.stringify({ trees, errors: serr, tailErrors, loadErrors }));
+}
+const lpath = path.join(dir, "snapshots_legacy.json");
+if (fs.existsSync(lpath)) {
+    const trees = {}, loaded = [], serr = {}, loadErrors = {};
+    for (const [d, cut, loadLong] of JSON.parse(fs.readFileSync(lpath))) {
+        try {
+            const r = await snapshotLegacyDoc(d, cut, loadLong);
+            trees[d] = r.tree;
+            loaded.push(r.loaded);
+            if (r.loadError) loadErrors[d] = r.loadError;
+        } catch (e) { // the summarizing SharedString itself throws (e.g. createOpsFromDelta)
+            serr[d] = String(e && e.message || e);
+            loaded.push(Buffer.alloc(0));
+        }
+    }
+    const off = Buffer.alloc(8 * (loaded.length + 1));
+    let acc = 0;
+    loaded.forEach((b, i) => { off.writeBigInt64LE(BigInt(acc), 8 * i); acc += b.length; });
+    off.writeBigInt64LE(BigInt(acc), 8 * loaded.length);
+    fs.writeFileSync(path.join(dir, "ref_legacy_loaded_dumps.bin"), Buffer.concat(loaded));
+    fs.writeFileSync(path.join(dir, "ref_legacy_loaded_off.bin"), off);
+    fs.writeFileSync(path.join(dir, "ref_snapshots_legacy.json"), JSON.stringify({ trees, errors: serr, loadErrors }));
 }
 if (!timeOnly) {
     const off = Buffer.alloc(8 * (ndocs + 1));

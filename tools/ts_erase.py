@@ -963,7 +963,8 @@ export const AttachState = { Detached: "Detached", Attaching: "Attaching", Attac
 """,
     "_shim_types": "// type-only packages have no runtime exports\nexport {};\n",
     "_shim_telemetry": """// shim of @fluidframework/telemetry-utils: a logger that records nothing
-const nop = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+// TelemetryLogger.shipAssert reports a failed condition as an error event; it does not throw
+const nop = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {}, shipAssert() {} };
 export const ChildLogger = { create() { return nop; } };
 """,
 }
