@@ -2311,7 +2311,7 @@ struct Replica {
         for (int32_t i = 0; i < z.h.nkeys; i++)
             if (z.keys[i] == key) return i;
         if (z.h.nkeys >= HT::K) {
-            fail(E_UNSUPPORTED);
+            fail(E_CAPACITY); /* the profile's key slots: a larger profile holds more (capacity promotion) */
             return -1;
         }
         z.keys[z.h.nkeys] = key;

@@ -358,6 +358,17 @@ struct ProfOps;
 
 struct mt_engine {
     const ProfOps* ops = nullptr; /* the profile's launchers (one translation unit per profile) */
+    /* capacity promotion (mt_engine_sync): the documents a replay left with E_CAPACITY replay again, from
+     * their staged logs, in an engine of the next profile (`over`); per-document queries route there */
+    bool promote = true;
+    bool ran = false;                 /* a replay was launched since the last sync */
+    mt_engine* over = nullptr;
+    std::vector<int32_t> pro;         /* doc -> index in `over`, -1: not promoted */
+    std::vector<int64_t> pro_docs;    /* index in `over` -> doc */
+    std::vector<int64_t> h_op_off, h_text_off, h_props_off, h_kv_off; /* host copies of the staged offsets */
+    std::vector<int32_t> h_local;     /* start_collab's local long ids */
+    mt_caps caps0 = {};               /* creation capacities */
+    bool borrowed = false;            /* text / props / kv point into the parent's staged pools */
     int device;
     int64_t ndocs;
     int32_t dcap = 0; /* delta event log words per document (0: off) */

@@ -39,6 +39,10 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->fx = caps->dcap > 0 || caps->rcap > 0;
     const char* g = getenv("MT_REPLAY_LDS");
     e->lds = g && g[0] == '1';
+    const char* np = getenv("MT_NO_PROMOTE");
+    e->promote = !(np && np[0] == '1');
+    e->caps0 = *caps;
+    e->pro.assign((size_t)ndocs, -1);
     e->waves = 8; /* occupancy of the HBM-resident small-profile kernel (mt_prof_small.hip) */
     e->profile = prof;
     e->ops = prof == 0 ? ops_small() : prof == 1 ? ops_mid() : prof == 3 ? ops_mat() : prof == 4 ? ops_huge() : ops_big();
@@ -79,8 +83,10 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
 
 void mt_engine_destroy(mt_engine* e) {
     if (!e) return;
+    mt_engine_destroy(e->over);
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->borrowed) e->text.p = e->props.p = e->kv.p = nullptr; /* the parent's */
     DevBuf* bufs[] = {&e->ops_buf, &e->op_off, &e->text, &e->text_off, &e->props,     &e->props_off,
                       &e->kv,     &e->kv_off, &e->tmp,  &e->local_ids, &e->prof};
     for (DevBuf* b : bufs)
@@ -104,6 +110,7 @@ int32_t mt_engine_start_collab(mt_engine* e, const int32_t* local_long_ids, int3
     if (rc) return rc;
     HIPCHK(e, hipMemcpyAsync(e->local_ids.p, local_long_ids, sizeof(int32_t) * e->ndocs, hipMemcpyHostToDevice,
                              e->stream));
+    e->h_local.assign(local_long_ids, local_long_ids + e->ndocs);
     e->min_seq0 = min_seq;
     e->cur_seq0 = cur_seq;
     e->collab = true;
@@ -180,6 +187,10 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
     if (nkv) HIPCHK(e, hipMemcpyAsync(e->kv.p, kv, sizeof(mt_kv) * nkv, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(e->kv_off.p, kv_off, sizeof(int64_t) * nd, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->h_op_off.assign(op_off, op_off + nd + 1);
+    e->h_text_off.assign(text_off, text_off + nd);
+    e->h_props_off.assign(props_off, props_off + nd);
+    e->h_kv_off.assign(kv_off, kv_off + nd);
     e->staged = true;
     return MT_OK;
 }
@@ -187,6 +198,8 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
 int32_t mt_engine_reset(mt_engine* e) {
     if (!e) return MT_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
+    std::fill(e->pro.begin(), e->pro.end(), -1);
+    e->pro_docs.clear();
     return launch_init(e);
 }
 
@@ -200,8 +213,11 @@ int32_t mt_engine_run(mt_engine* e) {
     int32_t rc = e->ops->replay(e);
     if (rc) return rc;
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+    e->ran = true;
     return MT_OK;
 }
+
+static int32_t promote(mt_engine* e);
 
 int32_t mt_engine_sync(mt_engine* e) {
     if (!e) return MT_E_ARG;
@@ -209,6 +225,14 @@ int32_t mt_engine_sync(mt_engine* e) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, e->ev0, e->ev1) == hipSuccess) e->last_ms = ms;
+    if (e->ran) {
+        e->ran = false;
+        if (e->promote) {
+            int32_t rc = promote(e);
+            if (rc) return rc;
+            if (e->over && !e->pro_docs.empty()) e->last_ms += e->over->last_ms;
+        }
+    }
     return MT_OK;
 }
 
@@ -231,17 +255,153 @@ static int32_t read_hdr(mt_engine* e, int32_t* err, int32_t* err_op, int32_t* st
     return MT_OK;
 }
 
+/* ---- capacity promotion ------------------------------------------------------------------------
+ * A document whose replay latched E_CAPACITY (row slots, nodes, heap, key slots, text arena, membership
+ * log, pending groups) replays again from its staged log, from an empty replica, in an engine of the
+ * next profile: small / config-5 -> HotMid (2,048 nodes, 24 key slots) -> HotBig (16,384) -> HotHuge
+ * (262,144, tiled), with four times the arena, membership and pending-group capacities. The promoted
+ * documents' records are gathered on the device; their text / props / kv pools stay the parent's. */
+static int32_t next_ncap(int profile) {
+    switch (profile) {
+    case 0: case 3: return HotMid::N;
+    case 1: return HotBig::N;
+    case 2: return HotHuge::N;
+    default: return -1;
+    }
+}
+extern "C++" {
+template <class T>
+static void scatter(T* dst, const std::vector<T>& src, const std::vector<int64_t>& docs, int k) {
+    for (size_t i = 0; i < docs.size(); i++)
+        for (int j = 0; j < k; j++) dst[docs[i] * k + j] = src[i * k + j];
+}
+}
+static int32_t promote(mt_engine* e) {
+    std::fill(e->pro.begin(), e->pro.end(), -1);
+    e->pro_docs.clear();
+    int32_t nc = next_ncap(e->profile);
+    if (nc < 0) return MT_OK;
+    int64_t nd = e->ndocs;
+    std::vector<int32_t> err((size_t)nd);
+    int32_t rc = read_hdr(e, err.data(), nullptr, nullptr, nullptr);
+    if (rc) return rc;
+    for (int64_t d = 0; d < nd; d++)
+        if (err[(size_t)d] == MT_E_CAPACITY) e->pro_docs.push_back(d);
+    int64_t m = (int64_t)e->pro_docs.size();
+    if (m == 0) return MT_OK;
+    mt_caps c = e->caps0;
+    c.ncap = nc;
+    c.hcap = std::max(c.hcap, 2 * nc);
+    c.acap = (int32_t)std::min<int64_t>(4 * (int64_t)c.acap, 1 << 23);
+    c.mcap = (int32_t)std::min<int64_t>(4 * (int64_t)c.mcap, 1 << 18);
+    c.gcap = (int32_t)std::min<int64_t>(4 * (int64_t)c.gcap, 1 << 16);
+    mt_engine* o = e->over;
+    if (o && (o->ndocs != m || o->caps0.ncap != c.ncap)) {
+        mt_engine_destroy(o);
+        o = e->over = nullptr;
+    }
+    if (!o) {
+        rc = mt_engine_create(e->device, m, &c, &o);
+        if (rc) return rc;
+        e->over = o;
+    }
+    o->promote = e->promote;
+    if (e->collab) {
+        std::vector<int32_t> loc((size_t)m);
+        for (int64_t i = 0; i < m; i++) loc[(size_t)i] = e->h_local[(size_t)e->pro_docs[(size_t)i]];
+        HIPCHK(o, hipSetDevice(o->device));
+        if ((rc = ensure(o, o->local_ids, sizeof(int32_t) * m))) return rc;
+        HIPCHK(o, hipMemcpyAsync(o->local_ids.p, loc.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, o->stream));
+        HIPCHK(o, hipStreamSynchronize(o->stream));
+        o->h_local = loc;
+        o->min_seq0 = e->min_seq0;
+        o->cur_seq0 = e->cur_seq0;
+        o->collab = true;
+    }
+    /* the promoted documents' records, gathered device to device; their pools are the parent's */
+    o->h_op_off.assign((size_t)m + 1, 0);
+    o->h_text_off.resize((size_t)m);
+    o->h_props_off.resize((size_t)m);
+    o->h_kv_off.resize((size_t)m);
+    for (int64_t i = 0; i < m; i++) {
+        int64_t d = e->pro_docs[(size_t)i];
+        o->h_op_off[(size_t)i + 1] = o->h_op_off[(size_t)i] + e->h_op_off[(size_t)d + 1] - e->h_op_off[(size_t)d];
+        o->h_text_off[(size_t)i] = e->h_text_off[(size_t)d];
+        o->h_props_off[(size_t)i] = e->h_props_off[(size_t)d];
+        o->h_kv_off[(size_t)i] = e->h_kv_off[(size_t)d];
+    }
+    if ((rc = ensure(o, o->ops_buf, sizeof(mt_op_rec) * o->h_op_off[(size_t)m]))) return rc;
+    if ((rc = ensure(o, o->op_off, sizeof(int64_t) * (m + 1)))) return rc;
+    if ((rc = ensure(o, o->text_off, sizeof(int64_t) * m))) return rc;
+    if ((rc = ensure(o, o->props_off, sizeof(int64_t) * m))) return rc;
+    if ((rc = ensure(o, o->kv_off, sizeof(int64_t) * m))) return rc;
+    for (int64_t i = 0; i < m; i++) {
+        int64_t d = e->pro_docs[(size_t)i], n = e->h_op_off[(size_t)d + 1] - e->h_op_off[(size_t)d];
+        if (n)
+            HIPCHK(o, hipMemcpyAsync((mt_op_rec*)o->ops_buf.p + o->h_op_off[(size_t)i],
+                                     (const mt_op_rec*)e->ops_buf.p + e->h_op_off[(size_t)d], sizeof(mt_op_rec) * n,
+                                     hipMemcpyDeviceToDevice, o->stream));
+    }
+    HIPCHK(o, hipMemcpyAsync(o->op_off.p, o->h_op_off.data(), sizeof(int64_t) * (m + 1), hipMemcpyHostToDevice, o->stream));
+    HIPCHK(o, hipMemcpyAsync(o->text_off.p, o->h_text_off.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, o->stream));
+    HIPCHK(o, hipMemcpyAsync(o->props_off.p, o->h_props_off.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, o->stream));
+    HIPCHK(o, hipMemcpyAsync(o->kv_off.p, o->h_kv_off.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, o->stream));
+    o->borrowed = true;
+    o->text = e->text;
+    o->props = e->props;
+    o->kv = e->kv;
+    o->staged = true;
+    /* an empty replica (create / reset state), the same local ids; then the replay, promoting further */
+    if ((rc = mt_engine_reset(o))) return rc;
+    if ((rc = mt_engine_run(o))) return rc;
+    if ((rc = mt_engine_sync(o))) return rc;
+    for (int64_t i = 0; i < m; i++) e->pro[(size_t)e->pro_docs[(size_t)i]] = (int32_t)i;
+    return MT_OK;
+}
+/* the engine and index that hold document `doc` (promoted documents live in `over`) */
+static mt_engine* route(mt_engine* e, int64_t* doc) {
+    while (e && e->over && *doc >= 0 && *doc < e->ndocs && e->pro[(size_t)*doc] >= 0) {
+        *doc = e->pro[(size_t)*doc];
+        e = e->over;
+    }
+    return e;
+}
+static bool promoted(const mt_engine* e) { return e->over && !e->pro_docs.empty(); }
+
 int32_t mt_engine_errors(mt_engine* e, int32_t* err, int32_t* err_op) {
     if (!e) return MT_E_ARG;
-    return read_hdr(e, err, err_op, nullptr, nullptr);
+    int32_t rc = read_hdr(e, err, err_op, nullptr, nullptr);
+    if (rc || !promoted(e)) return rc;
+    size_t m = e->pro_docs.size();
+    std::vector<int32_t> a(m), b(m);
+    if ((rc = mt_engine_errors(e->over, a.data(), b.data()))) return rc;
+    if (err) scatter(err, a, e->pro_docs, 1);
+    if (err_op) scatter(err_op, b, e->pro_docs, 1);
+    return MT_OK;
 }
 int32_t mt_engine_stats(mt_engine* e, int32_t* out4) {
     if (!e || !out4) return MT_E_ARG;
-    return read_hdr(e, nullptr, nullptr, out4, nullptr);
+    int32_t rc = read_hdr(e, nullptr, nullptr, out4, nullptr);
+    if (rc || !promoted(e)) return rc;
+    std::vector<int32_t> a(4 * e->pro_docs.size());
+    if ((rc = mt_engine_stats(e->over, a.data()))) return rc;
+    scatter(out4, a, e->pro_docs, 4);
+    return MT_OK;
 }
 int32_t mt_engine_work(mt_engine* e, int64_t* out3) {
     if (!e || !out3) return MT_E_ARG;
-    return read_hdr(e, nullptr, nullptr, nullptr, out3);
+    int32_t rc = read_hdr(e, nullptr, nullptr, nullptr, out3);
+    if (rc || !promoted(e)) return rc;
+    std::vector<int64_t> a(3 * e->pro_docs.size());
+    if ((rc = mt_engine_work(e->over, a.data()))) return rc;
+    scatter(out3, a, e->pro_docs, 3);
+    return MT_OK;
+}
+int64_t mt_engine_promoted(const mt_engine* e, int64_t* docs_out, int64_t cap) {
+    if (!e) return -MT_E_ARG;
+    int64_t m = promoted(e) ? (int64_t)e->pro_docs.size() : 0;
+    for (int64_t i = 0; i < m && i < cap && docs_out; i++) docs_out[i] = e->pro_docs[(size_t)i];
+    return m;
 }
 
 int32_t mt_engine_digests(mt_engine* e, uint64_t* out) {
@@ -253,11 +413,17 @@ int32_t mt_engine_digests(mt_engine* e, uint64_t* out) {
     if (rc) return rc;
     HIPCHK(e, hipMemcpyAsync(out, e->tmp.p, sizeof(uint64_t) * e->ndocs, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (promoted(e)) {
+        std::vector<uint64_t> a(e->pro_docs.size());
+        if ((rc = mt_engine_digests(e->over, a.data()))) return rc;
+        scatter(out, a, e->pro_docs, 1);
+    }
     return MT_OK;
 }
 
 int64_t mt_engine_dump(mt_engine* e, int64_t doc, uint8_t* out, int64_t cap) {
     if (!e || doc < 0 || doc >= e->ndocs || cap < 0) return -MT_E_ARG;
+    e = route(e, &doc);
     if (hipSetDevice(e->device) != hipSuccess) return -MT_E_HIP;
     size_t need = sizeof(int64_t) + (size_t)(out ? cap : 0) + 16;
     if (ensure(e, e->tmp, need)) return -MT_E_HIP;
@@ -277,6 +443,7 @@ int64_t mt_engine_dump(mt_engine* e, int64_t doc, uint8_t* out, int64_t cap) {
 
 int32_t mt_engine_get_length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t* out) {
     if (!e || !out || doc < 0 || doc >= e->ndocs) return MT_E_ARG;
+    e = route(e, &doc);
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc = ensure(e, e->tmp, 16);
     if (rc) return rc;
@@ -290,6 +457,7 @@ int32_t mt_engine_get_length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t
 int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* out,
                            int64_t cap) {
     if (!e || doc < 0 || doc >= e->ndocs || cap < 0) return -MT_E_ARG;
+    e = route(e, &doc);
     if (hipSetDevice(e->device) != hipSuccess) return -MT_E_HIP;
     if (ensure(e, e->tmp, 16 + 2 * (size_t)(out ? cap : 0) + 16)) return -MT_E_HIP;
     int64_t* dn = (int64_t*)e->tmp.p;
@@ -310,6 +478,7 @@ int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t l
 static int32_t seg_query(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,
                          int32_t long_client, int32_t* res7) {
     if (!e || doc < 0 || doc >= e->ndocs) return MT_E_ARG;
+    e = route(e, &doc);
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc = ensure(e, e->tmp, 64);
     if (rc) return rc;
@@ -371,11 +540,20 @@ int32_t mt_engine_delta_state(mt_engine* e, int64_t* n_out, uint64_t* hash_out) 
         if (n_out) n_out[d] = st[d].n;
         if (hash_out) hash_out[d] = st[d].h;
     }
+    if (promoted(e)) {
+        std::vector<int64_t> a(e->pro_docs.size());
+        std::vector<uint64_t> b(e->pro_docs.size());
+        int32_t rc = mt_engine_delta_state(e->over, a.data(), b.data());
+        if (rc) return rc;
+        if (n_out) scatter(n_out, a, e->pro_docs, 1);
+        if (hash_out) scatter(hash_out, b, e->pro_docs, 1);
+    }
     return MT_OK;
 }
 
 int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap) {
     if (!e || e->dcap <= 0 || doc < 0 || doc >= e->ndocs || cap < 0) return -MT_E_ARG;
+    e = route(e, &doc);
     if (hipSetDevice(e->device) != hipSuccess) return -MT_E_HIP;
     int64_t off, stride;
     delta_geometry(e, &off, &stride);
@@ -409,6 +587,13 @@ int32_t mt_engine_ref_positions(mt_engine* e, int32_t* nref_out, int32_t* pos_ou
     if (pos_out)
         HIPCHK(e, hipMemcpyAsync(pos_out, dpos, 4 * (size_t)n * e->rcap, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (promoted(e)) {
+        size_t m = e->pro_docs.size();
+        std::vector<int32_t> a(m), b(m * (size_t)e->rcap);
+        if ((rc = mt_engine_ref_positions(e->over, a.data(), b.data()))) return rc;
+        if (nref_out) scatter(nref_out, a, e->pro_docs, 1);
+        if (pos_out) scatter(pos_out, b, e->pro_docs, e->rcap);
+    }
     return MT_OK;
 }
 

@@ -55,6 +55,8 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_reset.argtypes = [vp]
         L.mt_engine_work.argtypes = [vp, vp]
         L.mt_engine_sync.argtypes = [vp]
+        L.mt_engine_promoted.argtypes = [vp, vp, i64]
+        L.mt_engine_promoted.restype = i64
         L.mt_engine_last_run_ms.argtypes = [vp]
         L.mt_engine_last_run_ms.restype = ctypes.c_float
         L.mt_engine_stream.argtypes = [vp]
@@ -219,6 +221,13 @@ class Engine:
         self._check(self.L.mt_engine_get_position(self.h, doc, seg.rid, seg.gen, ref_seq, long_client, ctypes.byref(v)),
                     "get_position")
         return v.value
+
+    def promoted(self) -> np.ndarray:
+        """The documents the last sync re-replayed in a larger profile (capacity promotion)."""
+        n = self.L.mt_engine_promoted(self.h, None, 0)
+        out = np.zeros(max(n, 1), np.int64)
+        self.L.mt_engine_promoted(self.h, _p(out), n)
+        return out[:n]
 
     def delta_state(self):
         """Per doc (words emitted since create/reset, FNV-1a-64 of them) of the delta stream."""

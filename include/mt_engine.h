@@ -41,8 +41,8 @@ enum {
     MT_E_INSERT_FAILED = 1, /* per doc: mergeTree.ts:2243-2249 "MergeTree insert failed"       */
     MT_E_ASSERT = 2,        /* per doc: a reference `assert` would have thrown                 */
     MT_E_INVALID_RANGE = 3, /* reserved (a local op getValidOpRange rejects is a no-op, client.ts:486) */
-    MT_E_UNSUPPORTED = 4,   /* per doc: >8 property keys or >8 overlapping removers            */
-    MT_E_CAPACITY = 5,      /* per doc: a capacity in mt_caps was exceeded                     */
+    MT_E_UNSUPPORTED = 4,   /* per doc: a path the engine does not model (mt_oplog.h)          */
+    MT_E_CAPACITY = 5,      /* per doc: a capacity was exceeded even after promotion (mt_engine_sync) */
     MT_E_ARG = 16,          /* engine: bad argument                                            */
     MT_E_HIP = 17,          /* engine: HIP runtime error (mt_engine_last_error has the text)  */
     MT_E_NOMEM = 18,        /* engine: device allocation failed                                */
@@ -69,7 +69,14 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
  * insertSegmentLocal / removeRangeLocal / annotateRangeLocal for local edits (202/189/164).
  * Asynchronous on the engine's HIP stream; mt_engine_sync waits. */
 int32_t mt_engine_run(mt_engine* e);
+/* Wait for the replay. Capacity promotion (on unless MT_NO_PROMOTE=1): documents whose replay latched
+ * MT_E_CAPACITY (nodes / row slots, heap, property key slots, text arena, membership log, pending
+ * groups) replay again from their staged logs in an engine of the next profile (small -> 2,048 nodes and
+ * 24 key slots -> 16,384 -> 262,144 tiled, 4x the arena, membership and pending-group capacities), as
+ * often as needed; every per-document call below then answers for them from there. */
 int32_t mt_engine_sync(mt_engine* e);
+/* The documents the last mt_engine_sync promoted (writes up to cap ids); returns their count. */
+int64_t mt_engine_promoted(const mt_engine* e, int64_t* docs_out, int64_t cap);
 /* Device time of the last mt_engine_run's replay kernel (HIP events on the engine stream). */
 float mt_engine_last_run_ms(const mt_engine* e);
 /* The engine's hipStream_t (as void*), for callers that time or order work around it. */

@@ -104,3 +104,49 @@ def test_caps_on_gpu():
         assert e.dump(0) == want[d]
         e.close()
     eng.close()
+
+
+@pytest.mark.gpu
+def test_capacity_promotion_mixed_batch():
+    """One engine of the small profile (192 nodes / 1,536 row slots, 8 property key slots) over a mixed
+    batch: config-3 documents that fit, one with 20 property keys and two coalescing-defeated documents
+    with thousands of rows. The ones that overflow latch E_CAPACITY, mt_engine_sync replays them again in
+    the next profiles, and every document's digest and dump equal the oracle's."""
+    from fluidframework_amd import gen
+    from fluidframework_amd.engine import Engine, default_caps
+    small = gen.generate(gen.config3(512), 12)
+    big = gen.generate(gen.config4(12000), 2)  # ~5k rows each
+    docs = [small.doc_arrays(d) for d in range(small.ndocs)]
+    local = [int(x) for x in small.local_long_id]
+    kl = keys_log()
+    docs.insert(5, kl.arrays())
+    local.insert(5, kl.local_long_id)
+    for d in range(big.ndocs):
+        docs.append(big.doc_arrays(d))
+        local.append(int(big.local_long_id[d]))
+    batch = ol.Batch.from_arrays(docs, np.asarray(local, np.int32))
+    want = []
+    for d, arrays in enumerate(docs):
+        c = oc.OracleClient()
+        c.start_collab(local[d])
+        assert c.replay_arrays(*arrays) == 0
+        want.append(c)
+    eng = Engine(batch.ndocs, **default_caps(512))
+    eng.start_collab(batch.local_long_id)
+    eng.replay(batch)
+    err, err_op = eng.errors()
+    assert (err == 0).all(), (err, err_op)
+    promoted = set(eng.promoted().tolist())
+    assert {5, batch.ndocs - 2, batch.ndocs - 1} <= promoted  # 20 keys; > 1,536 rows
+    assert len(promoted) < batch.ndocs // 2
+    dig = eng.digests()
+    for d in range(batch.ndocs):
+        assert dig[d] == want[d].digest(), f"doc {d}"
+        assert eng.dump(d) == want[d].dump(), f"doc {d}"
+    assert eng.get_text(batch.ndocs - 1) == want[-1].get_text()
+    # a second replay of the same staged batch promotes the same documents again
+    eng.reset()
+    eng.run()
+    eng.sync()
+    assert set(eng.promoted().tolist()) == promoted
+    assert (eng.digests() == dig).all()

@@ -32,8 +32,13 @@ def main():
     line = json.loads(open(os.path.join(out, "bench.json")).read().strip().splitlines()[-1])
     alg = line["roofline"]["alg_bytes_per_launch"]
     line["roofline"]["traffic"] = traffic
+    raw = int(fetch_kb * 1024 + write_kb * 1024)
     t = dict(kernel="k_replay", FETCH_SIZE_kb=fetch_kb, WRITE_SIZE_kb=write_kb, dispatches=[nf, nw],
              traffic_bytes_per_launch=traffic, alg_bytes_per_launch=alg, traffic_over_alg=traffic / alg,
+             traffic_raw_bytes_per_launch=raw, traffic_raw_over_alg=raw / alg,
+             correction_note="the x2 FETCH_SIZE correction is calibrated for 16 B/lane streaming reads only; with "
+                             "this kernel's mix of 16-byte and narrower accesses the read bytes lie between the raw "
+                             "(x1) and the corrected (x2) figure",
              traffic_GBps=traffic / (line["roofline"]["kernel_ms"] * 1e6),
              config=line["config"],
              note="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate runs of bench.py --steps 1 "
