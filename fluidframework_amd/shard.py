@@ -47,6 +47,19 @@ def assign(costs: Sequence[float], world: int) -> List[np.ndarray]:
     return [np.asarray(sorted(x), dtype=np.int64) for x in out]
 
 
+def doc_costs(batch) -> np.ndarray:
+    """Replay cost of each document of an op-log batch (oplog.Batch): events x rows. A flat-profile
+    event scans the document's rows (BASELINE.md A(op) = 16 B x R + ...), and the rows a log can
+    create are bounded by 1 + its insert records (a split adds one row per insert, zamboni only
+    merges), so events x (1 + inserts) is the bound the bin-packing balances. Known before any
+    replay, from the log alone, so every rank computes the same assignment."""
+    kinds = batch.ops["kind"] & 0x07
+    doc_of = np.repeat(np.arange(batch.ndocs), np.diff(batch.op_off))
+    events = np.diff(batch.op_off).astype(np.float64)
+    inserts = np.bincount(doc_of[kinds == 0], minlength=batch.ndocs).astype(np.float64)
+    return events * (1.0 + inserts)
+
+
 def loads(costs: Sequence[float], parts: Sequence[np.ndarray]) -> np.ndarray:
     c = np.asarray(costs, dtype=np.float64)
     return np.asarray([c[p].sum() for p in parts])

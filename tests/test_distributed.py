@@ -5,9 +5,11 @@
   the ranks by cost bin-packing (shard.assign), each rank replays only its shard, and the digests
   are all-gathered (shard.gather_digests, ranks holding different counts) and put back in document
   order (shard.in_doc_order).
-Either way the gathered digests must equal a single-process replay of all documents. The replay
-here is the CPU oracle (no GPU in this tier); bench.py runs the same shard/gather code over RCCL
-with the HIP engine."""
+Either way the gathered digests must equal a single-process replay of all documents. The ranks
+replay with the engine's own core (the serial host build of csrc/mt_core.h, libmtcore_host.so: the
+same Replica code the HIP kernels run, no GPU in this tier); the single-process reference they are
+compared with is the CPU oracle. bench.py runs the same shard/gather code over RCCL with the HIP
+engine."""
 import os
 import socket
 
@@ -50,13 +52,21 @@ def _init(rank, world, port):
     return dist
 
 
-def _weak_worker(rank, world, port, out):
+def _engine_replay(b):
+    """(seconds, digests, errors) of a batch replayed by the engine core's host build"""
     import sys
+    import time
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    import oracle_client as oc
+    import core_host
+    t0 = time.perf_counter()
+    dig, err, _ = core_host.replay_batch(b)
+    return time.perf_counter() - t0, dig, err
+
+
+def _weak_worker(rank, world, port, out):
     dist = _init(rank, world, port)
     b = gen.generate(gen.config3(OPS), ids=shard.weak_ids(rank, DOCS_PER_RANK), threads=2)
-    secs, dig, err = oc.replay_batch(b, threads=2)
+    secs, dig, err = _engine_replay(b)
     assert (err == 0).all()
     allg = shard.gather_digests(dig, dist)
     tmax = shard.max_over_ranks(secs, dist)
@@ -70,15 +80,11 @@ def _weak_worker(rank, world, port, out):
 
 
 def _strong_worker(rank, world, port, out):
-    import sys
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    import oracle_client as oc
     dist = _init(rank, world, port)
     full = _unequal_batch()
-    costs = np.diff(full.op_off)
-    parts = shard.assign(costs, world)
+    parts = shard.assign(shard.doc_costs(full), world)
     mine = full.subset(parts[rank])
-    _, dig, err = oc.replay_batch(mine, threads=2)
+    _, dig, err = _engine_replay(mine)
     assert (err == 0).all()
     allg = shard.in_doc_order(shard.gather_digests(dig, dist), parts, full.ndocs)
     if rank == 0:
@@ -129,3 +135,16 @@ def test_assign_balances_and_covers():
     # equal costs: an even split
     parts = shard.assign(np.ones(65536), 8)
     assert all(len(p) == 8192 for p in parts)
+
+
+def test_doc_costs_track_events_times_rows():
+    b = _unequal_batch()
+    c = shard.doc_costs(b)
+    ev = np.diff(b.op_off)
+    kinds = b.ops["kind"] & 7
+    for d in (0, 5, STRONG_DOCS - 1):
+        k = kinds[b.op_off[d]:b.op_off[d + 1]]
+        assert c[d] == ev[d] * (1 + (k == 0).sum())
+    parts = shard.assign(c, 2)
+    ld = shard.loads(c, parts)
+    assert ld.max() <= 4 / 3 * max(c.sum() / 2, c.max()) + 1e-9
