@@ -393,6 +393,7 @@ struct Replica {
     int32_t* wvs;
     uint8_t* wlx;
     int64_t cur; /* index of the record being applied in the current Pools (snapshot reload reads ahead) */
+    int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
         : d(doc), z(*doc.t), w(wave), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
@@ -776,15 +777,16 @@ struct Replica {
      * (mergeTree.ts:2033-2130): split the reference's segment at its offset unless the offset or the
      * segment's local length is 0, walk left over zero-length rows (leftExcursion, 2313-2344) taking
      * every one breakTie(0, 0, ...) accepts, and insert the new local segment right before that row. */
-    MT_HD void insert_at_ref(const mt_op_rec& op, const Pools& p) {
+    /* true if the insert happens: at leaf coordinate *atT (the caller's insert_segments) */
+    MT_HD bool insert_at_ref(const mt_op_rec& op, int32_t* atT) {
         if (op.pos1 < 0 || op.pos1 >= d.dstate()->nref) {
             fail(E_ASSERT);
-            return;
+            return false;
         }
         LRef r = d.refs()[op.pos1];
-        if (r.rid < 0 || seg_len(op) <= 0) return; /* DetachedPosition / a zero-length segment: no-op */
+        if (r.rid < 0 || seg_len(op) <= 0) return false; /* DetachedPosition / a zero-length segment: no-op */
         int32_t s = slot_of(r.rid, -1);
-        if (s < 0) return;
+        if (s < 0) return false;
         int32_t rs0 = z.rseq(s);
         int32_t off = (rs0 != NOREM && rs0 != 0) ? 0 : r.off; /* getOffset() */
         if (off != 0 && local_len(s) != 0) {
@@ -795,10 +797,10 @@ struct Replica {
              * assert(splitSeg.next) throws (mergeTree.ts:2082-2083): neither is modelled. */
             if (off >= z.len(s) && (z.flags(s) & RF_NOTEXT)) {
                 fail(E_UNSUPPORTED);
-                return;
+                return false;
             }
             int32_t rs = -1;
-            if (split_row(kpos(s / MAXN) * MAXN + (s & (MAXN - 1)), off, &rs) < 0 || rs < 0) return;
+            if (split_row(kpos(s / MAXN) * MAXN + (s & (MAXN - 1)), off, &rs) < 0 || rs < 0) return false;
             s = rs;
         }
         int32_t st = s, k = kpos(s / MAXN), j = s & (MAXN - 1);
@@ -814,8 +816,8 @@ struct Replica {
             if (local_len(q) != 0) break;
             if (break_tie(q, h.currentSeq, h.localShort)) st = q;
         }
-        insert_segments(op, p, h.currentSeq, h.localShort, UNASSIGNED_SEQ, 0, 0,
-                        kpos(st / MAXN) * MAXN + (st & (MAXN - 1)));
+        *atT = kpos(st / MAXN) * MAXN + (st & (MAXN - 1));
+        return true;
     }
     /* LocalReference.toPosition (localReference.ts:62-68): getPosition(segment) + getOffset() (0 on a
      * removed segment: `removedSeq` truthy), -1 when detached */
@@ -2871,13 +2873,32 @@ struct Replica {
             }
         }
     }
+    /* A zamboniSegments call the record makes (at the end of insertSegments / markRangeRemoved /
+     * annotateRange / ackPendingSegment, and in setMinSeq): queued and run when the record is done
+     * (run_zamboni), under the minSeq of the call. Nothing a record does after such a call reads what zamboni
+     * changes, so the order of effects is the reference's; and zamboni is inlined once, not at every caller
+     * (the replay kernel's code is several hundred KB: instruction-cache pressure). */
+    MT_HD void zamboni_soon() {
+        if (zq == 0) zms = h.minSeq;
+        zq++;
+    }
+    MT_HD void run_zamboni() {
+#pragma clang loop unroll(disable)
+        for (int32_t i = 0; i < zq; i++) { /* at most 2: the op's or the ack's, then setMinSeq's */
+            int32_t ms = h.minSeq;
+            if (i == 0) h.minSeq = zms;
+            zamboni();
+            h.minSeq = ms;
+        }
+        zq = 0;
+    }
     /* setMinSeq (mergeTree.ts:1751-1769) */
     MT_HD void set_min_seq(int32_t minSeq) {
         if (!(minSeq <= h.currentSeq)) fail(E_ASSERT);
         if (!(h.minSeq <= minSeq)) fail(E_ASSERT);
         if (minSeq > h.minSeq) {
             h.minSeq = minSeq;
-            zamboni();
+            zamboni_soon();
         }
     }
 
@@ -3062,7 +3083,7 @@ struct Replica {
                 dtail(1);
             }
         }
-        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
+        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni_soon();
     }
 
     /* ---- range ops: markRangeRemoved (2640-2752) / annotateRange (2598-2638) ----------- */
@@ -3313,7 +3334,7 @@ struct Replica {
             if (!dh) dhead(MT_DELTA_REMOVE);
             dtail(dn);
         }
-        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
+        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni_soon();
     }
     MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t refSeq,
                               int32_t client, int32_t seq) {
@@ -3347,7 +3368,64 @@ struct Replica {
             if (!dh) dhead(MT_DELTA_ANNOTATE);
             dtail(dn);
         }
-        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni();
+        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni_soon();
+    }
+
+    /* ---- relative positions: MergeTree.posFromRelativePos (mergeTree.ts:1976-1999) ---------- */
+    /* The row of the marker whose property `kid` (the marker-id key) holds value `vid` (getMarkerFromId,
+     * 1965-1967: the reference's idToSegment map, filled when a marker with an id is inserted): -1 none,
+     * -2 more than one (the reference keeps the last one it registered; not modelled) */
+    MT_HD int32_t marker_by_id(int32_t kid, int32_t vid) {
+        int32_t slot = -1;
+        for (int32_t k = 0; k < z.h.nkeys; k++)
+            if (z.keys[k] == kid) slot = k;
+        if (slot < 0 || (vid & ~MT_VALUE_FALSY) == 0) return -1;
+        int32_t found = -1, n = 0;
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+            int32_t lf = leaf_at(k), c = nch[lf];
+            for (int32_t j0 = 0; j0 < c; j0 += W::N) {
+                int32_t j = j0 + w.lane();
+                bool hit = false;
+                if (j < c) {
+                    int32_t q = lf * MAXN + j;
+                    uint8_t fl = z.flags(q);
+                    hit = (fl & RF_MARKER) && (fl & RF_PROPS) &&
+                          ((cold(q).pv[slot] ^ vid) & ~MT_VALUE_FALSY) == 0;
+                }
+                uint64_t m = w.ballot(hit);
+                if (m) {
+                    n += __builtin_popcountll(m);
+                    found = lf * MAXN + j0 + W::ffs(m);
+                }
+            }
+        }
+        return n > 1 ? -2 : found;
+    }
+    /* one relative position (spec units {vid, bits, off lo, off hi}) under (refSeq, client); false if the
+     * engine cannot resolve it as the reference would (no marker, or several) */
+    MT_HD bool rel_pos(int32_t kid, const uint16_t* u, int32_t refSeq, int32_t client, int32_t* pos) {
+        int32_t s = marker_by_id(kid, u[0]);
+        if (s < 0) return false;
+        int32_t off = (int32_t)((uint32_t)u[2] | ((uint32_t)u[3] << 16));
+        int32_t P = position_of(s, refSeq, client);
+        if (!(u[1] & 1)) {
+            P += z.len(s); /* after the marker: + cachedLength (+ offset) */
+            if (u[1] & 2) P += off;
+        } else if (u[1] & 2) {
+            P -= off;
+        }
+        *pos = P;
+        return true;
+    }
+    /* getValidOpRange's relative positions of a sequenced record (mt_oplog.h MT_SEG_RELPOS): the record
+     * with them resolved, or false */
+    MT_HD bool resolve_rel(const mt_op_rec& op, const Pools& p, int32_t client, mt_op_rec* out) {
+        const uint16_t* u = p.text + op.text_off + op.text_len;
+        *out = op;
+        out->seg_kind = (uint8_t)(op.seg_kind & 0x7F);
+        if ((u[1] & 1) && !rel_pos(u[0], u + 2, op.ref_seq, client, &out->pos1)) return false;
+        if ((u[1] & 2) && !rel_pos(u[0], u + 6, op.ref_seq, client, &out->pos2)) return false;
+        return true;
     }
 
     /* ---- reconnect: Client.regeneratePendingOp (client.ts:706-762, 855-893) -------------- */
@@ -3517,13 +3595,19 @@ struct Replica {
             /* drop the acked group's membership entries */
             mem_compact();
         }
-        zamboni();
+        zamboni_soon();
     }
 
     /* ---- Client.applyMsg (client.ts:797-819) / local edits ---------------------------- */
     MT_HD void apply(const mt_op_rec& op, const Pools& p) {
         MT_PROF_SCOPE(PH_APPLY);
         if (h.err) return;
+        apply_record(op, p);
+        run_zamboni();
+    }
+    /* One record. Every path that edits the tree ends in the one call site of insert_segments /
+     * mark_range_removed / annotate_range below (each is inlined once). */
+    MT_HD void apply_record(const mt_op_rec& op, const Pools& p) {
         int32_t kind = op.kind & MT_OP_KIND_MASK;
         if constexpr (DL) {
             if (Doc<HT>::has_fx(d.caps)) { /* delta events: this record's seq; none while a snapshot loads */
@@ -3541,8 +3625,8 @@ struct Replica {
             nkv = pr.nkv;
             rw = pr.combining == MT_COMBINE_REWRITE;
         }
-        if (kind >= MT_OP_RELOAD && !(op.kind & MT_OPF_LOCAL)) {
-            apply_load(op, p);
+        if ((op.seg_kind & MT_SEG_RELPOS) && (op.kind & (MT_OPF_LOCAL | MT_OPF_TREE) || kind > MT_OP_ANNOTATE)) {
+            fail(E_UNSUPPORTED); /* relative positions: sequenced op records only (mt_oplog.h) */
             h.opsDone++;
             return;
         }
@@ -3555,79 +3639,101 @@ struct Replica {
             h.opsDone++;
             return;
         }
-        if (op.kind & MT_OPF_LOCAL) {
-            int32_t client = h.collaborating ? h.localShort : -1;
-            int32_t refSeq = h.currentSeq;
-            int32_t seq = h.collaborating ? UNASSIGNED_SEQ : UNIVERSAL_SEQ;
+        /* the edit the record makes, if any */
+        mt_op_rec o = op;
+        bool edit = false, remote = false, grouped = false;
+        int32_t eref = 0, ecli = 0, eseq = 0, epre = 0, eat = -1;
+        uint8_t eprc = 0;
+        if (kind >= MT_OP_RELOAD && !(op.kind & MT_OPF_LOCAL) && !(op.kind & MT_OPF_TREE)) {
+            edit = apply_load(op, p, &o, &ecli, &epre, &eprc); /* snapshot load (mt_oplog.h) */
+            eref = UNIVERSAL_SEQ;
+            eseq = op.seq;
+        } else if (op.kind & MT_OPF_TREE) { /* MergeTree-level call with explicit (refSeq, clientId, seq) */
+            ecli = op.client == MT_CLIENT_LOCAL ? -1 : get_or_add_short(op.client);
+            if (op.client == MT_CLIENT_NONCOLLAB || (op.kind & MT_OPF_LOCAL) || kind > MT_OP_ANNOTATE ||
+                (kind == MT_OP_INSERT && op.seg_kind != MT_SEG_MARKER && op.text_len == 0)) {
+                fail(E_UNSUPPORTED);
+            } else {
+                edit = true;
+                eref = op.ref_seq;
+                eseq = op.seq;
+            }
+        } else if (op.kind & MT_OPF_LOCAL) {
+            ecli = h.collaborating ? h.localShort : -1;
+            eref = h.currentSeq;
+            eseq = h.collaborating ? UNASSIGNED_SEQ : UNIVERSAL_SEQ;
             /* getValidOpRange (client.ts:486-548) */
             int32_t length = length_local();
             int32_t start = op.pos1, end = op.pos2;
             bool bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
             if (kind != MT_OP_INSERT && end <= start) bad = true;
             if (kind == MT_OP_INSERT && (op.kind & MT_OPF_ATREF)) { /* pos1 is a reference, not a position */
-                if constexpr (DL)
-                    insert_at_ref(op, p);
-                else
+                if constexpr (DL) {
+                    edit = insert_at_ref(op, &eat);
+                    ecli = h.localShort;
+                    eseq = UNASSIGNED_SEQ;
+                } else {
                     fail(E_UNSUPPORTED); /* the client-feature build (caps.rcap > 0) replays these */
-                h.opsDone++;
-                return;
-            }
-            if (op.kind & MT_OPF_REGEN) { /* regeneratePendingOp of the head pending op (mt_oplog.h) */
+                }
+            } else if (op.kind & MT_OPF_REGEN) { /* regeneratePendingOp of the head pending op (mt_oplog.h) */
                 if constexpr (DL)
                     regen(kind);
                 else
                     fail(E_UNSUPPORTED);
-                h.opsDone++;
-                return;
-            }
-            if (bad) { /* rejected: no effect (the reference logs InvalidOpRange and returns undefined) */
-                h.opsDone++;
-                return;
-            }
-            if (kind == MT_OP_INSERT) {
-                if (op.seg_kind != MT_SEG_MARKER && op.text_len == 0) return;
-                insert_segments(op, p, refSeq, client, seq);
-            } else if (kind == MT_OP_REMOVE) {
-                mark_range_removed(start, end, refSeq, client, seq);
-            } else if (kind == MT_OP_ANNOTATE) {
-                annotate_range(start, end, kv, nkv, rw, refSeq, client, seq);
-            }
-            h.opsDone++;
-            return;
-        }
-        get_or_add_short(op.client);
-        bool grouped = (op.kind & MT_OPF_GROUPED) != 0; /* a group member before the last (mt_oplog.h) */
-        if (!grouped) z.h.seqOps++; /* one sequenced message per group */
-        if (grouped) {
-        } else if constexpr (TILED) /* BASELINE.md tile formula, in 16-byte units: 4 B per chunk summary,
-                                64 B per window row, 640 B for the target chunk's leaves + leaf line */
-            h.sumR += (4 * z.tl.nchunk + 64 * z.tl.wN + 640) / 16;
-        else
-            h.sumR += h.nrows;
-        if (kind != MT_OP_NOOP) {
-            if ((int32_t)op.client == h.localLong) {
-                ack(kind, kv, nkv, rw, op.seq);
+            } else if (bad) { /* rejected: no effect (the reference logs InvalidOpRange and returns undefined) */
+            } else if (kind == MT_OP_INSERT && op.seg_kind != MT_SEG_MARKER && op.text_len == 0) {
+                return; /* insertSegmentLocal of an empty segment */
             } else {
-                int32_t client = get_or_add_short(op.client);
-                if (kind == MT_OP_INSERT)
-                    insert_segments(op, p, op.ref_seq, client, op.seq);
-                else if (kind == MT_OP_REMOVE)
-                    mark_range_removed(op.pos1, op.pos2, op.ref_seq, client, op.seq);
-                else if (kind == MT_OP_ANNOTATE)
-                    annotate_range(op.pos1, op.pos2, kv, nkv, rw, op.ref_seq, client, op.seq);
+                edit = kind <= MT_OP_ANNOTATE;
+            }
+        } else {
+            remote = true;
+            get_or_add_short(op.client);
+            grouped = (op.kind & MT_OPF_GROUPED) != 0; /* a group member before the last (mt_oplog.h) */
+            if (!grouped) z.h.seqOps++; /* one sequenced message per group */
+            if (grouped) {
+            } else if constexpr (TILED) /* BASELINE.md tile formula, in 16-byte units: 4 B per chunk summary,
+                                    64 B per window row, 640 B for the target chunk's leaves + leaf line */
+                h.sumR += (4 * z.tl.nchunk + 64 * z.tl.wN + 640) / 16;
+            else
+                h.sumR += h.nrows;
+            if (kind != MT_OP_NOOP) {
+                if ((int32_t)op.client == h.localLong) {
+                    ack(kind, kv, nkv, rw, op.seq);
+                } else {
+                    ecli = get_or_add_short(op.client);
+                    eref = op.ref_seq;
+                    eseq = op.seq;
+                    edit = true;
+                    if (op.seg_kind & MT_SEG_RELPOS) { /* relative positions (mt_oplog.h) */
+                        if constexpr (DL)
+                            edit = resolve_rel(op, p, ecli, &o);
+                        else
+                            edit = false;
+                        if (!edit) fail(E_UNSUPPORTED);
+                    }
+                }
+            }
+        }
+        if (edit) {
+            if (kind == MT_OP_REMOVE)
+                mark_range_removed(o.pos1, o.pos2, eref, ecli, eseq);
+            else if (kind == MT_OP_ANNOTATE)
+                annotate_range(o.pos1, o.pos2, kv, nkv, rw, eref, ecli, eseq);
+            else
+                insert_segments(o, p, eref, ecli, eseq, epre, eprc, eat);
+            if (remote) {
                 if (!(h.currentSeq < op.seq)) fail(E_ASSERT);
                 if (!(h.minSeq <= op.min_seq)) fail(E_ASSERT);
             }
         }
-        if (grouped) { /* the message's seq update waits for its last member (client.ts:782-790, 615-622) */
-            h.opsDone++;
-            return;
+        if (remote && !grouped) { /* a group's seq update waits for its last member (client.ts:782-790) */
+            /* updateSeqNumbers (client.ts:821-828) */
+            if (!(h.currentSeq <= op.seq)) fail(E_ASSERT);
+            h.currentSeq = op.seq;
+            if (!(op.min_seq <= op.seq)) fail(E_ASSERT);
+            set_min_seq(op.min_seq);
         }
-        /* updateSeqNumbers (client.ts:821-828) */
-        if (!(h.currentSeq <= op.seq)) fail(E_ASSERT);
-        h.currentSeq = op.seq;
-        if (!(op.min_seq <= op.seq)) fail(E_ASSERT);
-        set_min_seq(op.min_seq);
         h.opsDone++;
     }
     /* high-water mark of row slots in use (stats), noted whenever the leaf count grows */
@@ -3744,7 +3850,10 @@ struct Replica {
         if constexpr (TILED) row_enter(s);
         return true;
     }
-    MT_HD void apply_load(const mt_op_rec& op, const Pools& p) {
+    /* a snapshot-load record; true if it is a body segment to insert (the caller's insert: *ins at the position
+     * loadBody computes, client *cl, removedSeq *pre by client *prc) */
+    MT_HD bool apply_load(const mt_op_rec& op, const Pools& p, mt_op_rec* ins, int32_t* cl, int32_t* pre,
+                          uint8_t* prc) {
         int32_t kind = op.kind & MT_OP_KIND_MASK;
         if (kind == MT_OP_RELOAD) {
             if (h.nrows == 0 && !h.collaborating) reload(p, op.pos1); /* the first of the header's records */
@@ -3754,28 +3863,56 @@ struct Replica {
             /* a batch of segments (one insertSegments call, blockInsert 2226-2256) starts at the local
              * length; its later members (GROUPED) go at the previous position + the previous
              * segment's whole length, removed or not */
-            mt_op_rec ins = op;
-            ins.pos1 = (op.kind & MT_OPF_GROUPED) ? z.h.loadPos : h.localLen;
-            z.h.loadPos = ins.pos1 + seg_len(op);
-            int32_t cl = loader_client(op.client);
+            *ins = op;
+            ins->pos1 = (op.kind & MT_OPF_GROUPED) ? z.h.loadPos : h.localLen;
+            z.h.loadPos = ins->pos1 + seg_len(op);
+            *cl = loader_client(op.client);
             int32_t rc = op.ref_seq > 0 ? loader_client((uint16_t)op.min_seq) : 0;
-            if (h.err) return;
-            insert_segments(ins, p, UNIVERSAL_SEQ, cl, op.seq, op.ref_seq > 0 ? op.ref_seq : 0,
-                            (uint8_t)(rc < 0 ? LOCAL_CLIENT : rc));
+            if (h.err) return false;
+            *pre = op.ref_seq > 0 ? op.ref_seq : 0;
+            *prc = (uint8_t)(rc < 0 ? LOCAL_CLIENT : rc);
+            return true;
         }
+        return false;
     }
 
     /* Client.getLength(): the local view's length, kept incrementally like root.cachedLength */
     MT_HD int32_t length_local() const { return h.localLen; }
 
     /* ---- reads: text (MergeTreeTextHelper.getText, textSegment.ts:154-275) ------------ */
-    /* Writes at most cap units; returns the text length under the perspective. */
+    /* getText(refSeq, clientId, placeholder, start, end): mapRange over [start, end) (getValidRange 174-186:
+     * start undefined = 0, end undefined = getLength; pass TEXT_RANGE_DEFAULT) visits every row with a
+     * non-zero perspective length v at position p where start < p + v and end > p (nodeMap). gatherText
+     * (188-271): a text row adds text.substring(start - p, end - p) with JavaScript's substring rules (the
+     * whole text when start <= p and end >= p + v); any other row adds `placeholder` v times when the
+     * placeholder is non-empty ("*", which prints Marker.toString(), is rejected by the callers). Writes at
+     * most cap units; returns the text length. */
+    static constexpr int32_t TEXT_RANGE_DEFAULT = INT32_MIN;
+    MT_HD static void text_piece(int32_t v, int32_t rs, int32_t re, int32_t* a, int32_t* b) {
+        if (rs <= 0 && re >= v) {
+            *a = 0, *b = v;
+            return;
+        }
+        int32_t x = rs < 0 ? 0 : rs, y = re >= v ? v : re; /* substring(x, y): clamp to [0, v], then order */
+        x = x < 0 ? 0 : (x > v ? v : x);
+        y = y < 0 ? 0 : (y > v ? v : y);
+        *a = x < y ? x : y, *b = x < y ? y : x;
+    }
     MT_HD int64_t get_text(int32_t refSeq, int32_t client, uint16_t* out, int64_t cap) {
+        return get_text_range(refSeq, client, 0, INT32_MAX, nullptr, 0, out, cap);
+    }
+    MT_HD int64_t get_text_range(int32_t refSeq, int32_t client, int32_t start, int32_t end, const uint16_t* ph,
+                                 int32_t pl, uint16_t* out, int64_t cap) {
+        if (start == TEXT_RANGE_DEFAULT) start = 0;
+        if (end == TEXT_RANGE_DEFAULT) end = length(refSeq, client);
+        if (start < 0) start = 0; /* the same rows and pieces as 0 (positions are >= 0); no overflow below */
+        if (end < -1) end = -1;   /* the same as -1: no row */
         int64_t n = 0;
+        int32_t P = 0; /* position of the pass's first row */
         const uint16_t* base = arena_base(h.arenaSide);
         if constexpr (W::N >= MAXN * MAXN) {
             /* 8 leaves x 8 slots per pass of the wave: each lane's row length under the perspective, one
-             * exclusive scan for the output offsets, and every lane copies its own row's text */
+             * scan for the positions and one for the output offsets, and every lane copies its own piece */
             int32_t k = 0;
             bool more = kvalid(0);
             while (more) {
@@ -3789,16 +3926,28 @@ struct Replica {
                 int32_t v = 0, s = -1;
                 if (leaf >= 0 && j < nch[leaf]) {
                     s = leaf * MAXN + j;
-                    if (!(z.flags(s) & RF_NOTEXT)) v = vis(s, refSeq, client);
+                    v = vis(s, refSeq, client);
                 }
+                int32_t vtot;
+                int32_t p = P + w.excl_scan(v, &vtot);
+                bool hit = v > 0 && start < p + v && end > p;
+                bool text = s >= 0 && !(z.flags(s) & RF_NOTEXT);
+                int32_t a = 0, b = 0;
+                if (hit && text) text_piece(v, start - p, end - p, &a, &b);
+                int32_t ol = !hit ? 0 : text ? b - a : pl * v;
                 int32_t tot;
-                int64_t o = n + w.excl_scan(v, &tot);
-                if (out && v > 0 && o < cap) {
-                    const uint16_t* src = base + cold(s).toff;
-                    int64_t m = v < cap - o ? v : cap - o;
-                    for (int64_t u = 0; u < m; u++) out[o + u] = src[u];
+                int64_t o = n + w.excl_scan(ol, &tot);
+                if (out && ol > 0 && o < cap) {
+                    int64_t m = ol < cap - o ? ol : cap - o;
+                    if (text) {
+                        const uint16_t* src = base + cold(s).toff + a;
+                        for (int64_t u = 0; u < m; u++) out[o + u] = src[u];
+                    } else {
+                        for (int64_t u = 0; u < m; u++) out[o + u] = ph[u % pl];
+                    }
                 }
                 n += tot;
+                P += vtot;
             }
             w.sync();
             return n;
@@ -3807,15 +3956,22 @@ struct Replica {
             int32_t lf = leaf_at(k), c = nch[lf];
             for (int32_t j = 0; j < c; j++) {
                 int32_t s = lf * MAXN + j;
-                if (z.flags(s) & RF_NOTEXT) continue;
-                int32_t v = vis(s, refSeq, client);
-                if (v <= 0) continue;
-                if (out) {
-                    int32_t m = v;
-                    if (n + m > cap) m = (int32_t)(cap - n > 0 ? cap - n : 0);
-                    arena_copy(out + n, base + cold(s).toff, m);
+                int32_t v = vis(s, refSeq, client), p = P;
+                P += v;
+                if (v <= 0 || !(start < p + v && end > p)) continue;
+                if (z.flags(s) & RF_NOTEXT) {
+                    for (int32_t u = 0; u < pl * v; u++, n++)
+                        if (out && n < cap) out[n] = ph[u % pl];
+                    continue;
                 }
-                n += v;
+                int32_t a, b;
+                text_piece(v, start - p, end - p, &a, &b);
+                if (out) {
+                    int64_t m = b - a;
+                    if (n + m > cap) m = cap - n > 0 ? cap - n : 0;
+                    arena_copy(out + n, base + cold(s).toff + a, (int32_t)m);
+                }
+                n += b - a;
             }
         }
         return n;

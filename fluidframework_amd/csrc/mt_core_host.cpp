@@ -139,6 +139,11 @@ int32_t mth_length_local(mth_store* s, int64_t doc) {
 }
 
 int64_t mth_text(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* out, int64_t cap) {
+    return mth_text_range(s, doc, ref_seq, long_client, nullptr, 0, INT32_MIN, INT32_MIN, out, cap);
+}
+
+int64_t mth_text_range(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client, const uint16_t* ph,
+                       int32_t pl, int32_t start, int32_t end, uint16_t* out, int64_t cap) {
     return with_replica(s, doc, [&](auto& r) {
         int32_t sh;
         int32_t rs = ref_seq;
@@ -149,7 +154,7 @@ int64_t mth_text(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client
             sh = r.short_of(long_client);
             if (sh < 0) sh = 0x7fff;
         }
-        return r.get_text(rs, sh, out, cap);
+        return r.get_text_range(rs, sh, start, end, ph, pl, out, cap);
     });
 }
 
@@ -230,3 +235,24 @@ void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {
 }
 
 } /* extern "C" */
+
+/* MergeTree.posFromRelativePos in the local view (long_client < 0) or (ref_seq, long_client); returns 0 and
+ * the position (-1: no marker holds the id), or MT_E_UNSUPPORTED (4) if several markers hold it */
+int32_t mth_pos_from_relpos(mth_store* s, int64_t doc, int32_t kid, int32_t vid, int32_t before, int32_t has_off,
+                            int32_t off, int32_t ref_seq, int32_t long_client, int32_t* out) {
+    return with_replica(s, doc, [&](auto& r) {
+        int32_t sh = long_client < 0 ? r.h.localShort : r.short_of(long_client);
+        int32_t rs = long_client < 0 ? r.h.currentSeq : ref_seq;
+        if (sh < 0) sh = 0x7fff;
+        int32_t m = r.marker_by_id(kid, vid);
+        if (m == -2) return (int32_t)4;
+        int32_t pos = -1;
+        if (m >= 0) {
+            pos = r.position_of(m, rs, sh);
+            if (!before) pos += r.z.len(m) + (has_off ? off : 0);
+            else if (has_off) pos -= off;
+        }
+        *out = pos;
+        return (int32_t)0;
+    });
+}

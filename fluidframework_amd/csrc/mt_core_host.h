@@ -23,6 +23,10 @@ int32_t mth_error_op(mth_store* s, int64_t doc);
 int32_t mth_length(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client);
 int32_t mth_length_local(mth_store* s, int64_t doc);
 int64_t mth_text(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* out, int64_t cap);
+int32_t mth_pos_from_relpos(mth_store* s, int64_t doc, int32_t kid, int32_t vid, int32_t before, int32_t has_off,
+                            int32_t off, int32_t ref_seq, int32_t long_client, int32_t* out);
+int64_t mth_text_range(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client, const uint16_t* ph,
+                       int32_t pl, int32_t start, int32_t end, uint16_t* out, int64_t cap);
 int64_t mth_dump(mth_store* s, int64_t doc, uint8_t* out, int64_t cap);
 uint64_t mth_digest(mth_store* s, int64_t doc);
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8);

@@ -42,12 +42,12 @@ __global__ __launch_bounds__(WG) void k_init(Store<HT> st, int64_t ndocs) {
 }
 
 template <class HT>
-__global__ __launch_bounds__(WG) void k_start_collab(Store<HT> st, int64_t ndocs, const int32_t* local_long,
-                                                    int32_t min_seq, int32_t cur_seq) {
+/* local[d] = doc d's local long id, local[ndocs + d] / local[2 ndocs + d] its minSeq / currentSeq */
+__global__ __launch_bounds__(WG) void k_start_collab(Store<HT> st, int64_t ndocs, const int32_t* local) {
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
     Replica<WaveGPU, HT> r(st.doc(d), WaveGPU());
-    r.start_collab(local_long[d], min_seq, cur_seq);
+    r.start_collab(local[d], local[ndocs + d], local[2 * ndocs + d]);
     r.commit();
 }
 
@@ -258,6 +258,7 @@ __global__ __launch_bounds__(WG) void k_length(Store<HT> st, int64_t doc, int32_
 
 template <class HT>
 __global__ __launch_bounds__(WG) void k_text(Store<HT> st, int64_t doc, int32_t ref_seq, int32_t long_client,
+                                            int32_t start, int32_t end, const uint16_t* ph, int32_t pl,
                                             uint16_t* out, int64_t cap, int64_t* n) {
     Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
     int32_t sh;
@@ -268,11 +269,12 @@ __global__ __launch_bounds__(WG) void k_text(Store<HT> st, int64_t doc, int32_t 
         sh = r.short_of(long_client);
         if (sh < 0) sh = 0x7fff;
     }
-    int64_t m = r.get_text(ref_seq, sh, out, cap);
+    int64_t m = r.get_text_range(ref_seq, sh, start, end, ph, pl, out, cap);
     if (threadIdx.x == 0) *n = m;
 }
 
-/* getContainingSegment (mode 0: a = pos) / getPosition (mode 1: a = rid, b = gen) of one document;
+/* getContainingSegment (mode 0: a = pos) / getPosition (mode 1: a = rid, b = gen) / a marker's position by
+ * id (mode 2: a = marker-id key, b = value) of one document;
  * out[0] = status (1 found / 0 none), then mt_seg_ref fields or the position */
 template <class HT>
 __global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t mode, int32_t a, int32_t b,
@@ -300,9 +302,17 @@ __global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t m
             res[5] = r.z.seq(s);
             res[6] = r.long_of(r.z.cli(s));
         }
-    } else {
+    } else if (mode == 1) {
         int32_t s = (a >= 0 && a < HT::S) ? r.slot_of(a, b) : -1;
         if (s >= 0) {
+            res[0] = 1;
+            res[1] = r.position_of(s, ref_seq, sh);
+        }
+    } else { /* mode 2: the marker whose property a (the marker-id key) is value b; res[0] = 2 if several */
+        int32_t s = r.marker_by_id(a, b);
+        if (s == -2) {
+            res[0] = 2;
+        } else if (s >= 0) {
             res[0] = 1;
             res[1] = r.position_of(s, ref_seq, sh);
         }
@@ -366,7 +376,7 @@ struct mt_engine {
     std::vector<int32_t> pro;         /* doc -> index in `over`, -1: not promoted */
     std::vector<int64_t> pro_docs;    /* index in `over` -> doc */
     std::vector<int64_t> h_op_off, h_text_off, h_props_off, h_kv_off; /* host copies of the staged offsets */
-    std::vector<int32_t> h_local;     /* start_collab's local long ids */
+    std::vector<int32_t> h_local;     /* start_collab's local long ids, then per doc minSeq, then currentSeq */
     mt_caps caps0 = {};               /* creation capacities */
     bool borrowed = false;            /* text / props / kv point into the parent's staged pools */
     int device;
@@ -388,7 +398,6 @@ struct mt_engine {
     float last_ms = 0.f;
     bool staged = false;
     DevBuf ops_buf, op_off, text, text_off, props, props_off, kv, kv_off, tmp, local_ids, prof;
-    int32_t min_seq0 = 0, cur_seq0 = 0;
     bool collab = false;
     std::string err;
 };
@@ -415,14 +424,14 @@ static inline dim3 flat_grid(int64_t n) { return dim3((unsigned)((n + 255) / 256
 /* The store-dependent launches of one profile. Device pointers come from the engine's buffers. */
 struct ProfOps {
     int32_t (*init)(mt_engine* e);                                    /* k_init (+ k_start_collab) */
-    int32_t (*start_collab)(mt_engine* e, int32_t min_seq, int32_t cur_seq);
+    int32_t (*start_collab)(mt_engine* e); /* k_start_collab from local_ids (ids, minSeq, currentSeq per doc) */
     int32_t (*replay)(mt_engine* e);                                  /* k_replay over the staged batch */
     int32_t (*hdr)(mt_engine* e, int32_t* de, int32_t* deo, int32_t* ds, int64_t* dw);
     int32_t (*digest)(mt_engine* e, uint64_t* dout);
     int32_t (*dump)(mt_engine* e, int64_t doc, uint8_t* dbuf, int64_t cap, int64_t* dn);
     int32_t (*length)(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t* dout);
-    int32_t (*text)(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* dbuf, int64_t cap,
-                    int64_t* dn);
+    int32_t (*text)(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t start, int32_t end,
+                    const uint16_t* dph, int32_t pl, uint16_t* dbuf, int64_t cap, int64_t* dn);
     int32_t (*seg)(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,
                    int32_t long_client, int32_t* dout);
     int32_t (*refpos)(mt_engine* e, int32_t* dn, int32_t* dpos);
@@ -462,12 +471,12 @@ struct Launch {
         int32_t rc = launch_check(e, "k_init");
         if (rc || !e->collab) return rc;
         hipLaunchKernelGGL((k_start_collab<HT>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, st, e->ndocs,
-                           (const int32_t*)e->local_ids.p, e->min_seq0, e->cur_seq0);
+                           (const int32_t*)e->local_ids.p);
         return launch_check(e, "k_start_collab");
     }
-    static int32_t start_collab(mt_engine* e, int32_t min_seq, int32_t cur_seq) {
+    static int32_t start_collab(mt_engine* e) {
         hipLaunchKernelGGL((k_start_collab<HT>), docs_grid(e->ndocs), dim3(WG), 0, e->stream, store_of<HT>(e),
-                           e->ndocs, (const int32_t*)e->local_ids.p, min_seq, cur_seq);
+                           e->ndocs, (const int32_t*)e->local_ids.p);
         return launch_check(e, "k_start_collab");
     }
     static int32_t hdr(mt_engine* e, int32_t* de, int32_t* deo, int32_t* ds, int64_t* dw) {
@@ -489,10 +498,10 @@ struct Launch {
                            long_client, dout);
         return launch_check(e, "k_length");
     }
-    static int32_t text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* dbuf, int64_t cap,
-                        int64_t* dn) {
+    static int32_t text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t start, int32_t end,
+                        const uint16_t* dph, int32_t pl, uint16_t* dbuf, int64_t cap, int64_t* dn) {
         hipLaunchKernelGGL((k_text<HT>), dim3(1), dim3(WG), 0, e->stream, store_of<HT>(e), doc, ref_seq, long_client,
-                           dbuf, cap, dn);
+                           start, end, dph, pl, dbuf, cap, dn);
         return launch_check(e, "k_text");
     }
     static int32_t seg(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,

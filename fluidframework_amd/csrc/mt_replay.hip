@@ -105,16 +105,24 @@ float mt_engine_last_run_ms(const mt_engine* e) { return e ? e->last_ms : 0.f; }
 
 int32_t mt_engine_start_collab(mt_engine* e, const int32_t* local_long_ids, int32_t min_seq, int32_t cur_seq) {
     if (!e || !local_long_ids) return MT_E_ARG;
+    std::vector<int32_t> mins((size_t)e->ndocs, min_seq), curs((size_t)e->ndocs, cur_seq);
+    return mt_engine_start_collab_docs(e, local_long_ids, mins.data(), curs.data());
+}
+
+int32_t mt_engine_start_collab_docs(mt_engine* e, const int32_t* local_long_ids, const int32_t* min_seqs,
+                                    const int32_t* cur_seqs) {
+    if (!e || !local_long_ids || !min_seqs || !cur_seqs) return MT_E_ARG;
+    int64_t nd = e->ndocs;
     HIPCHK(e, hipSetDevice(e->device));
-    int32_t rc = ensure(e, e->local_ids, sizeof(int32_t) * e->ndocs);
+    e->h_local.assign(local_long_ids, local_long_ids + nd);
+    e->h_local.insert(e->h_local.end(), min_seqs, min_seqs + nd);
+    e->h_local.insert(e->h_local.end(), cur_seqs, cur_seqs + nd);
+    int32_t rc = ensure(e, e->local_ids, sizeof(int32_t) * 3 * nd);
     if (rc) return rc;
-    HIPCHK(e, hipMemcpyAsync(e->local_ids.p, local_long_ids, sizeof(int32_t) * e->ndocs, hipMemcpyHostToDevice,
+    HIPCHK(e, hipMemcpyAsync(e->local_ids.p, e->h_local.data(), sizeof(int32_t) * 3 * nd, hipMemcpyHostToDevice,
                              e->stream));
-    e->h_local.assign(local_long_ids, local_long_ids + e->ndocs);
-    e->min_seq0 = min_seq;
-    e->cur_seq0 = cur_seq;
     e->collab = true;
-    rc = e->ops->start_collab(e, min_seq, cur_seq);
+    rc = e->ops->start_collab(e);
     if (rc) return rc;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return MT_OK;
@@ -139,8 +147,11 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
             for (int64_t i = op_off[d]; i < op_off[d + 1]; i++) {
                 const mt_op_rec& o = ops[i];
                 int kind = o.kind & MT_OP_KIND_MASK;
-                if (kind == MT_OP_INSERT && o.seg_kind == MT_SEG_TEXT &&
+                if (kind == MT_OP_INSERT && (o.seg_kind & 0x7F) == MT_SEG_TEXT &&
                     text_off[d] + (int64_t)o.text_off + o.text_len > text_units)
+                    return false;
+                if ((o.seg_kind & MT_SEG_RELPOS) &&
+                    text_off[d] + (int64_t)o.text_off + o.text_len + MT_RELPOS_UNITS > text_units)
                     return false;
                 /* snapshot-load records carry the segment length in pos2 (mt_oplog.h) */
                 if ((kind == MT_OP_RELOAD || kind == MT_OP_APPEND) && o.seg_kind == MT_SEG_TEXT &&
@@ -307,15 +318,15 @@ static int32_t promote(mt_engine* e) {
     }
     o->promote = e->promote;
     if (e->collab) {
-        std::vector<int32_t> loc((size_t)m);
-        for (int64_t i = 0; i < m; i++) loc[(size_t)i] = e->h_local[(size_t)e->pro_docs[(size_t)i]];
+        std::vector<int32_t> loc((size_t)(3 * m)); /* the promoted documents' ids, minSeqs, currentSeqs */
+        for (int64_t i = 0; i < m; i++)
+            for (int64_t k = 0; k < 3; k++)
+                loc[(size_t)(k * m + i)] = e->h_local[(size_t)(k * nd + e->pro_docs[(size_t)i])];
         HIPCHK(o, hipSetDevice(o->device));
-        if ((rc = ensure(o, o->local_ids, sizeof(int32_t) * m))) return rc;
-        HIPCHK(o, hipMemcpyAsync(o->local_ids.p, loc.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, o->stream));
+        if ((rc = ensure(o, o->local_ids, sizeof(int32_t) * 3 * m))) return rc;
+        HIPCHK(o, hipMemcpyAsync(o->local_ids.p, loc.data(), sizeof(int32_t) * 3 * m, hipMemcpyHostToDevice, o->stream));
         HIPCHK(o, hipStreamSynchronize(o->stream));
         o->h_local = loc;
-        o->min_seq0 = e->min_seq0;
-        o->cur_seq0 = e->cur_seq0;
         o->collab = true;
     }
     /* the promoted documents' records, gathered device to device; their pools are the parent's */
@@ -456,13 +467,28 @@ int32_t mt_engine_get_length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t
 
 int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* out,
                            int64_t cap) {
-    if (!e || doc < 0 || doc >= e->ndocs || cap < 0) return -MT_E_ARG;
+    return mt_engine_get_text_range(e, doc, ref_seq, long_client, nullptr, 0, MT_TEXT_DEFAULT, MT_TEXT_DEFAULT, out,
+                                    cap);
+}
+
+int64_t mt_engine_get_text_range(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client,
+                                 const uint16_t* placeholder, int32_t placeholder_len, int32_t start, int32_t end,
+                                 uint16_t* out, int64_t cap) {
+    if (!e || doc < 0 || doc >= e->ndocs || cap < 0 || placeholder_len < 0 || placeholder_len > 4096 ||
+        (placeholder_len > 0 && !placeholder))
+        return -MT_E_ARG;
+    if (placeholder_len == 1 && placeholder[0] == '*') return -MT_E_UNSUPPORTED; /* Marker.toString() */
     e = route(e, &doc);
     if (hipSetDevice(e->device) != hipSuccess) return -MT_E_HIP;
-    if (ensure(e, e->tmp, 16 + 2 * (size_t)(out ? cap : 0) + 16)) return -MT_E_HIP;
+    size_t phb = (2 * (size_t)placeholder_len + 15) & ~(size_t)15;
+    if (ensure(e, e->tmp, 16 + phb + 2 * (size_t)(out ? cap : 0) + 16)) return -MT_E_HIP;
     int64_t* dn = (int64_t*)e->tmp.p;
-    uint16_t* dbuf = out ? (uint16_t*)((uint8_t*)e->tmp.p + 16) : nullptr;
-    int32_t rc = e->ops->text(e, doc, ref_seq, long_client, dbuf, out ? cap : 0, dn);
+    uint16_t* dph = (uint16_t*)((uint8_t*)e->tmp.p + 16);
+    uint16_t* dbuf = out ? (uint16_t*)((uint8_t*)e->tmp.p + 16 + phb) : nullptr;
+    if (placeholder_len > 0 &&
+        hipMemcpyAsync(dph, placeholder, 2 * (size_t)placeholder_len, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+        return -MT_E_HIP;
+    int32_t rc = e->ops->text(e, doc, ref_seq, long_client, start, end, dph, placeholder_len, dbuf, out ? cap : 0, dn);
     if (rc) return -rc;
     int64_t n = 0;
     if (hipMemcpyAsync(&n, dn, sizeof(int64_t), hipMemcpyDeviceToHost, e->stream) != hipSuccess) return -MT_E_HIP;
@@ -512,6 +538,24 @@ int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t g
     if (rc) return rc;
     if (!r[0]) return MT_E_ARG;
     *out = r[1];
+    return MT_OK;
+}
+
+int32_t mt_engine_pos_from_relative_pos(mt_engine* e, int64_t doc, int32_t id_key, int32_t id_value, int32_t before,
+                                        int32_t has_offset, int32_t offset, int32_t ref_seq, int32_t long_client,
+                                        int32_t* out) {
+    if (!out) return MT_E_ARG;
+    int32_t r[7];
+    int32_t rc = seg_query(e, doc, 2, id_key, id_value, ref_seq, long_client, r);
+    if (rc) return rc;
+    if (r[0] == 2) return MT_E_UNSUPPORTED; /* several markers hold the id */
+    int32_t pos = -1;
+    if (r[0] == 1) { /* mergeTree.ts:1986-1996: a marker's cachedLength is 1 */
+        pos = r[1];
+        if (!before) pos += 1 + (has_offset ? offset : 0);
+        else if (has_offset) pos -= offset;
+    }
+    *out = pos;
     return MT_OK;
 }
 

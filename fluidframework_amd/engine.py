@@ -17,6 +17,7 @@ import numpy as np
 from . import native
 from . import oplog as ol
 
+TEXT_DEFAULT = -(1 << 31)  # MT_TEXT_DEFAULT: getValidRange's default start / end (mt_engine_get_text_range)
 ERRORS = {0: "ok", 1: "MergeTree insert failed", 2: "assertion", 3: "invalid op range", 4: "unsupported",
           5: "capacity exceeded"}
 
@@ -50,6 +51,8 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_last_error.argtypes = [vp]
         L.mt_engine_last_error.restype = ctypes.c_char_p
         L.mt_engine_start_collab.argtypes = [vp, vp, i32, i32]
+        L.mt_engine_start_collab_docs.argtypes = [vp, vp, vp, vp]
+        L.mt_engine_pos_from_relative_pos.argtypes = [vp, i64, i32, i32, i32, i32, i32, i32, i32, vp]
         L.mt_engine_submit.argtypes = [vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, i64, vp]
         L.mt_engine_run.argtypes = [vp]
         L.mt_engine_reset.argtypes = [vp]
@@ -68,6 +71,8 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_get_length.argtypes = [vp, i64, i32, i32, ctypes.POINTER(i32)]
         L.mt_engine_get_text.argtypes = [vp, i64, i32, i32, vp, i64]
         L.mt_engine_get_text.restype = i64
+        L.mt_engine_get_text_range.argtypes = [vp, i64, i32, i32, vp, i32, i32, i32, vp, i64]
+        L.mt_engine_get_text_range.restype = i64
         L.mt_engine_stats.argtypes = [vp, vp]
         L.mt_engine_get_containing_segment.argtypes = [vp, i64, i32, i32, i32, ctypes.POINTER(SegRef)]
         L.mt_engine_get_position.argtypes = [vp, i64, i32, i32, i32, i32, ctypes.POINTER(i32)]
@@ -132,9 +137,13 @@ class Engine:
             msg = self.L.mt_engine_last_error(self.h)
             raise EngineError(f"{what} failed: status {rc}: {msg.decode() if msg else ''}")
 
-    def start_collab(self, local_long_ids, min_seq: int = 0, cur_seq: int = 0):
-        ids = np.ascontiguousarray(np.broadcast_to(np.asarray(local_long_ids, np.int32), (self.ndocs,)))
-        self._check(self.L.mt_engine_start_collab(self.h, _p(ids), min_seq, cur_seq), "start_collab")
+    def start_collab(self, local_long_ids, min_seq=0, cur_seq=0):
+        """Client.startOrUpdateCollaboration for every document (client.ts:1053-1073); min_seq / cur_seq are
+        one value for all documents or one per document (mt_engine_start_collab_docs)."""
+        def per_doc(x):
+            return np.ascontiguousarray(np.broadcast_to(np.asarray(x, np.int32), (self.ndocs,)))
+        ids, mins, curs = per_doc(local_long_ids), per_doc(min_seq), per_doc(cur_seq)
+        self._check(self.L.mt_engine_start_collab_docs(self.h, _p(ids), _p(mins), _p(curs)), "start_collab")
 
     def submit(self, b: ol.Batch):
         if b.ndocs != self.ndocs:
@@ -199,13 +208,31 @@ class Engine:
         self._check(self.L.mt_engine_get_length(self.h, doc, ref_seq, long_client, ctypes.byref(v)), "get_length")
         return v.value
 
-    def get_text(self, doc: int, ref_seq: int = 0, long_client: int = -1) -> str:
-        n = self.L.mt_engine_get_text(self.h, doc, ref_seq, long_client, None, 0)
+    def get_text(self, doc: int, ref_seq: int = 0, long_client: int = -1, placeholder: str = "",
+                 start: Optional[int] = None, end: Optional[int] = None) -> str:
+        """MergeTreeTextHelper.getText(refSeq, clientId, placeholder, start, end) (textSegment.ts:154-186);
+        long_client < 0 = the local view (Client.getText). start / end None = getValidRange's defaults."""
+        ph = np.frombuffer(placeholder.encode("utf-16-le"), "<u2").copy() if placeholder else None
+        pl = 0 if ph is None else len(ph)
+        a = TEXT_DEFAULT if start is None else start
+        b = TEXT_DEFAULT if end is None else end
+        pp = None if ph is None else _p(ph)
+        n = self.L.mt_engine_get_text_range(self.h, doc, ref_seq, long_client, pp, pl, a, b, None, 0)
         if n < 0:
             raise EngineError(f"get_text failed {n}")
         buf = np.zeros(max(n, 1), "<u2")
-        self.L.mt_engine_get_text(self.h, doc, ref_seq, long_client, _p(buf), n)
+        self.L.mt_engine_get_text_range(self.h, doc, ref_seq, long_client, pp, pl, a, b, _p(buf), n)
         return buf[:n].tobytes().decode("utf-16-le")
+
+    def pos_from_relative_pos(self, doc: int, key_id: int, value_id: int, before: bool = False,
+                              offset: Optional[int] = None, ref_seq: int = 0, long_client: int = -1) -> int:
+        """MergeTree.posFromRelativePos (mergeTree.ts:1976-1999) of IRelativePosition {id, before, offset}: the
+        marker whose property key_id (the interned "markerId") holds value_id; -1 if none holds it."""
+        v = ctypes.c_int32()
+        self._check(self.L.mt_engine_pos_from_relative_pos(self.h, doc, key_id, value_id, int(before),
+                                                           int(offset is not None), offset or 0, ref_seq,
+                                                           long_client, ctypes.byref(v)), "pos_from_relative_pos")
+        return v.value
 
     def get_containing_segment(self, doc: int, pos: int, ref_seq: int = 0, long_client: int = -1) -> Optional[SegRef]:
         """MergeTree.getContainingSegment (mergeTree.ts:1656-1667); long_client < 0 = the local view

@@ -24,8 +24,14 @@ const OPF_LOCAL = 0x80;
 const OPF_GROUPED = 0x40;
 const OPF_ATREF = 0x08; // insertAtReferencePositionLocal
 const OPF_REGEN = 0x10; // regeneratePendingOp
+const OPF_TREE = 0x20; // a MergeTree-level call with explicit (refSeq, clientId, seq)
+const CLIENT_LOCAL = 0xfffe; // LocalClientId in a MergeTree-level record
+const LocalClientId = -1; // constants.ts
+const UnassignedSequenceNumber = -1;
 const ReferenceType = { Simple: 0x0, SlideOnRemove: 0x40 }; // ops.ts
 const SEG = { TEXT: 0, MARKER: 1 };
+const SEG_RELPOS = 0x80; // positions relative to markers (mt_oplog.h MT_SEG_RELPOS)
+const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
 const VALUE_FALSY = 0x8000;
 const ERRORS = { 1: "MergeTree insert failed", 2: "assertion", 3: "invalid op range", 4: "unsupported",
     5: "capacity exceeded" };
@@ -133,16 +139,19 @@ class ReplayEngine {
 
     client(doc) { return new GpuClient(this, doc); }
 
-    /* startOrUpdateCollaboration for every document at once (mt_engine_start_collab) */
+    /* startOrUpdateCollaboration for every document at once (client.ts:1053-1073; mt_engine_start_collab_docs):
+     * minSeq / currentSeq are one number for every document or an array with one per document */
     startCollaboration(localNames, minSeq = 0, currentSeq = 0) {
         this.flush(); // edits queued before collaboration apply as non-collaborating local edits
         const ids = new Int32Array(this.ndocs);
+        const per = (x) => Int32Array.from({ length: this.ndocs }, (_, d) => (Array.isArray(x) || ArrayBuffer.isView(x) ? x[d] : x));
+        const mins = per(minSeq), curs = per(currentSeq);
         for (let d = 0; d < this.ndocs; d++) {
             this.localNames[d] = localNames[d];
             ids[d] = this.longIndex(localNames[d]);
-            this.currentSeq[d] = currentSeq;
+            this.currentSeq[d] = curs[d];
         }
-        addon.startCollab(this.h, ids, minSeq, currentSeq);
+        addon.startCollab(this.h, ids, mins, curs);
         this.collab = true;
     }
 
@@ -170,6 +179,19 @@ class ReplayEngine {
             if (props) r.props = this.propsRecord(q, props, undefined);
         } else if (k === OP.ANNOTATE) {
             r.props = this.propsRecord(q, segOrProps.props, segOrProps.combiningOp);
+        }
+        if (fields.rel1 || fields.rel2) { // IRelativePosition(s): the spec follows the record's text (mt_oplog.h MT_SEG_RELPOS)
+            delete r.rel1; delete r.rel2;
+            if (!(k === OP.INSERT && r.seg_kind === SEG.TEXT)) { r.text_off = q.text.length; r.text_len = 0; }
+            q.text.push(this.interner.key(MARKER_ID_KEY), (fields.rel1 ? 1 : 0) | (fields.rel2 ? 2 : 0));
+            for (const rp of [fields.rel1, fields.rel2]) {
+                if (!rp) { q.text.push(0, 0, 0, 0); continue; }
+                if (typeof rp.id !== "string") throw new Error("a relative position needs a marker id");
+                const off = rp.offset === undefined ? 0 : rp.offset >>> 0;
+                q.text.push(this.interner.value(rp.id) & 0xffff, (rp.before ? 1 : 0) | (rp.offset === undefined ? 0 : 2),
+                    off & 0xffff, off >>> 16);
+            }
+            r.seg_kind |= SEG_RELPOS;
         }
         q.recs.push(r);
     }
@@ -226,9 +248,44 @@ class ReplayEngine {
     digests() { this.flush(); return addon.digests(this.h); }
 }
 
+/* The MergeTree-level calls of one replica with explicit (refSeq, clientId, seq) (mergeTree.ts:2001-2031,
+ * 2598-2738; mt_oplog.h MT_OPF_TREE): what applyRemoteOp and the local edits call underneath. clientId is a
+ * long client id (string) or LocalClientId; seq UnassignedSequenceNumber makes a local pending op. They do
+ * not touch the collaboration window (no ack, no getValidOpRange, no updateSeqNumbers). */
+class GpuMergeTree {
+    constructor(client) { this.client = client; }
+
+    fields(refSeq, clientId, seq) {
+        const e = this.client.engine;
+        return { ref_seq: refSeq, seq, client: clientId === LocalClientId ? CLIENT_LOCAL : e.longIndex(clientId) };
+    }
+
+    /* one segment per call: a string, {text, props} or {marker: {refType}, props} */
+    insertSegments(pos, segments, refSeq, clientId, seq) {
+        if (!Array.isArray(segments) || segments.length !== 1) throw new Error("insertSegments: one segment per call");
+        const c = this.client;
+        c.engine.enqueue(c.doc, OP.INSERT | OPF_TREE, { ...this.fields(refSeq, clientId, seq), pos1: pos }, segments[0]);
+        if (seq === UnassignedSequenceNumber) c.sent(OP.INSERT);
+    }
+
+    markRangeRemoved(start, end, refSeq, clientId, seq, overwrite = false) {
+        if (overwrite) throw new Error("markRangeRemoved: overwrite = true is not modelled");
+        const c = this.client;
+        c.engine.enqueue(c.doc, OP.REMOVE | OPF_TREE, { ...this.fields(refSeq, clientId, seq), pos1: start, pos2: end });
+        if (seq === UnassignedSequenceNumber) c.sent(OP.REMOVE);
+    }
+
+    annotateRange(start, end, props, combiningOp, refSeq, clientId, seq) {
+        const c = this.client;
+        c.engine.enqueue(c.doc, OP.ANNOTATE | OPF_TREE, { ...this.fields(refSeq, clientId, seq), pos1: start, pos2: end },
+            { props, combiningOp });
+        if (seq === UnassignedSequenceNumber) c.sent(OP.ANNOTATE);
+    }
+}
+
 /* one replica: the reference Client's surface (client.ts:43) */
 class GpuClient {
-    constructor(engine, doc) { this.engine = engine; this.doc = doc; }
+    constructor(engine, doc) { this.engine = engine; this.doc = doc; this.mergeTree = new GpuMergeTree(this); }
 
     get longClientId() { return this.engine.localNames[this.doc]; }
 
@@ -246,10 +303,14 @@ class GpuClient {
             const members = op.type === OP.GROUP ? op.ops : [op];
             members.forEach((m, i) => {
                 const flag = i < members.length - 1 ? OPF_GROUPED : 0;
-                if (m.type === OP.INSERT) e.enqueue(this.doc, OP.INSERT | flag, { ...base, pos1: m.pos1 }, m.seg);
-                else if (m.type === OP.REMOVE) e.enqueue(this.doc, OP.REMOVE | flag, { ...base, pos1: m.pos1, pos2: m.pos2 });
+                // getValidOpRange (client.ts:486-503): a relative position where the absolute one is undefined
+                const rel1 = m.pos1 === undefined ? m.relativePos1 : undefined;
+                const rel2 = m.pos2 === undefined ? m.relativePos2 : undefined;
+                const pos = { pos1: rel1 ? 0 : m.pos1, pos2: rel2 ? 0 : m.pos2, rel1, rel2 };
+                if (m.type === OP.INSERT) e.enqueue(this.doc, OP.INSERT | flag, { ...base, pos1: pos.pos1, rel1 }, m.seg);
+                else if (m.type === OP.REMOVE) e.enqueue(this.doc, OP.REMOVE | flag, { ...base, ...pos });
                 else if (m.type === OP.ANNOTATE) {
-                    e.enqueue(this.doc, OP.ANNOTATE | flag, { ...base, pos1: m.pos1, pos2: m.pos2 }, m);
+                    e.enqueue(this.doc, OP.ANNOTATE | flag, { ...base, ...pos }, m);
                 } else throw new Error(`op type ${m.type} unsupported`);
             });
         }
@@ -337,17 +398,43 @@ class GpuClient {
         return ops; // per regenerated op: type, findReconnectionPostition, the segment's length
     }
 
+    /* Client.posFromRelativePos (client.ts:308, mergeTree.ts:1976-1999) in the local view: the position
+     * before / after the marker whose "markerId" is relativePos.id (+/- offset); -1 if no marker holds it */
+    posFromRelativePos(relativePos) {
+        const e = this.engine;
+        const h = this.read();
+        const off = relativePos.offset;
+        return addon.posFromRelativePos(h, this.doc, e.interner.key(MARKER_ID_KEY), e.interner.value(relativePos.id) & 0xffff,
+            relativePos.before ? 1 : 0, off === undefined ? 0 : 1, off === undefined ? 0 : off, 0, -1);
+    }
+
+    /* SharedString.insertTextRelative / insertMarkerRelative (sharedString.ts:86-140) */
+    insertTextRelative(relativePos1, text, props) { return this.insertTextLocal(this.posFromRelativePos(relativePos1), text, props); }
+
+    insertMarkerRelative(relativePos1, refType, props) {
+        return this.insertMarkerLocal(this.posFromRelativePos(relativePos1), refType, props);
+    }
+
     /* reads flush the queued events first */
     read() { this.engine.flush(); this.engine.checkDoc(this.doc); return this.engine.h; }
 
     getLength() { return addon.getLength(this.read(), this.doc, 0, -1); }
 
-    getText() { return addon.getText(this.read(), this.doc, 0, -1); }
+    /* SharedString.getText(start?, end?) (sequence/src/sharedString.ts:222-225): the local view */
+    getText(start, end) { return addon.getText(this.read(), this.doc, 0, -1, "", start, end); }
+
+    /* SharedString.getTextWithPlaceholders / getTextRangeWithPlaceholders (sharedString.ts:228-236): every
+     * marker (or other non-text segment) as " " */
+    getTextWithPlaceholders(start, end) { return addon.getText(this.read(), this.doc, 0, -1, " ", start, end); }
 
     /* MergeTree.getLength / getText under (refSeq, clientId) (mergeTree.ts:1610, textSegment.ts:154) */
     getLengthAt(refSeq, longClientId) { return addon.getLength(this.read(), this.doc, refSeq, this.engine.longIndex(longClientId)); }
 
-    getTextAt(refSeq, longClientId) { return addon.getText(this.read(), this.doc, refSeq, this.engine.longIndex(longClientId)); }
+    /* MergeTreeTextHelper.getText(refSeq, clientId, placeholder, start, end) (textSegment.ts:154-186); the
+     * placeholder "*" (Marker.toString() per marker) is not supported and throws */
+    getTextAt(refSeq, longClientId, placeholder = "", start, end) {
+        return addon.getText(this.read(), this.doc, refSeq, this.engine.longIndex(longClientId), placeholder, start, end);
+    }
 
     /* Client.getContainingSegment (client.ts:1006-1008): {segment: handle | undefined, offset} */
     getContainingSegment(pos) {
@@ -363,4 +450,5 @@ class GpuClient {
     deltaEvents() { return decodeDeltas(addon.deltas(this.read(), this.doc), this.engine.interner); }
 }
 
-module.exports = { ReplayEngine, GpuClient, Interner, addon, OP, DEFAULT_CAPS, decodeDeltas, ReferenceType };
+module.exports = { ReplayEngine, GpuClient, GpuMergeTree, Interner, addon, OP, DEFAULT_CAPS, decodeDeltas, ReferenceType,
+    LocalClientId, UnassignedSequenceNumber };

@@ -126,20 +126,39 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
     return h;
 }
 
-/* startCollab(h, Int32Array localLongIds, minSeq, curSeq) */
+/* startCollab(h, Int32Array localLongIds, minSeq | Int32Array minSeqs, curSeq | Int32Array curSeqs):
+ * one (minSeq, currentSeq) for every document, or each document's own (mt_engine_start_collab_docs) */
+static bool seqs_of(napi_env env, napi_value v, int64_t nd, std::vector<int32_t>* out) {
+    bool typed = false;
+    if (napi_is_typedarray(env, v, &typed) == napi_ok && typed) {
+        void* p;
+        size_t n;
+        if (!view_of(env, v, &p, &n, napi_int32_array)) return false;
+        if ((int64_t)n != nd) {
+            napi_throw_range_error(env, nullptr, "one sequence number per document");
+            return false;
+        }
+        out->assign((const int32_t*)p, (const int32_t*)p + n);
+        return true;
+    }
+    int32_t x;
+    if (!i32_of(env, v, &x)) return false;
+    out->assign((size_t)nd, x);
+    return true;
+}
 static napi_value js_start_collab(napi_env env, napi_callback_info info) {
     napi_value argv[4];
     if (!get_args(env, info, 4, argv)) return nullptr;
     mt_engine* e = engine_of(env, argv[0]);
     void* ids;
     size_t n;
-    int32_t mn, cur;
-    if (!e || !view_of(env, argv[1], &ids, &n, napi_int32_array) || !i32_of(env, argv[2], &mn) ||
-        !i32_of(env, argv[3], &cur))
-        return nullptr;
-    if ((int64_t)n != mt_engine_ndocs(e)) return throw_status(env, e, MT_E_ARG, "startCollab (one id per doc)");
-    int32_t rc = mt_engine_start_collab(e, (const int32_t*)ids, mn, cur);
-    if (rc) return throw_status(env, e, rc, "mt_engine_start_collab");
+    if (!e || !view_of(env, argv[1], &ids, &n, napi_int32_array)) return nullptr;
+    int64_t nd = mt_engine_ndocs(e);
+    if ((int64_t)n != nd) return throw_status(env, e, MT_E_ARG, "startCollab (one id per doc)");
+    std::vector<int32_t> mins, curs;
+    if (!seqs_of(env, argv[2], nd, &mins) || !seqs_of(env, argv[3], nd, &curs)) return nullptr;
+    int32_t rc = mt_engine_start_collab_docs(e, (const int32_t*)ids, mins.data(), curs.data());
+    if (rc) return throw_status(env, e, rc, "mt_engine_start_collab_docs");
     return nullptr;
 }
 
@@ -291,19 +310,44 @@ static napi_value js_get_length(napi_env env, napi_callback_info info) {
     return num(env, out);
 }
 
-/* getText(h, doc, refSeq, longClient) -> string */
+/* getText(h, doc, refSeq, longClient[, placeholder[, start[, end]]]) -> string: MergeTreeTextHelper.getText
+ * (textSegment.ts:154-186); an undefined placeholder is "", an undefined start / end is getValidRange's
+ * default (mt_engine_get_text_range) */
+static bool opt_undefined(napi_env env, napi_value v) {
+    napi_valuetype t;
+    return napi_typeof(env, v, &t) == napi_ok && (t == napi_undefined || t == napi_null);
+}
 static napi_value js_get_text(napi_env env, napi_callback_info info) {
-    napi_value argv[4];
-    if (!get_args(env, info, 4, argv)) return nullptr;
+    napi_value argv[7];
+    size_t argc = 7;
+    if (napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr) != napi_ok || argc < 4) {
+        napi_throw_type_error(env, nullptr, "missing arguments");
+        return nullptr;
+    }
     mt_engine* e = engine_of(env, argv[0]);
     int64_t doc;
-    int32_t ref, cl;
+    int32_t ref, cl, start = MT_TEXT_DEFAULT, end = MT_TEXT_DEFAULT;
     if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &ref) || !i32_of(env, argv[3], &cl)) return nullptr;
-    int64_t n = mt_engine_get_text(e, doc, ref, cl, nullptr, 0);
-    if (n < 0) return throw_status(env, e, (int32_t)-n, "mt_engine_get_text");
+    std::vector<uint16_t> ph;
+    if (argc > 4 && !opt_undefined(env, argv[4])) {
+        size_t len = 0;
+        if (napi_get_value_string_utf16(env, argv[4], nullptr, 0, &len) != napi_ok) {
+            napi_throw_type_error(env, nullptr, "placeholder: expected a string");
+            return nullptr;
+        }
+        ph.resize(len + 1);
+        NAPI_OK(napi_get_value_string_utf16(env, argv[4], (char16_t*)ph.data(), len + 1, &len));
+        ph.resize(len);
+    }
+    if (argc > 5 && !opt_undefined(env, argv[5]) && !i32_of(env, argv[5], &start)) return nullptr;
+    if (argc > 6 && !opt_undefined(env, argv[6]) && !i32_of(env, argv[6], &end)) return nullptr;
+    const uint16_t* pp = ph.empty() ? nullptr : ph.data();
+    int32_t pl = (int32_t)ph.size();
+    int64_t n = mt_engine_get_text_range(e, doc, ref, cl, pp, pl, start, end, nullptr, 0);
+    if (n < 0) return throw_status(env, e, (int32_t)-n, "mt_engine_get_text_range");
     std::vector<uint16_t> buf((size_t)n + 1);
-    int64_t m = mt_engine_get_text(e, doc, ref, cl, buf.data(), n);
-    if (m < 0) return throw_status(env, e, (int32_t)-m, "mt_engine_get_text");
+    int64_t m = mt_engine_get_text_range(e, doc, ref, cl, pp, pl, start, end, buf.data(), n);
+    if (m < 0) return throw_status(env, e, (int32_t)-m, "mt_engine_get_text_range");
     napi_value s;
     NAPI_OK(napi_create_string_utf16(env, (const char16_t*)buf.data(), (size_t)n, &s));
     return s;
@@ -349,6 +393,21 @@ static napi_value js_get_position(napi_env env, napi_callback_info info) {
     return num(env, out);
 }
 
+/* posFromRelativePos(h, doc, keyId, valueId, before, hasOffset, offset, refSeq, longClient) -> number */
+static napi_value js_pos_from_relpos(napi_env env, napi_callback_info info) {
+    napi_value argv[9];
+    if (!get_args(env, info, 9, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t a[7], out = 0;
+    if (!e || !i64_of(env, argv[1], &doc)) return nullptr;
+    for (int i = 0; i < 7; i++)
+        if (!i32_of(env, argv[2 + i], &a[i])) return nullptr;
+    int32_t rc = mt_engine_pos_from_relative_pos(e, doc, a[0], a[1], a[2], a[3], a[4], a[5], a[6], &out);
+    if (rc) return throw_status(env, e, rc, "mt_engine_pos_from_relative_pos");
+    return num(env, out);
+}
+
 static napi_value js_ndocs(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (!get_args(env, info, 1, argv)) return nullptr;
@@ -372,7 +431,7 @@ static napi_value init(napi_env env, napi_value exports) {
     } fns[] = {{"create", js_create},       {"startCollab", js_start_collab}, {"submit", js_submit},
                {"run", js_run},             {"sync", js_sync},                {"reset", js_reset},
                {"errors", js_errors},       {"digests", js_digests},          {"getLength", js_get_length},
-               {"getText", js_get_text},    {"getContainingSegment", js_get_containing},
+               {"getText", js_get_text}, {"posFromRelativePos", js_pos_from_relpos},    {"getContainingSegment", js_get_containing},
                {"getPosition", js_get_position}, {"ndocs", js_ndocs},        {"lastRunMs", js_last_run_ms},
                {"deltas", js_deltas},       {"refPositions", js_ref_positions}};
     for (auto& f : fns) {

@@ -21,6 +21,9 @@ OP_RELOAD, OP_COLLAB, OP_APPEND = 5, 6, 7  # snapshot load records (mt_oplog.h)
 OPF_LOCAL = 0x80
 OPF_GROUPED = 0x40
 SEG_TEXT, SEG_MARKER, SEG_PERM = 0, 1, 2
+SEG_RELPOS = 0x80  # seg_kind flag: positions relative to markers (mt_oplog.h MT_SEG_RELPOS)
+RELPOS_UNITS = 10  # MT_RELPOS_UNITS
+MARKER_ID_KEY = "markerId"  # reservedMarkerIdKey (merge-tree properties / mergeTree.ts getId)
 CLIENT_NONCOLLAB = 0xFFFF
 _SEGMENT_KINDS = (OP_INSERT, OP_RELOAD, OP_APPEND)
 COMBINE_NONE, COMBINE_REWRITE = 0, 1
@@ -239,6 +242,29 @@ class DocLog:
             pos2, tlen = tlen, 0  # load records carry the length in pos2 (mt_oplog.h)
         pidx = self._props(props, combining)
         self.ops.append((kind, seg_kind, client, seq, ref_seq, min_seq, pos1, pos2, toff, tlen, pidx))
+
+    def add_relative(self, kind: int, rel1: Optional[tuple] = None, rel2: Optional[tuple] = None, **kw) -> None:
+        """One sequenced op record whose pos1 / pos2 are IRelativePosition (ops.ts:56-61) instead: rel =
+        (marker id, before, offset or None); the MT_RELPOS_UNITS spec follows the record's text in the text
+        pool (mt_oplog.h MT_SEG_RELPOS)."""
+        self.add(kind, **kw)
+        r = list(self.ops[-1])
+        if kind & 7 == OP_INSERT and r[1] == SEG_TEXT:
+            assert r[8] + r[9] == len(self.text)
+        else:
+            r[8], r[9] = len(self.text), 0
+        u = [self.interner.key(MARKER_ID_KEY), (1 if rel1 else 0) | (2 if rel2 else 0)]
+        for rel in (rel1, rel2):
+            if rel is None:
+                u += [0, 0, 0, 0]
+                continue
+            mid, before, off = rel
+            o = 0 if off is None else int(off) & 0xFFFFFFFF
+            u += [self.interner.value(mid) & 0xFFFF, (1 if before else 0) | (0 if off is None else 2), o & 0xFFFF,
+                  o >> 16]
+        self.text.extend(u)
+        r[1] |= SEG_RELPOS
+        self.ops[-1] = tuple(r)
 
     def arrays(self):
         ops = np.array(self.ops, dtype=OP_DTYPE) if self.ops else np.zeros(0, OP_DTYPE)

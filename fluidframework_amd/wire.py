@@ -9,8 +9,10 @@ minSeq. The records then go to the engine like any other batch (mt_engine_submit
 
 Supported segment specs: a string, `{text, props}`, `{marker: {refType}, props}` (textSegment.ts,
 mergeTree.ts:690-708) and `[length, start]` PermutationSegment rows (matrix permutationvector.ts:
-75-77). Positions must be absolute (`pos1`/`pos2`); `relativePos1/2` and combining ops other than
-`rewrite` raise ValueError (not on the path).
+75-77). `relativePos1/2` (IRelativePosition {id, before, offset}, ops.ts:56-61) become MT_SEG_RELPOS records that the
+engine resolves as Client.getValidOpRange does (posFromRelativePos under the op's refSeq and client); they
+need an engine with the client-feature build (caps.dcap or caps.rcap > 0). Combining ops other than
+`rewrite` raise ValueError.
 """
 from __future__ import annotations
 
@@ -22,30 +24,46 @@ from . import oplog as ol
 MSG_OP = "op"  # MessageType.Operation (protocol-definitions protocol.ts:16)
 
 
+def _rel(r: Optional[Dict[str, Any]]) -> Optional[tuple]:
+    if r is None:
+        return None
+    if not isinstance(r.get("id"), str):
+        raise ValueError("a relative position needs a marker id")
+    return (r["id"], bool(r.get("before")), r.get("offset"))
+
+
 def _op_record(log: ol.DocLog, kind: int, op: Dict[str, Any], common: Dict[str, int]) -> None:
     t = op["type"]
-    if "relativePos1" in op or "relativePos2" in op:
-        raise ValueError("relative positions are not supported")
+    # getValidOpRange (client.ts:486-503): an absolute position wins over a relative one
+    r1 = _rel(op.get("relativePos1")) if op.get("pos1") is None else None
+    r2 = _rel(op.get("relativePos2")) if op.get("pos2") is None else None
+    if r1 is not None or r2 is not None:
+        def add(k, **kw):
+            log.add_relative(k, r1, r2, **kw)
+    else:
+        add = log.add
+    p1 = 0 if r1 is not None else op.get("pos1")
+    p2 = 0 if r2 is not None else op.get("pos2")
     if t == ol.OP_INSERT:
         seg = op["seg"]
         if isinstance(seg, str):
-            log.add(kind, pos1=op["pos1"], text=seg, **common)
+            add(kind, pos1=p1, text=seg, **common)
         elif isinstance(seg, list):
-            log.add(kind, pos1=op["pos1"], perm=int(seg[0]), **common)
+            add(kind, pos1=p1, perm=int(seg[0]), **common)
         elif "marker" in seg:
-            log.add(kind, pos1=op["pos1"], marker=seg["marker"]["refType"], props=seg.get("props"), **common)
+            add(kind, pos1=p1, marker=seg["marker"]["refType"], props=seg.get("props"), **common)
         elif "text" in seg:
-            log.add(kind, pos1=op["pos1"], text=seg["text"], props=seg.get("props"), **common)
+            add(kind, pos1=p1, text=seg["text"], props=seg.get("props"), **common)
         else:
             raise ValueError(f"unsupported segment spec {seg!r}")
     elif t == ol.OP_REMOVE:
-        log.add(kind, pos1=op["pos1"], pos2=op["pos2"], **common)
+        add(kind, pos1=p1, pos2=p2, **common)
     elif t == ol.OP_ANNOTATE:
         comb = op.get("combiningOp")
         if comb is not None and comb.get("name") != "rewrite":
             raise ValueError(f"combining op {comb.get('name')!r} is not supported")
-        log.add(kind, pos1=op["pos1"], pos2=op["pos2"], props=op["props"],
-                combining=ol.COMBINE_REWRITE if comb is not None else ol.COMBINE_NONE, **common)
+        add(kind, pos1=p1, pos2=p2, props=op["props"],
+            combining=ol.COMBINE_REWRITE if comb is not None else ol.COMBINE_NONE, **common)
     else:
         raise ValueError(f"unsupported merge-tree op type {t}")
 

@@ -57,6 +57,11 @@ const char* mt_engine_last_error(const mt_engine* e);
 /* Client.startOrUpdateCollaboration(longClientId, minSeq, currentSeq) for every doc
  * (client.ts:1053-1073); local_long_ids[d] is doc d's own long-client index. */
 int32_t mt_engine_start_collab(mt_engine* e, const int32_t* local_long_ids, int32_t min_seq, int32_t cur_seq);
+/* The same with each document's own minSeq and currentSeq (client.ts:1053-1073 per replica): a
+ * batch of documents that join collaboration at different points of their streams (e.g. loaded from
+ * summaries taken at different sequence numbers). Reset returns every document to these. */
+int32_t mt_engine_start_collab_docs(mt_engine* e, const int32_t* local_long_ids, const int32_t* min_seqs,
+                                    const int32_t* cur_seqs);
 
 /* Stage a batch of per-doc event streams (host memory; copied to HBM). Doc d's events are
  * ops[op_off[d] .. op_off[d+1]), its pools start at text+text_off[d], props+props_off[d],
@@ -102,6 +107,16 @@ int32_t mt_engine_get_length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t
  * local view. Returns the length in UTF-16 units (writes at most cap), <0 on error. */
 int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, uint16_t* out,
                            int64_t cap);
+/* MergeTreeTextHelper.getText(refSeq, clientId, placeholder, start, end) (textSegment.ts:154-186): the text
+ * of [start, end) under the perspective (getValidRange: MT_TEXT_DEFAULT start = 0, end = getLength), every
+ * visited non-text segment (marker, permutation segment) adding `placeholder` cachedLength times
+ * (gatherText 188-271; placeholder_len 0 = ""). JavaScript substring rules apply to a text segment's
+ * piece (an end before the start swaps them). The placeholder "*" (Marker.toString()) returns
+ * -MT_E_UNSUPPORTED. Returns the length in UTF-16 units (writes at most cap), <0 on error. */
+#define MT_TEXT_DEFAULT INT32_MIN
+int64_t mt_engine_get_text_range(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client,
+                                 const uint16_t* placeholder, int32_t placeholder_len, int32_t start, int32_t end,
+                                 uint16_t* out, int64_t cap);
 /* A segment handle (the reference returns live ISegment objects, mergeTree.ts:87-117): the row's
  * stable id and its generation. A handle stops resolving once zamboni merges the row into its
  * neighbour or unlinks it (mergeTree.ts:1322-1398), as a detached reference segment would. */
@@ -121,6 +136,14 @@ int32_t mt_engine_get_containing_segment(mt_engine* e, int64_t doc, int32_t pos,
  * MT_E_ARG if the handle no longer resolves. long_client < 0 = Client.getPosition (client.ts:291). */
 int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t gen, int32_t ref_seq,
                                int32_t long_client, int32_t* out);
+/* MergeTree.posFromRelativePos(relativePos, refSeq, clientId) (mergeTree.ts:1976-1999; Client.posFromRelativePos
+ * client.ts:308, SharedString.insertTextRelative / insertMarkerRelative): the position of the marker whose
+ * property id_key (the interned "markerId" key) holds id_value, after it (+ cachedLength + offset) or before
+ * it (- offset); *out = -1 if no marker holds the id; MT_E_UNSUPPORTED if several do. long_client < 0 = the
+ * local view. */
+int32_t mt_engine_pos_from_relative_pos(mt_engine* e, int64_t doc, int32_t id_key, int32_t id_value, int32_t before,
+                                        int32_t has_offset, int32_t offset, int32_t ref_seq, int32_t long_client,
+                                        int32_t* out);
 /* Delta events (mt_oplog.h MT_DELTA_*; engines created with caps.dcap > 0): the stream a
  * SharedString "sequenceDelta" + "maintenance" listener would see (sequence.ts:136-150), batched.
  * mt_engine_delta_state: per doc the words emitted since create/reset (n_out, may exceed dcap) and

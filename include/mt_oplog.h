@@ -79,6 +79,14 @@ enum {
  * member record per regenerated op (a NOOP if there are none). REF, ATREF and REGEN records need the
  * client-feature build (caps.rcap or caps.dcap > 0); other engines latch MT_E_UNSUPPORTED. */
 #define MT_OPF_REGEN 0x10
+/* A record with MT_OPF_TREE (kind INSERT / REMOVE / ANNOTATE, without MT_OPF_LOCAL) is a MergeTree-level
+ * call with explicit (refSeq, clientId, seq): MergeTree.insertSegments (mergeTree.ts:2001-2031),
+ * markRangeRemoved (2640-2738, overwrite = false) or annotateRange (2598-2638) of the one segment / range
+ * the record holds — client = MT_CLIENT_LOCAL for LocalClientId (constants.ts:14), seq = -1
+ * (UnassignedSequenceNumber) for a local pending op. No ack, no getValidOpRange, no updateSeqNumbers: the
+ * caller owns the collaboration window, as the reference's Client does around these calls. */
+#define MT_OPF_TREE 0x20
+#define MT_CLIENT_LOCAL 0xFFFE /* LocalClientId (constants.ts:14) in an MT_OPF_TREE record */
 
 /* segment kinds */
 enum {
@@ -87,6 +95,18 @@ enum {
     MT_SEG_PERM = 2,   /* PermutationSegment (matrix permutationvector.ts:36-122): length =
                           text_len, no text, handle unallocated; any two such rows can append */
 };
+
+/* seg_kind bit: the record's positions are relative to markers (IRelativePosition, ops.ts:56-61;
+ * Client.getValidOpRange client.ts:486-503 resolves them with MergeTree.posFromRelativePos, mergeTree.ts:
+ * 1976-1999, under the op's refSeq and client). The spec follows the record's text in the text pool, at
+ * text_off + text_len: MT_RELPOS_UNITS UTF-16 units {key id of the marker-id property ("markerId",
+ * reservedMarkerIdKey), which (bit 0: pos1, bit 1: pos2 is relative), then per position {value id of the
+ * marker id, bits (bit 0: before, bit 1: offset present), offset low 16, offset high 16}}. Sequenced
+ * records only, in the client-feature build (caps.dcap or caps.rcap > 0; other engines latch
+ * MT_E_UNSUPPORTED), as are a marker id held by more than one marker and one no marker holds (the
+ * reference computes -1, or a position from an unlinked segment's stale parent). */
+#define MT_SEG_RELPOS 0x80
+#define MT_RELPOS_UNITS 10
 
 /* combining ops for annotate (ops.ts ICombiningOp); only none and "rewrite" are supported */
 enum {

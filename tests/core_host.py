@@ -40,6 +40,9 @@ def lib():
         L.mth_length_local.argtypes = [vp, i64]
         L.mth_text.argtypes = [vp, i64, i32, i32, vp, i64]
         L.mth_text.restype = i64
+        L.mth_text_range.argtypes = [vp, i64, i32, i32, vp, i32, i32, i32, vp, i64]
+        L.mth_text_range.restype = i64
+        L.mth_pos_from_relpos.argtypes = [vp, i64, i32, i32, i32, i32, i32, i32, i32, vp]
         L.mth_dump.argtypes = [vp, i64, vp, i64]
         L.mth_dump.restype = i64
         L.mth_digest.argtypes = [vp, i64]
@@ -101,6 +104,25 @@ class HostStore:
         buf = np.zeros(max(n, 1), "<u2")
         self.L.mth_text(self.h, doc, ref_seq, long_client, _p(buf), n)
         return buf[:n].tobytes().decode("utf-16-le")
+
+    def text_range(self, doc, ref_seq=0, long_client=-1, placeholder="", start=None, end=None) -> str:
+        """MergeTreeTextHelper.getText(refSeq, clientId, placeholder, start, end); None = default range end"""
+        ph = np.frombuffer(placeholder.encode("utf-16-le"), "<u2").copy() if placeholder else np.zeros(1, "<u2")
+        pl = len(placeholder.encode("utf-16-le")) // 2
+        a = -(1 << 31) if start is None else start
+        b = -(1 << 31) if end is None else end
+        n = self.L.mth_text_range(self.h, doc, ref_seq, long_client, _p(ph), pl, a, b, None, 0)
+        buf = np.zeros(max(n, 1), "<u2")
+        self.L.mth_text_range(self.h, doc, ref_seq, long_client, _p(ph), pl, a, b, _p(buf), n)
+        return buf[:n].tobytes().decode("utf-16-le")
+
+    def pos_from_relative_pos(self, doc, key_id, value_id, before=False, offset=None, ref_seq=0, long_client=-1):
+        out = np.zeros(1, np.int32)
+        rc = self.L.mth_pos_from_relpos(self.h, doc, key_id, value_id, int(before), offset is not None, offset or 0,
+                                        ref_seq, long_client, _p(out))
+        if rc:
+            raise RuntimeError("several markers hold the id")
+        return int(out[0])
 
     def containing(self, doc, pos, ref_seq=0, long_client=-1):
         out = np.zeros(6, np.int32)

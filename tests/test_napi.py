@@ -104,3 +104,39 @@ def test_known_answers_through_node():
     # type-erased reference gives these values
     assert (out["refBefore"], out["refSlid"], out["refText"], out["refAfterInsert"]) == (6, 5, "helloXrld", 6)
     assert out["regen"] == [{"type": 0, "pos1": 5, "length": 1}]
+
+
+@pytest.mark.gpu
+def test_merge_tree_calls_text_ranges_and_per_doc_seqs_through_node():
+    """tests/napi_kat2.js: MergeTree-level calls with explicit (refSeq, clientId, seq), per-document minSeq /
+    currentSeq at collaboration start and getText with placeholder / start / end, through node -> addon ->
+    GPU; the answers are the type-erased reference's for the same steps (tools/make_napi_kat2.mjs)"""
+    native.build_napi()
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "napi_kat2.js")], capture_output=True, text=True,
+                       cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "napi_kat2_expected.json")))
+    assert out["answers"] == want
+    assert out["starUnsupported"]  # the "*" placeholder (Marker.toString()) is not modelled
+
+
+def test_typings_declare_every_export_and_method():
+    """fluidframework_amd/js/mergetree_gpu.d.ts declares every name the facade exports and every public method
+    of its classes (no TypeScript compiler in this image: a textual check)"""
+    import re
+    js = open(os.path.join(ROOT, "fluidframework_amd", "js", "mergetree_gpu.js")).read()
+    dts = open(os.path.join(ROOT, "fluidframework_amd", "js", "mergetree_gpu.d.ts")).read()
+    exports = re.search(r"module\.exports = \{([^}]*)\}", js, re.S).group(1)
+    names = [n.strip() for n in exports.replace("\n", " ").split(",") if n.strip()]
+    for n in names:
+        assert re.search(rf"\b(class|const|function) {n}\b", dts), f"{n} is not declared in the typings"
+    for cls in ("ReplayEngine", "GpuClient", "GpuMergeTree"):
+        body = js[js.index(f"class {cls} "):]
+        body = body[: body.index("\n}\n")]
+        methods = set(re.findall(r"^    (?:get )?([a-zA-Z]\w*)\(", body, re.M)) - {"constructor", "if", "for"}
+        dbody = dts[dts.index(f"class {cls} "):]
+        dbody = dbody[: dbody.index("\n}\n")]
+        internal = {"enqueue", "propsRecord", "checkDoc", "fields", "sent", "read"}
+        for m in methods - internal:
+            assert re.search(rf"\b{m}\b", dbody), f"{cls}.{m} is not declared in the typings"

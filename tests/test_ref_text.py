@@ -1,0 +1,90 @@
+"""getText with placeholder / start / end (MergeTreeTextHelper.getText, textSegment.ts:154-271) against the
+REFERENCE (tests/golden/reftext_*.npz, tools/make_ref_goldens.py --texts).
+
+The reference replays each fixture log (config-3 logs with Marker inserts, tests/text_markers.py, and
+config-5 PermutationSegment logs) and answers getText(refSeq, clientId, placeholder, start, end) for the
+local view under the placeholders "", "#" and "<>" — the default range, inner ranges, an empty range, an
+end before the start (JavaScript substring swaps them), a negative start, an end past the text — and for
+the current-seq views of two remote clients. The host build of the engine core and the HIP engine must give
+every answer (length + FNV-1a-64 of its UTF-16LE units; document 0's answers in full)."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import gen
+import core_host
+import text_markers
+from make_goldens_sha import log_sha
+from test_ref_goldens import caps_for
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NAMES = [os.path.basename(f)[8:-4] for f in sorted(glob.glob(os.path.join(GOLDEN, "reftext_*.npz")))]
+DEFAULT = -(1 << 31)
+
+
+def fnv1a64(bs: bytes) -> int:
+    h = 0xCBF29CE484222325
+    for x in bs:
+        h = ((h ^ x) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def load(name):
+    z = np.load(os.path.join(GOLDEN, f"reftext_{name}.npz"), allow_pickle=False)
+    w = gen.Workload(**json.loads(str(z["workload"])))
+    b = gen.generate(w, ids=z["doc_ids"], threads=8)
+    if bool(z["markers"]):
+        b = text_markers.with_markers(b)
+    assert log_sha(b) == str(z["log_sha256"]), "the logs differ from the fixture's"
+    return z, w, b
+
+
+def check(z, answer):
+    """answer(doc, ref_seq, long_client, placeholder, start, end) -> str for every fixture query"""
+    q, ph = z["queries"], z["placeholders"]
+    doc0 = []
+    bad = []
+    for i in range(len(q)):
+        d, rs, cl, a, e = (int(x) for x in q[i])
+        t = answer(d, rs, cl, str(ph[i]), None if a == DEFAULT else a, None if e == DEFAULT else e)
+        u = t.encode("utf-16-le")
+        if len(t) != int(z["lengths"][i]) or fnv1a64(u) != int(z["fnv"][i]):
+            bad.append(i)
+        if d == 0:
+            doc0.append(u)
+    assert not bad, f"{len(bad)} of {len(q)} getText answers differ from the reference, e.g. query {q[bad[0]]}"
+    assert b"".join(doc0) == z["doc0_units"].tobytes()
+
+
+def test_text_fixture_sets():
+    assert set(NAMES) >= {"c3_markers", "c5_perm"}
+    z = np.load(os.path.join(GOLDEN, "reftext_c3_markers.npz"))
+    # the fixture exercises the placeholders and the substring edge cases
+    assert {str(p) for p in z["placeholders"]} == {"", "#", "<>"}
+    q = z["queries"]
+    assert ((q[:, 3] != DEFAULT) & (q[:, 4] != DEFAULT) & (q[:, 3] > q[:, 4])).any()
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_host_core_get_text_matches_reference(name):
+    z, w, b = load(name)
+    c = caps_for(w)
+    _, err, st = core_host.replay_batch(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
+    assert (err == 0).all()
+    check(z, lambda d, rs, cl, ph, a, e: st.text_range(d, rs, cl, ph, a, e))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_get_text_matches_reference(name):
+    from fluidframework_amd.engine import Engine
+    z, w, b = load(name)
+    eng = Engine(b.ndocs, **caps_for(w))
+    eng.start_collab(b.local_long_id)
+    eng.replay(b)
+    err, _ = eng.errors()
+    assert (err == 0).all()
+    check(z, lambda d, rs, cl, ph, a, e: eng.get_text(d, rs, cl, ph, a, e))

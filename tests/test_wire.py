@@ -114,8 +114,9 @@ def test_unsupported_wire_ops_raise():
     log = ol.DocLog(ol.Interner())
     base = {"clientId": "a", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
             "type": "op"}
-    with pytest.raises(ValueError):
-        wire.add_message(log, dict(base, contents={"type": 1, "relativePos1": {"id": "m"}, "pos2": 3}), wire.ClientNames())
+    with pytest.raises(ValueError):  # a relative position names a marker id
+        wire.add_message(log, dict(base, contents={"type": 1, "relativePos1": {"before": True}, "pos2": 3}),
+                         wire.ClientNames())
     with pytest.raises(ValueError):
         wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
                                                    "combiningOp": {"name": "incr"}}), wire.ClientNames())
@@ -137,3 +138,53 @@ def test_gpu_wire_ingestion_matches_reference(name):
     err, _ = eng.errors()
     assert (err == 0).all()
     assert (eng.digests() == z["digests"]).all()
+
+
+def test_wire_relative_positions_rebuild_the_fixture_logs():
+    """messages with relativePos1 / relativePos2 (the reference fixture logs of tests/test_ref_relpos.py, turned
+    back into wire JSON) ingest to the very records the fixture replays (mt_oplog.h MT_SEG_RELPOS)"""
+    import relpos_logs
+    b, interner, _ = relpos_logs.build(3, 300, 7)
+    for d in range(b.ndocs):
+        ops, text, props, kv = b.doc(d)
+        names = wire.ClientNames([f"c{i}" for i in range(8)])
+        log = ol.DocLog(interner, local_long_id=0)
+        for r in ops:
+            k = int(r["kind"]) & 7
+            c = {"type": k}
+            if k == ol.OP_INSERT:
+                sk = int(r["seg_kind"]) & 0x7F
+                if sk == ol.SEG_MARKER:
+                    c["seg"] = {"marker": {"refType": int(r["pos2"])}}
+                else:
+                    c["seg"] = text[int(r["text_off"]): int(r["text_off"]) + int(r["text_len"])].tobytes().decode("utf-16-le")
+                c["pos1"] = int(r["pos1"])
+            else:
+                c["pos1"], c["pos2"] = int(r["pos1"]), int(r["pos2"])
+            if r["props"]:
+                pr = props[int(r["props"]) - 1]
+                pset = {interner.key_str(int(x["key"])): interner.value_obj(int(x["value"]))
+                        for x in kv[int(pr["kv_off"]): int(pr["kv_off"]) + int(pr["nkv"])]}
+                if k == ol.OP_INSERT:
+                    c["seg"] = {"marker": c["seg"]["marker"], "props": pset} if isinstance(c["seg"], dict) else \
+                        {"text": c["seg"], "props": pset}
+                else:
+                    c["props"] = pset
+            if int(r["seg_kind"]) & ol.SEG_RELPOS:
+                u = text[int(r["text_off"]) + int(r["text_len"]):][: ol.RELPOS_UNITS].astype(np.int64)
+                for which, base, key in ((1, 2, "relativePos1"), (2, 6, "relativePos2")):
+                    if u[1] & which:
+                        rp = {"id": interner.value_obj(int(u[base]))}
+                        if u[base + 1] & 1:
+                            rp["before"] = True
+                        if u[base + 1] & 2:
+                            rp["offset"] = int(np.int32(np.uint32(int(u[base + 2]) | (int(u[base + 3]) << 16))))
+                        c[key] = rp
+                        c.pop("pos1" if which == 1 else "pos2")
+            msg = {"clientId": f"c{int(r['client'])}", "sequenceNumber": int(r["seq"]),
+                   "referenceSequenceNumber": int(r["ref_seq"]), "minimumSequenceNumber": int(r["min_seq"]),
+                   "type": "op", "contents": c}
+            wire.add_message(log, msg, names)
+        o2, t2, _, _ = log.arrays()
+        assert np.array_equal(o2, ops)
+        assert np.array_equal(t2[: len(t2)], text[: len(t2)])

@@ -341,6 +341,151 @@ def make_refs(names, node: str) -> None:
               f"references, {npast} of them past their segment's end", flush=True)
 
 
+TEXT_SETS = {"c3_markers": (gen.config3(1500), list(range(24))), "c5_perm": (gen.config5(1500), list(range(16)))}
+
+
+def text_queries(b, seed: int):
+    """getText queries per document: the local view under every placeholder ("", "#", "<>") with the default
+    range, inside ranges, an empty range, a range whose end precedes its start (JavaScript substring swaps
+    the ends), a negative start and an end past the text; plus the current-seq views of two remote clients.
+    Lengths are not known here, so ranges are drawn up to 4,000 and the reference clips them."""
+    q = []
+    rng = np.random.default_rng(seed)
+    for d in range(b.ndocs):
+        ops = b.doc(d)[0]
+        seq = int(ops["seq"][(ops["kind"] & 0x80) == 0].max())
+        for ph in ("", "#", "<>"):
+            q.append([d, 0, -1, ph, None, None])
+            for _ in range(2):
+                a, e = sorted(int(x) for x in rng.integers(0, 1500, 2))
+                q.append([d, 0, -1, ph, a, e])
+            a = int(rng.integers(0, 1500))
+            q.append([d, 0, -1, ph, a, a])
+            q.append([d, 0, -1, ph, a + 40, a])
+            q.append([d, 0, -1, ph, -5, int(rng.integers(0, 1500))])
+            q.append([d, 0, -1, ph, int(rng.integers(0, 1500)), 4000])
+        clients = sorted({int(c) for c in ops["client"][(ops["kind"] & 0x80) == 0]} - {int(b.local_long_id[d])})
+        for c in clients[:2]:
+            q.append([d, seq, c, "#", None, None])
+            a, e = sorted(int(x) for x in rng.integers(0, 1500, 2))
+            q.append([d, seq, c, "", a, e])
+    return q
+
+
+def make_texts(node: str) -> None:
+    """tests/golden/reftext_<set>.npz: MergeTreeTextHelper.getText(refSeq, clientId, placeholder, start, end)
+    of the reference after each document's replay (tools/ref_replay.mjs textqueries.json), for logs with
+    markers (tests/text_markers.py: remote length-1 text inserts made Marker inserts) and PermutationSegment
+    logs. Stored: the queries, each answer's length and FNV-1a-64 over its UTF-16LE units, and the answers
+    of document 0 in full."""
+    import text_markers
+    for name, (w, ids) in TEXT_SETS.items():
+        b = gen.generate(w, ids=ids, threads=8)
+        if name == "c3_markers":
+            b = text_markers.with_markers(b)
+        q = text_queries(b, 4242)
+        d = os.path.join(SCRATCH, name + "_text")
+        write_batch(b, gen.generator_interner(), d)
+        with open(os.path.join(d, "textqueries.json"), "w") as f:
+            json.dump(q, f)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d], capture_output=True,
+                           text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+        errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
+        if errs:
+            raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
+        texts = json.load(open(os.path.join(d, "ref_texts.json")))
+        assert len(texts) == len(q)
+        units = [t.encode("utf-16-le") for t in texts]
+        qa = np.asarray([[x[0], x[1], x[2], -(1 << 31) if x[4] is None else x[4], -(1 << 31) if x[5] is None else x[5]]
+                         for x in q], np.int32)
+        blob = np.frombuffer(b"".join(u for (x, u) in zip(q, units) if x[0] == 0), np.uint8)
+        np.savez_compressed(
+            os.path.join(GOLDEN, f"reftext_{name}.npz"),
+            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(b),
+            markers=name == "c3_markers", queries=qa, placeholders=np.asarray([x[3] for x in q]),
+            lengths=np.asarray([len(t) for t in texts], np.int64),
+            fnv=np.asarray([fnv1a64(u) for u in units], np.uint64), doc0_units=blob,
+            source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                    "tools/ref_replay.mjs: MergeTreeTextHelper.getText after each document's replay"),
+        )
+        print(f"reftext_{name}: {b.ndocs} docs, {len(q)} queries, {sum(len(t) for t in texts)} units", flush=True)
+
+
+TREE_SETS = ("c3_lagged", "c5_perm")
+
+
+def make_tree(node: str) -> None:
+    """tests/golden/reftree_<set>.npz: logs with MergeTree-level records (tests/tree_ops.py, mt_oplog.h
+    MT_OPF_TREE: MergeTree.insertSegments / markRangeRemoved / annotateRange with explicit refSeq, clientId,
+    seq) replayed by the reference; its digests, which must also equal the reference's digests of the
+    unconverted logs (the conversion calls what the Client itself calls)."""
+    import tree_ops
+    for name in TREE_SETS:
+        w, ids = SETS[name]
+        b = tree_ops.to_tree_ops(gen.generate(w, ids=ids, threads=8))
+        dumps, info, secs, _ = run_reference(b, os.path.join(SCRATCH, name + "_tree"), node)
+        digests = np.asarray([fnv1a64(x) for x in dumps], np.uint64)
+        orig = np.load(os.path.join(GOLDEN, f"ref_{name}.npz"))["digests"]
+        if not np.array_equal(digests, orig):
+            raise RuntimeError(f"{name}: the reference's digests of the MergeTree-level logs differ from its own "
+                               f"digests of the Client-level logs on {int((digests != orig).sum())} docs")
+        ntree = int(((b.ops["kind"] & tree_ops.OPF_TREE) != 0).sum())
+        np.savez_compressed(
+            os.path.join(GOLDEN, f"reftree_{name}.npz"),
+            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(b),
+            digests=digests, ntree=ntree,
+            source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                    "tools/ref_replay.mjs: MergeTree.insertSegments / markRangeRemoved / annotateRange records"),
+        )
+        print(f"reftree_{name}: {b.ndocs} docs, {ntree} MergeTree-level records, digests equal the Client-level "
+              f"logs' on every document", flush=True)
+
+
+def make_relpos(node: str) -> None:
+    """tests/golden/refrelpos.npz: logs whose ops name positions relative to markers (tests/relpos_logs.py,
+    mt_oplog.h MT_SEG_RELPOS; Client.getValidOpRange resolves them with MergeTree.posFromRelativePos)
+    replayed by the reference: its digests, and Client.posFromRelativePos of the live marker ids (before /
+    after, with and without offsets) and of an id no marker holds, after each document's replay."""
+    import relpos_logs
+    b, interner, live = relpos_logs.build(24, 600, 7)
+    d = os.path.join(SCRATCH, "relpos")
+    rng = np.random.default_rng(99)
+    q = []
+    for i in range(b.ndocs):
+        ids = live[i]
+        pick = [ids[int(k)] for k in rng.choice(len(ids), size=min(6, len(ids)), replace=False)] if ids else []
+        for mid in pick:
+            q += [[i, mid, False, None], [i, mid, True, None], [i, mid, False, int(rng.integers(0, 5))],
+                  [i, mid, True, int(rng.integers(0, 5))]]
+        q.append([i, "no-such-marker", False, None])
+    write_batch(b, interner, d)
+    with open(os.path.join(d, "relqueries.json"), "w") as f:
+        json.dump(q, f)
+    r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+    errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
+    if errs:
+        raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
+    blob = np.fromfile(os.path.join(d, "ref_dumps.bin"), np.uint8)
+    off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
+    digests = np.asarray([fnv1a64(blob[off[i]: off[i + 1]].tobytes()) for i in range(b.ndocs)], np.uint64)
+    ans = json.load(open(os.path.join(d, "ref_relpos.json")))
+    nrel = int(((b.ops["seg_kind"] & relpos_logs.SEG_RELPOS) != 0).sum())
+    np.savez_compressed(
+        os.path.join(GOLDEN, "refrelpos.npz"), ndocs=b.ndocs, nmsg=600, seed=7, log_sha256=log_sha(b),
+        digests=digests, nrel=nrel, q_doc=np.asarray([x[0] for x in q], np.int32), q_id=np.asarray([x[1] for x in q]),
+        q_before=np.asarray([x[2] for x in q]), q_offset=np.asarray([-1 if x[3] is None else x[3] for x in q], np.int32),
+        answers=np.asarray(ans, np.int32),
+        source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                "tools/ref_replay.mjs: relativePos1/relativePos2 ops through Client.applyMsg, posFromRelativePos"),
+    )
+    print(f"refrelpos: {b.ndocs} docs, {nrel} ops with relative positions, {len(q)} posFromRelativePos queries",
+          flush=True)
+
+
 REGEN_SETS = ("c1_farm", "c3_lagged", "c3_lagged_long", "c5_perm")
 
 
@@ -441,8 +586,20 @@ def main() -> None:
     ap.add_argument("--refs", action="store_true", help="write the local-reference fixtures (refrefs_*.npz) only")
     ap.add_argument("--regen", action="store_true", help="write the reconnect fixtures (refregen_*.npz) only")
     ap.add_argument("--legacy", action="store_true", help="write the legacy-summary fixtures (reflegacy_*.npz) only")
+    ap.add_argument("--texts", action="store_true", help="write the getText fixtures (reftext_*.npz) only")
+    ap.add_argument("--relpos", action="store_true", help="write the relative-position fixture (refrelpos.npz) only")
+    ap.add_argument("--tree", action="store_true", help="write the MergeTree-level record fixtures (reftree_*.npz) only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
+    if args.texts:
+        make_texts(args.node)
+        return
+    if args.tree:
+        make_tree(args.node)
+        return
+    if args.relpos:
+        make_relpos(args.node)
+        return
     if args.legacy:
         make_legacy([n for n in args.sets.split(",") if n in LEGACY_SETS], args.node)
         return

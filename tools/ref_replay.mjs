@@ -74,6 +74,23 @@ function record(i) {
 
 // the wire op (IMergeTreeOp, ops.ts:63-102) a record stands for
 function wireOp(doc, rec) {
+    const op = wireOpAbs(doc, { ...rec, seg_kind: rec.seg_kind & 0x7f });
+    if (rec.seg_kind & 0x80) { // MT_SEG_RELPOS: the positions are IRelativePosition objects (mt_oplog.h)
+        const b = 2 * (textOff[doc] + rec.text_off + rec.text_len);
+        const u = (k) => text.readUInt16LE(b + 2 * k);
+        const which = u(1);
+        const rel = (k) => {
+            const r = { id: JSON.parse(values[u(k) & ~FALSY]) };
+            if (u(k + 1) & 1) r.before = true;
+            if (u(k + 1) & 2) r.offset = (u(k + 2) | (u(k + 3) << 16)) | 0;
+            return r;
+        };
+        if (which & 1) { delete op.pos1; op.relativePos1 = rel(2); }
+        if (which & 2) { delete op.pos2; op.relativePos2 = rel(6); }
+    }
+    return op;
+}
+function wireOpAbs(doc, rec) {
     const kind = rec.kind & 7;
     const ps = propSet(doc, rec.props);
     if (kind === 0) {
@@ -122,6 +139,24 @@ function applyRange(client, doc, from, to) {
                 const groups = client.peekPendingSegmentGroups(ops.length);
                 const gs = ops.length === 1 ? [groups] : groups;
                 ops.forEach((o, i) => pendingOps.push({ op: o, group: gs[i] }));
+            }
+            continue;
+        }
+        if (rec.kind & 0x20) { // MT_OPF_TREE: MergeTree-level call with the record's (refSeq, clientId, seq)
+            const mt = client.mergeTree;
+            const cid = rec.client === 0xFFFE ? -1 : client.getOrAddShortClientId(name(rec.client));
+            const opArgs = { op: wireOp(doc, rec) };
+            const ps = propSet(doc, rec.props);
+            if (kind === 0) {
+                const seg = rec.seg_kind === 2 ? new PermutationSegment(rec.text_len)
+                    : rec.seg_kind === 1 ? Marker.make(rec.pos2, ps && ps.set) : TextSegment.make(textOf(doc, rec), ps && ps.set);
+                if (rec.seg_kind === 2 && ps) seg.addProperties(ps.set);
+                mt.insertSegments(rec.pos1, [seg], rec.ref_seq, cid, rec.seq, opArgs);
+            } else if (kind === 1) {
+                mt.markRangeRemoved(rec.pos1, rec.pos2, rec.ref_seq, cid, rec.seq, false, opArgs);
+            } else if (kind === 2) {
+                mt.annotateRange(rec.pos1, rec.pos2, ps ? ps.set : {}, ps ? ps.combiningOp : undefined, rec.ref_seq, cid,
+                    rec.seq, opArgs);
             }
             continue;
         }
@@ -428,6 +463,16 @@ const ndocs = opOff.length - 1;
 const qpath = path.join(dir, "queries.json");
 const queries = fs.existsSync(qpath) ? JSON.parse(fs.readFileSync(qpath)) : [];
 const answers = [];
+// optional getText queries (textqueries.json: [[doc, refSeq, longClient | -1 = local view, placeholder,
+// start | null, end | null], ...]): MergeTreeTextHelper.getText (textSegment.ts:154-186) -> ref_texts.json
+const tqpath = path.join(dir, "textqueries.json");
+const textQueries = fs.existsSync(tqpath) ? JSON.parse(fs.readFileSync(tqpath)) : [];
+const texts = [];
+// optional posFromRelativePos queries (relqueries.json: [[doc, markerId, before, offset | null], ...]) in the
+// replica's local view (Client.posFromRelativePos, client.ts:308) -> ref_relpos.json
+const rqpath = path.join(dir, "relqueries.json");
+const relQueries = fs.existsSync(rqpath) ? JSON.parse(fs.readFileSync(rqpath)) : [];
+const relAnswers = [];
 const t0 = process.hrtime.bigint();
 const dumps = [], errs = {};
 for (let d = 0; d < ndocs; d++) {
@@ -454,6 +499,22 @@ for (let d = 0; d < ndocs; d++) {
             const { segment, offset } = mt.getContainingSegment(pos, refSeq, cid);
             answers.push(segment === undefined ? [0, 0, 0, 0, 0, 0] : [1, offset, segment.cachedLength, segment.seq,
                 segment.clientId < 0 ? -1 : longOfName(c.getLongClientId(segment.clientId)), mt.getPosition(segment, refSeq, cid)]);
+        }
+        for (const [qd, ref, cl, ph, st, en] of textQueries) {
+            if (qd !== d) continue;
+            const mt = c.mergeTree;
+            const local = cl < 0;
+            const refSeq = local ? mt.collabWindow.currentSeq : ref;
+            const cid = local ? mt.collabWindow.clientId : c.getOrAddShortClientId(name(cl));
+            const helper = new MT.MergeTreeTextHelper(mt);
+            texts.push(helper.getText(refSeq, cid, ph, st === null ? undefined : st, en === null ? undefined : en));
+        }
+        for (const [qd, id, before, offset] of relQueries) {
+            if (qd !== d) continue;
+            const r = { id };
+            if (before) r.before = true;
+            if (offset !== null) r.offset = offset;
+            relAnswers.push(c.posFromRelativePos(r));
         }
         dumps.push(timeOnly ? Buffer.alloc(0) : dump(c));
     } catch (e) {
@@ -543,6 +604,8 @@ if (Object.keys(refPositions).length) {
 }
 fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
 if (queries.length) fs.writeFileSync(path.join(dir, "ref_answers.json"), JSON.stringify(answers));
+if (textQueries.length) fs.writeFileSync(path.join(dir, "ref_texts.json"), JSON.stringify(texts));
+if (relQueries.length) fs.writeFileSync(path.join(dir, "ref_relpos.json"), JSON.stringify(relAnswers));
 console.log(JSON.stringify({ ndocs, errors: Object.keys(errs).length, seconds: secs }));
 }
 main().catch((e) => { console.error(e); process.exit(1); });
