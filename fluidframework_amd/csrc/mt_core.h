@@ -82,6 +82,7 @@ struct Caps {
     int32_t gcap; /* pending segment groups (local ops in flight) */
     int32_t dcap; /* delta event log words (0 = delta events off; mt_oplog.h MT_DELTA_*) */
     int32_t rcap; /* local references (0 = none; mt_oplog.h MT_OP_REF) */
+    int32_t pcap; /* PermutationVector handle-table entries (0 = none; mt_oplog.h MT_OP_NOOP | MT_OPF_LOCAL) */
 };
 
 /* delta event stream state at the head of a document's delta region (mt_oplog.h) */
@@ -92,6 +93,8 @@ struct alignas(16) DState {
     int32_t on;  /* 0 while a snapshot-load record applies */
     int32_t nref;  /* local references created */
     int32_t ncoll; /* segments holding a LocalReferenceCollection (LColl) */
+    int32_t hlen;  /* PermutationVector's HandleTable: the length of its `handles` array (handletable.ts:23) */
+    int32_t _pad[3];
 };
 /* a local reference (localReference.ts:20-117): the row id of its segment (-1: detached), its offset
  * in the segment and its ReferenceType */
@@ -305,7 +308,7 @@ struct Doc {
     MT_HD static int64_t off_gq(const Caps& c) { return off_mrid(c) + align256c(4 * (int64_t)c.mcap); }
     /* client-feature region (only when c.dcap > 0 or c.rcap > 0): DState, dcap delta-log words, rcap
      * local references */
-    MT_HD static bool has_fx(const Caps& c) { return c.dcap > 0 || c.rcap > 0; }
+    MT_HD static bool has_fx(const Caps& c) { return c.dcap > 0 || c.rcap > 0 || c.pcap > 0; }
     MT_HD static int64_t off_gql(const Caps& c) { return off_gq(c) + align256c(4 * (int64_t)c.gcap); }
     MT_HD static int64_t off_dl(const Caps& c) { return off_gql(c) + align256c(4 * (int64_t)c.gcap); }
     MT_HD static int64_t off_refs(const Caps& c) {
@@ -313,13 +316,19 @@ struct Doc {
     }
     MT_HD static int64_t off_coll(const Caps& c) { return off_refs(c) + (int64_t)sizeof(LRef) * c.rcap; }
     MT_HD static int32_t coll_cap(const Caps& c) { return 4 * c.rcap; }
+    /* PermutationVector's HandleTable (handletable.ts:19-87): handles[0] = the free-list head, then pcap
+     * entries (0 = allocated, else the next free handle) */
+    MT_HD static int64_t off_ht(const Caps& c) {
+        return (off_coll(c) + (int64_t)sizeof(LColl) * coll_cap(c) + 15) & ~(int64_t)15;
+    }
     MT_HD static int64_t stride(const Caps& c) {
-        return has_fx(c) ? align256c(off_coll(c) + (int64_t)sizeof(LColl) * coll_cap(c)) : off_dl(c);
+        return has_fx(c) ? align256c(off_ht(c) + 4 * ((int64_t)c.pcap + 1)) : off_dl(c);
     }
     MT_HD DState* dstate() const { return (DState*)(b + off_dl(caps)); }
     MT_HD int32_t* dlog() const { return (int32_t*)(b + off_dl(caps) + (int64_t)sizeof(DState)); }
     MT_HD LRef* refs() const { return (LRef*)(b + off_refs(caps)); }
     MT_HD LColl* colls() const { return (LColl*)(b + off_coll(caps)); }
+    MT_HD int32_t* ht() const { return (int32_t*)(b + off_ht(caps)); }
     MT_HD typename HT::Cold* cold() const { return (typename HT::Cold*)(b + OFF_COLD); } /* HT::S records */
     MT_HD typename HT::IX* frid() const { return (typename HT::IX*)(b + OFF_FRID); } /* free row-id stack */
     MT_HD uint16_t* arena() const { return (uint16_t*)(b + OFF_ARENA); } /* 2 * acap */
@@ -557,8 +566,85 @@ struct Replica {
             st->on = 1;
             st->nref = 0;
             st->ncoll = 0;
+            st->hlen = 1; /* handles = [1] (handletable.ts:23) */
+            d.ht()[0] = 1;
         }
         w.sync();
+    }
+
+    /* ---- PermutationVector handles (permutationvector.ts:36-122, 157-183, 338-363; handletable.ts) ----
+     * A PermutationSegment row keeps its `start` handle in the cold row's toff (0 = Handle.unallocated:
+     * valid handles are >= 1). The document's HandleTable (off_ht) allocates lazily at
+     * getAllocatedHandle and takes the handles of every unlinked segment back, in the order of the
+     * maintenance callbacks. Client-feature build with caps.pcap > 0 only. */
+    MT_HD bool ht_on() const {
+        if constexpr (DL)
+            return d.caps.pcap > 0;
+        else
+            return false;
+    }
+    /* HandleTable.allocate (handletable.ts:35-40); 0 and E_CAPACITY when the table is full */
+    MT_HD int32_t ht_alloc() {
+        int32_t* t = d.ht();
+        DState* st = d.dstate();
+        int32_t f = t[0], len = st->hlen;
+        if (f > d.caps.pcap) {
+            fail(E_CAPACITY);
+            return 0;
+        }
+        int32_t nx = f < len ? t[f] : f + 1; /* handles[free] ?? free + 1 */
+        w.sync();
+        t[0] = nx;
+        t[f] = 0;
+        if (f >= len) st->hlen = f + 1;
+        w.sync();
+        return f;
+    }
+    /* onMaintenance UNLINK (permutationvector.ts:338-363): HandleTable.free (56-59) of start .. start + len - 1
+     * in increasing order */
+    MT_HD void ht_free_range(int32_t start, int32_t len) {
+        int32_t* t = d.ht();
+        int32_t nx = t[0];
+        w.sync();
+        for (int32_t b = 0; b < len; b += W::N) {
+            int32_t i = b + w.lane();
+            if (i < len) t[start + i] = i == 0 ? nx : start + i - 1;
+        }
+        if (len > 0) t[0] = start + len - 1;
+        w.sync();
+    }
+    /* the handles of a row zamboni unlinks */
+    MT_HD void ht_unlinked(int32_t rid, int32_t len) {
+        if ((int32_t)d.cold()[rid].toff != 0) ht_free_range((int32_t)d.cold()[rid].toff, len);
+    }
+    /* PermutationVector.getAllocatedHandle(pos) (157-183) in the local view: the handle of the row at pos
+     * (getMaybeHandle: start + offset when allocated), else walkSegments(pos, pos + 1, splitRange) splits a
+     * one-row segment out at pos and HandleTable.allocate()s its start */
+    MT_HD void alloc_handle(int32_t pos) {
+        if (!ht_on()) {
+            fail(E_UNSUPPORTED);
+            return;
+        }
+        if (pos < 0 || pos >= h.localLen) { /* assert(0 <= pos && pos < this.getLength()) */
+            fail(E_ASSERT);
+            return;
+        }
+        int32_t off = 0;
+        int32_t s = containing(pos, h.currentSeq, h.localShort, &off);
+        if (s < 0 || !(z.flags(s) & RF_PERM)) {
+            fail(s < 0 ? E_ASSERT : E_UNSUPPORTED);
+            return;
+        }
+        if (cold(s).toff != 0) return; /* isHandleValid(start + offset) */
+        ensure_boundary(pos, h.currentSeq, h.localShort);
+        ensure_boundary(pos + 1, h.currentSeq, h.localShort);
+        s = containing(pos, h.currentSeq, h.localShort, &off);
+        if (s < 0 || off != 0 || z.len(s) != 1) {
+            fail(E_ASSERT);
+            return;
+        }
+        int32_t hnd = ht_alloc();
+        if (hnd > 0) cold(s).toff = (uint32_t)hnd;
     }
 
     /* ---- delta events (§8 f3; stream format in mt_oplog.h): the reference's
@@ -1944,7 +2030,8 @@ struct Replica {
         int32_t lenL = z.len(ls);
         if (off < lenL) {
             z.len(rs) = lenL - off;
-            cr.toff = cl.toff + (uint32_t)off;
+            /* the text offset, or PermutationSegment.createSplitSegmentAt's start + pos (unallocated stays) */
+            cr.toff = ((z.flags(ls) & RF_PERM) && cl.toff == 0) ? 0u : cl.toff + (uint32_t)off;
             z.len(ls) = off;
             z.flags(ls) &= (uint8_t)~RF_NLK; /* the left part's last unit is not known any more */
         } else { /* a split at or past the end (a local reference past its segment's end): text.substring(off)
@@ -2391,12 +2478,18 @@ struct Replica {
     /* canAppend (textSegment.ts:63-68) */
     MT_HD bool can_append(int32_t a, int32_t b) {
         MT_PROF_SCOPE(PH_CAND);
-        /* PermutationSegment.canAppend (permutationvector.ts:87-93): both handles unallocated */
-        if ((z.flags(a) | z.flags(b)) & RF_PERM) return (z.flags(a) & z.flags(b) & RF_PERM) != 0;
+        /* PermutationSegment.canAppend (permutationvector.ts:87-93): both unallocated, or b's handles follow a's */
+        if ((z.flags(a) | z.flags(b)) & RF_PERM)
+            return (z.flags(a) & z.flags(b) & RF_PERM) != 0 && perm_follows(a, b, z.len(a));
         if (z.flags(a) & RF_MARKER) return false;
         if (ends_nl(a, z.len(a))) return false;
         if (z.flags(b) & RF_MARKER) return false;
         return z.len(a) <= GRANULARITY || z.len(b) <= GRANULARITY;
+    }
+    /* PermutationSegment.canAppend's handle rule for rows a (current length La) and b */
+    MT_HD bool perm_follows(int32_t a, int32_t b, int32_t La) {
+        uint32_t sa = cold(a).toff, sb = cold(b).toff;
+        return sa == 0 ? sb == 0 : sb == sa + (uint32_t)La;
     }
     /* the text of the row in slot a (current length La) ends with "\n" (textSegment.ts:64) */
     MT_HD bool ends_nl(int32_t a, int32_t La) {
@@ -2460,6 +2553,7 @@ struct Replica {
                             dseg(-1, z.len(s));
                             dtail(1);
                         }
+                        if (ht_on() && (z.flags(s) & RF_PERM)) ht_unlinked(z.rid[s], z.len(s));
                         if (refs_on()) { /* the segment loses its parent: its references detach */
                             refs_move(z.rid[s], INT32_MIN, REF_DETACHED, 0);
                             coll_drop(z.rid[s]);
@@ -2578,6 +2672,7 @@ struct Replica {
                 int32_t sp = w.bcast(n, prev) * MAXN + (prev & (MAXN - 1));
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
                 ok = match_props(sp, sk);
+                if (ok && permPair) ok = perm_follows(sp, sk, prevLen);
                 if (ok && !permPair) {
                     bool nl = ends_nl(sp, prevLen); /* caches RF_NLK/RF_NL in z.flags(sp) */
                     prevFl = (prevFl & ~(RF_NLK | RF_NL)) | RF_NLK | (nl ? RF_NL : 0);
@@ -2616,16 +2711,21 @@ struct Replica {
                 coll_drop(ur);
             }
         }
-        if (dl_on()) { /* UNLINK / APPEND maintenance events in the reference's walk order (lane order) */
+        if (dl_on() || ht_on()) { /* UNLINK / APPEND maintenance events in the reference's walk order (lane order) */
             uint64_t em = drop;
+            const bool dlo = dl_on();
             while (em) {
                 int32_t l = W::ffs(em);
                 em &= em - 1;
                 int32_t ln = w.bcast(r.len, l);
                 if (w.bcast(code, l) == 2) {
-                    dhead(MT_DELTA_UNLINK);
-                    dseg(-1, ln);
-                    dtail(1);
+                    if (dlo) {
+                        dhead(MT_DELTA_UNLINK);
+                        dseg(-1, ln);
+                        dtail(1);
+                    }
+                    if (ht_on() && (w.bcast((int32_t)fl, l) & RF_PERM)) ht_unlinked(w.bcast((int32_t)r.rid, l), ln);
+                } else if (!dlo) {
                 } else {
                     dhead(MT_DELTA_APPEND);
                     dseg(-1, w.bcast(alen, l));
@@ -3667,7 +3767,12 @@ struct Replica {
             int32_t start = op.pos1, end = op.pos2;
             bool bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
             if (kind != MT_OP_INSERT && end <= start) bad = true;
-            if (kind == MT_OP_INSERT && (op.kind & MT_OPF_ATREF)) { /* pos1 is a reference, not a position */
+            if (kind == MT_OP_NOOP) { /* PermutationVector.getAllocatedHandle(pos1) (mt_oplog.h) */
+                if constexpr (DL)
+                    alloc_handle(op.pos1);
+                else
+                    fail(E_UNSUPPORTED);
+            } else if (kind == MT_OP_INSERT && (op.kind & MT_OPF_ATREF)) { /* pos1 is a reference, not a position */
                 if constexpr (DL) {
                     edit = insert_at_ref(op, &eat);
                     ecli = h.localShort;
@@ -4090,9 +4195,11 @@ struct Replica {
             if (fl & RF_PROPS)
                 for (int k = 0; k < HT::K; k++)
                     if (cold(s).pv[k]) np++;
+            bool hnd = (fl & RF_PERM) && cold(s).toff != 0; /* an allocated PermutationSegment start */
             uint8_t b4[4] = {(uint8_t)((fl & RF_MARKER) ? MT_SEG_MARKER : (fl & RF_PERM) ? MT_SEG_PERM : MT_SEG_TEXT),
                              (uint8_t)(((fl & RF_PROPS) ? MT_DF_HAS_PROPS : 0) | (rem ? MT_DF_REMOVED : 0) |
-                                       ((fl & RF_LSEQ) ? MT_DF_LSEQ : 0) | ((fl & RF_LRSEQ) ? MT_DF_LRSEQ : 0)),
+                                       ((fl & RF_LSEQ) ? MT_DF_LSEQ : 0) | ((fl & RF_LRSEQ) ? MT_DF_LRSEQ : 0) |
+                                       (hnd ? MT_DF_HANDLE : 0)),
                              (uint8_t)nov, z.ng(s)};
             put_bytes(o, b4, 4);
             int32_t f[8] = {z.len(s),
@@ -4124,6 +4231,10 @@ struct Replica {
                 uint16_t kv2[2] = {(uint16_t)bk, cold(s).pv[best]};
                 put_bytes(o, kv2, 4);
                 last = bk;
+            }
+            if (hnd) {
+                int32_t st = (int32_t)cold(s).toff;
+                put_bytes(o, &st, 4);
             }
             if (!(fl & RF_NOTEXT)) put_bytes(o, base + cold(s).toff, 2 * (int64_t)z.len(s));
           }

@@ -68,9 +68,14 @@ mth_store* mth_create_dl(int64_t ndocs, const int32_t* caps6, int32_t dcap) {
 }
 
 mth_store* mth_create_fx(int64_t ndocs, const int32_t* caps6, int32_t dcap, int32_t rcap) {
+    return mth_create_fx2(ndocs, caps6, dcap, rcap, 0);
+}
+
+mth_store* mth_create_fx2(int64_t ndocs, const int32_t* caps6, int32_t dcap, int32_t rcap, int32_t pcap) {
     /* caps6 = (ncap, hcap[ignored: 2*ncap], acap, mcap, gcap, ccap[ignored: 64]); dcap: delta event
-     * log words per doc (mt_caps.dcap); rcap: local references per doc (mt_caps.rcap) */
-    Caps k = {caps6[2], caps6[3], caps6[4], dcap < 0 ? 0 : dcap, rcap < 0 ? 0 : rcap};
+     * log words per doc (mt_caps.dcap); rcap: local references per doc (mt_caps.rcap); pcap:
+     * PermutationVector handles per doc (mt_caps.pcap) */
+    Caps k = {caps6[2], caps6[3], caps6[4], dcap < 0 ? 0 : dcap, rcap < 0 ? 0 : rcap, pcap < 0 ? 0 : pcap};
     int prof = profile_for(caps6[0]);
     if (!caps_valid(k) || ndocs < 1 || prof < 0) return nullptr;
     mth_store* s = (mth_store*)calloc(1, sizeof(mth_store));
@@ -211,6 +216,28 @@ int32_t mth_ref_positions(mth_store* s, int64_t doc, int32_t* out, int32_t cap) 
         int32_t n = r.d.dstate()->nref;
         for (int32_t i = 0; i < n && i < cap; i++) out[i] = r.ref_position(i);
         return n;
+    });
+}
+
+/* the doc's HandleTable.snapshot(): its length (returned) and up to cap entries */
+int64_t mth_handle_table(mth_store* s, int64_t doc, int32_t* out, int64_t cap) {
+    return with_replica(s, doc, [&](auto& r) -> int64_t {
+        if (r.d.caps.pcap <= 0) return -1;
+        int64_t n = r.d.dstate()->hlen;
+        for (int64_t i = 0; out && i < n && i < cap; i++) out[i] = r.d.ht()[i];
+        return n;
+    });
+}
+
+/* HandleCache.getHandle(pos) in the local view: start + offset, INT32_MIN if unallocated; -1: no segment */
+int32_t mth_get_handle(mth_store* s, int64_t doc, int32_t pos, int32_t* out) {
+    return with_replica(s, doc, [&](auto& r) -> int32_t {
+        int32_t off = 0;
+        int32_t sl = r.containing(pos, r.h.currentSeq, r.h.localShort, &off);
+        if (sl < 0) return -1;
+        uint32_t st = (r.z.flags(sl) & RF_PERM) ? r.cold(sl).toff : 0u;
+        *out = st ? (int32_t)st + off : INT32_MIN;
+        return 0;
     });
 }
 

@@ -9,6 +9,9 @@ typedef struct mth_store mth_store;
 mth_store* mth_create(int64_t ndocs, const int32_t* caps6);
 mth_store* mth_create_dl(int64_t ndocs, const int32_t* caps6, int32_t dcap);
 mth_store* mth_create_fx(int64_t ndocs, const int32_t* caps6, int32_t dcap, int32_t rcap);
+mth_store* mth_create_fx2(int64_t ndocs, const int32_t* caps6, int32_t dcap, int32_t rcap, int32_t pcap);
+int64_t mth_handle_table(mth_store* s, int64_t doc, int32_t* out, int64_t cap);
+int32_t mth_get_handle(mth_store* s, int64_t doc, int32_t pos, int32_t* out);
 int32_t mth_ref_positions(mth_store* s, int64_t doc, int32_t* out, int32_t cap);
 int32_t mth_pending(mth_store* s, int64_t doc);
 int64_t mth_deltas(mth_store* s, int64_t doc, int32_t* out, int64_t cap, uint64_t* hash);

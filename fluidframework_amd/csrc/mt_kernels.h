@@ -308,6 +308,14 @@ __global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t m
             res[0] = 1;
             res[1] = r.position_of(s, ref_seq, sh);
         }
+    } else if (mode == 3) { /* HandleCache.getHandle(a): the PermutationSegment's start + offset, or unallocated */
+        int32_t off = 0;
+        int32_t s = r.containing(a, ref_seq, sh, &off);
+        if (s >= 0) {
+            uint32_t st = (r.z.flags(s) & RF_PERM) ? r.cold(s).toff : 0u;
+            res[0] = 1;
+            res[1] = st ? (int32_t)st + off : INT32_MIN;
+        }
     } else { /* mode 2: the marker whose property a (the marker-id key) is value b; res[0] = 2 if several */
         int32_t s = r.marker_by_id(a, b);
         if (s == -2) {
@@ -383,6 +391,7 @@ struct mt_engine {
     int64_t ndocs;
     int32_t dcap = 0; /* delta event log words per document (0: off) */
     int32_t rcap = 0; /* local references per document (0: none) */
+    int32_t pcap = 0; /* PermutationVector handles per document (0: none) */
     bool fx = false;  /* delta events or local references: the client-feature replay build */
     int profile = 0;
     bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */

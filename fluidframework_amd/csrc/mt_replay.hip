@@ -27,16 +27,18 @@ extern "C" {
 int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_engine** out) {
     if (!out || !caps || ndocs < 1 || ndocs > (int64_t)0x7fffffff) return MT_E_ARG;
     *out = nullptr;
-    Caps k = {caps->acap, caps->mcap, caps->gcap, caps->dcap, caps->rcap};
+    Caps k = {caps->acap, caps->mcap, caps->gcap, caps->dcap, caps->rcap, caps->pcap};
     int prof = profile_for(caps->ncap);
-    if (!caps_valid(k) || prof < 0 || caps->ccap > 254 || caps->dcap < 0 || caps->rcap < 0)
+    if (!caps_valid(k) || prof < 0 || caps->ccap > 254 || caps->dcap < 0 || caps->rcap < 0 || caps->pcap < 0 ||
+        caps->pcap > (1 << 24))
         return MT_E_ARG; /* short ids are bytes; 0xFF = LocalClientId */
     mt_engine* e = new mt_engine();
     e->device = device;
     e->ndocs = ndocs;
     e->dcap = caps->dcap;
     e->rcap = caps->rcap;
-    e->fx = caps->dcap > 0 || caps->rcap > 0;
+    e->pcap = caps->pcap;
+    e->fx = caps->dcap > 0 || caps->rcap > 0 || caps->pcap > 0;
     const char* g = getenv("MT_REPLAY_LDS");
     e->lds = g && g[0] == '1';
     const char* np = getenv("MT_NO_PROMOTE");
@@ -616,6 +618,46 @@ int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap) {
 }
 
 int32_t mt_engine_ref_capacity(const mt_engine* e) { return e ? e->rcap : 0; }
+
+static void ht_geometry(const mt_engine* e, int64_t* off, int64_t* dl) {
+    switch (e->profile) {
+    case 0: *off = Doc<HotSmall>::off_ht(e->s0.caps), *dl = Doc<HotSmall>::off_dl(e->s0.caps); break;
+    case 1: *off = Doc<HotMid>::off_ht(e->s1.caps), *dl = Doc<HotMid>::off_dl(e->s1.caps); break;
+    case 3: *off = Doc<HotMat>::off_ht(e->s3.caps), *dl = Doc<HotMat>::off_dl(e->s3.caps); break;
+    case 4: *off = Doc<HotHuge>::off_ht(e->s4.caps), *dl = Doc<HotHuge>::off_dl(e->s4.caps); break;
+    default: *off = Doc<HotBig>::off_ht(e->s2.caps), *dl = Doc<HotBig>::off_dl(e->s2.caps); break;
+    }
+}
+
+int64_t mt_engine_handle_table(mt_engine* e, int64_t doc, int32_t* out, int64_t cap) {
+    if (!e || e->pcap <= 0 || doc < 0 || doc >= e->ndocs || cap < 0) return -MT_E_ARG;
+    e = route(e, &doc);
+    if (hipSetDevice(e->device) != hipSuccess) return -MT_E_HIP;
+    int64_t off, dl, stride, o2;
+    ht_geometry(e, &off, &dl);
+    delta_geometry(e, &o2, &stride);
+    const uint8_t* base = (const uint8_t*)e->mem + doc * stride;
+    DState st;
+    if (hipMemcpyAsync(&st, base + dl, sizeof st, hipMemcpyDeviceToHost, e->stream) != hipSuccess) return -MT_E_HIP;
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
+    int64_t n = st.hlen, m = n < cap ? n : cap;
+    if (out && m > 0) {
+        if (hipMemcpyAsync(out, base + off, 4 * (size_t)m, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+            return -MT_E_HIP;
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
+    }
+    return n;
+}
+
+int32_t mt_engine_get_handle(mt_engine* e, int64_t doc, int32_t pos, int32_t* out) {
+    if (!out) return MT_E_ARG;
+    int32_t r[7];
+    int32_t rc = seg_query(e, doc, 3, pos, 0, 0, -1, r);
+    if (rc) return rc;
+    if (!r[0]) return MT_E_ARG; /* RangeError: no segment at pos (ensureRange) */
+    *out = r[1];
+    return MT_OK;
+}
 
 int32_t mt_engine_ref_positions(mt_engine* e, int32_t* nref_out, int32_t* pos_out) {
     if (!e || e->rcap <= 0) return MT_E_ARG;

@@ -32,7 +32,7 @@ class SegRef(ctypes.Structure):
 
 
 class _Caps(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_int32) for n in ("ncap", "hcap", "acap", "mcap", "gcap", "ccap", "dcap", "rcap")]
+    _fields_ = [(n, ctypes.c_int32) for n in ("ncap", "hcap", "acap", "mcap", "gcap", "ccap", "dcap", "rcap", "pcap")]
 
 
 _LIB = None
@@ -53,6 +53,9 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_start_collab.argtypes = [vp, vp, i32, i32]
         L.mt_engine_start_collab_docs.argtypes = [vp, vp, vp, vp]
         L.mt_engine_pos_from_relative_pos.argtypes = [vp, i64, i32, i32, i32, i32, i32, i32, i32, vp]
+        L.mt_engine_handle_table.argtypes = [vp, i64, vp, i64]
+        L.mt_engine_handle_table.restype = i64
+        L.mt_engine_get_handle.argtypes = [vp, i64, i32, vp]
         L.mt_engine_submit.argtypes = [vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, i64, vp]
         L.mt_engine_run.argtypes = [vp]
         L.mt_engine_reset.argtypes = [vp]
@@ -111,7 +114,8 @@ class Engine:
     """A batch of `ndocs` replicas on HIP device `device`. caps["dcap"] > 0 turns on the delta event
     stream (include/mt_oplog.h MT_DELTA_*: what SharedString "sequenceDelta" / "maintenance"
     listeners see), logging up to dcap words per document; caps["rcap"] > 0 keeps up to rcap local
-    references per document (MT_OP_REF records)."""
+    references per document (MT_OP_REF records); caps["pcap"] > 0 gives every document a PermutationVector
+    HandleTable of pcap handles (getAllocatedHandle records, MT_OP_NOOP | MT_OPF_LOCAL)."""
 
     def __init__(self, ndocs: int, device: int = 0, **caps):
         c = default_caps(0)
@@ -279,6 +283,21 @@ class Engine:
         pos = np.full((self.ndocs, max(self.caps.rcap, 1)), -1, np.int32)
         self._check(self.L.mt_engine_ref_positions(self.h, _p(n), _p(pos)), "ref_positions")
         return n, pos
+
+    def handle_table(self, doc: int) -> np.ndarray:
+        """PermutationVector's HandleTable.snapshot() of one document (handletable.ts:80-82)"""
+        n = self.L.mt_engine_handle_table(self.h, doc, None, 0)
+        if n < 0:
+            raise EngineError(f"handle_table failed {n}")
+        buf = np.zeros(max(n, 1), np.int32)
+        self.L.mt_engine_handle_table(self.h, doc, _p(buf), n)
+        return buf[:n]
+
+    def get_handle(self, doc: int, pos: int) -> int:
+        """PermutationVector.getMaybeHandle(pos) (HandleCache.getHandle): start + offset, -2**31 unallocated"""
+        v = ctypes.c_int32()
+        self._check(self.L.mt_engine_get_handle(self.h, doc, pos, ctypes.byref(v)), "get_handle")
+        return v.value
 
     def stats(self) -> np.ndarray:
         out = np.zeros((self.ndocs, 4), np.int32)

@@ -21,6 +21,8 @@ export interface Caps {
     dcap?: number;
     /** local references per document (0: none) */
     rcap?: number;
+    /** PermutationVector handles per document (0: no HandleTable) */
+    pcap?: number;
 }
 export declare const DEFAULT_CAPS: Caps;
 
@@ -120,6 +122,12 @@ export declare class GpuClient {
     /** SharedString.insertTextRelative / insertMarkerRelative */
     insertTextRelative(relativePos1: IRelativePosition, text: string, props?: PropertySet): MergeTreeOp | undefined;
     insertMarkerRelative(relativePos1: IRelativePosition, refType: number, props?: PropertySet): MergeTreeOp;
+    /** PermutationVector.getAllocatedHandle (engines with caps.pcap > 0): the row's handle, allocated if it had none */
+    getAllocatedHandle(pos: number): number;
+    /** PermutationVector.getMaybeHandle: -2^31 (Handle.unallocated) when the row has none */
+    getMaybeHandle(pos: number): number;
+    /** HandleTable.snapshot() of this replica's PermutationVector */
+    handleTable(): Int32Array;
     getLength(): number;
     /** SharedString.getText(start?, end?) of the local view */
     getText(start?: number, end?: number): string;

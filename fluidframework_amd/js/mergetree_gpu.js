@@ -29,7 +29,7 @@ const CLIENT_LOCAL = 0xfffe; // LocalClientId in a MergeTree-level record
 const LocalClientId = -1; // constants.ts
 const UnassignedSequenceNumber = -1;
 const ReferenceType = { Simple: 0x0, SlideOnRemove: 0x40 }; // ops.ts
-const SEG = { TEXT: 0, MARKER: 1 };
+const SEG = { TEXT: 0, MARKER: 1, PERM: 2 };
 const SEG_RELPOS = 0x80; // positions relative to markers (mt_oplog.h MT_SEG_RELPOS)
 const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
 const VALUE_FALSY = 0x8000;
@@ -168,6 +168,8 @@ class ReplayEngine {
             if (typeof seg === "string") {
                 r.text_off = q.text.length; r.text_len = seg.length;
                 for (let i = 0; i < seg.length; i++) q.text.push(seg.charCodeAt(i));
+            } else if (Array.isArray(seg)) { // PermutationSegment [length, start] (permutationvector.ts:40-43, 75-77)
+                r.seg_kind = SEG.PERM; r.text_len = seg[0];
             } else if (seg && seg.marker) {
                 r.seg_kind = SEG.MARKER; r.pos2 = seg.marker.refType; props = seg.props;
             } else if (seg && typeof seg.text === "string") {
@@ -414,6 +416,19 @@ class GpuClient {
     insertMarkerRelative(relativePos1, refType, props) {
         return this.insertMarkerLocal(this.posFromRelativePos(relativePos1), refType, props);
     }
+
+    /* PermutationVector (engines created with caps.pcap > 0; permutationvector.ts:157-183, 338-363):
+     * getAllocatedHandle(pos) queues the allocation (a local record) and answers the handle at the next read;
+     * getMaybeHandle(pos) reads it (Handle.unallocated = -2^31 when the row has none); handleTable() is
+     * HandleTable.snapshot(). Zamboni's unlinks free handles as the reference's onMaintenance does. */
+    getAllocatedHandle(pos) {
+        this.engine.enqueue(this.doc, OP.NOOP | OPF_LOCAL, { pos1: pos });
+        return this.getMaybeHandle(pos);
+    }
+
+    getMaybeHandle(pos) { return addon.getHandle(this.read(), this.doc, pos); }
+
+    handleTable() { return addon.handleTable(this.read(), this.doc); }
 
     /* reads flush the queued events first */
     read() { this.engine.flush(); this.engine.checkDoc(this.doc); return this.engine.h; }

@@ -107,10 +107,11 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
         NAPI_OK(napi_get_named_property(env, argv[2], names[i], &f));
         if (!i32_of(env, f, fields[i])) return nullptr;
     }
-    /* optional: delta event log words (mt_caps.dcap) and local references (mt_caps.rcap) per doc */
-    const char* opt[2] = {"dcap", "rcap"};
-    int32_t* ofield[2] = {&caps.dcap, &caps.rcap};
-    for (int i = 0; i < 2; i++) {
+    /* optional: delta event log words (mt_caps.dcap), local references (mt_caps.rcap) and PermutationVector
+     * handles (mt_caps.pcap) per doc */
+    const char* opt[3] = {"dcap", "rcap", "pcap"};
+    int32_t* ofield[3] = {&caps.dcap, &caps.rcap, &caps.pcap};
+    for (int i = 0; i < 3; i++) {
         bool has = false;
         NAPI_OK(napi_has_named_property(env, argv[2], opt[i], &has));
         if (!has) continue;
@@ -393,6 +394,37 @@ static napi_value js_get_position(napi_env env, napi_callback_info info) {
     return num(env, out);
 }
 
+/* handleTable(h, doc) -> Int32Array: PermutationVector's HandleTable.snapshot() (mt_engine_handle_table) */
+static napi_value js_handle_table(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    if (!e || !i64_of(env, argv[1], &doc)) return nullptr;
+    int64_t n = mt_engine_handle_table(e, doc, nullptr, 0);
+    if (n < 0) return throw_status(env, e, (int32_t)-n, "mt_engine_handle_table (engine created without caps.pcap)");
+    void* data = nullptr;
+    napi_value ab, arr;
+    NAPI_OK(napi_create_arraybuffer(env, 4 * (size_t)n, &data, &ab));
+    int64_t m = mt_engine_handle_table(e, doc, (int32_t*)data, n);
+    if (m < 0) return throw_status(env, e, (int32_t)-m, "mt_engine_handle_table");
+    NAPI_OK(napi_create_typedarray(env, napi_int32_array, (size_t)n, ab, 0, &arr));
+    return arr;
+}
+
+/* getHandle(h, doc, pos) -> number: getMaybeHandle (start + offset; -2^31 = Handle.unallocated) */
+static napi_value js_get_handle(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t pos, out = 0;
+    if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &pos)) return nullptr;
+    int32_t rc = mt_engine_get_handle(e, doc, pos, &out);
+    if (rc) return throw_status(env, e, rc, "mt_engine_get_handle");
+    return num(env, out);
+}
+
 /* posFromRelativePos(h, doc, keyId, valueId, before, hasOffset, offset, refSeq, longClient) -> number */
 static napi_value js_pos_from_relpos(napi_env env, napi_callback_info info) {
     napi_value argv[9];
@@ -431,7 +463,8 @@ static napi_value init(napi_env env, napi_value exports) {
     } fns[] = {{"create", js_create},       {"startCollab", js_start_collab}, {"submit", js_submit},
                {"run", js_run},             {"sync", js_sync},                {"reset", js_reset},
                {"errors", js_errors},       {"digests", js_digests},          {"getLength", js_get_length},
-               {"getText", js_get_text}, {"posFromRelativePos", js_pos_from_relpos},    {"getContainingSegment", js_get_containing},
+               {"getText", js_get_text}, {"posFromRelativePos", js_pos_from_relpos},
+               {"handleTable", js_handle_table},     {"getHandle", js_get_handle},    {"getContainingSegment", js_get_containing},
                {"getPosition", js_get_position}, {"ndocs", js_ndocs},        {"lastRunMs", js_last_run_ms},
                {"deltas", js_deltas},       {"refPositions", js_ref_positions}};
     for (auto& f : fns) {

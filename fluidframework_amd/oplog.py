@@ -154,7 +154,8 @@ def decode_deltas(words):
 
 
 # canonical-dump segment flag bits (include/mt_oplog.h MT_DF_*)
-DF_HAS_PROPS, DF_REMOVED, DF_LSEQ, DF_LRSEQ = 1, 2, 4, 8
+DF_HAS_PROPS, DF_REMOVED, DF_LSEQ, DF_LRSEQ, DF_HANDLE = 1, 2, 4, 8, 16
+HANDLE_UNALLOCATED = -0x80000000  # Handle.unallocated (matrix handletable.ts:11)
 
 
 def parse_dump(b: bytes):
@@ -173,13 +174,18 @@ def parse_dump(b: bytes):
         off += 4
         props = [struct.unpack_from("<2H", b, off + 4 * k) for k in range(nprops)]
         off += 4 * nprops
+        start = HANDLE_UNALLOCATED
+        if flags & DF_HANDLE:  # an allocated PermutationSegment start (mt_oplog.h MT_DF_HANDLE)
+            (start,) = struct.unpack_from("<i", b, off)
+            off += 4
         text = ""
         if kind == SEG_TEXT:
             text = b[off: off + 2 * f[0]].decode("utf-16-le")
             off += 2 * f[0]
         segs.append(dict(kind=kind, flags=flags, ngroups=ngroups, len=f[0], seq=f[1], client=f[2],
                          removedSeq=f[3] if flags & 2 else None, removedClient=f[4], localSeq=f[5],
-                         localRemovedSeq=f[6], leaf=f[7], overlap=ov, props=props, refType=ref_type, text=text))
+                         localRemovedSeq=f[6], leaf=f[7], overlap=ov, props=props, refType=ref_type, text=text,
+                         start=start))
     if off != len(b):
         raise ValueError("trailing bytes after the canonical dump")
     return dict(currentSeq=hdr[0], minSeq=hdr[1], localSeq=hdr[2], length=hdr[3], nsegs=hdr[4],

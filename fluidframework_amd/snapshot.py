@@ -51,12 +51,15 @@ def _json_spec(seg, props):
         if props is not None:
             j["props"] = props
         return j
-    return [seg["len"], UNALLOCATED]
+    return [seg["len"], seg.get("start", UNALLOCATED)]
 
 
 def _can_append(a, b) -> bool:
-    if a["kind"] == ol.SEG_PERM or b["kind"] == ol.SEG_PERM:  # PermutationSegment.canAppend: both unallocated
-        return a["kind"] == b["kind"]
+    if a["kind"] == ol.SEG_PERM or b["kind"] == ol.SEG_PERM:  # PermutationSegment.canAppend (87-93)
+        if a["kind"] != b["kind"]:
+            return False
+        sa, sb = a.get("start", UNALLOCATED), b.get("start", UNALLOCATED)
+        return sb == UNALLOCATED if sa == UNALLOCATED else sb == sa + a["len"]
     if a["kind"] != ol.SEG_TEXT or b["kind"] != ol.SEG_TEXT:  # Marker.canAppend is false
         return False
     return not a["text"].endswith("\n") and (a["len"] <= TEXT_GRANULARITY or b["len"] <= TEXT_GRANULARITY)
@@ -397,6 +400,9 @@ def load_records(tree: dict, log: ol.DocLog, client_index, local_client: Optiona
         if isinstance(spec, str):
             log.add(kind, text=spec, **common)
         elif isinstance(spec, list):  # PermutationSegment [length, start]
+            if len(spec) > 1 and spec[1] is not None and spec[1] >= 1:
+                raise ValueError("a PermutationSegment with allocated handles: loading the matrix's HandleTable "
+                                 "blob with it is not modelled")
             log.add(kind, perm=spec[0], **common)
         elif "marker" in spec:
             log.add(kind, marker=spec["marker"]["refType"], props=spec.get("props"), **common)

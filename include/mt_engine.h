@@ -33,6 +33,7 @@ typedef struct mt_caps {
     int32_t ccap; /* distinct clients per doc (<= 254)                                  */
     int32_t dcap; /* delta event log words per doc; 0 = no delta events (mt_oplog.h)   */
     int32_t rcap; /* local references per doc (MT_OP_REF records); 0 = none           */
+    int32_t pcap; /* PermutationVector handles per doc (getAllocatedHandle records); 0 = none */
 } mt_caps;
 
 /* status codes */
@@ -160,6 +161,13 @@ int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap);
  * only slid references, so refsByOffset[offset].at is undefined, localReference.ts:195-201); the
  * reference keeps no such reference, and the engine leaves the tree untouched for it. */
 int32_t mt_engine_ref_positions(mt_engine* e, int32_t* nref_out, int32_t* pos_out);
+/* PermutationVector (engines created with caps.pcap > 0): the document's HandleTable.snapshot()
+ * (handletable.ts:80-82: handles[0] = the free-list head, then 0 for an allocated handle or the next free one),
+ * `len` entries; writes min(len, cap) and returns len (<0 on error). */
+int64_t mt_engine_handle_table(mt_engine* e, int64_t doc, int32_t* out, int64_t cap);
+/* PermutationVector.getMaybeHandle(pos) (permutationvector.ts:157-161, HandleCache.getHandle): the handle of
+ * local position pos (segment start + offset; INT32_MIN = Handle.unallocated when the segment has none). */
+int32_t mt_engine_get_handle(mt_engine* e, int64_t doc, int32_t pos, int32_t* out);
 /* caps.rcap of the engine (the row length of mt_engine_ref_positions' pos_out) */
 int32_t mt_engine_ref_capacity(const mt_engine* e);
 /* Per-doc counters: nleaf, high-water row slots, high-water heap, events applied. */

@@ -40,7 +40,12 @@ enum {
      * refType (ReferenceType, ops.ts; SlideOnRemove = 0x40). The document's references are numbered in
      * creation order; a position past the end makes a detached reference. */
     MT_OP_REF = 3,
-    MT_OP_NOOP = 4, /* sequenced message that is not a merge-tree op: advances currentSeq/MSN only */
+    MT_OP_NOOP = 4, /* sequenced message that is not a merge-tree op: advances currentSeq/MSN only. With
+                     * MT_OPF_LOCAL: PermutationVector.getAllocatedHandle(pos1) (permutationvector.ts:
+                     * 157-183) in the local view: the PermutationSegment at pos1 keeps its handle if it has
+                     * one, else a one-row segment is split out at pos1 and gets HandleTable.allocate()
+                     * (handletable.ts:35-40); zamboni's unlinks free handles (onMaintenance, 338-363).
+                     * Client-feature build with caps.pcap > 0 (others latch MT_E_UNSUPPORTED). */
     /* Snapshot load (SnapshotLoader, snapshotLoader.ts:86-228), on an empty non-collaborating replica:
      *   RELOAD: one header segment; pos1 counts down n..1 over the header's n records, and the whole
      *           header becomes the tree at once (reloadFromSegments, mergeTree.ts:1229-1284: blocks of
@@ -156,6 +161,7 @@ typedef struct mt_kv {
  *         int32 len, seq, client, removedSeq, removedClient, localSeq, localRemovedSeq, leaf;
  *         int32 overlap[noverlap];
  *         uint16 nprops; uint16 refType; (key,value) x nprops sorted by key id;
+ *         int32 start (MT_DF_HANDLE only: a PermutationSegment's allocated handle, permutationvector.ts:38);
  *         text: len x uint16 (text segments only)
  * client fields are LONG client indices; -1 = the reference's "original" (LocalClientId).
  */
@@ -164,6 +170,8 @@ enum {
     MT_DF_REMOVED = 2,
     MT_DF_LSEQ = 4,
     MT_DF_LRSEQ = 8,
+    MT_DF_HANDLE = 16, /* a PermutationSegment whose start handle is allocated (never set without MT_OP_NOOP |
+                          MT_OPF_LOCAL records, so dumps of other logs are unchanged) */
 };
 
 #define MT_FNV_OFFSET 0xcbf29ce484222325ULL

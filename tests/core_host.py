@@ -26,6 +26,11 @@ def lib():
         L.mth_create_dl.argtypes = [i64, vp, i32]
         L.mth_create_fx.restype = vp
         L.mth_create_fx.argtypes = [i64, vp, i32, i32]
+        L.mth_create_fx2.restype = vp
+        L.mth_create_fx2.argtypes = [i64, vp, i32, i32, i32]
+        L.mth_handle_table.argtypes = [vp, i64, vp, i64]
+        L.mth_handle_table.restype = i64
+        L.mth_get_handle.argtypes = [vp, i64, i32, vp]
         L.mth_ref_positions.argtypes = [vp, i64, vp, i32]
         L.mth_pending.argtypes = [vp, i64]
         L.mth_deltas.argtypes = [vp, i64, vp, i64, vp]
@@ -61,11 +66,11 @@ DEFAULT_CAPS = (192, 256, 1 << 16, 4096, 1024, 64)
 
 
 class HostStore:
-    def __init__(self, ndocs: int, caps=DEFAULT_CAPS, dcap: int = 0, rcap: int = 0):
+    def __init__(self, ndocs: int, caps=DEFAULT_CAPS, dcap: int = 0, rcap: int = 0, pcap: int = 0):
         self.L = lib()
         self.caps = np.asarray(caps, np.int32)
         self.rcap = rcap
-        self.h = self.L.mth_create_fx(ndocs, _p(self.caps), dcap, rcap)
+        self.h = self.L.mth_create_fx2(ndocs, _p(self.caps), dcap, rcap, pcap)
         if not self.h:
             raise RuntimeError("mth_create failed")
         self.ndocs = ndocs
@@ -137,6 +142,20 @@ class HostStore:
         self.L.mth_deltas(self.h, doc, _p(buf), n, _p(h))
         return int(n), int(h[0]), buf[:n]
 
+    def handle_table(self, doc) -> np.ndarray:
+        """PermutationVector's HandleTable.snapshot() (handletable.ts:80-82)"""
+        n = self.L.mth_handle_table(self.h, doc, None, 0)
+        buf = np.zeros(max(n, 1), np.int32)
+        self.L.mth_handle_table(self.h, doc, _p(buf), n)
+        return buf[:n]
+
+    def get_handle(self, doc, pos) -> int:
+        """HandleCache.getHandle(pos): start + offset; -2**31 = Handle.unallocated"""
+        out = np.zeros(1, np.int32)
+        if self.L.mth_get_handle(self.h, doc, pos, _p(out)) != 0:
+            raise IndexError(pos)
+        return int(out[0])
+
     def pending(self, doc) -> int:
         """segment groups in flight (local ops not yet acked)"""
         return int(self.L.mth_pending(self.h, doc))
@@ -153,9 +172,9 @@ class HostStore:
         return dict(zip(("nleaf", "hw_slots", "hw_heap", "heap", "mem", "arena_top", "nodes", "ops"), out.tolist()))
 
 
-def replay_batch(batch: ol.Batch, caps=DEFAULT_CAPS, dcap: int = 0, rcap: int = 0):
+def replay_batch(batch: ol.Batch, caps=DEFAULT_CAPS, dcap: int = 0, rcap: int = 0, pcap: int = 0):
     """Replay every document of a batch on the host core; returns (digests, errors, store)."""
-    st = HostStore(batch.ndocs, caps, dcap, rcap)
+    st = HostStore(batch.ndocs, caps, dcap, rcap, pcap)
     dig = np.zeros(batch.ndocs, np.uint64)
     err = np.zeros(batch.ndocs, np.int32)
     for d in range(batch.ndocs):

@@ -3,7 +3,7 @@
 // -> Node-API addon -> libmtreplay.so on the GPU: MergeTree-level insertSegments / markRangeRemoved /
 // annotateRange with explicit (refSeq, clientId, seq), startCollaboration with per-document minSeq /
 // currentSeq, getText / getTextWithPlaceholders / getTextAt with placeholder, start and end, ops with relative
-// positions and posFromRelativePos. Prints the
+// positions and posFromRelativePos, PermutationVector getAllocatedHandle / getMaybeHandle / handleTable. Prints the
 // answers as one JSON line; tests/test_napi.py compares them with the reference's
 // (tests/golden/napi_kat2_expected.json, tools/make_napi_kat2.mjs).
 const fs = require("fs");
@@ -17,7 +17,8 @@ for (const st of steps) {
     const [op] = st;
     if (op === "collab") {
         const [, names, mins, curs] = st;
-        eng = new ReplayEngine(names.length, { ...DEFAULT_CAPS, dcap: 1024 }); // client-feature build: relative positions
+        // client-feature build: relative positions, PermutationVector handles
+        eng = new ReplayEngine(names.length, { ...DEFAULT_CAPS, dcap: 1024, pcap: 256 });
         clients = names.map((_, d) => eng.client(d));
         eng.startCollaboration(names, mins, curs);
         continue;
@@ -45,6 +46,12 @@ for (const st of steps) {
     } else if (op === "text_at") {
         const [, , ref, client, ph, a, b] = st;
         out.push(c.getTextAt(ref, client, ph, a === null ? undefined : a, b === null ? undefined : b));
+    } else if (op === "alloc") {
+        out.push(c.getAllocatedHandle(st[2]));
+    } else if (op === "handle") {
+        out.push(c.getMaybeHandle(st[2]));
+    } else if (op === "handles") {
+        out.push(Array.from(c.handleTable()));
     } else if (op === "relpos") {
         out.push(c.posFromRelativePos(st[2]));
     } else if (op === "length") {

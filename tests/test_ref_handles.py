@@ -1,0 +1,79 @@
+"""PermutationVector handle allocation and recycling (§8(f) f3; matrix permutationvector.ts:36-122, 157-183,
+279-363, handletable.ts) against the REFERENCE (tests/golden/refhandles_c5_perm.npz, tools/make_ref_goldens.py
+--handles).
+
+Config-5 logs (SharedMatrix row / column vectors of PermutationSegments) get 40 getAllocatedHandle records per
+document (tests/handles_inject.py, mt_oplog.h MT_OP_NOOP | MT_OPF_LOCAL). The reference Client, with the
+reference HandleTable and PermutationVector's bookkeeping around it, replays them: a row without a handle is
+split out to one row (walkSegments with splitRange) and allocated, split halves carry start + pos, zamboni
+appends only segments whose handles follow each other (canAppend) and its UNLINK callbacks free the handles in
+order. The digests of dumps that carry every allocated start (MT_DF_HANDLE) and each document's
+HandleTable.snapshot() must be reproduced by the host build of the engine core and by the HIP engine."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import gen
+import core_host
+import handles_inject
+from make_goldens_sha import log_sha
+from test_ref_goldens import caps_for
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+PCAP = 1 << 12
+
+
+def load():
+    z = np.load(os.path.join(GOLDEN, "refhandles_c5_perm.npz"), allow_pickle=False)
+    w = gen.Workload(**json.loads(str(z["workload"])))
+    c = caps_for(w)
+    caps = (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"])
+    b = handles_inject.inject(gen.generate(w, ids=z["doc_ids"], threads=8), caps)
+    assert log_sha(b) == str(z["log_sha256"]), "the injected logs differ from the fixture's"
+    return z, c, caps, b
+
+
+def table(z, d):
+    return z["tables"][z["table_off"][d]: z["table_off"][d + 1]]
+
+
+def test_host_core_handles_match_reference():
+    z, c, caps, b = load()
+    dig, err, st = core_host.replay_batch(b, caps, pcap=PCAP)
+    assert (err == 0).all()
+    assert np.array_equal(dig, z["digests"])
+    for d in range(b.ndocs):
+        assert np.array_equal(st.handle_table(d), table(z, d)), f"doc {d}"
+    # the fixture allocates, recycles and reuses handles
+    assert max(len(table(z, d)) for d in range(b.ndocs)) > 1
+    assert any((table(z, d)[1:] != 0).any() for d in range(b.ndocs))  # freed entries on the free list
+
+
+def test_get_handle_reads_start_plus_offset():
+    """HandleCache.getHandle: an allocated row answers start + offset, the rest Handle.unallocated"""
+    z, c, caps, b = load()
+    _, err, st = core_host.replay_batch(b.subset([0]), caps, pcap=PCAP)
+    assert err[0] == 0
+    L = st.L.mth_length_local(st.h, 0)
+    got = [st.get_handle(0, p) for p in range(L)]
+    alloc = [h for h in got if h != -(1 << 31)]
+    assert alloc and all(h >= 1 for h in alloc)
+    t = table(z, 0)
+    live = {i for i in range(1, len(t)) if t[i] == 0}  # allocated handles (slot value 0)
+    assert set(alloc) <= live
+
+
+@pytest.mark.gpu
+def test_gpu_handles_match_reference():
+    from fluidframework_amd.engine import Engine
+    z, c, caps, b = load()
+    eng = Engine(b.ndocs, **dict(c, pcap=PCAP))
+    eng.start_collab(b.local_long_id)
+    eng.replay(b)
+    err, _ = eng.errors()
+    assert (err == 0).all()
+    assert np.array_equal(eng.digests(), z["digests"])
+    for d in range(b.ndocs):
+        assert np.array_equal(eng.handle_table(d), table(z, d)), f"doc {d}"

@@ -15,7 +15,10 @@ const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPe
 async function main() {
     const MT = await import(path.join(erased, "index.mjs"));
     const { Client, TextSegment, Marker, MergeTreeTextHelper } = MT;
+    const { PermutationSegment } = await import(path.join(erased, "permutationSegment.mjs"));
+    const { HandleTable, isHandleValid } = await import(path.join(erased, "handletable.mjs"));
     const specToSegment = (spec) => {
+        if (Array.isArray(spec)) return PermutationSegment.fromJSONObject(spec);
         const seg = TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec);
         if (!seg) throw new Error(`bad segment spec ${JSON.stringify(spec)}`);
         return seg;
@@ -23,13 +26,33 @@ async function main() {
     const segOf = (s) => (typeof s === "string" ? TextSegment.make(s)
         : s.marker ? Marker.make(s.marker.refType, s.props) : TextSegment.make(s.text, s.props));
     let clients = [];
+    let tables = [];
+    // PermutationVector's handle bookkeeping (matrix permutationvector.ts:157-183, 297-309, 338-363) around the
+    // reference Client, with the reference HandleTable (as tools/ref_replay.mjs --handles)
+    const hook = (c, t) => {
+        c.mergeTreeDeltaCallback = (opArgs, args) => {
+            if (args.operation === 0) for (const { segment } of args.deltaSegments) if (segment.reset) segment.reset();
+        };
+        c.mergeTreeMaintenanceCallback = (args) => {
+            if (args.operation !== -3) return;
+            let freed = [];
+            for (const { segment } of args.deltaSegments) {
+                if (isHandleValid(segment.start)) {
+                    freed = freed.concat(new Array(segment.cachedLength).fill(0).map((v, i) => i + segment.start));
+                }
+            }
+            for (const h of freed) t.free(h);
+        };
+    };
     const out = [];
     for (const st of steps) {
         const [op] = st;
         if (op === "collab") {
             const [, names, mins, curs] = st;
+            tables = names.map(() => new HandleTable());
             clients = names.map((n, d) => {
                 const c = new Client(specToSegment, logger);
+                hook(c, tables[d]);
                 c.startOrUpdateCollaboration(n, mins[d], curs[d]);
                 return c;
             });
@@ -56,6 +79,20 @@ async function main() {
             const [ref, client, ph, a, b] = local ? [mt.collabWindow.currentSeq, null, st[2], st[3], st[4]] : st.slice(2);
             const who = local ? mt.collabWindow.clientId : cid(client);
             out.push(new MergeTreeTextHelper(mt).getText(ref, who, ph, a === null ? undefined : a, b === null ? undefined : b));
+        } else if (op === "alloc") { // getAllocatedHandle
+            const pos = st[2];
+            const { segment, offset } = c.getContainingSegment(pos);
+            let handle = segment.start + offset;
+            if (!isHandleValid(handle)) {
+                c.walkSegments((seg) => { seg.start = handle = tables[st[1]].allocate(); return true; }, pos, pos + 1,
+                    undefined, true);
+            }
+            out.push(handle);
+        } else if (op === "handle") { // getMaybeHandle
+            const { segment, offset } = c.getContainingSegment(st[2]);
+            out.push(isHandleValid(segment.start) ? segment.start + offset : -0x80000000);
+        } else if (op === "handles") {
+            out.push(tables[st[1]].snapshot().slice());
         } else if (op === "relpos") {
             out.push(c.posFromRelativePos(st[2]));
         } else if (op === "length") {

@@ -443,6 +443,47 @@ def make_tree(node: str) -> None:
               f"logs' on every document", flush=True)
 
 
+def make_handles(node: str) -> None:
+    """tests/golden/refhandles_c5_perm.npz: config-5 logs (PermutationSegment rows) with injected
+    PermutationVector.getAllocatedHandle records (tests/handles_inject.py) replayed by the reference Client with
+    PermutationVector's handle bookkeeping (tools/ref_replay.mjs --handles: the reference's HandleTable,
+    getAllocatedHandle / onDelta / onMaintenance restated). Stored: the digests of dumps that carry allocated
+    starts (MT_DF_HANDLE) and every document's HandleTable.snapshot()."""
+    import handles_inject
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_ref_goldens import caps_for
+    w, ids = SETS["c5_perm"]
+    b = gen.generate(w, ids=ids, threads=8)
+    c = caps_for(w)
+    hb = handles_inject.inject(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
+    d = os.path.join(SCRATCH, "handles")
+    write_batch(hb, gen.generator_interner(), d)
+    r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d, "--handles"],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+    errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
+    if errs:
+        raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
+    blob = np.fromfile(os.path.join(d, "ref_dumps.bin"), np.uint8)
+    off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
+    digests = np.asarray([fnv1a64(blob[off[i]: off[i + 1]].tobytes()) for i in range(hb.ndocs)], np.uint64)
+    ht = json.load(open(os.path.join(d, "ref_handles.json")))
+    tables = [np.asarray(ht[str(i)], np.int32) for i in range(hb.ndocs)]
+    toff = np.cumsum([0] + [len(t) for t in tables]).astype(np.int64)
+    nalloc = int((hb.ops["kind"] == (ol.OP_NOOP | ol.OPF_LOCAL)).sum())
+    with_start = sum(1 for i in range(hb.ndocs) if len(tables[i]) > 1)
+    np.savez_compressed(
+        os.path.join(GOLDEN, "refhandles_c5_perm.npz"), workload=json.dumps(dataclasses.asdict(w)),
+        doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(hb), digests=digests, nalloc=nalloc,
+        tables=np.concatenate(tables), table_off=toff,
+        source=("packages/dds/merge-tree/src + matrix handletable.ts (reference, type-erased by tools/ts_erase.py) "
+                "under node by tools/ref_replay.mjs --handles"),
+    )
+    print(f"refhandles_c5_perm: {hb.ndocs} docs, {nalloc} getAllocatedHandle records, {with_start} docs allocated, "
+          f"handle tables {min(len(t) for t in tables)}..{max(len(t) for t in tables)} entries", flush=True)
+
+
 def make_relpos(node: str) -> None:
     """tests/golden/refrelpos.npz: logs whose ops name positions relative to markers (tests/relpos_logs.py,
     mt_oplog.h MT_SEG_RELPOS; Client.getValidOpRange resolves them with MergeTree.posFromRelativePos)
@@ -587,6 +628,7 @@ def main() -> None:
     ap.add_argument("--regen", action="store_true", help="write the reconnect fixtures (refregen_*.npz) only")
     ap.add_argument("--legacy", action="store_true", help="write the legacy-summary fixtures (reflegacy_*.npz) only")
     ap.add_argument("--texts", action="store_true", help="write the getText fixtures (reftext_*.npz) only")
+    ap.add_argument("--handles", action="store_true", help="write the PermutationVector handle fixture only")
     ap.add_argument("--relpos", action="store_true", help="write the relative-position fixture (refrelpos.npz) only")
     ap.add_argument("--tree", action="store_true", help="write the MergeTree-level record fixtures (reftree_*.npz) only")
     args = ap.parse_args()
@@ -599,6 +641,9 @@ def main() -> None:
         return
     if args.relpos:
         make_relpos(args.node)
+        return
+    if args.handles:
+        make_handles(args.node)
         return
     if args.legacy:
         make_legacy([n for n in args.sets.split(",") if n in LEGACY_SETS], args.node)

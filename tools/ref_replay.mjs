@@ -19,8 +19,15 @@ const timeOnly = process.argv.includes("--time");
 // (the stream SharedString's "sequenceDelta" / "maintenance" listeners see, sequence.ts:136-150) in the
 // word format of include/mt_oplog.h (MT_DELTA_*) -> batch-dir/ref_deltas.bin + ref_delta_off.bin
 const withDeltas = process.argv.includes("--deltas");
+// --handles: every replica is also a PermutationVector's HandleTable owner (matrix permutationvector.ts:
+// 124-363): local NOOP records are getAllocatedHandle(pos1), zamboni's UNLINK callbacks free handles, inserted
+// segments reset their start; dumps carry allocated starts (MT_DF_HANDLE) -> batch-dir/ref_handles.json
+const withHandles = process.argv.includes("--handles");
 const traceDoc = process.argv.includes("--trace-refs") ? Number(process.argv[process.argv.indexOf("--trace-refs") + 1]) : -1;
 let Client, TextSegment, Marker, PermutationSegment, SnapshotV1, SnapshotLegacy, LocalReference; // bound in main() (Node 12 has no top-level await)
+let HandleTable, isHandleValid;
+let curHandles = null; // the HandleTable of the replica being replayed (--handles)
+const handleTables = {};
 
 const rd = (f) => fs.readFileSync(path.join(dir, f));
 const meta = JSON.parse(rd("meta.json"));
@@ -161,6 +168,10 @@ function applyRange(client, doc, from, to) {
             continue;
         }
         if (rec.kind & 0x80) { // local edit: insertSegmentLocal / removeRangeLocal / annotateRangeLocal
+            if (kind === 4) { // PermutationVector.getAllocatedHandle(pos1) (permutationvector.ts:157-183)
+                getAllocatedHandle(client, rec.pos1);
+                continue;
+            }
             if (kind === 0) {
                 const ps = propSet(doc, rec.props);
                 const seg = rec.seg_kind === 2 ? new PermutationSegment(rec.text_len)
@@ -231,6 +242,41 @@ function applyRange(client, doc, from, to) {
             pendingOps.splice(0, contents.type === 3 ? contents.ops.length : 1);
         }
     }
+}
+
+// PermutationVector's handle bookkeeping around the reference Client (permutationvector.ts:124-363, restated:
+// the class itself needs the container runtime), with the reference's own HandleTable (handletable.ts)
+function hookHandles(client, doc) {
+    const table = new HandleTable();
+    handleTables[doc] = table;
+    curHandles = table;
+    const prevDelta = client.mergeTreeDeltaCallback, prevMaint = client.mergeTreeMaintenanceCallback;
+    client.mergeTreeDeltaCallback = (opArgs, args) => {
+        if (args.operation === 0) for (const { segment } of args.deltaSegments) segment.reset(); // onDelta INSERT (297-309)
+        if (prevDelta) prevDelta(opArgs, args);
+    };
+    client.mergeTreeMaintenanceCallback = (args) => {
+        if (prevMaint) prevMaint(args);
+        if (args.operation === -3) { // onMaintenance UNLINK (338-363)
+            let freed = [];
+            for (const { segment } of args.deltaSegments) {
+                if (isHandleValid(segment.start)) {
+                    freed = freed.concat(new Array(segment.cachedLength).fill(0).map((v, i) => i + segment.start));
+                }
+            }
+            for (const h of freed) table.free(h);
+        }
+    };
+}
+// getAllocatedHandle (157-183): getMaybeHandle is HandleCache.getHandle = the containing segment's start +
+// offset (handlecache.ts:77-88); a miss allocates through walkSegments(pos, pos + 1, splitRange = true)
+function getAllocatedHandle(client, pos) {
+    if (!(0 <= pos && pos < client.getLength())) throw new Error(`getAllocatedHandle: position ${pos} out of range`);
+    const { segment, offset } = client.getContainingSegment(pos);
+    let handle = segment.start + offset;
+    if (isHandleValid(handle)) return handle;
+    client.walkSegments((seg) => { seg.start = handle = curHandles.allocate(); return true; }, pos, pos + 1, undefined, true);
+    return handle;
 }
 
 // the delta stream (include/mt_oplog.h): per callback op, seq, per delta segment (position in the
@@ -317,6 +363,7 @@ function replayDoc(doc, to = opOff[doc + 1], deltas = false) {
         deltaWords[doc] = words;
         hookDeltas(client, words);
     }
+    if (withHandles) hookHandles(client, doc);
     if (stash !== null) {
         client.mergeTreeDeltaCallback = (opArgs, args) => { if (rebaseSink !== null) opsFromDelta(client, args, rebaseSink); };
     }
@@ -424,10 +471,12 @@ function dump(client) {
             const isText = s.type === "TextSegment", isMarker = s.type === "Marker";
             const kind = isText ? 0 : isMarker ? 1 : 2;
             const hasProps = s.properties !== undefined;
+            const hnd = s.type === "PermutationSegment" && s.start >= 1; // an allocated start
             const removed = s.removedSeq !== undefined;
             const ov = s.removedClientOverlap || [];
             o.u8(kind);
-            o.u8((hasProps ? 1 : 0) | (removed ? 2 : 0) | (s.localSeq !== undefined ? 4 : 0) | (s.localRemovedSeq !== undefined ? 8 : 0));
+            o.u8((hasProps ? 1 : 0) | (removed ? 2 : 0) | (s.localSeq !== undefined ? 4 : 0) | (s.localRemovedSeq !== undefined ? 8 : 0) |
+                (hnd ? 16 : 0));
             o.u8(ov.length);
             o.u8(s.segmentGroups.size);
             o.i32(s.cachedLength); o.i32(s.seq); o.i32(longOf(s.clientId));
@@ -445,6 +494,7 @@ function dump(client) {
                 const falsy = v !== null && typeof v !== "object" && !v;
                 o.u16(k); o.u16(id | (falsy ? FALSY : 0));
             }
+            if (hnd) o.i32(s.start); // MT_DF_HANDLE
             if (isText) for (let j = 0; j < s.text.length; j++) o.u16(s.text.charCodeAt(j));
         }
     });
@@ -455,6 +505,7 @@ async function main() {
 MT = await import(path.join(erased, "index.mjs"));
 ({ Client, TextSegment, Marker, LocalReference } = MT);
 ({ PermutationSegment } = await import(path.join(erased, "permutationSegment.mjs")));
+({ HandleTable, isHandleValid } = await import(path.join(erased, "handletable.mjs")));
 ({ SnapshotV1 } = await import(path.join(erased, "snapshotV1.mjs")));
 ({ SnapshotLegacy } = await import(path.join(erased, "snapshotlegacy.mjs")));
 const ndocs = opOff.length - 1;
@@ -605,6 +656,11 @@ if (Object.keys(refPositions).length) {
 fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
 if (queries.length) fs.writeFileSync(path.join(dir, "ref_answers.json"), JSON.stringify(answers));
 if (textQueries.length) fs.writeFileSync(path.join(dir, "ref_texts.json"), JSON.stringify(texts));
+if (withHandles) {
+    const snap = {};
+    for (const d of Object.keys(handleTables)) snap[d] = handleTables[d].snapshot();
+    fs.writeFileSync(path.join(dir, "ref_handles.json"), JSON.stringify(snap));
+}
 if (relQueries.length) fs.writeFileSync(path.join(dir, "ref_relpos.json"), JSON.stringify(relAnswers));
 console.log(JSON.stringify({ ndocs, errors: Object.keys(errs).length, seconds: secs }));
 }
