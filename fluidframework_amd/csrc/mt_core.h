@@ -444,11 +444,10 @@ struct Replica {
         for (int i = 0; i < (int)(sizeof(typename HT::Cold) / 16); i++) st4(dst + 4 * i, v[i]);
     }
 
+    /* the first error latches (the reference throws); apply() records the failing record's index in
+     * z.h.errOp once, after the record, instead of a store at every one of the many inlined fail sites */
     MT_HD void fail(int32_t e) {
-        if (h.err == E_OK) {
-            h.err = e;
-            z.h.errOp = h.opsDone;
-        }
+        if (h.err == E_OK) h.err = e;
     }
 
     /* ---- node allocation ------------------------------------------------------------- */
@@ -1665,7 +1664,8 @@ struct Replica {
     MT_HD bool ovl_has(int32_t s, int32_t client) const {
         uint64_t ov = cold(s).ovl;
         for (int32_t b = cold(s).ovx;; b = z.ovn[b]) {
-            for (int k = 0; k < NOVL; k++) {
+#pragma clang loop unroll(disable)
+            for (int k = 0; k < NOVL; k++) { /* a rare path: kept rolled (it is inlined at every visibility test) */
                 uint32_t e = (uint32_t)((ov >> (8 * k)) & 0xFF);
                 if (e == 0) return false;
                 if ((int32_t)e - 1 == client) return true;
@@ -1768,6 +1768,7 @@ struct Replica {
             }
         }
         z.h.ovFree = 0;
+#pragma clang loop unroll(disable)
         for (int32_t b = OVB - 1; b >= 1; b--)
             if (!((used >> b) & 1)) {
                 z.ovn[b] = (uint16_t)z.h.ovFree;
@@ -1789,6 +1790,7 @@ struct Replica {
         }
         I4 Q = ld4(&z.seq(s0));
         I4 BY = ld4(z.bytes4(s0)); /* {cli, rcli, flags, ng} of the 4 slots */
+        int32_t ovq = 0;
         for (int q = 0; q < 4; q++) {
             uint32_t by = (uint32_t)BY.x[q];
             uint8_t cq = (uint8_t)by, rcq = (uint8_t)(by >> 8), fq = (uint8_t)(by >> 16);
@@ -1801,10 +1803,19 @@ struct Replica {
                 if (rc == client || (rs != UNASSIGNED_SEQ && rs <= refSeq))
                     ok = false;
                 else if (fq & RF_OVL)
-                    ok = !ovl_has(s0 + q, client);
+                    ovq |= 1 << q; /* removedClientOverlap: looked up once below, not in each unrolled slot */
             }
             v[q] = ok ? L.x[q] : 0;
         }
+        int32_t hid = 0; /* slots a removedClientOverlap entry hides from the client */
+#pragma clang loop unroll(disable)
+        while (ovq) {
+            int32_t q = __builtin_ctz(ovq);
+            ovq &= ovq - 1;
+            if (ovl_has(s0 + q, client)) hid |= 1 << q;
+        }
+        for (int q = 0; q < 4; q++)
+            if ((hid >> q) & 1) v[q] = 0;
     }
     /* Total length under a perspective (getLength, mergeTree.ts:1610). */
     MT_HD int32_t length(int32_t refSeq, int32_t client) {
@@ -3379,22 +3390,50 @@ struct Replica {
         visit_run(sa, sb, refSeq, client, leaf, dl);
     }
 
+    /* markRangeRemoved (2640-2752) and annotateRange (2598-2638) share one range walk (range_op is inlined once
+     * for both: the replay kernel's code size is what its instruction cache sees) */
     MT_HD void mark_range_removed(int32_t start, int32_t end, int32_t refSeq, int32_t client, int32_t seq) {
+        range_edit(true, start, end, nullptr, 0, false, refSeq, client, seq);
+    }
+    MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t refSeq,
+                              int32_t client, int32_t seq) {
+        range_edit(false, start, end, kv, nkv, rewrite, refSeq, client, seq);
+    }
+    MT_HD void range_edit(bool remove, int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite,
+                          int32_t refSeq, int32_t client, int32_t seq) {
         bool hasL = seq == UNASSIGNED_SEQ;
         int32_t localSeq = hasL ? ++h.localSeq : 0;
         bool created = false;
+        const bool collab = h.collaborating;
         const uint32_t rcl = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
         const bool dl = dl_on();
-        bool dh = false; /* the REMOVE event's head goes out after the boundary splits' SPLIT events */
+        bool dh = false; /* the event's head goes out after the boundary splits' SPLIT events */
         int32_t dn = 0;
         const bool rf = refs_on();
         bool saved = false;
+        const int32_t dop = remove ? MT_DELTA_REMOVE : MT_DELTA_ANNOTATE;
         range_op(start, end, refSeq, client, [&](int32_t s, int32_t dpos) {
             if (dl && !dh) {
-                dhead(MT_DELTA_REMOVE);
+                dhead(dop);
                 dh = true;
             }
             h.sumW++;
+            if (!remove) { /* annotateRange's annotateSegment (2606-2621) */
+                if (dl) { /* deltaSegments.push({segment, propertyDeltas}) (mergeTree.ts:2608-2609) */
+                    dput(dpos);
+                    dput(z.len(s));
+                    prop_deltas(s, kv, nkv, rewrite, seq, collab);
+                    dn++;
+                }
+                add_props(s, kv, nkv, rewrite, seq, collab);
+                if (collab) {
+                    if (hasL)
+                        pending_add(s, localSeq, &created);
+                    else
+                        add_lru(s, seq);
+                }
+                return;
+            }
             int32_t rs = z.rseq(s), L = z.len(s);
             uint32_t b4 = ld_bytes4(s); /* {cli, rcli, flags, ng}: one read, one write */
             uint32_t fl = (b4 >> 16) & 0xFF;
@@ -3422,7 +3461,7 @@ struct Replica {
                 }
             }
             if constexpr (TILED) row_removed(s);
-            if (h.collaborating) {
+            if (collab) {
                 if (rs == UNASSIGNED_SEQ && client == h.localShort)
                     pending_add(s, localSeq, &created);
                 else
@@ -3431,41 +3470,7 @@ struct Replica {
         }, dl);
         if (saved) refs_slide(start, refSeq, client);
         if (dl) {
-            if (!dh) dhead(MT_DELTA_REMOVE);
-            dtail(dn);
-        }
-        if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni_soon();
-    }
-    MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t refSeq,
-                              int32_t client, int32_t seq) {
-        int32_t localSeq = seq == UNASSIGNED_SEQ ? ++h.localSeq : 0;
-        bool created = false;
-        bool collab = h.collaborating;
-        const bool dl = dl_on();
-        bool dh = false;
-        int32_t dn = 0;
-        range_op(start, end, refSeq, client, [&](int32_t s, int32_t dpos) {
-            h.sumW++;
-            if (dl) { /* deltaSegments.push({segment, propertyDeltas}) (mergeTree.ts:2608-2609) */
-                if (!dh) {
-                    dhead(MT_DELTA_ANNOTATE);
-                    dh = true;
-                }
-                dput(dpos);
-                dput(z.len(s));
-                prop_deltas(s, kv, nkv, rewrite, seq, collab);
-                dn++;
-            }
-            add_props(s, kv, nkv, rewrite, seq, collab);
-            if (collab) {
-                if (seq == UNASSIGNED_SEQ)
-                    pending_add(s, localSeq, &created);
-                else
-                    add_lru(s, seq);
-            }
-        }, dl);
-        if (dl) {
-            if (!dh) dhead(MT_DELTA_ANNOTATE);
+            if (!dh) dhead(dop);
             dtail(dn);
         }
         if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni_soon();
@@ -3702,8 +3707,10 @@ struct Replica {
     MT_HD void apply(const mt_op_rec& op, const Pools& p) {
         MT_PROF_SCOPE(PH_APPLY);
         if (h.err) return;
+        int32_t at = h.opsDone;
         apply_record(op, p);
         run_zamboni();
+        if (h.err) z.h.errOp = at;
     }
     /* One record. Every path that edits the tree ends in the one call site of insert_segments /
      * mark_range_removed / annotate_range below (each is inlined once). */
@@ -3821,10 +3828,8 @@ struct Replica {
             }
         }
         if (edit) {
-            if (kind == MT_OP_REMOVE)
-                mark_range_removed(o.pos1, o.pos2, eref, ecli, eseq);
-            else if (kind == MT_OP_ANNOTATE)
-                annotate_range(o.pos1, o.pos2, kv, nkv, rw, eref, ecli, eseq);
+            if (kind == MT_OP_REMOVE || kind == MT_OP_ANNOTATE)
+                range_edit(kind == MT_OP_REMOVE, o.pos1, o.pos2, kv, nkv, rw, eref, ecli, eseq);
             else
                 insert_segments(o, p, eref, ecli, eseq, epre, eprc, eat);
             if (remote) {
