@@ -385,6 +385,12 @@ struct Replica {
     /* The tree skeleton's small per-node arrays and the zamboni heap are reached through these
      * pointers: they point into the image by default, and the HBM-resident GPU kernel points them
      * at LDS copies for the duration of a replay (latency-critical, 3.5 KB per document). */
+    /* the image's rarely-used header fields (DocHdr, z.h) and the client tables (l2s / s2l): reached through
+     * these, so the HBM-resident replay kernel can stage them in LDS with the skeleton (every sequenced
+     * message reads l2s and bumps seqOps: no vector-memory round trip for either) */
+    DocHdr* zh;
+    uint8_t* l2s;
+    uint16_t* s2l;
     IX* lo;  /* lorder */
     IX* lp;  /* lpos */
     IX* npar;
@@ -405,7 +411,7 @@ struct Replica {
     int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
-        : d(doc), z(*doc.t), w(wave), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
+        : d(doc), z(*doc.t), w(wave), zh(&z.h), l2s(z.l2s), s2l(z.s2l), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
           nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen), cdel(nullptr), wcp(nullptr), wvs(nullptr),
           wlx(nullptr), cur(0) {
         if constexpr (TILED) {
@@ -418,19 +424,19 @@ struct Replica {
     }
 
     MT_HD void load_hdr() {
-#define MT_HF(f) h.f = w.uniform(z.h.f);
+#define MT_HF(f) h.f = w.uniform(zh->f);
         MT_HDR_FIELDS(MT_HF)
 #undef MT_HF
-        h.sumR = z.h.sumR;
-        h.sumW = z.h.sumW;
+        h.sumR = zh->sumR;
+        h.sumW = zh->sumW;
     }
     /* write the register header back to the image; every mutating entry point ends with it */
     MT_HD void commit() {
-#define MT_HF(f) z.h.f = h.f;
+#define MT_HF(f) zh->f = h.f;
         MT_HDR_FIELDS(MT_HF)
 #undef MT_HF
-        z.h.sumR = h.sumR;
-        z.h.sumW = h.sumW;
+        zh->sumR = h.sumR;
+        zh->sumW = h.sumW;
         w.sync();
     }
 
@@ -445,20 +451,20 @@ struct Replica {
     }
 
     /* the first error latches (the reference throws); apply() records the failing record's index in
-     * z.h.errOp once, after the record, instead of a store at every one of the many inlined fail sites */
+     * zh->errOp once, after the record, instead of a store at every one of the many inlined fail sites */
     MT_HD void fail(int32_t e) {
         if (h.err == E_OK) h.err = e;
     }
 
     /* ---- node allocation ------------------------------------------------------------- */
     MT_HD int32_t alloc_node(int8_t level) {
-        int32_t n = z.h.freeHead;
+        int32_t n = zh->freeHead;
         if (n < 0) {
             fail(E_CAPACITY);
             return -1;
         }
-        z.h.freeHead = npar[n];
-        z.h.nfree--;
+        zh->freeHead = npar[n];
+        zh->nfree--;
         npar[n] = -1;
         nch[n] = 0;
         nlev[n] = level;
@@ -477,10 +483,10 @@ struct Replica {
         w.sync();
     }
     MT_HD void free_node(int32_t n) {
-        npar[n] = (IX)z.h.freeHead;
+        npar[n] = (IX)zh->freeHead;
         nch[n] = 0;
-        z.h.freeHead = n;
-        z.h.nfree++;
+        zh->freeHead = n;
+        zh->nfree++;
     }
 
     /* ---- init -------------------------------------------------------------------------- */
@@ -514,11 +520,11 @@ struct Replica {
         }
         w.sync();
         if constexpr (TILED) rope_init();
-        z.h.nfreeRid = HT::S;
-        z.h.gcEpoch = 0;
-        z.h.freeHead = 1;
-        z.h.nfree = ncap - 1;
-        z.h.root = 0;
+        zh->nfreeRid = HT::S;
+        zh->gcEpoch = 0;
+        zh->freeHead = 1;
+        zh->nfree = ncap - 1;
+        zh->root = 0;
         npar[0] = -1;
         lo[0] = 0;
         lp[0] = 0;
@@ -529,8 +535,8 @@ struct Replica {
         h.collaborating = 0;
         h.localShort = -1; /* collabWindow.clientId = LocalClientId */
         h.localLong = -1;
-        z.h.nclients = 0;
-        z.h.nextSid = 1;
+        zh->nclients = 0;
+        zh->nextSid = 1;
         h.heapN = 0;
         h.memN = 0;
         h.gqHead = 0;
@@ -538,24 +544,24 @@ struct Replica {
         h.arenaTop = 0;
         h.arenaSide = 0;
         h.err = 0;
-        z.h.errOp = -1;
-        z.h.nkeys = 0;
+        zh->errOp = -1;
+        zh->nkeys = 0;
         h.opsDone = 0;
-        z.h.hwSlots = 0;
-        z.h.hwHeap = 0;
+        zh->hwSlots = 0;
+        zh->hwHeap = 0;
         h.nrows = 0;
-        z.h.seqOps = 0;
+        zh->seqOps = 0;
         h.sumR = 0;
         h.sumW = 0;
         h.localLen = 0;
         h.heapTop = 0;
-        z.h.loadPos = 0;
-        z.h.gidNext = 0;
-        z.h.ovTop = 1; /* block 0 is the null link */
-        z.h.ovFree = 0;
+        zh->loadPos = 0;
+        zh->gidNext = 0;
+        zh->ovTop = 1; /* block 0 is the null link */
+        zh->ovFree = 0;
         for (int32_t b = 0; b < HT::C; b += W::N) {
             int32_t i = b + w.lane();
-            if (i < HT::C) z.l2s[i] = 0xFF;
+            if (i < HT::C) l2s[i] = 0xFF;
         }
         if (Doc<HT>::has_fx(d.caps)) {
             DState* st = d.dstate();
@@ -925,7 +931,7 @@ struct Replica {
         bool has = z.flags(s) & RF_PROPS;
         int32_t cv = 0, pd = 0;
         if (has)
-            for (int32_t k = 0; k < z.h.nkeys; k++)
+            for (int32_t k = 0; k < zh->nkeys; k++)
                 if (z.keys[k] == kid) {
                     cv = cold(s).pv[k];
                     pd = cold(s).pk[k];
@@ -956,7 +962,7 @@ struct Replica {
             int32_t last = -1, nd = 0;
             for (;;) { /* candidate keys (the doc's key slots and the op's keys) in id order */
                 int32_t best = 0x7fffffff;
-                for (int32_t k = 0; k < z.h.nkeys; k++)
+                for (int32_t k = 0; k < zh->nkeys; k++)
                     if (z.keys[k] > last && z.keys[k] < best) best = z.keys[k];
                 for (int32_t j = 0; j < nkv; j++)
                     if (kv[j].key > last && kv[j].key < best) best = kv[j].key;
@@ -974,24 +980,24 @@ struct Replica {
     /* ---- clients (client.ts:637-661) --------------------------------------------------- */
     MT_HD int32_t short_of(int32_t longId) {
         if ((uint32_t)longId < (uint32_t)HT::C) {
-            int32_t s = z.l2s[longId];
+            int32_t s = l2s[longId];
             return s == 0xFF ? -1 : s;
         }
-        for (int32_t i = 0; i < z.h.nclients; i++)
-            if (z.s2l[i] == longId) return i;
+        for (int32_t i = 0; i < zh->nclients; i++)
+            if (s2l[i] == longId) return i;
         return -1;
     }
     MT_HD int32_t get_or_add_short(int32_t longId) {
         int32_t s = short_of(longId);
         if (s >= 0) return s;
-        int32_t n = z.h.nclients;
+        int32_t n = zh->nclients;
         if (n >= HT::C || n >= 0xFE) {
             fail(E_CAPACITY);
             return 0;
         }
-        z.s2l[n] = (uint16_t)longId;
-        if ((uint32_t)longId < (uint32_t)HT::C) z.l2s[longId] = (uint8_t)n;
-        z.h.nclients = n + 1;
+        s2l[n] = (uint16_t)longId;
+        if ((uint32_t)longId < (uint32_t)HT::C) l2s[longId] = (uint8_t)n;
+        zh->nclients = n + 1;
         return n;
     }
     /* startOrUpdateCollaboration (client.ts:1053-1073) + startCollaboration (mergeTree.ts:1287) */
@@ -1166,17 +1172,17 @@ struct Replica {
     }
     /* cold row ids */
     MT_HD int32_t alloc_rid() {
-        int32_t n = z.h.nfreeRid;
+        int32_t n = zh->nfreeRid;
         if (n <= 0) {
             fail(E_CAPACITY);
             return 0;
         }
-        z.h.nfreeRid = n - 1;
+        zh->nfreeRid = n - 1;
         return d.frid()[n - 1];
     }
     MT_HD void free_rid(int32_t r) {
         z.rgen[r]++;
-        d.frid()[z.h.nfreeRid++] = (IX)r;
+        d.frid()[zh->nfreeRid++] = (IX)r;
     }
     /* record leaf n as the holder of its first `cnt` rows */
     MT_HD void set_leaf_of_rows(int32_t n, int32_t cnt) {
@@ -1740,13 +1746,13 @@ struct Replica {
         }
     }
     MT_HD int32_t ovb_alloc() {
-        if (!z.h.ovFree && z.h.ovTop >= OVB) ovb_sweep();
+        if (!zh->ovFree && zh->ovTop >= OVB) ovb_sweep();
         int32_t b;
-        if (z.h.ovFree) {
-            b = z.h.ovFree;
-            z.h.ovFree = z.ovn[b];
-        } else if (z.h.ovTop < OVB) {
-            b = z.h.ovTop++;
+        if (zh->ovFree) {
+            b = zh->ovFree;
+            zh->ovFree = z.ovn[b];
+        } else if (zh->ovTop < OVB) {
+            b = zh->ovTop++;
         } else {
             fail(E_CAPACITY);
             return 0;
@@ -1767,12 +1773,12 @@ struct Replica {
                     for (int32_t b = cold(s).ovx; b; b = z.ovn[b]) used |= 1ull << b;
             }
         }
-        z.h.ovFree = 0;
+        zh->ovFree = 0;
 #pragma clang loop unroll(disable)
         for (int32_t b = OVB - 1; b >= 1; b--)
             if (!((used >> b) & 1)) {
-                z.ovn[b] = (uint16_t)z.h.ovFree;
-                z.h.ovFree = b;
+                z.ovn[b] = (uint16_t)zh->ovFree;
+                zh->ovFree = b;
             }
     }
     /* nodeLength (mergeTree.ts:1692-1732) of the 4 slots from s0 under (refSeq, client); 0 for
@@ -1934,7 +1940,7 @@ struct Replica {
                 nch[r] = 2;
                 npar[n] = (IX)r;
                 npar[nn] = (IX)r;
-                z.h.root = r;
+                zh->root = r;
                 return first;
             }
             node_insert_child(p, child_index(p, n) + 1, nn);
@@ -1995,8 +2001,8 @@ struct Replica {
         int32_t from = h.arenaSide, to = from ^ 1;
         uint16_t* src = arena_base(from);
         uint16_t* dst = arena_base(to);
-        int32_t ep = z.h.gcEpoch % 255 + 1;
-        z.h.gcEpoch = ep;
+        int32_t ep = zh->gcEpoch % 255 + 1;
+        zh->gcEpoch = ep;
         int32_t top = 0;
         for (int32_t k = 0; kvalid(k); k = knext(k)) {
             int32_t n = leaf_at(k), c = nch[n];
@@ -2153,8 +2159,8 @@ struct Replica {
     }
     /* pendingSegments.enqueue of a new group (the caller checked the ring's room) */
     MT_HD void group_push(int32_t localSeq) {
-        int32_t gid = z.h.gidNext;
-        z.h.gidNext = gid + 1;
+        int32_t gid = zh->gidNext;
+        zh->gidNext = gid + 1;
         int32_t q = (h.gqHead + h.gqN) % d.caps.gcap;
         d.gq()[q] = gid;
         d.gql()[q] = localSeq;
@@ -2186,7 +2192,7 @@ struct Replica {
         }
         int32_t k = n + 1; /* L[k] (1-based) lives at index k-1 */
         h.heapN = n + 1;
-        if (n + 1 > z.h.hwHeap) z.h.hwHeap = n + 1;
+        if (n + 1 > zh->hwHeap) zh->hwHeap = n + 1;
         uint8_t gen = z.rgen[rid];
         if constexpr (W::N >= 32) {
             int32_t l = w.lane();
@@ -2408,14 +2414,14 @@ struct Replica {
 
     /* ---- properties (segmentPropertiesManager.ts:35-111) ---------------------------- */
     MT_HD int32_t key_slot(uint16_t key) {
-        for (int32_t i = 0; i < z.h.nkeys; i++)
+        for (int32_t i = 0; i < zh->nkeys; i++)
             if (z.keys[i] == key) return i;
-        if (z.h.nkeys >= HT::K) {
+        if (zh->nkeys >= HT::K) {
             fail(E_CAPACITY); /* the profile's key slots: a larger profile holds more (capacity promotion) */
             return -1;
         }
-        z.keys[z.h.nkeys] = key;
-        return z.h.nkeys++;
+        z.keys[zh->nkeys] = key;
+        return zh->nkeys++;
     }
     MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
         typename HT::Cold& c = cold(s); /* the row id is read once, not after every store */
@@ -2427,7 +2433,7 @@ struct Replica {
         if (c.prw > 0 && seq != UNASSIGNED_SEQ && collaborating) return;
         if (rewrite) {
             if (collaborating && seq == UNASSIGNED_SEQ) c.prw++;
-            for (int32_t k = 0; k < z.h.nkeys; k++) {
+            for (int32_t k = 0; k < zh->nkeys; k++) {
                 if (c.pv[k] == 0) continue;
                 bool inNew = false;
                 for (int32_t j = 0; j < nkv; j++)
@@ -2747,12 +2753,12 @@ struct Replica {
         }
         uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
         if ((drop >> q) & 1) {
-            int32_t pos = z.h.nfreeRid + __builtin_popcountll(drop & below);
+            int32_t pos = zh->nfreeRid + __builtin_popcountll(drop & below);
             z.rgen[r.rid]++;
             d.frid()[pos] = (IX)r.rid;
         }
         int32_t ndrop = __builtin_popcountll(drop);
-        z.h.nfreeRid += ndrop;
+        zh->nfreeRid += ndrop;
         h.nrows -= ndrop;
         /* compaction: kept rows move down within their leaf; vacated slots get length 0 */
         uint64_t lmask = n >= 0 ? (0xFFull << (8 * li)) : 0ull;
@@ -3482,7 +3488,7 @@ struct Replica {
      * -2 more than one (the reference keeps the last one it registered; not modelled) */
     MT_HD int32_t marker_by_id(int32_t kid, int32_t vid) {
         int32_t slot = -1;
-        for (int32_t k = 0; k < z.h.nkeys; k++)
+        for (int32_t k = 0; k < zh->nkeys; k++)
             if (z.keys[k] == kid) slot = k;
         if (slot < 0 || (vid & ~MT_VALUE_FALSY) == 0) return -1;
         int32_t found = -1, n = 0;
@@ -3710,7 +3716,7 @@ struct Replica {
         int32_t at = h.opsDone;
         apply_record(op, p);
         run_zamboni();
-        if (h.err) z.h.errOp = at;
+        if (h.err) zh->errOp = at;
     }
     /* One record. Every path that edits the tree ends in the one call site of insert_segments /
      * mark_range_removed / annotate_range below (each is inlined once). */
@@ -3802,7 +3808,7 @@ struct Replica {
             remote = true;
             get_or_add_short(op.client);
             grouped = (op.kind & MT_OPF_GROUPED) != 0; /* a group member before the last (mt_oplog.h) */
-            if (!grouped) z.h.seqOps++; /* one sequenced message per group */
+            if (!grouped) zh->seqOps++; /* one sequenced message per group */
             if (grouped) {
             } else if constexpr (TILED) /* BASELINE.md tile formula, in 16-byte units: 4 B per chunk summary,
                                     64 B per window row, 640 B for the target chunk's leaves + leaf line */
@@ -3848,7 +3854,7 @@ struct Replica {
     }
     /* high-water mark of row slots in use (stats), noted whenever the leaf count grows */
     MT_HD void note_leaves() {
-        if (h.nleaf * MAXN > z.h.hwSlots) z.h.hwSlots = h.nleaf * MAXN;
+        if (h.nleaf * MAXN > zh->hwSlots) zh->hwSlots = h.nleaf * MAXN;
     }
     /* ---- snapshot load (SnapshotLoader, snapshotLoader.ts:86-228; records in mt_oplog.h) ------- */
     /* the fields of a loaded segment (SnapshotLoader.specToSegment, snapshotLoader.ts:96-126) on an
@@ -3904,8 +3910,8 @@ struct Replica {
             cnt = m;
             lvl++;
         }
-        z.h.root = hrd[0];
-        npar[z.h.root] = -1;
+        zh->root = hrd[0];
+        npar[zh->root] = -1;
     }
     /* one loaded segment into slot s (a fresh row): text / marker / permutation, props, merge info */
     MT_HD bool place_loaded(const mt_op_rec& op, const Pools& p, int32_t s) {
@@ -3974,8 +3980,8 @@ struct Replica {
              * length; its later members (GROUPED) go at the previous position + the previous
              * segment's whole length, removed or not */
             *ins = op;
-            ins->pos1 = (op.kind & MT_OPF_GROUPED) ? z.h.loadPos : h.localLen;
-            z.h.loadPos = ins->pos1 + seg_len(op);
+            ins->pos1 = (op.kind & MT_OPF_GROUPED) ? zh->loadPos : h.localLen;
+            zh->loadPos = ins->pos1 + seg_len(op);
             *cl = loader_client(op.client);
             int32_t rc = op.ref_seq > 0 ? loader_client((uint16_t)op.min_seq) : 0;
             if (h.err) return false;
@@ -4169,7 +4175,7 @@ struct Replica {
             }
         k->n += len;
     }
-    MT_HD int32_t long_of(uint8_t sh) const { return sh == LOCAL_CLIENT ? -1 : (int32_t)z.s2l[sh]; }
+    MT_HD int32_t long_of(uint8_t sh) const { return sh == LOCAL_CLIENT ? -1 : (int32_t)s2l[sh]; }
     /* Serial dump (only lane 0 writes the buffer); returns the byte count. */
     MT_HD int64_t dump(uint8_t* out, int64_t cap) {
         Sink k = {w.lane() == 0 ? out : 0, cap, 0, MT_FNV_OFFSET, false};

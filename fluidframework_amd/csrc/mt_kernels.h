@@ -65,11 +65,14 @@ __device__ inline void copy_image(HT* dst, const HT* src) {
  * HBM-resident kernel (the rest of the hot image stays in HBM). */
 template <class HT>
 struct Skel {
+    DocHdr zh; /* the image's header fields (the replica keeps the hot ones in registers) */
     int16_t lorder[HT::N], lpos[HT::N], nparent[HT::N];
     int8_t nchild[HT::N], nlevel[HT::N], nscour[HT::N];
     int32_t hseq[HT::H];
     int16_t hrid[HT::H];
     uint8_t hgen[HT::H];
+    uint8_t l2s[HT::C];  /* long -> short client id */
+    uint16_t s2l[HT::C]; /* short -> long */
 };
 /* The scan-critical subset of the skeleton (document order, child counts, parents): staged alone
  * where the whole Skel would cap residency through LDS (config-5 profile). */
@@ -85,14 +88,19 @@ __device__ inline void wave_copy(T* dst, const T* src, int n) {
 template <class HT>
 __device__ inline void skel_move(Skel<HT>& k, HT& z, bool in) {
     constexpr int N = HT::N, H = HT::H;
+    constexpr int C = HT::C, NH = (int)(sizeof(DocHdr) / 4);
     if (in) {
+        wave_copy((int32_t*)&k.zh, (const int32_t*)&z.h, NH);
         wave_copy(k.lorder, z.lorder, N), wave_copy(k.lpos, z.lpos, N), wave_copy(k.nparent, z.nparent, N);
         wave_copy(k.nchild, z.nchild, N), wave_copy(k.nlevel, z.nlevel, N), wave_copy(k.nscour, z.nscour, N);
         wave_copy(k.hseq, z.hseq, H), wave_copy(k.hrid, z.hrid, H), wave_copy(k.hgen, z.hgen, H);
+        wave_copy(k.l2s, z.l2s, C), wave_copy(k.s2l, z.s2l, C);
     } else {
+        wave_copy((int32_t*)&z.h, (const int32_t*)&k.zh, NH);
         wave_copy(z.lorder, k.lorder, N), wave_copy(z.lpos, k.lpos, N), wave_copy(z.nparent, k.nparent, N);
         wave_copy(z.nchild, k.nchild, N), wave_copy(z.nlevel, k.nlevel, N), wave_copy(z.nscour, k.nscour, N);
         wave_copy(z.hseq, k.hseq, H), wave_copy(z.hrid, k.hrid, H), wave_copy(z.hgen, k.hgen, H);
+        wave_copy(z.l2s, k.l2s, C), wave_copy(z.s2l, k.s2l, C);
     }
 }
 
@@ -158,12 +166,14 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
             for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
 #endif
     } else if constexpr (SKM == 1 && sizeof(Skel<HT>) <= 12288) {
+        static_assert(sizeof(DocHdr) % 4 == 0, "the header is copied in dwords");
         __shared__ __attribute__((aligned(16))) Skel<HT> sk;
         skel_move(sk, *v.t, true);
         __syncthreads();
         Replica<WaveGPU, HT, DL> r(v, WaveGPU());
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild, r.nlev = sk.nlevel;
         r.nsc = sk.nscour, r.hsq = sk.hseq, r.hrd = sk.hrid, r.hgn = sk.hgen;
+        r.zh = &sk.zh, r.l2s = sk.l2s, r.s2l = sk.s2l;
         r.replay(p);
         r.commit();
         __syncthreads();
