@@ -20,6 +20,7 @@
  * host build uses W::N = 1 so the same code runs serially.
  */
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #include <type_traits>
@@ -160,6 +161,9 @@ struct alignas(16) ColdRowT {
     uint8_t pk[K];  /* pendingKeyUpdateCount per key slot */
 };
 static_assert(sizeof(ColdRowT<8>) % 16 == 0 && sizeof(ColdRowT<24>) % 16 == 0, "cold rows are 16-byte granular");
+static_assert(offsetof(ColdRowT<8>, lrseq) == 4 && offsetof(ColdRowT<8>, toff) == 8 && offsetof(ColdRowT<8>, prw) == 12 &&
+                  offsetof(ColdRowT<8>, ovx) == 14 && offsetof(ColdRowT<24>, ovx) == 14,
+              "insert_segments writes lseq, lrseq, toff and {prw, gc, ovx} as one 16-byte unit");
 static_assert((2 * 8) % 16 == 0 && (2 * 24) % 16 == 0, "pv spans whole 16-byte units");
 
 /* Position index of the large-document profile ("tiled", config 4: >100k live rows).
@@ -3154,26 +3158,26 @@ struct Replica {
             int32_t rid = alloc_rid();
             z.rid[s] = (IX)rid;
             typename HT::Cold& c = d.cold()[rid]; /* row id kept in a register, not re-read per field */
-            c.gc = 0;
             z.len(s) = L;
             z.seq(s) = seq;
             z.rseq(s) = preRseq > 0 ? preRseq : NOREM;
-            c.lseq = localSeq;
-            c.lrseq = 0;
             int32_t fl = (marker ? RF_MARKER : 0) | (perm ? RF_PERM : 0) | (hasL ? RF_LSEQ : 0);
-            c.ovl = 0; /* pv / pk / prw: set up by add_props with RF_PROPS */
-            c.ovx = 0;
+            /* the cold row's first 16 bytes in one store: lseq, lrseq = 0, toff (text offset / a marker's refType
+             * / an unallocated PermutationSegment start), prw = gc = ovx = 0; then the inline overlap list. pv / pk
+             * are set up by add_props with RF_PROPS. */
+            I4 c0;
+            c0.x[0] = localSeq;
+            c0.x[1] = 0;
+            c0.x[2] = marker ? op.pos2 : perm ? 0 : off;
+            c0.x[3] = 0;
+            st4(&c, c0);
+            c.ovl = 0;
             z.rleaf[rid] = (IX)(s / MAXN);
             h.nrows++;
             h.sumW++;
             if (preRseq <= 0) h.localLen += L;
-            if (marker) {
-                c.toff = (uint32_t)op.pos2;
-            } else if (perm) {
-                c.toff = 0;
-            } else {
+            if (!marker && !perm) {
                 MT_PROF_SCOPE(PH_TEXT);
-                c.toff = (uint32_t)off;
                 int32_t last = arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
                 fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
             }
