@@ -139,11 +139,14 @@ struct DocHdr {
  * nfree, freeHead, nfreeRid, hwHeap, seqOps) stay in the image and are read and written there (z.h),
  * which keeps the replay loop's scalar registers for the fields every event touches. The last six
  * took the config-3 kernel from 227 to 79 VGPR spills and from 164.8M to 184.7M ops/s
- * (profiles/r02_spill_variants.txt). */
+ * (profiles/r02_spill_variants.txt). Since round 3 the replay kernels stage the image's header in LDS
+ * (Replica::zh), so eight more fields the local-edit, ack, arena and zamboni paths use (localSeq, gqHead,
+ * gqN, memN, arenaSide, heapTop, sumR, sumW) live there too: SGPR spills 1,637 -> 686 and +3 % on config 3
+ * (profiles/r03_ab_*.json). */
 #define MT_HDR_FIELDS(X)                                                                          \
-    X(nleaf) X(currentSeq) X(minSeq) X(localSeq) X(collaborating)   \
-    X(localShort) X(localLong) X(heapN) X(memN) X(gqHead) X(gqN) X(arenaTop) X(arenaSide) X(err) \
-    X(opsDone) X(nrows) X(localLen) X(heapTop)
+    X(nleaf) X(currentSeq) X(minSeq) X(collaborating)   \
+    X(localShort) X(localLong) X(heapN) X(arenaTop) X(err) \
+    X(opsDone) X(nrows) X(localLen)
 
 /* Cold per-row data, indexed by a row id that does not move when the row's slot moves. K = the
  * profile's property key slots per document. */
@@ -431,16 +434,14 @@ struct Replica {
 #define MT_HF(f) h.f = w.uniform(zh->f);
         MT_HDR_FIELDS(MT_HF)
 #undef MT_HF
-        h.sumR = zh->sumR;
-        h.sumW = zh->sumW;
+
     }
     /* write the register header back to the image; every mutating entry point ends with it */
     MT_HD void commit() {
 #define MT_HF(f) zh->f = h.f;
         MT_HDR_FIELDS(MT_HF)
 #undef MT_HF
-        zh->sumR = h.sumR;
-        zh->sumW = h.sumW;
+
         w.sync();
     }
 
@@ -535,18 +536,18 @@ struct Replica {
         h.nleaf = 1;
         h.currentSeq = 0;
         h.minSeq = 0;
-        h.localSeq = 0;
+        zh->localSeq = 0;
         h.collaborating = 0;
         h.localShort = -1; /* collabWindow.clientId = LocalClientId */
         h.localLong = -1;
         zh->nclients = 0;
         zh->nextSid = 1;
         h.heapN = 0;
-        h.memN = 0;
-        h.gqHead = 0;
-        h.gqN = 0;
+        zh->memN = 0;
+        zh->gqHead = 0;
+        zh->gqN = 0;
         h.arenaTop = 0;
-        h.arenaSide = 0;
+        zh->arenaSide = 0;
         h.err = 0;
         zh->errOp = -1;
         zh->nkeys = 0;
@@ -555,10 +556,10 @@ struct Replica {
         zh->hwHeap = 0;
         h.nrows = 0;
         zh->seqOps = 0;
-        h.sumR = 0;
-        h.sumW = 0;
+        zh->sumR = 0;
+        zh->sumW = 0;
         h.localLen = 0;
-        h.heapTop = 0;
+        zh->heapTop = 0;
         zh->loadPos = 0;
         zh->gidNext = 0;
         zh->ovTop = 1; /* block 0 is the null link */
@@ -2002,7 +2003,7 @@ struct Replica {
     /* copy all live text rows into the other half, in document order. A row id is moved once
      * per GC even if its slot is transiently duplicated (scour compacts a slab in place). */
     MT_HD void arena_gc() {
-        int32_t from = h.arenaSide, to = from ^ 1;
+        int32_t from = zh->arenaSide, to = from ^ 1;
         uint16_t* src = arena_base(from);
         uint16_t* dst = arena_base(to);
         int32_t ep = zh->gcEpoch % 255 + 1;
@@ -2020,7 +2021,7 @@ struct Replica {
                 top += L;
             }
         }
-        h.arenaSide = to;
+        zh->arenaSide = to;
         h.arenaTop = top;
         w.sync();
     }
@@ -2063,7 +2064,7 @@ struct Replica {
             z.flags(rs) = (uint8_t)((z.flags(rs) & ~RF_NL) | RF_NLK);
         }
         h.nrows++;
-        h.sumW += 2;
+        zh->sumW += 2;
         if constexpr (TILED) {
             if (z.tl.xf[rs] & XF_W) win_add(z.rid[rs]);
             if (z.tl.xf[rs] & XF_STABLE) { /* the halves may sit in two leaves after a leaf split */
@@ -2075,11 +2076,11 @@ struct Replica {
          * same pending groups (in the row's FIFO order = log order), appended at the end of each
          * group's segment list */
         if (z.ng(ls)) {
-            if (h.memN + z.ng(ls) > d.caps.mcap) mem_compact();
-            int32_t head = h.gqN ? d.gq()[h.gqHead % d.caps.gcap] : 0x7fffffff;
+            if (zh->memN + z.ng(ls) > d.caps.mcap) mem_compact();
+            int32_t head = zh->gqN ? d.gq()[zh->gqHead % d.caps.gcap] : 0x7fffffff;
             int32_t lrid = z.rid[ls];
             int32_t rrid = z.rid[rs];
-            int32_t m0 = h.memN;
+            int32_t m0 = zh->memN;
             for (int32_t b = 0; b < m0; b += W::N) {
                 int32_t i = b + w.lane();
                 int32_t g = i < m0 ? d.mgid()[i] : -1;
@@ -2103,10 +2104,10 @@ struct Replica {
 
     /* ---- segment groups ---------------------------------------------------------------- */
     MT_HD void mem_append(int32_t gid, int32_t rid) {
-        int32_t m = h.memN;
+        int32_t m = zh->memN;
         if (m >= d.caps.mcap) {
             mem_compact();
-            m = h.memN;
+            m = zh->memN;
             if (m >= d.caps.mcap) {
                 fail(E_CAPACITY);
                 return;
@@ -2114,12 +2115,12 @@ struct Replica {
         }
         d.mgid()[m] = gid;
         d.mrid()[m] = rid;
-        h.memN = m + 1;
+        zh->memN = m + 1;
     }
     /* drop entries of groups already acked (gid < head gid): wave stream compaction */
     MT_HD void mem_compact() {
-        int32_t head = h.gqN ? d.gq()[h.gqHead % d.caps.gcap] : 0x7fffffff;
-        int32_t n = h.memN, wpos = 0;
+        int32_t head = zh->gqN ? d.gq()[zh->gqHead % d.caps.gcap] : 0x7fffffff;
+        int32_t n = zh->memN, wpos = 0;
         for (int32_t b = 0; b < n; b += W::N) {
             int32_t i = b + w.lane();
             int32_t g = i < n ? d.mgid()[i] : -1;
@@ -2135,7 +2136,7 @@ struct Replica {
             w.sync();
             wpos += tot;
         }
-        h.memN = wpos;
+        zh->memN = wpos;
     }
     /* SegmentGroupCollection.enqueue (segmentGroupCollection.ts:28-31) */
     MT_HD void row_enqueue_group(int32_t s, int32_t gid) {
@@ -2152,23 +2153,23 @@ struct Replica {
      * beside the queue keeps each group's SegmentGroup.localSeq (findReconnectionPostition uses it). */
     MT_HD void pending_add(int32_t s, int32_t localSeq, bool* created) {
         if (!*created) {
-            if (h.gqN >= d.caps.gcap) {
+            if (zh->gqN >= d.caps.gcap) {
                 fail(E_CAPACITY);
                 return;
             }
             group_push(localSeq);
             *created = true;
         }
-        row_enqueue_group(s, d.gq()[(h.gqHead + h.gqN - 1) % d.caps.gcap]);
+        row_enqueue_group(s, d.gq()[(zh->gqHead + zh->gqN - 1) % d.caps.gcap]);
     }
     /* pendingSegments.enqueue of a new group (the caller checked the ring's room) */
     MT_HD void group_push(int32_t localSeq) {
         int32_t gid = zh->gidNext;
         zh->gidNext = gid + 1;
-        int32_t q = (h.gqHead + h.gqN) % d.caps.gcap;
+        int32_t q = (zh->gqHead + zh->gqN) % d.caps.gcap;
         d.gq()[q] = gid;
         d.gql()[q] = localSeq;
-        h.gqN++;
+        zh->gqN++;
     }
 
     /* ---- zamboni heap (collections.ts:212-264, LRUSegmentComparer mergeTree.ts:957-960) ---- */
@@ -2224,7 +2225,7 @@ struct Replica {
                 hgn[fin - 1] = gen;
             }
             w.sync();
-            if (fin == 1) h.heapTop = seq;
+            if (fin == 1) zh->heapTop = seq;
         } else {
             hrd[k - 1] = (IX)rid;
             hsq[k - 1] = seq;
@@ -2233,7 +2234,7 @@ struct Replica {
                 heap_swap((k >> 1) - 1, k - 1);
                 k >>= 1;
             }
-            h.heapTop = hsq[0];
+            zh->heapTop = hsq[0];
         }
     }
     /* Heap.get (collections.ts:227-233) + fixdown (249-263). On the GPU every maxSeq is read in one
@@ -2307,7 +2308,7 @@ struct Replica {
                 hgn[k - 1] = xg;
             }
             w.sync();
-            h.heapTop = d > 0 ? w.bcast(ms, 0) : xs;
+            zh->heapTop = d > 0 ? w.bcast(ms, 0) : xs;
         } else if constexpr (W::N == 64) {
             /* Larger heaps: the sift-down looks 5 levels ahead at a time. The 62 nodes of the 5-level
              * subtree below the current node are read in one pass (lane l: depth dd, offset off), the
@@ -2386,7 +2387,7 @@ struct Replica {
                 hgn[fin - 1] = xg;
             }
             w.sync();
-            h.heapTop = d > 0 ? w.bcast(ms, 0) : xs;
+            zh->heapTop = d > 0 ? w.bcast(ms, 0) : xs;
         } else {
             *rid = hrd[0];
             *seq = hsq[0];
@@ -2404,7 +2405,7 @@ struct Replica {
                 heap_swap(k - 1, j - 1);
                 k = j;
             }
-            if (cnt > 0) h.heapTop = hsq[0];
+            if (cnt > 0) zh->heapTop = hsq[0];
         }
     }
     /* addToLRUSet (mergeTree.ts:1306-1316) */
@@ -2517,7 +2518,7 @@ struct Replica {
         int32_t f = z.flags(a);
         if (f & RF_NLK) return (f & RF_NL) != 0;
         MT_PROF_SCOPE(PH_CAND);
-        bool nl = La > 0 && arena_base(h.arenaSide)[cold(a).toff + La - 1] == '\n';
+        bool nl = La > 0 && arena_base(zh->arenaSide)[cold(a).toff + La - 1] == '\n';
         z.flags(a) = (uint8_t)(f | RF_NLK | (nl ? RF_NL : 0));
         return nl;
     }
@@ -2534,7 +2535,7 @@ struct Replica {
             z.len(a) = La + Lb;
             return;
         }
-        uint16_t* base = arena_base(h.arenaSide);
+        uint16_t* base = arena_base(zh->arenaSide);
         int32_t ta = (int32_t)cold(a).toff, tb = (int32_t)cold(b).toff; /* both reads in one round trip */
         if (ta + La == h.arenaTop && h.arenaTop + Lb <= d.caps.acap) {
             int32_t off = arena_alloc(Lb);
@@ -2544,7 +2545,7 @@ struct Replica {
         } else {
             int32_t off = arena_alloc(La + Lb);
             if (off < 0) return;
-            base = arena_base(h.arenaSide); /* a GC may have switched halves (and moved both texts) */
+            base = arena_base(zh->arenaSide); /* a GC may have switched halves (and moved both texts) */
             arena_copy(base + off, base + cold(a).toff, La);
             arena_copy(base + off + La, base + cold(b).toff, Lb);
             cold(a).toff = (uint32_t)off;
@@ -2979,7 +2980,7 @@ struct Replica {
         if (!h.collaborating) return;
         for (int i = 0; i < 2; i++) {
             if (h.heapN < 1) break;
-            if (h.heapTop > h.minSeq) break; /* peek (mergeTree.ts:1465-1468) */
+            if (zh->heapTop > h.minSeq) break; /* peek (mergeTree.ts:1465-1468) */
             int32_t rid, mseq, gen;
             heap_pop(&rid, &mseq, &gen);
             int32_t s = slot_of(rid, gen); /* -1: unlinked or merged away since it was queued */
@@ -3137,7 +3138,7 @@ struct Replica {
                                int32_t preRseq = 0, uint8_t preRcli = 0, int32_t atT = -1) {
         int32_t pos = op.pos1;
         bool hasL = seq == UNASSIGNED_SEQ;
-        int32_t localSeq = hasL ? ++h.localSeq : 0;
+        int32_t localSeq = hasL ? ++zh->localSeq : 0;
         bool marker = op.seg_kind == MT_SEG_MARKER;
         bool perm = op.seg_kind == MT_SEG_PERM; /* PermutationSegment(length) (permutationvector.ts:47-51) */
         int32_t L = seg_len(op);
@@ -3174,11 +3175,11 @@ struct Replica {
             c.ovl = 0;
             z.rleaf[rid] = (IX)(s / MAXN);
             h.nrows++;
-            h.sumW++;
+            zh->sumW++;
             if (preRseq <= 0) h.localLen += L;
             if (!marker && !perm) {
                 MT_PROF_SCOPE(PH_TEXT);
-                int32_t last = arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
+                int32_t last = arena_copy(arena_base(zh->arenaSide) + off, p.text + op.text_off, L);
                 fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
             }
             /* {cli, rcli, flags, ng = 0} in one store */
@@ -3412,7 +3413,7 @@ struct Replica {
     MT_HD void range_edit(bool remove, int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite,
                           int32_t refSeq, int32_t client, int32_t seq) {
         bool hasL = seq == UNASSIGNED_SEQ;
-        int32_t localSeq = hasL ? ++h.localSeq : 0;
+        int32_t localSeq = hasL ? ++zh->localSeq : 0;
         bool created = false;
         const bool collab = h.collaborating;
         const uint32_t rcl = (uint8_t)(client < 0 ? LOCAL_CLIENT : client);
@@ -3427,7 +3428,7 @@ struct Replica {
                 dhead(dop);
                 dh = true;
             }
-            h.sumW++;
+            zh->sumW++;
             if (!remove) { /* annotateRange's annotateSegment (2606-2621) */
                 if (dl) { /* deltaSegments.push({segment, propertyDeltas}) (mergeTree.ts:2608-2609) */
                     dput(dpos);
@@ -3583,27 +3584,27 @@ struct Replica {
      * drops. Any number of segments; room for their new entries is made before the group leaves the head
      * (a compaction after that would drop its entries). */
     MT_HD void regen(int32_t kind) {
-        if (h.gqN <= 0) {
+        if (zh->gqN <= 0) {
             fail(E_ASSERT); /* "Segment group not at head of merge tree pending queue" */
             return;
         }
-        int32_t hq = h.gqHead % d.caps.gcap;
+        int32_t hq = zh->gqHead % d.caps.gcap;
         int32_t g0 = d.gq()[hq], lseq0 = d.gql()[hq];
-        int32_t mn = h.memN, cnt = 0;
+        int32_t mn = zh->memN, cnt = 0;
         for (int32_t b = 0; b < mn; b += W::N) {
             int32_t i = b + w.lane();
             cnt += w.sum(i < mn && d.mgid()[i] == g0 ? 1 : 0);
         }
-        if (h.memN + cnt > d.caps.mcap) {
+        if (zh->memN + cnt > d.caps.mcap) {
             mem_compact();
-            if (h.memN + cnt > d.caps.mcap) {
+            if (zh->memN + cnt > d.caps.mcap) {
                 fail(E_CAPACITY);
                 return;
             }
         }
-        h.gqHead = (h.gqHead + 1) % d.caps.gcap;
-        h.gqN--;
-        mn = h.memN;
+        zh->gqHead = (zh->gqHead + 1) % d.caps.gcap;
+        zh->gqN--;
+        mn = zh->memN;
         for (int32_t b = 0; b < mn; b += W::N) { /* mark: each member's coordinate (per lane: its leaf's 8 slots) */
             int32_t i = b + w.lane();
             if (i < mn && d.mgid()[i] == g0) {
@@ -3649,12 +3650,12 @@ struct Replica {
             else if (kind == MT_OP_ANNOTATE && !(z.flags(s) & RF_PROPS)) fail(E_ASSERT);
             if (!op) continue;
             int32_t pos = recon_pos(s, lseq0);
-            if (h.gqN >= d.caps.gcap) {
+            if (zh->gqN >= d.caps.gcap) {
                 fail(E_CAPACITY);
                 break;
             }
             group_push(lseq0); /* { segments: [], localSeq: segmentGroup.localSeq } (client.ts:755-758) */
-            row_enqueue_group(s, d.gq()[(h.gqHead + h.gqN - 1) % d.caps.gcap]);
+            row_enqueue_group(s, d.gq()[(zh->gqHead + zh->gqN - 1) % d.caps.gcap]);
             if (dl) {
                 dput(pos);
                 dput(z.len(s));
@@ -3668,12 +3669,12 @@ struct Replica {
 
     /* ---- ack (mergeTree.ts:1926-1953, BaseSegment.ack 486-521) ------------------------ */
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
-        if (h.gqN > 0) {
+        if (zh->gqN > 0) {
             MT_PROF_SCOPE(PH_ACK);
-            int32_t gid = d.gq()[h.gqHead % d.caps.gcap];
-            h.gqHead = (h.gqHead + 1) % d.caps.gcap;
-            h.gqN--;
-            int32_t mn = h.memN;
+            int32_t gid = d.gq()[zh->gqHead % d.caps.gcap];
+            zh->gqHead = (zh->gqHead + 1) % d.caps.gcap;
+            zh->gqN--;
+            int32_t mn = zh->memN;
             for (int32_t b = 0; b < mn; b += W::N) {
                 int32_t i = b + w.lane();
                 int32_t rd = i < mn ? d.mrid()[i] : 0;
@@ -3816,9 +3817,9 @@ struct Replica {
             if (grouped) {
             } else if constexpr (TILED) /* BASELINE.md tile formula, in 16-byte units: 4 B per chunk summary,
                                     64 B per window row, 640 B for the target chunk's leaves + leaf line */
-                h.sumR += (4 * z.tl.nchunk + 64 * z.tl.wN + 640) / 16;
+                zh->sumR += (4 * z.tl.nchunk + 64 * z.tl.wN + 640) / 16;
             else
-                h.sumR += h.nrows;
+                zh->sumR += h.nrows;
             if (kind != MT_OP_NOOP) {
                 if ((int32_t)op.client == h.localLong) {
                     ack(kind, kv, nkv, rw, op.seq);
@@ -3956,7 +3957,7 @@ struct Replica {
             cold(s).toff = 0;
         } else {
             cold(s).toff = (uint32_t)off;
-            int32_t last = arena_copy(arena_base(h.arenaSide) + off, p.text + op.text_off, L);
+            int32_t last = arena_copy(arena_base(zh->arenaSide) + off, p.text + op.text_off, L);
             fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
         }
         z.flags(s) = (uint8_t)fl;
@@ -4029,7 +4030,7 @@ struct Replica {
         if (end < -1) end = -1;   /* the same as -1: no row */
         int64_t n = 0;
         int32_t P = 0; /* position of the pass's first row */
-        const uint16_t* base = arena_base(h.arenaSide);
+        const uint16_t* base = arena_base(zh->arenaSide);
         if constexpr (W::N >= MAXN * MAXN) {
             /* 8 leaves x 8 slots per pass of the wave: each lane's row length under the perspective, one
              * scan for the positions and one for the output offsets, and every lane copies its own piece */
@@ -4194,9 +4195,9 @@ struct Replica {
     MT_HD void dump_to(Sink* o) {
         int32_t nsegs = 0;
         for (int32_t k = 0; kvalid(k); k = knext(k)) nsegs += nch[leaf_at(k)];
-        int32_t hdr[6] = {h.currentSeq, h.minSeq, h.localSeq, length_local(), nsegs, h.nleaf};
+        int32_t hdr[6] = {h.currentSeq, h.minSeq, zh->localSeq, length_local(), nsegs, h.nleaf};
         put_bytes(o, hdr, sizeof(hdr));
-        const uint16_t* base = arena_base(h.arenaSide);
+        const uint16_t* base = arena_base(zh->arenaSide);
         int32_t ordinal = -1;
         for (int32_t k = 0; kvalid(k); k = knext(k)) {
           ordinal++;

@@ -243,19 +243,20 @@ int32_t mth_get_handle(mth_store* s, int64_t doc, int32_t pos, int32_t* out) {
 
 /* pending segment groups (local ops in flight) of one doc */
 int32_t mth_pending(mth_store* s, int64_t doc) {
-    return with_replica(s, doc, [](auto& r) { return r.h.gqN; });
+    return with_replica(s, doc, [](auto& r) { return r.zh->gqN; });
 }
 
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {
     with_replica(s, doc, [&](auto& r) {
-        DocHdr* h = &r.h;
+        DocHdr* h = &r.h;    /* the fields the replica keeps in registers (MT_HDR_FIELDS) */
+        DocHdr* zh = r.zh;   /* the rest (the image header) */
         out8[0] = h->nleaf;
-        out8[1] = r.z.h.hwSlots;
-        out8[2] = h->hwHeap;
+        out8[1] = zh->hwSlots;
+        out8[2] = zh->hwHeap;
         out8[3] = h->heapN;
-        out8[4] = h->memN;
+        out8[4] = zh->memN;
         out8[5] = h->arenaTop;
-        out8[6] = (int32_t)(sizeof(r.z.nparent) / sizeof(r.z.nparent[0])) - h->nfree;
+        out8[6] = (int32_t)(sizeof(r.z.nparent) / sizeof(r.z.nparent[0])) - zh->nfree;
         out8[7] = h->opsDone;
         return 0;
     });

@@ -78,6 +78,7 @@ struct Skel {
  * where the whole Skel would cap residency through LDS (config-5 profile). */
 template <class HT>
 struct SkelLite {
+    DocHdr zh; /* the image's header fields */
     int16_t lorder[HT::N], lpos[HT::N], nparent[HT::N];
     int8_t nchild[HT::N];
 };
@@ -106,11 +107,13 @@ __device__ inline void skel_move(Skel<HT>& k, HT& z, bool in) {
 
 template <class HT>
 __device__ inline void skel_lite_move(SkelLite<HT>& k, HT& z, bool in) {
-    constexpr int N = HT::N;
+    constexpr int N = HT::N, NH = (int)(sizeof(DocHdr) / 4);
     if (in) {
+        wave_copy((int32_t*)&k.zh, (const int32_t*)&z.h, NH);
         wave_copy(k.lorder, z.lorder, N), wave_copy(k.lpos, z.lpos, N), wave_copy(k.nparent, z.nparent, N);
         wave_copy(k.nchild, z.nchild, N);
     } else {
+        wave_copy((int32_t*)&z.h, (const int32_t*)&k.zh, NH);
         wave_copy(z.lorder, k.lorder, N), wave_copy(z.lpos, k.lpos, N), wave_copy(z.nparent, k.nparent, N);
         wave_copy(z.nchild, k.nchild, N);
     }
@@ -157,6 +160,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
         __syncthreads();
         Replica<WaveGPU, HT, DL> r(v, WaveGPU());
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild;
+        r.zh = &sk.zh;
         r.replay(p);
         r.commit();
         __syncthreads();
@@ -207,9 +211,12 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     __shared__ int32_t cdel[HT::TL::NCH];
     __shared__ int32_t wcp[HT::TL::WCAP], wvs[HT::TL::WCAP];
     __shared__ uint8_t wlx[HT::TL::WCAP];
+    __shared__ DocHdr zhs; /* the image's header fields, staged for the replay */
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
     for (int i = threadIdx.x; i < HT::TL::NCH; i += WG) cdel[i] = 0;
+    Doc<HT> v = st.doc(d);
+    wave_copy((int32_t*)&zhs, (const int32_t*)&v.t->h, (int)(sizeof(DocHdr) / 4));
     __syncthreads();
     Pools p;
     p.ops = ops + op_off[d];
@@ -217,13 +224,16 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     p.text = text + text_off[d];
     p.props = props + props_off[d];
     p.kv = kv + kv_off[d];
-    Replica<WaveGPU, HT, DL> r(st.doc(d), WaveGPU());
+    Replica<WaveGPU, HT, DL> r(v, WaveGPU());
     r.cdel = cdel;
     r.wcp = wcp;
     r.wvs = wvs;
     r.wlx = wlx;
+    r.zh = &zhs;
     r.replay(p);
     r.commit();
+    __syncthreads();
+    wave_copy((int32_t*)&v.t->h, (const int32_t*)&zhs, (int)(sizeof(DocHdr) / 4));
 #ifdef MT_PROF
     if (prof && threadIdx.x == 0)
         for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];

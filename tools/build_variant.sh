@@ -9,6 +9,6 @@ D=$B/obj-libmtreplay_$NAME
 rm -rf "$D"; mkdir -p "$D"
 cp $B/obj-libmtreplay/*.o "$D/"
 U=$(basename "$UNIT" .hip)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c -o "$D/$U.o" "$ROOT/fluidframework_amd/csrc/$U.hip"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c -o "$D/$U.o" "$ROOT/fluidframework_amd/${CSRC:-csrc}/$U.hip"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o "$B/libmtreplay_$NAME.so" "$D"/*.o
 echo "$B/libmtreplay_$NAME.so"
