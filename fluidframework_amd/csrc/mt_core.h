@@ -147,6 +147,12 @@ struct DocHdr {
     X(nleaf) X(currentSeq) X(minSeq) X(collaborating)   \
     X(localShort) X(localLong) X(heapN) X(arenaTop) X(err) \
     X(opsDone) X(nrows) X(localLen)
+/* the register header: only these fields, so a stale read of one that lives in the image does not compile */
+struct RegHdr {
+#define MT_HF(f) int32_t f;
+    MT_HDR_FIELDS(MT_HF)
+#undef MT_HF
+};
 
 /* Cold per-row data, indexed by a row id that does not move when the row's slot moves. K = the
  * profile's property key slots per document. */
@@ -384,7 +390,7 @@ struct Replica {
     HT& z; /* the hot image */
     W w;
 
-    DocHdr h; /* the document header, held in registers (SGPRs on the GPU) while the replica runs */
+    RegHdr h; /* the header fields held in registers (SGPRs on the GPU) while the replica runs; the rest: zh */
 #ifdef MT_PROF
     uint64_t prof[PH_N] = {};
 #endif
@@ -2671,6 +2677,37 @@ struct Replica {
         uint64_t pairs = cand & (cand << 1) & ~0x0101010101010101ull;
         uint64_t keep = w.ballot(code == 1) | (cand & ~pairs);
         int32_t fl = r.flags;
+        /* Every test of an append that does not depend on the run's length, for all pairs at once (their cold
+         * reads overlap): a run's head has the properties, type, handle chain and last text unit of the run's
+         * last row (appends require equal properties, keep the head's start, and end with the appended
+         * text), so "head + row k" is decided by rows k-1 and k. Lane k: the pair (k-1, k). */
+        bool pairOk = false;
+        /* the shuffles read the predecessor lane, which may not be a pair's lane: outside the branch, where
+         * every lane is active */
+        int32_t lenP = w.shfl(r.len, q - 1), flP = w.shfl(fl, q - 1);
+        if ((pairs >> q) & 1) {
+            int32_t sp = n * MAXN + j - 1, sk = n * MAXN + j;
+            bool permPair = (flP & fl & RF_PERM) != 0;
+            /* localNetLength > 0 on both sides: a zero-length row (the empty right part of a split past a
+             * segment's end) is held and leaves no prevSegment (mergeTree.ts:1355-1383) */
+            pairOk = lenP > 0 && r.len > 0 && ((flP ^ fl) & RF_PROPS) == 0 &&
+                     (permPair || !((flP | fl) & RF_NOTEXT));
+            if (pairOk && (fl & RF_PROPS)) { /* matchProperties (properties.ts:61-92) */
+                const typename HT::Cold& ca = cold(sp);
+                const typename HT::Cold& cb = cold(sk);
+                for (int i = 0; i < HT::K / 8; i++)
+                    if (!eq4(ld4((const int32_t*)&ca.pv[8 * i]), ld4((const int32_t*)&cb.pv[8 * i]))) pairOk = false;
+            }
+            if (pairOk && permPair) { /* PermutationSegment.canAppend: handles follow, or both unallocated */
+                uint32_t sa = cold(sp).toff, sb = cold(sk).toff;
+                pairOk = sa == 0 ? sb == 0 : sb == sa + (uint32_t)lenP;
+            } else if (pairOk) { /* TextSegment.canAppend: the run does not end with "\n" (textSegment.ts:64) */
+                bool nl = (flP & RF_NLK) ? (flP & RF_NL) != 0
+                                         : arena_base(zh->arenaSide)[cold(sp).toff + lenP - 1] == '\n';
+                pairOk = !nl;
+            }
+        }
+        uint64_t okm = w.ballot(pairOk);
         int32_t prev = -1, prevLen = 0, prevFl = 0;
         int32_t alen = 0; /* an appended row's lane: its prevSegment's length right after the append */
         uint64_t m = pairs;
@@ -2684,30 +2721,18 @@ struct Replica {
             }
             int32_t lk = w.bcast(r.len, k);
             int32_t fk = w.bcast(fl, k);
-            bool ok = false;
-            bool permPair = (prevFl & fk & RF_PERM) != 0;
-            /* localNetLength > 0 on both sides: a zero-length row (the empty right part of a split past a
-             * segment's end) is held and leaves no prevSegment (mergeTree.ts:1355-1383) */
-            if (prevLen > 0 && lk > 0 &&
-                (permPair || (!((prevFl | fk) & RF_NOTEXT) && (prevLen <= GRANULARITY || lk <= GRANULARITY))) &&
-                ((prevFl ^ fk) & RF_PROPS) == 0) {
+            bool ok = (okm >> k) & 1;
+            /* the serial part: a text append needs either side <= TextSegment granularity (the run grows) */
+            if (ok && !(prevFl & fk & RF_PERM)) ok = prevLen <= GRANULARITY || lk <= GRANULARITY;
+            if (ok) {
                 int32_t sp = w.bcast(n, prev) * MAXN + (prev & (MAXN - 1));
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
-                ok = match_props(sp, sk);
-                if (ok && permPair) ok = perm_follows(sp, sk, prevLen);
-                if (ok && !permPair) {
-                    bool nl = ends_nl(sp, prevLen); /* caches RF_NLK/RF_NL in z.flags(sp) */
-                    prevFl = (prevFl & ~(RF_NLK | RF_NL)) | RF_NLK | (nl ? RF_NL : 0);
-                    ok = !nl;
-                }
-                if (ok) {
-                    if (refs_on()) refs_append(z.rid[sp], z.rid[sk], prevLen);
-                    append_text(sp, sk); /* updates z.len(sp) (read by a GC inside it) and its NL bits */
-                    prevLen += lk;
-                    prevFl = (prevFl & ~(RF_NLK | RF_NL)) | (fk & (RF_NLK | RF_NL));
-                    nlen = w.writelane(prevLen, prev, nlen);
-                    alen = w.writelane(prevLen, k, alen);
-                }
+                if (refs_on()) refs_append(z.rid[sp], z.rid[sk], prevLen);
+                append_text(sp, sk); /* updates z.len(sp) (read by a GC inside it) and its NL bits */
+                prevLen += lk;
+                prevFl = (prevFl & ~(RF_NLK | RF_NL)) | (fk & (RF_NLK | RF_NL));
+                nlen = w.writelane(prevLen, prev, nlen);
+                alen = w.writelane(prevLen, k, alen);
                 fl = w.writelane(prevFl, prev, fl);
             }
             if (!ok) {

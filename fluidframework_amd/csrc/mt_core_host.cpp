@@ -248,7 +248,7 @@ int32_t mth_pending(mth_store* s, int64_t doc) {
 
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8) {
     with_replica(s, doc, [&](auto& r) {
-        DocHdr* h = &r.h;    /* the fields the replica keeps in registers (MT_HDR_FIELDS) */
+        const RegHdr* h = &r.h; /* the fields the replica keeps in registers (MT_HDR_FIELDS) */
         DocHdr* zh = r.zh;   /* the rest (the image header) */
         out8[0] = h->nleaf;
         out8[1] = zh->hwSlots;

@@ -19,6 +19,7 @@ struct WaveHost {
     int32_t max(int32_t v) const { return v; }
     uint64_t ballot(bool p) const { return p ? 1ull : 0ull; }
     int32_t bcast(int32_t v, int) const { return v; }
+    int32_t shfl(int32_t v, int) const { return v; }
     static int32_t uniform(int32_t v) { return v; }
     int32_t writelane(int32_t v, int, int32_t) const { return v; }
     static int ffs(uint64_t m) { return __builtin_ctzll(m); }
@@ -78,6 +79,8 @@ struct WaveGPU {
         return __builtin_amdgcn_readlane(v, l);
     }
     __device__ __attribute__((always_inline)) static int ffs(uint64_t m) { return __builtin_ctzll(m); }
+    /* every lane takes v of lane src (per-lane source: ds_bpermute) */
+    __device__ __attribute__((always_inline)) int32_t shfl(int32_t v, int src) const { return __shfl(v, src); }
     /* per-lane add into wave-shared scratch (LDS in the tiled replay kernel) */
     __device__ __attribute__((always_inline)) static void atomic_add(int32_t* p, int32_t v) { atomicAdd(p, v); }
     /* Order the wave's memory accesses between lanes. One wavefront replays one document, so every
