@@ -195,8 +195,9 @@ struct TileState {
 template <int N>
 struct TileState<N, true> {
     static constexpr int CH = 64;       /* leaves per chunk */
-    static constexpr int NCH = N / 32;  /* chunk capacity (the kernel's LDS scratch holds NCH counters) */
-    static constexpr int WCAP = 4096;   /* window-set capacity (rows; ~500 in use at lag 64) */
+    static constexpr int NCH = N / 64;  /* chunk capacity (a 1M-op config-4 document peaks at ~2,100 chunks);
+                                           the tiled kernel stages the chunk arrays in LDS */
+    static constexpr int WCAP = 2048;   /* window-set capacity (rows; under 100 in use at lag 64) */
     int32_t nchunk, wN, cfree, nfreeChunk;
     int32_t lst[N];         /* leaf node -> sum of its STABLE rows' lengths */
     int32_t lch[N];         /* leaf node -> chunk id */
@@ -420,18 +421,35 @@ struct Replica {
     int32_t* wcp;
     int32_t* wvs;
     uint8_t* wlx;
+    /* tiled profile: the rope's chunk arrays (document order, summaries, positions, leaf counts) and the
+     * window set, reached through these: they point into the image by default, and the tiled replay kernel
+     * points them at LDS copies for the duration of a replay (every position search and summary update
+     * reads them: ~3 dependent vector-memory round trips per search fewer) */
+    int32_t* tcord;
+    int32_t* tcst;
+    int32_t* tcpos;
+    int32_t* tccnt;
+    int32_t* twrid;
+    uint8_t* twgen;
     int64_t cur; /* index of the record being applied in the current Pools (snapshot reload reads ahead) */
     int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
         : d(doc), z(*doc.t), w(wave), zh(&z.h), l2s(z.l2s), s2l(z.s2l), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
           nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen), cdel(nullptr), wcp(nullptr), wvs(nullptr),
-          wlx(nullptr), cur(0) {
+          wlx(nullptr), tcord(nullptr), tcst(nullptr), tcpos(nullptr), tccnt(nullptr), twrid(nullptr), twgen(nullptr),
+          cur(0) {
         if constexpr (TILED) {
             cdel = z.tl.sdel;
             wcp = z.tl.swcp;
             wvs = z.tl.swvs;
             wlx = z.tl.swlx;
+            tcord = z.tl.cord;
+            tcst = z.tl.cst;
+            tcpos = z.tl.cpos;
+            tccnt = z.tl.ccnt;
+            twrid = z.tl.wrid;
+            twgen = z.tl.wgen;
         }
         load_hdr();
     }
@@ -871,7 +889,7 @@ struct Replica {
     }
     MT_HD int32_t kprev(int32_t k) const { /* the leaf position before k (k > 0) */
         if constexpr (TILED)
-            return (k & 63) ? k - 1 : ((((k >> 6) - 1) << 6) | (z.tl.ccnt[z.tl.cord[(k >> 6) - 1]] - 1));
+            return (k & 63) ? k - 1 : ((((k >> 6) - 1) << 6) | (tccnt[tcord[(k >> 6) - 1]] - 1));
         else
             return k - 1;
     }
@@ -1070,25 +1088,25 @@ struct Replica {
      * TILED; positions increase in document order (with gaps when tiled). */
     MT_HD int32_t leaf_at(int32_t k) const {
         if constexpr (TILED)
-            return z.tl.cleaf[z.tl.cord[k >> 6]][k & 63];
+            return z.tl.cleaf[tcord[k >> 6]][k & 63];
         else
             return lo[k];
     }
     MT_HD int32_t kpos(int32_t n) const {
         if constexpr (TILED)
-            return (z.tl.cpos[z.tl.lch[n]] << 6) | z.tl.lix[n];
+            return (tcpos[z.tl.lch[n]] << 6) | z.tl.lix[n];
         else
             return lp[n];
     }
     MT_HD bool kvalid(int32_t k) const {
         if constexpr (TILED)
-            return k >= 0 && (k >> 6) < z.tl.nchunk && (k & 63) < z.tl.ccnt[z.tl.cord[k >> 6]];
+            return k >= 0 && (k >> 6) < z.tl.nchunk && (k & 63) < tccnt[tcord[k >> 6]];
         else
             return k < h.nleaf;
     }
     MT_HD int32_t knext(int32_t k) const {
         if constexpr (TILED)
-            return (k & 63) + 1 < z.tl.ccnt[z.tl.cord[k >> 6]] ? k + 1 : ((k >> 6) + 1) << 6;
+            return (k & 63) + 1 < tccnt[tcord[k >> 6]] ? k + 1 : ((k >> 6) + 1) << 6;
         else
             return k + 1;
     }
@@ -1226,17 +1244,17 @@ struct Replica {
         for (int32_t b = 0; b < NCH; b += W::N) {
             int32_t i = b + w.lane();
             if (i < NCH) {
-                t.cpos[i] = i + 1; /* free list */
-                t.ccnt[i] = 0;
+                tcpos[i] = i + 1; /* free list */
+                tccnt[i] = 0;
                 t.sdel[i] = 0;
             }
         }
         w.sync();
         t.nchunk = 1;
-        t.cord[0] = 0;
-        t.cpos[0] = 0;
-        t.cst[0] = 0;
-        t.ccnt[0] = 1;
+        tcord[0] = 0;
+        tcpos[0] = 0;
+        tcst[0] = 0;
+        tccnt[0] = 1;
         t.cleaf[0][0] = 0;
         t.cfree = 1;
         t.nfreeChunk = NCH - 1;
@@ -1253,14 +1271,14 @@ struct Replica {
             fail(E_CAPACITY);
             return -1;
         }
-        t.cfree = t.cpos[c];
+        t.cfree = tcpos[c];
         t.nfreeChunk--;
-        t.ccnt[c] = 0;
+        tccnt[c] = 0;
         return c;
     }
     MT_HD void chunk_free(int32_t c) {
         auto& t = z.tl;
-        t.cpos[c] = t.cfree;
+        tcpos[c] = t.cfree;
         t.cfree = c;
         t.nfreeChunk++;
     }
@@ -1275,12 +1293,12 @@ struct Replica {
             if (W::N == 1) b = delta > 0 ? cnt - 1 - c : c;
             int32_t i = from + b + (W::N == 1 ? 0 : w.lane());
             bool ok = i < n && i >= from;
-            int32_t id = ok ? t.cord[i] : 0, sm = ok ? t.cst[i] : 0;
+            int32_t id = ok ? tcord[i] : 0, sm = ok ? tcst[i] : 0;
             w.sync();
             if (ok) {
-                t.cord[i + delta] = id;
-                t.cst[i + delta] = sm;
-                t.cpos[id] = i + delta;
+                tcord[i + delta] = id;
+                tcst[i + delta] = sm;
+                tcpos[id] = i + delta;
             }
             w.sync();
         }
@@ -1313,14 +1331,14 @@ struct Replica {
         auto& t = z.tl;
         constexpr int32_t CH = HT::TL::CH, HALF = CH / 2;
         int32_t c = t.lch[a], i = t.lix[a] + 1;
-        if (t.ccnt[c] >= CH) {
+        if (tccnt[c] >= CH) {
             int32_t c2 = chunk_alloc();
             if (c2 < 0) return;
-            int32_t p = t.cpos[c];
+            int32_t p = tcpos[c];
             cord_shift(p + 1, 1);
             t.nchunk++;
-            t.cord[p + 1] = c2;
-            t.cpos[c2] = p + 1;
+            tcord[p + 1] = c2;
+            tcpos[c2] = p + 1;
             int32_t moved = 0;
             for (int32_t bb = 0; bb < HALF; bb += W::N) {
                 int32_t l = bb + w.lane();
@@ -1335,34 +1353,34 @@ struct Replica {
                 moved += w.sum(v);
             }
             w.sync();
-            t.ccnt[c2] = HALF;
-            t.ccnt[c] = HALF;
-            t.cst[p + 1] = moved;
-            t.cst[p] -= moved;
+            tccnt[c2] = HALF;
+            tccnt[c] = HALF;
+            tcst[p + 1] = moved;
+            tcst[p] -= moved;
             if (i >= HALF) {
                 c = c2;
                 i -= HALF;
             }
         }
-        int32_t cnt = t.ccnt[c];
+        int32_t cnt = tccnt[c];
         chunk_shift(c, i, cnt, 1);
         t.cleaf[c][i] = b;
         t.lch[b] = c;
         t.lix[b] = (uint8_t)i;
-        t.ccnt[c] = cnt + 1;
-        t.cst[t.cpos[c]] += t.lst[b];
+        tccnt[c] = cnt + 1;
+        tcst[tcpos[c]] += t.lst[b];
         w.sync();
     }
     /* leaf b leaves the document order (its STABLE length leaves its chunk's summary) */
     MT_HD void rope_remove(int32_t b) {
         MT_PROF_SCOPE(PH_ROPE);
         auto& t = z.tl;
-        int32_t c = t.lch[b], i = t.lix[b], p = t.cpos[c];
-        t.cst[p] -= t.lst[b];
+        int32_t c = t.lch[b], i = t.lix[b], p = tcpos[c];
+        tcst[p] -= t.lst[b];
         t.lst[b] = 0;
-        int32_t cnt = t.ccnt[c];
+        int32_t cnt = tccnt[c];
         chunk_shift(c, i + 1, cnt, -1);
-        t.ccnt[c] = cnt - 1;
+        tccnt[c] = cnt - 1;
         if (cnt - 1 == 0) {
             cord_shift(p + 1, -1);
             t.nchunk--;
@@ -1373,7 +1391,7 @@ struct Replica {
     MT_HD void lst_add(int32_t n, int32_t d) {
         auto& t = z.tl;
         t.lst[n] += d;
-        t.cst[t.cpos[t.lch[n]]] += d;
+        tcst[tcpos[t.lch[n]]] += d;
     }
     /* recompute leaf n's STABLE length from its rows */
     MT_HD void leaf_restat(int32_t n) {
@@ -1400,8 +1418,8 @@ struct Replica {
             fail(E_CAPACITY);
             return;
         }
-        t.wrid[t.wN] = rid;
-        t.wgen[t.wN] = z.rgen[rid];
+        twrid[t.wN] = rid;
+        twgen[t.wN] = z.rgen[rid];
         t.wN++;
     }
     /* a row just placed (insert): STABLE if already settled (non-collaborating edits), else W */
@@ -1447,8 +1465,8 @@ struct Replica {
             for (int q = 0; q < NB; q++) { /* the entries */
                 int32_t i = b0 + q * W::N + w.lane();
                 bool ok = i < n;
-                rd[q] = ok ? t.wrid[i] : 0;
-                g[q] = ok ? t.wgen[i] : -1;
+                rd[q] = ok ? twrid[i] : 0;
+                g[q] = ok ? twgen[i] : -1;
             }
 #pragma unroll
             for (int q = 0; q < NB; q++) { /* the row is still the one added: its leaf */
@@ -1472,7 +1490,7 @@ struct Replica {
                 if (keep[q]) {
                     v[q] = vis(s[q], refSeq, client);
                     int32_t l = s[q] / MAXN;
-                    cp[q] = t.cpos[t.lch[l]];
+                    cp[q] = tcpos[t.lch[l]];
                     lx[q] = t.lix[l];
                 }
             }
@@ -1495,8 +1513,8 @@ struct Replica {
                 w.sync();
                 if (keep[q]) {
                     int32_t o = wpos + off;
-                    t.wrid[o] = rd[q];
-                    t.wgen[o] = (uint8_t)g[q];
+                    twrid[o] = rd[q];
+                    twgen[o] = (uint8_t)g[q];
                     wcp[o] = cp[q];
                     wlx[o] = (uint8_t)lx[q];
                     wvs[o] = v[q];
@@ -1530,7 +1548,7 @@ struct Replica {
         for (int32_t b = 0; b < nc; b += 4 * W::N) {
             int32_t p0 = b + 4 * w.lane();
             int32_t v[4];
-            for (int q = 0; q < 4; q++) v[q] = p0 + q < nc ? t.cst[p0 + q] + cdel[p0 + q] : 0;
+            for (int q = 0; q < 4; q++) v[q] = p0 + q < nc ? tcst[p0 + q] + cdel[p0 + q] : 0;
             int32_t tot;
             int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
             int32_t hq = -1, hp = 0;
@@ -1552,7 +1570,7 @@ struct Replica {
         }
         if (cpf < 0) return -1;
         /* leaves of the chunk: STABLE lengths + the window rows that sit in them */
-        int32_t c = t.cord[cpf], cnt = t.ccnt[c];
+        int32_t c = tcord[cpf], cnt = tccnt[c];
         int32_t nw = t.wN;
         int32_t ldel[HT::TL::CH / (W::N < 64 ? W::N : 64) + 1] = {};
         for (int32_t b = 0; b < nw; b += W::N) {
@@ -1661,7 +1679,7 @@ struct Replica {
         int32_t nc = z.tl.nchunk;
         for (int32_t b = 0; b < nc; b += W::N) {
             int32_t p = b + w.lane();
-            total += w.sum(p < nc ? z.tl.cst[p] : 0);
+            total += w.sum(p < nc ? tcst[p] : 0);
         }
         return total;
     }
@@ -3373,7 +3391,7 @@ struct Replica {
             int32_t nc = z.tl.nchunk;
             for (int32_t b = 0; b < nc; b += W::N) {
                 int32_t p = b + w.lane();
-                total += w.sum(p < nc ? z.tl.cst[p] : 0);
+                total += w.sum(p < nc ? tcst[p] : 0);
             }
             if (start >= total || end <= start) {
                 win_clear();
@@ -4142,10 +4160,10 @@ struct Replica {
             if (tiles_cover(refSeq, client)) { /* chunks before, leaves before in the chunk, rows before */
                 auto& t = z.tl;
                 win_pass(refSeq, client);
-                int32_t cp = k0 >> 6, li = k0 & 63, c = t.cord[cp];
+                int32_t cp = k0 >> 6, li = k0 & 63, c = tcord[cp];
                 for (int32_t b = 0; b < cp; b += W::N) {
                     int32_t p = b + w.lane();
-                    total += w.sum(p < cp ? t.cst[p] + cdel[p] : 0);
+                    total += w.sum(p < cp ? tcst[p] + cdel[p] : 0);
                 }
                 for (int32_t b = 0; b < li; b += W::N) {
                     int32_t l = b + w.lane();

@@ -208,15 +208,26 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
                                                      const int64_t* props_off, const mt_kv* kv, const int64_t* kv_off,
                                                      uint64_t* prof) {
     static_assert(HT::TILED, "tiled profile only");
-    __shared__ int32_t cdel[HT::TL::NCH];
-    __shared__ int32_t wcp[HT::TL::WCAP], wvs[HT::TL::WCAP];
-    __shared__ uint8_t wlx[HT::TL::WCAP];
+    constexpr int NCH = HT::TL::NCH, WCAP = HT::TL::WCAP;
+    __shared__ int32_t cdel[NCH];
+    __shared__ int32_t wcp[WCAP], wvs[WCAP];
+    __shared__ uint8_t wlx[WCAP];
     __shared__ DocHdr zhs; /* the image's header fields, staged for the replay */
+    /* the rope's chunk arrays and the window set, staged for the replay (written back at the end) */
+    __shared__ int32_t lcord[NCH], lcst[NCH], lcpos[NCH], lccnt[NCH], lwrid[WCAP];
+    __shared__ __attribute__((aligned(16))) uint8_t lwgen[WCAP];
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
-    for (int i = threadIdx.x; i < HT::TL::NCH; i += WG) cdel[i] = 0;
+    for (int i = threadIdx.x; i < NCH; i += WG) cdel[i] = 0;
     Doc<HT> v = st.doc(d);
+    auto& tl = v.t->tl;
     wave_copy((int32_t*)&zhs, (const int32_t*)&v.t->h, (int)(sizeof(DocHdr) / 4));
+    wave_copy(lcord, tl.cord, NCH);
+    wave_copy(lcst, tl.cst, NCH);
+    wave_copy(lcpos, tl.cpos, NCH);
+    wave_copy(lccnt, tl.ccnt, NCH);
+    wave_copy(lwrid, tl.wrid, WCAP);
+    wave_copy((int32_t*)lwgen, (const int32_t*)tl.wgen, WCAP / 4);
     __syncthreads();
     Pools p;
     p.ops = ops + op_off[d];
@@ -230,10 +241,22 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     r.wvs = wvs;
     r.wlx = wlx;
     r.zh = &zhs;
+    r.tcord = lcord;
+    r.tcst = lcst;
+    r.tcpos = lcpos;
+    r.tccnt = lccnt;
+    r.twrid = lwrid;
+    r.twgen = lwgen;
     r.replay(p);
     r.commit();
     __syncthreads();
     wave_copy((int32_t*)&v.t->h, (const int32_t*)&zhs, (int)(sizeof(DocHdr) / 4));
+    wave_copy(tl.cord, lcord, NCH);
+    wave_copy(tl.cst, lcst, NCH);
+    wave_copy(tl.cpos, lcpos, NCH);
+    wave_copy(tl.ccnt, lccnt, NCH);
+    wave_copy(tl.wrid, lwrid, WCAP);
+    wave_copy((int32_t*)tl.wgen, (const int32_t*)lwgen, WCAP / 4);
 #ifdef MT_PROF
     if (prof && threadIdx.x == 0)
         for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
