@@ -197,7 +197,7 @@ struct TileState<N, true> {
     static constexpr int CH = 64;       /* leaves per chunk */
     static constexpr int NCH = N / 64;  /* chunk capacity (a 1M-op config-4 document peaks at ~2,100 chunks);
                                            the tiled kernel stages the chunk arrays in LDS */
-    static constexpr int WCAP = 2048;   /* window-set capacity (rows; under 100 in use at lag 64) */
+    static constexpr int WCAP = 4096;   /* window-set capacity (rows; under 100 in use at lag 64, ~1,200 at lag 8,000) */
     int32_t nchunk, wN, cfree, nfreeChunk;
     int32_t lst[N];         /* leaf node -> sum of its STABLE rows' lengths */
     int32_t lch[N];         /* leaf node -> chunk id */
@@ -210,6 +210,7 @@ struct TileState<N, true> {
     int32_t cleaf[NCH][CH]; /* chunk id -> its leaves in order */
     int32_t wrid[WCAP];     /* window set: row ids */
     uint8_t wgen[WCAP];     /* their generations when added */
+    int32_t wslot[WCAP];    /* the slot each was last seen in (a hint: rows move; checked before use) */
     /* host-build scratch of a position search (the GPU kernel uses LDS instead) */
     int32_t sdel[NCH];
     int32_t swcp[WCAP], swvs[WCAP];
@@ -431,13 +432,14 @@ struct Replica {
     int32_t* tccnt;
     int32_t* twrid;
     uint8_t* twgen;
+    int32_t* twslot;
     int64_t cur; /* index of the record being applied in the current Pools (snapshot reload reads ahead) */
     int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
         : d(doc), z(*doc.t), w(wave), zh(&z.h), l2s(z.l2s), s2l(z.s2l), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
           nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen), cdel(nullptr), wcp(nullptr), wvs(nullptr),
-          wlx(nullptr), tcord(nullptr), tcst(nullptr), tcpos(nullptr), tccnt(nullptr), twrid(nullptr), twgen(nullptr),
+          wlx(nullptr), tcord(nullptr), tcst(nullptr), tcpos(nullptr), tccnt(nullptr), twrid(nullptr), twgen(nullptr), twslot(nullptr),
           cur(0) {
         if constexpr (TILED) {
             cdel = z.tl.sdel;
@@ -450,6 +452,7 @@ struct Replica {
             tccnt = z.tl.ccnt;
             twrid = z.tl.wrid;
             twgen = z.tl.wgen;
+            twslot = z.tl.wslot;
         }
         load_hdr();
     }
@@ -1408,11 +1411,15 @@ struct Replica {
         w.sync();
     }
     /* a row is settled when its insert and (if any) its removal are sequenced at or below minSeq */
+    MT_HD bool settled_of(const RowView& r) const {
+        return r.seq != UNASSIGNED_SEQ && r.seq <= h.minSeq &&
+               (r.rseq == NOREM || (r.rseq != UNASSIGNED_SEQ && r.rseq <= h.minSeq));
+    }
     MT_HD bool settled(int32_t s) const {
         int32_t sq = z.seq(s), rs = z.rseq(s);
         return sq != UNASSIGNED_SEQ && sq <= h.minSeq && (rs == NOREM || (rs != UNASSIGNED_SEQ && rs <= h.minSeq));
     }
-    MT_HD void win_add(int32_t rid) {
+    MT_HD void win_add(int32_t rid, int32_t s) {
         auto& t = z.tl;
         if (t.wN >= HT::TL::WCAP) {
             fail(E_CAPACITY);
@@ -1420,6 +1427,7 @@ struct Replica {
         }
         twrid[t.wN] = rid;
         twgen[t.wN] = z.rgen[rid];
+        twslot[t.wN] = s;
         t.wN++;
     }
     /* a row just placed (insert): STABLE if already settled (non-collaborating edits), else W */
@@ -1429,7 +1437,7 @@ struct Replica {
             if (z.rseq(s) == NOREM) lst_add(s / MAXN, z.len(s));
         } else {
             z.tl.xf[s] = XF_W;
-            win_add(z.rid[s]);
+            win_add(z.rid[s], s);
         }
     }
     /* a row just marked removed: leaves the STABLE summaries; W unless the removal is settled */
@@ -1441,7 +1449,7 @@ struct Replica {
         }
         if (!(x & XF_W) && !settled(s)) {
             x = XF_W;
-            win_add(z.rid[s]);
+            win_add(z.rid[s], s);
         }
         z.tl.xf[s] = x;
     }
@@ -1459,39 +1467,59 @@ struct Replica {
         constexpr int NB = W::N >= 64 ? 8 : 1;
         int32_t n = t.wN, wpos = 0, total = 0;
         for (int32_t b0 = 0; b0 < n; b0 += NB * W::N) {
-            int32_t rd[NB], g[NB], lf[NB], s[NB], v[NB], cp[NB], lx[NB];
+            int32_t rd[NB], g[NB], s[NB], v[NB], cp[NB], lx[NB];
             bool settle[NB], keep[NB];
 #pragma unroll
-            for (int q = 0; q < NB; q++) { /* the entries */
+            for (int q = 0; q < NB; q++) { /* the entries (LDS in the tiled kernel) */
                 int32_t i = b0 + q * W::N + w.lane();
                 bool ok = i < n;
                 rd[q] = ok ? twrid[i] : 0;
                 g[q] = ok ? twgen[i] : -1;
+                s[q] = ok ? twslot[i] : 0;
+            }
+            /* One round trip when the row is still in the slot it was last seen in: its generation, its leaf,
+             * the slot's row id and the leaf's child count check the hint, and the row itself and its leaf's
+             * rope links are read in the same pass. */
+            RowView rv[NB];
+            int32_t lc[NB];
+#pragma unroll
+            for (int q = 0; q < NB; q++) {
+                int32_t c = s[q], l = c / MAXN;
+                uint8_t gg = z.rgen[rd[q]]; /* every load of the pass unconditional: they issue together */
+                IX lr = z.rleaf[rd[q]], cr = z.rid[c];
+                int32_t cn = nch[l];
+                bool gok = g[q] >= 0 && gg == (uint8_t)g[q];
+                bool hit = gok & (lr == (IX)l) & ((c & (MAXN - 1)) < cn) & (cr == (IX)rd[q]);
+                rv[q] = row_view(c);
+                lc[q] = t.lch[l];
+                lx[q] = t.lix[l];
+                if (!hit) s[q] = gok ? -2 : -1; /* -2: look the row up */
             }
 #pragma unroll
-            for (int q = 0; q < NB; q++) { /* the row is still the one added: its leaf */
-                lf[q] = -1;
-                if (g[q] >= 0 && z.rgen[rd[q]] == (uint8_t)g[q]) lf[q] = z.rleaf[rd[q]];
-            }
-#pragma unroll
-            for (int q = 0; q < NB; q++) { /* its slot in the leaf */
-                s[q] = -1;
-                if (lf[q] >= 0) {
-                    int32_t c = nch[lf[q]];
+            for (int q = 0; q < NB; q++) { /* the rows that moved: leaf, slot, row */
+                if (s[q] == -2) {
+                    int32_t lf = z.rleaf[rd[q]];
+                    int32_t c = nch[lf];
+                    s[q] = -1;
                     for (int32_t j = 0; j < MAXN; j++)
-                        if (j < c && z.rid[lf[q] * MAXN + j] == rd[q]) s[q] = lf[q] * MAXN + j;
+                        if (j < c && z.rid[lf * MAXN + j] == (IX)rd[q]) s[q] = lf * MAXN + j;
+                    if (s[q] >= 0) {
+                        rv[q] = row_view(s[q]);
+                        lc[q] = t.lch[lf];
+                        lx[q] = t.lix[lf];
+                    }
                 }
             }
 #pragma unroll
             for (int q = 0; q < NB; q++) { /* settled, or its perspective length and chunk position */
-                settle[q] = s[q] >= 0 && settled(s[q]);
+                settle[q] = s[q] >= 0 && settled_of(rv[q]);
                 keep[q] = s[q] >= 0 && !settle[q];
-                v[q] = cp[q] = lx[q] = 0;
+                v[q] = cp[q] = 0;
                 if (keep[q]) {
-                    v[q] = vis(s[q], refSeq, client);
-                    int32_t l = s[q] / MAXN;
-                    cp[q] = tcpos[t.lch[l]];
-                    lx[q] = t.lix[l];
+                    v[q] = vis_of(s[q], rv[q], refSeq, client);
+                    cp[q] = tcpos[lc[q]];
+                } else {
+                    lx[q] = 0;
                 }
             }
             for (int q = 0; q < NB; q++) {
@@ -1515,6 +1543,7 @@ struct Replica {
                     int32_t o = wpos + off;
                     twrid[o] = rd[q];
                     twgen[o] = (uint8_t)g[q];
+                    twslot[o] = s[q];
                     wcp[o] = cp[q];
                     wlx[o] = (uint8_t)lx[q];
                     wvs[o] = v[q];
@@ -2090,7 +2119,7 @@ struct Replica {
         h.nrows++;
         zh->sumW += 2;
         if constexpr (TILED) {
-            if (z.tl.xf[rs] & XF_W) win_add(z.rid[rs]);
+            if (z.tl.xf[rs] & XF_W) win_add(z.rid[rs], rs);
             if (z.tl.xf[rs] & XF_STABLE) { /* the halves may sit in two leaves after a leaf split */
                 leaf_restat(ls / MAXN);
                 if (rs / MAXN != ls / MAXN) leaf_restat(rs / MAXN);

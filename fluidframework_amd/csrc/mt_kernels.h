@@ -198,9 +198,11 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
 }
 
 /* Config 4 (large documents, the tiled profile): one workgroup per document, which has the CU's LDS to
- * itself for the position-search scratch: per-chunk window deltas (NCH counters, all zero between
- * searches) and each window row's chunk position / leaf index / perspective length. The image, the
- * rope and the summaries stay in HBM (~0.2 GB per 1M-op document). */
+ * itself (155 KB): the position-search scratch (per-chunk window deltas, all zero between searches, and each
+ * window row's chunk position / leaf index / perspective length) and, for the duration of the replay, the
+ * rope's chunk arrays and the window set (with each row's last-seen slot). The rows, the leaf summaries,
+ * the per-leaf rope links and the zamboni heap stay in HBM (~0.2 GB per 1M-op document; an LDS copy of
+ * the heap measured no faster). */
 template <class HT, bool DL = false>
 __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                                      const int64_t* op_off, const uint16_t* text,
@@ -216,6 +218,7 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     /* the rope's chunk arrays and the window set, staged for the replay (written back at the end) */
     __shared__ int32_t lcord[NCH], lcst[NCH], lcpos[NCH], lccnt[NCH], lwrid[WCAP];
     __shared__ __attribute__((aligned(16))) uint8_t lwgen[WCAP];
+    __shared__ int32_t lwslot[WCAP];
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
     for (int i = threadIdx.x; i < NCH; i += WG) cdel[i] = 0;
@@ -228,6 +231,7 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     wave_copy(lccnt, tl.ccnt, NCH);
     wave_copy(lwrid, tl.wrid, WCAP);
     wave_copy((int32_t*)lwgen, (const int32_t*)tl.wgen, WCAP / 4);
+    wave_copy(lwslot, tl.wslot, WCAP);
     __syncthreads();
     Pools p;
     p.ops = ops + op_off[d];
@@ -247,6 +251,7 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     r.tccnt = lccnt;
     r.twrid = lwrid;
     r.twgen = lwgen;
+    r.twslot = lwslot;
     r.replay(p);
     r.commit();
     __syncthreads();
@@ -257,6 +262,7 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     wave_copy(tl.ccnt, lccnt, NCH);
     wave_copy(tl.wrid, lwrid, WCAP);
     wave_copy((int32_t*)tl.wgen, (const int32_t*)lwgen, WCAP / 4);
+    wave_copy(tl.wslot, lwslot, WCAP);
 #ifdef MT_PROF
     if (prof && threadIdx.x == 0)
         for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];

@@ -212,3 +212,41 @@ def test_250_client_ids():
     from test_core_host import many_clients_batch
     b = many_clients_batch()
     _check_batch(b, 3000, ndump=2, every=True)
+
+
+def stalled_window_log(nbase: int = 30000, nwin: int = 3800) -> ol.DocLog:
+    """A settled document of `nbase` rows (single "c\\n" segments: a newline ends every append), then a
+    collaboration window of `nwin` sequenced inserts scattered over it under a minSeq that stays put (a
+    client that does not advance its refSeq), then the minSeq catches up. The zamboni heap (one entry per
+    leaf with rows in the window) grows to ~2,900 entries,
+    with ~3,800 rows in the window set (its capacity is 4,096), and drains again."""
+    it = ol.Interner()
+    log = ol.DocLog(it, local_long_id=0)
+    seq = 0
+    rng = np.random.default_rng(7)
+    length = 0
+    for i in range(nbase + nwin):
+        seq += 1
+        ms = seq - 1 if i < nbase else nbase
+        p = int(rng.integers(0, length // 2 + 1)) * 2
+        log.add(ol.OP_INSERT, client=1 + i % 3, seq=seq, ref_seq=seq - 1, min_seq=ms, pos1=p, text="c\n")
+        length += 2
+    for i in range(600):  # the minSeq catches up in steps; each zamboni call pops two heap entries
+        seq += 1
+        log.add(ol.OP_NOOP, client=1, seq=seq, ref_seq=seq - 1, min_seq=min(seq - 1, nbase + (i + 1) * nwin // 300))
+    return log
+
+
+def test_tiled_deep_collaboration_window():
+    from fluidframework_amd.engine import Engine, default_caps
+    log = stalled_window_log()
+    c = oc.OracleClient(log.interner)
+    c.start_collab(log.local_long_id)
+    assert c.replay_arrays(*log.arrays()) == 0
+    eng = Engine(1, **default_caps(40_000, config=4))
+    eng.start_collab([0])
+    eng.replay(ol.Batch.from_logs([log]))
+    err, _ = eng.errors()
+    assert err[0] == 0
+    assert eng.dump(0) == c.dump()
+    assert eng.get_text(0) == c.get_text()
