@@ -1525,13 +1525,15 @@ struct Replica {
             for (int q = 0; q < NB; q++) {
                 if (b0 + q * W::N >= n) break;
                 uint64_t m = w.ballot(settle[q]);
-                while (m) { /* a few rows per op: serial */
+                while (m) { /* a few rows per op: serial, on the values this pass read (row, leaf's chunk) */
                     int32_t l = W::ffs(m);
                     m &= m - 1;
                     int32_t ss = w.bcast(s[q], l);
-                    if (z.rseq(ss) == NOREM) {
+                    if (w.bcast(rv[q].rseq, l) == NOREM) {
                         t.xf[ss] = XF_STABLE;
-                        lst_add(ss / MAXN, z.len(ss));
+                        int32_t dl = w.bcast(rv[q].len, l);
+                        t.lst[ss / MAXN] += dl;
+                        tcst[tcpos[w.bcast(lc[q], l)]] += dl;
                     } else {
                         t.xf[ss] = 0;
                     }
