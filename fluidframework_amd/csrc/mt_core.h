@@ -1410,6 +1410,35 @@ struct Replica {
         lst_add(n, v - z.tl.lst[n]);
         w.sync();
     }
+    /* leaf_restat of cnt <= 8 distinct leaves at once (a split leaf's halves, a pack's new leaves): lane q reads
+     * row q & 7 of leaf q >> 3 and the leaf's old summary and chunk in one pass; the chunk summaries (LDS in
+     * the tiled kernel) are updated leaf by leaf */
+    MT_HD void leaves_restat(const int32_t* nl, int32_t cnt) {
+        if constexpr (W::N >= MAXN * MAXN) {
+            MT_PROF_SCOPE(PH_RESTAT);
+            auto& t = z.tl;
+            int32_t q = w.lane(), i = q >> 3, j = q & (MAXN - 1);
+            int32_t n = -1;
+            for (int32_t k = 0; k < MAXN; k++)
+                if (k == i && k < cnt) n = nl[k];
+            int32_t old = n >= 0 ? t.lst[n] : 0, ch = n >= 0 ? t.lch[n] : 0;
+            int32_t c = n >= 0 ? nch[n] : 0;
+            int32_t x = 0;
+            if (j < c && (t.xf[n * MAXN + j] & XF_STABLE)) x = z.len(n * MAXN + j);
+            x += w.shfl_xor(x, 1);
+            x += w.shfl_xor(x, 2);
+            x += w.shfl_xor(x, 4);
+            w.sync();
+            if (n >= 0 && j == 0) t.lst[n] = x;
+            for (int32_t k = 0; k < cnt; k++) {
+                int32_t dk = w.bcast(x - old, MAXN * k);
+                if (dk) tcst[tcpos[w.bcast(ch, MAXN * k)]] += dk;
+            }
+            w.sync();
+        } else {
+            for (int32_t k = 0; k < cnt; k++) leaf_restat(nl[k]);
+        }
+    }
     /* a row is settled when its insert and (if any) its removal are sequenced at or below minSeq */
     MT_HD bool settled_of(const RowView& r) const {
         return r.seq != UNASSIGNED_SEQ && r.seq <= h.minSeq &&
@@ -1987,8 +2016,8 @@ struct Replica {
             if (lvl == 0) lorder_insert_after(n, nn);
             if constexpr (TILED) {
                 if (lvl == 0) {
-                    leaf_restat(n);
-                    leaf_restat(nn);
+                    int32_t two[2] = {n, nn};
+                    leaves_restat(two, 2);
                 }
             }
             int32_t p = npar[n];
@@ -2123,8 +2152,8 @@ struct Replica {
         if constexpr (TILED) {
             if (z.tl.xf[rs] & XF_W) win_add(z.rid[rs], rs);
             if (z.tl.xf[rs] & XF_STABLE) { /* the halves may sit in two leaves after a leaf split */
-                leaf_restat(ls / MAXN);
-                if (rs / MAXN != ls / MAXN) leaf_restat(rs / MAXN);
+                int32_t two[2] = {ls / MAXN, rs / MAXN};
+                leaves_restat(two, rs / MAXN != ls / MAXN ? 2 : 1);
             }
         }
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
@@ -2951,7 +2980,7 @@ struct Replica {
             if constexpr (TILED) { /* the rope: extra leaves after the kept ones, surplus ones out */
                 for (int32_t i = pc; i < cc; i++) rope_insert_after(newk[i - 1], newk[i]);
                 for (int32_t i = cc; i < pc; i++) rope_remove(oldk[i]);
-                for (int32_t i = 0; i < cc; i++) leaf_restat(newk[i]);
+                leaves_restat(newk, cc);
             }
             for (int32_t i = cc; i < pc; i++) free_node(oldk[i]);
             if constexpr (!TILED) {

@@ -20,6 +20,7 @@ struct WaveHost {
     uint64_t ballot(bool p) const { return p ? 1ull : 0ull; }
     int32_t bcast(int32_t v, int) const { return v; }
     int32_t shfl(int32_t v, int) const { return v; }
+    int32_t shfl_xor(int32_t v, int) const { return v; }
     static int32_t uniform(int32_t v) { return v; }
     int32_t writelane(int32_t v, int, int32_t) const { return v; }
     static int ffs(uint64_t m) { return __builtin_ctzll(m); }
@@ -81,6 +82,8 @@ struct WaveGPU {
     __device__ __attribute__((always_inline)) static int ffs(uint64_t m) { return __builtin_ctzll(m); }
     /* every lane takes v of lane src (per-lane source: ds_bpermute) */
     __device__ __attribute__((always_inline)) int32_t shfl(int32_t v, int src) const { return __shfl(v, src); }
+    /* every lane takes v of lane (lane ^ m) */
+    __device__ __attribute__((always_inline)) int32_t shfl_xor(int32_t v, int m) const { return __shfl_xor(v, m); }
     /* per-lane add into wave-shared scratch (LDS in the tiled replay kernel) */
     __device__ __attribute__((always_inline)) static void atomic_add(int32_t* p, int32_t v) { atomicAdd(p, v); }
     /* Order the wave's memory accesses between lanes. One wavefront replays one document, so every
