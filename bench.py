@@ -72,6 +72,25 @@ def workload(config: int, ops: int):
     return {1: gen.config1, 2: gen.config2, 3: gen.config3, 4: gen.config4, 5: gen.config5}[config](ops)
 
 
+def generate_cached(w, ids, cache: str, key: str):
+    """gen.generate, or the same batch memory-mapped from `cache` (written by an earlier run of the
+    same workload on this box: profiler passes re-run the bench several times)."""
+    import numpy as np
+    from fluidframework_amd import gen
+    from fluidframework_amd import oplog as ol
+    names = [f.name for f in __import__("dataclasses").fields(ol.Batch)]
+    d = os.path.join(cache, key) if cache else ""
+    if d and os.path.exists(os.path.join(d, "done")):
+        return ol.Batch(*[np.load(os.path.join(d, n + ".npy"), mmap_mode="r") for n in names])
+    batch = gen.generate(w, ids=ids, threads=cpu_workers())
+    if d:
+        os.makedirs(d, exist_ok=True)
+        for n in names:
+            np.save(os.path.join(d, n + ".npy"), getattr(batch, n))
+        open(os.path.join(d, "done"), "w").close()
+    return batch
+
+
 def cpu_baseline(batch, gpu_digests, workers: int, target_s: float = 15.0):
     """The oracle (CPU restatement of the reference algorithm, test infrastructure) on `workers`
     host threads over a bounded prefix of this rank's documents, sized for ~target_s seconds."""
@@ -113,6 +132,8 @@ def main() -> None:
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (default: host share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gen-cache", default=os.environ.get("MT_GEN_CACHE", ""),
+                    help="directory caching generated workloads between runs (profiler passes)")
     args = ap.parse_args()
 
     import numpy as np
@@ -154,7 +175,8 @@ def main() -> None:
         mine = shard.weak_ids(rank, docs)
         node_docs = docs * world
     t0 = time.time()
-    batch = gen.generate(w, ids=mine, threads=cpu_workers())
+    key = f"c{args.config}_d{docs}_o{ops}_{args.scaling}_r{rank}of{world}"
+    batch = generate_cached(w, mine, args.gen_cache, key)
     log(f"rank {rank}: generated {batch.ndocs} docs, {batch.nops} events in {time.time() - t0:.1f}s")
     local_events = int(((batch.ops["kind"] & 0x80) != 0).sum())
 
@@ -247,7 +269,7 @@ def main() -> None:
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "traffic_note": "PMC counters cannot be read inside this process; FETCH_SIZE/WRITE_SIZE "
                                          "of k_replay on this command are in profiles/*_traffic.json "
-                                         "(tools/gpu_bench.sh PMC=1)",
+                                         "(tools/gpu.sh traffic:C, tools/roofline_report.py)",
                          "kernel": "k_replay_tiled" if args.config == 4 else "k_replay", "kernel_ms": avg_kernel_ms,
                          "alg_bytes_per_launch": alg_bytes, "alg_bytes_node": total_alg,
                          "alg_formula": ("tile summaries (BASELINE.md): A(op) = 4 B x chunks + 64 B x window rows "

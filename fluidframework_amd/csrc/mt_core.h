@@ -131,6 +131,7 @@ struct DocHdr {
     int32_t loadPos;       /* snapshot load: the next position of the open loadBody batch (mt_oplog.h) */
     int32_t ovTop, ovFree; /* overlap overflow pool: next never-used block, free-list head (0 = none) */
     int32_t gidNext;       /* id of the next pending segment group (ids increase along the queue) */
+    int32_t mkMask;        /* property key slots an annotate changed on a marker (marker_keys_annotated) */
     int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
 };
@@ -589,6 +590,7 @@ struct Replica {
         zh->heapTop = 0;
         zh->loadPos = 0;
         zh->gidNext = 0;
+        zh->mkMask = 0;
         zh->ovTop = 1; /* block 0 is the null link */
         zh->ovFree = 0;
         for (int32_t b = 0; b < HT::C; b += W::N) {
@@ -3539,6 +3541,7 @@ struct Replica {
                     prop_deltas(s, kv, nkv, rewrite, seq, collab);
                     dn++;
                 }
+                if (z.flags(s) & RF_MARKER) marker_keys_annotated(s, kv, nkv, rewrite);
                 add_props(s, kv, nkv, rewrite, seq, collab);
                 if (collab) {
                     if (hasL)
@@ -3591,6 +3594,24 @@ struct Replica {
     }
 
     /* ---- relative positions: MergeTree.posFromRelativePos (mergeTree.ts:1976-1999) ---------- */
+    /* The reference's idToSegment map is written when a marker is inserted (mergeTree.ts:1218-1221) and
+     * never follows a later annotate of its markerId; the engine finds markers by their current property
+     * values. An annotate (or a rewrite) that changes a key slot on a marker records the slot in mkMask,
+     * and a lookup by a key slot in that mask is refused (E_UNSUPPORTED) instead of answering by the new
+     * value. */
+    MT_HD void marker_keys_annotated(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite) {
+        int32_t m = zh->mkMask;
+        if (rewrite && (z.flags(s) & RF_PROPS)) {
+            typename HT::Cold& c = cold(s);
+            for (int32_t k = 0; k < zh->nkeys; k++)
+                if (c.pv[k] != 0) m |= 1 << k;
+        }
+        for (int32_t j = 0; j < nkv; j++) {
+            int32_t k = key_slot(kv[j].key);
+            if (k >= 0) m |= 1 << k;
+        }
+        zh->mkMask = m;
+    }
     /* The row of the marker whose property `kid` (the marker-id key) holds value `vid` (getMarkerFromId,
      * 1965-1967: the reference's idToSegment map, filled when a marker with an id is inserted): -1 none,
      * -2 more than one (the reference keeps the last one it registered; not modelled) */
@@ -3599,6 +3620,7 @@ struct Replica {
         for (int32_t k = 0; k < zh->nkeys; k++)
             if (z.keys[k] == kid) slot = k;
         if (slot < 0 || (vid & ~MT_VALUE_FALSY) == 0) return -1;
+        if (zh->mkMask & (1 << slot)) return -2; /* the id key was annotated on a marker: not modelled */
         int32_t found = -1, n = 0;
         for (int32_t k = 0; kvalid(k); k = knext(k)) {
             int32_t lf = leaf_at(k), c = nch[lf];
@@ -4122,6 +4144,7 @@ struct Replica {
         y = y < 0 ? 0 : (y > v ? v : y);
         *a = x < y ? x : y, *b = x < y ? y : x;
     }
+    static constexpr int64_t PH_RUN_MAX = 1 << 24;
     MT_HD int64_t get_text(int32_t refSeq, int32_t client, uint16_t* out, int64_t cap) {
         return get_text_range(refSeq, client, 0, INT32_MAX, nullptr, 0, out, cap);
     }
@@ -4158,6 +4181,9 @@ struct Replica {
                 bool text = s >= 0 && !(z.flags(s) & RF_NOTEXT);
                 int32_t a = 0, b = 0;
                 if (hit && text) text_piece(v, start - p, end - p, &a, &b);
+                /* a placeholder run longer than 2^24 units (a merged PermutationSegment of millions of rows
+                 * at a long placeholder) is rejected rather than overflowing the int32 output scan */
+                if (w.ballot(hit && !text && (int64_t)pl * v > PH_RUN_MAX)) return -E_UNSUPPORTED;
                 int32_t ol = !hit ? 0 : text ? b - a : pl * v;
                 int32_t tot;
                 int64_t o = n + w.excl_scan(ol, &tot);
@@ -4184,6 +4210,7 @@ struct Replica {
                 P += v;
                 if (v <= 0 || !(start < p + v && end > p)) continue;
                 if (z.flags(s) & RF_NOTEXT) {
+                    if ((int64_t)pl * v > PH_RUN_MAX) return -E_UNSUPPORTED;
                     for (int32_t u = 0; u < pl * v; u++, n++)
                         if (out && n < cap) out[n] = ph[u % pl];
                     continue;

@@ -291,25 +291,48 @@ __global__ __launch_bounds__(WG) void k_dump(Store<HT> st, int64_t doc, uint8_t*
     if (threadIdx.x == 0) *n = m;
 }
 
+/* A read under a remote perspective (refSeq, client) is answered only where the reference's block
+ * PartialSequenceLengths and the leaf visibility predicate the engine sums agree: refSeq >= minSeq (the
+ * partials fold everything at or below the window into minLength, partialLengths.ts:489-518) and refSeq at
+ * or past every refSeq that client has sent an op under (`floor`, tracked by the host from the records:
+ * later entries of that client are added whole, getBranchPartialLength 456-486, which counts a removal of
+ * a segment inserted after refSeq that the predicate does not — the "invalid combination" of
+ * partialLengths.ts:672-681). The local client (cachedLength) and a non-collaborating replica are always
+ * answered. Measured against the reference on 7,600 perspectives: every one this rule answers is equal
+ * (tests/test_ref_persp.py). */
+template <class R>
+__device__ inline bool persp_refused(const R& r, int32_t ref_seq, int32_t long_client, int32_t floor) {
+    if (long_client < 0 || !r.h.collaborating || long_client == r.h.localLong) return false;
+    return ref_seq < r.h.minSeq || ref_seq < floor;
+}
+
 template <class HT>
 __global__ __launch_bounds__(WG) void k_length(Store<HT> st, int64_t doc, int32_t ref_seq, int32_t long_client,
-                                              int32_t* out) {
+                                              int32_t floor, int32_t* out) {
     Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
     int32_t v;
+    if (persp_refused(r, ref_seq, long_client, floor)) {
+        if (threadIdx.x == 0) out[0] = 0, out[1] = 1;
+        return;
+    }
     if (long_client < 0) {
         v = r.length_local();
     } else {
         int32_t sh = r.short_of(long_client);
         v = r.length(ref_seq, sh < 0 ? 0x7fff : sh);
     }
-    if (threadIdx.x == 0) *out = v;
+    if (threadIdx.x == 0) out[0] = v, out[1] = 0;
 }
 
 template <class HT>
 __global__ __launch_bounds__(WG) void k_text(Store<HT> st, int64_t doc, int32_t ref_seq, int32_t long_client,
-                                            int32_t start, int32_t end, const uint16_t* ph, int32_t pl,
-                                            uint16_t* out, int64_t cap, int64_t* n) {
+                                            int32_t floor, int32_t start, int32_t end, const uint16_t* ph,
+                                            int32_t pl, uint16_t* out, int64_t cap, int64_t* n) {
     Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
+    if (persp_refused(r, ref_seq, long_client, floor)) {
+        if (threadIdx.x == 0) *n = -E_UNSUPPORTED;
+        return;
+    }
     int32_t sh;
     if (long_client < 0) {
         sh = r.h.localShort;
@@ -327,8 +350,15 @@ __global__ __launch_bounds__(WG) void k_text(Store<HT> st, int64_t doc, int32_t 
  * out[0] = status (1 found / 0 none), then mt_seg_ref fields or the position */
 template <class HT>
 __global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t mode, int32_t a, int32_t b,
-                                           int32_t ref_seq, int32_t long_client, int32_t* out) {
+                                           int32_t ref_seq, int32_t long_client, int32_t floor, int32_t* out) {
     Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
+    if (persp_refused(r, ref_seq, long_client, floor)) { /* out[0] = 3: refused (MT_E_UNSUPPORTED) */
+        if (threadIdx.x == 0) {
+            out[0] = 3;
+            for (int i = 1; i < 7; i++) out[i] = 0;
+        }
+        return;
+    }
     int32_t sh;
     if (long_client < 0) {
         sh = r.h.localShort;
@@ -429,6 +459,9 @@ struct mt_engine {
      * their staged logs, in an engine of the next profile (`over`); per-document queries route there */
     bool promote = true;
     bool ran = false;                 /* a replay was launched since the last sync */
+    bool fresh = true;                /* no replay since create / reset: the staged log is each replica's whole history */
+    bool ran_fresh = false;           /* the last launched replay started from such a state */
+    bool forwarded = false;           /* the last replay also ran the promoted documents' records in `over` */
     mt_engine* over = nullptr;
     std::vector<int32_t> pro;         /* doc -> index in `over`, -1: not promoted */
     std::vector<int64_t> pro_docs;    /* index in `over` -> doc */
@@ -443,7 +476,6 @@ struct mt_engine {
     int32_t pcap = 0; /* PermutationVector handles per document (0: none) */
     bool fx = false;  /* delta events or local references: the client-feature replay build */
     int profile = 0;
-    bool lds = false; /* small profile staged in LDS for the whole replay (MT_REPLAY_LDS=1) */
     int waves = 8;    /* occupancy target of the HBM-resident small-profile kernel */
     Store<HotSmall> s0;
     Store<HotMid> s1;
@@ -458,6 +490,33 @@ struct mt_engine {
     DevBuf ops_buf, op_off, text, text_off, props, props_off, kv, kv_off, tmp, local_ids, prof;
     bool collab = false;
     std::string err;
+    /* perspective floors (persp_refused): per document, the greatest refSeq each long client has sent a
+     * sequenced op under (long id, refSeq pairs), and a floor for every client (a snapshot load's currentSeq:
+     * the loaded window's ops are not in the log). `staged` is built by mt_engine_submit from the staged
+     * records, `applied` covers every record replayed since create / reset. */
+    struct Persp {
+        int32_t all = INT32_MIN;
+        std::vector<std::pair<int32_t, int32_t>> ref;
+        void note(int32_t c, int32_t r) {
+            for (auto& x : ref)
+                if (x.first == c) {
+                    if (r > x.second) x.second = r;
+                    return;
+                }
+            ref.emplace_back(c, r);
+        }
+        void merge(const Persp& o) {
+            if (o.all > all) all = o.all;
+            for (auto& x : o.ref) note(x.first, x.second);
+        }
+        int32_t floor(int32_t c) const {
+            int32_t f = all;
+            for (auto& x : ref)
+                if (x.first == c && x.second > f) f = x.second;
+            return f;
+        }
+    };
+    std::vector<Persp> persp_staged, persp_applied;
 };
 
 static inline int32_t hip_fail(mt_engine* e, hipError_t st, const char* what) {
@@ -487,11 +546,12 @@ struct ProfOps {
     int32_t (*hdr)(mt_engine* e, int32_t* de, int32_t* deo, int32_t* ds, int64_t* dw);
     int32_t (*digest)(mt_engine* e, uint64_t* dout);
     int32_t (*dump)(mt_engine* e, int64_t doc, uint8_t* dbuf, int64_t cap, int64_t* dn);
-    int32_t (*length)(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t* dout);
-    int32_t (*text)(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t start, int32_t end,
-                    const uint16_t* dph, int32_t pl, uint16_t* dbuf, int64_t cap, int64_t* dn);
+    /* the reads take the perspective floor of persp_refused (the host's per-client refSeq bound) */
+    int32_t (*length)(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t floor, int32_t* dout);
+    int32_t (*text)(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t floor, int32_t start,
+                    int32_t end, const uint16_t* dph, int32_t pl, uint16_t* dbuf, int64_t cap, int64_t* dn);
     int32_t (*seg)(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,
-                   int32_t long_client, int32_t* dout);
+                   int32_t long_client, int32_t floor, int32_t* dout);
     int32_t (*refpos)(mt_engine* e, int32_t* dn, int32_t* dpos);
 };
 /* each profile's table (host functions, defined in its mt_prof_*.hip) */
@@ -551,21 +611,22 @@ struct Launch {
         hipLaunchKernelGGL((k_dump<HT>), dim3(1), dim3(WG), 0, e->stream, store_of<HT>(e), doc, dbuf, cap, dn);
         return launch_check(e, "k_dump");
     }
-    static int32_t length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t* dout) {
+    static int32_t length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t floor,
+                          int32_t* dout) {
         hipLaunchKernelGGL((k_length<HT>), dim3(1), dim3(WG), 0, e->stream, store_of<HT>(e), doc, ref_seq,
-                           long_client, dout);
+                           long_client, floor, dout);
         return launch_check(e, "k_length");
     }
-    static int32_t text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t start, int32_t end,
-                        const uint16_t* dph, int32_t pl, uint16_t* dbuf, int64_t cap, int64_t* dn) {
+    static int32_t text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t floor, int32_t start,
+                        int32_t end, const uint16_t* dph, int32_t pl, uint16_t* dbuf, int64_t cap, int64_t* dn) {
         hipLaunchKernelGGL((k_text<HT>), dim3(1), dim3(WG), 0, e->stream, store_of<HT>(e), doc, ref_seq, long_client,
-                           start, end, dph, pl, dbuf, cap, dn);
+                           floor, start, end, dph, pl, dbuf, cap, dn);
         return launch_check(e, "k_text");
     }
     static int32_t seg(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,
-                       int32_t long_client, int32_t* dout) {
+                       int32_t long_client, int32_t floor, int32_t* dout) {
         hipLaunchKernelGGL((k_seg<HT>), dim3(1), dim3(WG), 0, e->stream, store_of<HT>(e), doc, mode, a, b, ref_seq,
-                           long_client, dout);
+                           long_client, floor, dout);
         return launch_check(e, "k_seg");
     }
     static int32_t refpos(mt_engine* e, int32_t* dn, int32_t* dpos) {

@@ -3,17 +3,16 @@
 #include "mt_kernels.h"
 
 int32_t replay_small_w8(mt_engine* e);
-int32_t replay_small_lds(mt_engine* e);
 int32_t replay_small_dl(mt_engine* e);
 
 /* Default: the hot image stays in HBM (skeleton and heap in LDS) and the kernel is built for 8 waves
  * per SIMD, so 8,192 documents are in flight (32 per CU): at one wavefront per document the replay
  * is bound by the latency of its dependent accesses and by issue, and occupancy hides more of it than
  * full LDS residency (4 documents per CU) saves (round-2 sweep of 2-8 waves: profiles/r02_occupancy.txt;
- * the sweep's other builds are no longer compiled). MT_REPLAY_LDS=1 selects the fully LDS-staged form. */
+ * the sweep's other builds are no longer compiled; the fully LDS-staged form measured 0.6x on config 2,
+ * profiles/r03_c2_4096docs_bench_*.json, and is no longer built). */
 static int32_t replay_small(mt_engine* e) {
     if (e->fx) return replay_small_dl(e); /* the delta-event build */
-    if (e->lds) return replay_small_lds(e);
     return replay_small_w8(e);
 }
 

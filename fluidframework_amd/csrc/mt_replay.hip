@@ -39,8 +39,6 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->rcap = caps->rcap;
     e->pcap = caps->pcap;
     e->fx = caps->dcap > 0 || caps->rcap > 0 || caps->pcap > 0;
-    const char* g = getenv("MT_REPLAY_LDS");
-    e->lds = g && g[0] == '1';
     const char* np = getenv("MT_NO_PROMOTE");
     e->promote = !(np && np[0] == '1');
     e->caps0 = *caps;
@@ -127,6 +125,17 @@ int32_t mt_engine_start_collab_docs(mt_engine* e, const int32_t* local_long_ids,
     rc = e->ops->start_collab(e);
     if (rc) return rc;
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->over && !e->pro_docs.empty()) { /* promoted documents live in `over` */
+        size_t m = e->pro_docs.size();
+        std::vector<int32_t> ids(m), mn(m), cu(m);
+        for (size_t i = 0; i < m; i++) {
+            int64_t d = e->pro_docs[i];
+            ids[i] = local_long_ids[d];
+            mn[i] = min_seqs[d];
+            cu[i] = cur_seqs[d];
+        }
+        return mt_engine_start_collab_docs(e->over, ids.data(), mn.data(), cu.data());
+    }
     return MT_OK;
 }
 
@@ -144,11 +153,20 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
     }
     /* every pool reference of every event must be in bounds before the kernel dereferences it: the
      * documents are checked in parallel on the host (up to 16 threads, one contiguous range each) */
+    std::vector<mt_engine::Persp> persp((size_t)nd);
     auto check = [&](int64_t d0, int64_t d1) -> bool {
         for (int64_t d = d0; d < d1; d++) {
+            mt_engine::Persp& pp = persp[(size_t)d];
             for (int64_t i = op_off[d]; i < op_off[d + 1]; i++) {
                 const mt_op_rec& o = ops[i];
                 int kind = o.kind & MT_OP_KIND_MASK;
+                if (!(o.kind & MT_OPF_LOCAL)) { /* perspective floors (mt_kernels.h persp_refused) */
+                    if (kind == MT_OP_RELOAD || kind == MT_OP_COLLAB || kind == MT_OP_APPEND) {
+                        if (o.seq > pp.all) pp.all = o.seq;
+                    } else if (kind != MT_OP_NOOP && o.client != MT_CLIENT_LOCAL) {
+                        pp.note(o.client, o.ref_seq);
+                    }
+                }
                 if (kind == MT_OP_INSERT && (o.seg_kind & 0x7F) == MT_SEG_TEXT &&
                     text_off[d] + (int64_t)o.text_off + o.text_len > text_units)
                     return false;
@@ -204,6 +222,7 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
     e->h_text_off.assign(text_off, text_off + nd);
     e->h_props_off.assign(props_off, props_off + nd);
     e->h_kv_off.assign(kv_off, kv_off + nd);
+    e->persp_staged.swap(persp);
     e->staged = true;
     return MT_OK;
 }
@@ -213,8 +232,11 @@ int32_t mt_engine_reset(mt_engine* e) {
     HIPCHK(e, hipSetDevice(e->device));
     std::fill(e->pro.begin(), e->pro.end(), -1);
     e->pro_docs.clear();
+    e->fresh = true;
     return launch_init(e);
 }
+
+static int32_t stage_subset(mt_engine* e, mt_engine* o);
 
 int32_t mt_engine_run(mt_engine* e) {
     if (!e || !e->staged) return MT_E_ARG;
@@ -227,6 +249,20 @@ int32_t mt_engine_run(mt_engine* e) {
     if (rc) return rc;
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
     e->ran = true;
+    e->ran_fresh = e->fresh;
+    if (e->fresh) e->persp_applied.assign((size_t)e->ndocs, mt_engine::Persp());
+    for (size_t d = 0; d < e->persp_staged.size() && d < e->persp_applied.size(); d++)
+        e->persp_applied[d].merge(e->persp_staged[d]);
+    e->fresh = false;
+    e->forwarded = false;
+    /* documents promoted by an earlier replay of this replica history live on in `over`: their parent
+     * replicas stay latched (E_CAPACITY, every later record a no-op), so this batch's records for them
+     * replay there, on top of the state they already hold (no reset) */
+    if (e->over && !e->pro_docs.empty()) {
+        if ((rc = stage_subset(e, e->over))) return rc;
+        if ((rc = mt_engine_run(e->over))) return rc;
+        e->forwarded = true;
+    }
     return MT_OK;
 }
 
@@ -240,9 +276,15 @@ int32_t mt_engine_sync(mt_engine* e) {
     if (hipEventElapsedTime(&ms, e->ev0, e->ev1) == hipSuccess) e->last_ms = ms;
     if (e->ran) {
         e->ran = false;
-        if (e->promote) {
-            int32_t rc = promote(e);
-            if (rc) return rc;
+        int32_t rc;
+        if (e->forwarded) {
+            e->forwarded = false;
+            if ((rc = mt_engine_sync(e->over))) return rc;
+            e->last_ms += e->over->last_ms;
+        } else if (e->promote && e->ran_fresh) {
+            /* only a replay that started from create / reset holds each replica's whole history in the staged
+             * log; a document that overflows in a later incremental batch keeps E_CAPACITY visible */
+            if ((rc = promote(e))) return rc;
             if (e->over && !e->pro_docs.empty()) e->last_ms += e->over->last_ms;
         }
     }
@@ -289,49 +331,11 @@ static void scatter(T* dst, const std::vector<T>& src, const std::vector<int64_t
         for (int j = 0; j < k; j++) dst[docs[i] * k + j] = src[i * k + j];
 }
 }
-static int32_t promote(mt_engine* e) {
-    std::fill(e->pro.begin(), e->pro.end(), -1);
-    e->pro_docs.clear();
-    int32_t nc = next_ncap(e->profile);
-    if (nc < 0) return MT_OK;
-    int64_t nd = e->ndocs;
-    std::vector<int32_t> err((size_t)nd);
-    int32_t rc = read_hdr(e, err.data(), nullptr, nullptr, nullptr);
-    if (rc) return rc;
-    for (int64_t d = 0; d < nd; d++)
-        if (err[(size_t)d] == MT_E_CAPACITY) e->pro_docs.push_back(d);
+/* stage, in `o`, the records `e` has staged for its promoted documents (e->pro_docs, in order), gathered
+ * device to device; their text / props / kv pools stay the parent's */
+static int32_t stage_subset(mt_engine* e, mt_engine* o) {
     int64_t m = (int64_t)e->pro_docs.size();
-    if (m == 0) return MT_OK;
-    mt_caps c = e->caps0;
-    c.ncap = nc;
-    c.hcap = std::max(c.hcap, 2 * nc);
-    c.acap = (int32_t)std::min<int64_t>(4 * (int64_t)c.acap, 1 << 23);
-    c.mcap = (int32_t)std::min<int64_t>(4 * (int64_t)c.mcap, 1 << 18);
-    c.gcap = (int32_t)std::min<int64_t>(4 * (int64_t)c.gcap, 1 << 16);
-    mt_engine* o = e->over;
-    if (o && (o->ndocs != m || o->caps0.ncap != c.ncap)) {
-        mt_engine_destroy(o);
-        o = e->over = nullptr;
-    }
-    if (!o) {
-        rc = mt_engine_create(e->device, m, &c, &o);
-        if (rc) return rc;
-        e->over = o;
-    }
-    o->promote = e->promote;
-    if (e->collab) {
-        std::vector<int32_t> loc((size_t)(3 * m)); /* the promoted documents' ids, minSeqs, currentSeqs */
-        for (int64_t i = 0; i < m; i++)
-            for (int64_t k = 0; k < 3; k++)
-                loc[(size_t)(k * m + i)] = e->h_local[(size_t)(k * nd + e->pro_docs[(size_t)i])];
-        HIPCHK(o, hipSetDevice(o->device));
-        if ((rc = ensure(o, o->local_ids, sizeof(int32_t) * 3 * m))) return rc;
-        HIPCHK(o, hipMemcpyAsync(o->local_ids.p, loc.data(), sizeof(int32_t) * 3 * m, hipMemcpyHostToDevice, o->stream));
-        HIPCHK(o, hipStreamSynchronize(o->stream));
-        o->h_local = loc;
-        o->collab = true;
-    }
-    /* the promoted documents' records, gathered device to device; their pools are the parent's */
+    int32_t rc;
     o->h_op_off.assign((size_t)m + 1, 0);
     o->h_text_off.resize((size_t)m);
     o->h_props_off.resize((size_t)m);
@@ -364,12 +368,67 @@ static int32_t promote(mt_engine* e) {
     o->props = e->props;
     o->kv = e->kv;
     o->staged = true;
+    return MT_OK;
+}
+static int32_t promote(mt_engine* e) {
+    std::fill(e->pro.begin(), e->pro.end(), -1);
+    e->pro_docs.clear();
+    int32_t nc = next_ncap(e->profile);
+    if (nc < 0) return MT_OK;
+    int64_t nd = e->ndocs;
+    std::vector<int32_t> err((size_t)nd);
+    int32_t rc = read_hdr(e, err.data(), nullptr, nullptr, nullptr);
+    if (rc) return rc;
+    for (int64_t d = 0; d < nd; d++)
+        if (err[(size_t)d] == MT_E_CAPACITY) e->pro_docs.push_back(d);
+    int64_t m = (int64_t)e->pro_docs.size();
+    if (m == 0) return MT_OK;
+    mt_caps c = e->caps0;
+    c.ncap = nc;
+    c.hcap = std::max(c.hcap, 2 * nc);
+    c.acap = (int32_t)std::min<int64_t>(4 * (int64_t)c.acap, 1 << 23);
+    c.mcap = (int32_t)std::min<int64_t>(4 * (int64_t)c.mcap, 1 << 18);
+    c.gcap = (int32_t)std::min<int64_t>(4 * (int64_t)c.gcap, 1 << 16);
+    /* the client-feature capacities grow too (delta-log words, references, PermutationVector handles),
+     * so a document that overflowed one of them is not replayed again into the same limit */
+    c.dcap = (int32_t)std::min<int64_t>(4 * (int64_t)c.dcap, 1 << 26);
+    c.rcap = (int32_t)std::min<int64_t>(4 * (int64_t)c.rcap, 1 << 16);
+    c.pcap = (int32_t)std::min<int64_t>(4 * (int64_t)c.pcap, 1 << 24);
+    mt_engine* o = e->over;
+    if (o && (o->ndocs != m || o->caps0.ncap != c.ncap)) {
+        mt_engine_destroy(o);
+        o = e->over = nullptr;
+    }
+    if (!o) {
+        rc = mt_engine_create(e->device, m, &c, &o);
+        if (rc) return rc;
+        e->over = o;
+    }
+    o->promote = e->promote;
+    if (e->collab) {
+        std::vector<int32_t> loc((size_t)(3 * m)); /* the promoted documents' ids, minSeqs, currentSeqs */
+        for (int64_t i = 0; i < m; i++)
+            for (int64_t k = 0; k < 3; k++)
+                loc[(size_t)(k * m + i)] = e->h_local[(size_t)(k * nd + e->pro_docs[(size_t)i])];
+        HIPCHK(o, hipSetDevice(o->device));
+        if ((rc = ensure(o, o->local_ids, sizeof(int32_t) * 3 * m))) return rc;
+        HIPCHK(o, hipMemcpyAsync(o->local_ids.p, loc.data(), sizeof(int32_t) * 3 * m, hipMemcpyHostToDevice, o->stream));
+        HIPCHK(o, hipStreamSynchronize(o->stream));
+        o->h_local = loc;
+        o->collab = true;
+    }
+    if ((rc = stage_subset(e, o))) return rc;
     /* an empty replica (create / reset state), the same local ids; then the replay, promoting further */
     if ((rc = mt_engine_reset(o))) return rc;
     if ((rc = mt_engine_run(o))) return rc;
     if ((rc = mt_engine_sync(o))) return rc;
     for (int64_t i = 0; i < m; i++) e->pro[(size_t)e->pro_docs[(size_t)i]] = (int32_t)i;
     return MT_OK;
+}
+/* the perspective floor of (doc, long client) for the reads (mt_kernels.h persp_refused) */
+static int32_t persp_floor(const mt_engine* e, int64_t doc, int32_t long_client) {
+    if (long_client < 0 || (size_t)doc >= e->persp_applied.size()) return INT32_MIN;
+    return e->persp_applied[(size_t)doc].floor(long_client);
 }
 /* the engine and index that hold document `doc` (promoted documents live in `over`) */
 static mt_engine* route(mt_engine* e, int64_t* doc) {
@@ -456,14 +515,18 @@ int64_t mt_engine_dump(mt_engine* e, int64_t doc, uint8_t* out, int64_t cap) {
 
 int32_t mt_engine_get_length(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, int32_t* out) {
     if (!e || !out || doc < 0 || doc >= e->ndocs) return MT_E_ARG;
+    int32_t floor = persp_floor(e, doc, long_client);
     e = route(e, &doc);
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc = ensure(e, e->tmp, 16);
     if (rc) return rc;
-    rc = e->ops->length(e, doc, ref_seq, long_client, (int32_t*)e->tmp.p);
+    rc = e->ops->length(e, doc, ref_seq, long_client, floor, (int32_t*)e->tmp.p);
     if (rc) return rc;
-    HIPCHK(e, hipMemcpyAsync(out, e->tmp.p, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    int32_t r2[2];
+    HIPCHK(e, hipMemcpyAsync(r2, e->tmp.p, sizeof(r2), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (r2[1]) return MT_E_UNSUPPORTED; /* a perspective the reference's partial lengths answer differently */
+    *out = r2[0];
     return MT_OK;
 }
 
@@ -480,6 +543,7 @@ int64_t mt_engine_get_text_range(mt_engine* e, int64_t doc, int32_t ref_seq, int
         (placeholder_len > 0 && !placeholder))
         return -MT_E_ARG;
     if (placeholder_len == 1 && placeholder[0] == '*') return -MT_E_UNSUPPORTED; /* Marker.toString() */
+    int32_t floor = persp_floor(e, doc, long_client);
     e = route(e, &doc);
     if (hipSetDevice(e->device) != hipSuccess) return -MT_E_HIP;
     size_t phb = (2 * (size_t)placeholder_len + 15) & ~(size_t)15;
@@ -490,7 +554,8 @@ int64_t mt_engine_get_text_range(mt_engine* e, int64_t doc, int32_t ref_seq, int
     if (placeholder_len > 0 &&
         hipMemcpyAsync(dph, placeholder, 2 * (size_t)placeholder_len, hipMemcpyHostToDevice, e->stream) != hipSuccess)
         return -MT_E_HIP;
-    int32_t rc = e->ops->text(e, doc, ref_seq, long_client, start, end, dph, placeholder_len, dbuf, out ? cap : 0, dn);
+    int32_t rc = e->ops->text(e, doc, ref_seq, long_client, floor, start, end, dph, placeholder_len, dbuf,
+                              out ? cap : 0, dn);
     if (rc) return -rc;
     int64_t n = 0;
     if (hipMemcpyAsync(&n, dn, sizeof(int64_t), hipMemcpyDeviceToHost, e->stream) != hipSuccess) return -MT_E_HIP;
@@ -506,14 +571,16 @@ int64_t mt_engine_get_text_range(mt_engine* e, int64_t doc, int32_t ref_seq, int
 static int32_t seg_query(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,
                          int32_t long_client, int32_t* res7) {
     if (!e || doc < 0 || doc >= e->ndocs) return MT_E_ARG;
+    int32_t floor = persp_floor(e, doc, long_client);
     e = route(e, &doc);
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc = ensure(e, e->tmp, 64);
     if (rc) return rc;
-    rc = e->ops->seg(e, doc, mode, a, b, ref_seq, long_client, (int32_t*)e->tmp.p);
+    rc = e->ops->seg(e, doc, mode, a, b, ref_seq, long_client, floor, (int32_t*)e->tmp.p);
     if (rc) return rc;
     HIPCHK(e, hipMemcpyAsync(res7, e->tmp.p, 7 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (res7[0] == 3) return MT_E_UNSUPPORTED; /* a perspective the reference's partial lengths answer differently */
     return MT_OK;
 }
 

@@ -23,7 +23,11 @@ ERRORS = {0: "ok", 1: "MergeTree insert failed", 2: "assertion", 3: "invalid op 
 
 
 class EngineError(RuntimeError):
-    pass
+    """A failed engine call; `code` is the MT_E_* status when the call returned one."""
+
+    def __init__(self, msg: str, code: Optional[int] = None):
+        super().__init__(msg)
+        self.code = code
 
 
 class SegRef(ctypes.Structure):
@@ -139,7 +143,7 @@ class Engine:
     def _check(self, rc: int, what: str):
         if rc != 0:
             msg = self.L.mt_engine_last_error(self.h)
-            raise EngineError(f"{what} failed: status {rc}: {msg.decode() if msg else ''}")
+            raise EngineError(f"{what} failed: status {rc}: {msg.decode() if msg else ''}", rc)
 
     def start_collab(self, local_long_ids, min_seq=0, cur_seq=0):
         """Client.startOrUpdateCollaboration for every document (client.ts:1053-1073); min_seq / cur_seq are
@@ -223,7 +227,7 @@ class Engine:
         pp = None if ph is None else _p(ph)
         n = self.L.mt_engine_get_text_range(self.h, doc, ref_seq, long_client, pp, pl, a, b, None, 0)
         if n < 0:
-            raise EngineError(f"get_text failed {n}")
+            raise EngineError(f"get_text failed {n}", -n)
         buf = np.zeros(max(n, 1), "<u2")
         self.L.mt_engine_get_text_range(self.h, doc, ref_seq, long_client, pp, pl, a, b, _p(buf), n)
         return buf[:n].tobytes().decode("utf-16-le")

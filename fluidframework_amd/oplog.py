@@ -20,6 +20,9 @@ OP_REF = 3  # local reference (mt_oplog.h MT_OP_REF; always with OPF_LOCAL)
 OP_RELOAD, OP_COLLAB, OP_APPEND = 5, 6, 7  # snapshot load records (mt_oplog.h)
 OPF_LOCAL = 0x80
 OPF_GROUPED = 0x40
+OPF_TREE = 0x20  # MergeTree-level call (mt_oplog.h MT_OPF_TREE)
+OPF_REGEN = 0x10  # regeneratePendingOp (MT_OPF_REGEN)
+OPF_ATREF = 0x08  # insertAtReferencePositionLocal (MT_OPF_ATREF)
 SEG_TEXT, SEG_MARKER, SEG_PERM = 0, 1, 2
 SEG_RELPOS = 0x80  # seg_kind flag: positions relative to markers (mt_oplog.h MT_SEG_RELPOS)
 RELPOS_UNITS = 10  # MT_RELPOS_UNITS

@@ -110,14 +110,47 @@ def _props_of(props, kv, pidx: int, interner: ol.Interner):
     return ps, ({"name": "rewrite"} if int(pr["combining"]) == ol.COMBINE_REWRITE else None)
 
 
+def _relpos_of(rec, text, interner: ol.Interner):
+    """(relativePos1, relativePos2) of an MT_SEG_RELPOS record: the MT_RELPOS_UNITS spec after the
+    record's text (oplog.DocLog.add_relative), None for an absolute end."""
+    base = int(rec["text_off"]) + int(rec["text_len"])
+    u = [int(x) for x in text[base: base + ol.RELPOS_UNITS]]
+    out = []
+    for i in range(2):
+        if not u[1] & (1 << i):
+            out.append(None)
+            continue
+        mid, fl, lo, hi = u[2 + 4 * i: 6 + 4 * i]
+        r = {"id": interner.value_obj(mid), "before": bool(fl & 1)}
+        if fl & 2:
+            off = lo | (hi << 16)
+            r["offset"] = off - (1 << 32) if off & 0x80000000 else off
+        out.append(r)
+    return out
+
+
 def record_op(rec, text, props, kv, interner: ol.Interner) -> Dict[str, Any]:
-    """The IMergeTreeOp (ops.ts:63-102) a (non-load) record stands for: the inverse of _op_record."""
+    """The IMergeTreeOp (ops.ts:63-102) a (non-load) record stands for: the inverse of _op_record,
+    including relativePos1/2 (MT_SEG_RELPOS records carry placeholder pos1/pos2 for a relative end)."""
     kind = int(rec["kind"]) & 7
+    if int(rec["kind"]) & ol.OPF_TREE:
+        raise ValueError("a MergeTree-level record (MT_OPF_TREE) is not a sequenced message")
     ps, comb = _props_of(props, kv, int(rec["props"]), interner)
+    sk = int(rec["seg_kind"])
+    rel = _relpos_of(rec, text, interner) if sk & ol.SEG_RELPOS else (None, None)
+    op = _record_op(rec, kind, sk & 0x7F, ps, comb, text)
+    for i, r in enumerate(rel):
+        if r is not None:
+            op.pop(f"pos{i + 1}", None)
+            op[f"relativePos{i + 1}"] = r
+    return op
+
+
+def _record_op(rec, kind, sk, ps, comb, text) -> Dict[str, Any]:
     if kind == ol.OP_INSERT:
-        if int(rec["seg_kind"]) == ol.SEG_PERM:
+        if sk == ol.SEG_PERM:
             seg = [int(rec["text_len"]), UNALLOCATED]
-        elif int(rec["seg_kind"]) == ol.SEG_MARKER:
+        elif sk == ol.SEG_MARKER:
             seg = {"marker": {"refType": int(rec["pos2"])}}
             if ps is not None:
                 seg["props"] = ps
@@ -145,6 +178,8 @@ def record_messages(ops, text, props, kv, interner: ol.Interner, long_name: Call
         k = int(rec["kind"])
         if k & ol.OPF_LOCAL or (k & 7) >= ol.OP_RELOAD:
             continue
+        if k & ol.OPF_TREE:
+            raise ValueError(f"record {i}: a MergeTree-level record (MT_OPF_TREE) is not a sequenced message")
         if k & ol.OPF_GROUPED:
             members.append(record_op(rec, text, props, kv, interner))
             continue

@@ -150,3 +150,53 @@ def test_capacity_promotion_mixed_batch():
     eng.sync()
     assert set(eng.promoted().tolist()) == promoted
     assert (eng.digests() == dig).all()
+
+
+@pytest.mark.gpu
+def test_capacity_promotion_incremental_batches():
+    """Two submit / run / sync rounds without a reset (what GpuClient's flush does on every read): the
+    coalescing-defeated documents overflow the small profile in the first round and are promoted; the
+    second round's records for them replay in the promoted engine on top of the state they hold. Every
+    document ends equal to the oracle over its whole log (a re-promotion from the second batch
+    alone used to drop the first batch's records)."""
+    from fluidframework_amd import gen
+    from fluidframework_amd.engine import Engine, default_caps
+    small = gen.generate(gen.config3(512), 6)
+    big = gen.generate(gen.config4(12000), 2)
+    docs = [small.doc_arrays(d) for d in range(small.ndocs)] + [big.doc_arrays(d) for d in range(big.ndocs)]
+    local = [int(x) for x in small.local_long_id] + [int(x) for x in big.local_long_id]
+    local = np.asarray(local, np.int32)
+
+    def cut(ops):  # a record boundary that does not split a group
+        i = len(ops) // 2
+        while i < len(ops) and ops["kind"][i] & 0x40:
+            i += 1
+        return i
+
+    halves = []
+    for part in (0, 1):
+        arr = []
+        for o, t, p, k in docs:
+            c = cut(o)
+            arr.append((o[:c] if part == 0 else o[c:], t, p, k))
+        halves.append(ol.Batch.from_arrays(arr, local))
+    want = []
+    for d, arrays in enumerate(docs):
+        c = oc.OracleClient()
+        c.start_collab(int(local[d]))
+        assert c.replay_arrays(*arrays) == 0
+        want.append(c)
+    eng = Engine(len(docs), **default_caps(512))
+    eng.start_collab(local)
+    eng.replay(halves[0])
+    first = set(eng.promoted().tolist())
+    assert {len(docs) - 2, len(docs) - 1} <= first
+    eng.replay(halves[1])  # no reset: the promoted documents continue in the promoted engine
+    err, err_op = eng.errors()
+    assert (err == 0).all(), (err, err_op)
+    assert set(eng.promoted().tolist()) == first
+    dig = eng.digests()
+    for d in range(len(docs)):
+        assert dig[d] == want[d].digest(), f"doc {d}"
+    assert eng.get_text(len(docs) - 1) == want[-1].get_text()
+    eng.close()

@@ -7,6 +7,8 @@ import pytest
 from fluidframework_amd import gen
 from fluidframework_amd import oplog as ol
 import oracle_client as oc
+import persp_logs
+from fluidframework_amd.engine import EngineError
 from replicas import parse_dump
 
 pytestmark = pytest.mark.gpu
@@ -168,7 +170,15 @@ def test_matrix_permutation_vectors_config5():
         c.replay_arrays(ops, text, props, kv)
         cur = c.current_seq
         for k in (0, 3):
-            assert eng.get_length(d, cur - 5, k) == c.get_length_at(cur - 5, k)
+            # a perspective past every refSeq client k has sent an op under is answered (and equals the
+            # oracle); an earlier one is refused (tests/test_ref_persp.py, mt_kernels.h persp_refused)
+            if persp_logs.answered(ops, int(b.local_long_id[d]), cur - 5, k):
+                assert eng.get_length(d, cur - 5, k) == c.get_length_at(cur - 5, k)
+            else:
+                with pytest.raises(EngineError) as ex:
+                    eng.get_length(d, cur - 5, k)
+                assert ex.value.code == 4
+            assert eng.get_length(d, cur, k) == c.get_length_at(cur, k)
 
 
 def test_containing_segment_and_position():

@@ -75,3 +75,54 @@ def test_gpu_relative_positions_match_reference():
     assert np.array_equal(eng.digests(), z["digests"])
     got = [eng.pos_from_relative_pos(d, k, v, bf, o) for d, k, v, bf, o in queries(z, interner)]
     assert got == z["answers"].tolist()
+
+
+def _annotated_id_log():
+    """a marker inserted with markerId "a" whose markerId a later annotate sets to "b"; then a relative
+    insert after "b". The reference's idToSegment still maps "a" (written at insert, mergeTree.ts:1218-1221)
+    and has no "b", so it would place the insert at -1; the engine refuses the lookup."""
+    from fluidframework_amd import oplog as ol
+    it = ol.Interner()
+    L = ol.DocLog(it, local_long_id=0)
+    base = dict(client=1, ref_seq=0, min_seq=0)
+    L.add(ol.OP_INSERT, seq=1, pos1=0, text="abc", **base)
+    L.add(ol.OP_INSERT, seq=2, pos1=1, marker=0, props={"markerId": "a"}, **base)
+    L.add(ol.OP_ANNOTATE, seq=3, pos1=1, pos2=2, props={"markerId": "b"}, **base)
+    L.add(ol.OP_INSERT, seq=4, pos1=0, text="y", **base)
+    n = len(L.ops)
+    relpos_logs.add_rel(L, ol.OP_INSERT, ("b", False, None), None, seq=5, pos1=0, text="x", **base)
+    return it, L, n
+
+
+def test_annotated_marker_id_is_refused_host():
+    it, L, n = _annotated_id_log()
+    from fluidframework_amd import oplog as ol
+    b = ol.Batch.from_logs([L])
+    _, err, st = core_host.replay_batch(b, CAPS, dcap=64)
+    assert err[0] == 4 and st.error_op(0) == n
+    b0 = ol.Batch.from_arrays([tuple(a[:n] if i == 0 else a for i, a in enumerate(L.arrays()))], [0])
+    _, err, st = core_host.replay_batch(b0, CAPS, dcap=64)
+    assert err[0] == 0
+    kid = it.key(relpos_logs.MARKER_KEY)
+    with pytest.raises(RuntimeError):
+        st.pos_from_relative_pos(0, kid, it.value("b"))
+
+
+@pytest.mark.gpu
+def test_annotated_marker_id_is_refused_gpu():
+    from fluidframework_amd import oplog as ol
+    from fluidframework_amd.engine import Engine, EngineError
+    it, L, n = _annotated_id_log()
+    eng = Engine(1, ncap=192, hcap=256, acap=1 << 16, mcap=4096, gcap=1024, ccap=64, dcap=64)
+    eng.start_collab([0])
+    eng.replay(ol.Batch.from_logs([L]))
+    err, err_op = eng.errors()
+    assert err[0] == 4 and err_op[0] == n
+    eng.close()
+    eng = Engine(1, ncap=192, hcap=256, acap=1 << 16, mcap=4096, gcap=1024, ccap=64)  # hot build: query path
+    eng.start_collab([0])
+    eng.replay(ol.Batch.from_arrays([tuple(a[:n] if i == 0 else a for i, a in enumerate(L.arrays()))], [0]))
+    assert (eng.errors()[0] == 0).all()
+    with pytest.raises(EngineError):
+        eng.pos_from_relative_pos(0, it.key(relpos_logs.MARKER_KEY), it.value("b"))
+    eng.close()

@@ -188,3 +188,36 @@ def test_wire_relative_positions_rebuild_the_fixture_logs():
         o2, t2, _, _ = log.arrays()
         assert np.array_equal(o2, ops)
         assert np.array_equal(t2[: len(t2)], text[: len(t2)])
+
+
+def test_record_messages_round_trip_relative_positions():
+    """wire.record_messages (the catch-up messages of a legacy summary) is the inverse of wire.add_message on
+    logs with relativePos1/2: relative ends come back as IRelativePosition, not as their placeholder
+    pos1/pos2 = 0, relative marker inserts stay markers, and re-ingesting the messages gives the records again;
+    a MergeTree-level record (MT_OPF_TREE) is not a message and raises."""
+    import relpos_logs
+    b, interner, _ = relpos_logs.build(3, 300, 11)
+    for d in range(b.ndocs):
+        ops, text, props, kv = b.doc(d)
+        names = wire.ClientNames([f"c{i}" for i in range(8)])
+        msgs = wire.record_messages(ops, text, props, kv, interner, lambda i: f"c{i}")
+        assert len(msgs) == len(ops)
+        nrel = 0
+        for (m, i) in msgs:
+            c = m["contents"]
+            if int(ops[i]["seg_kind"]) & ol.SEG_RELPOS:
+                nrel += 1
+                assert "relativePos1" in c or "relativePos2" in c
+                if "relativePos1" in c:
+                    assert "pos1" not in c and isinstance(c["relativePos1"]["id"], str)
+            if c["type"] == ol.OP_INSERT and (int(ops[i]["seg_kind"]) & 0x7F) == ol.SEG_MARKER:
+                assert "marker" in c["seg"]
+        assert nrel > 0
+        log = ol.DocLog(interner, local_long_id=0)
+        wire.add_messages(log, [m for m, _ in msgs], names)
+        o2, t2, _, _ = log.arrays()
+        assert np.array_equal(o2, ops)
+    tree = ops.copy()
+    tree["kind"][0] |= ol.OPF_TREE
+    with pytest.raises(ValueError):
+        wire.record_messages(tree, text, props, kv, interner, lambda i: f"c{i}")

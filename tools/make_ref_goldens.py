@@ -619,6 +619,58 @@ def make_legacy(names, node: str) -> None:
               f"{[len(json.loads(sn_blobs(t)['catchupOps'])) if t else -1 for t in trees[:8]]}", flush=True)
 
 
+def make_persp(node: str) -> None:
+    """tests/golden/refpersp_<set>.npz: the reference's getLength, getContainingSegment + getPosition and
+    getText answers at past (refSeq, clientId) perspectives inside and below the collaboration window
+    (tests/persp_logs.py), after replaying whole and cut logs. Stored: the cuts, the queries, every answer
+    (lengths; containing-segment tuples; text lengths and FNV-1a-64 of the UTF-16LE units)."""
+    import persp_logs as pl
+    for name in pl.SETS:
+        b, cuts = pl.batch(name)
+        q = pl.queries(b, 9000 + len(name))
+        d = os.path.join(SCRATCH, name + "_persp")
+        write_batch(b, gen.generator_interner(), d)
+        lq = [[int(x[1]), int(x[2]), int(x[3])] for x in q if x[0] == pl.Q_LEN]
+        sq = [[int(x[1]), int(x[4]), int(x[2]), int(x[3])] for x in q if x[0] == pl.Q_SEG]
+        tq = [[int(x[1]), int(x[2]), int(x[3]), "", None if x[4] == -(1 << 31) else int(x[4]),
+               None if x[5] == -(1 << 31) else int(x[5])] for x in q if x[0] == pl.Q_TEXT]
+        for f, v in (("lenqueries.json", lq), ("queries.json", sq), ("textqueries.json", tq)):
+            with open(os.path.join(d, f), "w") as fh:
+                json.dump(v, fh)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d], capture_output=True,
+                           text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+        errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
+        if errs:
+            raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
+        lens = json.load(open(os.path.join(d, "ref_lengths.json")))
+        segs = json.load(open(os.path.join(d, "ref_answers.json")))
+        texts = json.load(open(os.path.join(d, "ref_texts.json")))
+        ans = np.zeros((len(q), 6), np.int64)
+        il = iter(lens)
+        isg = iter(segs)
+        it = iter(texts)
+        for i, x in enumerate(q):
+            if x[0] == pl.Q_LEN:
+                ans[i, 0] = next(il)
+            elif x[0] == pl.Q_SEG:
+                ans[i, :] = next(isg)
+            else:
+                t = next(it)
+                ans[i, 0] = len(t)
+                ans[i, 1] = np.int64(np.uint64(fnv1a64(t.encode("utf-16-le"))).view(np.int64))
+        legal = np.asarray([pl.answered(b.doc(int(x[1]))[0], int(b.local_long_id[int(x[1])]), int(x[2]), int(x[3]))
+                            for x in q])
+        np.savez_compressed(
+            os.path.join(GOLDEN, f"refpersp_{name}.npz"), cuts=cuts, log_sha256=log_sha(b), queries=q, answers=ans,
+            source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                    "tools/ref_replay.mjs: MergeTree.getLength / getContainingSegment + getPosition / "
+                    "MergeTreeTextHelper.getText at past perspectives"))
+        print(f"refpersp_{name}: {b.ndocs} docs, {len(q)} queries, {int(legal.sum())} at perspectives the engine "
+              f"answers", flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default=",".join(SETS))
@@ -631,8 +683,12 @@ def main() -> None:
     ap.add_argument("--handles", action="store_true", help="write the PermutationVector handle fixture only")
     ap.add_argument("--relpos", action="store_true", help="write the relative-position fixture (refrelpos.npz) only")
     ap.add_argument("--tree", action="store_true", help="write the MergeTree-level record fixtures (reftree_*.npz) only")
+    ap.add_argument("--persp", action="store_true", help="write the past-perspective read fixtures (refpersp_*.npz) only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
+    if args.persp:
+        make_persp(args.node)
+        return
     if args.texts:
         make_texts(args.node)
         return

@@ -29,6 +29,8 @@ def main():
         build()
         return
     import numpy as np
+    if not os.path.exists(LIB):  # kept out of the default push (.gpurunignore): built where it runs
+        build()
     os.environ["MT_REPLAY_LIB"] = LIB
     from fluidframework_amd import gen
     from fluidframework_amd.engine import Engine, default_caps, lib

@@ -524,6 +524,12 @@ const texts = [];
 const rqpath = path.join(dir, "relqueries.json");
 const relQueries = fs.existsSync(rqpath) ? JSON.parse(fs.readFileSync(rqpath)) : [];
 const relAnswers = [];
+// optional getLength queries (lenqueries.json: [[doc, refSeq, longClient | -1 = local view], ...]):
+// MergeTree.getLength(refSeq, clientId) (mergeTree.ts:1610-1612: the root's PartialSequenceLengths for a
+// remote perspective, cachedLength for the local client) -> ref_lengths.json
+const lqpath = path.join(dir, "lenqueries.json");
+const lenQueries = fs.existsSync(lqpath) ? JSON.parse(fs.readFileSync(lqpath)) : [];
+const lengths = [];
 const t0 = process.hrtime.bigint();
 const dumps = [], errs = {};
 for (let d = 0; d < ndocs; d++) {
@@ -559,6 +565,14 @@ for (let d = 0; d < ndocs; d++) {
             const cid = local ? mt.collabWindow.clientId : c.getOrAddShortClientId(name(cl));
             const helper = new MT.MergeTreeTextHelper(mt);
             texts.push(helper.getText(refSeq, cid, ph, st === null ? undefined : st, en === null ? undefined : en));
+        }
+        for (const [qd, ref, cl] of lenQueries) {
+            if (qd !== d) continue;
+            const mt = c.mergeTree;
+            const local = cl < 0;
+            const refSeq = local ? mt.collabWindow.currentSeq : ref;
+            const cid = local ? mt.collabWindow.clientId : c.getOrAddShortClientId(name(cl));
+            lengths.push(mt.getLength(refSeq, cid));
         }
         for (const [qd, id, before, offset] of relQueries) {
             if (qd !== d) continue;
@@ -656,6 +670,7 @@ if (Object.keys(refPositions).length) {
 fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
 if (queries.length) fs.writeFileSync(path.join(dir, "ref_answers.json"), JSON.stringify(answers));
 if (textQueries.length) fs.writeFileSync(path.join(dir, "ref_texts.json"), JSON.stringify(texts));
+if (lenQueries.length) fs.writeFileSync(path.join(dir, "ref_lengths.json"), JSON.stringify(lengths));
 if (withHandles) {
     const snap = {};
     for (const d of Object.keys(handleTables)) snap[d] = handleTables[d].snapshot();
