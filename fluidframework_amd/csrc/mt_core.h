@@ -108,6 +108,10 @@ enum : int32_t {
     REF_DETACHED = -1,
     REF_SAVED = -2, /* on a row the current remove took (mergeTree.ts:2673-2676) */
     REF_GHOST = -3, /* addLocalReference threw: refsByOffset[offset].at is undefined (localReference.ts:195-201) */
+    /* removeLocalReference took it out of its segment's collection (localReference.ts:225-264): the
+     * LocalReference keeps `segment` and `offset` (toPosition still answers) but no longer follows splits,
+     * appends or slides. Stored as rid = REF_FROZEN - (the row id), ek = the row's generation then. */
+    REF_FROZEN = -16,
 };
 /* a segment's LocalReferenceCollection: its row id and refsByOffset.length, which is what an append adds
  * to the offsets of the references it takes over (localReference.ts:211-223). That length follows the
@@ -852,6 +856,32 @@ struct Replica {
         d.refs()[n] = r;
         st->nref = n + 1;
     }
+    /* Client.removeLocalReference (client.ts:299-301) -> MergeTree.removeLocalReference (mergeTree.ts:
+     * 2761-2769) -> LocalReferenceCollection.removeLocalRef (localReference.ts:225-264) of reference i: found
+     * in its segment's refsByOffset[offset] lists, it leaves the collection (refCount--; the array keeps its
+     * length; hierRefCount only counts labelled references, which MT_OP_REF does not make). A detached
+     * reference (segment undefined: the reference's call throws before touching the tree), one whose add
+     * threw, or one already removed is not in any collection: no-op. */
+    MT_HD void remove_ref(int32_t i) {
+        if (i < 0 || i >= d.dstate()->nref) {
+            fail(E_ASSERT);
+            return;
+        }
+        LRef r = d.refs()[i];
+        if (r.rid < 0) return;
+        if (w.lane() == 0) {
+            d.refs()[i].rid = REF_FROZEN - r.rid;
+            d.refs()[i].ek = z.rgen[r.rid];
+        }
+        w.sync();
+    }
+    /* the slot of a reference's segment, -1 when it has none in the tree (detached, ghost, or a removed
+     * reference whose segment left the tree: appended into its neighbour or unlinked, `parent` undefined) */
+    MT_HD int32_t ref_slot(const LRef& r) {
+        if (r.rid >= 0) return slot_of(r.rid, -1);
+        if (r.rid <= REF_FROZEN) return slot_of(REF_FROZEN - r.rid, r.ek);
+        return -1;
+    }
     /* after a remove took rows holding references (markRangeRemoved, mergeTree.ts:2703-2732): under the
      * op's perspective, SlideOnRemove references go to offset 0 of the segment at `start`
      * (addBeforeTombstones) or, past the end, to the last offset of the last segment (addAfterTombstones);
@@ -909,9 +939,13 @@ struct Replica {
             return false;
         }
         LRef r = d.refs()[op.pos1];
-        if (r.rid < 0 || seg_len(op) <= 0) return false; /* DetachedPosition / a zero-length segment: no-op */
-        int32_t s = slot_of(r.rid, -1);
-        if (s < 0) return false;
+        if ((r.rid < 0 && r.rid > REF_FROZEN) || seg_len(op) <= 0)
+            return false; /* DetachedPosition / a zero-length segment: no-op */
+        int32_t s = ref_slot(r);
+        if (s < 0) { /* a removed reference whose segment left the tree: not modelled */
+            if (r.rid <= REF_FROZEN) fail(E_UNSUPPORTED);
+            return false;
+        }
         int32_t rs0 = z.rseq(s);
         int32_t off = (rs0 != NOREM && rs0 != 0) ? 0 : r.off; /* getOffset() */
         if (off != 0 && local_len(s) != 0) {
@@ -949,8 +983,7 @@ struct Replica {
     MT_HD int32_t ref_position(int32_t i) {
         LRef r = d.refs()[i];
         if (r.rid == REF_GHOST) return -2;
-        if (r.rid < 0) return -1;
-        int32_t s = slot_of(r.rid, -1);
+        int32_t s = ref_slot(r);
         if (s < 0) return -1;
         int32_t rs = z.rseq(s);
         return local_pos(s) + (rs != NOREM && rs != 0 ? 0 : r.off);
@@ -3875,7 +3908,10 @@ struct Replica {
         }
         if (kind == MT_OP_REF) { /* a local reference (mt_oplog.h): the client-feature build keeps them */
             if constexpr (DL) {
-                if (op.kind & MT_OPF_LOCAL) add_ref(op.pos1, op.pos2);
+                if ((op.kind & MT_OPF_LOCAL) && op.seg_kind == MT_REF_REMOVE)
+                    remove_ref(op.pos1);
+                else if (op.kind & MT_OPF_LOCAL)
+                    add_ref(op.pos1, op.pos2);
             } else {
                 fail(E_UNSUPPORTED);
             }

@@ -114,6 +114,8 @@ export declare class GpuClient {
     createLocalReference(pos: number, refType?: number): LocalReferenceHandle;
     /** LocalReference.toPosition(): -1 detached; throws where the reference's addLocalReference threw */
     localReferencePosition(ref: LocalReferenceHandle): number;
+    /** Client.removeLocalReference: the reference leaves its segment's collection (keeps segment and offset) */
+    removeLocalReference(ref: LocalReferenceHandle): void;
     insertAtReferencePositionLocal(ref: LocalReferenceHandle, text: string): void;
     /** Client.regeneratePendingOp for every op in flight (engines with caps.dcap > 0) */
     regeneratePendingOps(): Array<{ type: number; pos1: number; length: number }>;

@@ -20,6 +20,7 @@ const addon = require(process.env.MT_NAPI_ADDON || path.join(__dirname, "..", "b
 
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, GROUP: 3, NOOP: 4 };
 const OP_REF = 3; // record kind of a local reference (include/mt_oplog.h MT_OP_REF)
+const REF_REMOVE = 1; // seg_kind of an MT_OP_REF record that removes the reference (MT_REF_REMOVE)
 const OPF_LOCAL = 0x80;
 const OPF_GROUPED = 0x40;
 const OPF_ATREF = 0x08; // insertAtReferencePositionLocal
@@ -363,6 +364,14 @@ class GpuClient {
     createLocalReference(pos, refType = ReferenceType.SlideOnRemove) {
         this.engine.enqueue(this.doc, OP_REF | OPF_LOCAL, { pos1: pos, pos2: refType });
         return { doc: this.doc, index: this.engine.nrefs[this.doc]++ };
+    }
+
+    /* Client.removeLocalReference (client.ts:299-301 -> LocalReferenceCollection.removeLocalRef,
+     * localReference.ts:225-264): the reference leaves its segment's collection and stops following splits,
+     * appends and slides; it keeps its segment and offset (localReferencePosition still answers, -1 once that
+     * segment leaves the tree). A detached reference's removal throws in the reference: a no-op here. */
+    removeLocalReference(ref) {
+        this.engine.enqueue(this.doc, OP_REF | OPF_LOCAL, { pos1: ref.index, seg_kind: REF_REMOVE });
     }
 
     /* LocalReference.toPosition() (localReference.ts:62-68): -1 detached. A reference whose creation the

@@ -355,12 +355,15 @@ def _chunks(tree: dict):
     return head, body, catchup
 
 
-def load_records(tree: dict, log: ol.DocLog, client_index, local_client: Optional[str] = "snapshot") -> dict:
+def load_records(tree: dict, log: ol.DocLog, client_index, local_client: Optional[str] = "snapshot",
+                 catchup: bool = True) -> dict:
     """Append a snapshot's load records to `log` (one document's event stream); returns the header
     metadata. `client_index(name)` maps a long client id to the batch's long-client index;
     `local_client` is the id startOrUpdateCollaboration gets (None: a detached load, no collaboration,
-    snapshotLoader.ts:135-151)."""
-    head, chunks, catchup = _chunks(tree)
+    snapshotLoader.ts:135-151). `catchup` False leaves out the catch-up messages a legacy summary carries (what
+    TestClient.createFromSnapshot does: it awaits them but applies none, testClient.ts:57-73)."""
+    head, chunks, ops = _chunks(tree)
+    catchup = ops if catchup else []
     md = head["headerMetadata"]
     body = [spec for c in chunks for spec in c["segments"]]
 

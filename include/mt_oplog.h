@@ -39,7 +39,7 @@ enum {
      * offset Client.getContainingSegment(pos1) returns in the local view (client.ts:1006); pos2 =
      * refType (ReferenceType, ops.ts; SlideOnRemove = 0x40). The document's references are numbered in
      * creation order; a position past the end makes a detached reference. */
-    MT_OP_REF = 3,
+    MT_OP_REF = 3, /* with seg_kind = MT_REF_REMOVE: Client.removeLocalReference of reference pos1 */
     MT_OP_NOOP = 4, /* sequenced message that is not a merge-tree op: advances currentSeq/MSN only. With
                      * MT_OPF_LOCAL: PermutationVector.getAllocatedHandle(pos1) (permutationvector.ts:
                      * 157-183) in the local view: the PermutationSegment at pos1 keeps its handle if it has
@@ -67,6 +67,10 @@ enum {
 #define MT_CLIENT_NONCOLLAB 0xFFFF /* NonCollabClient (constants.ts:15) */
 #define MT_OP_KIND_MASK 0x07
 #define MT_OPF_LOCAL 0x80 /* unsequenced local edit made by this replica */
+/* seg_kind of an MT_OP_REF | MT_OPF_LOCAL record that removes reference pos1 (creation order) from its
+ * segment's LocalReferenceCollection (Client.removeLocalReference, client.ts:299-301 ->
+ * LocalReferenceCollection.removeLocalRef, localReference.ts:225-264); 0 creates one */
+#define MT_REF_REMOVE 1
 /* A group op (MergeTreeDeltaType.GROUP, ops.ts:33, 100; e.g. SharedString.replaceRange,
  * sequence.ts:464) is one sequenced message carrying several member ops: it is sent as its member
  * records in order, all with the message's client/seq/ref_seq/min_seq, every member but the last

@@ -73,3 +73,45 @@ def inject(b: ol.Batch, caps, nref: int = 24, seed: int = 4242) -> ol.Batch:
         out.append(merged)
         off.append(off[-1] + len(merged))
     return dataclasses.replace(b, ops=np.concatenate(out), op_off=np.asarray(off, np.int64))
+
+
+REF_REMOVE = 1  # mt_oplog.h MT_REF_REMOVE (seg_kind of an MT_OP_REF record)
+
+
+def add_removals(b: ol.Batch, frac: float = 0.4, seed: int = 777) -> ol.Batch:
+    """Client.removeLocalReference records (MT_OP_REF | MT_OPF_LOCAL, seg_kind MT_REF_REMOVE, pos1 = the
+    reference's creation index): about `frac` of each document's references are removed at a seeded point
+    after their creation (never inside a group message), a few of them twice; the rest of the stream then
+    splits, appends and slides around them."""
+    out, off = [], [0]
+    for d in range(b.ndocs):
+        ops = b.ops[b.op_off[d]: b.op_off[d + 1]]
+        rng = np.random.default_rng(seed + d)
+        is_ref = ((ops["kind"] & 7) == ol.OP_REF) & ((ops["kind"] & ol.OPF_LOCAL) != 0)
+        created = np.nonzero(is_ref)[0]
+        grouped = (ops["kind"] & ol.OPF_GROUPED) != 0
+        ok = np.ones(len(ops) + 1, bool)
+        ok[1:] = ~grouped
+        ins = []  # (insert before index, reference index)
+        for k, ci in enumerate(created):
+            if rng.random() >= frac:
+                continue
+            cand = np.nonzero(ok[ci + 1:])[0] + ci + 1
+            at = int(rng.choice(cand))
+            ins.append((at, k))
+            if rng.random() < 0.15:  # a second removal of the same reference: a no-op in the reference
+                ins.append((int(rng.choice(cand[cand >= at])), k))
+        ins.sort(key=lambda x: x[0])
+        pieces, prev = [], 0
+        for at, k in ins:
+            r = np.zeros(1, ol.OP_DTYPE)
+            r["kind"] = ol.OP_REF | ol.OPF_LOCAL
+            r["seg_kind"] = REF_REMOVE
+            r["pos1"] = k
+            pieces += [ops[prev:at], r]
+            prev = at
+        pieces.append(ops[prev:])
+        merged = np.concatenate(pieces)
+        out.append(merged)
+        off.append(off[-1] + len(merged))
+    return dataclasses.replace(b, ops=np.concatenate(out), op_off=np.asarray(off, np.int64))

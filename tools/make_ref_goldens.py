@@ -300,7 +300,7 @@ def run_refs(rb, d: str, node: str):
     return nref, pos, digests, inside, past
 
 
-def make_refs(names, node: str) -> None:
+def make_refs(names, node: str, removals: bool = False) -> None:
     """tests/golden/refrefs_<set>.npz: local references (MT_OP_REF records injected by tests/refs_inject.py)
     replayed by the reference, then up to 4 insertAtReferencePositionLocal records per document appended
     at the end of its stream on references the first pass left attached. Stored: the targets, and after
@@ -315,6 +315,8 @@ def make_refs(names, node: str) -> None:
         b = gen.generate(w, ids=ids, threads=8)
         c = caps_for(w)
         rb = refs_inject.inject(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
+        if removals:  # Client.removeLocalReference records (MT_REF_REMOVE) after the references' creation
+            rb = refs_inject.add_removals(rb)
         _, pos1, _, inside, past = run_refs(rb, os.path.join(SCRATCH, name + "_refs"), node)
         targets = np.full((rb.ndocs, 4), -1, np.int32)
         for i in range(rb.ndocs):
@@ -329,14 +331,15 @@ def make_refs(names, node: str) -> None:
         nref, pos, digests, _, _ = run_refs(rb2, os.path.join(SCRATCH, name + "_refs2"), node)
         npast = int(sum(past[i, t[t >= 0]].sum() for i, t in enumerate(targets)))
         np.savez_compressed(
-            os.path.join(GOLDEN, f"refrefs_{name}.npz"),
+            os.path.join(GOLDEN, f"{'refunref' if removals else 'refrefs'}_{name}.npz"),
+            nremove=int((((rb2.ops["kind"] & 7) == ol.OP_REF) & (rb2.ops["seg_kind"] == refs_inject.REF_REMOVE)).sum()),
             workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(rb2),
             nref=nref, positions=pos, digests=digests, atref_targets=targets, atref_past_end=npast,
             source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
                     "tools/ref_replay.mjs: LocalReference + Client.addLocalReference, "
                     "insertAtReferencePositionLocal, toPosition() at the end"),
         )
-        print(f"refrefs_{name}: {rb2.ndocs} docs, {int(nref.sum())} references: {int((pos >= 0).sum())} attached, "
+        print(f"{'refunref' if removals else 'refrefs'}_{name}: {rb2.ndocs} docs, {int(nref.sum())} references: {int((pos >= 0).sum())} attached, "
               f"{int((pos == -2).sum())} the reference could not add; {int((targets >= 0).sum())} inserts at "
               f"references, {npast} of them past their segment's end", flush=True)
 
@@ -683,6 +686,7 @@ def main() -> None:
     ap.add_argument("--handles", action="store_true", help="write the PermutationVector handle fixture only")
     ap.add_argument("--relpos", action="store_true", help="write the relative-position fixture (refrelpos.npz) only")
     ap.add_argument("--tree", action="store_true", help="write the MergeTree-level record fixtures (reftree_*.npz) only")
+    ap.add_argument("--unref", action="store_true", help="write the removeLocalReference fixtures (refunref_*.npz) only")
     ap.add_argument("--persp", action="store_true", help="write the past-perspective read fixtures (refpersp_*.npz) only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
@@ -709,6 +713,9 @@ def main() -> None:
         return
     if args.refs:
         make_refs([n for n in args.sets.split(",") if n in REF_SETS], args.node)
+        return
+    if args.unref:
+        make_refs([n for n in args.sets.split(",") if n in REF_SETS], args.node, removals=True)
         return
     if args.deltas:
         make_deltas([n for n in args.sets.split(",") if n in SETS], args.node)

@@ -201,6 +201,15 @@ function applyRange(client, doc, from, to) {
                 const ps = propSet(doc, rec.props);
                 const sent = client.annotateRangeLocal(rec.pos1, rec.pos2, ps ? ps.set : {}, ps ? ps.combiningOp : undefined);
                 if (sent && client.getCollabWindow().collaborating) pendingOps.push({ op: sent, group: client.peekPendingSegmentGroups() });
+            } else if (kind === 3 && rec.seg_kind === 1) { // MT_REF_REMOVE: Client.removeLocalReference
+                const r = curRefs[rec.pos1];
+                if (r) {
+                    try {
+                        client.removeLocalReference(r);
+                    } catch (e) { // a detached reference (segment undefined): the call throws, the tree is
+                        removeThrew++; // untouched
+                    }
+                }
             } else if (kind === 3) { // a local reference (mt_oplog.h MT_OP_REF) at getContainingSegment(pos1)
                 const { segment, offset } = client.getContainingSegment(rec.pos1);
                 let lref = null;
@@ -349,6 +358,7 @@ let curRefs = []; // the local references of the document being replayed, in cre
 let pendingOps = [];
 const regenWords = [];
 const threwRefs = new Set(); // references whose addLocalReference threw
+let removeThrew = 0; // removeLocalReference calls that threw (detached references)
 const refPositions = {};
 const refInside = {};
 const refPastEnd = {};
@@ -677,6 +687,6 @@ if (withHandles) {
     fs.writeFileSync(path.join(dir, "ref_handles.json"), JSON.stringify(snap));
 }
 if (relQueries.length) fs.writeFileSync(path.join(dir, "ref_relpos.json"), JSON.stringify(relAnswers));
-console.log(JSON.stringify({ ndocs, errors: Object.keys(errs).length, seconds: secs }));
+console.log(JSON.stringify({ ndocs, errors: Object.keys(errs).length, seconds: secs, removeThrew }));
 }
 main().catch((e) => { console.error(e); process.exit(1); });
