@@ -663,6 +663,15 @@ struct Replica {
     /* PermutationVector.getAllocatedHandle(pos) (157-183) in the local view: the handle of the row at pos
      * (getMaybeHandle: start + offset when allocated), else walkSegments(pos, pos + 1, splitRange) splits a
      * one-row segment out at pos and HandleTable.allocate()s its start */
+    /* MergeTree.mapRange's splitRange (mergeTree.ts:2830-2838) in the local view (Client.walkSegments,
+     * client.ts:276-285): ensureIntervalBoundary at a truthy start, then at a truthy end (one call site) */
+    MT_HD void split_range(int32_t a, int32_t b) {
+#pragma clang loop unroll(disable)
+        for (int32_t i = 0; i < 2; i++) {
+            int32_t p = i ? b : a;
+            if (p) ensure_boundary(p, h.currentSeq, h.localShort);
+        }
+    }
     MT_HD void alloc_handle(int32_t pos) {
         if (!ht_on()) {
             fail(E_UNSUPPORTED);
@@ -679,8 +688,7 @@ struct Replica {
             return;
         }
         if (cold(s).toff != 0) return; /* isHandleValid(start + offset) */
-        ensure_boundary(pos, h.currentSeq, h.localShort);
-        ensure_boundary(pos + 1, h.currentSeq, h.localShort);
+        split_range(pos, pos + 1); /* walkSegments(pos, pos + 1, ..., splitRange = true) */
         s = containing(pos, h.currentSeq, h.localShort, &off);
         if (s < 0 || off != 0 || z.len(s) != 1) {
             fail(E_ASSERT);
@@ -3946,11 +3954,15 @@ struct Replica {
             int32_t start = op.pos1, end = op.pos2;
             bool bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
             if (kind != MT_OP_INSERT && end <= start) bad = true;
-            if (kind == MT_OP_NOOP) { /* PermutationVector.getAllocatedHandle(pos1) (mt_oplog.h) */
-                if constexpr (DL)
-                    alloc_handle(op.pos1);
-                else
+            if (kind == MT_OP_NOOP) { /* PermutationVector.getAllocatedHandle(pos1), or walkSegments' split (mt_oplog.h) */
+                if constexpr (DL) {
+                    if (op.seg_kind == MT_NOOP_SPLIT)
+                        split_range(op.pos1, op.pos2);
+                    else
+                        alloc_handle(op.pos1);
+                } else {
                     fail(E_UNSUPPORTED);
+                }
             } else if (kind == MT_OP_INSERT && (op.kind & MT_OPF_ATREF)) { /* pos1 is a reference, not a position */
                 if constexpr (DL) {
                     edit = insert_at_ref(op, &eat);
@@ -4276,6 +4288,12 @@ struct Replica {
         return slot_at(t);
     }
     /* getPosition: the summed perspective lengths of every row before slot s in document order */
+    /* the index of slot s in walkAllSegments order (the canonical dump's record index): every row before it */
+    MT_HD int32_t ordinal_of(int32_t s) {
+        int32_t ks = kpos(s / MAXN), total = s & (MAXN - 1);
+        for (int32_t k = 0; kvalid(k) && k != ks; k = knext(k)) total += nch[leaf_at(k)];
+        return total;
+    }
     MT_HD int32_t position_of(int32_t s, int32_t refSeq, int32_t client) {
         int32_t k0 = kpos(s / MAXN), j0 = s & (MAXN - 1);
         int32_t total = 0;

@@ -345,18 +345,44 @@ __global__ __launch_bounds__(WG) void k_text(Store<HT> st, int64_t doc, int32_t 
     if (threadIdx.x == 0) *n = m;
 }
 
-/* getContainingSegment (mode 0: a = pos) / getPosition (mode 1: a = rid, b = gen) / a marker's position by
- * id (mode 2: a = marker-id key, b = value) of one document;
- * out[0] = status (1 found / 0 none), then mt_seg_ref fields or the position */
+/* Per-document segment queries (one workgroup); out[0] = status (1 found / 0 none / 2 several markers /
+ * 3 refused perspective), then by mode:
+ *   0 getContainingSegment(a = pos): mt_seg_ref fields {rid, gen, offset, length, seq, client, removedSeq,
+ *     removedClient, ordinal} in out[1..9]
+ *   1 getPosition(a = rid, b = gen): out[1]
+ *   2 posFromRelativePos' marker (a = marker-id key, b = value): its position, out[1]
+ *   3 HandleCache.getHandle(a = pos): out[1]
+ *   4 a remote client's position a under (ref_seq, long_client) in the local view (resolveRemoteClientPosition,
+ *     mergeTree.ts:2140-2160; PermutationVector.adjustPosition, permutationvector.ts:185-196): found: out[1] =
+ *     getPosition(segment) + offset, out[2] = the segment's removal flag; none: out[3] = getLength under the
+ *     remote perspective, out[4] = the local length
+ *   5 getMarkerFromId (a = key, b = value): mt_seg_ref fields of the marker, as mode 0
+ *   6 PermutationVector.handleToPosition (a = handle, b = localSeq; permutationvector.ts:198-253): the segment
+ *     whose allocated handles hold a, findReconnectionPostition(segment, localSeq) + its offset, out[1] */
+template <class R>
+__device__ inline void seg_fields(R& r, int32_t s, int32_t off, int32_t* res) {
+    int32_t rid = r.z.rid[s], rs = r.z.rseq(s);
+    res[0] = 1;
+    res[1] = rid;
+    res[2] = r.z.rgen[rid];
+    res[3] = off;
+    res[4] = r.z.len(s);
+    res[5] = r.z.seq(s);
+    res[6] = r.long_of(r.z.cli(s));
+    res[7] = rs;
+    res[8] = rs == NOREM ? 0 : r.long_of(r.z.rcli(s));
+    res[9] = r.ordinal_of(s);
+}
+#define MT_SEGQ_N 10
 template <class HT>
 __global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t mode, int32_t a, int32_t b,
                                            int32_t ref_seq, int32_t long_client, int32_t floor, int32_t* out) {
     Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
-    if (persp_refused(r, ref_seq, long_client, floor)) { /* out[0] = 3: refused (MT_E_UNSUPPORTED) */
-        if (threadIdx.x == 0) {
-            out[0] = 3;
-            for (int i = 1; i < 7; i++) out[i] = 0;
-        }
+    int32_t res[MT_SEGQ_N] = {0, -1, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (persp_refused(r, ref_seq, long_client, floor)) { /* res[0] = 3: refused (MT_E_UNSUPPORTED) */
+        res[0] = 3;
+        if (threadIdx.x == 0)
+            for (int i = 0; i < MT_SEGQ_N; i++) out[i] = res[i];
         return;
     }
     int32_t sh;
@@ -367,20 +393,10 @@ __global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t m
         sh = r.short_of(long_client);
         if (sh < 0) sh = 0x7fff; /* a client the replica has not seen: sequenced content only */
     }
-    int32_t res[7] = {0, -1, 0, 0, 0, 0, 0};
     if (mode == 0) {
         int32_t off = 0;
         int32_t s = r.containing(a, ref_seq, sh, &off);
-        if (s >= 0) {
-            int32_t rid = r.z.rid[s];
-            res[0] = 1;
-            res[1] = rid;
-            res[2] = r.z.rgen[rid];
-            res[3] = off;
-            res[4] = r.z.len(s);
-            res[5] = r.z.seq(s);
-            res[6] = r.long_of(r.z.cli(s));
-        }
+        if (s >= 0) seg_fields(r, s, off, res);
     } else if (mode == 1) {
         int32_t s = (a >= 0 && a < HT::S) ? r.slot_of(a, b) : -1;
         if (s >= 0) {
@@ -395,17 +411,70 @@ __global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t m
             res[0] = 1;
             res[1] = st ? (int32_t)st + off : INT32_MIN;
         }
-    } else { /* mode 2: the marker whose property a (the marker-id key) is value b; res[0] = 2 if several */
+    } else if (mode == 4) {
+        int32_t off = 0;
+        int32_t s = r.containing(a, ref_seq, sh, &off);
+        if (s >= 0) {
+            res[0] = 1;
+            res[1] = r.local_pos(s) + off;
+            res[2] = r.z.rseq(s) != NOREM;
+        } else {
+            res[3] = r.length(ref_seq, sh);
+            res[4] = r.length_local();
+        }
+    } else if (mode == 6) {
+        int32_t s = -1, off = 0;
+        for (int32_t k = 0; s < 0 && r.kvalid(k); k = r.knext(k)) { /* walkAllSegments: the first match */
+            int32_t n = r.leaf_at(k), c = r.nch[n];
+            int32_t j = threadIdx.x;
+            bool hit = false;
+            int32_t q = n * MAXN + (j & (MAXN - 1));
+            if (j < c && j < MAXN && (r.z.flags(q) & RF_PERM)) {
+                int32_t h0 = (int32_t)r.cold(q).toff;
+                hit = h0 != 0 && h0 <= a && a < h0 + r.z.len(q);
+            }
+            uint64_t m = r.w.ballot(hit);
+            if (m) {
+                s = n * MAXN + r.w.ffs(m);
+                off = a - (int32_t)r.cold(s).toff;
+            }
+        }
+        if (s >= 0) {
+            res[0] = 1;
+            res[1] = r.recon_pos(s, b) + off;
+        }
+    } else { /* modes 2 and 5: the marker whose property a (the marker-id key) is value b; res[0] = 2 if several */
         int32_t s = r.marker_by_id(a, b);
         if (s == -2) {
             res[0] = 2;
+        } else if (s >= 0 && mode == 5) {
+            seg_fields(r, s, 0, res);
         } else if (s >= 0) {
             res[0] = 1;
             res[1] = r.position_of(s, ref_seq, sh);
         }
     }
     if (threadIdx.x == 0)
-        for (int i = 0; i < 7; i++) out[i] = res[i];
+        for (int i = 0; i < MT_SEGQ_N; i++) out[i] = res[i];
+}
+
+/* every segment's handle in walkAllSegments order (the canonical dump's record order): out[2i] = row id,
+ * out[2i+1] = its generation; *n = the segment count (writes at most cap pairs) */
+template <class HT>
+__global__ __launch_bounds__(WG) void k_segids(Store<HT> st, int64_t doc, int32_t* out, int64_t cap, int64_t* n) {
+    Replica<WaveGPU, HT> r(st.doc(doc), WaveGPU());
+    int64_t base = 0;
+    for (int32_t k = 0; r.kvalid(k); k = r.knext(k)) {
+        int32_t lf = r.leaf_at(k), c = r.nch[lf];
+        int32_t j = threadIdx.x;
+        if (j < c && j < MAXN && base + j < cap) {
+            int32_t rid = r.z.rid[lf * MAXN + j];
+            out[2 * (base + j)] = rid;
+            out[2 * (base + j) + 1] = r.z.rgen[rid];
+        }
+        base += c;
+    }
+    if (threadIdx.x == 0) *n = base;
 }
 
 /* local references: per doc their count and LocalReference.toPosition() of each (-1 detached) */
@@ -553,6 +622,7 @@ struct ProfOps {
     int32_t (*seg)(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,
                    int32_t long_client, int32_t floor, int32_t* dout);
     int32_t (*refpos)(mt_engine* e, int32_t* dn, int32_t* dpos);
+    int32_t (*segids)(mt_engine* e, int64_t doc, int32_t* dout, int64_t cap, int64_t* dn);
 };
 /* each profile's table (host functions, defined in its mt_prof_*.hip) */
 const ProfOps* ops_small();
@@ -634,7 +704,11 @@ struct Launch {
                            e->rcap, dn, dpos);
         return launch_check(e, "k_refpos");
     }
+    static int32_t segids(mt_engine* e, int64_t doc, int32_t* dout, int64_t cap, int64_t* dn) {
+        hipLaunchKernelGGL((k_segids<HT>), dim3(1), dim3(WG), 0, e->stream, store_of<HT>(e), doc, dout, cap, dn);
+        return launch_check(e, "k_segids");
+    }
     static ProfOps table(int32_t (*replay)(mt_engine*)) {
-        return ProfOps{init, start_collab, replay, hdr, digest, dump, length, text, seg, refpos};
+        return ProfOps{init, start_collab, replay, hdr, digest, dump, length, text, seg, refpos, segids};
     }
 };

@@ -568,8 +568,19 @@ int64_t mt_engine_get_text_range(mt_engine* e, int64_t doc, int32_t ref_seq, int
     return n;
 }
 
+static void seg_ref_of(const int32_t* r, mt_seg_ref* out) {
+    out->rid = r[0] == 1 ? r[1] : -1;
+    out->gen = r[2];
+    out->offset = r[3];
+    out->length = r[4];
+    out->seq = r[5];
+    out->client = r[6];
+    out->removed_seq = r[7];
+    out->removed_client = r[8];
+    out->ordinal = r[9];
+}
 static int32_t seg_query(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int32_t b, int32_t ref_seq,
-                         int32_t long_client, int32_t* res7) {
+                         int32_t long_client, int32_t* res7) { /* res7: MT_SEGQ_N words (mt_kernels.h k_seg) */
     if (!e || doc < 0 || doc >= e->ndocs) return MT_E_ARG;
     int32_t floor = persp_floor(e, doc, long_client);
     e = route(e, &doc);
@@ -578,7 +589,7 @@ static int32_t seg_query(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int
     if (rc) return rc;
     rc = e->ops->seg(e, doc, mode, a, b, ref_seq, long_client, floor, (int32_t*)e->tmp.p);
     if (rc) return rc;
-    HIPCHK(e, hipMemcpyAsync(res7, e->tmp.p, 7 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(res7, e->tmp.p, MT_SEGQ_N * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (res7[0] == 3) return MT_E_UNSUPPORTED; /* a perspective the reference's partial lengths answer differently */
     return MT_OK;
@@ -587,22 +598,17 @@ static int32_t seg_query(mt_engine* e, int64_t doc, int32_t mode, int32_t a, int
 int32_t mt_engine_get_containing_segment(mt_engine* e, int64_t doc, int32_t pos, int32_t ref_seq, int32_t long_client,
                                          mt_seg_ref* out) {
     if (!out) return MT_E_ARG;
-    int32_t r[7];
+    int32_t r[MT_SEGQ_N];
     int32_t rc = seg_query(e, doc, 0, pos, 0, ref_seq, long_client, r);
     if (rc) return rc;
-    out->rid = r[0] ? r[1] : -1;
-    out->gen = r[2];
-    out->offset = r[3];
-    out->length = r[4];
-    out->seq = r[5];
-    out->client = r[6];
+    seg_ref_of(r, out);
     return MT_OK;
 }
 
 int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t gen, int32_t ref_seq,
                                int32_t long_client, int32_t* out) {
     if (!out) return MT_E_ARG;
-    int32_t r[7];
+    int32_t r[MT_SEGQ_N];
     int32_t rc = seg_query(e, doc, 1, rid, gen, ref_seq, long_client, r);
     if (rc) return rc;
     if (!r[0]) return MT_E_ARG;
@@ -614,7 +620,7 @@ int32_t mt_engine_pos_from_relative_pos(mt_engine* e, int64_t doc, int32_t id_ke
                                         int32_t has_offset, int32_t offset, int32_t ref_seq, int32_t long_client,
                                         int32_t* out) {
     if (!out) return MT_E_ARG;
-    int32_t r[7];
+    int32_t r[MT_SEGQ_N];
     int32_t rc = seg_query(e, doc, 2, id_key, id_value, ref_seq, long_client, r);
     if (rc) return rc;
     if (r[0] == 2) return MT_E_UNSUPPORTED; /* several markers hold the id */
@@ -626,6 +632,66 @@ int32_t mt_engine_pos_from_relative_pos(mt_engine* e, int64_t doc, int32_t id_ke
     }
     *out = pos;
     return MT_OK;
+}
+
+int32_t mt_engine_resolve_remote_client_position(mt_engine* e, int64_t doc, int32_t pos, int32_t ref_seq,
+                                                 int32_t long_client, int32_t* out) {
+    if (!out) return MT_E_ARG;
+    int32_t r[MT_SEGQ_N];
+    int32_t rc = seg_query(e, doc, 4, pos, 0, ref_seq, long_client, r);
+    if (rc) return rc;
+    *out = r[0] == 1 ? r[1] : (pos == r[3] ? r[4] : -1);
+    return MT_OK;
+}
+
+int32_t mt_engine_adjust_position(mt_engine* e, int64_t doc, int32_t pos, int32_t from_seq, int32_t long_client,
+                                  int32_t* out) {
+    if (!out) return MT_E_ARG;
+    int32_t r[MT_SEGQ_N];
+    int32_t rc = seg_query(e, doc, 4, pos, 0, from_seq, long_client, r);
+    if (rc) return rc;
+    *out = r[0] == 1 && !r[2] ? r[1] : -1;
+    return MT_OK;
+}
+
+int32_t mt_engine_handle_to_position(mt_engine* e, int64_t doc, int32_t handle, int32_t local_seq, int32_t* out) {
+    if (!out) return MT_E_ARG;
+    int32_t r[MT_SEGQ_N];
+    int32_t rc = seg_query(e, doc, 6, handle, local_seq, 0, -1, r);
+    if (rc) return rc;
+    if (r[0] != 1) return MT_E_ARG; /* assert(isHandleValid(containingSegment.start)) */
+    *out = r[1];
+    return MT_OK;
+}
+
+int32_t mt_engine_get_marker_from_id(mt_engine* e, int64_t doc, int32_t id_key, int32_t id_value, mt_seg_ref* out) {
+    if (!out) return MT_E_ARG;
+    int32_t r[MT_SEGQ_N];
+    int32_t rc = seg_query(e, doc, 5, id_key, id_value, 0, -1, r);
+    if (rc) return rc;
+    if (r[0] == 2) return MT_E_UNSUPPORTED; /* several markers hold the id, or an annotate changed it */
+    seg_ref_of(r, out);
+    return MT_OK;
+}
+
+int64_t mt_engine_segment_ids(mt_engine* e, int64_t doc, int32_t* out, int64_t cap) {
+    if (!e || doc < 0 || doc >= e->ndocs || cap < 0) return -MT_E_ARG;
+    e = route(e, &doc);
+    if (hipSetDevice(e->device) != hipSuccess) return -MT_E_HIP;
+    if (ensure(e, e->tmp, 16 + 8 * (size_t)(out ? cap : 0) + 16)) return -MT_E_HIP;
+    int64_t* dn = (int64_t*)e->tmp.p;
+    int32_t* dbuf = (int32_t*)((uint8_t*)e->tmp.p + 16);
+    int32_t rc = e->ops->segids(e, doc, dbuf, out ? cap : 0, dn);
+    if (rc) return -rc;
+    int64_t n = 0;
+    if (hipMemcpyAsync(&n, dn, sizeof(int64_t), hipMemcpyDeviceToHost, e->stream) != hipSuccess) return -MT_E_HIP;
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
+    int64_t m = n < cap ? n : cap;
+    if (out && m > 0) {
+        if (hipMemcpyAsync(out, dbuf, 8 * (size_t)m, hipMemcpyDeviceToHost, e->stream) != hipSuccess) return -MT_E_HIP;
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
+    }
+    return n;
 }
 
 /* the delta region of every document: offset inside a document's block, and the block stride */
@@ -718,7 +784,7 @@ int64_t mt_engine_handle_table(mt_engine* e, int64_t doc, int32_t* out, int64_t 
 
 int32_t mt_engine_get_handle(mt_engine* e, int64_t doc, int32_t pos, int32_t* out) {
     if (!out) return MT_E_ARG;
-    int32_t r[7];
+    int32_t r[MT_SEGQ_N];
     int32_t rc = seg_query(e, doc, 3, pos, 0, 0, -1, r);
     if (rc) return rc;
     if (!r[0]) return MT_E_ARG; /* RangeError: no segment at pos (ensureRange) */

@@ -32,7 +32,8 @@ class EngineError(RuntimeError):
 
 class SegRef(ctypes.Structure):
     """mt_seg_ref: a segment handle (row id + generation) and where the position falls in it."""
-    _fields_ = [(n, ctypes.c_int32) for n in ("rid", "gen", "offset", "length", "seq", "client")]
+    _fields_ = [(n, ctypes.c_int32) for n in ("rid", "gen", "offset", "length", "seq", "client", "removed_seq",
+                                                "removed_client", "ordinal")]
 
 
 class _Caps(ctypes.Structure):
@@ -87,6 +88,12 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_ref_positions.argtypes = [vp, vp, vp]
         L.mt_engine_deltas.argtypes = [vp, i64, vp, i64]
         L.mt_engine_deltas.restype = i64
+        L.mt_engine_resolve_remote_client_position.argtypes = [vp, i64, i32, i32, i32, ctypes.POINTER(i32)]
+        L.mt_engine_adjust_position.argtypes = [vp, i64, i32, i32, i32, ctypes.POINTER(i32)]
+        L.mt_engine_handle_to_position.argtypes = [vp, i64, i32, i32, ctypes.POINTER(i32)]
+        L.mt_engine_get_marker_from_id.argtypes = [vp, i64, i32, i32, ctypes.POINTER(SegRef)]
+        L.mt_engine_segment_ids.argtypes = [vp, i64, vp, i64]
+        L.mt_engine_segment_ids.restype = i64
         L.mt_engine_ndocs.argtypes = [vp]
         L.mt_engine_ndocs.restype = i64
         _LIB = L
@@ -256,6 +263,45 @@ class Engine:
         self._check(self.L.mt_engine_get_position(self.h, doc, seg.rid, seg.gen, ref_seq, long_client, ctypes.byref(v)),
                     "get_position")
         return v.value
+
+    def resolve_remote_client_position(self, doc: int, pos: int, ref_seq: int, long_client: int) -> Optional[int]:
+        """MergeTree.resolveRemoteClientPosition (mergeTree.ts:2140-2160); None = undefined."""
+        v = ctypes.c_int32()
+        self._check(self.L.mt_engine_resolve_remote_client_position(self.h, doc, pos, ref_seq, long_client,
+                                                                    ctypes.byref(v)), "resolve_remote_client_position")
+        return None if v.value < 0 else v.value
+
+    def adjust_position(self, doc: int, pos: int, from_seq: int, long_client: int) -> Optional[int]:
+        """PermutationVector.adjustPosition (permutationvector.ts:185-196); None = undefined."""
+        v = ctypes.c_int32()
+        self._check(self.L.mt_engine_adjust_position(self.h, doc, pos, from_seq, long_client, ctypes.byref(v)),
+                    "adjust_position")
+        return None if v.value < 0 else v.value
+
+    def handle_to_position(self, doc: int, handle: int, local_seq: int) -> int:
+        """PermutationVector.handleToPosition (permutationvector.ts:198-253)."""
+        v = ctypes.c_int32()
+        self._check(self.L.mt_engine_handle_to_position(self.h, doc, handle, local_seq, ctypes.byref(v)),
+                    "handle_to_position")
+        return v.value
+
+    def get_marker_from_id(self, doc: int, key_id: int, value_id: int) -> Optional[SegRef]:
+        """MergeTree.getMarkerFromId (mergeTree.ts:1965-1967); None if no marker holds the id."""
+        r = SegRef()
+        self._check(self.L.mt_engine_get_marker_from_id(self.h, doc, key_id, value_id, ctypes.byref(r)),
+                    "get_marker_from_id")
+        return None if r.rid < 0 else r
+
+    def segment_ids(self, doc: int) -> np.ndarray:
+        """(nsegs, 2) int32: every segment's (rid, gen) in walkAllSegments (canonical dump) order."""
+        n = self.L.mt_engine_segment_ids(self.h, doc, None, 0)
+        if n < 0:
+            raise EngineError(f"segment_ids failed {n}", -n)
+        out = np.zeros((max(n, 1), 2), np.int32)
+        m = self.L.mt_engine_segment_ids(self.h, doc, _p(out), n)
+        if m != n:
+            raise EngineError("segment count changed")
+        return out[:n]
 
     def promoted(self) -> np.ndarray:
         """The documents the last sync re-replayed in a larger profile (capacity promotion)."""

@@ -54,7 +54,29 @@ export interface SequencedMessage {
 }
 
 /** a segment handle (mt_seg_ref): the row's stable id and generation, where the position falls in it */
-export interface SegmentHandle { rid: number; gen: number; offset: number; length: number; seq: number; client: number }
+export interface SegmentHandle {
+    rid: number; gen: number; offset: number; length: number; seq: number; client: number;
+    /** undefined when not removed; -1 = a pending local remove */
+    removedSeq: number | undefined; removedClient: number;
+    /** the segment's index in walkAllSegments order (its record in the canonical dump) */
+    ordinal: number;
+}
+
+/** a segment as the reference's ISegment reads (decodeDump / GpuClient.segments()), with its handle and local position */
+export interface SegmentObject {
+    type: "TextSegment" | "Marker" | "PermutationSegment";
+    cachedLength: number; seq: number; clientId: string | -1;
+    removedSeq?: number; removedClientId?: string | -1; localSeq?: number; localRemovedSeq?: number;
+    properties?: PropertySet; text?: string; refType?: number; start?: number;
+    leaf: number; ordinal: number; rid?: number; gen?: number;
+    /** position and localNetLength in the local view when read */
+    pos?: number; len?: number;
+}
+
+export interface DecodedDump {
+    currentSeq: number; minSeq: number; localSeq: number; length: number; nleaf: number; localLength?: number;
+    segments: SegmentObject[];
+}
 
 export interface LocalReferenceHandle { doc: number; index: number }
 
@@ -71,6 +93,9 @@ export declare class Interner {
 }
 
 export declare function decodeDeltas(words: Int32Array, interner: Interner): DeltaEvent[];
+
+/** the canonical segment dump (include/mt_oplog.h) as segment objects; nameOf maps long client indices to ids */
+export declare function decodeDump(bytes: Uint8Array, interner: Interner, nameOf: (i: number) => string | -1): DecodedDump;
 
 /** A batch of documents resident in one GPU's HBM; queued events apply at the next read (one launch per read). */
 export declare class ReplayEngine {
@@ -141,6 +166,31 @@ export declare class GpuClient {
     getContainingSegment(pos: number): { segment: SegmentHandle | undefined; offset: number | undefined };
     getPosition(segment: SegmentHandle): number;
     deltaEvents(): DeltaEvent[];
+    /** every segment in walkAllSegments order, with its handle and local-view position */
+    segments(): DecodedDump;
+    /** Client.walkSegments (client.ts:276-285); splitRange needs caps.dcap, rcap or pcap > 0 */
+    walkSegments<T>(handler: (segment: SegmentObject, pos: number, refSeq: number, clientId: string | undefined,
+        start: number, end: number, accum?: T) => boolean, start?: number, end?: number, accum?: T, splitRange?: boolean): void;
+    /** Client.getPropertiesAtPosition (client.ts:1011-1025) */
+    getPropertiesAtPosition(pos: number): PropertySet | undefined;
+    /** Client.getRangeExtentsOfPosition (client.ts:1026-1044) */
+    getRangeExtentsOfPosition(pos: number): { posStart: number | undefined; posAfterEnd: number | undefined };
+    /** MergeTree.resolveRemoteClientPosition (mergeTree.ts:2140-2160); throws "unsupported" where mt_engine.h says */
+    resolveRemoteClientPosition(remoteClientPosition: number, remoteClientRefSeq: number, remoteLongClientId: string): number | undefined;
+    /** Client.localTransaction (client.ts:961-981): every member a local op */
+    localTransaction(groupOp: { type: 3; ops: MergeTreeOp[] }): void;
+    /** Client.insertSegmentLocal for a segment spec (string, {text, props}, {marker, props}, [length, start]) */
+    insertSegmentLocal(pos: number, spec: SegmentSpec | [number, number]): MergeTreeOp | undefined;
+    /** Client.findTile (client.ts:1075-1078): the nearest Tile marker with the label, preceding startPos or after it */
+    findTile(startPos: number | undefined, tileLabel: string, preceding?: boolean): { tile: SegmentObject; pos: number } | undefined;
+    /** Client.getMarkerFromId (client.ts:312) */
+    getMarkerFromId(id: string): SegmentObject | undefined;
+    /** Client.annotateMarker (client.ts:143-154): the op with relative positions, or undefined */
+    annotateMarker(marker: SegmentObject, props: PropertySet, combiningOp?: ICombiningOp): MergeTreeOp | undefined;
+    /** PermutationVector.adjustPosition (permutationvector.ts:185-196) */
+    adjustPosition(pos: number, fromSeq: number, longClientId: string): number | undefined;
+    /** PermutationVector.handleToPosition (permutationvector.ts:198-253); localSeq defaults to the last local op's */
+    handleToPosition(handle: number, localSeq?: number): number;
 }
 
 /** the Node-API addon itself (mt_napi.node) */

@@ -29,7 +29,10 @@ const OPF_TREE = 0x20; // a MergeTree-level call with explicit (refSeq, clientId
 const CLIENT_LOCAL = 0xfffe; // LocalClientId in a MergeTree-level record
 const LocalClientId = -1; // constants.ts
 const UnassignedSequenceNumber = -1;
-const ReferenceType = { Simple: 0x0, SlideOnRemove: 0x40 }; // ops.ts
+const ReferenceType = { Simple: 0x0, Tile: 0x1, NestBegin: 0x2, NestEnd: 0x4, SlideOnRemove: 0x40 }; // ops.ts:6-15
+const NOOP_SPLIT = 1; // seg_kind of a local NOOP record: walkSegments' splitRange (mt_oplog.h MT_NOOP_SPLIT)
+const TILE_LABELS_KEY = "referenceTileLabels"; // reservedTileLabelsKey (mergeTree.ts:615)
+const HANDLE_UNALLOCATED = -0x80000000; // Handle.unallocated (matrix handletable.ts:11)
 const SEG = { TEXT: 0, MARKER: 1, PERM: 2 };
 const SEG_RELPOS = 0x80; // positions relative to markers (mt_oplog.h MT_SEG_RELPOS)
 const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
@@ -112,6 +115,65 @@ function decodeDeltas(words, interner) {
         events.push({ operation: DELTA_OPS[op], seq, deltaSegments });
     }
     return events;
+}
+
+/* The canonical segment dump (include/mt_oplog.h) as the reference's segment objects: per segment its type,
+ * cachedLength, seq / clientId (long client names; LocalClientId = -1), removedSeq / removedClientId
+ * (undefined when not removed), localSeq / localRemovedSeq, properties, text / refType / start, the leaf block
+ * ordinal and its index (ordinal) in walkAllSegments order. */
+function decodeDump(bytes, interner, nameOf) {
+    const dv = new DataView(bytes.buffer, bytes.byteOffset, bytes.byteLength);
+    const keyName = new Map([...interner.keys].map(([k, i]) => [i, k]));
+    const valueOf = new Map([...interner.values].map(([v, i]) => [i, JSON.parse(v)]));
+    const hdr = [0, 1, 2, 3, 4, 5].map((k) => dv.getInt32(4 * k, true));
+    let o = 24;
+    const segments = [];
+    for (let i = 0; i < hdr[4]; i++) {
+        const kind = dv.getUint8(o), flags = dv.getUint8(o + 1), nov = dv.getUint8(o + 2);
+        o += 4;
+        const f = [0, 1, 2, 3, 4, 5, 6, 7].map((k) => dv.getInt32(o + 4 * k, true));
+        o += 32 + 4 * nov;
+        const np = dv.getUint16(o, true), refType = dv.getUint16(o + 2, true);
+        o += 4;
+        let properties;
+        if (flags & 1) {
+            properties = {};
+            for (let k = 0; k < np; k++) {
+                const v = dv.getUint16(o + 4 * k + 2, true) & ~VALUE_FALSY;
+                properties[keyName.get(dv.getUint16(o + 4 * k, true))] = v === 0 ? null : valueOf.get(v);
+            }
+        }
+        o += 4 * np;
+        let start = HANDLE_UNALLOCATED;
+        if (flags & 16) { start = dv.getInt32(o, true); o += 4; }
+        const seg = {
+            type: kind === SEG.TEXT ? "TextSegment" : kind === SEG.MARKER ? "Marker" : "PermutationSegment",
+            cachedLength: f[0], seq: f[1], clientId: nameOf(f[2]),
+            removedSeq: flags & 2 ? f[3] : undefined, removedClientId: flags & 2 ? nameOf(f[4]) : undefined,
+            localSeq: flags & 4 ? f[5] : undefined, localRemovedSeq: flags & 8 ? f[6] : undefined,
+            properties, leaf: f[7], ordinal: i,
+        };
+        if (kind === SEG.TEXT) {
+            let t = "";
+            for (let j = 0; j < f[0]; j++) t += String.fromCharCode(dv.getUint16(o + 2 * j, true));
+            o += 2 * f[0];
+            seg.text = t;
+        } else if (kind === SEG.MARKER) {
+            seg.refType = refType;
+        } else {
+            seg.start = start;
+        }
+        segments.push(seg);
+    }
+    return { currentSeq: hdr[0], minSeq: hdr[1], localSeq: hdr[2], length: hdr[3], nleaf: hdr[5], segments };
+}
+
+/* a marker's tile labels as Marker.hasTileLabel reads them (mergeTree.ts:620-635: Tile refType and the
+ * referenceTileLabels property) */
+function hasTileLabel(seg, label) {
+    if (seg.type !== "Marker" || !(seg.refType & ReferenceType.Tile) || !seg.properties) return false;
+    const labels = seg.properties[TILE_LABELS_KEY];
+    return Array.isArray(labels) && labels.includes(label);
 }
 
 class DocQueue {
@@ -469,10 +531,167 @@ class GpuClient {
     /* Client.getPosition (client.ts:291) of a handle from getContainingSegment */
     getPosition(segment) { return addon.getPosition(this.read(), this.doc, segment.rid, segment.gen, 0, -1); }
 
+    /* The replica's segments in walkAllSegments order (decodeDump), each with its handle (rid, gen: getPosition
+     * and getContainingSegment's handles) and its position in the local view (pos; localNetLength in len) */
+    segments() {
+        const h = this.read();
+        const names = [...this.engine.clientIds.keys()];
+        const d = decodeDump(addon.dump(h, this.doc), this.engine.interner, (i) => (i < 0 ? LocalClientId : names[i]));
+        const ids = addon.segmentIds(h, this.doc);
+        let pos = 0;
+        d.segments.forEach((seg, i) => {
+            seg.rid = ids[2 * i];
+            seg.gen = ids[2 * i + 1];
+            seg.pos = pos;
+            seg.len = seg.removedSeq !== undefined ? 0 : seg.cachedLength; // localNetLength
+            pos += seg.len;
+        });
+        d.localLength = pos;
+        return d;
+    }
+
+    /* Client.walkSegments(handler, start, end, accum, splitRange) (client.ts:276-285 -> MergeTree.mapRange /
+     * nodeMap, mergeTree.ts:2830-2998): handler(segment, pos, refSeq, clientId, start, end, accum) for every
+     * segment of the local view with a length, inside [start, end), in order, start / end relative to the
+     * segment; a falsy return stops the walk. splitRange first splits the segments at start and end (a local
+     * record; engines with caps.dcap, rcap or pcap > 0). Segments are the objects segments() returns. */
+    walkSegments(handler, start, end, accum, splitRange = false) {
+        if (splitRange) this.engine.enqueue(this.doc, OP.NOOP | OPF_LOCAL, { seg_kind: NOOP_SPLIT, pos1: start || 0, pos2: end || 0 });
+        const d = this.segments();
+        let a = start === undefined ? 0 : start, b = end === undefined ? d.localLength : end;
+        for (const seg of d.segments) {
+            if (b > 0 && seg.len > 0 && a < seg.len) {
+                if (!handler(seg, seg.pos, d.currentSeq, this.longClientId, a, b, accum)) break;
+            }
+            a -= seg.len;
+            b -= seg.len;
+        }
+    }
+
+    /* Client.getPropertiesAtPosition (client.ts:1011-1025): the properties of the segment at pos (local view) */
+    getPropertiesAtPosition(pos) {
+        const r = addon.getContainingSegment(this.read(), this.doc, pos, 0, -1);
+        if (r === undefined) return undefined;
+        return this.segments().segments[r.ordinal].properties;
+    }
+
+    /* Client.getRangeExtentsOfPosition (client.ts:1026-1044): {posStart, posAfterEnd} of the segment at pos */
+    getRangeExtentsOfPosition(pos) {
+        const { segment } = this.getContainingSegment(pos);
+        if (segment === undefined) return { posStart: undefined, posAfterEnd: undefined };
+        const posStart = this.getPosition(segment);
+        return { posStart, posAfterEnd: posStart + segment.length };
+    }
+
+    /* MergeTree.resolveRemoteClientPosition (mergeTree.ts:2140-2160; SharedSegmentSequence.resolveRemoteClientPosition,
+     * sequence.ts:314): where a remote client's position (under its refSeq) is in the local view; undefined if
+     * nothing there. A perspective the engine does not answer (mt_engine.h) throws "unsupported". */
+    resolveRemoteClientPosition(remoteClientPosition, remoteClientRefSeq, remoteLongClientId) {
+        return addon.resolveRemoteClientPosition(this.read(), this.doc, remoteClientPosition, remoteClientRefSeq,
+            this.engine.longIndex(remoteLongClientId));
+    }
+
+    /* Client.localTransaction(groupOp) (client.ts:961-981): every member applied as a local op */
+    localTransaction(groupOp) {
+        for (const op of groupOp.ops) {
+            if (op.pos1 === undefined || (op.type !== OP.INSERT && op.pos2 === undefined)) {
+                throw new Error("localTransaction: relative positions are not modelled for local ops");
+            }
+            if (op.type === OP.INSERT) this.insertSegmentLocal(op.pos1, op.seg);
+            else if (op.type === OP.REMOVE) this.removeRangeLocal(op.pos1, op.pos2);
+            else if (op.type === OP.ANNOTATE) this.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp);
+        }
+    }
+
+    /* Client.insertSegmentLocal(pos, segment) (client.ts:202-211) for a segment spec: a string, {text, props},
+     * {marker: {refType}, props} or a PermutationSegment [length, start] */
+    insertSegmentLocal(pos, spec) {
+        if (typeof spec === "string" || (spec && typeof spec.text === "string")) {
+            const text = typeof spec === "string" ? spec : spec.text;
+            return this.insertTextLocal(pos, text, typeof spec === "string" ? undefined : spec.props);
+        }
+        if (spec && spec.marker) return this.insertMarkerLocal(pos, spec.marker.refType, spec.props);
+        if (Array.isArray(spec)) {
+            this.engine.enqueue(this.doc, OP.INSERT | OPF_LOCAL, { pos1: pos }, spec);
+            this.sent(OP.INSERT);
+            return { type: OP.INSERT, pos1: pos, seg: spec };
+        }
+        throw new Error("insertSegmentLocal: unsupported segment spec");
+    }
+
+    /* Client.findTile(startPos, tileLabel, preceding) (client.ts:1075-1078 -> MergeTree.findTile, mergeTree.ts:
+     * 1796-1822, search / backwardSearch with recordTileStart / tileShift, 1030-1069): the nearest marker with
+     * the Tile refType and the label in its referenceTileLabels, at or before startPos (preceding) or at or after
+     * it, in the local view; {tile, pos} or undefined. Blocks contribute their rightmost / leftmost tiles from
+     * markers of non-zero local length (addNodeReferences 262-300), the segment the search stops at counts as it
+     * is (backwardSearch from the document's end stops at its last segment, whatever its length). */
+    findTile(startPos, tileLabel, preceding = true) {
+        const d = this.segments();
+        const segs = d.segments;
+        const ok = (seg) => seg.len > 0 && hasTileLabel(seg, tileLabel);
+        let stop = -1; // the segment the search reaches
+        let tile;
+        if (preceding) {
+            if (startPos !== undefined) stop = segs.findIndex((seg) => seg.len > 0 && seg.pos <= startPos && startPos < seg.pos + seg.len);
+            const shifted = stop < 0 ? segs.length : stop;
+            for (let i = 0; i < shifted; i++) if (ok(segs[i])) tile = segs[i];
+        } else {
+            if (startPos !== undefined && startPos > d.localLength) return undefined;
+            if (startPos !== undefined) {
+                for (let i = segs.length - 1; i >= 0; i--) {
+                    if (startPos >= segs[i].pos) { stop = i; break; } // segpos = segEnd - len <= pos
+                }
+            }
+            for (let i = segs.length - 1; i > stop; i--) if (ok(segs[i])) tile = segs[i];
+        }
+        if (stop >= 0 && hasTileLabel(segs[stop], tileLabel)) tile = segs[stop];
+        return tile === undefined ? undefined : { tile, pos: tile.pos };
+    }
+
+    /* Client.getMarkerFromId (client.ts:312-314; mergeTree.ts:1965-1967): the marker whose markerId is id, as a
+     * segments() object; undefined if none. An id an annotate changed on a marker, or one several markers
+     * hold, throws "unsupported" (mt_engine_get_marker_from_id). */
+    getMarkerFromId(id) {
+        const e = this.engine;
+        const r = addon.getMarkerFromId(this.read(), this.doc, e.interner.key(MARKER_ID_KEY), e.interner.value(id) & 0xffff);
+        return r === undefined ? undefined : this.segments().segments[r.ordinal];
+    }
+
+    /* Client.annotateMarker(marker, props, combiningOp) (client.ts:143-154; createAnnotateMarkerOp opBuilder.ts:
+     * 25-38): annotates [pos, pos + 1) of the marker its markerId names, as the op's relative positions resolve
+     * (getValidOpRange, client.ts:486-548); returns the op, or undefined (no id, or an invalid range) */
+    annotateMarker(marker, props, combiningOp) {
+        const id = marker && marker.properties ? marker.properties[MARKER_ID_KEY] : undefined;
+        if (!id) return undefined;
+        const m = this.getMarkerFromId(id);
+        if (m === undefined) return undefined;
+        const len = this.getLength();
+        if (!(m.pos >= 0 && m.pos < len && m.pos + m.cachedLength <= len)) return undefined;
+        const op = { combiningOp, props, relativePos1: { id, before: true }, relativePos2: { id }, type: OP.ANNOTATE };
+        this.engine.enqueue(this.doc, OP.ANNOTATE | OPF_LOCAL, { pos1: m.pos, pos2: m.pos + m.cachedLength },
+            { props, combiningOp });
+        this.sent(OP.ANNOTATE);
+        return op;
+    }
+
+    /* PermutationVector.adjustPosition(pos, fromSeq, clientId) (permutationvector.ts:185-196): a remote
+     * client's row / col position in the local view, undefined when its segment is gone or removed */
+    adjustPosition(pos, fromSeq, longClientId) {
+        return addon.adjustPosition(this.read(), this.doc, pos, fromSeq, this.engine.longIndex(longClientId));
+    }
+
+    /* PermutationVector.handleToPosition(handle, localSeq) (permutationvector.ts:198-253): the position of a
+     * handle for an op resubmitted at localSeq (default: the last local op's) */
+    handleToPosition(handle, localSeq) {
+        const h = this.read();
+        if (localSeq === undefined) localSeq = this.segments().localSeq;
+        return addon.handleToPosition(h, this.doc, handle, localSeq);
+    }
+
     /* Every "sequenceDelta" / "maintenance" event this replica has fired since the engine was created
      * (engines created with caps.dcap > 0), decoded (decodeDeltas) */
     deltaEvents() { return decodeDeltas(addon.deltas(this.read(), this.doc), this.engine.interner); }
 }
 
-module.exports = { ReplayEngine, GpuClient, GpuMergeTree, Interner, addon, OP, DEFAULT_CAPS, decodeDeltas, ReferenceType,
-    LocalClientId, UnassignedSequenceNumber };
+module.exports = { ReplayEngine, GpuClient, GpuMergeTree, Interner, addon, OP, DEFAULT_CAPS, decodeDeltas, decodeDump,
+    ReferenceType, LocalClientId, UnassignedSequenceNumber };

@@ -354,7 +354,28 @@ static napi_value js_get_text(napi_env env, napi_callback_info info) {
     return s;
 }
 
-/* getContainingSegment(h, doc, pos, refSeq, longClient) -> {rid, gen, offset, length, seq, client} | undefined */
+/* an mt_seg_ref as {rid, gen, offset, length, seq, client, removedSeq, removedClient, ordinal}; undefined for none
+ * (removedSeq: undefined when not removed, as the reference's ISegment.removedSeq) */
+static napi_value seg_ref_value(napi_env env, const mt_seg_ref& r) {
+    napi_value out;
+    if (r.rid < 0) {
+        NAPI_OK(napi_get_undefined(env, &out));
+        return out;
+    }
+    NAPI_OK(napi_create_object(env, &out));
+    const char* names[8] = {"rid", "gen", "offset", "length", "seq", "client", "removedClient", "ordinal"};
+    int32_t vals[8] = {r.rid, r.gen, r.offset, r.length, r.seq, r.client, r.removed_client, r.ordinal};
+    for (int i = 0; i < 8; i++) NAPI_OK(napi_set_named_property(env, out, names[i], num(env, vals[i])));
+    napi_value rs;
+    if (r.removed_seq == MT_NOT_REMOVED)
+        NAPI_OK(napi_get_undefined(env, &rs));
+    else
+        rs = num(env, r.removed_seq);
+    NAPI_OK(napi_set_named_property(env, out, "removedSeq", rs));
+    return out;
+}
+
+/* getContainingSegment(h, doc, pos, refSeq, longClient) -> {rid, gen, offset, length, seq, client, ...} | undefined */
 static napi_value js_get_containing(napi_env env, napi_callback_info info) {
     napi_value argv[5];
     if (!get_args(env, info, 5, argv)) return nullptr;
@@ -372,11 +393,7 @@ static napi_value js_get_containing(napi_env env, napi_callback_info info) {
         NAPI_OK(napi_get_undefined(env, &out));
         return out;
     }
-    NAPI_OK(napi_create_object(env, &out));
-    const char* names[6] = {"rid", "gen", "offset", "length", "seq", "client"};
-    int32_t vals[6] = {r.rid, r.gen, r.offset, r.length, r.seq, r.client};
-    for (int i = 0; i < 6; i++) NAPI_OK(napi_set_named_property(env, out, names[i], num(env, vals[i])));
-    return out;
+    return seg_ref_value(env, r);
 }
 
 /* getPosition(h, doc, rid, gen, refSeq, longClient) -> number */
@@ -440,6 +457,93 @@ static napi_value js_pos_from_relpos(napi_env env, napi_callback_info info) {
     return num(env, out);
 }
 
+/* resolveRemoteClientPosition(h, doc, pos, refSeq, longClient) / adjustPosition(h, doc, pos, fromSeq,
+ * longClient) -> number | undefined */
+static napi_value remote_pos(napi_env env, napi_callback_info info, bool adjust) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t pos, ref, cl, out = -1;
+    if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &pos) || !i32_of(env, argv[3], &ref) ||
+        !i32_of(env, argv[4], &cl))
+        return nullptr;
+    int32_t rc = adjust ? mt_engine_adjust_position(e, doc, pos, ref, cl, &out)
+                        : mt_engine_resolve_remote_client_position(e, doc, pos, ref, cl, &out);
+    if (rc) return throw_status(env, e, rc, adjust ? "mt_engine_adjust_position" : "mt_engine_resolve_remote_client_position");
+    napi_value v;
+    if (out < 0)
+        NAPI_OK(napi_get_undefined(env, &v));
+    else
+        v = num(env, out);
+    return v;
+}
+static napi_value js_resolve_remote(napi_env env, napi_callback_info info) { return remote_pos(env, info, false); }
+static napi_value js_adjust_position(napi_env env, napi_callback_info info) { return remote_pos(env, info, true); }
+
+/* handleToPosition(h, doc, handle, localSeq) -> number */
+static napi_value js_handle_to_position(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t hnd, ls, out = 0;
+    if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &hnd) || !i32_of(env, argv[3], &ls)) return nullptr;
+    int32_t rc = mt_engine_handle_to_position(e, doc, hnd, ls, &out);
+    if (rc) return throw_status(env, e, rc, "mt_engine_handle_to_position");
+    return num(env, out);
+}
+
+/* getMarkerFromId(h, doc, keyId, valueId) -> segment handle | undefined */
+static napi_value js_marker_from_id(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t k, v;
+    if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &k) || !i32_of(env, argv[3], &v)) return nullptr;
+    mt_seg_ref r;
+    int32_t rc = mt_engine_get_marker_from_id(e, doc, k, v, &r);
+    if (rc) return throw_status(env, e, rc, "mt_engine_get_marker_from_id");
+    return seg_ref_value(env, r);
+}
+
+/* dump(h, doc) -> Uint8Array: the canonical segment dump (include/mt_oplog.h) */
+static napi_value js_dump(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    if (!e || !i64_of(env, argv[1], &doc)) return nullptr;
+    int64_t n = mt_engine_dump(e, doc, nullptr, 0);
+    if (n < 0) return throw_status(env, e, (int32_t)-n, "mt_engine_dump");
+    void* data = nullptr;
+    napi_value ab, arr;
+    NAPI_OK(napi_create_arraybuffer(env, (size_t)n, &data, &ab));
+    int64_t m = mt_engine_dump(e, doc, (uint8_t*)data, n);
+    if (m != n) return throw_status(env, e, MT_E_ARG, "mt_engine_dump");
+    NAPI_OK(napi_create_typedarray(env, napi_uint8_array, (size_t)n, ab, 0, &arr));
+    return arr;
+}
+
+/* segmentIds(h, doc) -> Int32Array [rid, gen] per segment in dump order (mt_engine_segment_ids) */
+static napi_value js_segment_ids(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    if (!e || !i64_of(env, argv[1], &doc)) return nullptr;
+    int64_t n = mt_engine_segment_ids(e, doc, nullptr, 0);
+    if (n < 0) return throw_status(env, e, (int32_t)-n, "mt_engine_segment_ids");
+    void* data = nullptr;
+    napi_value ab, arr;
+    NAPI_OK(napi_create_arraybuffer(env, 8 * (size_t)n, &data, &ab));
+    int64_t m = mt_engine_segment_ids(e, doc, (int32_t*)data, n);
+    if (m != n) return throw_status(env, e, MT_E_ARG, "mt_engine_segment_ids");
+    NAPI_OK(napi_create_typedarray(env, napi_int32_array, 2 * (size_t)n, ab, 0, &arr));
+    return arr;
+}
+
 static napi_value js_ndocs(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (!get_args(env, info, 1, argv)) return nullptr;
@@ -466,7 +570,10 @@ static napi_value init(napi_env env, napi_value exports) {
                {"getText", js_get_text}, {"posFromRelativePos", js_pos_from_relpos},
                {"handleTable", js_handle_table},     {"getHandle", js_get_handle},    {"getContainingSegment", js_get_containing},
                {"getPosition", js_get_position}, {"ndocs", js_ndocs},        {"lastRunMs", js_last_run_ms},
-               {"deltas", js_deltas},       {"refPositions", js_ref_positions}};
+               {"deltas", js_deltas},       {"refPositions", js_ref_positions},
+               {"resolveRemoteClientPosition", js_resolve_remote}, {"adjustPosition", js_adjust_position},
+               {"handleToPosition", js_handle_to_position}, {"getMarkerFromId", js_marker_from_id},
+               {"dump", js_dump},           {"segmentIds", js_segment_ids}};
     for (auto& f : fns) {
         napi_value fn;
         NAPI_OK(napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn));

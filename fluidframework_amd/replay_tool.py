@@ -126,6 +126,7 @@ class Log:
     trees: Dict[str, dict] = field(default_factory=dict)  # full path -> merge-tree snapshot
     messages: List[Dict[str, Any]] = field(default_factory=list)  # sequenced messages, contents = the op
     paths: List[str] = field(default_factory=list)  # each message's merge tree
+    clients: List[str] = field(default_factory=list)  # clients that sent an op to a merge tree, first-seen order
 
 
 def parse(messages: Iterable[Dict[str, Any]]) -> Log:
@@ -157,21 +158,21 @@ def parse(messages: Iterable[Dict[str, Any]]) -> Log:
             if not isinstance(content, dict):
                 continue
             path = "/".join(str(p) for p in parts + [content.get("address")])
-            if path in log.trees and not _parse(content["contents"]).get("key"):
-                log.messages.append(dict(m, contents=_parse(content["contents"])))
-                log.paths.append(path)
+            if path in log.trees:
+                if m["clientId"] not in log.clients:  # clients.set, before the interval-op test (161-163)
+                    log.clients.append(m["clientId"])
+                if not _parse(content["contents"]).get("key"):  # interval-collection ops are not replayed
+                    log.messages.append(dict(m, contents=_parse(content["contents"])))
+                    log.paths.append(path)
         elif t == ATTACH:
             log.trees.update(merge_trees_of(_parse(m["contents"])))
     return log
 
 
 def clients_of(log: Log) -> List[str]:
-    """The clients that sent merge-tree ops, in first-seen order, then the observer (clients.set, 161, 190)."""
-    seen = []
-    for m in log.messages:
-        if m["clientId"] not in seen:
-            seen.append(m["clientId"])
-    return seen + [READONLY]
+    """The clients that sent an op to a merge tree, in first-seen order, then the observer (clients.set, 161,
+    190; a client whose only ops are interval-collection ops is one, with no own messages)."""
+    return list(log.clients) + [READONLY] if log.trees else []
 
 
 @dataclass
@@ -227,3 +228,64 @@ def streams(log: Log, interner: Optional[ol.Interner] = None) -> Streams:
         for i in pending:
             apply(i)
     return Streams(ol.Batch.from_logs(logs), docs, names, interner)
+
+
+def replay(log: Log, device: int = 0, **caps):
+    """Replay every (merge tree, client) replica of a recorded log in one engine launch on `device`; returns
+    [(path, client, text, length)] in clientReplayTool's order (clients, then merge trees)."""
+    from .engine import Engine, default_caps
+    st = streams(log)
+    c = default_caps(0)
+    c.update(ncap=2048, hcap=4096, acap=1 << 20, mcap=8192)  # capacity promotion covers larger replicas
+    c.update(caps)
+    eng = Engine(st.batch.ndocs, device=device, **c)  # no start_collab: each replica's COLLAB record starts it
+    try:
+        eng.replay(st.batch)
+        err, err_op = eng.errors()
+        bad = [i for i in range(st.batch.ndocs) if err[i]]
+        if bad:
+            i = bad[0]
+            raise RuntimeError(f"replica {st.docs[i]} failed at record {err_op[i]}: error {err[i]}")
+        return [(p, c_, eng.get_text(i), eng.get_length(i)) for i, (p, c_) in enumerate(st.docs)]
+    finally:
+        eng.close()
+
+
+def main(argv=None) -> int:
+    """`python -m fluidframework_amd.replay_tool --indir DIR [--to N] [--verbose]`: ReplayArgs (replayArgs.ts,
+    main.ts) over DIR/messages.json (FileDeltaStorageService, fileDeltaStorageService.ts:18-20: the first N
+    messages, getFromWebSocket(0, to)); every client's replica of every merge tree must equal the readonly
+    observer's text and length (clientReplayTool.ts:246-257). Exit status 0 when they all do."""
+    import argparse
+    import os
+    import sys
+    ap = argparse.ArgumentParser(prog="replay_tool")
+    ap.add_argument("--indir", required=True)
+    ap.add_argument("--to", type=int, default=2 ** 53 - 1)
+    ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--quiet", action="store_true")
+    a = ap.parse_args(argv)
+    with open(os.path.join(a.indir, "messages.json"), encoding="utf-8") as f:
+        msgs = json.load(f)[: a.to]
+    log = parse(msgs)
+    for path in log.trees:
+        print(f"MergeTree Found:\n {json.dumps({'fullPath': path, 'type': SHARED_STRING})}")
+    if a.verbose:
+        for p, m in zip(log.paths, log.messages):
+            print(f"MergeTree op {p}:\n {json.dumps(m['contents'])}")
+    reps = replay(log)
+    obs = {p: (t, n) for p, c, t, n in reps if c == READONLY}
+    errors = 0
+    for p, c, t, n in reps:
+        if (t, n) != obs[p]:
+            errors += 1
+            if errors <= 5:
+                print(f"{c} {p}: length {n} text differs from the readonly client's (length {obs[p][1]})",
+                      file=sys.stderr)
+    print(json.dumps({"merge_trees": len(log.trees), "messages": len(log.messages), "replicas": len(reps),
+                      "errors": errors}))
+    return 0 if errors == 0 else 1
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

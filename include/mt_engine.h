@@ -128,7 +128,11 @@ typedef struct mt_seg_ref {
     int32_t length; /* cachedLength */
     int32_t seq;    /* the segment's seq (-1: local, unacked) */
     int32_t client; /* long client index of its inserter, -1 = LocalClientId */
+    int32_t removed_seq;    /* removedSeq: MT_NOT_REMOVED (the reference's undefined), -1 = a pending local remove */
+    int32_t removed_client; /* long client index of the remover (0 when not removed), -1 = LocalClientId */
+    int32_t ordinal;        /* the segment's index in walkAllSegments order (its canonical dump record) */
 } mt_seg_ref;
+#define MT_NOT_REMOVED INT32_MIN
 /* MergeTree.getContainingSegment(pos, refSeq, clientId) (mergeTree.ts:1656-1667); long_client < 0 =
  * Client.getContainingSegment, the local view (client.ts:1006-1008). */
 int32_t mt_engine_get_containing_segment(mt_engine* e, int64_t doc, int32_t pos, int32_t ref_seq, int32_t long_client,
@@ -145,6 +149,29 @@ int32_t mt_engine_get_position(mt_engine* e, int64_t doc, int32_t rid, int32_t g
 int32_t mt_engine_pos_from_relative_pos(mt_engine* e, int64_t doc, int32_t id_key, int32_t id_value, int32_t before,
                                         int32_t has_offset, int32_t offset, int32_t ref_seq, int32_t long_client,
                                         int32_t* out);
+/* MergeTree.resolveRemoteClientPosition(pos, refSeq, clientId) (mergeTree.ts:2140-2160; SharedSegmentSequence,
+ * sequence.ts:314): the local position of what a remote client saw at `pos` under its (refSeq, client):
+ * getPosition(segment) + offset in the local view, the local length when pos is that client's length, else
+ * *out = -1 (undefined). A perspective persp_refused names (include note at mt_engine_get_length) returns
+ * MT_E_UNSUPPORTED. */
+int32_t mt_engine_resolve_remote_client_position(mt_engine* e, int64_t doc, int32_t pos, int32_t ref_seq,
+                                                 int32_t long_client, int32_t* out);
+/* PermutationVector.adjustPosition(pos, fromSeq, clientId) (permutationvector.ts:185-196; SharedMatrix.processCore,
+ * matrix.ts:597-605): as resolveRemoteClientPosition for a segment that exists and is not removed, else -1. */
+int32_t mt_engine_adjust_position(mt_engine* e, int64_t doc, int32_t pos, int32_t from_seq, int32_t long_client,
+                                  int32_t* out);
+/* PermutationVector.handleToPosition(handle, localSeq) (permutationvector.ts:198-253; matrix.ts:532-533): the
+ * segment whose allocated handles hold `handle` (walkAllSegments order), at findReconnectionPostition(segment,
+ * localSeq) + offset (client.ts:675-705). MT_E_ARG if no segment holds it (the reference's assert). */
+int32_t mt_engine_handle_to_position(mt_engine* e, int64_t doc, int32_t handle, int32_t local_seq, int32_t* out);
+/* Client.getMarkerFromId / MergeTree.getMarkerFromId (client.ts:312, mergeTree.ts:1965-1967): the marker whose
+ * property id_key holds id_value (the engine's lookup, with mt_engine_pos_from_relative_pos's limits: several
+ * markers, or an id an annotate changed, return MT_E_UNSUPPORTED); out->rid = -1 if none. */
+int32_t mt_engine_get_marker_from_id(mt_engine* e, int64_t doc, int32_t id_key, int32_t id_value, mt_seg_ref* out);
+/* Every segment's handle in walkAllSegments order (mergeTree.ts:3002-3016), i.e. aligned with the canonical
+ * dump's records: out[2i] = rid, out[2i+1] = gen for at most cap segments; returns the segment count (<0 on
+ * error). With the dump this is what Client.walkSegments / getPropertiesAtPosition / findTile read. */
+int64_t mt_engine_segment_ids(mt_engine* e, int64_t doc, int32_t* out, int64_t cap);
 /* Delta events (mt_oplog.h MT_DELTA_*; engines created with caps.dcap > 0): the stream a
  * SharedString "sequenceDelta" + "maintenance" listener would see (sequence.ts:136-150), batched.
  * mt_engine_delta_state: per doc the words emitted since create/reset (n_out, may exceed dcap) and

@@ -71,6 +71,11 @@ enum {
  * segment's LocalReferenceCollection (Client.removeLocalReference, client.ts:299-301 ->
  * LocalReferenceCollection.removeLocalRef, localReference.ts:225-264); 0 creates one */
 #define MT_REF_REMOVE 1
+/* seg_kind of an MT_OP_NOOP | MT_OPF_LOCAL record that is the splitRange of Client.walkSegments(..., pos1, pos2,
+ * accum, splitRange = true) (client.ts:276-285 -> MergeTree.mapRange, mergeTree.ts:2830-2838): ensureIntervalBoundary
+ * at pos1, then at pos2, each only when non-zero, in the local view (client-feature build); 0 is
+ * PermutationVector.getAllocatedHandle(pos1) */
+#define MT_NOOP_SPLIT 1
 /* A group op (MergeTreeDeltaType.GROUP, ops.ts:33, 100; e.g. SharedString.replaceRange,
  * sequence.ts:464) is one sequenced message carrying several member ops: it is sent as its member
  * records in order, all with the message's client/seq/ref_seq/min_seq, every member but the last

@@ -121,6 +121,25 @@ def test_merge_tree_calls_text_ranges_and_per_doc_seqs_through_node():
     assert out["starUnsupported"]  # the "*" placeholder (Marker.toString()) is not modelled
 
 
+@pytest.mark.gpu
+def test_client_surface_through_node():
+    """tests/napi_kat3.js: the rest of the Client surface SharedString / SharedSegmentSequence / SharedMatrix call
+    (walkSegments with splitRange, getPropertiesAtPosition, getRangeExtentsOfPosition, resolveRemoteClientPosition,
+    localTransaction, insertSegmentLocal, findTile, getMarkerFromId, annotateMarker, removeLocalReference,
+    PermutationVector adjustPosition / handleToPosition) through node -> addon -> GPU; the answers are the
+    type-erased reference's for the same steps (tools/make_napi_kat3.mjs)"""
+    native.build_napi()
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "napi_kat3.js")], capture_output=True, text=True,
+                       cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "napi_kat3_expected.json")))
+    assert len(out["answers"]) == len(want)
+    for i, (g, w) in enumerate(zip(out["answers"], want)):
+        assert g == w, (i, g, w)
+    assert out["refused"]  # a perspective the reference's partial lengths answer differently is refused
+
+
 def test_typings_declare_every_export_and_method():
     """fluidframework_amd/js/mergetree_gpu.d.ts declares every name the facade exports and every public method
     of its classes (no TypeScript compiler in this image: a textual check)"""

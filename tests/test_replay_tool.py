@@ -1,0 +1,104 @@
+"""The client replay tool's per-client reconstruction (fluidframework_amd/replay_tool.py; SURVEY §8(f) f2,
+VERDICT r3 missing #2) against the REFERENCE (tests/golden/refreplaytool.npz, tools/make_ref_goldens.py
+--replaytool: clientReplayTool.ts's steps over the reference Client, tools/ref_replay_tool.mjs).
+
+Two recorded documents (tests/replaylog.py: a 7-client conflict farm's sequenced messages on a SharedString
+attach snapshot, as a container Attach message and as a legacy attach inside the envelopes, with chunked ops,
+JSON-string envelopes, non-op messages, unattached-channel and interval-collection ops) are reconstructed
+into one replica per (merge tree, client): the attach snapshot loaded as that client, its own ops as local
+transactions after the messages it had seen, every message applied once. Each replica's getText and
+getLength must equal the reference tool's, on the host core and on the GPU, and every replica converges to
+the observer's text."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import core_host
+import replaylog
+from fluidframework_amd import replay_tool as rt
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CAPS = dict(ncap=2048, hcap=4096, acap=1 << 17, mcap=4096, gcap=1024, ccap=64)
+
+
+def fnv(units: str) -> int:
+    h = 0xcbf29ce484222325
+    for x in units.encode("utf-16-le"):
+        h = ((h ^ x) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def load():
+    z = np.load(os.path.join(GOLDEN, "refreplaytool.npz"), allow_pickle=False)
+    docs = replaylog.documents()
+    for k, msgs in enumerate(docs):
+        assert hashlib.sha256(json.dumps(msgs).encode()).hexdigest() == str(z["log_sha256"][k]), "logs changed"
+    return z, docs
+
+
+def expected(z, k):
+    m = z["doc"] == k
+    return list(zip(z["path"][m], z["client"][m], z["text_len"][m], z["text_fnv"][m], z["length"][m]))
+
+
+def test_parse_steps():
+    """chunked ops reassembled, envelopes unwrapped, both attach forms found, noise skipped; a client with only
+    interval-collection ops is still a replica (clientReplayTool.ts:161-163)"""
+    z, docs = load()
+    for k, msgs in enumerate(docs):
+        log = rt.parse(msgs)
+        assert len(log.trees) == 1 and len(log.messages) == 2000
+        assert {m["type"] for m in msgs} >= {"chunkedOp", "op", "noop"}
+        assert [(p, c) for p, c, *_ in expected(z, k)] == [(p, c) for c in rt.clients_of(log) for p in log.trees]
+    assert "c99" in rt.clients_of(rt.parse(docs[0]))
+    with pytest.raises(ValueError):
+        rt.reassemble([{"clientId": "a", "type": "chunkedOp", "contents": json.dumps(
+            {"chunkId": 1, "totalChunks": 2, "contents": "x", "originalType": "op"})}] * 2)
+
+
+def test_host_core_replicas_match_reference_tool():
+    z, docs = load()
+    for k, msgs in enumerate(docs):
+        st = rt.streams(rt.parse(msgs))
+        caps = (CAPS["ncap"], CAPS["hcap"], CAPS["acap"], CAPS["mcap"], CAPS["gcap"], CAPS["ccap"])
+        hs = core_host.HostStore(st.batch.ndocs, caps)  # no start_collab: the load records' COLLAB starts it
+        err = np.asarray([hs.replay(d, *st.batch.doc(d)) for d in range(st.batch.ndocs)])
+        assert (err == 0).all(), err
+        for i, (path, client, tlen, tf, length) in enumerate(expected(z, k)):
+            t = hs.text(i)
+            assert (len(t), fnv(t), hs.L.mth_length_local(hs.h, i)) == (tlen, int(tf), length), (k, path, client)
+        assert hs.text(st.batch.ndocs - 1) == str(z["observer_texts"][k])
+
+
+@pytest.mark.gpu
+def test_gpu_replicas_match_reference_tool():
+    from fluidframework_amd.engine import Engine
+    z, docs = load()
+    for k, msgs in enumerate(docs):
+        st = rt.streams(rt.parse(msgs))
+        eng = Engine(st.batch.ndocs, **CAPS)  # no start_collab: the load records' COLLAB starts it
+        eng.replay(st.batch)
+        err, err_op = eng.errors()
+        assert (err == 0).all(), (err, err_op)
+        for i, (path, client, tlen, tf, length) in enumerate(expected(z, k)):
+            t = eng.get_text(i)
+            assert (len(t), fnv(t), eng.get_length(i)) == (tlen, int(tf), length), (k, path, client)
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_replay_tool_cli_on_gpu(tmp_path):
+    """python -m fluidframework_amd.replay_tool --indir DIR: the tool's own check, every replica equals the
+    readonly observer, on a recorded log written as FileDeltaStorageService reads it (messages.json)"""
+    import subprocess
+    import sys
+    _, docs = load()
+    (tmp_path / "messages.json").write_text(json.dumps(docs[1]))
+    r = subprocess.run([sys.executable, "-m", "fluidframework_amd.replay_tool", "--indir", str(tmp_path)],
+                       capture_output=True, text=True, cwd=os.path.dirname(os.path.dirname(GOLDEN)), timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out == {"merge_trees": 1, "messages": 2000, "replicas": 8, "errors": 0}

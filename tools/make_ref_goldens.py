@@ -674,6 +674,40 @@ def make_persp(node: str) -> None:
               f"answers", flush=True)
 
 
+def make_replaytool(node: str) -> None:
+    """tests/golden/refreplaytool.npz: the reference merge-tree client replay tool's per-client replicas
+    (clientReplayTool.ts:113-258, restated over the reference Client by tools/ref_replay_tool.mjs) for the
+    recorded-document logs of tests/replaylog.py: per replica its merge tree, client, getLength and the length
+    and FNV-1a-64 (UTF-16LE) of getText; the logs' SHA-256; the observer's full texts."""
+    import replaylog
+    rows, texts, shas = [], [], []
+    for k, msgs in enumerate(replaylog.documents()):
+        d = os.path.join(SCRATCH, f"replaytool_{k}")
+        os.makedirs(d, exist_ok=True)
+        blob = json.dumps(msgs)
+        shas.append(hashlib.sha256(blob.encode()).hexdigest())
+        with open(os.path.join(d, "messages.json"), "w") as f:
+            f.write(blob)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay_tool.mjs"), ERASED,
+                            os.path.join(d, "messages.json"), os.path.join(d, "out.json")], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay tool failed: {r.stderr[-2000:]}")
+        reps = json.load(open(os.path.join(d, "out.json")))["replicas"]
+        for path, client, text, length in reps:
+            rows.append([k, path, client, len(text), fnv1a64(text.encode("utf-16-le")), length])
+            if client == "readonly":
+                texts.append(text)
+        print(f"replaytool doc {k}: {len(reps)} replicas, lengths {sorted(set(x[3] for x in reps))}", flush=True)
+    np.savez_compressed(
+        os.path.join(GOLDEN, "refreplaytool.npz"),
+        doc=np.asarray([x[0] for x in rows], np.int32), path=np.asarray([x[1] for x in rows]),
+        client=np.asarray([x[2] for x in rows]), text_len=np.asarray([x[3] for x in rows], np.int64),
+        text_fnv=np.asarray([x[4] for x in rows], np.uint64), length=np.asarray([x[5] for x in rows], np.int64),
+        observer_texts=np.asarray(texts), log_sha256=np.asarray(shas),
+        source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                "tools/ref_replay_tool.mjs: clientReplayTool.ts's reconstruction over the reference Client"))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default=",".join(SETS))
@@ -688,8 +722,12 @@ def main() -> None:
     ap.add_argument("--tree", action="store_true", help="write the MergeTree-level record fixtures (reftree_*.npz) only")
     ap.add_argument("--unref", action="store_true", help="write the removeLocalReference fixtures (refunref_*.npz) only")
     ap.add_argument("--persp", action="store_true", help="write the past-perspective read fixtures (refpersp_*.npz) only")
+    ap.add_argument("--replaytool", action="store_true", help="write the client replay tool fixture only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
+    if args.replaytool:
+        make_replaytool(args.node)
+        return
     if args.persp:
         make_persp(args.node)
         return
