@@ -132,6 +132,7 @@ def main() -> None:
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (default: host share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--digests-out", default="", help="save the per-document digests (.npy) after the run")
     ap.add_argument("--gen-cache", default=os.environ.get("MT_GEN_CACHE", ""),
                     help="directory caching generated workloads between runs (profiler passes)")
     args = ap.parse_args()
@@ -226,6 +227,8 @@ def main() -> None:
     seq_ops = int(work[:, 0].sum())
     alg_bytes = 16 * int(work[:, 1].sum()) + 32 * int(work[:, 2].sum())
     digests = eng.digests()
+    if args.digests_out:
+        np.save(args.digests_out, digests)
 
     if dist:
         dev = f"cuda:{device}"

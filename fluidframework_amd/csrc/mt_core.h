@@ -1529,6 +1529,9 @@ struct Replica {
      * STABLE summaries (or DEAD), entries of freed rows drop out, and every remaining row's chunk
      * position, leaf index and perspective length go to the scratch, its length scattered onto
      * cdel[chunk position]. Returns the sum of those lengths. */
+#ifndef MT_WIN_NB
+#define MT_WIN_NB 8 /* wave passes of the window set issued together (r04 A/B: tools/gpu.sh ab) */
+#endif
     MT_HD int32_t win_pass(int32_t refSeq, int32_t client) {
         MT_PROF_SCOPE(PH_WIN);
         auto& t = z.tl;
@@ -1536,7 +1539,7 @@ struct Replica {
          * together (one round trip per stage, not one per stage per pass); the settling and the
          * compaction then run pass by pass, in entry order. Every read of a block precedes its writes,
          * and the compaction only writes entries at or before the ones read. */
-        constexpr int NB = W::N >= 64 ? 8 : 1;
+        constexpr int NB = W::N >= 64 ? MT_WIN_NB : 1;
         int32_t n = t.wN, wpos = 0, total = 0;
         for (int32_t b0 = 0; b0 < n; b0 += NB * W::N) {
             int32_t rd[NB], g[NB], s[NB], v[NB], cp[NB], lx[NB];

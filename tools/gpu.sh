@@ -13,6 +13,7 @@
 #   wait:C           SQ wait / busy / LDS bank-conflict pass        -> OUT/pmc_wait_cC
 #   phase:C          per-phase cycle clocks (profiling build)       -> OUT/phase_cC.txt
 #   py:SCRIPT        python -u SCRIPT (a helper under tools/)       -> OUT/py_<name>.txt
+#   ab:C:L1,L2,...   bench.py --config C per library build/Lk (MT_REPLAY_LIB), digests compared with L1
 # Per-config extra bench arguments: ARGS_C (e.g. ARGS_4="--ops-per-doc 300000"); PHASE_C for phase:C.
 # Generated workloads are cached under /tmp/mtgen between the steps of one call (bench.py --gen-cache).
 set -o pipefail
@@ -76,6 +77,19 @@ for S in "$@"; do
       timeout -k 10 $(prof_lim "$A") python -u tools/phase_profile.py --config "$A" ${!v} > "$OUT/phase_c$A.txt" 2>&1 \
         || fail "$S" $? "$OUT/phase_c$A.txt"
       cat "$OUT/phase_c$A.txt" ;;
+    ab)  # ab:C:libA,libB,... : one bench line per library (MT_REPLAY_LIB), digests compared with the first
+      C=${A%%:*}; LIBS=${A#*:}
+      first=""
+      for L in ${LIBS//,/ }; do
+        n=$(basename "$L" .so)
+        MT_REPLAY_LIB=$PWD/fluidframework_amd/build/$L timeout -k 10 $(prof_lim "$C") python -u bench.py $(bargs "$C") \
+          --no-cpu-baseline --digests-out "$OUT/dig_c${C}_$n.npy" > "$OUT/ab_c${C}_$n.json" 2> "$OUT/ab_c${C}_$n.err" \
+          || fail "$S/$n" $? "$OUT/ab_c${C}_$n.err"
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['value']/1e6,3), 'Mops/s', round(d['roofline']['kernel_ms'],1), 'ms')" "$OUT/ab_c${C}_$n.json" "$n"
+        if [ -z "$first" ]; then first=$n; else
+          python -c "import numpy as np,sys; a=np.load(sys.argv[1]); b=np.load(sys.argv[2]); print('  digests equal to', sys.argv[3], bool((a==b).all()))" "$OUT/dig_c${C}_$first.npy" "$OUT/dig_c${C}_$n.npy" "$first"
+        fi
+      done ;;
     py)
       n=$(basename "${A%% *}" .py)
       timeout -k 10 600 python -u $A > "$OUT/py_$n.txt" 2>&1 || fail "$S" $? "$OUT/py_$n.txt"
