@@ -213,6 +213,7 @@ struct TileState<N, true> {
     int32_t cpos[NCH];      /* chunk id -> position (free chunks: next free id) */
     int32_t ccnt[NCH];      /* chunk id -> leaf count */
     int32_t cleaf[NCH][CH]; /* chunk id -> its leaves in order */
+    int32_t cls[NCH][CH];   /* chunk id -> its leaves' lst, in the same order (a chunk search reads one line) */
     int32_t wrid[WCAP];     /* window set: row ids */
     uint8_t wgen[WCAP];     /* their generations when added */
     int32_t wslot[WCAP];    /* the slot each was last seen in (a hint: rows move; checked before use) */
@@ -439,6 +440,7 @@ struct Replica {
     uint8_t* twgen;
     int32_t* twslot;
     int64_t cur; /* index of the record being applied in the current Pools (snapshot reload reads ahead) */
+    int32_t* pfcur = nullptr; /* tiled kernel: where the prefetch helper waves read `cur` (LDS) */
     int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
@@ -1307,6 +1309,7 @@ struct Replica {
         t.lch[0] = 0;
         t.lix[0] = 0;
         t.lst[0] = 0;
+        t.cls[0][0] = 0;
         t.wN = 0;
         w.sync();
     }
@@ -1355,10 +1358,11 @@ struct Replica {
         if constexpr (W::N >= 64) {
             int32_t i = i0 + w.lane();
             bool ok = i < cnt;
-            int32_t lf = ok ? t.cleaf[c][i] : 0;
+            int32_t lf = ok ? t.cleaf[c][i] : 0, ls = ok ? t.cls[c][i] : 0;
             w.sync();
             if (ok) {
                 t.cleaf[c][i + delta] = lf;
+                t.cls[c][i + delta] = ls;
                 t.lix[lf] = (uint8_t)(i + delta);
             }
             w.sync();
@@ -1367,6 +1371,7 @@ struct Replica {
                 int32_t i = delta > 0 ? cnt - 1 - q : i0 + q;
                 int32_t lf = t.cleaf[c][i];
                 t.cleaf[c][i + delta] = lf;
+                t.cls[c][i + delta] = t.cls[c][i];
                 t.lix[lf] = (uint8_t)(i + delta);
             }
         }
@@ -1391,10 +1396,11 @@ struct Replica {
                 int32_t v = 0;
                 if (l < HALF) {
                     int32_t lf = t.cleaf[c][HALF + l];
+                    v = t.cls[c][HALF + l];
                     t.cleaf[c2][l] = lf;
+                    t.cls[c2][l] = v;
                     t.lch[lf] = c2;
                     t.lix[lf] = (uint8_t)l;
-                    v = t.lst[lf];
                 }
                 moved += w.sum(v);
             }
@@ -1410,11 +1416,13 @@ struct Replica {
         }
         int32_t cnt = tccnt[c];
         chunk_shift(c, i, cnt, 1);
+        int32_t lb = t.lst[b];
         t.cleaf[c][i] = b;
+        t.cls[c][i] = lb;
         t.lch[b] = c;
         t.lix[b] = (uint8_t)i;
         tccnt[c] = cnt + 1;
-        tcst[tcpos[c]] += t.lst[b];
+        tcst[tcpos[c]] += lb;
         w.sync();
     }
     /* leaf b leaves the document order (its STABLE length leaves its chunk's summary) */
@@ -1436,8 +1444,10 @@ struct Replica {
     }
     MT_HD void lst_add(int32_t n, int32_t d) {
         auto& t = z.tl;
+        int32_t c = t.lch[n];
         t.lst[n] += d;
-        tcst[tcpos[t.lch[n]]] += d;
+        t.cls[c][t.lix[n]] += d;
+        tcst[tcpos[c]] += d;
     }
     /* recompute leaf n's STABLE length from its rows */
     MT_HD void leaf_restat(int32_t n) {
@@ -1464,7 +1474,7 @@ struct Replica {
             int32_t n = -1;
             for (int32_t k = 0; k < MAXN; k++)
                 if (k == i && k < cnt) n = nl[k];
-            int32_t old = n >= 0 ? t.lst[n] : 0, ch = n >= 0 ? t.lch[n] : 0;
+            int32_t old = n >= 0 ? t.lst[n] : 0, ch = n >= 0 ? t.lch[n] : 0, ix = n >= 0 ? t.lix[n] : 0;
             int32_t c = n >= 0 ? nch[n] : 0;
             int32_t x = 0;
             if (j < c && (t.xf[n * MAXN + j] & XF_STABLE)) x = z.len(n * MAXN + j);
@@ -1472,7 +1482,10 @@ struct Replica {
             x += w.shfl_xor(x, 2);
             x += w.shfl_xor(x, 4);
             w.sync();
-            if (n >= 0 && j == 0) t.lst[n] = x;
+            if (n >= 0 && j == 0) {
+                t.lst[n] = x;
+                t.cls[ch][ix] = x;
+            }
             for (int32_t k = 0; k < cnt; k++) {
                 int32_t dk = w.bcast(x - old, MAXN * k);
                 if (dk) tcst[tcpos[w.bcast(ch, MAXN * k)]] += dk;
@@ -1530,7 +1543,7 @@ struct Replica {
      * position, leaf index and perspective length go to the scratch, its length scattered onto
      * cdel[chunk position]. Returns the sum of those lengths. */
 #ifndef MT_WIN_NB
-#define MT_WIN_NB 8 /* wave passes of the window set issued together (r04 A/B: tools/gpu.sh ab) */
+#define MT_WIN_NB 2 /* wave passes of the window set issued together: the set is ~80-100 rows, so 2 passes cover it in one round trip without the dead issue of 8 (r04e A/B at 256 x 300k: 8.81 -> 9.66M ops/s) */
 #endif
     MT_HD int32_t win_pass(int32_t refSeq, int32_t client) {
         MT_PROF_SCOPE(PH_WIN);
@@ -1593,8 +1606,6 @@ struct Replica {
                 if (keep[q]) {
                     v[q] = vis_of(s[q], rv[q], refSeq, client);
                     cp[q] = tcpos[lc[q]];
-                } else {
-                    lx[q] = 0;
                 }
             }
             for (int q = 0; q < NB; q++) {
@@ -1606,9 +1617,10 @@ struct Replica {
                     int32_t ss = w.bcast(s[q], l);
                     if (w.bcast(rv[q].rseq, l) == NOREM) {
                         t.xf[ss] = XF_STABLE;
-                        int32_t dl = w.bcast(rv[q].len, l);
+                        int32_t dl = w.bcast(rv[q].len, l), lcl = w.bcast(lc[q], l);
                         t.lst[ss / MAXN] += dl;
-                        tcst[tcpos[w.bcast(lc[q], l)]] += dl;
+                        t.cls[lcl][w.bcast(lx[q], l)] += dl;
+                        tcst[tcpos[lcl]] += dl;
                     } else {
                         t.xf[ss] = 0;
                     }
@@ -1646,7 +1658,7 @@ struct Replica {
     /* Leaf position k and start offset P of the leaf holding the first row with
      * P < pos <= P + vis, from the chunk and leaf summaries plus the window scratch of the last
      * win_pass (same perspective). -1 if pos is beyond the length. */
-    MT_HD int32_t tile_find(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+    MT_HD int32_t tile_find(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout, int32_t* Nout) {
         MT_PROF_SCOPE(PH_TFIND);
         auto& t = z.tl;
         int32_t nc = t.nchunk;
@@ -1696,14 +1708,18 @@ struct Replica {
         }
         for (int32_t b = 0; b < cnt; b += W::N) {
             int32_t l = b + w.lane();
-            int32_t v = 0;
-            if (l < cnt) v = t.lst[t.cleaf[c][l]] + (W::N >= 64 ? ldel[0] : ldel[l]);
+            int32_t v = 0, nl = 0;
+            if (l < cnt) { /* the leaf's summary and its node id: one round trip */
+                v = t.cls[c][l] + (W::N >= 64 ? ldel[0] : ldel[l]);
+                nl = t.cleaf[c][l];
+            }
             int32_t tot;
             int32_t p = run + w.excl_scan(v, &tot);
             uint64_t m = w.ballot(l < cnt && p < pos && pos <= p + v);
             if (m) {
                 int32_t ll = W::ffs(m);
                 *Pout = w.bcast(p, ll);
+                *Nout = w.bcast(nl, ll);
                 return (cpf << 6) | (b + ll);
             }
             run += tot;
@@ -1712,9 +1728,10 @@ struct Replica {
         return -1;
     }
     /* within leaf position k (start offset P): the row t = k*8+j with P < pos <= P + vis */
-    MT_HD int32_t leaf_find(int32_t k, int32_t P, int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+    /* n: the leaf node at k (tile_find's) */
+    MT_HD int32_t leaf_find(int32_t k, int32_t n, int32_t P, int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
         MT_PROF_SCOPE(PH_LFIND);
-        int32_t n = leaf_at(k), c = nch[n];
+        int32_t c = nch[n];
         if constexpr (W::N >= MAXN) { /* lane j: child j; one prefix scan */
             int32_t j = w.lane();
             int32_t v = j < c ? vis(n * MAXN + (j & (MAXN - 1)), refSeq, client) : 0;
@@ -1766,10 +1783,11 @@ struct Replica {
         if (!tiles_cover(refSeq, client)) return find_reach_walk(pos, refSeq, client, Pout);
         win_pass(refSeq, client);
         int32_t P;
-        int32_t k = tile_find(pos, refSeq, client, &P);
+        int32_t n = 0;
+        int32_t k = tile_find(pos, refSeq, client, &P, &n);
         win_clear();
         if (k < 0) return -1;
-        return leaf_find(k, P, pos, refSeq, client, Pout);
+        return leaf_find(k, n, P, pos, refSeq, client, Pout);
     }
     MT_HD int32_t length_tiled(int32_t refSeq, int32_t client) {
         if (!tiles_cover(refSeq, client)) {
@@ -3505,15 +3523,16 @@ struct Replica {
             }
             int32_t last = end < total ? end : total;
             int32_t P1, P2;
-            int32_t k1 = tile_find(start + 1, refSeq, client, &P1);
-            int32_t k2 = tile_find(last, refSeq, client, &P2);
+            int32_t n1 = 0, n2 = 0;
+            int32_t k1 = tile_find(start + 1, refSeq, client, &P1, &n1);
+            int32_t k2 = tile_find(last, refSeq, client, &P2, &n2);
             win_clear();
             if (k1 < 0 || k2 < 0) {
                 fail(E_ASSERT);
                 return;
             }
-            tf = leaf_find(k1, P1, start + 1, refSeq, client, &Pf);
-            tg = leaf_find(k2, P2, last, refSeq, client, &Pg);
+            tf = leaf_find(k1, n1, P1, start + 1, refSeq, client, &Pf);
+            tg = leaf_find(k2, n2, P2, last, refSeq, client, &Pg);
         } else {
             int32_t total = length_tiled(refSeq, client);
             if (start >= total || end <= start) return;
@@ -4311,7 +4330,7 @@ struct Replica {
                 }
                 for (int32_t b = 0; b < li; b += W::N) {
                     int32_t l = b + w.lane();
-                    total += w.sum(l < li ? t.lst[t.cleaf[c][l]] : 0);
+                    total += w.sum(l < li ? t.cls[c][l] : 0);
                 }
                 int32_t nw = t.wN;
                 for (int32_t b = 0; b < nw; b += W::N) {
@@ -4468,6 +4487,8 @@ struct Replica {
                 mt_op_rec op;
                 __builtin_memcpy(&op, u, sizeof(op));
                 cur = b + k;
+                if constexpr (TILED)
+                    if (pfcur) *(volatile int32_t*)pfcur = (int32_t)cur; /* the prefetch helpers run ahead of it */
                 apply(op, p);
                 if (h.err) return;
             }

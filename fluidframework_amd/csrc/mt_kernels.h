@@ -203,8 +203,98 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
  * rope's chunk arrays and the window set (with each row's last-seen slot). The rows, the leaf summaries,
  * the per-leaf rope links and the zamboni heap stay in HBM (~0.2 GB per 1M-op document; an LDS copy of
  * the heap measured no faster). */
+#ifndef MT_PF_HELPERS
+#define MT_PF_HELPERS 1 /* prefetch helper waves per config-4 document (0: one wave per document) */
+#endif
+#ifndef MT_PF_AHEAD
+#define MT_PF_AHEAD 2 /* records ahead of the replaying wave each helper looks */
+#endif
+/* The helper waves of a config-4 workgroup (k_replay_tiled). A document's events are one dependent chain, so
+ * the other SIMDs of the document's CU cannot share the replay; they run ahead of it instead: for the records
+ * after the one being applied, a helper resolves each position approximately from the current summaries
+ * (chunk scan over the staged LDS summaries without the window deltas, then the chunk's leaf summaries) and
+ * loads what the replay will read there — the chunk's leaf-summary line, the leaf's 128-byte line and its
+ * neighbour's, the leaf's row ids and child count, and the first 16 bytes of its rows' cold records — and,
+ * for the zamboni that follows, the leaf of the row at the heap's top. Those reads then hit the L2 / MALL when
+ * the replay makes them. Helpers only read (the summaries they scan may be mid-update: an approximate answer
+ * only changes what is prefetched); every index is clamped to its array; they exit when the replay is done. */
+template <class HT>
+__device__ void tiled_prefetch(Doc<HT> v, const mt_op_rec* ops, int64_t nops, const volatile int32_t* cur,
+                               const volatile int32_t* done, const int32_t* lcord, const int32_t* lcst,
+                               const int32_t* lccnt, int32_t* sink) {
+    constexpr int NCH = HT::TL::NCH, N = HT::N, S = HT::S;
+    const HT* t = v.t;
+    const auto& tl = t->tl;
+    const typename HT::Cold* cold = v.cold();
+    WaveGPU w;
+    const int32_t lane = w.lane(), helper = (int32_t)(threadIdx.x / WG) - 1;
+    uint32_t acc = 0;
+    int64_t last = -1;
+    auto touch_leaf = [&](int32_t leaf) {
+        leaf = leaf < 0 ? 0 : (leaf >= N ? N - 1 : leaf);
+        const int32_t* line = (const int32_t*)&t->lf[leaf];
+        int32_t j = lane & 7;
+        int32_t r = t->rid[leaf * 8 + j];
+        r = r < 0 ? 0 : (r >= S ? S - 1 : r);
+        uint32_t x = lane < 32 ? (uint32_t)line[lane] : (uint32_t)t->nchild[leaf];
+        const uint32_t* cr = (const uint32_t*)&cold[r];
+        x ^= lane < 8 ? cr[0] ^ cr[1] ^ cr[2] ^ cr[3] : (uint32_t)t->rleaf[r] ^ t->rgen[r];
+        acc ^= x ^ (uint32_t)r;
+    };
+    while (!*done) {
+        int64_t k = (int64_t)*cur + 1 + helper * MT_PF_AHEAD;
+        if (k <= last) k = last + 1;
+        if (k >= nops || k > (int64_t)*cur + (helper + 1) * MT_PF_AHEAD) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        last = k;
+        mt_op_rec op = ops[k];
+        int32_t kind = op.kind & MT_OP_KIND_MASK;
+        if (kind > MT_OP_ANNOTATE || (op.kind & (MT_OPF_LOCAL | MT_OPF_TREE))) continue;
+        int32_t nch = tl.nchunk;
+        nch = nch < 1 ? 1 : (nch > NCH ? NCH : nch);
+        for (int32_t e = 0; e < (kind == MT_OP_INSERT ? 1 : 2); e++) {
+            int32_t pos = e ? op.pos2 : op.pos1;
+            int32_t run = 0, cp = nch - 1;
+            for (int32_t b = 0; b < nch; b += WG) { /* chunk scan over the staged STABLE summaries */
+                int32_t i = b + lane;
+                int32_t x = i < nch ? lcst[i] : 0;
+                int32_t tot;
+                int32_t q = run + w.excl_scan(x, &tot);
+                uint64_t m = w.ballot(i < nch && q + x >= pos);
+                if (m) {
+                    int32_t l = WaveGPU::ffs(m);
+                    cp = b + l;
+                    run = w.bcast(q, l);
+                    break;
+                }
+                run += tot;
+            }
+            int32_t c = lcord[cp];
+            c = c < 0 ? 0 : (c >= NCH ? NCH - 1 : c);
+            int32_t cnt = lccnt[c];
+            cnt = cnt < 1 ? 1 : (cnt > 64 ? 64 : cnt);
+            int32_t x = lane < cnt ? tl.cls[c][lane] : 0; /* the chunk's leaf summaries: one line */
+            int32_t tot;
+            int32_t q = run + w.excl_scan(x, &tot);
+            uint64_t m = w.ballot(lane < cnt && q + x >= pos);
+            int32_t li = m ? WaveGPU::ffs(m) : cnt - 1;
+            int32_t leaf = tl.cleaf[c][li];
+            touch_leaf(leaf);
+            touch_leaf(tl.cleaf[c][li + 1 < cnt ? li + 1 : li]);
+        }
+        if (t->h.heapN > 0) { /* the zamboni after it: the leaf of the row at the heap's top */
+            int32_t r = t->hrid[0];
+            r = r < 0 ? 0 : (r >= S ? S - 1 : r);
+            touch_leaf(t->rleaf[r]);
+        }
+    }
+    if (acc == 0x9e3779b9u && lane == 0) *sink = (int32_t)acc; /* keeps the loads */
+}
+
 template <class HT, bool DL = false>
-__global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
+__global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                                      const int64_t* op_off, const uint16_t* text,
                                                      const int64_t* text_off, const mt_props_rec* props,
                                                      const int64_t* props_off, const mt_kv* kv, const int64_t* kv_off,
@@ -219,19 +309,27 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     __shared__ int32_t lcord[NCH], lcst[NCH], lcpos[NCH], lccnt[NCH], lwrid[WCAP];
     __shared__ __attribute__((aligned(16))) uint8_t lwgen[WCAP];
     __shared__ int32_t lwslot[WCAP];
+    __shared__ int32_t pfcur, pfdone, pfsink; /* the replaying wave's record, its end, the helpers' sink */
     int64_t d = blockIdx.x;
     if (d >= ndocs) return;
-    for (int i = threadIdx.x; i < NCH; i += WG) cdel[i] = 0;
     Doc<HT> v = st.doc(d);
     auto& tl = v.t->tl;
-    wave_copy((int32_t*)&zhs, (const int32_t*)&v.t->h, (int)(sizeof(DocHdr) / 4));
-    wave_copy(lcord, tl.cord, NCH);
-    wave_copy(lcst, tl.cst, NCH);
-    wave_copy(lcpos, tl.cpos, NCH);
-    wave_copy(lccnt, tl.ccnt, NCH);
-    wave_copy(lwrid, tl.wrid, WCAP);
-    wave_copy((int32_t*)lwgen, (const int32_t*)tl.wgen, WCAP / 4);
-    wave_copy(lwslot, tl.wslot, WCAP);
+    const bool replayer = threadIdx.x < WG;
+    if (replayer) {
+        for (int i = threadIdx.x; i < NCH; i += WG) cdel[i] = 0;
+        wave_copy((int32_t*)&zhs, (const int32_t*)&v.t->h, (int)(sizeof(DocHdr) / 4));
+        wave_copy(lcord, tl.cord, NCH);
+        wave_copy(lcst, tl.cst, NCH);
+        wave_copy(lcpos, tl.cpos, NCH);
+        wave_copy(lccnt, tl.ccnt, NCH);
+        wave_copy(lwrid, tl.wrid, WCAP);
+        wave_copy((int32_t*)lwgen, (const int32_t*)tl.wgen, WCAP / 4);
+        wave_copy(lwslot, tl.wslot, WCAP);
+        if (threadIdx.x == 0) {
+            pfcur = 0;
+            pfdone = 0;
+        }
+    }
     __syncthreads();
     Pools p;
     p.ops = ops + op_off[d];
@@ -239,34 +337,42 @@ __global__ __launch_bounds__(WG) void k_replay_tiled(Store<HT> st, int64_t ndocs
     p.text = text + text_off[d];
     p.props = props + props_off[d];
     p.kv = kv + kv_off[d];
-    Replica<WaveGPU, HT, DL> r(v, WaveGPU());
-    r.cdel = cdel;
-    r.wcp = wcp;
-    r.wvs = wvs;
-    r.wlx = wlx;
-    r.zh = &zhs;
-    r.tcord = lcord;
-    r.tcst = lcst;
-    r.tcpos = lcpos;
-    r.tccnt = lccnt;
-    r.twrid = lwrid;
-    r.twgen = lwgen;
-    r.twslot = lwslot;
-    r.replay(p);
-    r.commit();
-    __syncthreads();
-    wave_copy((int32_t*)&v.t->h, (const int32_t*)&zhs, (int)(sizeof(DocHdr) / 4));
-    wave_copy(tl.cord, lcord, NCH);
-    wave_copy(tl.cst, lcst, NCH);
-    wave_copy(tl.cpos, lcpos, NCH);
-    wave_copy(tl.ccnt, lccnt, NCH);
-    wave_copy(tl.wrid, lwrid, WCAP);
-    wave_copy((int32_t*)tl.wgen, (const int32_t*)lwgen, WCAP / 4);
-    wave_copy(tl.wslot, lwslot, WCAP);
+    if (!replayer) {
+        tiled_prefetch<HT>(v, p.ops, p.nops, &pfcur, &pfdone, lcord, lcst, lccnt, &pfsink);
+    } else {
+        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
+        r.cdel = cdel;
+        r.wcp = wcp;
+        r.wvs = wvs;
+        r.wlx = wlx;
+        r.zh = &zhs;
+        r.tcord = lcord;
+        r.tcst = lcst;
+        r.tcpos = lcpos;
+        r.tccnt = lccnt;
+        r.twrid = lwrid;
+        r.twgen = lwgen;
+        r.twslot = lwslot;
+        if (MT_PF_HELPERS > 0) r.pfcur = &pfcur;
+        r.replay(p);
+        r.commit();
+        if (threadIdx.x == 0) *(volatile int32_t*)&pfdone = 1;
 #ifdef MT_PROF
-    if (prof && threadIdx.x == 0)
-        for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
+        if (prof && threadIdx.x == 0)
+            for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
 #endif
+    }
+    __syncthreads();
+    if (replayer) {
+        wave_copy((int32_t*)&v.t->h, (const int32_t*)&zhs, (int)(sizeof(DocHdr) / 4));
+        wave_copy(tl.cord, lcord, NCH);
+        wave_copy(tl.cst, lcst, NCH);
+        wave_copy(tl.cpos, lcpos, NCH);
+        wave_copy(tl.ccnt, lccnt, NCH);
+        wave_copy(tl.wrid, lwrid, WCAP);
+        wave_copy((int32_t*)tl.wgen, (const int32_t*)lwgen, WCAP / 4);
+        wave_copy(tl.wslot, lwslot, WCAP);
+    }
 }
 
 /* K5: per-doc digest of the canonical dump */
@@ -642,8 +748,8 @@ static inline Store<HT>& store_of(mt_engine* e) {
 
 /* one replay kernel over the staged batch (a document per workgroup) */
 template <class HT, class K>
-static inline int32_t launch_replay(mt_engine* e, K kern) {
-    hipLaunchKernelGGL(kern, docs_grid(e->ndocs), dim3(WG), 0, e->stream, store_of<HT>(e), e->ndocs,
+static inline int32_t launch_replay(mt_engine* e, K kern, int block = WG) {
+    hipLaunchKernelGGL(kern, docs_grid(e->ndocs), dim3(block), 0, e->stream, store_of<HT>(e), e->ndocs,
                        (const mt_op_rec*)e->ops_buf.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
                        (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p, (const int64_t*)e->props_off.p,
                        (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p, (uint64_t*)e->prof.p);
