@@ -1729,28 +1729,36 @@ struct Replica {
     }
     /* within leaf position k (start offset P): the row t = k*8+j with P < pos <= P + vis */
     /* n: the leaf node at k (tile_find's) */
-    MT_HD int32_t leaf_find(int32_t k, int32_t n, int32_t P, int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+    /* *Sout / *Vout (optional): the row's slot and its perspective length */
+    MT_HD int32_t leaf_find(int32_t k, int32_t n, int32_t P, int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout,
+                            int32_t* Sout = nullptr, int32_t* Vout = nullptr) {
         MT_PROF_SCOPE(PH_LFIND);
-        int32_t c = nch[n];
         if constexpr (W::N >= MAXN) { /* lane j: child j; one prefix scan */
             int32_t j = w.lane();
-            int32_t v = j < c ? vis(n * MAXN + (j & (MAXN - 1)), refSeq, client) : 0;
+            int32_t s = n * MAXN + (j & (MAXN - 1));
+            RowView r = row_view(s); /* the leaf's slab is always in bounds: loaded with the child count */
+            int32_t c = nch[n];
+            int32_t v = j < c ? vis_of(s, r, refSeq, client) : 0;
             int32_t tot;
             int32_t p = P + w.excl_scan(v, &tot);
             uint64_t m = w.ballot(j < c && p < pos && pos <= p + v);
             if (m) {
                 int32_t l = W::ffs(m);
                 *Pout = w.bcast(p, l);
+                if (Sout) *Sout = n * MAXN + l;
+                if (Vout) *Vout = w.bcast(v, l);
                 return k * MAXN + l;
             }
             fail(E_ASSERT);
             return -1;
         }
-        int32_t run = P;
+        int32_t run = P, c = nch[n];
         for (int32_t j = 0; j < c; j++) {
             int32_t v = vis(n * MAXN + j, refSeq, client);
             if (run < pos && pos <= run + v) {
                 *Pout = run;
+                if (Sout) *Sout = n * MAXN + j;
+                if (Vout) *Vout = v;
                 return k * MAXN + j;
             }
             run += v;
@@ -1763,7 +1771,8 @@ struct Replica {
         return is_local(client) || refSeq >= h.minSeq;
     }
     /* find_reach by a walk over every leaf (any perspective; O(rows)) */
-    MT_HD int32_t find_reach_walk(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+    MT_HD int32_t find_reach_walk(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout, int32_t* Sout = nullptr,
+                                  int32_t* Vout = nullptr) {
         int32_t run = 0;
         for (int32_t k = 0; kvalid(k); k = knext(k)) {
             int32_t n = leaf_at(k), c = nch[n];
@@ -1771,6 +1780,8 @@ struct Replica {
                 int32_t v = vis(n * MAXN + j, refSeq, client);
                 if (run < pos && pos <= run + v) {
                     *Pout = run;
+                    if (Sout) *Sout = n * MAXN + j;
+                    if (Vout) *Vout = v;
                     return k * MAXN + j;
                 }
                 run += v;
@@ -1778,16 +1789,17 @@ struct Replica {
         }
         return -1;
     }
-    MT_HD int32_t find_reach_tiled(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+    MT_HD int32_t find_reach_tiled(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout, int32_t* Sout,
+                                   int32_t* Vout) {
         if (pos <= 0) return -1;
-        if (!tiles_cover(refSeq, client)) return find_reach_walk(pos, refSeq, client, Pout);
+        if (!tiles_cover(refSeq, client)) return find_reach_walk(pos, refSeq, client, Pout, Sout, Vout);
         win_pass(refSeq, client);
         int32_t P;
         int32_t n = 0;
         int32_t k = tile_find(pos, refSeq, client, &P, &n);
         win_clear();
         if (k < 0) return -1;
-        return leaf_find(k, n, P, pos, refSeq, client, Pout);
+        return leaf_find(k, n, P, pos, refSeq, client, Pout, Sout, Vout);
     }
     MT_HD int32_t length_tiled(int32_t refSeq, int32_t client) {
         if (!tiles_cover(refSeq, client)) {
@@ -1989,22 +2001,25 @@ struct Replica {
         return total;
     }
     /* First row (document order) with P < pos <= P + vis; returns t (lorder coordinate) or -1,
-     * and P of that row. */
-    MT_HD int32_t find_reach(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout) {
+     * and P of that row; *Sout / *Vout (optional): its slot and perspective length. */
+    MT_HD int32_t find_reach(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout, int32_t* Sout = nullptr,
+                             int32_t* Vout = nullptr) {
         MT_PROF_SCOPE(PH_FIND);
-        if constexpr (TILED) return find_reach_tiled(pos, refSeq, client, Pout);
+        if constexpr (TILED) return find_reach_tiled(pos, refSeq, client, Pout, Sout, Vout);
         int32_t run = 0;
         int32_t T = h.nleaf * MAXN;
         for (int32_t b = 0; b < T; b += 4 * W::N) {
             int32_t v[4];
-            quad_vis(quad_slot(b + 4 * w.lane()), refSeq, client, v);
+            int32_t s0 = quad_slot(b + 4 * w.lane());
+            quad_vis(s0, refSeq, client, v);
             int32_t tot;
             int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
-            int32_t hq = -1, hp = 0;
+            int32_t hq = -1, hp = 0, hv = 0;
             for (int q = 0; q < 4; q++) {
                 if (hq < 0 && p < pos && pos <= p + v[q]) {
                     hq = q;
                     hp = p;
+                    hv = v[q];
                 }
                 p += v[q];
             }
@@ -2012,6 +2027,8 @@ struct Replica {
             if (m) {
                 int32_t l = W::ffs(m);
                 *Pout = w.bcast(hp, l);
+                if (Sout) *Sout = w.bcast(s0 + hq, l);
+                if (Vout) *Vout = w.bcast(hv, l);
                 return b + 4 * l + w.bcast(hq, l);
             }
             run += tot;
@@ -3243,11 +3260,9 @@ struct Replica {
     }
     /* ensureIntervalBoundary (2274-2278): split the row strictly containing pos */
     MT_HD void ensure_boundary(int32_t pos, int32_t refSeq, int32_t client) {
-        int32_t P;
-        int32_t t = find_reach(pos, refSeq, client, &P);
+        int32_t P, s, v;
+        int32_t t = find_reach(pos, refSeq, client, &P, &s, &v);
         if (t < 0) return;
-        int32_t s = slot_at(t);
-        int32_t v = vis(s, refSeq, client);
         if (P + v > pos) split_row(t, pos - P);
     }
     /* returns the slot of the inserted row or -1 */
@@ -3261,11 +3276,9 @@ struct Replica {
             k = 0;
             j = 0;
         } else {
-            int32_t P;
-            int32_t t = find_reach(pos, refSeq, client, &P);
+            int32_t P, s, v;
+            int32_t t = find_reach(pos, refSeq, client, &P, &s, &v);
             if (t < 0) return -1;
-            int32_t s = slot_at(t);
-            int32_t v = vis(s, refSeq, client);
             if (P + v > pos && !(z.flags(s) & RF_MARKER)) {
                 int32_t ls = split_row(t, pos - P);
                 if (ls < 0) return -1;
@@ -3411,12 +3424,13 @@ struct Replica {
         }
         int32_t run = 0;
         int32_t T = h.nleaf * MAXN;
-        int32_t tf = -1, Pf = 0, vf = 0, tg = -1, Pg = 0, vg = 0;
+        int32_t tf = -1, Pf = 0, vf = 0, tg = -1, Pg = 0, vg = 0, sf = -1, sg = -1;
         {
             MT_PROF_SCOPE(PH_FIND);
             for (int32_t b = 0; b < T; b += 4 * W::N) {
                 int32_t v[4];
-                quad_vis(quad_slot(b + 4 * w.lane()), refSeq, client, v);
+                int32_t s0 = quad_slot(b + 4 * w.lane());
+                quad_vis(s0, refSeq, client, v);
                 int32_t tot;
                 int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
                 int32_t hf = -1, pf = 0, lf = 0, hl = -1, pl = 0, ll = 0;
@@ -3438,11 +3452,13 @@ struct Replica {
                     if (tf < 0) {
                         int32_t l = W::ffs(m);
                         tf = b + 4 * l + w.bcast(hf, l);
+                        sf = w.bcast(s0 + hf, l);
                         Pf = w.bcast(pf, l);
                         vf = w.bcast(lf, l);
                     }
                     int32_t l2 = 63 - __builtin_clzll(m);
                     tg = b + 4 * l2 + w.bcast(hl, l2);
+                    sg = w.bcast(s0 + hl, l2);
                     Pg = w.bcast(pl, l2);
                     vg = w.bcast(ll, l2);
                 }
@@ -3451,30 +3467,34 @@ struct Replica {
             }
         }
         if (tf < 0) return;
-        int32_t ridLast = z.rid[slot_at(tg)];
-        int32_t ridFirst = z.rid[slot_at(tf)];
-        if (Pf < start) { /* start falls inside the first row: split it; its right part is first */
-            int32_t rs = -1;
-            if (split_row(tf, start - Pf, &rs) < 0 || rs < 0) return;
-            if (tf == tg) {
-                ridLast = z.rid[rs];
-                vg = Pf + vf - start;
-                Pg = start;
+        int32_t sa = sf, sb = sg; /* no split: the rows stay where the scan found them */
+        if (Pf < start || Pg + vg > end) {
+            int32_t ridLast = z.rid[sg];
+            int32_t ridFirst = z.rid[sf];
+            if (Pf < start) { /* start falls inside the first row: split it; its right part is first */
+                int32_t rs = -1;
+                if (split_row(tf, start - Pf, &rs) < 0 || rs < 0) return;
+                if (tf == tg) {
+                    ridLast = z.rid[rs];
+                    vg = Pf + vf - start;
+                    Pg = start;
+                }
+                ridFirst = z.rid[rs];
             }
-            ridFirst = z.rid[rs];
-        }
-        if (Pg + vg > end) { /* end falls inside the last row: split it; its left part keeps the id */
-            int32_t sg = slot_of(ridLast, -1);
-            if (sg < 0) {
+            if (Pg + vg > end) { /* end falls inside the last row: split it; its left part keeps the id */
+                int32_t sl = slot_of(ridLast, -1);
+                if (sl < 0) {
+                    fail(E_ASSERT);
+                    return;
+                }
+                if (split_row(kpos(sl / MAXN) * MAXN + (sl & (MAXN - 1)), end - Pg) < 0) return;
+            }
+            sa = slot_of(ridFirst, -1);
+            sb = slot_of(ridLast, -1);
+            if (sa < 0 || sb < 0) {
                 fail(E_ASSERT);
                 return;
             }
-            if (split_row(kpos(sg / MAXN) * MAXN + (sg & (MAXN - 1)), end - Pg) < 0) return;
-        }
-        int32_t sa = slot_of(ridFirst, -1), sb = slot_of(ridLast, -1);
-        if (sa < 0 || sb < 0) {
-            fail(E_ASSERT);
-            return;
         }
         if (dl) { /* delta events need each visited row's position: the serial visit */
             visit_run(sa, sb, refSeq, client, leaf, true);
@@ -3509,7 +3529,7 @@ struct Replica {
      * two splits; then the rows with length > 0 between them are visited leaf by leaf. */
     template <class F>
     MT_HD void range_op_tiled(int32_t start, int32_t end, int32_t refSeq, int32_t client, F& leaf, bool dl) {
-        int32_t tf, Pf, tg, Pg;
+        int32_t tf, Pf, tg, Pg, sf = -1, vf = 0, sg = -1, vg = 0;
         if (tiles_cover(refSeq, client)) {
             int32_t total = win_pass(refSeq, client);
             int32_t nc = z.tl.nchunk;
@@ -3531,18 +3551,21 @@ struct Replica {
                 fail(E_ASSERT);
                 return;
             }
-            tf = leaf_find(k1, n1, P1, start + 1, refSeq, client, &Pf);
-            tg = leaf_find(k2, n2, P2, last, refSeq, client, &Pg);
+            tf = leaf_find(k1, n1, P1, start + 1, refSeq, client, &Pf, &sf, &vf);
+            tg = leaf_find(k2, n2, P2, last, refSeq, client, &Pg, &sg, &vg);
         } else {
             int32_t total = length_tiled(refSeq, client);
             if (start >= total || end <= start) return;
-            tf = find_reach_walk(start + 1, refSeq, client, &Pf);
-            tg = find_reach_walk(end < total ? end : total, refSeq, client, &Pg);
+            tf = find_reach_walk(start + 1, refSeq, client, &Pf, &sf, &vf);
+            tg = find_reach_walk(end < total ? end : total, refSeq, client, &Pg, &sg, &vg);
         }
         if (tf < 0 || tg < 0) return;
-        int32_t vf = vis(slot_at(tf), refSeq, client), vg = vis(slot_at(tg), refSeq, client);
-        int32_t ridLast = z.rid[slot_at(tg)];
-        int32_t ridFirst = z.rid[slot_at(tf)];
+        if (Pf >= start && Pg + vg <= end) { /* no split: the rows stay where the searches found them */
+            visit_run(sf, sg, refSeq, client, leaf, dl);
+            return;
+        }
+        int32_t ridLast = z.rid[sg];
+        int32_t ridFirst = z.rid[sf];
         if (Pf < start) {
             int32_t rs = -1;
             if (split_row(tf, start - Pf, &rs) < 0 || rs < 0) return;
@@ -3554,12 +3577,12 @@ struct Replica {
             ridFirst = z.rid[rs];
         }
         if (Pg + vg > end) {
-            int32_t sg = slot_of(ridLast, -1);
-            if (sg < 0) {
+            int32_t sl = slot_of(ridLast, -1);
+            if (sl < 0) {
                 fail(E_ASSERT);
                 return;
             }
-            if (split_row(kpos(sg / MAXN) * MAXN + (sg & (MAXN - 1)), end - Pg) < 0) return;
+            if (split_row(kpos(sl / MAXN) * MAXN + (sl & (MAXN - 1)), end - Pg) < 0) return;
         }
         int32_t sa = slot_of(ridFirst, -1), sb = slot_of(ridLast, -1);
         if (sa < 0 || sb < 0) {
@@ -4303,11 +4326,11 @@ struct Replica {
      * with pos < length: the first row with P <= pos < P + vis); *off = pos - P. -1 if none. */
     MT_HD int32_t containing(int32_t pos, int32_t refSeq, int32_t client, int32_t* off) {
         if (pos < 0) return -1;
-        int32_t P = 0;
-        int32_t t = find_reach(pos + 1, refSeq, client, &P);
+        int32_t P = 0, s = -1;
+        int32_t t = find_reach(pos + 1, refSeq, client, &P, &s);
         if (t < 0) return -1;
         *off = pos - P;
-        return slot_at(t);
+        return s;
     }
     /* getPosition: the summed perspective lengths of every row before slot s in document order */
     /* the index of slot s in walkAllSegments order (the canonical dump's record index): every row before it */

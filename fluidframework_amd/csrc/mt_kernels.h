@@ -204,7 +204,8 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
  * the per-leaf rope links and the zamboni heap stay in HBM (~0.2 GB per 1M-op document; an LDS copy of
  * the heap measured no faster). */
 #ifndef MT_PF_HELPERS
-#define MT_PF_HELPERS 1 /* prefetch helper waves per config-4 document (0: one wave per document) */
+#define MT_PF_HELPERS 0 /* prefetch helper waves per config-4 document (0: one wave per document; 1 and 2
+                           * measured 2.4 % and 3.2 % slower at 256 x 300k, profiles/r04f_ab) */
 #endif
 #ifndef MT_PF_AHEAD
 #define MT_PF_AHEAD 2 /* records ahead of the replaying wave each helper looks */

@@ -1669,20 +1669,13 @@ static int seqNumberLocal(mto_client* c) { /* getLocalSequenceNumber (952-960) *
     return c->cw.collaborating ? UnassignedSequenceNumber : UniversalSequenceNumber;
 }
 
-/* applyInsertOp / applyRemoveRangeOp / applyAnnotateRangeOp (client.ts:321-442) */
-static void applyOp(mto_client* c, const mt_op_rec* op, int isLocal, int clientId, int refSeq, int seq) {
+/* the MergeTree call of an edit record: insertSegments (mergeTree.ts:2001-2040), markRangeRemoved
+ * (2640-2752) or annotateRange (2598-2638) */
+static void applyEdit(mto_client* c, const mt_op_rec* op, int clientId, int refSeq, int seq) {
     int kind = op->kind & MT_OP_KIND_MASK;
     int start = op->pos1, end = op->pos2;
-    if (isLocal) { /* getValidOpRange (486-548) */
-        int length = c->root->hdr.cachedLength;
-        int bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
-        if (kind != MT_OP_INSERT && end <= start) bad = 1;
-        if (bad) return; /* logs InvalidOpRange and returns undefined: the op has no effect */
-    }
     if (kind == MT_OP_INSERT) {
-        Seg* s = specToSegment(c, op);
-        if (isLocal && s->hdr.cachedLength <= 0) return; /* insertSegmentLocal (202-205) */
-        insertSegments(c, start, s, refSeq, clientId, seq);
+        insertSegments(c, start, specToSegment(c, op), refSeq, clientId, seq);
     } else if (kind == MT_OP_REMOVE) {
         markRangeRemoved(c, start, end, refSeq, clientId, seq);
     } else if (kind == MT_OP_ANNOTATE) {
@@ -1696,6 +1689,20 @@ static void applyOp(mto_client* c, const mt_op_rec* op, int isLocal, int clientI
         }
         annotateRange(c, start, end, kv, nkv, rw, refSeq, clientId, seq);
     }
+}
+/* applyInsertOp / applyRemoveRangeOp / applyAnnotateRangeOp (client.ts:321-442) */
+static void applyOp(mto_client* c, const mt_op_rec* op, int isLocal, int clientId, int refSeq, int seq) {
+    int kind = op->kind & MT_OP_KIND_MASK;
+    int start = op->pos1, end = op->pos2;
+    if (isLocal) { /* getValidOpRange (486-548) */
+        int length = c->root->hdr.cachedLength;
+        int bad = start < 0 || start > length || (start == length && kind != MT_OP_INSERT);
+        if (kind != MT_OP_INSERT && end <= start) bad = 1;
+        if (bad) return; /* logs InvalidOpRange and returns undefined: the op has no effect */
+        /* insertSegmentLocal (202-205): an empty segment is not inserted */
+        if (kind == MT_OP_INSERT && op->seg_kind != MT_SEG_MARKER && op->text_len <= 0) return;
+    }
+    applyEdit(c, op, clientId, refSeq, seq);
     if (!isLocal) { /* completeAndLogOp asserts (462-465) */
         if (!(c->cw.currentSeq < seq)) FAIL(c, MTO_ERR_ASSERT);
         if (!(c->cw.minSeq <= op->min_seq)) FAIL(c, MTO_ERR_ASSERT);
@@ -1770,6 +1777,17 @@ int mto_apply(mto_client* c, const mt_op_rec* op, const uint16_t* text, const mt
     c->propsPool = props;
     c->kvPool = kv;
     int kind = op->kind & MT_OP_KIND_MASK;
+    if (op->kind & MT_OPF_TREE) { /* a MergeTree-level call with explicit (refSeq, clientId, seq) (mt_oplog.h):
+                                    * no getValidOpRange, no ack, no updateSeqNumbers */
+        if (op->client == MT_CLIENT_NONCOLLAB || (op->kind & MT_OPF_LOCAL) || kind > MT_OP_ANNOTATE ||
+            (kind == MT_OP_INSERT && op->seg_kind != MT_SEG_MARKER && op->text_len == 0)) {
+            FAIL(c, MTO_ERR_UNSUPPORTED);
+            return c->err;
+        }
+        int sid = op->client == MT_CLIENT_LOCAL ? LocalClientId : getOrAddShortClientId(c, op->client);
+        applyEdit(c, op, sid, op->ref_seq, op->seq);
+        return c->err;
+    }
     if (op->kind & MT_OPF_LOCAL) {
         applyOp(c, op, 1, c->cw.clientId, c->cw.currentSeq, seqNumberLocal(c));
         return c->err;

@@ -42,6 +42,16 @@ def test_host_core_tree_records_match_reference(name):
     assert np.array_equal(dig, z["digests"])
 
 
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_tree_records_match_reference(name):
+    """the oracle restates the MergeTree-level calls too (mt_oracle.c applyEdit): pinned by the same fixtures"""
+    import oracle_client as oc
+    z, _, b = load(name)
+    _, dig, err = oc.replay_batch(b, threads=8)
+    assert (err == 0).all()
+    assert np.array_equal(dig, z["digests"])
+
+
 def test_tree_record_flag_rules():
     """a TREE record that is also LOCAL, or an empty text insert, latches MT_E_UNSUPPORTED"""
     from fluidframework_amd import oplog as ol
@@ -52,6 +62,9 @@ def test_tree_record_flag_rules():
     b = ol.Batch.from_logs([L])
     dig, err, st = core_host.replay_batch(b)
     assert err[0] == 4 and st.error_op(0) == 2
+    import oracle_client as oc
+    o = oc.OracleClient(L.interner)
+    assert o.replay(L) == 4  # MTO_ERR_UNSUPPORTED at the same record
 
 
 @pytest.mark.gpu
