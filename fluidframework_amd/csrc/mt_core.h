@@ -372,7 +372,11 @@ struct Pools {
  * cycles accumulated per phase in registers and written out per document. */
 enum { PH_APPLY, PH_ZAMBONI, PH_FIND, PH_MAP, PH_SPLIT, PH_ACK, PH_TEXT, PH_HEAP, PH_SCOUR, PH_PACK, PH_APPEND,
        PH_CAND, PH_S1, PH_S2, PH_S3, PH_P1, PH_P2, PH_INSROW, PH_LEAFINS,
-       PH_WIN, PH_TFIND, PH_LFIND, PH_ROPE, PH_RESTAT, PH_N }; /* the last five: tiled profile */
+       PH_WIN, PH_TFIND, PH_LFIND, PH_ROPE, PH_RESTAT, /* tiled profile */
+       PH_VISIT, PH_PLACE, /* a range op's visit; an insert's row set-up after placement */
+       PH_C_INS, PH_C_RANGE, PH_C_WROWS, PH_C_WMISS, PH_C_SCOUR, PH_C_PACK, /* event counts, not cycles */
+       PH_C_HEAPN, PH_C_POP, PH_C_PUSH,
+       PH_N };
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {
     uint64_t* acc;
@@ -381,8 +385,10 @@ struct ProfScope {
     __device__ ~ProfScope() { *acc += __builtin_amdgcn_s_memtime() - t0; }
 };
 #define MT_PROF_SCOPE(i) ProfScope _ps##i(&prof[i])
+#define MT_PROF_COUNT(i, n) (prof[i] += (uint64_t)(n))
 #else
 #define MT_PROF_SCOPE(i)
+#define MT_PROF_COUNT(i, n)
 #endif
 
 /* ------------------------------------------------------------------------------------------
@@ -441,7 +447,12 @@ struct Replica {
     int32_t* twslot;
     int64_t cur; /* index of the record being applied in the current Pools (snapshot reload reads ahead) */
     int32_t* pfcur = nullptr; /* tiled kernel: where the prefetch helper waves read `cur` (LDS) */
+    /* an upper bound of every maxSeq in the zamboni heap (INT32_MAX: unknown), set when a replay starts: an
+     * entry at or above it cannot move up, so heap_add appends it without reading its ancestors */
+    int32_t hmax = INT32_MAX;
     int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
+    bool runOnly = false;      /* range_op_tiled: find and split only, leaving the run's first / last slot in */
+    int32_t runA = -1, runB = -1; /* runA / runB for remove_run (no visit) */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
         : d(doc), z(*doc.t), w(wave), zh(&z.h), l2s(z.l2s), s2l(z.s2l), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
@@ -1281,7 +1292,8 @@ struct Replica {
             return -1;
         }
         int32_t j = w.lane();
-        uint64_t m = w.ballot(j < c && z.rid[leaf * MAXN + (j & (MAXN - 1))] == rid);
+        int32_t r = z.rid[leaf * MAXN + (j & (MAXN - 1))]; /* with the child count: one round trip */
+        uint64_t m = w.ballot(j < c && r == rid);
         return m ? leaf * MAXN + W::ffs(m) : -1;
     }
 
@@ -1582,6 +1594,11 @@ struct Replica {
                 lc[q] = t.lch[l];
                 lx[q] = t.lix[l];
                 if (!hit) s[q] = gok ? -2 : -1; /* -2: look the row up */
+            }
+#pragma unroll
+            for (int q = 0; q < NB; q++) {
+                MT_PROF_COUNT(PH_C_WROWS, __builtin_popcountll(w.ballot(b0 + q * W::N + w.lane() < n)));
+                MT_PROF_COUNT(PH_C_WMISS, __builtin_popcountll(w.ballot(s[q] == -2)));
             }
 #pragma unroll
             for (int q = 0; q < NB; q++) { /* the rows that moved: leaf, slot, row */
@@ -2360,10 +2377,22 @@ struct Replica {
             fail(E_CAPACITY);
             return;
         }
+        MT_PROF_COUNT(PH_C_PUSH, 1);
         int32_t k = n + 1; /* L[k] (1-based) lives at index k-1 */
         h.heapN = n + 1;
         if (n + 1 > zh->hwHeap) zh->hwHeap = n + 1;
         uint8_t gen = z.rgen[rid];
+        if (seq >= hmax) { /* every ancestor's maxSeq <= hmax <= seq: the fixup moves nothing (collections.ts:240-247) */
+            hmax = seq;
+            if (w.lane() == 0) {
+                hrd[n] = (IX)rid;
+                hsq[n] = seq;
+                hgn[n] = gen;
+            }
+            w.sync();
+            if (n == 0) zh->heapTop = seq;
+            return;
+        }
         if constexpr (W::N >= 32) {
             int32_t l = w.lane();
             int32_t a = l < 31 ? (k >> (l + 1)) : 0; /* ancestor l+1 (0 = none) */
@@ -2402,18 +2431,24 @@ struct Replica {
             zh->heapTop = hsq[0];
         }
     }
-    /* Heap.get (collections.ts:227-233) + fixdown (249-263). On the GPU every maxSeq is read in one
-     * pass (lane = index mod 64, one register per 64 entries), the descent is taken on scalars, and
-     * the entries on the path move up one level in one parallel pass. */
+    /* Heap.get (collections.ts:227-233) + fixdown (249-263). On the GPU, for a heap of at most 256
+     * entries, every entry is read in one pass (lane = index mod 64, one register per 64 entries and
+     * field), the descent is taken on scalars, and the entries on the path move up one level in one
+     * parallel pass whose values come from those registers (lane shuffles): one round trip per pop. */
     MT_HD void heap_pop(int32_t* rid, int32_t* seq, int32_t* gen) {
         MT_PROF_SCOPE(PH_HEAP);
+        MT_PROF_COUNT(PH_C_POP, 1);
         int32_t cnt = h.heapN;
-        if constexpr (W::N == 64 && HT::H <= 256) {
+        if (W::N == 64 && (HT::H <= 256 || cnt <= 256)) {
             int32_t l = w.lane();
             int32_t c0 = l < cnt ? hsq[l] : 0;
             int32_t c1 = 64 + l < cnt ? hsq[64 + l] : 0;
             int32_t c2 = 128 + l < cnt ? hsq[128 + l] : 0;
             int32_t c3 = 192 + l < cnt ? hsq[192 + l] : 0;
+            int32_t r0 = l < cnt ? (int32_t)hrd[l] : 0, g0 = l < cnt ? hgn[l] : 0;
+            int32_t r1 = 64 + l < cnt ? (int32_t)hrd[64 + l] : 0, g1 = 64 + l < cnt ? hgn[64 + l] : 0;
+            int32_t r2 = 128 + l < cnt ? (int32_t)hrd[128 + l] : 0, g2 = 128 + l < cnt ? hgn[128 + l] : 0;
+            int32_t r3 = 192 + l < cnt ? (int32_t)hrd[192 + l] : 0, g3 = 192 + l < cnt ? hgn[192 + l] : 0;
             int32_t last = cnt - 1; /* index of the entry that moves to the root */
             IX xr = hrd[last];
             uint8_t xg = hgn[last];
@@ -2447,20 +2482,21 @@ struct Replica {
                 k = j;
             }
             /* lane t < d: the entry at path[t] moves to its parent (path[t-1], or the root) */
-            int32_t src = 0, dst = 0;
+            int32_t src = 1, dst = 0;
             for (int32_t t = 0; t < 8; t++)
                 if (t == l && t < d) {
                     src = path[t];
                     dst = t == 0 ? 1 : path[t - 1];
                 }
-            IX mr = 0;
-            uint8_t mg = 0;
-            int32_t ms = 0;
-            if (l < d) {
-                mr = hrd[src - 1];
-                mg = hgn[src - 1];
-                ms = hsq[src - 1];
-            }
+            /* its fields from the registers of the first pass (every lane active: the shuffles read other lanes) */
+            int32_t sx = src - 1, sl = sx & 63, sc = sx >> 6;
+            auto pick = [&](int32_t v0, int32_t v1, int32_t v2, int32_t v3) -> int32_t {
+                int32_t a0 = w.shfl(v0, sl), a1 = w.shfl(v1, sl), a2 = w.shfl(v2, sl), a3 = w.shfl(v3, sl);
+                return sc == 0 ? a0 : sc == 1 ? a1 : sc == 2 ? a2 : a3;
+            };
+            IX mr = (IX)pick(r0, r1, r2, r3);
+            uint8_t mg = (uint8_t)pick(g0, g1, g2, g3);
+            int32_t ms = pick(c0, c1, c2, c3);
             w.sync();
             if (l < d) {
                 hrd[dst - 1] = mr;
@@ -2798,7 +2834,9 @@ struct Replica {
      * fields (v_readlane), with cold data (props values, the trailing character) read only for a
      * candidate pair; the frees and the slab compaction are again one parallel pass. cnt[i] gets the
      * new child count of leaf i. Same result as scour_leaf on each leaf in turn. */
-    MT_HD void scour_par(const int32_t* leaves, int32_t nl, int32_t* cnt) {
+    /* pre (one leaf): lanes < 8 hold its rows and preC its child count, read by the caller */
+    MT_HD void scour_par(const int32_t* leaves, int32_t nl, int32_t* cnt, const HotRow* pre = nullptr,
+                         int32_t preC = 0) {
         MT_PROF_SCOPE(PH_SCOUR);
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
         uint64_t _t0 = __builtin_amdgcn_s_memtime();
@@ -2808,10 +2846,10 @@ struct Replica {
         int32_t n = -1;
         for (int32_t i = 0; i < MAXN; i++)
             if (i == li && i < nl) n = leaves[i];
-        int32_t c = n >= 0 ? nch[n] : 0;
+        int32_t c = n >= 0 ? (pre ? preC : nch[n]) : 0;
         bool valid = j < c;
         HotRow r = {};
-        if (valid) r = load_row(n * MAXN + j);
+        if (valid) r = pre ? *pre : load_row(n * MAXN + j);
         int32_t minSeq = h.minSeq;
         /* 0: no row; 1: held, resets prevSegment; 2: unlinked, resets prevSegment; 3: merge candidate */
         int32_t code = 0;
@@ -3167,15 +3205,38 @@ struct Replica {
             if (zh->heapTop > h.minSeq) break; /* peek (mergeTree.ts:1465-1468) */
             int32_t rid, mseq, gen;
             heap_pop(&rid, &mseq, &gen);
-            int32_t s = slot_of(rid, gen); /* -1: unlinked or merged away since it was queued */
-            if (s < 0) continue;
-            int32_t n = s / MAXN;
-            if (nsc[n] == 0) continue;
-            int32_t before = nch[n];
-            int32_t after = scour_one(n);
+            int32_t n, before, after, par;
+            if constexpr (W::N >= MAXN * MAXN) {
+                /* slot_of, needsScour and scourNode's row reads in two round trips: the row's leaf, then
+                 * everything about that leaf */
+                int32_t g = z.rgen[rid];
+                n = z.rleaf[rid];
+                if (g != (uint8_t)gen) continue; /* unlinked since it was queued */
+                int32_t j = w.lane();
+                HotRow r = load_row(n * MAXN + (j & (MAXN - 1)));
+                before = nch[n];
+                int32_t sc = nsc[n];
+                par = npar[n];
+                if (!w.ballot(j < before && r.rid == (IX)rid)) continue; /* merged away since it was queued */
+                if (sc == 0) continue;
+                MT_PROF_COUNT(PH_C_SCOUR, 1);
+                int32_t cnt1[1];
+                scour_par(&n, 1, cnt1, &r, before);
+                after = cnt1[0];
+            } else {
+                int32_t s = slot_of(rid, gen); /* -1: unlinked or merged away since it was queued */
+                if (s < 0) continue;
+                n = s / MAXN;
+                if (nsc[n] == 0) continue;
+                before = nch[n];
+                MT_PROF_COUNT(PH_C_SCOUR, 1);
+                after = scour_one(n);
+                par = npar[n];
+            }
             nsc[n] = 0;
             if (after < before) {
-                if (after < MAXN / 2 && npar[n] >= 0) pack(n);
+                MT_PROF_COUNT(PH_C_PACK, after < MAXN / 2 && par >= 0);
+                if (after < MAXN / 2 && par >= 0) pack(n);
             }
         }
     }
@@ -3271,6 +3332,7 @@ struct Replica {
      * at pos if pos falls strictly inside it; placement then resumes right after its left part. */
     MT_HD int32_t insert_row(int32_t pos, int32_t refSeq, int32_t client, int32_t seq) {
         MT_PROF_SCOPE(PH_INSROW);
+        MT_PROF_COUNT(PH_C_INS, 1);
         int32_t k, j;
         if (pos == 0) {
             k = 0;
@@ -3336,6 +3398,7 @@ struct Replica {
                 fail(E_INSERT_FAILED);
                 return;
             }
+            MT_PROF_SCOPE(PH_PLACE);
             int32_t rid = alloc_rid();
             z.rid[s] = (IX)rid;
             typename HT::Cold& c = d.cold()[rid]; /* row id kept in a register, not re-read per field */
@@ -3402,6 +3465,7 @@ struct Replica {
      * after its own visit (a REMOVE drops a visited row's; an ANNOTATE changes none). */
     template <class F>
     MT_HD void visit_run(int32_t sa, int32_t sb, int32_t refSeq, int32_t client, F& leaf, bool dl) {
+        MT_PROF_SCOPE(PH_VISIT);
         int32_t run = dl ? local_pos(sa) : 0;
         int32_t ka = kpos(sa / MAXN), kb = kpos(sb / MAXN);
         for (int32_t k = ka;; k = knext(k)) {
@@ -3418,6 +3482,7 @@ struct Replica {
     template <class F>
     MT_HD void range_op(int32_t start, int32_t end, int32_t refSeq, int32_t client, F&& leaf, bool dl = false) {
         MT_PROF_SCOPE(PH_MAP);
+        MT_PROF_COUNT(PH_C_RANGE, 1);
         if constexpr (TILED) {
             range_op_tiled(start, end, refSeq, client, leaf, dl);
             return;
@@ -3561,6 +3626,11 @@ struct Replica {
         }
         if (tf < 0 || tg < 0) return;
         if (Pf >= start && Pg + vg <= end) { /* no split: the rows stay where the searches found them */
+            if (runOnly) {
+                runA = sf;
+                runB = sg;
+                return;
+            }
             visit_run(sf, sg, refSeq, client, leaf, dl);
             return;
         }
@@ -3589,7 +3659,101 @@ struct Replica {
             fail(E_ASSERT);
             return;
         }
+        if (runOnly) {
+            runA = sa;
+            runB = sb;
+            return;
+        }
         visit_run(sa, sb, refSeq, client, leaf, dl);
+    }
+    /* markRangeRemoved's per-segment step (mergeTree.ts:2660-2700, the range_edit callback below) on the rows with
+     * vis > 0 from slot sa to slot sb, a leaf at a time with one lane per row (tiled profile, no delta events, no
+     * local references): every row's fields are read in one pass and the row updates are made in parallel; the
+     * steps whose order is observable — overlap-list pushes, window-set appends, the leaf's LRU entry (added by
+     * its first such row), pending-group entries — are taken in row order. Same result as the serial visit. */
+    MT_HD void remove_run(int32_t sa, int32_t sb, int32_t refSeq, int32_t client, int32_t seq, int32_t localSeq,
+                          bool hasL, uint32_t rcl, bool collab, bool* created) {
+        MT_PROF_SCOPE(PH_VISIT);
+        static_assert(W::N >= MAXN * MAXN, "one lane per row of a leaf");
+        auto& t = z.tl;
+        const int32_t j = w.lane();
+        const uint64_t below = j ? (~0ull >> (64 - j)) : 0ull;
+        int32_t ka = kpos(sa / MAXN), kb = kpos(sb / MAXN);
+        for (int32_t k = ka;; k = knext(k)) {
+            int32_t n = leaf_at(k);
+            int32_t s = n * MAXN + (j & (MAXN - 1));
+            RowView r = row_view(s); /* the row, its window flags and id, the leaf's child count: one round trip */
+            uint8_t x = t.xf[s];
+            int32_t rid = z.rid[s];
+            int32_t c = nch[n];
+            int32_t j0 = k == ka ? (sa & (MAXN - 1)) : 0;
+            int32_t j1 = k == kb ? (sb & (MAXN - 1)) : c - 1;
+            bool sel = j < MAXN && j >= j0 && j <= j1 && vis_of(s, r, refSeq, client) > 0;
+            int32_t rs = r.rseq, L = r.len;
+            uint32_t b4 = r.b4, fl = (b4 >> 16) & 0xFF;
+            bool fresh = sel && rs == NOREM, unas = sel && rs == UNASSIGNED_SEQ;
+            int32_t nrs = fresh || unas ? seq : rs; /* rs after the update */
+            uint64_t sm = w.ballot(sel);
+            zh->sumW += __builtin_popcountll(sm);
+            h.localLen -= w.sum(fresh ? L : 0); /* the rows leave the local view */
+            if (fresh) {
+                z.rseq(s) = seq;
+                cold(s).lrseq = localSeq;
+                uint32_t f2 = hasL ? (fl | RF_LRSEQ) : (fl & ~(uint32_t)RF_LRSEQ);
+                st_bytes4(s, (b4 & 0xFF0000FFu) | (rcl << 8) | (f2 << 16));
+            } else if (unas) {
+                z.rseq(s) = seq;
+                st_bytes4(s, (b4 & 0xFF0000FFu) | (rcl << 8) | ((fl & ~(uint32_t)RF_LRSEQ) << 16));
+            }
+            uint64_t om = sm & ~w.ballot(fresh || unas);
+            while (om) { /* removed already by another client: removedClientOverlap (rare) */
+                int32_t l = W::ffs(om);
+                om &= om - 1;
+                int32_t sl = w.bcast(s, l);
+                uint32_t bl = (uint32_t)w.bcast((int32_t)b4, l);
+                ovl_push(sl, client);
+                st_bytes4(sl, (bl & 0xFF00FFFFu) | ((((bl >> 16) & 0xFF) | RF_OVL) << 16));
+            }
+            /* row_removed: out of the STABLE summaries; into the window set unless the removal is settled */
+            bool stable = sel && (x & XF_STABLE);
+            int32_t lsd = w.sum(stable ? L : 0);
+            uint8_t x2 = stable ? 0 : x;
+            bool st = r.seq != UNASSIGNED_SEQ && r.seq <= h.minSeq &&
+                      (nrs == NOREM || (nrs != UNASSIGNED_SEQ && nrs <= h.minSeq));
+            bool wadd = sel && !(x2 & XF_W) && !st;
+            if (wadd) x2 = XF_W;
+            uint8_t g = wadd ? z.rgen[rid] : 0;
+            if (sel) t.xf[s] = x2;
+            if (lsd) lst_add(n, -lsd);
+            uint64_t wm = w.ballot(wadd);
+            if (wm) {
+                int32_t wn = t.wN, cnt = __builtin_popcountll(wm);
+                if (wn + cnt > HT::TL::WCAP) {
+                    fail(E_CAPACITY);
+                    return;
+                }
+                if (wadd) {
+                    int32_t o = wn + __builtin_popcountll(wm & below);
+                    twrid[o] = rid;
+                    twgen[o] = g;
+                    twslot[o] = s;
+                }
+                w.sync();
+                t.wN = wn + cnt;
+            }
+            if (collab) {
+                bool pend = (fresh || unas) && seq == UNASSIGNED_SEQ && client == h.localShort;
+                uint64_t pm = w.ballot(pend);
+                while (pm) {
+                    int32_t l = W::ffs(pm);
+                    pm &= pm - 1;
+                    pending_add(w.bcast(s, l), localSeq, created);
+                }
+                uint64_t lm = sm & ~w.ballot(pend);
+                if (lm) add_lru(w.bcast(s, W::ffs(lm)), seq); /* the leaf's first: add_lru marks the leaf */
+            }
+            if (k == kb || !kvalid(knext(k))) break;
+        }
     }
 
     /* markRangeRemoved (2640-2752) and annotateRange (2598-2638) share one range walk (range_op is inlined once
@@ -3614,6 +3778,22 @@ struct Replica {
         const bool rf = refs_on();
         bool saved = false;
         const int32_t dop = remove ? MT_DELTA_REMOVE : MT_DELTA_ANNOTATE;
+        if constexpr (TILED && W::N >= MAXN * MAXN) {
+            if (remove && !dl && !rf) { /* find and split, then the lane-parallel visit */
+                auto none = [](int32_t, int32_t) {};
+                runOnly = true;
+                runA = -1;
+                {
+                    MT_PROF_SCOPE(PH_MAP);
+                    MT_PROF_COUNT(PH_C_RANGE, 1);
+                    range_op_tiled(start, end, refSeq, client, none, false);
+                }
+                runOnly = false;
+                if (runA >= 0 && !h.err) remove_run(runA, runB, refSeq, client, seq, localSeq, hasL, rcl, collab, &created);
+                if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni_soon();
+                return;
+            }
+        }
         range_op(start, end, refSeq, client, [&](int32_t s, int32_t dpos) {
             if (dl && !dh) {
                 dhead(dop);
@@ -3930,6 +4110,7 @@ struct Replica {
         MT_PROF_SCOPE(PH_APPLY);
         if (h.err) return;
         int32_t at = h.opsDone;
+        MT_PROF_COUNT(PH_C_HEAPN, h.heapN);
         apply_record(op, p);
         run_zamboni();
         if (h.err) zh->errOp = at;
@@ -4499,6 +4680,12 @@ struct Replica {
      * round trip per W::N events instead of one per event. */
     MT_HD void replay(const Pools& p) {
         static_assert(sizeof(mt_op_rec) == 32, "op record is 8 dwords");
+        hmax = INT32_MIN; /* the heap's largest maxSeq */
+        for (int32_t b = 0; b < h.heapN; b += W::N) {
+            int32_t i = b + w.lane();
+            int32_t m = w.max(i < h.heapN ? hsq[i] : INT32_MIN);
+            if (m > hmax) hmax = m;
+        }
         for (int64_t b = 0; b < p.nops; b += W::N) {
             int64_t i = b + w.lane();
             int32_t rec[8] = {0, 0, 0, 0, 0, 0, 0, 0};

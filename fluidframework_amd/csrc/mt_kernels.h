@@ -201,8 +201,9 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
  * itself (155 KB): the position-search scratch (per-chunk window deltas, all zero between searches, and each
  * window row's chunk position / leaf index / perspective length) and, for the duration of the replay, the
  * rope's chunk arrays and the window set (with each row's last-seen slot). The rows, the leaf summaries,
- * the per-leaf rope links and the zamboni heap stay in HBM (~0.2 GB per 1M-op document; an LDS copy of
- * the heap measured no faster). */
+ * the per-leaf rope links and the zamboni heap stay in HBM (~0.2 GB per 1M-op document). An LDS copy of the
+ * heap (~60 entries in use at lag 64) measured slower: a heap that can be in either memory is reached through
+ * flat accesses, which wait for both counters (r04j A/B: 10.75 -> 10.33M ops/s at 256 x 300k). */
 #ifndef MT_PF_HELPERS
 #define MT_PF_HELPERS 0 /* prefetch helper waves per config-4 document (0: one wave per document; 1 and 2
                            * measured 2.4 % and 3.2 % slower at 256 x 300k, profiles/r04f_ab) */

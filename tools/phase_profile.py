@@ -10,8 +10,10 @@ sys.path.insert(0, ROOT)
 from fluidframework_amd import native
 
 PHASES = ["APPLY", "ZAMBONI", "FIND", "MAP", "SPLIT", "ACK", "TEXT", "HEAP", "SCOUR", "PACK", "APPEND", "CAND", "S1load", "S2walk", "S3compact", "P1leaf", "P2interior", "INSROW", "LEAFINS",
-          "WIN", "TFIND", "LFIND", "ROPE", "RESTAT"]
-LIB = native.lib_path("libmtreplay_prof.so")
+          "WIN", "TFIND", "LFIND", "ROPE", "RESTAT", "VISIT", "PLACE",
+          "#ins", "#range", "#winrows", "#winmiss", "#scour", "#pack",
+          "#heapsize", "#pop", "#push"]
+LIB = os.environ.get("MT_PROF_LIB") or native.lib_path("libmtreplay_prof.so")  # MT_PROF_LIB: a prebuilt copy
 
 
 def build():
@@ -47,7 +49,14 @@ def main():
     ev = b.nops
     print(f"config {a.config} docs {b.ndocs} events {ev} kernel {eng.last_run_ms:.1f} ms")
     for i, n in enumerate(PHASES):
-        print(f"{n:8s} {tot[i] / ev:10.0f} cycles/event  {100 * tot[i] / tot[0]:5.1f}% of APPLY")
+        if n.startswith("#"):  # event counts
+            print(f"{n:8s} {tot[i] / ev:10.3f} per event")
+        else:
+            print(f"{n:8s} {tot[i] / ev:10.0f} cycles/event  {100 * tot[i] / tot[0]:5.1f}% of APPLY")
+    ci, cr = tot[PHASES.index("#ins")], tot[PHASES.index("#range")]
+    if ci and cr:
+        print(f"per insert: INSROW {tot[PHASES.index('INSROW')] / ci:.0f} PLACE {tot[PHASES.index('PLACE')] / ci:.0f}; "
+              f"per range op: MAP {tot[PHASES.index('MAP')] / cr:.0f} VISIT {tot[PHASES.index('VISIT')] / cr:.0f}")
 
 
 if __name__ == "__main__":
