@@ -152,11 +152,11 @@ def main() -> None:
                              f"torch.distributed.run --nproc-per-node {args.gpus}")
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
     dist = None
-    if world > 1:
+    if world > 1 or "LOCAL_WORLD_SIZE" in os.environ:  # under torch.distributed.run: RCCL even for one rank
         import torch.distributed as dist
 
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = local_rank
 
     ndef, odef, desc = CONFIGS[args.config]

@@ -1266,7 +1266,7 @@ struct Replica {
             return 0;
         }
         zh->nfreeRid = n - 1;
-        return d.frid()[n - 1];
+        return d.frid()[n - 1]; /* (a read-ahead of the next entry measured slower: r04l, r04m) */
     }
     MT_HD void free_rid(int32_t r) {
         z.rgen[r]++;
@@ -2445,10 +2445,15 @@ struct Replica {
             int32_t c1 = 64 + l < cnt ? hsq[64 + l] : 0;
             int32_t c2 = 128 + l < cnt ? hsq[128 + l] : 0;
             int32_t c3 = 192 + l < cnt ? hsq[192 + l] : 0;
-            int32_t r0 = l < cnt ? (int32_t)hrd[l] : 0, g0 = l < cnt ? hgn[l] : 0;
-            int32_t r1 = 64 + l < cnt ? (int32_t)hrd[64 + l] : 0, g1 = 64 + l < cnt ? hgn[64 + l] : 0;
-            int32_t r2 = 128 + l < cnt ? (int32_t)hrd[128 + l] : 0, g2 = 128 + l < cnt ? hgn[128 + l] : 0;
-            int32_t r3 = 192 + l < cnt ? (int32_t)hrd[192 + l] : 0, g3 = 192 + l < cnt ? hgn[192 + l] : 0;
+            /* the image's heap (tiled profile): every field in this pass; an LDS heap re-reads the moved entries */
+            constexpr bool PICK = TILED;
+            int32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, g0 = 0, g1 = 0, g2 = 0, g3 = 0;
+            if (PICK) {
+                r0 = l < cnt ? (int32_t)hrd[l] : 0, g0 = l < cnt ? hgn[l] : 0;
+                r1 = 64 + l < cnt ? (int32_t)hrd[64 + l] : 0, g1 = 64 + l < cnt ? hgn[64 + l] : 0;
+                r2 = 128 + l < cnt ? (int32_t)hrd[128 + l] : 0, g2 = 128 + l < cnt ? hgn[128 + l] : 0;
+                r3 = 192 + l < cnt ? (int32_t)hrd[192 + l] : 0, g3 = 192 + l < cnt ? hgn[192 + l] : 0;
+            }
             int32_t last = cnt - 1; /* index of the entry that moves to the root */
             IX xr = hrd[last];
             uint8_t xg = hgn[last];
@@ -2494,9 +2499,18 @@ struct Replica {
                 int32_t a0 = w.shfl(v0, sl), a1 = w.shfl(v1, sl), a2 = w.shfl(v2, sl), a3 = w.shfl(v3, sl);
                 return sc == 0 ? a0 : sc == 1 ? a1 : sc == 2 ? a2 : a3;
             };
-            IX mr = (IX)pick(r0, r1, r2, r3);
-            uint8_t mg = (uint8_t)pick(g0, g1, g2, g3);
-            int32_t ms = pick(c0, c1, c2, c3);
+            IX mr = 0;
+            uint8_t mg = 0;
+            int32_t ms = 0;
+            if (PICK) {
+                mr = (IX)pick(r0, r1, r2, r3);
+                mg = (uint8_t)pick(g0, g1, g2, g3);
+                ms = pick(c0, c1, c2, c3);
+            } else if (l < d) {
+                mr = hrd[src - 1];
+                mg = hgn[src - 1];
+                ms = hsq[src - 1];
+            }
             w.sync();
             if (l < d) {
                 hrd[dst - 1] = mr;
@@ -3561,6 +3575,11 @@ struct Replica {
                 return;
             }
         }
+        if (runOnly) {
+            runA = sa;
+            runB = sb;
+            return;
+        }
         if (dl) { /* delta events need each visited row's position: the serial visit */
             visit_run(sa, sb, refSeq, client, leaf, true);
             return;
@@ -3670,7 +3689,8 @@ struct Replica {
      * vis > 0 from slot sa to slot sb, a leaf at a time with one lane per row (tiled profile, no delta events, no
      * local references): every row's fields are read in one pass and the row updates are made in parallel; the
      * steps whose order is observable — overlap-list pushes, window-set appends, the leaf's LRU entry (added by
-     * its first such row), pending-group entries — are taken in row order. Same result as the serial visit. */
+     * its first such row), pending-group entries — are taken in row order. Same result as the serial visit.
+     * Both profiles (the window set and STABLE summaries are the tiled profile's). */
     MT_HD void remove_run(int32_t sa, int32_t sb, int32_t refSeq, int32_t client, int32_t seq, int32_t localSeq,
                           bool hasL, uint32_t rcl, bool collab, bool* created) {
         MT_PROF_SCOPE(PH_VISIT);
@@ -3683,7 +3703,8 @@ struct Replica {
             int32_t n = leaf_at(k);
             int32_t s = n * MAXN + (j & (MAXN - 1));
             RowView r = row_view(s); /* the row, its window flags and id, the leaf's child count: one round trip */
-            uint8_t x = t.xf[s];
+            uint8_t x = 0;
+            if constexpr (TILED) x = t.xf[s];
             int32_t rid = z.rid[s];
             int32_t c = nch[n];
             int32_t j0 = k == ka ? (sa & (MAXN - 1)) : 0;
@@ -3714,6 +3735,7 @@ struct Replica {
                 ovl_push(sl, client);
                 st_bytes4(sl, (bl & 0xFF00FFFFu) | ((((bl >> 16) & 0xFF) | RF_OVL) << 16));
             }
+            if constexpr (TILED) {
             /* row_removed: out of the STABLE summaries; into the window set unless the removal is settled */
             bool stable = sel && (x & XF_STABLE);
             int32_t lsd = w.sum(stable ? L : 0);
@@ -3740,6 +3762,7 @@ struct Replica {
                 }
                 w.sync();
                 t.wN = wn + cnt;
+            }
             }
             if (collab) {
                 bool pend = (fresh || unas) && seq == UNASSIGNED_SEQ && client == h.localShort;
@@ -3778,16 +3801,12 @@ struct Replica {
         const bool rf = refs_on();
         bool saved = false;
         const int32_t dop = remove ? MT_DELTA_REMOVE : MT_DELTA_ANNOTATE;
-        if constexpr (TILED && W::N >= MAXN * MAXN) {
+        if constexpr (W::N >= MAXN * MAXN) {
             if (remove && !dl && !rf) { /* find and split, then the lane-parallel visit */
                 auto none = [](int32_t, int32_t) {};
                 runOnly = true;
                 runA = -1;
-                {
-                    MT_PROF_SCOPE(PH_MAP);
-                    MT_PROF_COUNT(PH_C_RANGE, 1);
-                    range_op_tiled(start, end, refSeq, client, none, false);
-                }
+                range_op(start, end, refSeq, client, none, false);
                 runOnly = false;
                 if (runA >= 0 && !h.err) remove_run(runA, runB, refSeq, client, seq, localSeq, hasL, rcl, collab, &created);
                 if (h.collaborating && seq != UNASSIGNED_SEQ) zamboni_soon();
