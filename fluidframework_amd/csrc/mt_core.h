@@ -1847,6 +1847,10 @@ struct Replica {
         if (k >= h.nleaf) return -1;
         return lo[k] * MAXN + (t0 & 4);
     }
+#ifndef MT_SCAN_NB
+#define MT_SCAN_NB 1 /* flat-profile position scans: wave blocks (256 slots each) per round trip; 2 and 3 measured
+                        * 9 % and 27 % slower on config 3 (r04n: the second block's 16 registers spill at 8 waves) */
+#endif
     /* ---- removedClientOverlap: 8 entries inline in the cold row, then chains of 8-entry blocks
      * in a per-document pool (entries are short id + 1; 0 ends a list) ------------------------ */
     MT_HD bool ovl_has(int32_t s, int32_t client) const {
@@ -1963,21 +1967,42 @@ struct Replica {
                 zh->ovFree = b;
             }
     }
+    /* the scan columns of the 4 slots from s0 (len, rseq; seq and {cli, rcli, flags, ng} unless the
+     * perspective is the local view), loaded apart from their use so that a scan can issue several quads'
+     * loads in one round trip */
+    struct QuadRows {
+        I4 L, R, Q, BY;
+    };
+    MT_HD QuadRows quad_load(int32_t s0, bool local) const {
+        QuadRows x = {};
+        if (s0 >= 0) {
+            x.L = ld4(&z.len(s0));
+            x.R = ld4(&z.rseq(s0));
+            if (!local) {
+                x.Q = ld4(&z.seq(s0));
+                x.BY = ld4(z.bytes4(s0));
+            }
+        }
+        return x;
+    }
     /* nodeLength (mergeTree.ts:1692-1732) of the 4 slots from s0 under (refSeq, client); 0 for
      * empty slots */
     MT_HD void quad_vis(int32_t s0, int32_t refSeq, int32_t client, int32_t v[4]) const {
+        quad_vis_of(s0, quad_load(s0, is_local(client)), refSeq, client, v);
+    }
+    MT_HD void quad_vis_of(int32_t s0, const QuadRows& x, int32_t refSeq, int32_t client, int32_t v[4]) const {
         if (s0 < 0) {
             v[0] = v[1] = v[2] = v[3] = 0;
             return;
         }
-        I4 L = ld4(&z.len(s0));
-        I4 R = ld4(&z.rseq(s0));
+        const I4& L = x.L;
+        const I4& R = x.R;
         if (is_local(client)) { /* localNetLength (mergeTree.ts:1195-1206) */
             for (int q = 0; q < 4; q++) v[q] = R.x[q] == NOREM ? L.x[q] : 0;
             return;
         }
-        I4 Q = ld4(&z.seq(s0));
-        I4 BY = ld4(z.bytes4(s0)); /* {cli, rcli, flags, ng} of the 4 slots */
+        const I4& Q = x.Q;
+        const I4& BY = x.BY; /* {cli, rcli, flags, ng} of the 4 slots */
         int32_t ovq = 0;
         for (int q = 0; q < 4; q++) {
             uint32_t by = (uint32_t)BY.x[q];
@@ -2025,31 +2050,43 @@ struct Replica {
         if constexpr (TILED) return find_reach_tiled(pos, refSeq, client, Pout, Sout, Vout);
         int32_t run = 0;
         int32_t T = h.nleaf * MAXN;
-        for (int32_t b = 0; b < T; b += 4 * W::N) {
-            int32_t v[4];
-            int32_t s0 = quad_slot(b + 4 * w.lane());
-            quad_vis(s0, refSeq, client, v);
-            int32_t tot;
-            int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
-            int32_t hq = -1, hp = 0, hv = 0;
-            for (int q = 0; q < 4; q++) {
-                if (hq < 0 && p < pos && pos <= p + v[q]) {
-                    hq = q;
-                    hp = p;
-                    hv = v[q];
+        const bool loc = is_local(client);
+        constexpr int NB = W::N >= 64 ? MT_SCAN_NB : 1; /* wave blocks whose loads are issued together */
+        for (int32_t b0 = 0; b0 < T; b0 += NB * 4 * W::N) {
+            int32_t s0[NB];
+            QuadRows x[NB];
+#pragma unroll
+            for (int q = 0; q < NB; q++) s0[q] = quad_slot(b0 + q * 4 * W::N + 4 * w.lane());
+#pragma unroll
+            for (int q = 0; q < NB; q++) x[q] = quad_load(s0[q], loc);
+#pragma unroll
+            for (int bq = 0; bq < NB; bq++) {
+                int32_t b = b0 + bq * 4 * W::N;
+                if (b >= T) return -1;
+                int32_t v[4];
+                quad_vis_of(s0[bq], x[bq], refSeq, client, v);
+                int32_t tot;
+                int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
+                int32_t hq = -1, hp = 0, hv = 0;
+                for (int q = 0; q < 4; q++) {
+                    if (hq < 0 && p < pos && pos <= p + v[q]) {
+                        hq = q;
+                        hp = p;
+                        hv = v[q];
+                    }
+                    p += v[q];
                 }
-                p += v[q];
+                uint64_t m = w.ballot(hq >= 0);
+                if (m) {
+                    int32_t l = W::ffs(m);
+                    *Pout = w.bcast(hp, l);
+                    if (Sout) *Sout = w.bcast(s0[bq] + hq, l);
+                    if (Vout) *Vout = w.bcast(hv, l);
+                    return b + 4 * l + w.bcast(hq, l);
+                }
+                run += tot;
+                if (run >= pos && pos > 0) return -1;
             }
-            uint64_t m = w.ballot(hq >= 0);
-            if (m) {
-                int32_t l = W::ffs(m);
-                *Pout = w.bcast(hp, l);
-                if (Sout) *Sout = w.bcast(s0 + hq, l);
-                if (Vout) *Vout = w.bcast(hv, l);
-                return b + 4 * l + w.bcast(hq, l);
-            }
-            run += tot;
-            if (run >= pos && pos > 0) break;
         }
         return -1;
     }
@@ -3506,43 +3543,62 @@ struct Replica {
         int32_t tf = -1, Pf = 0, vf = 0, tg = -1, Pg = 0, vg = 0, sf = -1, sg = -1;
         {
             MT_PROF_SCOPE(PH_FIND);
-            for (int32_t b = 0; b < T; b += 4 * W::N) {
-                int32_t v[4];
-                int32_t s0 = quad_slot(b + 4 * w.lane());
-                quad_vis(s0, refSeq, client, v);
-                int32_t tot;
-                int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
-                int32_t hf = -1, pf = 0, lf = 0, hl = -1, pl = 0, ll = 0;
-                for (int q = 0; q < 4; q++) {
-                    if (v[q] > 0 && p < end && p + v[q] > start) {
-                        if (hf < 0) {
-                            hf = q;
-                            pf = p;
-                            lf = v[q];
+            const bool loc = is_local(client);
+            constexpr int NB = W::N >= 64 ? MT_SCAN_NB : 1; /* wave blocks whose loads are issued together */
+            bool done = false;
+            for (int32_t b0 = 0; b0 < T && !done; b0 += NB * 4 * W::N) {
+                int32_t s0[NB];
+                QuadRows x[NB];
+#pragma unroll
+                for (int q = 0; q < NB; q++) s0[q] = quad_slot(b0 + q * 4 * W::N + 4 * w.lane());
+#pragma unroll
+                for (int q = 0; q < NB; q++) x[q] = quad_load(s0[q], loc);
+#pragma unroll
+                for (int bq = 0; bq < NB; bq++) {
+                    int32_t b = b0 + bq * 4 * W::N;
+                    if (b >= T) {
+                        done = true;
+                        break;
+                    }
+                    int32_t v[4];
+                    quad_vis_of(s0[bq], x[bq], refSeq, client, v);
+                    int32_t tot;
+                    int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
+                    int32_t hf = -1, pf = 0, lf = 0, hl = -1, pl = 0, ll = 0;
+                    for (int q = 0; q < 4; q++) {
+                        if (v[q] > 0 && p < end && p + v[q] > start) {
+                            if (hf < 0) {
+                                hf = q;
+                                pf = p;
+                                lf = v[q];
+                            }
+                            hl = q;
+                            pl = p;
+                            ll = v[q];
                         }
-                        hl = q;
-                        pl = p;
-                        ll = v[q];
+                        p += v[q];
                     }
-                    p += v[q];
-                }
-                uint64_t m = w.ballot(hf >= 0);
-                if (m) {
-                    if (tf < 0) {
-                        int32_t l = W::ffs(m);
-                        tf = b + 4 * l + w.bcast(hf, l);
-                        sf = w.bcast(s0 + hf, l);
-                        Pf = w.bcast(pf, l);
-                        vf = w.bcast(lf, l);
+                    uint64_t m = w.ballot(hf >= 0);
+                    if (m) {
+                        if (tf < 0) {
+                            int32_t l = W::ffs(m);
+                            tf = b + 4 * l + w.bcast(hf, l);
+                            sf = w.bcast(s0[bq] + hf, l);
+                            Pf = w.bcast(pf, l);
+                            vf = w.bcast(lf, l);
+                        }
+                        int32_t l2 = 63 - __builtin_clzll(m);
+                        tg = b + 4 * l2 + w.bcast(hl, l2);
+                        sg = w.bcast(s0[bq] + hl, l2);
+                        Pg = w.bcast(pl, l2);
+                        vg = w.bcast(ll, l2);
                     }
-                    int32_t l2 = 63 - __builtin_clzll(m);
-                    tg = b + 4 * l2 + w.bcast(hl, l2);
-                    sg = w.bcast(s0 + hl, l2);
-                    Pg = w.bcast(pl, l2);
-                    vg = w.bcast(ll, l2);
+                    run += tot;
+                    if (run >= end) {
+                        done = true;
+                        break;
+                    }
                 }
-                run += tot;
-                if (run >= end) break;
             }
         }
         if (tf < 0) return;
