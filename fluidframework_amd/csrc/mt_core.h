@@ -2933,25 +2933,25 @@ struct Replica {
         /* the shuffles read the predecessor lane, which may not be a pair's lane: outside the branch, where
          * every lane is active */
         int32_t lenP = w.shfl(r.len, q - 1), flP = w.shfl(fl, q - 1);
+        int32_t ridP = w.shfl((int32_t)r.rid, q - 1); /* the pair's cold rows by the ids this pass read */
         if ((pairs >> q) & 1) {
-            int32_t sp = n * MAXN + j - 1, sk = n * MAXN + j;
             bool permPair = (flP & fl & RF_PERM) != 0;
             /* localNetLength > 0 on both sides: a zero-length row (the empty right part of a split past a
              * segment's end) is held and leaves no prevSegment (mergeTree.ts:1355-1383) */
             pairOk = lenP > 0 && r.len > 0 && ((flP ^ fl) & RF_PROPS) == 0 &&
                      (permPair || !((flP | fl) & RF_NOTEXT));
+            const typename HT::Cold& ca = d.cold()[ridP];
+            const typename HT::Cold& cb = d.cold()[(int32_t)r.rid];
             if (pairOk && (fl & RF_PROPS)) { /* matchProperties (properties.ts:61-92) */
-                const typename HT::Cold& ca = cold(sp);
-                const typename HT::Cold& cb = cold(sk);
                 for (int i = 0; i < HT::K / 8; i++)
                     if (!eq4(ld4((const int32_t*)&ca.pv[8 * i]), ld4((const int32_t*)&cb.pv[8 * i]))) pairOk = false;
             }
             if (pairOk && permPair) { /* PermutationSegment.canAppend: handles follow, or both unallocated */
-                uint32_t sa = cold(sp).toff, sb = cold(sk).toff;
+                uint32_t sa = ca.toff, sb = cb.toff;
                 pairOk = sa == 0 ? sb == 0 : sb == sa + (uint32_t)lenP;
             } else if (pairOk) { /* TextSegment.canAppend: the run does not end with "\n" (textSegment.ts:64) */
                 bool nl = (flP & RF_NLK) ? (flP & RF_NL) != 0
-                                         : arena_base(zh->arenaSide)[cold(sp).toff + lenP - 1] == '\n';
+                                         : arena_base(zh->arenaSide)[ca.toff + lenP - 1] == '\n';
                 pairOk = !nl;
             }
         }
