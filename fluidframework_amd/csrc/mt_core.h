@@ -2246,12 +2246,102 @@ struct Replica {
     }
 
     /* ---- splitAt (mergeTree.ts:523-567, textSegment.ts:103-111) ------------------------ */
+    /* split_row on the GPU without delta events or local references, in two round trips: the leaf's rows (the
+     * row being split and the ones the slab shift moves), its child count and the free row-id stack's top are
+     * read in one pass, the row's cold record (one dword per lane) in a second; the shift, the new row and its
+     * cold copy are then written from registers. Same result as the serial form below. */
+    MT_HD int32_t split_row_par(int32_t n, int32_t j, int32_t off, int32_t* rsOut) {
+        constexpr int CW = (int)(sizeof(typename HT::Cold) / 4);
+        static_assert(W::N >= CW && W::N >= MAXN, "a lane per cold dword and per slot");
+        const int32_t l = w.lane();
+        int32_t s0 = n * MAXN + j;
+        HotRow rr = load_row(n * MAXN + (l & (MAXN - 1)));
+        int32_t c = nch[n];
+        int32_t nfr = zh->nfreeRid;
+        int32_t frr = d.frid()[nfr > 0 ? nfr - 1 : 0];
+        uint32_t fl0 = (uint32_t)w.bcast((int32_t)rr.flags, j);
+        if (fl0 & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
+        int32_t rid0 = w.bcast((int32_t)rr.rid, j), len0 = w.bcast(rr.len, j);
+        uint32_t ng0 = (uint32_t)w.bcast((int32_t)rr.ng, j), xf0 = (uint32_t)w.bcast((int32_t)rr.xf, j);
+        typename HT::Cold* cd = d.cold();
+        const int32_t* csrc = (const int32_t*)&cd[rid0];
+        int32_t cv = l < CW ? csrc[l] : 0; /* the row's cold record: toff is dword 2, ovx the top of dword 3 */
+        /* leaf_insert_slot(n, j + 1, dup): rows j..c-1 move right one slot; slot j + 1 starts as row j */
+        bool willSplit = c + 1 >= MAXN;
+        {
+            MT_PROF_SCOPE(PH_LEAFINS);
+            bool mv = l >= j && l < c && l < MAXN;
+            w.sync();
+            if (mv) store_row(n * MAXN + l + 1, rr);
+            w.sync();
+            z.rid[n * MAXN + j + 1] = -1; /* not a row yet (a leaf split must not re-home it) */
+            nch[n] = (int8_t)(c + 1);
+        }
+        int32_t rs = n * MAXN + j + 1;
+        if (willSplit) {
+            MT_PROF_SCOPE(PH_LEAFINS);
+            int32_t nn = split_node(n);
+            if (nn < 0) return -1;
+            if (j + 1 >= 4) rs = nn * MAXN + (j + 1 - 4);
+        }
+        /* the left part stays at n*8+j unless the leaf split moved children 4..7 (then it sits just before the
+         * new slot, in the new leaf) */
+        int32_t ls = willSplit && j >= 4 ? rs - 1 : s0;
+        int32_t rrid;
+        if (zh->nfreeRid == nfr && nfr > 0) { /* alloc_rid, with the stack's top read above */
+            zh->nfreeRid = nfr - 1;
+            rrid = frr;
+        } else {
+            rrid = alloc_rid();
+        }
+        z.rid[rs] = (IX)rrid;
+        z.rleaf[rrid] = (IX)(rs / MAXN);
+        /* splitAt copies every field (mergeTree.ts:523-567); the right part's text offset (or a PermutationSegment's
+         * start + pos, unallocated staying 0) and its length differ */
+        uint32_t toff0 = (uint32_t)w.bcast(cv, 2);
+        uint32_t ovx0 = (uint32_t)w.bcast(cv, 3) >> 16;
+        uint32_t rtoff;
+        int32_t lenR;
+        if (off < len0) {
+            lenR = len0 - off;
+            rtoff = ((fl0 & RF_PERM) && toff0 == 0) ? 0u : toff0 + (uint32_t)off;
+        } else { /* a split at or past the end: the right part is an empty segment (textSegment.ts:103-111) */
+            lenR = 0;
+            rtoff = toff0 + (uint32_t)len0;
+        }
+        int32_t* cdst = (int32_t*)&cd[rrid];
+        if (l < CW) cdst[l] = l == 2 ? (int32_t)rtoff : cv;
+        w.sync();
+        if (ovx0) ovl_clone(rs, ls);
+        z.len(rs) = lenR;
+        if (off < len0) {
+            z.len(ls) = off;
+            z.flags(ls) = (uint8_t)(fl0 & ~(uint32_t)RF_NLK); /* the left part's last unit is not known any more */
+        } else {
+            z.flags(rs) = (uint8_t)((fl0 & ~(uint32_t)RF_NL) | RF_NLK);
+        }
+        h.nrows++;
+        zh->sumW += 2;
+        if constexpr (TILED) {
+            if (xf0 & XF_W) win_add(rrid, rs);
+            if (xf0 & XF_STABLE) { /* the halves may sit in two leaves after a leaf split */
+                int32_t two[2] = {ls / MAXN, rs / MAXN};
+                leaves_restat(two, rs / MAXN != ls / MAXN ? 2 : 1);
+            }
+        }
+        if (ng0) split_groups(rid0, rrid, (int32_t)ng0); /* segmentGroups.copyTo */
+        if (rsOut) *rsOut = rs;
+        return ls;
+    }
     /* Split the row at lorder coordinate t at offset off (0 < off < len). Returns the slot of
      * the LEFT part afterwards (the right part is the next row in document order). */
     MT_HD int32_t split_row(int32_t t, int32_t off, int32_t* rsOut = nullptr) {
         MT_PROF_SCOPE(PH_SPLIT);
         int32_t n = leaf_at(t >> 3), j = t & 7;
         int32_t s0 = n * MAXN + j;
+        if constexpr (W::N >= 64) {
+            if (!dl_on() && !refs_on()) return split_row_par(n, j, off, rsOut);
+        }
         if (z.flags(s0) & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
         bool willSplit = nch[n] + 1 >= MAXN;
         int32_t rs = leaf_insert_slot(n, j + 1, true); /* rs starts as a copy of the row */
@@ -2294,23 +2384,7 @@ struct Replica {
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
          * same pending groups (in the row's FIFO order = log order), appended at the end of each
          * group's segment list */
-        if (z.ng(ls)) {
-            if (zh->memN + z.ng(ls) > d.caps.mcap) mem_compact();
-            int32_t head = zh->gqN ? d.gq()[zh->gqHead % d.caps.gcap] : 0x7fffffff;
-            int32_t lrid = z.rid[ls];
-            int32_t rrid = z.rid[rs];
-            int32_t m0 = zh->memN;
-            for (int32_t b = 0; b < m0; b += W::N) {
-                int32_t i = b + w.lane();
-                int32_t g = i < m0 ? d.mgid()[i] : -1;
-                uint64_t m = w.ballot(i < m0 && d.mrid()[i] == lrid && g >= head);
-                while (m) {
-                    int32_t l = W::ffs(m);
-                    m &= m - 1;
-                    mem_append(w.bcast(g, l), rrid);
-                }
-            }
-        }
+        if (z.ng(ls)) split_groups(z.rid[ls], z.rid[rs], z.ng(ls));
         if (dl_on()) { /* MergeTreeMaintenanceType.SPLIT (mergeTree.ts:2264-2269): [segment, next] */
             dhead(MT_DELTA_SPLIT);
             dseg(-1, z.len(ls));
@@ -2322,6 +2396,24 @@ struct Replica {
     }
 
     /* ---- segment groups ---------------------------------------------------------------- */
+    /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39) of a split: the right part (rrid) joins the same
+     * pending groups as the left (lrid, in ng of them), in the row's FIFO order = log order, appended at the end
+     * of each group's segment list */
+    MT_HD void split_groups(int32_t lrid, int32_t rrid, int32_t ng) {
+        if (zh->memN + ng > d.caps.mcap) mem_compact();
+        int32_t head = zh->gqN ? d.gq()[zh->gqHead % d.caps.gcap] : 0x7fffffff;
+        int32_t m0 = zh->memN;
+        for (int32_t b = 0; b < m0; b += W::N) {
+            int32_t i = b + w.lane();
+            int32_t g = i < m0 ? d.mgid()[i] : -1;
+            uint64_t m = w.ballot(i < m0 && d.mrid()[i] == lrid && g >= head);
+            while (m) {
+                int32_t l = W::ffs(m);
+                m &= m - 1;
+                mem_append(w.bcast(g, l), rrid);
+            }
+        }
+    }
     MT_HD void mem_append(int32_t gid, int32_t rid) {
         int32_t m = zh->memN;
         if (m >= d.caps.mcap) {
@@ -2776,19 +2868,29 @@ struct Replica {
     }
     /* TextSegment.append (textSegment.ts:74-85): the merged text is rebuilt at the arena top */
     MT_HD void append_text(int32_t a, int32_t b) {
+        uint32_t xa = 0, xb = 0;
+        if constexpr (TILED) {
+            xa = z.tl.xf[a];
+            xb = z.tl.xf[b];
+        }
+        append_rows(a, b, z.rid[a], z.rid[b], z.len(a), z.len(b), z.flags(a), z.flags(b), xa, xb);
+    }
+    /* append_text with the two rows' ids, lengths, flags and window flags as the caller read them (scour) */
+    MT_HD void append_rows(int32_t a, int32_t b, int32_t ra, int32_t rb, int32_t La, int32_t Lb, uint32_t fa,
+                           uint32_t fb, uint32_t xa, uint32_t xb) {
         MT_PROF_SCOPE(PH_APPEND);
-        int32_t La = z.len(a), Lb = z.len(b);
         if constexpr (TILED) { /* b's length joins a's row: keep the leaf's STABLE sum exact */
-            bool sa = z.tl.xf[a] & XF_STABLE, sb = z.tl.xf[b] & XF_STABLE;
+            bool sa = xa & XF_STABLE, sb = xb & XF_STABLE;
             if (sa && !sb) lst_add(a / MAXN, Lb);
             if (!sa && sb) lst_add(a / MAXN, -Lb);
         }
-        if (z.flags(a) & RF_PERM) { /* PermutationSegment.append (permutationvector.ts:95-101) */
+        if (fa & RF_PERM) { /* PermutationSegment.append (permutationvector.ts:95-101) */
             z.len(a) = La + Lb;
             return;
         }
+        typename HT::Cold* cd = d.cold();
         uint16_t* base = arena_base(zh->arenaSide);
-        int32_t ta = (int32_t)cold(a).toff, tb = (int32_t)cold(b).toff; /* both reads in one round trip */
+        int32_t ta = (int32_t)cd[ra].toff, tb = (int32_t)cd[rb].toff; /* both reads in one round trip */
         if (ta + La == h.arenaTop && h.arenaTop + Lb <= d.caps.acap) {
             int32_t off = arena_alloc(Lb);
             arena_copy(base + off, base + tb, Lb);
@@ -2798,13 +2900,13 @@ struct Replica {
             int32_t off = arena_alloc(La + Lb);
             if (off < 0) return;
             base = arena_base(zh->arenaSide); /* a GC may have switched halves (and moved both texts) */
-            arena_copy(base + off, base + cold(a).toff, La);
-            arena_copy(base + off + La, base + cold(b).toff, Lb);
-            cold(a).toff = (uint32_t)off;
+            arena_copy(base + off, base + cd[ra].toff, La);
+            arena_copy(base + off + La, base + cd[rb].toff, Lb);
+            cd[ra].toff = (uint32_t)off;
         }
         z.len(a) = La + Lb;
         /* the merged text ends where b's did */
-        z.flags(a) = (uint8_t)((z.flags(a) & ~(RF_NLK | RF_NL)) | (z.flags(b) & (RF_NLK | RF_NL)));
+        z.flags(a) = (uint8_t)((fa & ~(uint32_t)(RF_NLK | RF_NL)) | (fb & (RF_NLK | RF_NL)));
     }
     /* scourNode on leaf n: compacts the slab in place; returns the new child count. Rows are
      * merged into their predecessor or unlinked exactly as the reference decides. */
@@ -2975,8 +3077,11 @@ struct Replica {
             if (ok) {
                 int32_t sp = w.bcast(n, prev) * MAXN + (prev & (MAXN - 1));
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
-                if (refs_on()) refs_append(z.rid[sp], z.rid[sk], prevLen);
-                append_text(sp, sk); /* updates z.len(sp) (read by a GC inside it) and its NL bits */
+                int32_t rp = w.bcast((int32_t)r.rid, prev), rk = w.bcast((int32_t)r.rid, k);
+                if (refs_on()) refs_append(rp, rk, prevLen);
+                /* updates z.len(sp) (read by a GC inside it) and its NL bits */
+                append_rows(sp, sk, rp, rk, prevLen, lk, (uint32_t)prevFl, (uint32_t)fk,
+                            TILED ? (uint32_t)w.bcast((int32_t)r.xf, prev) : 0u, TILED ? (uint32_t)w.bcast((int32_t)r.xf, k) : 0u);
                 prevLen += lk;
                 prevFl = (prevFl & ~(RF_NLK | RF_NL)) | (fk & (RF_NLK | RF_NL));
                 nlen = w.writelane(prevLen, prev, nlen);
@@ -3775,7 +3880,7 @@ struct Replica {
             h.localLen -= w.sum(fresh ? L : 0); /* the rows leave the local view */
             if (fresh) {
                 z.rseq(s) = seq;
-                cold(s).lrseq = localSeq;
+                d.cold()[rid].lrseq = localSeq;
                 uint32_t f2 = hasL ? (fl | RF_LRSEQ) : (fl & ~(uint32_t)RF_LRSEQ);
                 st_bytes4(s, (b4 & 0xFF0000FFu) | (rcl << 8) | (f2 << 16));
             } else if (unas) {
