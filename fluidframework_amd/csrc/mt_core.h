@@ -1527,6 +1527,25 @@ struct Replica {
         twslot[t.wN] = s;
         t.wN++;
     }
+    /* row_enter of a row whose id, generation, seq, removedSeq and length the caller holds */
+    MT_HD void row_enter_known(int32_t s, int32_t rid, int32_t gen, int32_t seq, int32_t rseq, int32_t len) {
+        bool st = seq != UNASSIGNED_SEQ && seq <= h.minSeq && (rseq == NOREM || (rseq != UNASSIGNED_SEQ && rseq <= h.minSeq));
+        if (st) {
+            z.tl.xf[s] = rseq == NOREM ? XF_STABLE : 0;
+            if (rseq == NOREM) lst_add(s / MAXN, len);
+        } else {
+            z.tl.xf[s] = XF_W;
+            auto& t = z.tl;
+            if (t.wN >= HT::TL::WCAP) {
+                fail(E_CAPACITY);
+                return;
+            }
+            twrid[t.wN] = rid;
+            twgen[t.wN] = (uint8_t)gen;
+            twslot[t.wN] = s;
+            t.wN++;
+        }
+    }
     /* a row just placed (insert): STABLE if already settled (non-collaborating edits), else W */
     MT_HD void row_enter(int32_t s) {
         if (settled(s)) {
@@ -2499,7 +2518,8 @@ struct Replica {
      * ancestors of the new leaf position are read in parallel (lane i: the (i+1)-th ancestor), the
      * ones it passes are exactly the leading run with maxSeq greater than it (ancestors are ordered
      * along a path), and they all move down one level at once. */
-    MT_HD void heap_add(int32_t rid, int32_t seq) {
+    /* gen: the row id's generation if the caller has read it (-1: read here) */
+    MT_HD void heap_add(int32_t rid, int32_t seq, int32_t knownGen = -1) {
         MT_PROF_SCOPE(PH_HEAP);
         int32_t n = h.heapN;
         if (n >= HT::H) {
@@ -2510,7 +2530,7 @@ struct Replica {
         int32_t k = n + 1; /* L[k] (1-based) lives at index k-1 */
         h.heapN = n + 1;
         if (n + 1 > zh->hwHeap) zh->hwHeap = n + 1;
-        uint8_t gen = z.rgen[rid];
+        uint8_t gen = knownGen >= 0 ? (uint8_t)knownGen : z.rgen[rid];
         if (seq >= hmax) { /* every ancestor's maxSeq <= hmax <= seq: the fixup moves nothing (collections.ts:240-247) */
             hmax = seq;
             if (w.lane() == 0) {
@@ -2758,6 +2778,13 @@ struct Replica {
         if (nsc[n] != 1 && seq > h.currentSeq) {
             nsc[n] = 1;
             heap_add(z.rid[s], seq);
+        }
+    }
+    /* add_lru of a row whose id, generation and leaf's needsScour the caller has read */
+    MT_HD void add_lru_known(int32_t n, int32_t rid, int32_t gen, int32_t sc, int32_t seq) {
+        if (sc != 1 && seq > h.currentSeq) {
+            nsc[n] = 1;
+            heap_add(rid, seq, gen);
         }
     }
 
@@ -3542,6 +3569,15 @@ struct Replica {
         int32_t L = seg_len(op);
         if (L <= 0) ensure_boundary(pos, refSeq, client); /* the split still happens (2004) */
         if (L > 0) {
+            /* tiled profile: read ahead of the position search, the free row-id stack's top and (a text of at
+             * most a wave's length) the op's text, one unit per lane (config 4 +2.2 %; at config 3's 8 waves per
+             * SIMD the live registers cost more than the round trips: -2.8 %, r04r) */
+            constexpr bool RA = TILED && W::N >= 64;
+            const bool text = !marker && !perm;
+            int32_t nfr = RA ? zh->nfreeRid : 0;
+            int32_t frr = RA ? (int32_t)d.frid()[nfr > 0 ? nfr - 1 : 0] : 0;
+            const bool tpreOk = RA && text && L <= W::N;
+            int32_t tpre = tpreOk && w.lane() < L ? p.text[op.text_off + w.lane()] : 0;
             int32_t off = 0;
             if (!marker && !perm) {
                 MT_PROF_SCOPE(PH_TEXT);
@@ -3555,7 +3591,18 @@ struct Replica {
                 return;
             }
             MT_PROF_SCOPE(PH_PLACE);
-            int32_t rid = alloc_rid();
+            int32_t rid;
+            if (RA && zh->nfreeRid == nfr && nfr > 0) { /* alloc_rid, with the stack's top read above */
+                zh->nfreeRid = nfr - 1;
+                rid = frr;
+            } else {
+                rid = alloc_rid();
+            }
+            int32_t gen = 0, sc = 0;
+            if (RA) { /* for the window set and the LRU entry: one round trip */
+                gen = z.rgen[rid];
+                sc = nsc[s / MAXN];
+            }
             z.rid[s] = (IX)rid;
             typename HT::Cold& c = d.cold()[rid]; /* row id kept in a register, not re-read per field */
             z.len(s) = L;
@@ -3576,15 +3623,25 @@ struct Replica {
             h.nrows++;
             zh->sumW++;
             if (preRseq <= 0) h.localLen += L;
-            if (!marker && !perm) {
+            if (text) {
                 MT_PROF_SCOPE(PH_TEXT);
-                int32_t last = arena_copy(arena_base(zh->arenaSide) + off, p.text + op.text_off, L);
+                int32_t last;
+                if (tpreOk) {
+                    if (w.lane() < L) arena_base(zh->arenaSide)[off + w.lane()] = (uint16_t)tpre;
+                    last = w.bcast(tpre, L - 1);
+                    w.sync();
+                } else {
+                    last = arena_copy(arena_base(zh->arenaSide) + off, p.text + op.text_off, L);
+                }
                 fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
             }
             /* {cli, rcli, flags, ng = 0} in one store */
             st_bytes4(s, (uint32_t)(uint8_t)(client < 0 ? LOCAL_CLIENT : client) |
                              ((uint32_t)(preRseq > 0 ? preRcli : 0) << 8) | ((uint32_t)(uint8_t)fl << 16));
-            if constexpr (TILED) row_enter(s);
+            if constexpr (RA)
+                row_enter_known(s, rid, gen, seq, preRseq > 0 ? preRseq : NOREM, L);
+            else if constexpr (TILED)
+                row_enter(s);
             if (op.props) { /* TextSegment.make(text, props): addProperties without collab */
                 const mt_props_rec& pr = p.props[op.props - 1];
                 add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE, 0, false);
@@ -3594,7 +3651,10 @@ struct Replica {
                     bool created = false;
                     pending_add(s, localSeq, &created);
                 } else if (seq > h.minSeq) {
-                    add_lru(s, seq);
+                    if (RA)
+                        add_lru_known(s / MAXN, rid, gen, sc, seq);
+                    else
+                        add_lru(s, seq);
                 }
             }
             if (dl_on()) { /* INSERT delta (mergeTree.ts:2014-2021), after blockInsert */
