@@ -396,7 +396,10 @@ struct ProfScope {
  * ---------------------------------------------------------------------------------------- */
 /* DL: this build emits delta events (mt_oplog.h) when the engine has a delta log; the hot replay
  * kernels are built without (DL = false), so the emission costs them no registers or code */
-template <class W, class HT, bool DL = false>
+/* LOAD: applies snapshot-load records (mt_oplog.h MT_OP_RELOAD / COLLAB / APPEND); the plain config-2/3 replay
+ * kernel is built without them (its scalar registers: SGPR spills 1,321 -> 1,041, +2.2 % on config 3, r04s) and
+ * the engine runs a batch that holds any with the full build */
+template <class W, class HT, bool DL = false, bool LOAD = true>
 struct Replica {
     typedef typename HT::IX IX;
     static constexpr bool TILED = HT::TILED;
@@ -4398,7 +4401,10 @@ struct Replica {
         int32_t eref = 0, ecli = 0, eseq = 0, epre = 0, eat = -1;
         uint8_t eprc = 0;
         if (kind >= MT_OP_RELOAD && !(op.kind & MT_OPF_LOCAL) && !(op.kind & MT_OPF_TREE)) {
-            edit = apply_load(op, p, &o, &ecli, &epre, &eprc); /* snapshot load (mt_oplog.h) */
+            if constexpr (LOAD)
+                edit = apply_load(op, p, &o, &ecli, &epre, &eprc); /* snapshot load (mt_oplog.h) */
+            else
+                fail(E_UNSUPPORTED); /* the engine routes such batches to the full build */
             eref = UNIVERSAL_SEQ;
             eseq = op.seq;
         } else if (op.kind & MT_OPF_TREE) { /* MergeTree-level call with explicit (refSeq, clientId, seq) */

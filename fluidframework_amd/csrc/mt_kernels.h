@@ -125,7 +125,7 @@ __device__ inline void skel_lite_move(SkelLite<HT>& k, HT& z, bool in) {
 /* VAR tags a build variant compiled with other flags in its own translation unit (1: compiler-chosen
  * inlining): the kernel's name must differ, since a host launch resolves the kernel by name. */
 /* DL: the delta-event build (engines created with caps.dcap > 0) */
-template <class HT, bool LDS, int MINW = 1, int SKM = 1, int VAR = 0, bool DL = false> /* SKM: 1 Skel, 2 SkelLite, 0 none */
+template <class HT, bool LDS, int MINW = 1, int SKM = 1, int VAR = 0, bool DL = false, bool LOAD = true> /* SKM: 1 Skel, 2 SkelLite, 0 none */
 __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
         copy_image(&hot, g);
         __syncthreads();
         v.t = &hot;
-        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
+        Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
         r.replay(p);
         r.commit();
 #ifdef MT_PROF
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
         __shared__ __attribute__((aligned(16))) SkelLite<HT> sk;
         skel_lite_move(sk, *v.t, true);
         __syncthreads();
-        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
+        Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild;
         r.zh = &sk.zh;
         r.replay(p);
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
         __shared__ __attribute__((aligned(16))) Skel<HT> sk;
         skel_move(sk, *v.t, true);
         __syncthreads();
-        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
+        Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild, r.nlev = sk.nlevel;
         r.nsc = sk.nscour, r.hsq = sk.hseq, r.hrd = sk.hrid, r.hgn = sk.hgen;
         r.zh = &sk.zh, r.l2s = sk.l2s, r.s2l = sk.s2l;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
             for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
 #endif
     } else {
-        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
+        Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
         r.replay(p);
         r.commit();
 #ifdef MT_PROF
@@ -652,6 +652,7 @@ struct mt_engine {
     int32_t rcap = 0; /* local references per document (0: none) */
     int32_t pcap = 0; /* PermutationVector handles per document (0: none) */
     bool fx = false;  /* delta events or local references: the client-feature replay build */
+    bool loads = false; /* the staged batch holds snapshot-load records (the config-2/3 kernel's full build) */
     int profile = 0;
     int waves = 8;    /* occupancy target of the HBM-resident small-profile kernel */
     Store<HotSmall> s0;

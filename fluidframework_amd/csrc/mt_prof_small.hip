@@ -4,6 +4,7 @@
 
 int32_t replay_small_w8(mt_engine* e);
 int32_t replay_small_dl(mt_engine* e);
+int32_t replay_small_load(mt_engine* e);
 
 /* Default: the hot image stays in HBM (skeleton and heap in LDS) and the kernel is built for 8 waves
  * per SIMD, so 8,192 documents are in flight (32 per CU): at one wavefront per document the replay
@@ -13,6 +14,7 @@ int32_t replay_small_dl(mt_engine* e);
  * profiles/r03_c2_4096docs_bench_*.json, and is no longer built). */
 static int32_t replay_small(mt_engine* e) {
     if (e->fx) return replay_small_dl(e); /* the delta-event build */
+    if (e->loads) return replay_small_load(e); /* snapshot-load records */
     return replay_small_w8(e);
 }
 

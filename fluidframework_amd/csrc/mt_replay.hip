@@ -154,6 +154,7 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
     /* every pool reference of every event must be in bounds before the kernel dereferences it: the
      * documents are checked in parallel on the host (up to 16 threads, one contiguous range each) */
     std::vector<mt_engine::Persp> persp((size_t)nd);
+    std::vector<char> loads((size_t)nd, 0);
     auto check = [&](int64_t d0, int64_t d1) -> bool {
         for (int64_t d = d0; d < d1; d++) {
             mt_engine::Persp& pp = persp[(size_t)d];
@@ -162,6 +163,7 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
                 int kind = o.kind & MT_OP_KIND_MASK;
                 if (!(o.kind & MT_OPF_LOCAL)) { /* perspective floors (mt_kernels.h persp_refused) */
                     if (kind == MT_OP_RELOAD || kind == MT_OP_COLLAB || kind == MT_OP_APPEND) {
+                        if (!(o.kind & MT_OPF_TREE)) loads[(size_t)d] = 1; /* a snapshot load: the full build */
                         if (o.seq > pp.all) pp.all = o.seq;
                     } else if (kind != MT_OP_NOOP && o.client != MT_CLIENT_LOCAL) {
                         pp.note(o.client, o.ref_seq);
@@ -223,6 +225,7 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
     e->h_props_off.assign(props_off, props_off + nd);
     e->h_kv_off.assign(kv_off, kv_off + nd);
     e->persp_staged.swap(persp);
+    e->loads = std::find(loads.begin(), loads.end(), 1) != loads.end();
     e->staged = true;
     return MT_OK;
 }

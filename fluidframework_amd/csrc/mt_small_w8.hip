@@ -5,4 +5,7 @@
 #define MT_SMALL_W 8
 #endif
 
-int32_t replay_small_w8(mt_engine* e) { return launch_replay<HotSmall>(e, k_replay<HotSmall, false, MT_SMALL_W>); }
+/* without snapshot-load records (Replica LOAD = false): the engine's default config-2/3 kernel */
+int32_t replay_small_w8(mt_engine* e) {
+    return launch_replay<HotSmall>(e, k_replay<HotSmall, false, MT_SMALL_W, 1, 0, false, false>);
+}
