@@ -3090,20 +3090,25 @@ struct Replica {
         uint64_t okm = w.ballot(pairOk);
         int32_t prev = -1, prevLen = 0, prevFl = 0;
         int32_t alen = 0; /* an appended row's lane: its prevSegment's length right after the append */
-        uint64_t m = pairs;
+        /* Only a pair that passed the tests above can append; every other pair is kept. The walk visits those
+         * pairs in order: a pair whose left row was not appended starts from that row as prevSegment (it
+         * opened a run, or was kept; either way it has absorbed nothing yet), otherwise the run goes on. */
+        keep |= pairs & ~okm;
+        uint64_t app = 0; /* rows appended so far */
+        uint64_t m = pairs & okm;
         while (m) {
             int32_t k = W::ffs(m);
             m &= m - 1;
-            if (!((pairs >> (k - 1)) & 1)) { /* k - 1 opened this run */
+            if (!((app >> (k - 1)) & 1)) {
                 prev = k - 1;
                 prevLen = w.bcast(r.len, prev);
                 prevFl = w.bcast(fl, prev);
             }
             int32_t lk = w.bcast(r.len, k);
             int32_t fk = w.bcast(fl, k);
-            bool ok = (okm >> k) & 1;
+            bool ok = true;
             /* the serial part: a text append needs either side <= TextSegment granularity (the run grows) */
-            if (ok && !(prevFl & fk & RF_PERM)) ok = prevLen <= GRANULARITY || lk <= GRANULARITY;
+            if (!(prevFl & fk & RF_PERM)) ok = prevLen <= GRANULARITY || lk <= GRANULARITY;
             if (ok) {
                 int32_t sp = w.bcast(n, prev) * MAXN + (prev & (MAXN - 1));
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
@@ -3117,12 +3122,9 @@ struct Replica {
                 nlen = w.writelane(prevLen, prev, nlen);
                 alen = w.writelane(prevLen, k, alen);
                 fl = w.writelane(prevFl, prev, fl);
-            }
-            if (!ok) {
-                keep |= 1ull << k;
-                prev = k; /* prevLen 0 (a zero-length row) stands for "no prevSegment" */
-                prevLen = lk;
-                prevFl = fk;
+                app |= 1ull << k;
+            } else {
+                keep |= 1ull << k; /* kept: the next pair, if it tests ok, starts from this row */
             }
         }
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
