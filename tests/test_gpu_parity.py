@@ -150,6 +150,14 @@ def test_config4_tiled_over_100k_live_rows():
     _check_batch(b, 300_000, ndump=1, **default_caps(300_000, config=4))
 
 
+def test_config4_full_length_documents():
+    """Two config-4 documents at the bench's full length (1,000,000 sequenced messages each, ~400k live
+    rows) on the tiled profile, bit-exact against the oracle."""
+    from fluidframework_amd.engine import default_caps
+    b = gen.generate(gen.config4(1_000_000), 2)
+    _check_batch(b, 1_000_000, ndump=1, **default_caps(1_000_000, config=4))
+
+
 def test_tiled_profile_local_pending_config3():
     """The tiled profile on config-3 documents (local-pending edits, acks, lag): same digests."""
     from fluidframework_amd.engine import default_caps
