@@ -2622,8 +2622,10 @@ struct Replica {
             cnt--;
             h.heapN = cnt;
             if (cnt == 0) return;
-            int32_t path[8];
+            /* lane t < d: the t-th entry of the descent (src) moves to its parent (dst), written into lane t as
+             * the descent goes (no path array: a dynamically indexed one lives in scratch memory) */
             int32_t d = 0, k = 1;
+            int32_t src = 1, dst = 1;
             while ((k << 1) <= cnt) {
                 int32_t j = k << 1;
                 int32_t sj = L(j);
@@ -2635,16 +2637,11 @@ struct Replica {
                     }
                 }
                 if (xs - sj <= 0) break;
-                path[d++] = j;
+                src = w.writelane(j, d, src);
+                dst = w.writelane(k, d, dst);
+                d++;
                 k = j;
             }
-            /* lane t < d: the entry at path[t] moves to its parent (path[t-1], or the root) */
-            int32_t src = 1, dst = 0;
-            for (int32_t t = 0; t < 8; t++)
-                if (t == l && t < d) {
-                    src = path[t];
-                    dst = t == 0 ? 1 : path[t - 1];
-                }
             /* its fields from the registers of the first pass (every lane active: the shuffles read other lanes) */
             int32_t sx = src - 1, sl = sx & 63, sc = sx >> 6;
             auto pick = [&](int32_t v0, int32_t v1, int32_t v2, int32_t v3) -> int32_t {
@@ -2694,8 +2691,8 @@ struct Replica {
             if (cnt == 0) return;
             int32_t dd = l < 2 ? 1 : l < 6 ? 2 : l < 14 ? 3 : l < 30 ? 4 : l < 62 ? 5 : 0;
             int32_t off = dd ? l - ((1 << dd) - 2) : 0;
-            int32_t path[24];
-            int32_t d = 0, k = 1;
+            int32_t d = 0, k = 1, lastj = 1;
+            int32_t src = 0, dst = 0; /* lane t < d: the t-th entry of the descent and its parent (as above) */
             bool done = false;
             while (!done) {
                 int32_t node = dd ? (k << dd) + off : 0;
@@ -2722,18 +2719,15 @@ struct Replica {
                         done = true;
                         break;
                     }
-                    path[d++] = j;
+                    src = w.writelane(j, d, src);
+                    dst = w.writelane(lastj, d, dst); /* the root (1) for the first */
+                    lastj = j;
+                    d++;
                     cur = c2;
                 }
-                if (!done) k = path[d - 1];
+                if (!done) k = lastj;
             }
-            int32_t fin = d > 0 ? path[d - 1] : 1;
-            int32_t src = 0, dst = 0;
-            for (int32_t t = 0; t < 24; t++)
-                if (t == l && t < d) {
-                    src = path[t];
-                    dst = t == 0 ? 1 : path[t - 1];
-                }
+            int32_t fin = d > 0 ? lastj : 1;
             IX mr = 0;
             uint8_t mg = 0;
             int32_t ms = 0;
@@ -4304,6 +4298,42 @@ struct Replica {
     }
 
     /* ---- ack (mergeTree.ts:1926-1953, BaseSegment.ack 486-521) ------------------------ */
+    /* ackPendingSegment's per-segment step (mergeTree.ts:1140-1193) for an insert or remove group, one lane per
+     * member row (mem: this lane holds a member, rd its row id): the slot lookup, the checks and the row updates
+     * in parallel, the LRU entries (addToLRUSet) in member order. Same result as the serial loop in ack(). */
+    MT_HD void ack_rows(int32_t kind, int32_t rd, bool mem, int32_t seq) {
+        int32_t leaf = mem ? (int32_t)z.rleaf[rd] : 0;
+        int32_t c = nch[leaf];
+        int32_t s = -1;
+#pragma unroll
+        for (int32_t j = 0; j < MAXN; j++) /* the leaf's row ids: one round trip */
+            if (mem && j < c && z.rid[leaf * MAXN + j] == (IX)rd) s = leaf * MAXN + j;
+        bool bad = mem && s < 0;
+        bool ok = mem && s >= 0;
+        if (ok) {
+            int32_t ng = z.ng(s);
+            if (ng < 1) bad = true;
+            if (ng > 0) z.ng(s) = (uint8_t)(ng - 1);
+            if (kind == MT_OP_INSERT) {
+                if (z.seq(s) != UNASSIGNED_SEQ) bad = true;
+                z.seq(s) = seq;
+                z.flags(s) &= (uint8_t)~RF_LSEQ;
+            } else {
+                int32_t rs = z.rseq(s);
+                if (rs == NOREM || rs == 0) bad = true;
+                z.flags(s) &= (uint8_t)~RF_LRSEQ;
+                if (rs == UNASSIGNED_SEQ) z.rseq(s) = seq;
+            }
+        }
+        if (w.ballot(bad)) fail(E_ASSERT);
+        w.sync();
+        uint64_t om = w.ballot(ok);
+        while (om) {
+            int32_t l = W::ffs(om);
+            om &= om - 1;
+            add_lru(w.bcast(s, l), seq);
+        }
+    }
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
         if (zh->gqN > 0) {
             MT_PROF_SCOPE(PH_ACK);
@@ -4315,6 +4345,12 @@ struct Replica {
                 int32_t i = b + w.lane();
                 int32_t rd = i < mn ? d.mrid()[i] : 0;
                 uint64_t msk = w.ballot(i < mn && d.mgid()[i] == gid);
+                if constexpr (W::N >= 64) {
+                    if (kind == MT_OP_INSERT || kind == MT_OP_REMOVE) { /* a lane per member row; LRU entries in member order */
+                        if (msk) ack_rows(kind, rd, (msk >> w.lane()) & 1, seq);
+                        continue;
+                    }
+                }
                 while (msk) {
                     int32_t l = W::ffs(msk);
                     msk &= msk - 1;
