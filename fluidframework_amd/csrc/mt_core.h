@@ -3181,7 +3181,9 @@ struct Replica {
         if (valid && j >= newc) z.len(n * MAXN + j) = 0; /* disjoint from every kept row's target */
         if (n >= 0 && j == 0) nch[n] = (int8_t)newc;
         w.sync();
-        for (int32_t i = 0; i < nl; i++) cnt[i] = __builtin_popcountll(keep & (0xFFull << (8 * i)));
+#pragma unroll
+        for (int32_t i = 0; i < MAXN; i++) /* constant indices: the caller's array stays in registers */
+            if (i < nl) cnt[i] = __builtin_popcountll(keep & (0xFFull << (8 * i)));
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
         prof[PH_S3] += __builtin_amdgcn_s_memtime() - _t2;
 #endif
@@ -3196,6 +3198,94 @@ struct Replica {
             return scour_leaf(n);
         }
     }
+    /* pack's leaf level on the GPU (mergeTree.ts:1401-1446): scour the pc sibling leaves under `parent`, then
+     * redistribute their rows over cc = total / 4 leaves (the old node ids first, in order). The per-leaf values
+     * are lane arrays (lane i: leaf i's node id / row count / first row), read by lane broadcasts: no locally
+     * indexed array, which the compiler would keep in scratch memory. Same result as the serial form in pack(). */
+    MT_HD bool pack_leaves(int32_t parent, int32_t pc) { /* false: out of nodes (pack stops, as the serial form) */
+        const int32_t q = w.lane();
+        {
+            int32_t sib[MAXN], cnt[MAXN];
+#pragma unroll
+            for (int32_t i = 0; i < MAXN; i++) sib[i] = i < pc ? z.kids[parent * MAXN + i] : -1;
+            scour_par(sib, pc, cnt);
+        }
+        MT_PROF_SCOPE(PH_P1);
+        int32_t okv = q < pc ? (int32_t)z.kids[parent * MAXN + (q & (MAXN - 1))] : 0; /* lane i: old leaf i */
+        int32_t ocv = q < pc ? (int32_t)nch[okv] : 0;                                 /* its rows after scour */
+        int32_t total;
+        int32_t oex = w.excl_scan(ocv, &total); /* lane i: leaf i's first row in the run of all rows */
+        int32_t cc = total / (MAXN / 2);
+        if (cc > MAXN - 1) cc = MAXN - 1;
+        if (cc < 1) cc = 1;
+        int32_t base = total / cc, extra = total % cc;
+        int32_t firstPos = TILED ? 0 : (int32_t)lp[w.bcast(okv, 0)];
+        /* new leaf ni: the old node id ni < pc, else a new node; ncv its row count, nex its first row */
+        int32_t nkv = q < pc ? okv : 0;
+        for (int32_t ni = pc; ni < cc; ni++) {
+            int32_t nb = alloc_node(0);
+            if (nb < 0) return false;
+            nkv = w.writelane(nb, ni, nkv);
+        }
+        int32_t ncv = q < cc ? base + (q < extra ? 1 : 0) : 0;
+        int32_t ntot;
+        int32_t nex = w.excl_scan(ncv, &ntot);
+        /* move the held rows (<= 49) from old positions to new ones: read all, then write */
+        bool has = q < total;
+        int32_t src = 0, dst = 0;
+#pragma unroll
+        for (int32_t t = 0; t < MAXN; t++) {
+            int32_t os = w.bcast(oex, t), oc = w.bcast(ocv, t), ok = w.bcast(okv, t);
+            if (t < pc && q >= os && q < os + oc) src = ok * MAXN + (q - os);
+            int32_t ns = w.bcast(nex, t), nc = w.bcast(ncv, t), nk = w.bcast(nkv, t);
+            if (t < cc && q >= ns && q < ns + nc) dst = nk * MAXN + (q - ns);
+        }
+        HotRow r;
+        if (has) r = load_row(src);
+        w.sync();
+        if (has) {
+            store_row(dst, r);
+            z.rleaf[r.rid] = (IX)(dst / MAXN);
+        }
+        w.sync();
+        if (q < cc) { /* the new leaves' headers, a lane each */
+            nch[nkv] = (int8_t)ncv;
+            npar[nkv] = (IX)parent;
+            nlev[nkv] = 0;
+            nsc[nkv] = -1;
+        }
+        w.sync();
+        for (int32_t ni = 0; ni < cc; ni++) {
+            int32_t nc = w.bcast(ncv, ni);
+            if (nc < MAXN) clear_slots(w.bcast(nkv, ni) * MAXN + nc, MAXN - nc);
+        }
+        int32_t nl = h.nleaf;
+        int32_t delta = cc - pc;
+        if constexpr (TILED) { /* the rope: extra leaves after the kept ones, surplus ones out */
+            for (int32_t i = pc; i < cc; i++) rope_insert_after(w.bcast(nkv, i - 1), w.bcast(nkv, i));
+            for (int32_t i = cc; i < pc; i++) rope_remove(w.bcast(okv, i));
+            int32_t nk[MAXN];
+#pragma unroll
+            for (int32_t i = 0; i < MAXN; i++) nk[i] = w.bcast(nkv, i);
+            leaves_restat(nk, cc);
+        }
+        for (int32_t i = cc; i < pc; i++) free_node(w.bcast(okv, i));
+        if constexpr (!TILED) {
+            /* lorder: [firstPos, firstPos+pc) becomes [firstPos, firstPos+cc) */
+            lorder_shift(firstPos + pc, nl, delta);
+            if (q >= pc && q < cc) {
+                lo[firstPos + q] = (IX)nkv;
+                lp[nkv] = (IX)(firstPos + q);
+            }
+            w.sync();
+        }
+        h.nleaf = nl + delta;
+        if (delta > 0) note_leaves();
+        if (q < cc) z.kids[parent * MAXN + q] = (IX)nkv;
+        w.sync();
+        nch[parent] = (int8_t)cc;
+        return true;
+    }
     /* pack (mergeTree.ts:1401-1453) of `block`'s parent */
     MT_HD void pack(int32_t block0) {
         MT_PROF_SCOPE(PH_PACK);
@@ -3205,6 +3295,9 @@ struct Replica {
         int32_t pc = nch[parent];
         int8_t lvl = nlev[block];
         if (lvl == 0) {
+          if constexpr (W::N >= MAXN * MAXN) {
+            if (!pack_leaves(parent, pc)) return;
+          } else {
             /* scour every sibling leaf, then redistribute their rows over new leaves */
             int32_t total = 0;
             if constexpr (W::N >= MAXN * MAXN) {
@@ -3296,6 +3389,7 @@ struct Replica {
             if (delta > 0) note_leaves();
             for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (IX)newk[i];
             nch[parent] = (int8_t)cc;
+          }
         } else {
             MT_PROF_SCOPE(PH_P2);
             if constexpr (W::N >= MAXN * MAXN) {
