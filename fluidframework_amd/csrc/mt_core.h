@@ -3409,32 +3409,32 @@ struct Replica {
                 if (cc > MAXN - 1) cc = MAXN - 1;
                 if (cc < 1) cc = 1;
                 int32_t base = total / cc, extra = total % cc;
-                int32_t oldk[MAXN];
-                for (int32_t k = 0; k < pc; k++) oldk[k] = w.bcast(cb, k * MAXN);
-                for (int32_t k = 0; k < pc; k++) free_node(oldk[k]);
-                int32_t nbk[MAXN];
+                /* the old children, then the new nodes: lane broadcasts and a lane array (lane ni: new node ni),
+                 * not locally indexed arrays (scratch memory) */
+                for (int32_t k = 0; k < pc; k++) free_node(w.bcast(cb, k * MAXN));
+                int32_t nbv = 0;
                 for (int32_t ni = 0; ni < cc; ni++) {
-                    nbk[ni] = alloc_node(lvl);
-                    if (nbk[ni] < 0) return;
+                    int32_t nb = alloc_node(lvl);
+                    if (nb < 0) return;
+                    nbv = w.writelane(nb, ni, nbv);
                 }
                 /* the first `extra` nodes take base + 1 children */
                 int32_t big = extra * (base + 1);
                 int32_t ni = rank < big ? rank / (base + 1) : extra + (rank - big) / base;
                 int32_t slot = rank < big ? rank - ni * (base + 1) : rank - big - (ni - extra) * base;
-                int32_t nb = -1;
-                for (int32_t k = 0; k < MAXN; k++)
-                    if (k == ni && k < cc) nb = nbk[k];
+                int32_t nb = w.shfl(nbv, ni >= 0 && ni < cc ? ni : 0); /* every lane active: a shuffle */
                 w.sync();
                 if (has) {
                     z.kids[nb * MAXN + slot] = (IX)ch;
                     npar[ch] = (IX)nb;
                 }
                 w.sync();
-                for (int32_t k = 0; k < cc; k++) {
-                    nch[nbk[k]] = (int8_t)(base + (k < extra ? 1 : 0));
-                    npar[nbk[k]] = (IX)parent;
-                    z.kids[parent * MAXN + k] = (IX)nbk[k];
+                if (q < cc) {
+                    nch[nbv] = (int8_t)(base + (q < extra ? 1 : 0));
+                    npar[nbv] = (IX)parent;
+                    z.kids[parent * MAXN + q] = (IX)nbv;
                 }
+                w.sync();
                 nch[parent] = (int8_t)cc;
             } else {
                 IX hold[MAXN * MAXN];
