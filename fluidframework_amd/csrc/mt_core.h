@@ -5053,9 +5053,7 @@ struct Replica {
         return h;
     }
 
-    /* Apply a whole event stream. The records are fetched W::N at a time, one per lane (8 dwords
-     * each), and handed to apply() through lane broadcasts, so the stream costs one global-memory
-     * round trip per W::N events instead of one per event. */
+    /* Apply a whole event stream, one record at a time. */
     MT_HD void replay(const Pools& p) {
         static_assert(sizeof(mt_op_rec) == 32, "op record is 8 dwords");
         hmax = INT32_MIN; /* the heap's largest maxSeq */
@@ -5064,22 +5062,24 @@ struct Replica {
             int32_t m = w.max(i < h.heapN ? hsq[i] : INT32_MIN);
             if (m > hmax) hmax = m;
         }
-        for (int64_t b = 0; b < p.nops; b += W::N) {
-            int64_t i = b + w.lane();
-            int32_t rec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (i < p.nops) __builtin_memcpy(rec, &p.ops[i], sizeof(rec));
-            int64_t cnt = p.nops - b < W::N ? p.nops - b : W::N;
-            for (int64_t k = 0; k < cnt; k++) {
-                int32_t u[8];
-                for (int q = 0; q < 8; q++) u[q] = w.bcast(rec[q], (int)k);
-                mt_op_rec op;
-                __builtin_memcpy(&op, u, sizeof(op));
-                cur = b + k;
-                if constexpr (TILED)
-                    if (pfcur) *(volatile int32_t*)pfcur = (int32_t)cur; /* the prefetch helpers run ahead of it */
-                apply(op, p);
-                if (h.err) return;
+        /* One record per event, read uniformly when its turn comes: nothing is held across apply(). (Reading a
+         * wave's worth of records at once and broadcasting them kept 8 registers live through every event,
+         * which the config-3 kernel spilled to scratch: 333.97 -> 344.63M ops/s without it, r04zr.) */
+        for (int64_t i = 0; i < p.nops; i++) {
+            const int32_t* src = (const int32_t*)&p.ops[i];
+            I4 a0 = ld4(src), a1 = ld4(src + 4);
+            int32_t u[8];
+            for (int q = 0; q < 4; q++) {
+                u[q] = w.uniform(a0.x[q]);
+                u[4 + q] = w.uniform(a1.x[q]);
             }
+            mt_op_rec op;
+            __builtin_memcpy(&op, u, sizeof(op));
+            cur = i;
+            if constexpr (TILED)
+                if (pfcur) *(volatile int32_t*)pfcur = (int32_t)cur; /* the prefetch helpers run ahead of it */
+            apply(op, p);
+            if (h.err) return;
         }
     }
 };
