@@ -133,6 +133,8 @@ def main() -> None:
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (default: host share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--digests-out", default="", help="save the per-document digests (.npy) after the run")
+    ap.add_argument("--order", choices=("cost", "doc"), default="cost",
+                    help="replay dispatch order: longest-first by shard.doc_costs (cost) or document order (doc)")
     ap.add_argument("--gen-cache", default=os.environ.get("MT_GEN_CACHE", ""),
                     help="directory caching generated workloads between runs (profiler passes)")
     args = ap.parse_args()
@@ -183,6 +185,9 @@ def main() -> None:
 
     eng = Engine(batch.ndocs, device=device, **default_caps(ops, config=args.config))
     log("engine created")
+    costs = shard.doc_costs(batch)
+    if args.order == "cost":  # longest-first list schedule of the documents over the GPU's wave slots
+        eng.set_order(np.lexsort((np.arange(batch.ndocs), -costs)).astype(np.int32))
     eng.start_collab(batch.local_long_id)
     eng.submit(batch)  # HtoD once: inputs are resident in HBM for every step
     log("inputs resident in HBM")
@@ -223,6 +228,14 @@ def main() -> None:
     e2e_kernel_ms = step()
     t_e2e = time.perf_counter() - t_e2e
 
+    # per-document replay times of that step (GPU constant clock, 100 MHz): the spread behind the launch's tail
+    tt = eng.doc_times().astype(np.float64)
+    dur = (tt[:, 1] - tt[:, 0]) / 1e5  # ms
+    span = (tt[:, 1].max() - tt[:, 0].min()) / 1e5
+    doc_ms = {"mean": float(dur.mean()), "p50": float(np.median(dur)), "p99": float(np.percentile(dur, 99)),
+              "max": float(dur.max()), "span": span, "order": args.order,
+              "cost_corr": float(np.corrcoef(costs, dur)[0, 1]) if batch.ndocs > 2 and dur.std() > 0 else None,
+              "last_start_frac": float((tt[:, 0].max() - tt[:, 0].min()) / max(1.0, tt[:, 1].max() - tt[:, 0].min()))}
     work = eng.work()  # per doc (sequenced msgs, sum R, sum W) of the last step
     seq_ops = int(work[:, 0].sum())
     alg_bytes = 16 * int(work[:, 1].sum()) + 32 * int(work[:, 2].sum())
@@ -279,6 +292,7 @@ def main() -> None:
                                          "+ 640 B + 32 B x rows written" if args.config == 4 else
                                          "flat scan (BASELINE.md): A(op) = 16 B x rows + 32 B x rows written")},
             "cpu_baseline": cpu,
+            "doc_time_ms": doc_ms,
             "end_to_end": {"value": seq_ops / t_e2e, "unit": "ops/s", "ms": t_e2e * 1000.0,
                            "kernel_ms": e2e_kernel_ms, "rank": 0,
                            "covers": "mt_engine_submit (host bounds checks + H2D of the op logs from pageable "

@@ -103,6 +103,12 @@ struct alignas(16) LRef {
     int32_t rid, off, type;
     int32_t ek; /* the refsByOffset entry it sits in was created by addLocalRef (0: has an `at` list) or by
                    a tombstone slide (1: `before` / `after` only) */
+    /* a removed reference (rid <= REF_FROZEN) also keeps the refsByOffset ENTRY it left: removeLocalRef only
+     * splices the reference out of the entry's lists (localReference.ts:225-264), so the entry stays defined,
+     * with its shape, in its collection and moves with that collection's splits and appends as the live
+     * references do: erid = the row id of the collection holding it now (-1: gone with the collection), eoff
+     * its offset there, ekd its kind (as ek) */
+    int32_t erid, eoff, ekd, _pad;
 };
 enum : int32_t {
     REF_DETACHED = -1,
@@ -138,6 +144,7 @@ struct DocHdr {
     int32_t mkMask;        /* property key slots an annotate changed on a marker (marker_keys_annotated) */
     int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
+    int64_t tStart, tEnd; /* the last replay kernel's start / end for this document (s_memrealtime ticks) */
 };
 /* the int32 fields of DocHdr the replica keeps in registers while it runs; the rarely used ones
  * (nclients, nextSid, errOp, nkeys, hwSlots, gcEpoch, loadPos, ovTop, ovFree, and since round 2 root,
@@ -768,6 +775,12 @@ struct Replica {
                 R[i].off += delta;
             }
             moved += w.sum(mv ? 1 : 0);
+            /* the entries removed references left ride along; a collection that goes away (to < 0: the
+             * segment was removed or unlinked) takes them with it */
+            if (i < n && R[i].rid <= REF_FROZEN && R[i].erid == from && R[i].eoff >= o0) {
+                R[i].erid = to >= 0 ? to : -1;
+                R[i].eoff += delta;
+            }
         }
         w.sync();
         return moved;
@@ -799,6 +812,7 @@ struct Replica {
         return i;
     }
     MT_HD void coll_drop(int32_t rid) { /* segment.localRefs = undefined, or the segment left the tree */
+        refs_move(rid, INT32_MIN, REF_DETACHED, 0); /* the entries of removed references go with it */
         int32_t i = coll_find(rid);
         if (i < 0) return;
         DState* st = d.dstate();
@@ -852,6 +866,8 @@ struct Replica {
             int32_t i = b + w.lane();
             uint64_t m = w.ballot(i < n && R[i].rid == rid && R[i].off == off);
             if (m && k < 0) k = R[b + W::ffs(m)].ek;
+            uint64_t e = w.ballot(i < n && R[i].rid <= REF_FROZEN && R[i].erid == rid && R[i].eoff == off);
+            if (e && k < 0) k = R[b + W::ffs(e)].ekd; /* an entry whose references were all removed */
         }
         return k;
     }
@@ -865,7 +881,7 @@ struct Replica {
         }
         int32_t off = 0;
         int32_t s = containing(pos, h.currentSeq, h.localShort, &off);
-        LRef r = {s >= 0 ? (int32_t)z.rid[s] : REF_DETACHED, s >= 0 ? off : 0, type, 0};
+        LRef r = {s >= 0 ? (int32_t)z.rid[s] : REF_DETACHED, s >= 0 ? off : 0, type, 0, -1, 0, 0, 0};
         if (s >= 0 && entry_kind(r.rid, off) == 1) { /* the reference's addLocalRef throws here: the tree */
             r.rid = REF_GHOST;                            /* is untouched and the reference is not kept */
             d.refs()[n] = r;
@@ -896,6 +912,9 @@ struct Replica {
         if (w.lane() == 0) {
             d.refs()[i].rid = REF_FROZEN - r.rid;
             d.refs()[i].ek = z.rgen[r.rid];
+            d.refs()[i].erid = r.rid; /* the entry it leaves stays (localReference.ts:225-264) */
+            d.refs()[i].eoff = r.off;
+            d.refs()[i].ekd = r.ek;
         }
         w.sync();
     }
@@ -2157,7 +2176,30 @@ struct Replica {
             int32_t nn = alloc_node(lvl);
             if (nn < 0) return -1;
             if (first < 0) first = nn;
-            if (lvl == 0) {
+            if constexpr (W::N >= MAXN) {
+                /* children 4..7 move to the new node in one pass, a lane each: rows (with their leaf link,
+                 * from the ids just read, and the vacated slots' lengths) or child nodes (with their parent) */
+                const int32_t l = w.lane();
+                const bool mv = l < 4;
+                if (lvl == 0) {
+                    HotRow r;
+                    if (mv) r = load_row(n * MAXN + 4 + l);
+                    w.sync();
+                    if (mv) {
+                        store_row(nn * MAXN + l, r);
+                        if ((int32_t)r.rid >= 0) z.rleaf[r.rid] = (IX)nn; /* a slot awaiting its row holds -1 */
+                        z.len(n * MAXN + 4 + l) = 0;
+                    }
+                } else {
+                    int32_t c = mv ? (int32_t)z.kids[n * MAXN + 4 + l] : 0;
+                    w.sync();
+                    if (mv) {
+                        z.kids[nn * MAXN + l] = (IX)c;
+                        npar[c] = (IX)nn;
+                    }
+                }
+                w.sync();
+            } else if (lvl == 0) {
                 move_rows(nn * MAXN, n * MAXN + 4, 4);
                 set_leaf_of_rows(nn, 4);
                 clear_slots(n * MAXN + 4, 4);
@@ -2189,7 +2231,23 @@ struct Replica {
                 zh->root = r;
                 return first;
             }
-            node_insert_child(p, child_index(p, n) + 1, nn);
+            if constexpr (W::N >= MAXN) {
+                /* child_index + node_insert_child in one pass: lane i reads child i of p; the children after n
+                 * move right one place from registers */
+                const int32_t l = w.lane();
+                int32_t cnt = nch[p];
+                int32_t kid = l < MAXN ? (int32_t)z.kids[p * MAXN + (l & (MAXN - 1))] : -1;
+                uint64_t m = w.ballot(l < cnt && kid == n);
+                int32_t idx = (m ? W::ffs(m) : -1) + 1;
+                w.sync();
+                if (l >= idx && l < cnt) z.kids[p * MAXN + l + 1] = (IX)kid;
+                if (l == 0) z.kids[p * MAXN + idx] = (IX)nn;
+                w.sync();
+                nch[p] = (int8_t)(cnt + 1);
+                npar[nn] = (IX)p;
+            } else {
+                node_insert_child(p, child_index(p, n) + 1, nn);
+            }
             if (nch[p] < MAXN) return first;
             n = p;
         }
@@ -2796,7 +2854,93 @@ struct Replica {
         z.keys[zh->nkeys] = key;
         return zh->nkeys++;
     }
+#ifndef MT_PROPS_PAR
+#define MT_PROPS_PAR 1
+#endif
+#ifndef MT_ACKANN_PAR
+#define MT_ACKANN_PAR 1
+#endif
+    /* add_props on the GPU: lane k holds key slot k (its key id, the row's value and pending-key count), lane j
+     * the op's j-th key / value; everything is read in one pass, the fold runs on those registers in the
+     * reference's order (rewrite deletions, then the op's keys in order, new key slots in first-appearance
+     * order), and the row's property state is written back in one pass. Same result as the serial form. */
+    MT_HD void add_props_par(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
+        static_assert(HT::K <= W::N, "a lane per key slot");
+        typename HT::Cold& c = cold(s);
+        const int32_t l = w.lane();
+        const bool kl = l < HT::K;
+        const int32_t kx = kl ? l : 0; /* K is 8 or 24: not a mask */
+        uint32_t fl = z.flags(s);
+        int32_t prw = c.prw;
+        int32_t pv = kl ? (int32_t)c.pv[kx] : 0;
+        int32_t pk = kl ? (int32_t)c.pk[kx] : 0;
+        int32_t key = kl ? (int32_t)z.keys[kx] : -1;
+        int32_t nk = zh->nkeys;
+        int32_t ok = l < nkv ? (int32_t)kv[l].key : -1, ov = l < nkv ? (int32_t)kv[l].value : 0;
+        const bool fresh = !(fl & RF_PROPS);
+        if (fresh) { /* propertyManager / properties created: every slot absent, no pending counts */
+            prw = 0;
+            pv = 0;
+            pk = 0;
+        }
+        if (!(prw > 0 && seq != UNASSIGNED_SEQ && collaborating)) {
+            if (rewrite) {
+                if (collaborating && seq == UNASSIGNED_SEQ) prw++;
+                bool inNew = false;
+                for (int32_t j = 0; j < nkv; j++) {
+                    int32_t vj = w.bcast(ov, j);
+                    if (key == w.bcast(ok, j) && vj != 0 && !(vj & MT_VALUE_FALSY)) inNew = true;
+                }
+                bool modify = seq == UNASSIGNED_SEQ || pk == 0;
+                if (l < nk && pv != 0 && !inNew && modify) pv = 0;
+            }
+            for (int32_t j = 0; j < nkv; j++) {
+                int32_t kj = w.bcast(ok, j), vj = w.bcast(ov, j);
+                uint64_t m = w.ballot(l < nk && key == kj);
+                int32_t k;
+                if (m) {
+                    k = W::ffs(m);
+                } else { /* a new key slot (key_slot) */
+                    if (nk >= HT::K) {
+                        fail(E_CAPACITY);
+                        break;
+                    }
+                    k = nk++;
+                    key = w.writelane(kj, k, key);
+                    if (l == 0) z.keys[k] = (uint16_t)kj;
+                }
+                int32_t pkk = w.bcast(pk, k);
+                if (collaborating) {
+                    if (seq == UNASSIGNED_SEQ) {
+                        if (pkk == 0xFF) {
+                            fail(E_CAPACITY);
+                            break;
+                        }
+                        pk = w.writelane(pkk + 1, k, pk);
+                    } else if (pkk != 0) {
+                        continue;
+                    }
+                }
+                pv = w.writelane(vj, k, pv);
+            }
+            zh->nkeys = nk;
+        }
+        w.sync();
+        if (kl) {
+            c.pv[kx] = (uint16_t)pv;
+            c.pk[kx] = (uint8_t)pk;
+        }
+        if (l == 0) c.prw = (uint8_t)prw;
+        if (fresh && l == 0) z.flags(s) = (uint8_t)(fl | RF_PROPS);
+        w.sync();
+    }
     MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
+        if constexpr (W::N >= 32 && MT_PROPS_PAR) {
+            if (nkv <= W::N) {
+                add_props_par(s, kv, nkv, rewrite, seq, collaborating);
+                return;
+            }
+        }
         typename HT::Cold& c = cold(s); /* the row id is read once, not after every store */
         if (!(z.flags(s) & RF_PROPS)) {
             c.prw = 0;
@@ -4395,15 +4539,46 @@ struct Replica {
     /* ackPendingSegment's per-segment step (mergeTree.ts:1140-1193) for an insert or remove group, one lane per
      * member row (mem: this lane holds a member, rd its row id): the slot lookup, the checks and the row updates
      * in parallel, the LRU entries (addToLRUSet) in member order. Same result as the serial loop in ack(). */
-    MT_HD void ack_rows(int32_t kind, int32_t rd, bool mem, int32_t seq) {
+    MT_HD void ack_rows(int32_t kind, int32_t rd, bool mem, int32_t seq, const mt_kv* kv = nullptr, int32_t nkv = 0,
+                        bool rewrite = false) {
         int32_t leaf = mem ? (int32_t)z.rleaf[rd] : 0;
         int32_t c = nch[leaf];
         int32_t s = -1;
+        /* an annotate's keys: their slots (the doc's key ids, a lane each, read with the rows) */
+        const int32_t l = w.lane();
+        int32_t key = kind == MT_OP_ANNOTATE && l < HT::K ? (int32_t)z.keys[l < HT::K ? l : 0] : -1;
 #pragma unroll
         for (int32_t j = 0; j < MAXN; j++) /* the leaf's row ids: one round trip */
             if (mem && j < c && z.rid[leaf * MAXN + j] == (IX)rd) s = leaf * MAXN + j;
         bool bad = mem && s < 0;
         bool ok = mem && s >= 0;
+        if (kind == MT_OP_ANNOTATE) { /* ackPendingProperties (segmentPropertiesManager.ts:19-33), a lane per row */
+            if (ok && !(z.flags(s) & RF_PROPS)) bad = true;
+            typename HT::Cold& cr = d.cold()[ok ? rd : 0];
+            if (ok) {
+                int32_t ng = z.ng(s);
+                if (ng < 1) bad = true;
+                if (ng > 0) z.ng(s) = (uint8_t)(ng - 1);
+                if (rewrite) cr.prw = (uint8_t)(cr.prw - 1);
+            }
+            for (int32_t j = 0; j < nkv; j++) {
+                int32_t kj = kv[j].key;
+                uint64_t m = w.ballot(l < zh->nkeys && key == kj);
+                int32_t k = m ? W::ffs(m) : key_slot((uint16_t)kj);
+                if (k < 0) return;
+                if (!m) key = w.writelane(kj, k, key);
+                if (ok && cr.pk[k]) cr.pk[k] = (uint8_t)(cr.pk[k] - 1);
+            }
+            if (w.ballot(bad)) fail(E_ASSERT);
+            w.sync();
+            uint64_t om = w.ballot(ok);
+            while (om) {
+                int32_t q = W::ffs(om);
+                om &= om - 1;
+                add_lru(w.bcast(s, q), seq);
+            }
+            return;
+        }
         if (ok) {
             int32_t ng = z.ng(s);
             if (ng < 1) bad = true;
@@ -4440,8 +4615,9 @@ struct Replica {
                 int32_t rd = i < mn ? d.mrid()[i] : 0;
                 uint64_t msk = w.ballot(i < mn && d.mgid()[i] == gid);
                 if constexpr (W::N >= 64) {
-                    if (kind == MT_OP_INSERT || kind == MT_OP_REMOVE) { /* a lane per member row; LRU entries in member order */
-                        if (msk) ack_rows(kind, rd, (msk >> w.lane()) & 1, seq);
+                    if (kind == MT_OP_INSERT || kind == MT_OP_REMOVE || (MT_ACKANN_PAR && kind == MT_OP_ANNOTATE)) {
+                        /* a lane per member row; LRU entries in member order */
+                        if (msk) ack_rows(kind, rd, (msk >> w.lane()) & 1, seq, kv, nkv, rewrite);
                         continue;
                     }
                 }

@@ -119,6 +119,27 @@ __device__ inline void skel_lite_move(SkelLite<HT>& k, HT& z, bool in) {
     }
 }
 
+/* Per-launch extras of the replay kernels: the profiling build's per-document phase clocks, and the dispatch
+ * order (workgroup b replays document order[b]; the hardware dispatches workgroups in index order as slots free
+ * up, so a longest-first order is list scheduling by cost, mt_engine_set_order). */
+struct ReplayAux {
+    uint64_t* prof;
+    const int32_t* order;
+};
+__device__ inline int64_t aux_doc(const ReplayAux& a) { return a.order ? a.order[blockIdx.x] : (int64_t)blockIdx.x; }
+/* the document's replay start / end on the constant-rate clock (s_memrealtime, 100 MHz), kept in its image header
+ * (DocHdr.tStart / tEnd: no register stays live for it through the replay; mt_engine_doc_times) */
+template <class HT>
+__device__ inline void doc_stamp(HT* t, int end) {
+    if (threadIdx.x == 0) {
+        int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
+        if (end)
+            t->h.tEnd = now;
+        else
+            t->h.tStart = now;
+    }
+}
+
 /* K1-K4 fused: the whole event stream of a document, one wave per document. LDS = true stages the
  * whole small-profile hot image in LDS; otherwise the image stays in HBM and only the skeleton and
  * the heap (Skel, 3.5 KB for the small profile) are staged. */
@@ -129,9 +150,11 @@ template <class HT, bool LDS, int MINW = 1, int SKM = 1, int VAR = 0, bool DL = 
 __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
-                                              const int64_t* kv_off, uint64_t* prof) {
-    int64_t d = blockIdx.x;
-    if (d >= ndocs) return;
+                                              const int64_t* kv_off, ReplayAux aux) {
+    if ((int64_t)blockIdx.x >= ndocs) return;
+    const int64_t d = aux_doc(aux);
+    uint64_t* prof = aux.prof;
+    (void)prof;
     Pools p;
     p.ops = ops + op_off[d];
     p.nops = op_off[d + 1] - op_off[d];
@@ -139,6 +162,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
     p.props = props + props_off[d];
     p.kv = kv + kv_off[d];
     Doc<HT> v = st.doc(d);
+    doc_stamp(v.t, 0);
     if constexpr (LDS) {
         __shared__ __attribute__((aligned(16))) HT hot;
         HT* g = v.t;
@@ -195,6 +219,7 @@ __global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs
             for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
 #endif
     }
+    doc_stamp(v.t, 1);
 }
 
 /* Config 4 (large documents, the tiled profile): one workgroup per document, which has the CU's LDS to
@@ -300,7 +325,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
                                                      const int64_t* op_off, const uint16_t* text,
                                                      const int64_t* text_off, const mt_props_rec* props,
                                                      const int64_t* props_off, const mt_kv* kv, const int64_t* kv_off,
-                                                     uint64_t* prof) {
+                                                     ReplayAux aux) {
     static_assert(HT::TILED, "tiled profile only");
     constexpr int NCH = HT::TL::NCH, WCAP = HT::TL::WCAP;
     __shared__ int32_t cdel[NCH];
@@ -312,9 +337,12 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     __shared__ __attribute__((aligned(16))) uint8_t lwgen[WCAP];
     __shared__ int32_t lwslot[WCAP];
     __shared__ int32_t pfcur, pfdone, pfsink; /* the replaying wave's record, its end, the helpers' sink */
-    int64_t d = blockIdx.x;
-    if (d >= ndocs) return;
+    if ((int64_t)blockIdx.x >= ndocs) return;
+    const int64_t d = aux_doc(aux);
+    uint64_t* prof = aux.prof;
+    (void)prof;
     Doc<HT> v = st.doc(d);
+    if (threadIdx.x < WG) doc_stamp(v.t, 0);
     auto& tl = v.t->tl;
     const bool replayer = threadIdx.x < WG;
     if (replayer) {
@@ -374,6 +402,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         wave_copy(tl.wrid, lwrid, WCAP);
         wave_copy((int32_t*)tl.wgen, (const int32_t*)lwgen, WCAP / 4);
         wave_copy(tl.wslot, lwslot, WCAP);
+        doc_stamp(v.t, 1);
     }
 }
 
@@ -532,7 +561,9 @@ __global__ __launch_bounds__(WG) void k_seg(Store<HT> st, int64_t doc, int32_t m
         }
     } else if (mode == 6) {
         int32_t s = -1, off = 0;
-        for (int32_t k = 0; s < 0 && r.kvalid(k); k = r.knext(k)) { /* walkAllSegments: the first match */
+        /* assert(localSeq <= collabWindow.localSeq) (permutationvector.ts:199 -> client.ts:676): res[0] stays 0 */
+        const bool inRange = b <= r.zh->localSeq;
+        for (int32_t k = 0; inRange && s < 0 && r.kvalid(k); k = r.knext(k)) { /* walkAllSegments: the first match */
             int32_t n = r.leaf_at(k), c = r.nch[n];
             int32_t j = threadIdx.x;
             bool hit = false;
@@ -601,10 +632,15 @@ __global__ __launch_bounds__(WG) void k_refpos(Store<HT> st, int64_t ndocs, int3
 
 /* per-doc header fields: errors, stats, roofline work counters */
 template <class HT>
-__global__ void k_hdr(Store<HT> st, int64_t ndocs, int32_t* err, int32_t* err_op, int32_t* stats4, int64_t* work3) {
+__global__ void k_hdr(Store<HT> st, int64_t ndocs, int32_t* err, int32_t* err_op, int32_t* stats4, int64_t* work3,
+                      int64_t* times2) {
     int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= ndocs) return;
     const DocHdr& h = st.doc(d).t->h;
+    if (times2) {
+        times2[2 * d] = h.tStart;
+        times2[2 * d + 1] = h.tEnd;
+    }
     if (err) err[d] = h.err;
     if (err_op) err_op[d] = h.errOp;
     if (stats4) {
@@ -666,6 +702,7 @@ struct mt_engine {
     float last_ms = 0.f;
     bool staged = false;
     DevBuf ops_buf, op_off, text, text_off, props, props_off, kv, kv_off, tmp, local_ids, prof;
+    DevBuf order;    /* dispatch order of the replay kernel (empty: document order) */
     bool collab = false;
     std::string err;
     /* perspective floors (persp_refused): per document, the greatest refSeq each long client has sent a
@@ -721,7 +758,7 @@ struct ProfOps {
     int32_t (*init)(mt_engine* e);                                    /* k_init (+ k_start_collab) */
     int32_t (*start_collab)(mt_engine* e); /* k_start_collab from local_ids (ids, minSeq, currentSeq per doc) */
     int32_t (*replay)(mt_engine* e);                                  /* k_replay over the staged batch */
-    int32_t (*hdr)(mt_engine* e, int32_t* de, int32_t* deo, int32_t* ds, int64_t* dw);
+    int32_t (*hdr)(mt_engine* e, int32_t* de, int32_t* deo, int32_t* ds, int64_t* dw, int64_t* dt);
     int32_t (*digest)(mt_engine* e, uint64_t* dout);
     int32_t (*dump)(mt_engine* e, int64_t doc, uint8_t* dbuf, int64_t cap, int64_t* dn);
     /* the reads take the perspective floor of persp_refused (the host's per-client refSeq bound) */
@@ -755,7 +792,8 @@ static inline int32_t launch_replay(mt_engine* e, K kern, int block = WG) {
     hipLaunchKernelGGL(kern, docs_grid(e->ndocs), dim3(block), 0, e->stream, store_of<HT>(e), e->ndocs,
                        (const mt_op_rec*)e->ops_buf.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
                        (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p, (const int64_t*)e->props_off.p,
-                       (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p, (uint64_t*)e->prof.p);
+                       (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p,
+                       ReplayAux{(uint64_t*)e->prof.p, (const int32_t*)e->order.p});
     return launch_check(e, "k_replay");
 }
 
@@ -776,9 +814,9 @@ struct Launch {
                            e->ndocs, (const int32_t*)e->local_ids.p);
         return launch_check(e, "k_start_collab");
     }
-    static int32_t hdr(mt_engine* e, int32_t* de, int32_t* deo, int32_t* ds, int64_t* dw) {
+    static int32_t hdr(mt_engine* e, int32_t* de, int32_t* deo, int32_t* ds, int64_t* dw, int64_t* dt) {
         hipLaunchKernelGGL((k_hdr<HT>), flat_grid(e->ndocs), dim3(256), 0, e->stream, store_of<HT>(e), e->ndocs, de,
-                           deo, ds, dw);
+                           deo, ds, dw, dt);
         return launch_check(e, "k_hdr");
     }
     static int32_t digest(mt_engine* e, uint64_t* dout) {

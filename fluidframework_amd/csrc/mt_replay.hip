@@ -88,7 +88,7 @@ void mt_engine_destroy(mt_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->borrowed) e->text.p = e->props.p = e->kv.p = nullptr; /* the parent's */
     DevBuf* bufs[] = {&e->ops_buf, &e->op_off, &e->text, &e->text_off, &e->props,     &e->props_off,
-                      &e->kv,     &e->kv_off, &e->tmp,  &e->local_ids, &e->prof};
+                      &e->kv,     &e->kv_off, &e->tmp,  &e->local_ids, &e->prof, &e->order};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (e->mem) (void)hipFree(e->mem);
@@ -294,21 +294,24 @@ int32_t mt_engine_sync(mt_engine* e) {
     return MT_OK;
 }
 
-static int32_t read_hdr(mt_engine* e, int32_t* err, int32_t* err_op, int32_t* stats4, int64_t* work3) {
+static int32_t read_hdr(mt_engine* e, int32_t* err, int32_t* err_op, int32_t* stats4, int64_t* work3,
+                        int64_t* times2 = nullptr) {
     HIPCHK(e, hipSetDevice(e->device));
     int64_t n = e->ndocs;
-    int32_t rc = ensure(e, e->tmp, (size_t)n * (4 + 4 + 16 + 24));
+    int32_t rc = ensure(e, e->tmp, (size_t)n * (4 + 4 + 16 + 24 + 16));
     if (rc) return rc;
     int32_t* de = (int32_t*)e->tmp.p;
     int32_t* deo = de + n;
     int32_t* ds = deo + n;
     int64_t* dw = (int64_t*)(ds + 4 * n);
-    rc = e->ops->hdr(e, de, deo, ds, dw);
+    int64_t* dt = dw + 3 * n;
+    rc = e->ops->hdr(e, de, deo, ds, dw, times2 ? dt : nullptr);
     if (rc) return rc;
     if (err) HIPCHK(e, hipMemcpyAsync(err, de, 4 * n, hipMemcpyDeviceToHost, e->stream));
     if (err_op) HIPCHK(e, hipMemcpyAsync(err_op, deo, 4 * n, hipMemcpyDeviceToHost, e->stream));
     if (stats4) HIPCHK(e, hipMemcpyAsync(stats4, ds, 16 * n, hipMemcpyDeviceToHost, e->stream));
     if (work3) HIPCHK(e, hipMemcpyAsync(work3, dw, 24 * n, hipMemcpyDeviceToHost, e->stream));
+    if (times2) HIPCHK(e, hipMemcpyAsync(times2, dt, 16 * n, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return MT_OK;
 }
@@ -463,6 +466,35 @@ int32_t mt_engine_stats(mt_engine* e, int32_t* out4) {
     scatter(out4, a, e->pro_docs, 4);
     return MT_OK;
 }
+int32_t mt_engine_doc_times(mt_engine* e, int64_t* out2) {
+    if (!e || !out2) return MT_E_ARG;
+    int32_t rc = read_hdr(e, nullptr, nullptr, nullptr, nullptr, out2);
+    if (rc || !promoted(e)) return rc;
+    std::vector<int64_t> a(2 * e->pro_docs.size());
+    if ((rc = mt_engine_doc_times(e->over, a.data()))) return rc;
+    scatter(out2, a, e->pro_docs, 2);
+    return MT_OK;
+}
+
+int32_t mt_engine_set_order(mt_engine* e, const int32_t* order) {
+    if (!e) return MT_E_ARG;
+    HIPCHK(e, hipSetDevice(e->device));
+    if (!order) {
+        if (e->order.p) (void)hipFree(e->order.p);
+        e->order = DevBuf();
+        return MT_OK;
+    }
+    std::vector<char> seen((size_t)e->ndocs, 0);
+    for (int64_t i = 0; i < e->ndocs; i++) {
+        if (order[i] < 0 || order[i] >= e->ndocs || seen[(size_t)order[i]]) return MT_E_ARG; /* a permutation */
+        seen[(size_t)order[i]] = 1;
+    }
+    if (ensure(e, e->order, sizeof(int32_t) * e->ndocs)) return MT_E_NOMEM;
+    HIPCHK(e, hipMemcpyAsync(e->order.p, order, sizeof(int32_t) * e->ndocs, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return MT_OK;
+}
+
 int32_t mt_engine_work(mt_engine* e, int64_t* out3) {
     if (!e || !out3) return MT_E_ARG;
     int32_t rc = read_hdr(e, nullptr, nullptr, nullptr, out3);
@@ -662,7 +694,8 @@ int32_t mt_engine_handle_to_position(mt_engine* e, int64_t doc, int32_t handle, 
     int32_t r[MT_SEGQ_N];
     int32_t rc = seg_query(e, doc, 6, handle, local_seq, 0, -1, r);
     if (rc) return rc;
-    if (r[0] != 1) return MT_E_ARG; /* assert(isHandleValid(containingSegment.start)) */
+    /* assert(localSeq <= collabWindow.localSeq) (client.ts:676) and assert(isHandleValid(containingSegment.start)) */
+    if (r[0] != 1) return MT_E_ARG;
     *out = r[1];
     return MT_OK;
 }

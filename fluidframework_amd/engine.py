@@ -65,6 +65,8 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_run.argtypes = [vp]
         L.mt_engine_reset.argtypes = [vp]
         L.mt_engine_work.argtypes = [vp, vp]
+        L.mt_engine_doc_times.argtypes = [vp, vp]
+        L.mt_engine_set_order.argtypes = [vp, vp]
         L.mt_engine_sync.argtypes = [vp]
         L.mt_engine_promoted.argtypes = [vp, vp, i64]
         L.mt_engine_promoted.restype = i64
@@ -177,6 +179,23 @@ class Engine:
         out = np.zeros((self.ndocs, 3), np.int64)
         self._check(self.L.mt_engine_work(self.h, _p(out)), "work")
         return out
+
+    def doc_times(self) -> np.ndarray:
+        """(ndocs, 2) int64: each document's replay start / end in the last run, GPU constant-clock ticks
+        (100 MHz, s_memrealtime)."""
+        out = np.zeros((self.ndocs, 2), np.int64)
+        self._check(self.L.mt_engine_doc_times(self.h, _p(out)), "doc_times")
+        return out
+
+    def set_order(self, order=None):
+        """Dispatch order of the replay kernel (a permutation of the documents; None: document order)."""
+        if order is None:
+            self._check(self.L.mt_engine_set_order(self.h, None), "set_order")
+            return
+        o = np.ascontiguousarray(order, np.int32)
+        if o.shape != (self.ndocs,):
+            raise EngineError("set_order needs one entry per document")
+        self._check(self.L.mt_engine_set_order(self.h, _p(o)), "set_order")
 
     def run(self):
         self._check(self.L.mt_engine_run(self.h), "run")

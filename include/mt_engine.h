@@ -94,6 +94,14 @@ int32_t mt_engine_reset(mt_engine* e);
 /* Per-doc work counters for roofline accounting: out3[3d..3d+2] = (sequenced messages applied,
  * sum over them of rows in the table before the message, rows written). */
 int32_t mt_engine_work(mt_engine* e, int64_t* out3);
+/* Per document, when the last replay's workgroup for it started and finished: out2[2d], out2[2d + 1] in ticks of
+ * the GPU's constant 100 MHz clock (s_memrealtime; comparable across documents of one device): the per-document
+ * time spread and the launch's tail. Promoted documents report their replay in the larger profile. */
+int32_t mt_engine_doc_times(mt_engine* e, int64_t* out2);
+/* Dispatch order of the replay kernel: workgroup b replays document order[b] (a permutation of [0, ndocs); NULL
+ * restores document order). The GPU dispatches workgroups in index order as slots free up, so the documents in
+ * decreasing order of expected cost make a longest-first list schedule. No effect on results. */
+int32_t mt_engine_set_order(mt_engine* e, const int32_t* order);
 
 /* Per-doc latched error code (MT_E_*) and index of the event that raised it (-1 if none). */
 int32_t mt_engine_errors(mt_engine* e, int32_t* err, int32_t* err_op);
@@ -162,7 +170,8 @@ int32_t mt_engine_adjust_position(mt_engine* e, int64_t doc, int32_t pos, int32_
                                   int32_t* out);
 /* PermutationVector.handleToPosition(handle, localSeq) (permutationvector.ts:198-253; matrix.ts:532-533): the
  * segment whose allocated handles hold `handle` (walkAllSegments order), at findReconnectionPostition(segment,
- * localSeq) + offset (client.ts:675-705). MT_E_ARG if no segment holds it (the reference's assert). */
+ * localSeq) + offset (client.ts:675-705). MT_E_ARG if no segment holds it or local_seq is past the replica's
+ * collabWindow.localSeq (the reference's asserts, permutationvector.ts:199, client.ts:676). */
 int32_t mt_engine_handle_to_position(mt_engine* e, int64_t doc, int32_t handle, int32_t local_seq, int32_t* out);
 /* Client.getMarkerFromId / MergeTree.getMarkerFromId (client.ts:312, mergeTree.ts:1965-1967): the marker whose
  * property id_key holds id_value (the engine's lookup, with mt_engine_pos_from_relative_pos's limits: several

@@ -77,3 +77,30 @@ def test_gpu_handles_match_reference():
     assert np.array_equal(eng.digests(), z["digests"])
     for d in range(b.ndocs):
         assert np.array_equal(eng.handle_table(d), table(z, d)), f"doc {d}"
+
+
+@pytest.mark.gpu
+def test_gpu_handle_to_position_local_seq_bound():
+    """handleToPosition(handle, localSeq) asserts localSeq <= collabWindow.localSeq (permutationvector.ts:199,
+    client.ts:676): MT_E_ARG past the replica's localSeq, an answer at it."""
+    import struct
+    from fluidframework_amd.engine import Engine, EngineError
+    z, c, caps, b = load()
+    eng = Engine(b.ndocs, **dict(c, pcap=PCAP))
+    eng.start_collab(b.local_long_id)
+    eng.replay(b)
+    checked = 0
+    for d in range(b.ndocs):
+        t = table(z, d)
+        alloc = [h for h in range(1, len(t)) if t[h] == 0]  # allocated handles (free-list entries are non-zero)
+        if not alloc:
+            continue
+        local_seq = struct.unpack_from("<6i", eng.dump(d))[2]  # dump header: currentSeq, minSeq, localSeq, ...
+        try:
+            eng.handle_to_position(d, alloc[0], local_seq)
+        except EngineError:
+            continue  # the handle's segment left the tree (removed and unlinked): the reference asserts too
+        with pytest.raises(EngineError):
+            eng.handle_to_position(d, alloc[0], local_seq + 1)
+        checked += 1
+    assert checked > 0

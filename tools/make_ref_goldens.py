@@ -300,6 +300,22 @@ def run_refs(rb, d: str, node: str):
     return nref, pos, digests, inside, past
 
 
+def make_refentry(node: str) -> None:
+    """tests/golden/refentry_kat.npz: the refsByOffset-entry KATs (tests/refs_entry_logs.py) replayed by the
+    reference: LocalReference.toPosition() of every reference (-2: addLocalReference threw) and the digests."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import refs_entry_logs as rel
+    rb = rel.batch()
+    nref, pos, digests, _, _ = run_refs(rb, os.path.join(SCRATCH, "refentry"), node)
+    np.savez_compressed(
+        os.path.join(GOLDEN, "refentry_kat.npz"), log_sha256=log_sha(rb), nref=nref, positions=pos, digests=digests,
+        source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                "tools/ref_replay.mjs: LocalReference + Client.addLocalReference / removeLocalReference, "
+                "toPosition() at the end"))
+    print(f"refentry_kat: {rb.ndocs} docs, {int(nref.sum())} references, {int((pos == -2).sum())} the reference "
+          f"could not add, {int((pos == -1).sum())} detached", flush=True)
+
+
 def make_refs(names, node: str, removals: bool = False) -> None:
     """tests/golden/refrefs_<set>.npz: local references (MT_OP_REF records injected by tests/refs_inject.py)
     replayed by the reference, then up to 4 insertAtReferencePositionLocal records per document appended
@@ -720,6 +736,7 @@ def main() -> None:
     ap.add_argument("--handles", action="store_true", help="write the PermutationVector handle fixture only")
     ap.add_argument("--relpos", action="store_true", help="write the relative-position fixture (refrelpos.npz) only")
     ap.add_argument("--tree", action="store_true", help="write the MergeTree-level record fixtures (reftree_*.npz) only")
+    ap.add_argument("--refentry", action="store_true", help="write the refsByOffset-entry KAT fixture only")
     ap.add_argument("--unref", action="store_true", help="write the removeLocalReference fixtures (refunref_*.npz) only")
     ap.add_argument("--persp", action="store_true", help="write the past-perspective read fixtures (refpersp_*.npz) only")
     ap.add_argument("--replaytool", action="store_true", help="write the client replay tool fixture only")
@@ -751,6 +768,9 @@ def main() -> None:
         return
     if args.refs:
         make_refs([n for n in args.sets.split(",") if n in REF_SETS], args.node)
+        return
+    if args.refentry:
+        make_refentry(args.node)
         return
     if args.unref:
         make_refs([n for n in args.sets.split(",") if n in REF_SETS], args.node, removals=True)
