@@ -666,6 +666,33 @@ struct Replica {
         w.sync();
         return f;
     }
+    /* HandleTable.load(handleTableData) (handletable.ts:84-86) of PermutationVector.load (permutationvector.ts:270-
+     * 275): entries [pos1, pos1 + text_len / 2) of the summary's `handles` array (each as two UTF-16 units of the
+     * text pool, low then high), whose length is pos2 (mt_oplog.h MT_NOOP_HTLOAD) */
+    MT_HD void ht_load(const mt_op_rec& op, const Pools& p) {
+        if (!ht_on()) {
+            fail(E_UNSUPPORTED);
+            return;
+        }
+        int32_t first = op.pos1, len = op.pos2, n = op.text_len / 2;
+        if (first < 0 || len < 1 || first + n > len) {
+            fail(E_ASSERT);
+            return;
+        }
+        if (len - 1 > d.caps.pcap) {
+            fail(E_CAPACITY);
+            return;
+        }
+        int32_t* t = d.ht();
+        const uint16_t* u = p.text + op.text_off;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            if (i < n) t[first + i] = (int32_t)((uint32_t)u[2 * i] | ((uint32_t)u[2 * i + 1] << 16));
+        }
+        w.sync();
+        d.dstate()->hlen = len;
+        w.sync();
+    }
     /* onMaintenance UNLINK (permutationvector.ts:338-363): HandleTable.free (56-59) of start .. start + len - 1
      * in increasing order */
     MT_HD void ht_free_range(int32_t start, int32_t len) {
@@ -3852,7 +3879,8 @@ struct Replica {
             I4 c0;
             c0.x[0] = localSeq;
             c0.x[1] = 0;
-            c0.x[2] = marker ? op.pos2 : perm ? 0 : off;
+            /* a PermutationSegment's start: unallocated, except a loaded body segment's (APPEND records carry it) */
+            c0.x[2] = marker ? op.pos2 : perm ? ((op.kind & MT_OP_KIND_MASK) == MT_OP_APPEND ? (int32_t)op.text_off : 0) : off;
             c0.x[3] = 0;
             st4(&c, c0);
             c.ovl = 0;
@@ -4738,6 +4766,8 @@ struct Replica {
                 if constexpr (DL) {
                     if (op.seg_kind == MT_NOOP_SPLIT)
                         split_range(op.pos1, op.pos2);
+                    else if (op.seg_kind == MT_NOOP_HTLOAD)
+                        ht_load(op, p);
                     else
                         alloc_handle(op.pos1);
                 } else {
@@ -4907,7 +4937,7 @@ struct Replica {
         if (marker) {
             cold(s).toff = (uint32_t)op.pos2;
         } else if (perm) {
-            cold(s).toff = 0;
+            cold(s).toff = op.text_off; /* a loaded PermutationSegment's start ([length, start] spec): 0 = unallocated */
         } else {
             cold(s).toff = (uint32_t)off;
             int32_t last = arena_copy(arena_base(zh->arenaSide) + off, p.text + op.text_off, L);

@@ -172,6 +172,9 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
                 if (kind == MT_OP_INSERT && (o.seg_kind & 0x7F) == MT_SEG_TEXT &&
                     text_off[d] + (int64_t)o.text_off + o.text_len > text_units)
                     return false;
+                if (kind == MT_OP_NOOP && (o.kind & MT_OPF_LOCAL) && o.seg_kind == MT_NOOP_HTLOAD &&
+                    text_off[d] + (int64_t)o.text_off + o.text_len > text_units)
+                    return false;
                 if ((o.seg_kind & MT_SEG_RELPOS) &&
                     text_off[d] + (int64_t)o.text_off + o.text_len + MT_RELPOS_UNITS > text_units)
                     return false;

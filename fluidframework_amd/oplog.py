@@ -107,7 +107,10 @@ def concat_records(a, b):
     ao, at, ap, akv = a
     bo, bt, bp, bkv = b
     bo = bo.copy()
-    bo["text_off"] += np.uint32(len(at))
+    # a PermutationSegment load record's text_off is its start handle, not a pool reference (mt_oplog.h)
+    k = bo["kind"] & 7
+    handle = ((k == OP_RELOAD) | (k == OP_APPEND)) & ((bo["seg_kind"] & 0x7F) == SEG_PERM)
+    bo["text_off"][~handle] += np.uint32(len(at))
     has = bo["props"] != 0
     bo["props"][has] += np.uint16(len(ap))
     bp = bp.copy()

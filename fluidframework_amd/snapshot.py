@@ -355,14 +355,42 @@ def _chunks(tree: dict):
     return head, body, catchup
 
 
+NOOP_HTLOAD = 2  # seg_kind of a local NOOP record loading PermutationVector's HandleTable (mt_oplog.h MT_NOOP_HTLOAD)
+
+
+def handle_table_records(log: ol.DocLog, handles) -> None:
+    """PermutationVector.load's HandleTable.load(handleTableData) (permutationvector.ts:270-275, handletable.ts:84-86):
+    the summary's `handles` array (handles[0] = the free-list head, then 0 for an allocated handle or the next
+    free one) as MT_NOOP_HTLOAD records, each entry two text-pool units (low, high), up to 16,383 entries a
+    record (text_len is 16 bits)."""
+    h = [int(x) for x in handles]
+    step = 16383
+    for first in range(0, len(h), step):
+        part = h[first: first + step]
+        toff = len(log.text)
+        for v in part:
+            v &= 0xFFFFFFFF
+            log.text.extend((v & 0xFFFF, v >> 16))
+        log.add(ol.OP_NOOP | ol.OPF_LOCAL, pos1=first, pos2=len(h))
+        r = list(log.ops[-1])
+        r[1], r[8], r[9] = NOOP_HTLOAD, toff, 2 * len(part)  # seg_kind, text_off, text_len
+        log.ops[-1] = tuple(r)
+
+
 def load_records(tree: dict, log: ol.DocLog, client_index, local_client: Optional[str] = "snapshot",
-                 catchup: bool = True) -> dict:
+                 catchup: bool = True, handle_table=None, perm_vector: bool = False) -> dict:
     """Append a snapshot's load records to `log` (one document's event stream); returns the header
     metadata. `client_index(name)` maps a long client id to the batch's long-client index;
     `local_client` is the id startOrUpdateCollaboration gets (None: a detached load, no collaboration,
     snapshotLoader.ts:135-151). `catchup` False leaves out the catch-up messages a legacy summary carries (what
-    TestClient.createFromSnapshot does: it awaits them but applies none, testClient.ts:57-73)."""
+    TestClient.createFromSnapshot does: it awaits them but applies none, testClient.ts:57-73).
+    SharedMatrix vectors: `handle_table` = the summary's handleTable blob (loaded first, as PermutationVector.load
+    does); PermutationSegment specs keep their allocated start ([length, start]), except that with `perm_vector`
+    a body segment's start is reset as PermutationVector's onDelta INSERT resets every inserted segment's
+    (permutationvector.ts:297-309: loadBody inserts through insertSegments, whose delta callback fires)."""
     head, chunks, ops = _chunks(tree)
+    if handle_table is not None:
+        handle_table_records(log, handle_table)
     catchup = ops if catchup else []
     md = head["headerMetadata"]
     body = [spec for c in chunks for spec in c["segments"]]
@@ -402,11 +430,15 @@ def load_records(tree: dict, log: ol.DocLog, client_index, local_client: Optiona
         common = dict(client=client, seq=seq, ref_seq=rseq, min_seq=rcl, pos1=countdown)
         if isinstance(spec, str):
             log.add(kind, text=spec, **common)
-        elif isinstance(spec, list):  # PermutationSegment [length, start]
-            if len(spec) > 1 and spec[1] is not None and spec[1] >= 1:
-                raise ValueError("a PermutationSegment with allocated handles: loading the matrix's HandleTable "
-                                 "blob with it is not modelled")
+        elif isinstance(spec, list):  # PermutationSegment [length, start] (permutationvector.ts:40-43, 75-77)
+            start = spec[1] if len(spec) > 1 and spec[1] is not None and spec[1] >= 1 else 0
+            if perm_vector and (kind & 7) == ol.OP_APPEND:
+                start = 0
             log.add(kind, perm=spec[0], **common)
+            if start:
+                r = list(log.ops[-1])
+                r[8] = int(start)  # text_off: the loaded segment's start handle (mt_oplog.h)
+                log.ops[-1] = tuple(r)
         elif "marker" in spec:
             log.add(kind, marker=spec["marker"]["refType"], props=spec.get("props"), **common)
         else:

@@ -55,7 +55,8 @@ enum {
  *           seq); consecutive segments without seq/client go in one batch insertSegments call whose
  *           members after the first are flagged MT_OPF_GROUPED (placed at the previous member's
  *           position + its length, blockInsert mergeTree.ts:2226-2256).
-     * Segment fields of RELOAD / APPEND: seg_kind, text_off, props; pos2 = the segment's length in
+     * Segment fields of RELOAD / APPEND: seg_kind, text_off (a PERM segment: its start handle, 0 = unallocated),
+     * props; pos2 = the segment's length in
      * UTF-16 units (TEXT) or rows (PERM), a marker's refType (MARKER) — a loaded segment may exceed
      * text_len's 16 bits; seq (0 = UniversalSequenceNumber); client = the spec's long client,
      * MT_CLIENT_NONCOLLAB if absent; ref_seq = removedSeq (> 0) or 0 if not removed; min_seq = the
@@ -76,6 +77,12 @@ enum {
  * at pos1, then at pos2, each only when non-zero, in the local view (client-feature build); 0 is
  * PermutationVector.getAllocatedHandle(pos1) */
 #define MT_NOOP_SPLIT 1
+/* seg_kind of an MT_OP_NOOP | MT_OPF_LOCAL record that loads PermutationVector's HandleTable from a summary
+ * (PermutationVector.load -> HandleTable.load, permutationvector.ts:270-275, handletable.ts:84-86): entries
+ * [pos1, pos1 + text_len / 2) of the `handles` array, each as two text-pool units (low, high), pos2 = the array's
+ * length. A loaded PermutationSegment's start ([length, start] spec) rides in its RELOAD / APPEND record's
+ * text_off (0 = unallocated). Client-feature build with caps.pcap >= length - 1. */
+#define MT_NOOP_HTLOAD 2
 /* A group op (MergeTreeDeltaType.GROUP, ops.ts:33, 100; e.g. SharedString.replaceRange,
  * sequence.ts:464) is one sequenced message carrying several member ops: it is sent as its member
  * records in order, all with the message's client/seq/ref_seq/min_seq, every member but the last

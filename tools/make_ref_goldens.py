@@ -112,13 +112,13 @@ def canonical_tree(tree: dict) -> str:
     return json.dumps({k: json.loads(v) for k, v in blobs.items()}, sort_keys=True, separators=(",", ":"))
 
 
-def run_reference(b: ol.Batch, d: str, node: str, cuts=None, interner=None):
+def run_reference(b: ol.Batch, d: str, node: str, cuts=None, interner=None, extra=()):
     write_batch(b, interner or gen.generator_interner(), d)
     if cuts is not None:
         with open(os.path.join(d, "snapshots.json"), "w") as f:
             json.dump([[i, int(c), int(b.local_long_id[i])] for i, c in enumerate(cuts)], f)
     t0 = time.time()
-    r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d], capture_output=True,
+    r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d, *extra], capture_output=True,
                        text=True)
     if r.returncode != 0:
         raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
@@ -462,6 +462,56 @@ def make_tree(node: str) -> None:
               f"logs' on every document", flush=True)
 
 
+def make_handle_snaps(node: str) -> None:
+    """tests/golden/refhsnap_c5_perm.npz: SharedMatrix vectors summarized with allocated handles and loaded again
+    (VERDICT r4 #5). The refhandles logs (config 5 + getAllocatedHandle records) run under the reference with
+    PermutationVector's bookkeeping (tools/ref_replay.mjs --handles); at a cut with nothing pending the replica is
+    summarized as PermutationVector.snapshot does (SnapshotV1 segments, PermutationSegment specs [length, start],
+    plus the HandleTable blob, permutationvector.ts:256-268), a fresh replica loads both as PermutationVector.load
+    does (HandleTable.load, then Client.load under its delta hooks: loadBody's inserts reset their starts) and
+    applies the rest of the log. Stored: the summaries (trees, blobs), the loaded replicas' final digests (dumps
+    with allocated starts) and HandleTable.snapshot()s, and where the reference could not load or continue."""
+    import handles_inject
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_ref_goldens import caps_for
+    w, ids = SETS["c5_perm"]
+    b = gen.generate(w, ids=ids, threads=8)
+    c = caps_for(w)
+    hb = handles_inject.inject(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
+    cuts = []
+    for i in range(hb.ndocs):  # getAllocatedHandle records are local but never sent: not pending ops
+        ops = hb.doc(i)[0]
+        keep = ~(((ops["kind"] & 7) == ol.OP_NOOP) & ((ops["kind"] & ol.OPF_LOCAL) != 0))
+        idx = np.nonzero(keep)[0]
+        c0 = snapshot_cut(ops[keep], int(hb.local_long_id[i]))
+        cuts.append(int(idx[c0]) if c0 < len(idx) else len(ops))
+    d = os.path.join(SCRATCH, "hsnap")
+    # default chunk size: every summary is one header chunk (with 200-row chunks the reference's own loadBody
+    # throws on all 64 documents: their body chunks hold window segments, snapshotLoader.ts:200-213)
+    dumps, info, secs, snaps = run_reference(hb, d, node, cuts, extra=("--handles",))
+    trees, loaded, tail_err, tail_msgs, load_err, load_msgs = snaps
+    sh = json.load(open(os.path.join(d, "ref_snap_handles.json")))
+    blobs = [np.asarray(sh[str(i)]["blob"], np.int32) for i in range(hb.ndocs)]
+    finals = [np.asarray(sh[str(i)].get("final", []), np.int32) for i in range(hb.ndocs)]
+    nstart = sum(1 for t in trees for v in json.loads(canonical_tree(t)).values() if isinstance(v, dict)
+                 for seg in v.get("segments", v.get("segmentTexts", [])) if isinstance(seg, list) and len(seg) > 1
+                 and seg[1] is not None and seg[1] >= 1)
+    boff = np.cumsum([0] + [len(x) for x in blobs]).astype(np.int64)
+    foff = np.cumsum([0] + [len(x) for x in finals]).astype(np.int64)
+    np.savez_compressed(
+        os.path.join(GOLDEN, "refhsnap_c5_perm.npz"), workload=json.dumps(dataclasses.asdict(w)),
+        doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(hb), cuts=np.asarray(cuts, np.int64),
+        trees=json.dumps(trees), blobs=np.concatenate(blobs), blob_off=boff, finals=np.concatenate(finals), final_off=foff,
+        loaded_digests=np.asarray([fnv1a64(x) for x in loaded], np.uint64), tail_error=tail_err, load_error=load_err,
+        source=("packages/dds/merge-tree/src + matrix handletable.ts (reference, type-erased by tools/ts_erase.py) "
+                "under node by tools/ref_replay.mjs --handles with snapshots.json"),
+    )
+    print(f"refhsnap_c5_perm: {hb.ndocs} docs, {nstart} summarized segments with allocated starts, blobs "
+          f"{min(len(x) for x in blobs)}..{max(len(x) for x in blobs)} entries; {int(load_err.sum())} do not load, "
+          f"{int((tail_err >= 0).sum())} cannot apply their tail: {sorted(set(m for _, m in tail_msgs.values()))[:3]}",
+          flush=True)
+
+
 def make_handles(node: str) -> None:
     """tests/golden/refhandles_c5_perm.npz: config-5 logs (PermutationSegment rows) with injected
     PermutationVector.getAllocatedHandle records (tests/handles_inject.py) replayed by the reference Client with
@@ -736,6 +786,7 @@ def main() -> None:
     ap.add_argument("--handles", action="store_true", help="write the PermutationVector handle fixture only")
     ap.add_argument("--relpos", action="store_true", help="write the relative-position fixture (refrelpos.npz) only")
     ap.add_argument("--tree", action="store_true", help="write the MergeTree-level record fixtures (reftree_*.npz) only")
+    ap.add_argument("--hsnap", action="store_true", help="write the SharedMatrix summary-with-handles fixture only")
     ap.add_argument("--refentry", action="store_true", help="write the refsByOffset-entry KAT fixture only")
     ap.add_argument("--unref", action="store_true", help="write the removeLocalReference fixtures (refunref_*.npz) only")
     ap.add_argument("--persp", action="store_true", help="write the past-perspective read fixtures (refpersp_*.npz) only")
@@ -771,6 +822,9 @@ def main() -> None:
         return
     if args.refentry:
         make_refentry(args.node)
+        return
+    if args.hsnap:
+        make_handle_snaps(args.node)
         return
     if args.unref:
         make_refs([n for n in args.sets.split(",") if n in REF_SETS], args.node, removals=True)

@@ -255,8 +255,7 @@ function applyRange(client, doc, from, to) {
 
 // PermutationVector's handle bookkeeping around the reference Client (permutationvector.ts:124-363, restated:
 // the class itself needs the container runtime), with the reference's own HandleTable (handletable.ts)
-function hookHandles(client, doc) {
-    const table = new HandleTable();
+function hookHandles(client, doc, table = new HandleTable()) {
     handleTables[doc] = table;
     curHandles = table;
     const prevDelta = client.mergeTreeDeltaCallback, prevMaint = client.mergeTreeMaintenanceCallback;
@@ -411,6 +410,7 @@ async function snapshotLegacyDoc(doc, cut, loadLong) {
     } catch (e) {
         return { tree, loaded: Buffer.alloc(0), loadError: String(e && e.message || e) };
     }
+    if (withHandles) snapHandles[doc].final = handleTables[doc].snapshot();
     return { tree, loaded: dump(b) };
 }
 
@@ -431,12 +431,26 @@ const runtimeOf = (clientId) => ({
     IFluidHandleContext: undefined,
     logger: { ...logger, shipAssert(cond, ev) { if (!cond) throw new Error(`shipAssert ${JSON.stringify(ev)}`); } },
 });
+// With --handles the replica is a PermutationVector's: its summary also holds the HandleTable blob
+// (PermutationVector.snapshot, permutationvector.ts:256-268), and the loading replica installs its delta /
+// maintenance hooks over HandleTable.load(blob) before Client.load, as PermutationVector's constructor and load
+// do (129-145, 270-275): loadBody's inserts then reset their segments' starts (onDelta INSERT).
+const snapHandles = {};
+const chunkArg = process.argv.find((x) => x.startsWith("--chunk="));
+const snapChunk = chunkArg ? Number(chunkArg.slice(8)) : 0; // mergeTreeSnapshotChunkSize (snapshotV1.ts:56); 0: default
 async function snapshotDoc(doc, cut, loadLong) {
     const a = replayDoc(doc, opOff[doc] + cut);
+    if (snapChunk > 0) a.mergeTree.options = Object.assign({}, a.mergeTree.options, { mergeTreeSnapshotChunkSize: snapChunk });
     const snap = new SnapshotV1(a.mergeTree, logger);
     snap.extractSync();
     const tree = snap.emit();
     const b = new Client(specToSegment, logger);
+    let blob = null;
+    if (withHandles) {
+        blob = JSON.parse(JSON.stringify(handleTables[doc].snapshot()));
+        hookHandles(b, doc, HandleTable.load(JSON.parse(JSON.stringify(blob))));
+        snapHandles[doc] = { blob };
+    }
     try {
         const { catchupOpsP } = await b.load(runtimeOf(name(loadLong)), storageOf(tree));
         await catchupOpsP;
@@ -448,6 +462,7 @@ async function snapshotDoc(doc, cut, loadLong) {
     } catch (e) { // the loaded replica cannot apply the rest of the log: report where (tail-relative)
         return { tree, loaded: Buffer.alloc(0), tailError: [applying - opOff[doc] - cut, String(e && e.message || e)] };
     }
+    if (withHandles) snapHandles[doc].final = handleTables[doc].snapshot();
     return { tree, loaded: dump(b) };
 }
 
@@ -620,6 +635,7 @@ if (fs.existsSync(spath)) {
     fs.writeFileSync(path.join(dir, "ref_loaded_dumps.bin"), Buffer.concat(loaded));
     fs.writeFileSync(path.join(dir, "ref_loaded_off.bin"), off);
     fs.writeFileSync(path.join(dir, "ref_snapshots.json"), JSON.stringify({ trees, errors: serr, tailErrors, loadErrors }));
+    if (withHandles) fs.writeFileSync(path.join(dir, "ref_snap_handles.json"), JSON.stringify(snapHandles));
 }
 const lpath = path.join(dir, "snapshots_legacy.json");
 if (fs.existsSync(lpath)) {
