@@ -1063,8 +1063,9 @@ struct Replica {
     MT_HD int32_t local_pos(int32_t s) { return position_of(s, h.currentSeq, h.localShort); }
     /* the propertyDeltas addProperties (segmentPropertiesManager.ts:35-111) returns for row s and this
      * annotate, read before the row changes: nd, then (key << 16 | previous value) by key id */
-    MT_HD bool prop_delta(int32_t s, int32_t kid, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collab,
+    MT_HD bool prop_delta(int32_t s, int32_t kid, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collab,
                           int32_t* val) {
+        const bool rewrite = comb == MT_COMBINE_REWRITE;
         bool has = z.flags(s) & RF_PROPS;
         int32_t cv = 0, pd = 0;
         if (has)
@@ -1084,13 +1085,14 @@ struct Replica {
             in = del = true;
             *val = cv;
         }
-        if (inNew && !(collab && seq != UNASSIGNED_SEQ && pd != 0)) { /* deltas[key] = previous ?? null */
+        /* shouldModifyKey: a combining op modifies every key (segmentPropertiesManager.ts:59-65) */
+        if (inNew && (comb >= MT_COMBINE_INCR || !(collab && seq != UNASSIGNED_SEQ && pd != 0))) { /* deltas[key] = previous ?? null */
             in = true;
             *val = del ? 0 : cv;
         }
         return in;
     }
-    MT_HD void prop_deltas(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collab) {
+    MT_HD void prop_deltas(int32_t s, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collab) {
         if ((z.flags(s) & RF_PROPS) && cold(s).prw > 0 && seq != UNASSIGNED_SEQ && collab) {
             dput(-1); /* outstanding local rewrites: addProperties returns undefined */
             return;
@@ -1106,7 +1108,7 @@ struct Replica {
                 if (best == 0x7fffffff) break;
                 last = best;
                 int32_t v = 0;
-                if (!prop_delta(s, best, kv, nkv, rewrite, seq, collab, &v)) continue;
+                if (!prop_delta(s, best, kv, nkv, comb, seq, collab, &v)) continue;
                 nd++;
                 if (pass) dput((int32_t)(((uint32_t)best << 16) | ((uint32_t)v & 0xFFFF)));
             }
@@ -2891,8 +2893,9 @@ struct Replica {
      * the op's j-th key / value; everything is read in one pass, the fold runs on those registers in the
      * reference's order (rewrite deletions, then the op's keys in order, new key slots in first-appearance
      * order), and the row's property state is written back in one pass. Same result as the serial form. */
-    MT_HD void add_props_par(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
+    MT_HD void add_props_par(int32_t s, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collaborating) {
         static_assert(HT::K <= W::N, "a lane per key slot");
+        const bool rewrite = comb == MT_COMBINE_REWRITE;
         typename HT::Cold& c = cold(s);
         const int32_t l = w.lane();
         const bool kl = l < HT::K;
@@ -2944,9 +2947,13 @@ struct Replica {
                             break;
                         }
                         pk = w.writelane(pkk + 1, k, pk);
-                    } else if (pkk != 0) {
+                    } else if (pkk != 0 && comb < MT_COMBINE_INCR) {
                         continue;
                     }
+                }
+                if (comb >= MT_COMBINE_INCR) { /* combine_unsupported: latched, or the value stays */
+                    if (combine_unsupported(comb, w.bcast(pv, k))) break;
+                    continue;
                 }
                 pv = w.writelane(vj, k, pv);
             }
@@ -2961,10 +2968,21 @@ struct Replica {
         if (fresh && l == 0) z.flags(s) = (uint8_t)(fl | RF_PROPS);
         w.sync();
     }
-    MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq, bool collaborating) {
+    /* Properties.combine (properties.ts:26-59) as addProperties calls it (segmentPropertiesManager.ts:96-97): with
+     * newValue still undefined. "incr" makes the key's value NaN (current + undefined; a string
+     * gets "undefined" appended); "consensus" over an absent value (no defaultValue: wire.py refuses one) makes an
+     * {value: undefined, seq} object, over a present one returns it unchanged. Values the engine cannot hold latch
+     * E_UNSUPPORTED (true); an unchanged value is kept (false). */
+    MT_HD bool combine_unsupported(int32_t comb, int32_t cur) {
+        if (comb == MT_COMBINE_CONSENSUS && cur != 0) return false;
+        fail(E_UNSUPPORTED);
+        return true;
+    }
+    MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collaborating) {
+        const bool rewrite = comb == MT_COMBINE_REWRITE;
         if constexpr (W::N >= 32 && MT_PROPS_PAR) {
             if (nkv <= W::N) {
-                add_props_par(s, kv, nkv, rewrite, seq, collaborating);
+                add_props_par(s, kv, nkv, comb, seq, collaborating);
                 return;
             }
         }
@@ -2996,9 +3014,13 @@ struct Replica {
                         return;
                     }
                     c.pk[k]++;
-                } else if (!(c.pk[k] == 0)) {
+                } else if (!(c.pk[k] == 0) && comb < MT_COMBINE_INCR) {
                     continue;
                 }
+            }
+            if (comb >= MT_COMBINE_INCR) {
+                if (combine_unsupported(comb, c.pv[k])) return;
+                continue;
             }
             c.pv[k] = kv[j].value;
         }
@@ -3909,7 +3931,8 @@ struct Replica {
                 row_enter(s);
             if (op.props) { /* TextSegment.make(text, props): addProperties without collab */
                 const mt_props_rec& pr = p.props[op.props - 1];
-                add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE, 0, false);
+                add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE ? MT_COMBINE_REWRITE : MT_COMBINE_NONE,
+                          0, false);
             }
             if (h.collaborating) { /* saveIfLocal (2197-2212) */
                 if (seq == UNASSIGNED_SEQ && client == h.localShort) {
@@ -4268,13 +4291,13 @@ struct Replica {
     /* markRangeRemoved (2640-2752) and annotateRange (2598-2638) share one range walk (range_op is inlined once
      * for both: the replay kernel's code size is what its instruction cache sees) */
     MT_HD void mark_range_removed(int32_t start, int32_t end, int32_t refSeq, int32_t client, int32_t seq) {
-        range_edit(true, start, end, nullptr, 0, false, refSeq, client, seq);
+        range_edit(true, start, end, nullptr, 0, MT_COMBINE_NONE, refSeq, client, seq);
     }
-    MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t refSeq,
+    MT_HD void annotate_range(int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t refSeq,
                               int32_t client, int32_t seq) {
-        range_edit(false, start, end, kv, nkv, rewrite, refSeq, client, seq);
+        range_edit(false, start, end, kv, nkv, comb, refSeq, client, seq);
     }
-    MT_HD void range_edit(bool remove, int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, bool rewrite,
+    MT_HD void range_edit(bool remove, int32_t start, int32_t end, const mt_kv* kv, int32_t nkv, int32_t comb,
                           int32_t refSeq, int32_t client, int32_t seq) {
         bool hasL = seq == UNASSIGNED_SEQ;
         int32_t localSeq = hasL ? ++zh->localSeq : 0;
@@ -4309,11 +4332,11 @@ struct Replica {
                 if (dl) { /* deltaSegments.push({segment, propertyDeltas}) (mergeTree.ts:2608-2609) */
                     dput(dpos);
                     dput(z.len(s));
-                    prop_deltas(s, kv, nkv, rewrite, seq, collab);
+                    prop_deltas(s, kv, nkv, comb, seq, collab);
                     dn++;
                 }
-                if (z.flags(s) & RF_MARKER) marker_keys_annotated(s, kv, nkv, rewrite);
-                add_props(s, kv, nkv, rewrite, seq, collab);
+                if (z.flags(s) & RF_MARKER) marker_keys_annotated(s, kv, nkv, comb == MT_COMBINE_REWRITE);
+                add_props(s, kv, nkv, comb, seq, collab);
                 if (collab) {
                     if (hasL)
                         pending_add(s, localSeq, &created);
@@ -4708,11 +4731,13 @@ struct Replica {
         const mt_kv* kv = 0;
         int32_t nkv = 0;
         bool rw = false;
+        int32_t comb = MT_COMBINE_NONE;
         if (op.props && kind == MT_OP_ANNOTATE) {
             const mt_props_rec& pr = p.props[op.props - 1];
             kv = p.kv + pr.kv_off;
             nkv = pr.nkv;
-            rw = pr.combining == MT_COMBINE_REWRITE;
+            comb = pr.combining;
+            rw = comb == MT_COMBINE_REWRITE;
         }
         if ((op.seg_kind & MT_SEG_RELPOS) && (op.kind & (MT_OPF_LOCAL | MT_OPF_TREE) || kind > MT_OP_ANNOTATE)) {
             fail(E_UNSUPPORTED); /* relative positions: sequenced op records only (mt_oplog.h) */
@@ -4791,6 +4816,10 @@ struct Replica {
                 return; /* insertSegmentLocal of an empty segment */
             } else {
                 edit = kind <= MT_OP_ANNOTATE;
+                /* a local consensus annotate: its ack calls updateConsensusProperty, which needs the marker-relative
+                 * position and the pending-consensus callback of annotateMarkerNotifyConsensus (client.ts:982-989,
+                 * 248-274); neither is modelled, and a plain one throws there in the reference */
+                if (comb == MT_COMBINE_CONSENSUS) fail(E_UNSUPPORTED);
             }
         } else {
             remote = true;
@@ -4823,7 +4852,7 @@ struct Replica {
         }
         if (edit) {
             if (kind == MT_OP_REMOVE || kind == MT_OP_ANNOTATE)
-                range_edit(kind == MT_OP_REMOVE, o.pos1, o.pos2, kv, nkv, rw, eref, ecli, eseq);
+                range_edit(kind == MT_OP_REMOVE, o.pos1, o.pos2, kv, nkv, comb, eref, ecli, eseq);
             else
                 insert_segments(o, p, eref, ecli, eseq, epre, eprc, eat);
             if (remote) {
@@ -4946,7 +4975,8 @@ struct Replica {
         z.flags(s) = (uint8_t)fl;
         if (op.props) {
             const mt_props_rec& pr = p.props[op.props - 1];
-            add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE, 0, false);
+            add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE ? MT_COMBINE_REWRITE : MT_COMBINE_NONE, 0,
+                      false);
         }
         if constexpr (TILED) z.tl.xf[s] = 0;
         h.nrows++;

@@ -265,8 +265,13 @@ class ReplayEngine {
         const off = q.kv.length;
         const keys = Object.keys(props);
         for (const k of keys) q.kv.push([this.interner.key(k), this.interner.value(props[k])]);
-        if (combiningOp && combiningOp.name !== "rewrite") throw new Error(`combiningOp ${combiningOp.name} unsupported`);
-        q.props.push([off, keys.length, combiningOp ? 1 : 0]);
+        // ICombiningOp -> mt_oplog.h MT_COMBINE_*: rewrite 1, incr 2, consensus 3 (without defaultValue / minValue)
+        const COMB = { rewrite: 1, incr: 2, consensus: 3 };
+        if (combiningOp && (COMB[combiningOp.name] === undefined ||
+            (combiningOp.name !== "rewrite" && (combiningOp.defaultValue !== undefined || combiningOp.minValue !== undefined)))) {
+            throw new Error(`combiningOp ${combiningOp.name} unsupported`);
+        }
+        q.props.push([off, keys.length, combiningOp ? COMB[combiningOp.name] : 0]);
         return q.props.length;
     }
 

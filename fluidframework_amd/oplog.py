@@ -29,7 +29,7 @@ RELPOS_UNITS = 10  # MT_RELPOS_UNITS
 MARKER_ID_KEY = "markerId"  # reservedMarkerIdKey (merge-tree properties / mergeTree.ts getId)
 CLIENT_NONCOLLAB = 0xFFFF
 _SEGMENT_KINDS = (OP_INSERT, OP_RELOAD, OP_APPEND)
-COMBINE_NONE, COMBINE_REWRITE = 0, 1
+COMBINE_NONE, COMBINE_REWRITE, COMBINE_INCR, COMBINE_CONSENSUS = 0, 1, 2, 3  # mt_oplog.h MT_COMBINE_*
 VALUE_FALSY = 0x8000
 
 OP_DTYPE = np.dtype(

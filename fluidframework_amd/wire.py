@@ -59,13 +59,26 @@ def _op_record(log: ol.DocLog, kind: int, op: Dict[str, Any], common: Dict[str, 
     elif t == ol.OP_REMOVE:
         add(kind, pos1=p1, pos2=p2, **common)
     elif t == ol.OP_ANNOTATE:
-        comb = op.get("combiningOp")
-        if comb is not None and comb.get("name") != "rewrite":
-            raise ValueError(f"combining op {comb.get('name')!r} is not supported")
-        add(kind, pos1=p1, pos2=p2, props=op["props"],
-            combining=ol.COMBINE_REWRITE if comb is not None else ol.COMBINE_NONE, **common)
+        add(kind, pos1=p1, pos2=p2, props=op["props"], combining=combining_kind(op.get("combiningOp")), **common)
     else:
         raise ValueError(f"unsupported merge-tree op type {t}")
+
+
+def combining_kind(comb) -> int:
+    """An annotate's ICombiningOp (ops.ts) as mt_oplog.h MT_COMBINE_*: "rewrite", or "incr" / "consensus", which the
+    engine applies as the reference's addProperties does (combine with newValue undefined, properties.ts:26-59:
+    incr's NaN and consensus's new objects latch MT_E_UNSUPPORTED). A defaultValue / minValue would change what
+    combine starts from: refused, as are other names."""
+    if comb is None:
+        return ol.COMBINE_NONE
+    name = comb.get("name")
+    if name == "rewrite":
+        return ol.COMBINE_REWRITE
+    if name in ("incr", "consensus"):
+        if comb.get("defaultValue") is not None or comb.get("minValue") is not None:
+            raise ValueError(f"combining op {name!r} with a defaultValue / minValue is not supported")
+        return ol.COMBINE_INCR if name == "incr" else ol.COMBINE_CONSENSUS
+    raise ValueError(f"combining op {name!r} is not supported")
 
 
 def add_message(log: ol.DocLog, msg: Dict[str, Any], client_index: Callable[[str], int]) -> None:

@@ -129,10 +129,16 @@ enum {
 #define MT_SEG_RELPOS 0x80
 #define MT_RELPOS_UNITS 10
 
-/* combining ops for annotate (ops.ts ICombiningOp); only none and "rewrite" are supported */
+/* combining ops for annotate (ops.ts ICombiningOp, properties.ts:26-59) */
 enum {
     MT_COMBINE_NONE = 0,
     MT_COMBINE_REWRITE = 1,
+    /* "incr" / "consensus" (properties.ts:26-59) as addProperties applies them (segmentPropertiesManager.ts:92-106:
+     * every key is modified, pending local updates notwithstanding, and combine gets newValue undefined, SURVEY
+     * Appendix A2): incr makes the value NaN, consensus over an absent value a {value: undefined, seq} object —
+     * both latch MT_E_UNSUPPORTED where the reference computes them; consensus over a present value keeps it. */
+    MT_COMBINE_INCR = 2,
+    MT_COMBINE_CONSENSUS = 3,
 };
 
 typedef struct mt_op_rec {

@@ -59,6 +59,19 @@ def test_parse_steps():
             {"chunkId": 1, "totalChunks": 2, "contents": "x", "originalType": "op"})}] * 2)
 
 
+def test_tool_loop_as_written_cannot_replay_the_logs():
+    """Why replay_tool.py (and tools/ref_replay_tool.mjs) follow the loop's intent: the fixture records what the
+    reference tool's loop does AS WRITTEN (clientReplayTool.ts:190-256, `message.clientId !== clientId` at 211;
+    tools/ref_replay_tool.mjs --literal): it applies another client's op as a local transaction, queues it twice,
+    and throws on the first re-applied message of each log, before its own asserts are reached."""
+    z, docs = load()
+    lit = json.loads(str(z["literal"]))
+    assert len(lit) == len(docs)
+    for r in lit:
+        assert r["outcome"] == "threw"
+        assert "sequence#" in r["error"]  # client.ts:462-465: the seq of a remote op must exceed currentSeq
+
+
 def test_host_core_replicas_match_reference_tool():
     z, docs = load()
     for k, msgs in enumerate(docs):

@@ -300,6 +300,57 @@ def run_refs(rb, d: str, node: str):
     return nref, pos, digests, inside, past
 
 
+def make_combine(node: str) -> None:
+    """tests/golden/refcombine.npz: annotates with combining ops incr / consensus (tests/combine_inject.py) in
+    config-3 and config-5 logs, replayed by the reference with tools/ref_replay.mjs --combine-watch: per document the
+    first record after which a segment holds a value only Properties.combine makes (NaN, a {value, seq} object;
+    -1: none) and, for the documents with none, the digest of the final replica."""
+    import combine_inject
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    out = {}
+    for name, w, n in (("c3", gen.config3(1500), 64), ("c5", gen.config5(1500), 32)):
+        b = combine_inject.inject(gen.generate(w, ids=range(n), threads=8))
+        d = os.path.join(SCRATCH, f"combine_{name}")
+        write_batch(b, gen.generator_interner(), d)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, d, "--combine-watch"],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay failed: {r.stderr[-2000:]}")
+        errs = json.load(open(os.path.join(d, "ref_err.json")))["errors"]
+        if errs:
+            raise RuntimeError(f"reference threw on {len(errs)} docs: {list(errs.items())[:3]}")
+        at = json.load(open(os.path.join(d, "ref_combine.json")))
+        first = np.asarray([at.get(str(i), -1) for i in range(n)], np.int64)
+        blob = np.fromfile(os.path.join(d, "ref_dumps.bin"), np.uint8)
+        off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
+        dig = np.asarray([fnv1a64(blob[off[i]: off[i + 1]].tobytes()) if first[i] < 0 else 0 for i in range(n)],
+                         np.uint64)
+        # the replicas right before that record (the prefix [0, first)): pins what the kept values did until then
+        pre = ol.Batch.from_arrays([tuple(x if k else x[: (first[i] if first[i] >= 0 else len(x))]
+                                          for k, x in enumerate(b.doc_arrays(i))) for i in range(n)], b.local_long_id)
+        dp = os.path.join(SCRATCH, f"combine_{name}_pre")
+        write_batch(pre, gen.generator_interner(), dp)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, dp, "--combine-watch"],
+                           capture_output=True, text=True)
+        if r.returncode != 0 or json.load(open(os.path.join(dp, "ref_err.json")))["errors"]:
+            raise RuntimeError(f"reference prefix replay failed: {r.stderr[-2000:]}")
+        if json.load(open(os.path.join(dp, "ref_combine.json"))):
+            raise RuntimeError("a prefix reaches a combined value")
+        pb = np.fromfile(os.path.join(dp, "ref_dumps.bin"), np.uint8)
+        po = np.fromfile(os.path.join(dp, "ref_dump_off.bin"), "<i8")
+        out[f"{name}_prefix_digests"] = np.asarray([fnv1a64(pb[po[i]: po[i + 1]].tobytes()) for i in range(n)], np.uint64)
+        out[f"{name}_workload"] = json.dumps(dataclasses.asdict(w))
+        out[f"{name}_log_sha256"] = log_sha(b)
+        out[f"{name}_first"] = first
+        out[f"{name}_digests"] = dig
+        ncomb = int(((b.props[b.ops["props"][b.ops["props"] > 0].astype(np.int64) - 1]["combining"]) >= 2).sum())
+        print(f"refcombine {name}: {n} docs, {ncomb} combining annotates; {int((first >= 0).sum())} documents reach a "
+              f"combined value", flush=True)
+    np.savez_compressed(os.path.join(GOLDEN, "refcombine.npz"), **out,
+                        source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node "
+                                "by tools/ref_replay.mjs --combine-watch"))
+
+
 def make_refentry(node: str) -> None:
     """tests/golden/refentry_kat.npz: the refsByOffset-entry KATs (tests/refs_entry_logs.py) replayed by the
     reference: LocalReference.toPosition() of every reference (-2: addLocalReference threw) and the digests."""
@@ -744,9 +795,11 @@ def make_replaytool(node: str) -> None:
     """tests/golden/refreplaytool.npz: the reference merge-tree client replay tool's per-client replicas
     (clientReplayTool.ts:113-258, restated over the reference Client by tools/ref_replay_tool.mjs) for the
     recorded-document logs of tests/replaylog.py: per replica its merge tree, client, getLength and the length
-    and FNV-1a-64 (UTF-16LE) of getText; the logs' SHA-256; the observer's full texts."""
+    and FNV-1a-64 (UTF-16LE) of getText; the logs' SHA-256; the observer's full texts; and `literal`: per log
+    what the tool's loop does as written (tools/ref_replay_tool.mjs --literal: the exception that ends it, or
+    its assert's outcome)."""
     import replaylog
-    rows, texts, shas = [], [], []
+    rows, texts, shas, literal = [], [], [], []
     for k, msgs in enumerate(replaylog.documents()):
         d = os.path.join(SCRATCH, f"replaytool_{k}")
         os.makedirs(d, exist_ok=True)
@@ -764,12 +817,20 @@ def make_replaytool(node: str) -> None:
             if client == "readonly":
                 texts.append(text)
         print(f"replaytool doc {k}: {len(reps)} replicas, lengths {sorted(set(x[3] for x in reps))}", flush=True)
+        # the tool's loop as written (clientReplayTool.ts:211 tests `!==`): what it does on the same log
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay_tool.mjs"), ERASED,
+                            os.path.join(d, "messages.json"), os.path.join(d, "literal.json"), "--literal"],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay tool (literal) failed: {r.stderr[-2000:]}")
+        literal.append(json.load(open(os.path.join(d, "literal.json")))["literal"])
+        print(f"replaytool doc {k}: the loop as written: {literal[-1]}", flush=True)
     np.savez_compressed(
         os.path.join(GOLDEN, "refreplaytool.npz"),
         doc=np.asarray([x[0] for x in rows], np.int32), path=np.asarray([x[1] for x in rows]),
         client=np.asarray([x[2] for x in rows]), text_len=np.asarray([x[3] for x in rows], np.int64),
         text_fnv=np.asarray([x[4] for x in rows], np.uint64), length=np.asarray([x[5] for x in rows], np.int64),
-        observer_texts=np.asarray(texts), log_sha256=np.asarray(shas),
+        observer_texts=np.asarray(texts), log_sha256=np.asarray(shas), literal=json.dumps(literal),
         source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
                 "tools/ref_replay_tool.mjs: clientReplayTool.ts's reconstruction over the reference Client"))
 
@@ -786,6 +847,7 @@ def main() -> None:
     ap.add_argument("--handles", action="store_true", help="write the PermutationVector handle fixture only")
     ap.add_argument("--relpos", action="store_true", help="write the relative-position fixture (refrelpos.npz) only")
     ap.add_argument("--tree", action="store_true", help="write the MergeTree-level record fixtures (reftree_*.npz) only")
+    ap.add_argument("--combine", action="store_true", help="write the incr / consensus combining-op fixture only")
     ap.add_argument("--hsnap", action="store_true", help="write the SharedMatrix summary-with-handles fixture only")
     ap.add_argument("--refentry", action="store_true", help="write the refsByOffset-entry KAT fixture only")
     ap.add_argument("--unref", action="store_true", help="write the removeLocalReference fixtures (refunref_*.npz) only")
@@ -825,6 +887,9 @@ def main() -> None:
         return
     if args.hsnap:
         make_handle_snaps(args.node)
+        return
+    if args.combine:
+        make_combine(args.node)
         return
     if args.unref:
         make_refs([n for n in args.sets.split(",") if n in REF_SETS], args.node, removals=True)

@@ -59,7 +59,7 @@ function propSet(doc, idx) {
         const k = kv.readUInt16LE(q), v = kv.readUInt16LE(q + 2) & ~FALSY;
         set[keys[k]] = v === 0 ? null : JSON.parse(values[v]);
     }
-    return { set, combiningOp: comb === 1 ? { name: "rewrite" } : undefined };
+    return { set, combiningOp: comb === 1 ? { name: "rewrite" } : comb === 2 ? { name: "incr" } : comb === 3 ? { name: "consensus" } : undefined };
 }
 
 function textOf(doc, rec) {
@@ -122,11 +122,34 @@ const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPe
 // apply records [from, to) of `doc` to `client` (applyMsg / the local-edit entry points)
 let applying = -1; // the record being applied (for error reports)
 let curSeq = 0; // seq of the record being applied (-1: a local edit), the delta stream's event seq
+// --combine-watch: per document, the first record after which a segment holds a value only Properties.combine
+// makes as addProperties calls it (newValue undefined, properties.ts:26-59): NaN, a string ending in "undefined"
+// (incr), or a {value, seq} object (consensus) -> batch-dir/ref_combine.json
+const combineWatch = process.argv.includes("--combine-watch");
+const combineAt = {};
+function combinedValue(v) {
+    return (typeof v === "number" && Number.isNaN(v)) || (typeof v === "string" && v.endsWith("undefined")) ||
+        (v !== null && typeof v === "object" && "seq" in v);
+}
+function watchCombine(client, doc, i) {
+    if (combineAt[doc] !== undefined) return;
+    client.mergeTree.walkAllSegments(client.mergeTree.root, (seg) => {
+        if (seg.properties) for (const k of Object.keys(seg.properties)) if (combinedValue(seg.properties[k])) combineAt[doc] = i - opOff[doc];
+        return combineAt[doc] === undefined;
+    });
+}
 function applyRange(client, doc, from, to) {
     let members = []; // members of a group message so far (records flagged GROUPED, mt_oplog.h)
-    for (let i = from; i < to; i++) {
+    let prevComb = false; // the previous record carried an incr / consensus annotate (--combine-watch)
+    for (let i = from; i <= to; i++) {
+        if (prevComb) watchCombine(client, doc, i - 1);
+        if (i === to) break;
         applying = i;
         const rec = record(i);
+        prevComb = combineWatch && (rec.kind & 7) === 2 && rec.props > 0 && (() => {
+            const ps = propSet(doc, rec.props);
+            return ps && ps.combiningOp && ps.combiningOp.name !== "rewrite";
+        })();
         const kind = rec.kind & 7;
         curSeq = rec.kind & 0x80 ? -1 : rec.seq;
         if ((rec.kind & 0x90) === 0x90) { // MT_OPF_REGEN: Client.regeneratePendingOp for the head pending op
@@ -606,7 +629,8 @@ for (let d = 0; d < ndocs; d++) {
             if (offset !== null) r.offset = offset;
             relAnswers.push(c.posFromRelativePos(r));
         }
-        dumps.push(timeOnly ? Buffer.alloc(0) : dump(c));
+        // a replica holding a value only combine makes (NaN, a {value, seq} object) has no canonical dump
+        dumps.push(timeOnly || (combineWatch && combineAt[d] !== undefined) ? Buffer.alloc(0) : dump(c));
     } catch (e) {
         errs[d] = String(e && e.message || e);
         dumps.push(Buffer.alloc(0));
@@ -703,6 +727,7 @@ if (withHandles) {
     fs.writeFileSync(path.join(dir, "ref_handles.json"), JSON.stringify(snap));
 }
 if (relQueries.length) fs.writeFileSync(path.join(dir, "ref_relpos.json"), JSON.stringify(relAnswers));
+if (combineWatch) fs.writeFileSync(path.join(dir, "ref_combine.json"), JSON.stringify(combineAt));
 console.log(JSON.stringify({ ndocs, errors: Object.keys(errs).length, seconds: secs, removeThrew }));
 }
 main().catch((e) => { console.error(e); process.exit(1); });

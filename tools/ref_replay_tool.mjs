@@ -13,7 +13,8 @@
 // which would apply the other clients' ops locally and then remotely and never the client's own; the
 // evident intent is restated, as fluidframework_amd/replay_tool.py does.)
 //
-// usage: node ref_replay_tool.mjs <erased-dir> <messages.json> <out.json>
+// usage: node ref_replay_tool.mjs <erased-dir> <messages.json> <out.json> [--literal]
+//   --literal: run the tool's loop exactly as written instead (line 211's `!==`) and report its outcome
 //   out.json: {"replicas": [[path, client, text, length], ...]} in (client, path) order
 import fs from "fs";
 import path from "path";
@@ -70,6 +71,60 @@ function processAttach(attach, attachTrees) { // processAttachMessage (264-320),
     }
 }
 
+const literal = process.argv.includes("--literal");
+// clientReplayTool.ts:190-256 exactly as written: `message.clientId !== clientId` (211) — every OTHER client's op is
+// pushed to the pending queue, applied as this client's local transaction, and pushed again; the client's own
+// ops are skipped. The first exception ends the tool (it rethrows); otherwise its final asserts compare every
+// replica's length and text with the readonly replica's. Returns what happened.
+async function literalRun(MT, clients, attachTrees, mtMessages, specToSegment) {
+    const { Client, createGroupOp, MergeTreeDeltaType } = MT;
+    clients = new Map(clients);
+    clients.set("readonly", new Map());
+    for (const clientId of clients.keys()) {
+        const client = clients.get(clientId);
+        for (const id of attachTrees.keys()) {
+            const c = new Client(specToSegment, logger);
+            const { catchupOpsP } = await c.load(runtimeOf(clientId), storageOf(attachTrees.get(id)));
+            await catchupOpsP;
+            client.set(id, c);
+        }
+        const pending = [];
+        let step = "";
+        try {
+            for (const message of mtMessages) {
+                if (message.clientId !== clientId) {
+                    pending.push(message);
+                    while (pending.length > 0 && pending[0].sequenceNumber <= message.referenceSequenceNumber) {
+                        const m = pending.shift();
+                        step = `applyMsg seq ${m.sequenceNumber}`;
+                        client.get(m.fullPath).applyMsg(m);
+                    }
+                    const op = message.contents;
+                    step = `localTransaction of seq ${message.sequenceNumber}`;
+                    client.get(message.fullPath).localTransaction(op.type === MergeTreeDeltaType.GROUP ? op : createGroupOp(op));
+                    pending.push(message);
+                }
+            }
+            for (const m of pending) {
+                step = `final applyMsg seq ${m.sequenceNumber}`;
+                client.get(m.fullPath).applyMsg(m);
+            }
+        } catch (e) {
+            return { outcome: "threw", client: clientId, step, error: String(e && e.message || e) };
+        }
+    }
+    const ro = clients.get("readonly");
+    for (const [clientId, client] of clients) {
+        for (const [id, c] of client) {
+            const r = ro.get(id);
+            if (c.getLength() !== r.getLength() || c.getText() !== r.getText()) {
+                return { outcome: "assert", client: clientId, path: id, length: c.getLength(), readonlyLength: r.getLength() };
+            }
+        }
+    }
+    return { outcome: "passed" };
+}
+
 async function main() {
     const MT = await import(path.join(erased, "index.mjs"));
     const { Client, TextSegment, Marker, createGroupOp, MergeTreeDeltaType } = MT;
@@ -124,6 +179,11 @@ async function main() {
         }
     }
     const out = [];
+    if (literal && attachTrees.size > 0) { // the loop as written (190-256), to record what it does
+        fs.writeFileSync(outPath, JSON.stringify({ literal: await literalRun(MT, clients, attachTrees, mtMessages, specToSegment) }));
+        console.log(JSON.stringify({ literal: true, messages: mtMessages.length }));
+        return;
+    }
     if (attachTrees.size > 0) {
         clients.set("readonly", new Map());
         for (const clientId of clients.keys()) {
