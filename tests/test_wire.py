@@ -117,9 +117,17 @@ def test_unsupported_wire_ops_raise():
     with pytest.raises(ValueError):  # a relative position names a marker id
         wire.add_message(log, dict(base, contents={"type": 1, "relativePos1": {"before": True}, "pos2": 3}),
                          wire.ClientNames())
-    with pytest.raises(ValueError):
+    with pytest.raises(ValueError):  # a combining op that starts from a defaultValue
         wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
-                                                   "combiningOp": {"name": "incr"}}), wire.ClientNames())
+                                                   "combiningOp": {"name": "incr", "defaultValue": 3}}),
+                         wire.ClientNames())
+    with pytest.raises(ValueError):  # an unknown combining op
+        wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
+                                                   "combiningOp": {"name": "max"}}), wire.ClientNames())
+    for name, kind in (("incr", ol.COMBINE_INCR), ("consensus", ol.COMBINE_CONSENSUS)):
+        wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
+                                                   "combiningOp": {"name": name}}), wire.ClientNames())
+        assert log.props[log.ops[-1][10] - 1][2] == kind
     names = wire.ClientNames(["x"])
     wire.add_message(log, dict(base, clientId="y", type="noop"), names)
     assert names.name(1) == "y" and log.ops[-1][0] == ol.OP_NOOP
