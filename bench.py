@@ -133,6 +133,7 @@ def main() -> None:
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (default: host share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--digests-out", default="", help="save the per-document digests (.npy) after the run")
+    ap.add_argument("--doc-times-out", default="", help="save each document's replay start / end (.npy, 100 MHz ticks)")
     ap.add_argument("--order", choices=("cost", "doc"), default="cost",
                     help="replay dispatch order: longest-first by shard.doc_costs (cost) or document order (doc)")
     ap.add_argument("--gen-cache", default=os.environ.get("MT_GEN_CACHE", ""),
@@ -230,6 +231,8 @@ def main() -> None:
 
     # per-document replay times of that step (GPU constant clock, 100 MHz): the spread behind the launch's tail
     tt = eng.doc_times().astype(np.float64)
+    if args.doc_times_out:
+        np.save(args.doc_times_out, tt)
     dur = (tt[:, 1] - tt[:, 0]) / 1e5  # ms
     span = (tt[:, 1].max() - tt[:, 0].min()) / 1e5
     doc_ms = {"mean": float(dur.mean()), "p50": float(np.median(dur)), "p99": float(np.percentile(dur, 99)),

@@ -406,10 +406,21 @@ struct ProfScope {
 /* LOAD: applies snapshot-load records (mt_oplog.h MT_OP_RELOAD / COLLAB / APPEND); the plain config-2/3 replay
  * kernel is built without them (its scalar registers: SGPR spills 1,321 -> 1,041, +2.2 % on config 3, r04s) and
  * the engine runs a batch that holds any with the full build */
-template <class W, class HT, bool DL = false, bool LOAD = true>
+/* NARROW: the tiled kernel's variant that keeps the zamboni heap in LDS beside a narrower window set (MT_NARROW_H /
+ * MT_NARROW_W entries, mt_kernels.h k_replay_tiled); a document that outgrows either latches E_CAPACITY and replays
+ * again in the wide variant (capacity promotion, mt_replay.hip) */
+#ifndef MT_NARROW_W
+#define MT_NARROW_W 2048
+#endif
+#ifndef MT_NARROW_H
+#define MT_NARROW_H 2048
+#endif
+template <class W, class HT, bool DL = false, bool LOAD = true, bool NARROW = false>
 struct Replica {
     typedef typename HT::IX IX;
     static constexpr bool TILED = HT::TILED;
+    static constexpr int WCAPR = NARROW ? MT_NARROW_W : HT::TL::WCAP; /* window-set entries */
+    static constexpr int HCAPR = NARROW ? MT_NARROW_H : HT::H;        /* zamboni heap entries */
     Doc<HT> d;
     HT& z; /* the hot image */
     W w;
@@ -1569,7 +1580,7 @@ struct Replica {
     }
     MT_HD void win_add(int32_t rid, int32_t s) {
         auto& t = z.tl;
-        if (t.wN >= HT::TL::WCAP) {
+        if (t.wN >= WCAPR) {
             fail(E_CAPACITY);
             return;
         }
@@ -1587,7 +1598,7 @@ struct Replica {
         } else {
             z.tl.xf[s] = XF_W;
             auto& t = z.tl;
-            if (t.wN >= HT::TL::WCAP) {
+            if (t.wN >= WCAPR) {
                 fail(E_CAPACITY);
                 return;
             }
@@ -2612,7 +2623,7 @@ struct Replica {
     MT_HD void heap_add(int32_t rid, int32_t seq, int32_t knownGen = -1) {
         MT_PROF_SCOPE(PH_HEAP);
         int32_t n = h.heapN;
-        if (n >= HT::H) {
+        if (n >= HCAPR) {
             fail(E_CAPACITY);
             return;
         }
@@ -2685,7 +2696,7 @@ struct Replica {
             int32_t c2 = 128 + l < cnt ? hsq[128 + l] : 0;
             int32_t c3 = 192 + l < cnt ? hsq[192 + l] : 0;
             /* the image's heap (tiled profile): every field in this pass; an LDS heap re-reads the moved entries */
-            constexpr bool PICK = TILED;
+            constexpr bool PICK = TILED && !NARROW;
             int32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, g0 = 0, g1 = 0, g2 = 0, g3 = 0;
             if (PICK) {
                 r0 = l < cnt ? (int32_t)hrd[l] : 0, g0 = l < cnt ? hgn[l] : 0;
@@ -4259,7 +4270,7 @@ struct Replica {
             uint64_t wm = w.ballot(wadd);
             if (wm) {
                 int32_t wn = t.wN, cnt = __builtin_popcountll(wm);
-                if (wn + cnt > HT::TL::WCAP) {
+                if (wn + cnt > WCAPR) {
                     fail(E_CAPACITY);
                     return;
                 }
@@ -4908,6 +4919,7 @@ struct Replica {
             for (int32_t k = 0; kvalid(k); k = knext(k)) leaf_restat(leaf_at(k));
         /* interior levels; the previous level's nodes in order go through the (empty) heap arrays */
         int32_t cnt = 0;
+        IX* hrd = z.hrid; /* the image's own heap array (N + 64 entries): an LDS heap may be smaller */
         for (int32_t k = 0; kvalid(k); k = knext(k)) hrd[cnt++] = (IX)leaf_at(k);
         int8_t lvl = 1;
         while (cnt > 1) {

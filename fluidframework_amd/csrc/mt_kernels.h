@@ -320,14 +320,19 @@ __device__ void tiled_prefetch(Doc<HT> v, const mt_op_rec* ops, int64_t nops, co
     if (acc == 0x9e3779b9u && lane == 0) *sink = (int32_t)acc; /* keeps the loads */
 }
 
-template <class HT, bool DL = false>
+/* NARROW (the default config-4 kernel): the zamboni heap in LDS too (~60 entries in use at lag 64: every pop and
+ * push an LDS pass instead of an HBM round trip), beside a window set of MT_NARROW_W entries; a document whose
+ * heap or window set would outgrow them latches E_CAPACITY and the engine replays it in the wide variant
+ * (NARROW = false: the heap in HBM, the full window set) — capacity promotion (mt_replay.hip). */
+template <class HT, bool DL = false, bool NARROW = false>
 __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                                      const int64_t* op_off, const uint16_t* text,
                                                      const int64_t* text_off, const mt_props_rec* props,
                                                      const int64_t* props_off, const mt_kv* kv, const int64_t* kv_off,
                                                      ReplayAux aux) {
     static_assert(HT::TILED, "tiled profile only");
-    constexpr int NCH = HT::TL::NCH, WCAP = HT::TL::WCAP;
+    typedef Replica<WaveGPU, HT, DL, true, NARROW> R;
+    constexpr int NCH = HT::TL::NCH, WCAP = R::WCAPR, HL = NARROW ? R::HCAPR : 1;
     __shared__ int32_t cdel[NCH];
     __shared__ int32_t wcp[WCAP], wvs[WCAP];
     __shared__ uint8_t wlx[WCAP];
@@ -336,6 +341,9 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     __shared__ int32_t lcord[NCH], lcst[NCH], lcpos[NCH], lccnt[NCH], lwrid[WCAP];
     __shared__ __attribute__((aligned(16))) uint8_t lwgen[WCAP];
     __shared__ int32_t lwslot[WCAP];
+    __shared__ int32_t lhseq[HL]; /* NARROW: the zamboni heap */
+    __shared__ typename HT::IX lhrid[HL];
+    __shared__ uint8_t lhgen[HL];
     __shared__ int32_t pfcur, pfdone, pfsink; /* the replaying wave's record, its end, the helpers' sink */
     if ((int64_t)blockIdx.x >= ndocs) return;
     const int64_t d = aux_doc(aux);
@@ -345,7 +353,10 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     if (threadIdx.x < WG) doc_stamp(v.t, 0);
     auto& tl = v.t->tl;
     const bool replayer = threadIdx.x < WG;
-    if (replayer) {
+    /* what the staged arrays cannot hold: nothing is staged, the replica latches E_CAPACITY */
+    const bool fits = !NARROW || (tl.wN <= WCAP && v.t->h.heapN <= HL);
+    const int32_t nheap = NARROW ? v.t->h.heapN : 0;
+    if (replayer && fits) {
         for (int i = threadIdx.x; i < NCH; i += WG) cdel[i] = 0;
         wave_copy((int32_t*)&zhs, (const int32_t*)&v.t->h, (int)(sizeof(DocHdr) / 4));
         wave_copy(lcord, tl.cord, NCH);
@@ -355,6 +366,11 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         wave_copy(lwrid, tl.wrid, WCAP);
         wave_copy((int32_t*)lwgen, (const int32_t*)tl.wgen, WCAP / 4);
         wave_copy(lwslot, tl.wslot, WCAP);
+        if constexpr (NARROW) {
+            wave_copy(lhseq, v.t->hseq, nheap);
+            wave_copy(lhrid, v.t->hrid, nheap);
+            wave_copy(lhgen, v.t->hgen, nheap);
+        }
         if (threadIdx.x == 0) {
             pfcur = 0;
             pfdone = 0;
@@ -369,8 +385,13 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     p.kv = kv + kv_off[d];
     if (!replayer) {
         tiled_prefetch<HT>(v, p.ops, p.nops, &pfcur, &pfdone, lcord, lcst, lccnt, &pfsink);
+    } else if (!fits) {
+        R r(v, WaveGPU());
+        r.fail(E_CAPACITY);
+        r.commit();
+        if (threadIdx.x == 0) *(volatile int32_t*)&pfdone = 1;
     } else {
-        Replica<WaveGPU, HT, DL> r(v, WaveGPU());
+        R r(v, WaveGPU());
         r.cdel = cdel;
         r.wcp = wcp;
         r.wvs = wvs;
@@ -383,6 +404,11 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         r.twrid = lwrid;
         r.twgen = lwgen;
         r.twslot = lwslot;
+        if constexpr (NARROW) {
+            r.hsq = lhseq;
+            r.hrd = lhrid;
+            r.hgn = lhgen;
+        }
         if (MT_PF_HELPERS > 0) r.pfcur = &pfcur;
         r.replay(p);
         r.commit();
@@ -393,7 +419,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
 #endif
     }
     __syncthreads();
-    if (replayer) {
+    if (replayer && fits) {
         wave_copy((int32_t*)&v.t->h, (const int32_t*)&zhs, (int)(sizeof(DocHdr) / 4));
         wave_copy(tl.cord, lcord, NCH);
         wave_copy(tl.cst, lcst, NCH);
@@ -402,8 +428,14 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         wave_copy(tl.wrid, lwrid, WCAP);
         wave_copy((int32_t*)tl.wgen, (const int32_t*)lwgen, WCAP / 4);
         wave_copy(tl.wslot, lwslot, WCAP);
-        doc_stamp(v.t, 1);
+        if constexpr (NARROW) {
+            int32_t n = zhs.heapN <= HL ? zhs.heapN : HL;
+            wave_copy(v.t->hseq, lhseq, n);
+            wave_copy(v.t->hrid, lhrid, n);
+            wave_copy(v.t->hgen, lhgen, n);
+        }
     }
+    if (replayer) doc_stamp(v.t, 1);
 }
 
 /* K5: per-doc digest of the canonical dump */
@@ -691,6 +723,7 @@ struct mt_engine {
     bool loads = false; /* the staged batch holds snapshot-load records (the config-2/3 kernel's full build) */
     int profile = 0;
     int waves = 8;    /* occupancy target of the HBM-resident small-profile kernel */
+    bool wide = false; /* tiled profile: the variant with the heap in HBM and the full window set (promotion target) */
     Store<HotSmall> s0;
     Store<HotMid> s1;
     Store<HotBig> s2;

@@ -325,11 +325,12 @@ static int32_t read_hdr(mt_engine* e, int32_t* err, int32_t* err_op, int32_t* st
  * next profile: small / config-5 -> HotMid (2,048 nodes, 24 key slots) -> HotBig (16,384) -> HotHuge
  * (262,144, tiled), with four times the arena, membership and pending-group capacities. The promoted
  * documents' records are gathered on the device; their text / props / kv pools stay the parent's. */
-static int32_t next_ncap(int profile) {
-    switch (profile) {
+static int32_t next_ncap(const mt_engine* e) {
+    switch (e->profile) {
     case 0: case 3: return HotMid::N;
     case 1: return HotBig::N;
     case 2: return HotHuge::N;
+    case 4: return e->fx || e->wide ? -1 : HotHuge::N; /* the tiled kernel's LDS heap -> its wide variant */
     default: return -1;
     }
 }
@@ -382,7 +383,7 @@ static int32_t stage_subset(mt_engine* e, mt_engine* o) {
 static int32_t promote(mt_engine* e) {
     std::fill(e->pro.begin(), e->pro.end(), -1);
     e->pro_docs.clear();
-    int32_t nc = next_ncap(e->profile);
+    int32_t nc = next_ncap(e);
     if (nc < 0) return MT_OK;
     int64_t nd = e->ndocs;
     std::vector<int32_t> err((size_t)nd);
@@ -414,6 +415,7 @@ static int32_t promote(mt_engine* e) {
         e->over = o;
     }
     o->promote = e->promote;
+    o->wide = e->profile == 4; /* HotHuge -> HotHuge: the same layout, the wide kernel */
     if (e->collab) {
         std::vector<int32_t> loc((size_t)(3 * m)); /* the promoted documents' ids, minSeqs, currentSeqs */
         for (int64_t i = 0; i < m; i++)
