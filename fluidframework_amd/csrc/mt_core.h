@@ -1359,6 +1359,25 @@ struct Replica {
         return m ? leaf * MAXN + W::ffs(m) : -1;
     }
 
+    /* slot_of(ra, -1) and slot_of(rb, -1) with both lookups' reads issued together (two round trips, not four) */
+    MT_HD void slot_of2(int32_t ra, int32_t rb, int32_t* sa, int32_t* sb) {
+        if constexpr (W::N >= 2 * MAXN) {
+            int32_t la = z.rleaf[ra], lb = z.rleaf[rb];
+            int32_t ca = nch[la], cb = nch[lb];
+            const int32_t j = w.lane();
+            const bool first = j < MAXN;
+            int32_t lf = first ? la : lb;
+            int32_t r = j < 2 * MAXN ? (int32_t)z.rid[lf * MAXN + (j & (MAXN - 1))] : -1;
+            uint64_t m = w.ballot(j < 2 * MAXN && (j & (MAXN - 1)) < (first ? ca : cb) && r == (first ? ra : rb));
+            uint64_t ma = m & 0xFFull, mb = (m >> MAXN) & 0xFFull;
+            *sa = ma ? la * MAXN + W::ffs(ma) : -1;
+            *sb = mb ? lb * MAXN + W::ffs(mb) : -1;
+        } else {
+            *sa = slot_of(ra, -1);
+            *sb = slot_of(rb, -1);
+        }
+    }
+
     /* ---- tiled profile: rope of leaves, STABLE summaries, window set ------------------- */
     MT_HD void rope_init() {
         auto& t = z.tl;
@@ -2370,7 +2389,10 @@ struct Replica {
      * row being split and the ones the slab shift moves), its child count and the free row-id stack's top are
      * read in one pass, the row's cold record (one dword per lane) in a second; the shift, the new row and its
      * cold copy are then written from registers. Same result as the serial form below. */
-    MT_HD int32_t split_row_par(int32_t n, int32_t j, int32_t off, int32_t* rsOut) {
+    /* gapOut (an insert placed right after the left part, insert_row): when the leaf has room for both, the same
+     * write pass also leaves an empty slot between the halves for the new row (rows after the split move two
+     * slots), which *gapOut returns — the shift leaf_insert_slot would make with a second read of the leaf */
+    MT_HD int32_t split_row_par(int32_t n, int32_t j, int32_t off, int32_t* rsOut, int32_t* gapOut = nullptr) {
         constexpr int CW = (int)(sizeof(typename HT::Cold) / 4);
         static_assert(W::N >= CW && W::N >= MAXN, "a lane per cold dword and per slot");
         const int32_t l = w.lane();
@@ -2386,18 +2408,24 @@ struct Replica {
         typename HT::Cold* cd = d.cold();
         const int32_t* csrc = (const int32_t*)&cd[rid0];
         int32_t cv = l < CW ? csrc[l] : 0; /* the row's cold record: toff is dword 2, ovx the top of dword 3 */
-        /* leaf_insert_slot(n, j + 1, dup): rows j..c-1 move right one slot; slot j + 1 starts as row j */
+        /* leaf_insert_slot(n, j + 1, dup): rows j..c-1 move right one slot; slot j + 1 starts as row j (with a gap:
+         * two slots, slot j + 2 starts as row j and slot j + 1 is the new row's) */
+        const int32_t g = gapOut && c + 2 < MAXN ? 1 : 0;
         bool willSplit = c + 1 >= MAXN;
         {
             MT_PROF_SCOPE(PH_LEAFINS);
             bool mv = l >= j && l < c && l < MAXN;
             w.sync();
-            if (mv) store_row(n * MAXN + l + 1, rr);
+            if (mv) store_row(n * MAXN + l + 1 + g, rr);
             w.sync();
             z.rid[n * MAXN + j + 1] = -1; /* not a row yet (a leaf split must not re-home it) */
-            nch[n] = (int8_t)(c + 1);
+            if (g) {
+                if constexpr (TILED) z.tl.xf[n * MAXN + j + 1] = 0;
+                *gapOut = n * MAXN + j + 1;
+            }
+            nch[n] = (int8_t)(c + 1 + g);
         }
-        int32_t rs = n * MAXN + j + 1;
+        int32_t rs = n * MAXN + j + 1 + g;
         if (willSplit) {
             MT_PROF_SCOPE(PH_LEAFINS);
             int32_t nn = split_node(n);
@@ -2455,12 +2483,12 @@ struct Replica {
     }
     /* Split the row at lorder coordinate t at offset off (0 < off < len). Returns the slot of
      * the LEFT part afterwards (the right part is the next row in document order). */
-    MT_HD int32_t split_row(int32_t t, int32_t off, int32_t* rsOut = nullptr) {
+    MT_HD int32_t split_row(int32_t t, int32_t off, int32_t* rsOut = nullptr, int32_t* gapOut = nullptr) {
         MT_PROF_SCOPE(PH_SPLIT);
         int32_t n = leaf_at(t >> 3), j = t & 7;
         int32_t s0 = n * MAXN + j;
         if constexpr (W::N >= 64) {
-            if (!dl_on() && !refs_on()) return split_row_par(n, j, off, rsOut);
+            if (!dl_on() && !refs_on()) return split_row_par(n, j, off, rsOut, gapOut);
         }
         if (z.flags(s0) & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
         bool willSplit = nch[n] + 1 >= MAXN;
@@ -3822,8 +3850,14 @@ struct Replica {
             int32_t t = find_reach(pos, refSeq, client, &P, &s, &v);
             if (t < 0) return -1;
             if (P + v > pos && !(z.flags(s) & RF_MARKER)) {
-                int32_t ls = split_row(t, pos - P);
+                int32_t rs = -1, gap = -1;
+                int32_t ls = split_row(t, pos - P, &rs, &gap);
                 if (ls < 0) return -1;
+                /* the right part (visible: the row was) starts the run at pos and captures the insert, which goes
+                 * right before it when no leaf boundary falls between the halves (Appendix C); no row read, and on
+                 * the GPU the split's own write pass left the slot */
+                if (gap >= 0) return gap;
+                if (rs >= 0 && rs / MAXN == ls / MAXN) return leaf_insert_slot(ls / MAXN, (ls & (MAXN - 1)) + 1);
                 k = kpos(ls / MAXN);
                 j = (ls & (MAXN - 1)) + 1;
             } else {
@@ -4070,26 +4104,28 @@ struct Replica {
         if (Pf < start || Pg + vg > end) {
             int32_t ridLast = z.rid[sg];
             int32_t ridFirst = z.rid[sf];
+            int32_t sl = sg; /* the last row's slot, while nothing has moved it */
             if (Pf < start) { /* start falls inside the first row: split it; its right part is first */
                 int32_t rs = -1;
                 if (split_row(tf, start - Pf, &rs) < 0 || rs < 0) return;
+                sl = -1;
                 if (tf == tg) {
                     ridLast = z.rid[rs];
+                    sl = rs;
                     vg = Pf + vf - start;
                     Pg = start;
                 }
                 ridFirst = z.rid[rs];
             }
             if (Pg + vg > end) { /* end falls inside the last row: split it; its left part keeps the id */
-                int32_t sl = slot_of(ridLast, -1);
+                if (sl < 0) sl = slot_of(ridLast, -1);
                 if (sl < 0) {
                     fail(E_ASSERT);
                     return;
                 }
                 if (split_row(kpos(sl / MAXN) * MAXN + (sl & (MAXN - 1)), end - Pg) < 0) return;
             }
-            sa = slot_of(ridFirst, -1);
-            sb = slot_of(ridLast, -1);
+            slot_of2(ridFirst, ridLast, &sa, &sb);
             if (sa < 0 || sb < 0) {
                 fail(E_ASSERT);
                 return;
@@ -4175,25 +4211,29 @@ struct Replica {
         }
         int32_t ridLast = z.rid[sg];
         int32_t ridFirst = z.rid[sf];
+        int32_t sl = sg; /* the last row's slot, while nothing has moved it */
         if (Pf < start) {
             int32_t rs = -1;
             if (split_row(tf, start - Pf, &rs) < 0 || rs < 0) return;
+            sl = -1;
             if (tf == tg) {
                 ridLast = z.rid[rs];
+                sl = rs;
                 vg = Pf + vf - start;
                 Pg = start;
             }
             ridFirst = z.rid[rs];
         }
         if (Pg + vg > end) {
-            int32_t sl = slot_of(ridLast, -1);
+            if (sl < 0) sl = slot_of(ridLast, -1);
             if (sl < 0) {
                 fail(E_ASSERT);
                 return;
             }
             if (split_row(kpos(sl / MAXN) * MAXN + (sl & (MAXN - 1)), end - Pg) < 0) return;
         }
-        int32_t sa = slot_of(ridFirst, -1), sb = slot_of(ridLast, -1);
+        int32_t sa, sb;
+        slot_of2(ridFirst, ridLast, &sa, &sb);
         if (sa < 0 || sb < 0) {
             fail(E_ASSERT);
             return;
