@@ -192,6 +192,7 @@ class ReplayEngine {
         this.currentSeq = new Array(ndocs).fill(0);
         this.nrefs = new Array(ndocs).fill(0);   // local references created per document
         this.pending = Array.from({ length: ndocs }, () => []); // op types in flight, per pending group
+        this.version = 0; // bumped by every enqueued record and every collaboration start: cached reads expire
     }
 
     longIndex(name) {
@@ -216,9 +217,11 @@ class ReplayEngine {
         }
         addon.startCollab(this.h, ids, mins, curs);
         this.collab = true;
+        this.version++;
     }
 
     enqueue(doc, kind, fields, segOrProps) {
+        this.version++;
         const q = this.queues[doc];
         const r = { kind, seg_kind: 0, client: 0, seq: 0, ref_seq: 0, min_seq: 0, pos1: 0, pos2: 0, text_off: 0,
             text_len: 0, props: 0, ...fields };
@@ -539,6 +542,17 @@ class GpuClient {
     /* The replica's segments in walkAllSegments order (decodeDump), each with its handle (rid, gen: getPosition
      * and getContainingSegment's handles) and its position in the local view (pos; localNetLength in len) */
     segments() {
+        /* decoded once per replica state: every read of it (walkSegments, findTile, getPropertiesAtPosition,
+         * getMarkerFromId, ...) reuses the decode until the next enqueued record (ADVICE r4) */
+        const e = this.engine;
+        if (this._seg && this._segVersion === e.version) return this._seg;
+        const d = this._decodeSegments();
+        this._seg = d;
+        this._segVersion = e.version;
+        return d;
+    }
+
+    _decodeSegments() {
         const h = this.read();
         const names = [...this.engine.clientIds.keys()];
         const d = decodeDump(addon.dump(h, this.doc), this.engine.interner, (i) => (i < 0 ? LocalClientId : names[i]));
