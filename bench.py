@@ -19,7 +19,8 @@ node at 65k docs"); --scaling weak gives every rank --docs documents of its own 
 data-path collective; RCCL all-gathers per-document digests once, after timing.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|4|5] [--docs D]
-                       [--ops-per-doc O] [--scaling strong|weak] [--no-cpu-baseline]
+                       [--ops-per-doc O] [--scaling strong|weak] [--assign uniform|cost] [--share R/N]
+                       [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -136,6 +137,13 @@ def main() -> None:
     ap.add_argument("--doc-times-out", default="", help="save each document's replay start / end (.npy, 100 MHz ticks)")
     ap.add_argument("--order", choices=("cost", "doc"), default="doc",
                     help="replay dispatch order: document order (doc, default: the configs' documents are uniform and r05b measured cost order 3 %% slower on config 3) or longest-first by shard.doc_costs (cost)")
+    ap.add_argument("--assign", choices=("uniform", "cost"), default="uniform",
+                    help="strong scaling: bin-pack the node's documents on their message count (uniform: every "
+                         "config draws the same number per document, no generation beyond the rank's share) or on "
+                         "shard.doc_costs of the generated logs (cost: every rank generates the node's logs first)")
+    ap.add_argument("--share", default="",
+                    help="R/N: on one GPU, replay the share rank R of an N-rank strong-scaling run would get (the "
+                         "per-GPU load of the multi-GPU bench, measured without the other ranks; value = that share)")
     ap.add_argument("--gen-cache", default=os.environ.get("MT_GEN_CACHE", ""),
                     help="directory caching generated workloads between runs (profiler passes)")
     args = ap.parse_args()
@@ -168,19 +176,34 @@ def main() -> None:
     w = workload(args.config, ops)
 
     # ---- this rank's documents ----
+    a_rank, a_world = rank, world  # the share of the assignment this process replays
+    if args.share:
+        if world != 1 or args.scaling != "strong":
+            raise SystemExit("--share simulates one rank's strong-scaling share on a single process")
+        a_rank, a_world = (int(x) for x in args.share.split("/"))
+        if not 0 <= a_rank < a_world:
+            raise SystemExit(f"--share {args.share}: need 0 <= R < N")
+    t0 = time.time()
     if args.scaling == "strong":
-        # cost model: every document of a config draws the same number of sequenced messages, so
-        # the LPT bin-packing (shard.assign) gives an even split; farms (config 1) stay whole
+        # LPT bin-packing (shard.assign) of the node's documents; farms (config 1) stay whole
         unit = w.nclients if args.config == 1 else 1
-        groups = shard.assign(np.full(docs // unit, float(ops)), world)
-        mine = np.concatenate([g[:, None] * unit + np.arange(unit) for g in groups[rank:rank + 1]]).ravel()
+        if args.assign == "cost" and unit == 1:
+            # every rank generates the node's logs and packs on shard.doc_costs (deterministic: no exchange)
+            full = generate_cached(w, np.arange(docs), args.gen_cache, f"c{args.config}_d{docs}_o{ops}_all")
+            groups = shard.assign(shard.doc_costs(full), a_world)
+        else:
+            # every document of a config draws the same number of sequenced messages: an even split
+            full = None
+            groups = shard.assign(np.full(docs // unit, float(ops)), a_world)
+        mine = np.concatenate([g[:, None] * unit + np.arange(unit) for g in groups[a_rank:a_rank + 1]]).ravel()
         node_docs = docs
     else:
+        full = None
         mine = shard.weak_ids(rank, docs)
         node_docs = docs * world
-    t0 = time.time()
-    key = f"c{args.config}_d{docs}_o{ops}_{args.scaling}_r{rank}of{world}"
-    batch = generate_cached(w, mine, args.gen_cache, key)
+    key = f"c{args.config}_d{docs}_o{ops}_{args.scaling}_{args.assign}_r{a_rank}of{a_world}"
+    batch = full.subset(mine) if full is not None else generate_cached(w, mine, args.gen_cache, key)
+    del full
     log(f"rank {rank}: generated {batch.ndocs} docs, {batch.nops} events in {time.time() - t0:.1f}s")
     local_events = int(((batch.ops["kind"] & 0x80) != 0).sum())
 
@@ -282,7 +305,10 @@ def main() -> None:
             "data": "synthetic (mt_gen: splitmix64(0x5EED0000+doc) xoshiro256**)",
             "config": {"workload": desc.format(ops=ops, docs=docs), "config": args.config,
                        "docs_per_node": node_docs, "docs_rank0": int(batch.ndocs), "ops_per_doc": ops,
-                       "local_edits_rank0": local_events, "parallelism": f"docs bin-packed x{world}",
+                       "local_edits_rank0": local_events,
+                       "parallelism": (f"share {a_rank}/{a_world} of the docs bin-packed x{a_world} ({args.assign} "
+                                       f"costs), one GPU: value is that share's rate" if args.share else
+                                       f"docs bin-packed x{world} ({args.assign} costs)"),
                        "docs_promoted_rank0": promoted, "docs_in_error_rank0": int(len(bad))},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -146,8 +146,13 @@ __device__ inline void doc_stamp(HT* t, int end) {
 /* VAR tags a build variant compiled with other flags in its own translation unit (1: compiler-chosen
  * inlining): the kernel's name must differ, since a host launch resolves the kernel by name. */
 /* DL: the delta-event build (engines created with caps.dcap > 0) */
+#ifdef MT_NUM_SGPR /* experiment: an explicit SGPR budget for the flat kernel */
+#define MT_SGPR_ATTR __attribute__((amdgpu_num_sgpr(MT_NUM_SGPR)))
+#else
+#define MT_SGPR_ATTR
+#endif
 template <class HT, bool LDS, int MINW = 1, int SKM = 1, int VAR = 0, bool DL = false, bool LOAD = true> /* SKM: 1 Skel, 2 SkelLite, 0 none */
-__global__ __launch_bounds__(WG, MINW) void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
+__global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                               const int64_t* op_off, const uint16_t* text, const int64_t* text_off,
                                               const mt_props_rec* props, const int64_t* props_off, const mt_kv* kv,
                                               const int64_t* kv_off, ReplayAux aux) {

@@ -57,16 +57,18 @@ def replay_units() -> list:
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
 
-def build_replay(force: bool = False, defines: tuple = (), name: str = "libmtreplay.so", jobs: int = 0) -> str:
+def build_replay(force: bool = False, defines: tuple = (), name: str = "libmtreplay.so", jobs: int = 0,
+                 extra: tuple = ()) -> str:
     """The product library: HIP kernels for gfx950 + the C ABI of include/mt_engine.h. Each unit
-    compiles to its own object (build/obj-<name>/), up to `jobs` at once, then one link."""
+    compiles to its own object (build/obj-<name>/), up to `jobs` at once, then one link. `extra`: more hipcc
+    flags (e.g. -gline-tables-only for a build whose PC samples map to source lines)."""
     out = lib_path(name)
     units = replay_units()
     hdrs = [os.path.join(CSRC, f) for f in CORE_HDRS + ("mt_kernels.h",)] + [
         os.path.join(ROOT, "include", "mt_engine.h"), os.path.join(ROOT, "include", "mt_oplog.h")]
     objdir = os.path.join(BUILD, "obj-" + name.replace(".so", ""))
     os.makedirs(objdir, exist_ok=True)
-    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"] + ["-D" + d for d in defines]
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"] + ["-D" + d for d in defines] + list(extra)
     todo = []
     objs = []
     for u in units:
