@@ -1654,6 +1654,9 @@ struct Replica {
      * STABLE summaries (or DEAD), entries of freed rows drop out, and every remaining row's chunk
      * position, leaf index and perspective length go to the scratch, its length scattered onto
      * cdel[chunk position]. Returns the sum of those lengths. */
+#ifndef MT_FIND2
+#define MT_FIND2 1 /* a tiled range op's two ends found in the same passes (tile_find2 / leaf_find2) */
+#endif
 #ifndef MT_WIN_NB
 #define MT_WIN_NB 2 /* wave passes of the window set issued together: the set is ~80-100 rows, so 2 passes cover it in one round trip without the dead issue of 8 (r04e A/B at 256 x 300k: 8.81 -> 9.66M ops/s) */
 #endif
@@ -1843,6 +1846,136 @@ struct Replica {
         }
         fail(E_ASSERT); /* the chunk's leaves must add up to its summary */
         return -1;
+    }
+    /* tile_find of two positions pa <= pb in the same passes (a range op's first and last rows): one chunk scan
+     * finds both chunks, and both chunks' leaf-summary lines are read in one round trip. Same answers as two
+     * tile_find calls. */
+    MT_HD void tile_find2(int32_t pa, int32_t pb, int32_t* ka, int32_t* Pa, int32_t* Na, int32_t* kb, int32_t* Pb,
+                          int32_t* Nb) {
+        MT_PROF_SCOPE(PH_TFIND);
+        static_assert(W::N >= HT::TL::CH, "a lane per leaf of a chunk");
+        auto& t = z.tl;
+        int32_t nc = t.nchunk;
+        int32_t run = 0, ra = 0, rb = 0, cpa = -1, cpb = -1;
+        *ka = *kb = -1;
+        for (int32_t b = 0; b < nc && cpb < 0; b += 4 * W::N) {
+            int32_t p0 = b + 4 * w.lane();
+            int32_t v[4];
+            for (int q = 0; q < 4; q++) v[q] = p0 + q < nc ? tcst[p0 + q] + cdel[p0 + q] : 0;
+            int32_t tot;
+            int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
+            int32_t ha = -1, hpa = 0, hb = -1, hpb = 0;
+            for (int q = 0; q < 4; q++) {
+                if (ha < 0 && p < pa && pa <= p + v[q]) {
+                    ha = q;
+                    hpa = p;
+                }
+                if (hb < 0 && p < pb && pb <= p + v[q]) {
+                    hb = q;
+                    hpb = p;
+                }
+                p += v[q];
+            }
+            uint64_t m = w.ballot(ha >= 0);
+            if (cpa < 0 && m) {
+                int32_t l = W::ffs(m);
+                ra = w.bcast(hpa, l);
+                cpa = b + 4 * l + w.bcast(ha, l);
+            }
+            m = w.ballot(hb >= 0);
+            if (m) {
+                int32_t l = W::ffs(m);
+                rb = w.bcast(hpb, l);
+                cpb = b + 4 * l + w.bcast(hb, l);
+            }
+            run += tot;
+        }
+        if (cpa < 0 || cpb < 0) return;
+        int32_t ca = tcord[cpa], cb = tcord[cpb], na = tccnt[ca], nb = tccnt[cb];
+        int32_t nw = t.wN;
+        int32_t lda = 0, ldb = 0; /* lane l: the window rows' lengths in leaf l of each chunk */
+        for (int32_t b = 0; b < nw; b += W::N) {
+            int32_t i = b + w.lane();
+            int32_t cp = i < nw ? wcp[i] : -1;
+            uint64_t m = w.ballot(cp == cpa || cp == cpb);
+            while (m) {
+                int32_t l = W::ffs(m);
+                m &= m - 1;
+                int32_t lx = w.bcast(i < nw ? wlx[i] : 0, l);
+                int32_t vv = w.bcast(i < nw ? wvs[i] : 0, l);
+                int32_t c2 = w.bcast(cp, l);
+                if (w.lane() == lx) {
+                    if (c2 == cpa) lda += vv;
+                    if (c2 == cpb) ldb += vv;
+                }
+            }
+        }
+        int32_t l = w.lane();
+        int32_t va = 0, la = 0, vb = 0, lb = 0;
+        if (l < na) { /* both chunks' leaf summaries and node ids: one round trip */
+            va = t.cls[ca][l];
+            la = t.cleaf[ca][l];
+        }
+        if (l < nb) {
+            vb = t.cls[cb][l];
+            lb = t.cleaf[cb][l];
+        }
+        va += lda;
+        vb += ldb;
+        int32_t tot;
+        int32_t p = ra + w.excl_scan(l < na ? va : 0, &tot);
+        uint64_t m = w.ballot(l < na && p < pa && pa <= p + va);
+        if (m) {
+            int32_t x = W::ffs(m);
+            *Pa = w.bcast(p, x);
+            *Na = w.bcast(la, x);
+            *ka = (cpa << 6) | x;
+        }
+        p = rb + w.excl_scan(l < nb ? vb : 0, &tot);
+        m = w.ballot(l < nb && p < pb && pb <= p + vb);
+        if (m) {
+            int32_t x = W::ffs(m);
+            *Pb = w.bcast(p, x);
+            *Nb = w.bcast(lb, x);
+            *kb = (cpb << 6) | x;
+        }
+        if (*ka < 0 || *kb < 0) fail(E_ASSERT); /* the chunk's leaves must add up to its summary */
+    }
+    /* leaf_find of two (leaf, position) pairs in one round trip: lanes 0-7 read leaf na's rows, lanes 8-15 leaf
+     * nb's. Same answers as two leaf_find calls. */
+    MT_HD void leaf_find2(int32_t ka, int32_t na, int32_t Pa, int32_t pa, int32_t kb, int32_t nb, int32_t Pb, int32_t pb,
+                          int32_t refSeq, int32_t client, int32_t* ta, int32_t* Poa, int32_t* Sa, int32_t* Va,
+                          int32_t* tb, int32_t* Pob, int32_t* Sb, int32_t* Vb) {
+        MT_PROF_SCOPE(PH_LFIND);
+        static_assert(W::N >= 2 * MAXN, "a lane per row of two leaves");
+        int32_t j = w.lane();
+        bool A = j < MAXN, B = j >= MAXN && j < 2 * MAXN;
+        int32_t n = A ? na : nb;
+        int32_t s = n * MAXN + (j & (MAXN - 1));
+        RowView r = row_view(s);
+        int32_t c = nch[n];
+        int32_t v = (A || B) && (j & (MAXN - 1)) < c ? vis_of(s, r, refSeq, client) : 0;
+        int32_t tot;
+        int32_t p = Pa + w.excl_scan(A ? v : 0, &tot);
+        uint64_t m = w.ballot(A && p < pa && pa <= p + v);
+        *ta = *tb = -1;
+        if (m) {
+            int32_t l = W::ffs(m);
+            *Poa = w.bcast(p, l);
+            *Sa = na * MAXN + l;
+            *Va = w.bcast(v, l);
+            *ta = ka * MAXN + l;
+        }
+        p = Pb + w.excl_scan(B ? v : 0, &tot);
+        m = w.ballot(B && p < pb && pb <= p + v);
+        if (m) {
+            int32_t l = W::ffs(m);
+            *Pob = w.bcast(p, l);
+            *Sb = nb * MAXN + (l - MAXN);
+            *Vb = w.bcast(v, l);
+            *tb = kb * MAXN + (l - MAXN);
+        }
+        if (*ta < 0 || *tb < 0) fail(E_ASSERT);
     }
     /* within leaf position k (start offset P): the row t = k*8+j with P < pos <= P + vis */
     /* n: the leaf node at k (tile_find's) */
@@ -3132,14 +3265,17 @@ struct Replica {
         append_rows(a, b, z.rid[a], z.rid[b], z.len(a), z.len(b), z.flags(a), z.flags(b), xa, xb);
     }
     /* append_text with the two rows' ids, lengths, flags and window flags as the caller read them (scour) */
-    MT_HD void append_rows(int32_t a, int32_t b, int32_t ra, int32_t rb, int32_t La, int32_t Lb, uint32_t fa,
-                           uint32_t fb, uint32_t xa, uint32_t xb) {
-        MT_PROF_SCOPE(PH_APPEND);
+    MT_HD void append_stat(int32_t a, int32_t Lb, uint32_t xa, uint32_t xb) {
         if constexpr (TILED) { /* b's length joins a's row: keep the leaf's STABLE sum exact */
             bool sa = xa & XF_STABLE, sb = xb & XF_STABLE;
             if (sa && !sb) lst_add(a / MAXN, Lb);
             if (!sa && sb) lst_add(a / MAXN, -Lb);
         }
+    }
+    MT_HD void append_rows(int32_t a, int32_t b, int32_t ra, int32_t rb, int32_t La, int32_t Lb, uint32_t fa,
+                           uint32_t fb, uint32_t xa, uint32_t xb) {
+        MT_PROF_SCOPE(PH_APPEND);
+        append_stat(a, Lb, xa, xb);
         if (fa & RF_PERM) { /* PermutationSegment.append (permutationvector.ts:95-101) */
             z.len(a) = La + Lb;
             return;
@@ -3163,6 +3299,29 @@ struct Replica {
         z.len(a) = La + Lb;
         /* the merged text ends where b's did */
         z.flags(a) = (uint8_t)((fa & ~(uint32_t)(RF_NLK | RF_NL)) | (fb & (RF_NLK | RF_NL)));
+    }
+#ifndef MT_APPEND_BATCH
+#define MT_APPEND_BATCH 1 /* scour's text appends planned on scalars during the walk, their copies made together after it */
+#endif
+    /* copy jobs of scour's append walk: lane j < nj holds job j (destination, source, units in the current arena
+     * half); all of them in one wave-parallel copy, a lane per unit, every load of a block before its stores (the
+     * sources are texts from before the walk, the destinations fresh space above them) */
+    MT_HD void copy_jobs(int32_t jd, int32_t js, int32_t jn, int32_t nj) {
+        uint16_t* base = arena_base(zh->arenaSide);
+        int32_t tot;
+        int32_t pre = w.excl_scan(w.lane() < nj ? jn : 0, &tot);
+        for (int32_t b = 0; b < tot; b += W::N) {
+            int32_t i = b + w.lane();
+            int32_t jj = 0;
+            for (int32_t t = 1; t < nj; t++)
+                if (w.bcast(pre, t) <= i) jj = t;
+            int32_t o = i - w.shfl(pre, jj);
+            int32_t src = w.shfl(js, jj), dst = w.shfl(jd, jj);
+            uint16_t v = i < tot ? base[src + o] : 0;
+            w.sync();
+            if (i < tot) base[dst + o] = v;
+        }
+        w.sync();
     }
     /* scourNode on leaf n: compacts the slab in place; returns the new child count. Rows are
      * merged into their predecessor or unlinked exactly as the reference decides. */
@@ -3288,6 +3447,7 @@ struct Replica {
          * last row (appends require equal properties, keep the head's start, and end with the appended
          * text), so "head + row k" is decided by rows k-1 and k. Lane k: the pair (k-1, k). */
         bool pairOk = false;
+        int32_t tofP = 0, tofK = 0; /* a pair's text offsets (its left and right row), read with its tests */
         /* the shuffles read the predecessor lane, which may not be a pair's lane: outside the branch, where
          * every lane is active */
         int32_t lenP = w.shfl(r.len, q - 1), flP = w.shfl(fl, q - 1);
@@ -3300,16 +3460,18 @@ struct Replica {
                      (permPair || !((flP | fl) & RF_NOTEXT));
             const typename HT::Cold& ca = d.cold()[ridP];
             const typename HT::Cold& cb = d.cold()[(int32_t)r.rid];
+            tofP = (int32_t)ca.toff;
+            tofK = (int32_t)cb.toff;
             if (pairOk && (fl & RF_PROPS)) { /* matchProperties (properties.ts:61-92) */
                 for (int i = 0; i < HT::K / 8; i++)
                     if (!eq4(ld4((const int32_t*)&ca.pv[8 * i]), ld4((const int32_t*)&cb.pv[8 * i]))) pairOk = false;
             }
             if (pairOk && permPair) { /* PermutationSegment.canAppend: handles follow, or both unallocated */
-                uint32_t sa = ca.toff, sb = cb.toff;
+                uint32_t sa = (uint32_t)tofP, sb = (uint32_t)tofK;
                 pairOk = sa == 0 ? sb == 0 : sb == sa + (uint32_t)lenP;
             } else if (pairOk) { /* TextSegment.canAppend: the run does not end with "\n" (textSegment.ts:64) */
                 bool nl = (flP & RF_NLK) ? (flP & RF_NL) != 0
-                                         : arena_base(zh->arenaSide)[ca.toff + lenP - 1] == '\n';
+                                         : arena_base(zh->arenaSide)[tofP + lenP - 1] == '\n';
                 pairOk = !nl;
             }
         }
@@ -3322,6 +3484,14 @@ struct Replica {
         keep |= pairs & ~okm;
         uint64_t app = 0; /* rows appended so far */
         uint64_t m = pairs & okm;
+#if MT_APPEND_BATCH
+        /* TextSegment.append's arena work planned on the run head's text offset (prevT): copy jobs (lane j: job j)
+         * and the heads whose text moved (lane: the new offset), applied after the walk; the same arena decisions
+         * as append_rows. A walk that needs a GC applies what it planned and goes on through append_rows. */
+        int32_t jd = 0, js = 0, jn = 0, nj = 0, ntof = 0, prevT = 0;
+        uint64_t moved = 0;
+        bool serial = false;
+#endif
         while (m) {
             int32_t k = W::ffs(m);
             m &= m - 1;
@@ -3329,6 +3499,9 @@ struct Replica {
                 prev = k - 1;
                 prevLen = w.bcast(r.len, prev);
                 prevFl = w.bcast(fl, prev);
+#if MT_APPEND_BATCH
+                prevT = w.bcast(tofP, k);
+#endif
             }
             int32_t lk = w.bcast(r.len, k);
             int32_t fk = w.bcast(fl, k);
@@ -3340,9 +3513,51 @@ struct Replica {
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
                 int32_t rp = w.bcast((int32_t)r.rid, prev), rk = w.bcast((int32_t)r.rid, k);
                 if (refs_on()) refs_append(rp, rk, prevLen);
+                uint32_t xp = TILED ? (uint32_t)w.bcast((int32_t)r.xf, prev) : 0u, xk = TILED ? (uint32_t)w.bcast((int32_t)r.xf, k) : 0u;
+#if MT_APPEND_BATCH
+                if (!serial && (prevFl & RF_PERM)) {
+                    append_stat(sp, lk, xp, xk); /* PermutationSegment.append: the length, written by the compaction */
+                } else if (!serial) {
+                    MT_PROF_SCOPE(PH_APPEND);
+                    append_stat(sp, lk, xp, xk);
+                    int32_t tb = w.bcast(tofK, k), top = h.arenaTop, cap = d.caps.acap;
+                    if (prevT + prevLen == top && top + lk <= cap) { /* the head's text ends at the top: extend it */
+                        jd = w.writelane(top, nj, jd);
+                        js = w.writelane(tb, nj, js);
+                        jn = w.writelane(lk, nj, jn);
+                        nj++;
+                        h.arenaTop = top + lk;
+                    } else if (prevT + prevLen == tb) { /* already contiguous */
+                    } else if (top + prevLen + lk <= cap) { /* both texts to the top */
+                        jd = w.writelane(top, nj, jd);
+                        js = w.writelane(prevT, nj, js);
+                        jn = w.writelane(prevLen, nj, jn);
+                        jd = w.writelane(top + prevLen, nj + 1, jd);
+                        js = w.writelane(tb, nj + 1, js);
+                        jn = w.writelane(lk, nj + 1, jn);
+                        nj += 2;
+                        prevT = top;
+                        ntof = w.writelane(top, prev, ntof);
+                        moved |= 1ull << prev;
+                        h.arenaTop = top + prevLen + lk;
+                    } else { /* a GC: the copies, the heads' lengths and moved offsets land first (it reads them) */
+                        copy_jobs(jd, js, jn, nj);
+                        nj = 0;
+                        if (valid && nlen != r.len) z.len(n * MAXN + j) = nlen;
+                        if ((moved >> q) & 1) d.cold()[r.rid].toff = (uint32_t)ntof;
+                        moved = 0;
+                        w.sync();
+                        serial = true;
+                        append_rows(sp, sk, rp, rk, prevLen, lk, (uint32_t)prevFl, (uint32_t)fk, 0u, 0u);
+                    }
+                    if (nj > W::N - 2) { /* room for the next append's two jobs */
+                        copy_jobs(jd, js, jn, nj);
+                        nj = 0;
+                    }
+                } else
+#endif
                 /* updates z.len(sp) (read by a GC inside it) and its NL bits */
-                append_rows(sp, sk, rp, rk, prevLen, lk, (uint32_t)prevFl, (uint32_t)fk,
-                            TILED ? (uint32_t)w.bcast((int32_t)r.xf, prev) : 0u, TILED ? (uint32_t)w.bcast((int32_t)r.xf, k) : 0u);
+                append_rows(sp, sk, rp, rk, prevLen, lk, (uint32_t)prevFl, (uint32_t)fk, xp, xk);
                 prevLen += lk;
                 prevFl = (prevFl & ~(RF_NLK | RF_NL)) | (fk & (RF_NLK | RF_NL));
                 nlen = w.writelane(prevLen, prev, nlen);
@@ -3353,6 +3568,10 @@ struct Replica {
                 keep |= 1ull << k; /* kept: the next pair, if it tests ok, starts from this row */
             }
         }
+#if MT_APPEND_BATCH
+        if (nj) copy_jobs(jd, js, jn, nj);
+        if ((moved >> q) & 1) d.cold()[r.rid].toff = (uint32_t)ntof;
+#endif
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
         uint64_t _t2 = __builtin_amdgcn_s_memtime();
         prof[PH_S2] += _t2 - _t1;
@@ -4182,17 +4401,32 @@ struct Replica {
                 return;
             }
             int32_t last = end < total ? end : total;
-            int32_t P1, P2;
-            int32_t n1 = 0, n2 = 0;
-            int32_t k1 = tile_find(start + 1, refSeq, client, &P1, &n1);
-            int32_t k2 = tile_find(last, refSeq, client, &P2, &n2);
+            int32_t P1 = 0, P2 = 0;
+            int32_t n1 = 0, n2 = 0, k1, k2;
+#if MT_FIND2
+            if constexpr (W::N >= 64) {
+                tile_find2(start + 1, last, &k1, &P1, &n1, &k2, &P2, &n2);
+            } else
+#endif
+            {
+                k1 = tile_find(start + 1, refSeq, client, &P1, &n1);
+                k2 = tile_find(last, refSeq, client, &P2, &n2);
+            }
             win_clear();
             if (k1 < 0 || k2 < 0) {
                 fail(E_ASSERT);
                 return;
             }
-            tf = leaf_find(k1, n1, P1, start + 1, refSeq, client, &Pf, &sf, &vf);
-            tg = leaf_find(k2, n2, P2, last, refSeq, client, &Pg, &sg, &vg);
+#if MT_FIND2
+            if constexpr (W::N >= 64) {
+                leaf_find2(k1, n1, P1, start + 1, k2, n2, P2, last, refSeq, client, &tf, &Pf, &sf, &vf, &tg, &Pg, &sg,
+                           &vg);
+            } else
+#endif
+            {
+                tf = leaf_find(k1, n1, P1, start + 1, refSeq, client, &Pf, &sf, &vf);
+                tg = leaf_find(k2, n2, P2, last, refSeq, client, &Pg, &sg, &vg);
+            }
         } else {
             int32_t total = length_tiled(refSeq, client);
             if (start >= total || end <= start) return;
