@@ -385,14 +385,23 @@ enum { PH_APPLY, PH_ZAMBONI, PH_FIND, PH_MAP, PH_SPLIT, PH_ACK, PH_TEXT, PH_HEAP
        PH_C_HEAPN, PH_C_POP, PH_C_PUSH,
        PH_N };
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
-struct ProfScope {
+struct ProfScope { /* no live register across the scope: the LDS counter takes -start at entry and +end at exit */
     uint64_t* acc;
-    uint64_t t0;
-    __device__ ProfScope(uint64_t* a) : acc(a), t0(__builtin_amdgcn_s_memtime()) {}
-    __device__ ~ProfScope() { *acc += __builtin_amdgcn_s_memtime() - t0; }
+    __device__ ProfScope(uint64_t* a) : acc(a) {
+        if (acc) *acc -= __builtin_amdgcn_s_memtime();
+    }
+    __device__ ~ProfScope() {
+        if (acc) *acc += __builtin_amdgcn_s_memtime();
+    }
 };
-#define MT_PROF_SCOPE(i) ProfScope _ps##i(&prof[i])
-#define MT_PROF_COUNT(i, n) (prof[i] += (uint64_t)(n))
+/* the clocks live in LDS (the replay kernels point prof at a __shared__ array; other kernels leave it null): an
+ * array of PH_N 64-bit counters held in registers spilled the profiled config-3 kernel to 900 B of scratch per lane */
+#ifdef MT_PROF_NOSCOPE
+#define MT_PROF_SCOPE(i)
+#else
+#define MT_PROF_SCOPE(i) ProfScope _ps##i(prof ? &prof[i] : nullptr)
+#endif
+#define MT_PROF_COUNT(i, n) (prof ? (void)(prof[i] += (uint64_t)(n)) : (void)0)
 #else
 #define MT_PROF_SCOPE(i)
 #define MT_PROF_COUNT(i, n)
@@ -427,7 +436,7 @@ struct Replica {
 
     RegHdr h; /* the header fields held in registers (SGPRs on the GPU) while the replica runs; the rest: zh */
 #ifdef MT_PROF
-    uint64_t prof[PH_N] = {};
+    uint64_t* prof = nullptr; /* LDS (the replay kernels), or none */
 #endif
 
     /* The tree skeleton's small per-node arrays and the zamboni heap are reached through these
@@ -1945,15 +1954,19 @@ struct Replica {
      * nb's. Same answers as two leaf_find calls. */
     MT_HD void leaf_find2(int32_t ka, int32_t na, int32_t Pa, int32_t pa, int32_t kb, int32_t nb, int32_t Pb, int32_t pb,
                           int32_t refSeq, int32_t client, int32_t* ta, int32_t* Poa, int32_t* Sa, int32_t* Va,
-                          int32_t* tb, int32_t* Pob, int32_t* Sb, int32_t* Vb) {
+                          int32_t* tb, int32_t* Pob, int32_t* Sb, int32_t* Vb, HotRow* rowsA, int32_t* cA) {
         MT_PROF_SCOPE(PH_LFIND);
         static_assert(W::N >= 2 * MAXN, "a lane per row of two leaves");
         int32_t j = w.lane();
         bool A = j < MAXN, B = j >= MAXN && j < 2 * MAXN;
         int32_t n = A ? na : nb;
         int32_t s = n * MAXN + (j & (MAXN - 1));
-        RowView r = row_view(s);
+        HotRow hr = load_row(s); /* lanes 0-7: leaf na's rows in full, for the split of the first row (split_row's pre) */
+        RowView r{hr.len, hr.seq, hr.rseq,
+                  (uint32_t)hr.cli | ((uint32_t)hr.rcli << 8) | ((uint32_t)hr.flags << 16) | ((uint32_t)hr.ng << 24)};
+        *rowsA = hr;
         int32_t c = nch[n];
+        *cA = w.bcast(c, 0);
         int32_t v = (A || B) && (j & (MAXN - 1)) < c ? vis_of(s, r, refSeq, client) : 0;
         int32_t tot;
         int32_t p = Pa + w.excl_scan(A ? v : 0, &tot);
@@ -1980,14 +1993,26 @@ struct Replica {
     /* within leaf position k (start offset P): the row t = k*8+j with P < pos <= P + vis */
     /* n: the leaf node at k (tile_find's) */
     /* *Sout / *Vout (optional): the row's slot and its perspective length */
+    /* rowsOut / cOut (GPU): every lane's row (lane j: child j & 7) in full and the child count, for a split of the
+     * found row that follows without another read of the leaf (split_row's pre) */
     MT_HD int32_t leaf_find(int32_t k, int32_t n, int32_t P, int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout,
-                            int32_t* Sout = nullptr, int32_t* Vout = nullptr) {
+                            int32_t* Sout = nullptr, int32_t* Vout = nullptr, HotRow* rowsOut = nullptr,
+                            int32_t* cOut = nullptr) {
         MT_PROF_SCOPE(PH_LFIND);
         if constexpr (W::N >= MAXN) { /* lane j: child j; one prefix scan */
             int32_t j = w.lane();
             int32_t s = n * MAXN + (j & (MAXN - 1));
-            RowView r = row_view(s); /* the leaf's slab is always in bounds: loaded with the child count */
+            RowView r;
+            if (rowsOut) { /* the whole row in the same pass */
+                HotRow hr = load_row(s);
+                r = RowView{hr.len, hr.seq, hr.rseq,
+                            (uint32_t)hr.cli | ((uint32_t)hr.rcli << 8) | ((uint32_t)hr.flags << 16) | ((uint32_t)hr.ng << 24)};
+                *rowsOut = hr;
+            } else {
+                r = row_view(s); /* the leaf's slab is always in bounds: loaded with the child count */
+            }
             int32_t c = nch[n];
+            if (cOut) *cOut = c;
             int32_t v = j < c ? vis_of(s, r, refSeq, client) : 0;
             int32_t tot;
             int32_t p = P + w.excl_scan(v, &tot);
@@ -2040,7 +2065,7 @@ struct Replica {
         return -1;
     }
     MT_HD int32_t find_reach_tiled(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout, int32_t* Sout,
-                                   int32_t* Vout) {
+                                   int32_t* Vout, HotRow* rowsOut = nullptr, int32_t* cOut = nullptr) {
         if (pos <= 0) return -1;
         if (!tiles_cover(refSeq, client)) return find_reach_walk(pos, refSeq, client, Pout, Sout, Vout);
         win_pass(refSeq, client);
@@ -2049,7 +2074,7 @@ struct Replica {
         int32_t k = tile_find(pos, refSeq, client, &P, &n);
         win_clear();
         if (k < 0) return -1;
-        return leaf_find(k, n, P, pos, refSeq, client, Pout, Sout, Vout);
+        return leaf_find(k, n, P, pos, refSeq, client, Pout, Sout, Vout, rowsOut, cOut);
     }
     MT_HD int32_t length_tiled(int32_t refSeq, int32_t client) {
         if (!tiles_cover(refSeq, client)) {
@@ -2278,9 +2303,10 @@ struct Replica {
     /* First row (document order) with P < pos <= P + vis; returns t (lorder coordinate) or -1,
      * and P of that row; *Sout / *Vout (optional): its slot and perspective length. */
     MT_HD int32_t find_reach(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout, int32_t* Sout = nullptr,
-                             int32_t* Vout = nullptr) {
+                             int32_t* Vout = nullptr, HotRow* rowsOut = nullptr,
+                             int32_t* cOut = nullptr) {
         MT_PROF_SCOPE(PH_FIND);
-        if constexpr (TILED) return find_reach_tiled(pos, refSeq, client, Pout, Sout, Vout);
+        if constexpr (TILED) return find_reach_tiled(pos, refSeq, client, Pout, Sout, Vout, rowsOut, cOut);
         int32_t run = 0;
         int32_t T = h.nleaf * MAXN;
         const bool loc = is_local(client);
@@ -2525,13 +2551,14 @@ struct Replica {
     /* gapOut (an insert placed right after the left part, insert_row): when the leaf has room for both, the same
      * write pass also leaves an empty slot between the halves for the new row (rows after the split move two
      * slots), which *gapOut returns — the shift leaf_insert_slot would make with a second read of the leaf */
-    MT_HD int32_t split_row_par(int32_t n, int32_t j, int32_t off, int32_t* rsOut, int32_t* gapOut = nullptr) {
+    MT_HD int32_t split_row_par(int32_t n, int32_t j, int32_t off, int32_t* rsOut, int32_t* gapOut = nullptr,
+                                const HotRow* pre = nullptr, int32_t preC = -1) {
         constexpr int CW = (int)(sizeof(typename HT::Cold) / 4);
         static_assert(W::N >= CW && W::N >= MAXN, "a lane per cold dword and per slot");
         const int32_t l = w.lane();
         int32_t s0 = n * MAXN + j;
-        HotRow rr = load_row(n * MAXN + (l & (MAXN - 1)));
-        int32_t c = nch[n];
+        HotRow rr = pre ? *pre : load_row(n * MAXN + (l & (MAXN - 1)));
+        int32_t c = pre ? preC : nch[n];
         int32_t nfr = zh->nfreeRid;
         int32_t frr = d.frid()[nfr > 0 ? nfr - 1 : 0];
         uint32_t fl0 = (uint32_t)w.bcast((int32_t)rr.flags, j);
@@ -2616,12 +2643,14 @@ struct Replica {
     }
     /* Split the row at lorder coordinate t at offset off (0 < off < len). Returns the slot of
      * the LEFT part afterwards (the right part is the next row in document order). */
-    MT_HD int32_t split_row(int32_t t, int32_t off, int32_t* rsOut = nullptr, int32_t* gapOut = nullptr) {
+    /* pre / preC (GPU): the leaf's rows (lane l: child l & 7) and child count as a search just read them */
+    MT_HD int32_t split_row(int32_t t, int32_t off, int32_t* rsOut = nullptr, int32_t* gapOut = nullptr,
+                            const HotRow* pre = nullptr, int32_t preC = -1) {
         MT_PROF_SCOPE(PH_SPLIT);
         int32_t n = leaf_at(t >> 3), j = t & 7;
         int32_t s0 = n * MAXN + j;
         if constexpr (W::N >= 64) {
-            if (!dl_on() && !refs_on()) return split_row_par(n, j, off, rsOut, gapOut);
+            if (!dl_on() && !refs_on()) return split_row_par(n, j, off, rsOut, gapOut, pre, preC);
         }
         if (z.flags(s0) & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
         bool willSplit = nch[n] + 1 >= MAXN;
@@ -3433,7 +3462,7 @@ struct Replica {
         uint64_t vmask = w.ballot(valid);
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
         uint64_t _t1 = __builtin_amdgcn_s_memtime();
-        prof[PH_S1] += _t1 - _t0;
+        if (prof) prof[PH_S1] += _t1 - _t0;
 #endif
         /* Only a candidate whose predecessor in the same leaf is a candidate can be appended; every
          * other row is decided by its own code: held rows (1) are kept, unlinked rows (2) are
@@ -3574,7 +3603,7 @@ struct Replica {
 #endif
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
         uint64_t _t2 = __builtin_amdgcn_s_memtime();
-        prof[PH_S2] += _t2 - _t1;
+        if (prof) prof[PH_S2] += _t2 - _t1;
 #endif
         /* frees: every valid row not kept (unlinked or appended) */
         uint64_t drop = vmask & ~keep;
@@ -3636,7 +3665,7 @@ struct Replica {
         for (int32_t i = 0; i < MAXN; i++) /* constant indices: the caller's array stays in registers */
             if (i < nl) cnt[i] = __builtin_popcountll(keep & (0xFFull << (8 * i)));
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
-        prof[PH_S3] += __builtin_amdgcn_s_memtime() - _t2;
+        if (prof) prof[PH_S3] += __builtin_amdgcn_s_memtime() - _t2;
 #endif
     }
     /* scourNode of one leaf: the parallel form on the GPU, the serial walk on the host */
@@ -4066,11 +4095,15 @@ struct Replica {
             j = 0;
         } else {
             int32_t P, s, v;
-            int32_t t = find_reach(pos, refSeq, client, &P, &s, &v);
+            HotRow lr;
+            int32_t lc = -1; /* the found leaf's rows and child count (tiled GPU search): the split reuses them */
+            constexpr bool PRE = TILED && W::N >= 64;
+            int32_t t = find_reach(pos, refSeq, client, &P, &s, &v, PRE ? &lr : nullptr, PRE ? &lc : nullptr);
             if (t < 0) return -1;
-            if (P + v > pos && !(z.flags(s) & RF_MARKER)) {
+            int32_t fls = PRE && lc >= 0 ? w.bcast((int32_t)lr.flags, s & (MAXN - 1)) : z.flags(s);
+            if (P + v > pos && !(fls & RF_MARKER)) {
                 int32_t rs = -1, gap = -1;
-                int32_t ls = split_row(t, pos - P, &rs, &gap);
+                int32_t ls = split_row(t, pos - P, &rs, &gap, PRE && lc >= 0 ? &lr : nullptr, PRE ? lc : -1);
                 if (ls < 0) return -1;
                 /* the right part (visible: the row was) starts the run at pos and captures the insert, which goes
                  * right before it when no leaf boundary falls between the halves (Appendix C); no row read, and on
@@ -4389,6 +4422,8 @@ struct Replica {
     template <class F>
     MT_HD void range_op_tiled(int32_t start, int32_t end, int32_t refSeq, int32_t client, F& leaf, bool dl) {
         int32_t tf, Pf, tg, Pg, sf = -1, vf = 0, sg = -1, vg = 0;
+        HotRow fr;
+        int32_t fc = -1; /* the first row's leaf as the search read it (lanes 0-7), for its split */
         if (tiles_cover(refSeq, client)) {
             int32_t total = win_pass(refSeq, client);
             int32_t nc = z.tl.nchunk;
@@ -4420,7 +4455,7 @@ struct Replica {
 #if MT_FIND2
             if constexpr (W::N >= 64) {
                 leaf_find2(k1, n1, P1, start + 1, k2, n2, P2, last, refSeq, client, &tf, &Pf, &sf, &vf, &tg, &Pg, &sg,
-                           &vg);
+                           &vg, &fr, &fc);
             } else
 #endif
             {
@@ -4448,7 +4483,7 @@ struct Replica {
         int32_t sl = sg; /* the last row's slot, while nothing has moved it */
         if (Pf < start) {
             int32_t rs = -1;
-            if (split_row(tf, start - Pf, &rs) < 0 || rs < 0) return;
+            if (split_row(tf, start - Pf, &rs, nullptr, fc >= 0 ? &fr : nullptr, fc) < 0 || rs < 0) return;
             sl = -1;
             if (tf == tg) {
                 ridLast = z.rid[rs];

@@ -160,6 +160,14 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
     const int64_t d = aux_doc(aux);
     uint64_t* prof = aux.prof;
     (void)prof;
+#ifdef MT_PROF
+    __shared__ uint64_t sprof[PH_N]; /* the replica's phase clocks (LDS, not registers) */
+    for (int i = threadIdx.x; i < PH_N; i += WG) sprof[i] = 0;
+    __syncthreads();
+#define MT_PROF_ATTACH(r) (r).prof = sprof
+#else
+#define MT_PROF_ATTACH(r) (void)0
+#endif
     Pools p;
     p.ops = ops + op_off[d];
     p.nops = op_off[d + 1] - op_off[d];
@@ -175,6 +183,7 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
         __syncthreads();
         v.t = &hot;
         Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
+        MT_PROF_ATTACH(r);
         r.replay(p);
         r.commit();
 #ifdef MT_PROF
@@ -188,6 +197,7 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
         skel_lite_move(sk, *v.t, true);
         __syncthreads();
         Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
+        MT_PROF_ATTACH(r);
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild;
         r.zh = &sk.zh;
         r.replay(p);
@@ -204,6 +214,7 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
         skel_move(sk, *v.t, true);
         __syncthreads();
         Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
+        MT_PROF_ATTACH(r);
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild, r.nlev = sk.nlevel;
         r.nsc = sk.nscour, r.hsq = sk.hseq, r.hrd = sk.hrid, r.hgn = sk.hgen;
         r.zh = &sk.zh, r.l2s = sk.l2s, r.s2l = sk.s2l;
@@ -217,6 +228,7 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
 #endif
     } else {
         Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
+        MT_PROF_ATTACH(r);
         r.replay(p);
         r.commit();
 #ifdef MT_PROF
@@ -350,6 +362,10 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     __shared__ typename HT::IX lhrid[HL];
     __shared__ uint8_t lhgen[HL];
     __shared__ int32_t pfcur, pfdone, pfsink; /* the replaying wave's record, its end, the helpers' sink */
+#ifdef MT_PROF
+    __shared__ uint64_t sprof[PH_N];
+    for (int i = threadIdx.x; i < PH_N; i += blockDim.x) sprof[i] = 0;
+#endif
     if ((int64_t)blockIdx.x >= ndocs) return;
     const int64_t d = aux_doc(aux);
     uint64_t* prof = aux.prof;
@@ -397,6 +413,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         if (threadIdx.x == 0) *(volatile int32_t*)&pfdone = 1;
     } else {
         R r(v, WaveGPU());
+        MT_PROF_ATTACH(r);
         r.cdel = cdel;
         r.wcp = wcp;
         r.wvs = wvs;
