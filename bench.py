@@ -135,8 +135,11 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--digests-out", default="", help="save the per-document digests (.npy) after the run")
     ap.add_argument("--doc-times-out", default="", help="save each document's replay start / end (.npy, 100 MHz ticks)")
-    ap.add_argument("--order", choices=("cost", "doc"), default="doc",
-                    help="replay dispatch order: document order (doc, default: the configs' documents are uniform and r05b measured cost order 3 %% slower on config 3) or longest-first by shard.doc_costs (cost)")
+    ap.add_argument("--order", choices=("cost", "doc", "measured"), default="doc",
+                    help="replay dispatch order: document order (doc, default: the configs' documents are uniform and "
+                         "r05b measured cost order 3 %% slower on config 3), longest-first by shard.doc_costs (cost), or "
+                         "longest-first by the replay times the warm-up steps measured (measured; one more untimed step "
+                         "runs in that order before timing)")
     ap.add_argument("--assign", choices=("uniform", "cost"), default="uniform",
                     help="strong scaling: bin-pack the node's documents on their message count (uniform: every "
                          "config draws the same number per document, no generation beyond the rank's share) or on "
@@ -224,6 +227,10 @@ def main() -> None:
 
     for _ in range(args.warmup):
         log(f"warmup step: {step():.1f} ms")
+    if args.order == "measured":  # list scheduling on the measured per-document replay times
+        tt = eng.doc_times().astype(np.float64)
+        eng.set_order(np.lexsort((np.arange(batch.ndocs), -(tt[:, 1] - tt[:, 0]))).astype(np.int32))
+        log(f"reordered step: {step():.1f} ms")
     # documents that outgrow the profile are re-replayed in a larger one inside mt_engine_sync (capacity
     # promotion, include/mt_engine.h); any document still in error is reported, not a reason to stop
     err, err_op = eng.errors()
