@@ -217,6 +217,8 @@ struct TileState<N, true> {
     uint8_t xf[N * 8];      /* slot -> XF_* state of the row it holds */
     int32_t cord[NCH];      /* chunk ids in document order */
     int32_t cst[NCH];       /* sum of lst over the chunk at each position */
+    static constexpr int NG = NCH / 64; /* chunk groups: positions [64 g, 64 g + 64) */
+    int32_t gst[NG];        /* sum of cst over each group (a chunk search scans the groups, then one group) */
     int32_t cpos[NCH];      /* chunk id -> position (free chunks: next free id) */
     int32_t ccnt[NCH];      /* chunk id -> leaf count */
     int32_t cleaf[NCH][CH]; /* chunk id -> its leaves in order */
@@ -226,6 +228,7 @@ struct TileState<N, true> {
     int32_t wslot[WCAP];    /* the slot each was last seen in (a hint: rows move; checked before use) */
     /* host-build scratch of a position search (the GPU kernel uses LDS instead) */
     int32_t sdel[NCH];
+    int32_t sgdel[NG];
     int32_t swcp[WCAP], swvs[WCAP];
     uint8_t swlx[WCAP];
 };
@@ -470,6 +473,8 @@ struct Replica {
      * reads them: ~3 dependent vector-memory round trips per search fewer) */
     int32_t* tcord;
     int32_t* tcst;
+    int32_t* tgst; /* chunk-group sums of tcst (TileState::gst) */
+    int32_t* gdel; /* chunk-group sums of cdel */
     int32_t* tcpos;
     int32_t* tccnt;
     int32_t* twrid;
@@ -482,12 +487,16 @@ struct Replica {
     int32_t hmax = INT32_MAX;
     int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
     bool runOnly = false;      /* range_op_tiled: find and split only, leaving the run's first / last slot in */
+    /* tiled GPU insert: the free row ids insert_segments read ahead (raRid), their generations and the found leaf's
+     * nscour (raLeaf / raSc), which insert_row reads with the split's round trip so the row set-up has them */
+    int32_t raRid[2] = {0, 0}, raGen[2] = {-1, -1}, raLeaf = -1, raSc = 0;
+    bool raOn = false;
     int32_t runA = -1, runB = -1; /* runA / runB for remove_run (no visit) */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
         : d(doc), z(*doc.t), w(wave), zh(&z.h), l2s(z.l2s), s2l(z.s2l), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
           nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen), cdel(nullptr), wcp(nullptr), wvs(nullptr),
-          wlx(nullptr), tcord(nullptr), tcst(nullptr), tcpos(nullptr), tccnt(nullptr), twrid(nullptr), twgen(nullptr), twslot(nullptr),
+          wlx(nullptr), tcord(nullptr), tcst(nullptr), tgst(nullptr), gdel(nullptr), tcpos(nullptr), tccnt(nullptr), twrid(nullptr), twgen(nullptr), twslot(nullptr),
           cur(0) {
         if constexpr (TILED) {
             cdel = z.tl.sdel;
@@ -496,6 +505,8 @@ struct Replica {
             wlx = z.tl.swlx;
             tcord = z.tl.cord;
             tcst = z.tl.cst;
+            tgst = z.tl.gst;
+            gdel = z.tl.sgdel;
             tcpos = z.tl.cpos;
             tccnt = z.tl.ccnt;
             twrid = z.tl.wrid;
@@ -1400,6 +1411,13 @@ struct Replica {
             }
         }
         w.sync();
+        for (int32_t b = 0; b < HT::TL::NG; b += W::N) {
+            int32_t g = b + w.lane();
+            if (g < HT::TL::NG) {
+                tgst[g] = 0;
+                t.sgdel[g] = 0;
+            }
+        }
         t.nchunk = 1;
         tcord[0] = 0;
         tcpos[0] = 0;
@@ -1432,6 +1450,31 @@ struct Replica {
         tcpos[c] = t.cfree;
         t.cfree = c;
         t.nfreeChunk++;
+    }
+    /* a chunk summary changes by d: its group's sum with it */
+    MT_HD void cst_add(int32_t p, int32_t d) {
+        tcst[p] += d;
+        tgst[p >> 6] += d;
+    }
+    /* the group sums from position p's group on, after chunk positions moved (a chunk split or freed: rare) */
+    MT_HD void gst_rebuild(int32_t p) {
+        int32_t nc = z.tl.nchunk;
+        for (int32_t g = p >> 6; g < HT::TL::NG; g++) {
+            int32_t v = 0;
+            for (int32_t b = 0; b < 64; b += W::N) {
+                int32_t i = 64 * g + b + w.lane();
+                v += w.sum(i < nc && b + w.lane() < 64 ? tcst[i] : 0);
+            }
+            w.sync();
+            tgst[g] = v;
+            w.sync();
+            if (64 * g + 64 >= nc) { /* the groups past the last chunk are empty */
+                for (int32_t b = g + 1; b < HT::TL::NG; b += W::N)
+                    if (b + w.lane() < HT::TL::NG) tgst[b + w.lane()] = 0;
+                w.sync();
+                break;
+            }
+        }
     }
     /* move chunk positions [from, nchunk) by delta (+1 / -1) with their summaries; fix cpos */
     MT_HD void cord_shift(int32_t from, int32_t delta) {
@@ -1511,6 +1554,7 @@ struct Replica {
             tccnt[c] = HALF;
             tcst[p + 1] = moved;
             tcst[p] -= moved;
+            gst_rebuild(p); /* positions after p moved one up */
             if (i >= HALF) {
                 c = c2;
                 i -= HALF;
@@ -1524,7 +1568,7 @@ struct Replica {
         t.lch[b] = c;
         t.lix[b] = (uint8_t)i;
         tccnt[c] = cnt + 1;
-        tcst[tcpos[c]] += lb;
+        cst_add(tcpos[c], lb);
         w.sync();
     }
     /* leaf b leaves the document order (its STABLE length leaves its chunk's summary) */
@@ -1532,7 +1576,7 @@ struct Replica {
         MT_PROF_SCOPE(PH_ROPE);
         auto& t = z.tl;
         int32_t c = t.lch[b], i = t.lix[b], p = tcpos[c];
-        tcst[p] -= t.lst[b];
+        cst_add(p, -t.lst[b]);
         t.lst[b] = 0;
         int32_t cnt = tccnt[c];
         chunk_shift(c, i + 1, cnt, -1);
@@ -1541,6 +1585,7 @@ struct Replica {
             cord_shift(p + 1, -1);
             t.nchunk--;
             chunk_free(c);
+            gst_rebuild(p); /* positions after p moved one down */
         }
         w.sync();
     }
@@ -1549,7 +1594,7 @@ struct Replica {
         int32_t c = t.lch[n];
         t.lst[n] += d;
         t.cls[c][t.lix[n]] += d;
-        tcst[tcpos[c]] += d;
+        cst_add(tcpos[c], d);
     }
     /* recompute leaf n's STABLE length from its rows */
     MT_HD void leaf_restat(int32_t n) {
@@ -1590,7 +1635,7 @@ struct Replica {
             }
             for (int32_t k = 0; k < cnt; k++) {
                 int32_t dk = w.bcast(x - old, MAXN * k);
-                if (dk) tcst[tcpos[w.bcast(ch, MAXN * k)]] += dk;
+                if (dk) cst_add(tcpos[w.bcast(ch, MAXN * k)], dk);
             }
             w.sync();
         } else {
@@ -1749,7 +1794,7 @@ struct Replica {
                         int32_t dl = w.bcast(rv[q].len, l), lcl = w.bcast(lc[q], l);
                         t.lst[ss / MAXN] += dl;
                         t.cls[lcl][w.bcast(lx[q], l)] += dl;
-                        tcst[tcpos[lcl]] += dl;
+                        cst_add(tcpos[lcl], dl);
                     } else {
                         t.xf[ss] = 0;
                     }
@@ -1765,7 +1810,10 @@ struct Replica {
                     wcp[o] = cp[q];
                     wlx[o] = (uint8_t)lx[q];
                     wvs[o] = v[q];
-                    if (v[q]) W::atomic_add(&cdel[cp[q]], v[q]);
+                    if (v[q]) {
+                        W::atomic_add(&cdel[cp[q]], v[q]);
+                        W::atomic_add(&gdel[cp[q] >> 6], v[q]);
+                    }
                 }
                 w.sync();
                 wpos += tot;
@@ -1780,9 +1828,79 @@ struct Replica {
         int32_t n = z.tl.wN;
         for (int32_t b = 0; b < n; b += W::N) {
             int32_t i = b + w.lane();
-            if (i < n) cdel[wcp[i]] = 0;
+            if (i < n) {
+                cdel[wcp[i]] = 0;
+                gdel[wcp[i] >> 6] = 0;
+            }
         }
         w.sync();
+    }
+    /* The chunk position holding position pos (the first with P < pos <= P + its total, window deltas included)
+     * and the total before it: on the GPU the group sums first, then that group's chunks (two LDS passes, not
+     * one per 256 chunks); on the host the chunk scan. -1 if pos is beyond the length. */
+    MT_HD int32_t chunk_find(int32_t pos, int32_t* runOut) {
+        int32_t nc = z.tl.nchunk;
+        if constexpr (W::N >= 64) {
+            static_assert(HT::TL::NG <= W::N, "one pass over the groups");
+            int32_t ng = (nc + 63) >> 6, l = w.lane();
+            int32_t v = l < ng ? tgst[l] + gdel[l] : 0;
+            int32_t tot;
+            int32_t p = w.excl_scan(v, &tot);
+            uint64_t m = w.ballot(l < ng && p < pos && pos <= p + v);
+            if (!m) return -1;
+            int32_t g = W::ffs(m);
+            int32_t run = w.bcast(p, g);
+            int32_t i = 64 * g + l;
+            int32_t x = i < nc ? tcst[i] + cdel[i] : 0;
+            int32_t q = run + w.excl_scan(x, &tot);
+            m = w.ballot(i < nc && q < pos && pos <= q + x);
+            if (!m) {
+                fail(E_ASSERT); /* a group's chunks must add up to its sum */
+                return -1;
+            }
+            int32_t c = W::ffs(m);
+            *runOut = w.bcast(q, c);
+            return 64 * g + c;
+        } else {
+            int32_t run = 0;
+            for (int32_t b = 0; b < nc; b += 4 * W::N) {
+                int32_t p0 = b + 4 * w.lane();
+                int32_t v[4];
+                for (int q = 0; q < 4; q++) v[q] = p0 + q < nc ? tcst[p0 + q] + cdel[p0 + q] : 0;
+                int32_t tot;
+                int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
+                int32_t hq = -1, hp = 0;
+                for (int q = 0; q < 4; q++) {
+                    if (hq < 0 && p < pos && pos <= p + v[q]) {
+                        hq = q;
+                        hp = p;
+                    }
+                    p += v[q];
+                }
+                uint64_t m = w.ballot(hq >= 0);
+                if (m) {
+                    int32_t l = W::ffs(m);
+                    *runOut = w.bcast(hp, l);
+                    return b + 4 * l + w.bcast(hq, l);
+                }
+                run += tot;
+            }
+            return -1;
+        }
+    }
+    /* the sum of every chunk's STABLE total (the group sums; on the host checked against the chunks) */
+    MT_HD int32_t stable_total() {
+        int32_t total = 0;
+        for (int32_t b = 0; b < HT::TL::NG; b += W::N) {
+            int32_t g = b + w.lane();
+            total += w.sum(g < HT::TL::NG ? tgst[g] : 0);
+        }
+#ifndef __HIP_DEVICE_COMPILE__
+        int32_t chk = 0;
+        for (int32_t p = 0; p < z.tl.nchunk; p++) chk += tcst[p];
+        if (chk != total) fail(E_ASSERT);
+#endif
+        return total;
     }
     /* Leaf position k and start offset P of the leaf holding the first row with
      * P < pos <= P + vis, from the chunk and leaf summaries plus the window scratch of the last
@@ -1790,31 +1908,8 @@ struct Replica {
     MT_HD int32_t tile_find(int32_t pos, int32_t refSeq, int32_t client, int32_t* Pout, int32_t* Nout) {
         MT_PROF_SCOPE(PH_TFIND);
         auto& t = z.tl;
-        int32_t nc = t.nchunk;
-        int32_t run = 0, cpf = -1;
-        for (int32_t b = 0; b < nc; b += 4 * W::N) {
-            int32_t p0 = b + 4 * w.lane();
-            int32_t v[4];
-            for (int q = 0; q < 4; q++) v[q] = p0 + q < nc ? tcst[p0 + q] + cdel[p0 + q] : 0;
-            int32_t tot;
-            int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
-            int32_t hq = -1, hp = 0;
-            for (int q = 0; q < 4; q++) {
-                if (hq < 0 && p < pos && pos <= p + v[q]) {
-                    hq = q;
-                    hp = p;
-                }
-                p += v[q];
-            }
-            uint64_t m = w.ballot(hq >= 0);
-            if (m) {
-                int32_t l = W::ffs(m);
-                run = w.bcast(hp, l);
-                cpf = b + 4 * l + w.bcast(hq, l);
-                break;
-            }
-            run += tot;
-        }
+        int32_t run = 0;
+        int32_t cpf = chunk_find(pos, &run);
         if (cpf < 0) return -1;
         /* leaves of the chunk: STABLE lengths + the window rows that sit in them */
         int32_t c = tcord[cpf], cnt = tccnt[c];
@@ -1856,49 +1951,17 @@ struct Replica {
         fail(E_ASSERT); /* the chunk's leaves must add up to its summary */
         return -1;
     }
-    /* tile_find of two positions pa <= pb in the same passes (a range op's first and last rows): one chunk scan
-     * finds both chunks, and both chunks' leaf-summary lines are read in one round trip. Same answers as two
-     * tile_find calls. */
+    /* tile_find of two positions pa <= pb (a range op's first and last rows): both chunks' leaf-summary lines are
+     * read in one round trip. Same answers as two tile_find calls. */
     MT_HD void tile_find2(int32_t pa, int32_t pb, int32_t* ka, int32_t* Pa, int32_t* Na, int32_t* kb, int32_t* Pb,
                           int32_t* Nb) {
         MT_PROF_SCOPE(PH_TFIND);
         static_assert(W::N >= HT::TL::CH, "a lane per leaf of a chunk");
         auto& t = z.tl;
-        int32_t nc = t.nchunk;
-        int32_t run = 0, ra = 0, rb = 0, cpa = -1, cpb = -1;
+        int32_t ra = 0, rb = 0;
         *ka = *kb = -1;
-        for (int32_t b = 0; b < nc && cpb < 0; b += 4 * W::N) {
-            int32_t p0 = b + 4 * w.lane();
-            int32_t v[4];
-            for (int q = 0; q < 4; q++) v[q] = p0 + q < nc ? tcst[p0 + q] + cdel[p0 + q] : 0;
-            int32_t tot;
-            int32_t p = run + w.excl_scan(v[0] + v[1] + v[2] + v[3], &tot);
-            int32_t ha = -1, hpa = 0, hb = -1, hpb = 0;
-            for (int q = 0; q < 4; q++) {
-                if (ha < 0 && p < pa && pa <= p + v[q]) {
-                    ha = q;
-                    hpa = p;
-                }
-                if (hb < 0 && p < pb && pb <= p + v[q]) {
-                    hb = q;
-                    hpb = p;
-                }
-                p += v[q];
-            }
-            uint64_t m = w.ballot(ha >= 0);
-            if (cpa < 0 && m) {
-                int32_t l = W::ffs(m);
-                ra = w.bcast(hpa, l);
-                cpa = b + 4 * l + w.bcast(ha, l);
-            }
-            m = w.ballot(hb >= 0);
-            if (m) {
-                int32_t l = W::ffs(m);
-                rb = w.bcast(hpb, l);
-                cpb = b + 4 * l + w.bcast(hb, l);
-            }
-            run += tot;
-        }
+        int32_t cpa = chunk_find(pa, &ra);
+        int32_t cpb = chunk_find(pb, &rb);
         if (cpa < 0 || cpb < 0) return;
         int32_t ca = tcord[cpa], cb = tcord[cpb], na = tccnt[ca], nb = tccnt[cb];
         int32_t nw = t.wN;
@@ -2003,7 +2066,11 @@ struct Replica {
             int32_t j = w.lane();
             int32_t s = n * MAXN + (j & (MAXN - 1));
             RowView r;
-            if (rowsOut) { /* the whole row in the same pass */
+            if (rowsOut) { /* the whole row in the same pass (and the leaf's nscour, for the insert's LRU entry) */
+                if (raOn) {
+                    raLeaf = n;
+                    raSc = nsc[n];
+                }
                 HotRow hr = load_row(s);
                 r = RowView{hr.len, hr.seq, hr.rseq,
                             (uint32_t)hr.cli | ((uint32_t)hr.rcli << 8) | ((uint32_t)hr.flags << 16) | ((uint32_t)hr.ng << 24)};
@@ -2087,12 +2154,7 @@ struct Replica {
         }
         int32_t total = win_pass(refSeq, client);
         win_clear();
-        int32_t nc = z.tl.nchunk;
-        for (int32_t b = 0; b < nc; b += W::N) {
-            int32_t p = b + w.lane();
-            total += w.sum(p < nc ? tcst[p] : 0);
-        }
-        return total;
+        return total + stable_total();
     }
 
     /* ---- perspective scans ------------------------------------------------------------- */
@@ -2586,6 +2648,12 @@ struct Replica {
             nch[n] = (int8_t)(c + 1 + g);
         }
         int32_t rs = n * MAXN + j + 1 + g;
+        if constexpr (TILED) { /* a leaf split re-sums both leaves (split_node): the halves' lengths go first */
+            if (willSplit && (xf0 & XF_STABLE)) {
+                z.len(s0) = off < len0 ? off : len0;
+                z.len(rs) = off < len0 ? len0 - off : 0;
+            }
+        }
         if (willSplit) {
             MT_PROF_SCOPE(PH_LEAFINS);
             int32_t nn = split_node(n);
@@ -2632,10 +2700,8 @@ struct Replica {
         zh->sumW += 2;
         if constexpr (TILED) {
             if (xf0 & XF_W) win_add(rrid, rs);
-            if (xf0 & XF_STABLE) { /* the halves may sit in two leaves after a leaf split */
-                int32_t two[2] = {ls / MAXN, rs / MAXN};
-                leaves_restat(two, rs / MAXN != ls / MAXN ? 2 : 1);
-            }
+            /* STABLE halves: in one leaf, its sum is unchanged; after a leaf split, split_node re-summed both
+             * leaves with the halves' lengths written above */
         }
         if (ng0) split_groups(rid0, rrid, (int32_t)ng0); /* segmentGroups.copyTo */
         if (rsOut) *rsOut = rs;
@@ -4098,8 +4164,13 @@ struct Replica {
             HotRow lr;
             int32_t lc = -1; /* the found leaf's rows and child count (tiled GPU search): the split reuses them */
             constexpr bool PRE = TILED && W::N >= 64;
+            if (PRE && raOn) raLeaf = -1;
             int32_t t = find_reach(pos, refSeq, client, &P, &s, &v, PRE ? &lr : nullptr, PRE ? &lc : nullptr);
             if (t < 0) return -1;
+            if (PRE && raOn) { /* the read-ahead row ids' generations: with the split's reads, for the row set-up */
+                raGen[0] = z.rgen[raRid[0]];
+                raGen[1] = z.rgen[raRid[1]];
+            }
             int32_t fls = PRE && lc >= 0 ? w.bcast((int32_t)lr.flags, s & (MAXN - 1)) : z.flags(s);
             if (P + v > pos && !(fls & RF_MARKER)) {
                 int32_t rs = -1, gap = -1;
@@ -4157,8 +4228,10 @@ struct Replica {
              * SIMD the live registers cost more than the round trips: -2.8 %, r04r) */
             constexpr bool RA = TILED && W::N >= 64;
             const bool text = !marker && !perm;
+            /* the stack's top two: a split of the row at pos takes the top for its right part, the new row the next */
             int32_t nfr = RA ? zh->nfreeRid : 0;
             int32_t frr = RA ? (int32_t)d.frid()[nfr > 0 ? nfr - 1 : 0] : 0;
+            int32_t frr2 = RA ? (int32_t)d.frid()[nfr > 1 ? nfr - 2 : 0] : 0;
             const bool tpreOk = RA && text && L <= W::N;
             int32_t tpre = tpreOk && w.lane() < L ? p.text[op.text_off + w.lane()] : 0;
             int32_t off = 0;
@@ -4168,7 +4241,15 @@ struct Replica {
                 if (off < 0) return;
             }
             /* atT >= 0: right before the row at document coordinate atT (insertAtReferencePosition) */
+            if constexpr (RA) {
+                raRid[0] = frr;
+                raRid[1] = frr2;
+                raGen[0] = raGen[1] = -1;
+                raLeaf = -1;
+                raOn = atT < 0 && pos > 0;
+            }
             int32_t s = atT >= 0 ? leaf_insert_slot(leaf_at(atT >> 3), atT & (MAXN - 1)) : insert_row(pos, refSeq, client, seq);
+            if constexpr (RA) raOn = false;
             if (s < 0) {
                 fail(E_INSERT_FAILED);
                 return;
@@ -4178,13 +4259,23 @@ struct Replica {
             if (RA && zh->nfreeRid == nfr && nfr > 0) { /* alloc_rid, with the stack's top read above */
                 zh->nfreeRid = nfr - 1;
                 rid = frr;
+            } else if (RA && zh->nfreeRid == nfr - 1 && nfr > 1) { /* a split took the top */
+                zh->nfreeRid = nfr - 2;
+                rid = frr2;
             } else {
                 rid = alloc_rid();
             }
             int32_t gen = 0, sc = 0;
-            if (RA) { /* for the window set and the LRU entry: one round trip */
-                gen = z.rgen[rid];
-                sc = nsc[s / MAXN];
+            if (RA) { /* for the window set and the LRU entry: one round trip, unless insert_row read them */
+                bool g0 = rid == frr && raGen[0] >= 0, g1 = rid == frr2 && raGen[1] >= 0;
+                bool scOk = raLeaf >= 0 && raLeaf == s / MAXN;
+                if (g0 || g1) {
+                    gen = g0 ? raGen[0] : raGen[1];
+                    sc = scOk ? raSc : nsc[s / MAXN];
+                } else {
+                    gen = z.rgen[rid];
+                    sc = scOk ? raSc : nsc[s / MAXN];
+                }
             }
             z.rid[s] = (IX)rid;
             typename HT::Cold& c = d.cold()[rid]; /* row id kept in a register, not re-read per field */
@@ -4425,12 +4516,7 @@ struct Replica {
         HotRow fr;
         int32_t fc = -1; /* the first row's leaf as the search read it (lanes 0-7), for its split */
         if (tiles_cover(refSeq, client)) {
-            int32_t total = win_pass(refSeq, client);
-            int32_t nc = z.tl.nchunk;
-            for (int32_t b = 0; b < nc; b += W::N) {
-                int32_t p = b + w.lane();
-                total += w.sum(p < nc ? tcst[p] : 0);
-            }
+            int32_t total = win_pass(refSeq, client) + stable_total();
             if (start >= total || end <= start) {
                 win_clear();
                 return;

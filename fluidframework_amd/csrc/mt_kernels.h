@@ -355,7 +355,9 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     __shared__ uint8_t wlx[WCAP];
     __shared__ DocHdr zhs; /* the image's header fields, staged for the replay */
     /* the rope's chunk arrays and the window set, staged for the replay (written back at the end) */
+    constexpr int NG = HT::TL::NG;
     __shared__ int32_t lcord[NCH], lcst[NCH], lcpos[NCH], lccnt[NCH], lwrid[WCAP];
+    __shared__ int32_t lgst[NG], lgdel[NG]; /* chunk-group sums of lcst and of cdel */
     __shared__ __attribute__((aligned(16))) uint8_t lwgen[WCAP];
     __shared__ int32_t lwslot[WCAP];
     __shared__ int32_t lhseq[HL]; /* NARROW: the zamboni heap */
@@ -379,6 +381,8 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     const int32_t nheap = NARROW ? v.t->h.heapN : 0;
     if (replayer && fits) {
         for (int i = threadIdx.x; i < NCH; i += WG) cdel[i] = 0;
+        for (int i = threadIdx.x; i < NG; i += WG) lgdel[i] = 0;
+        wave_copy(lgst, tl.gst, NG);
         wave_copy((int32_t*)&zhs, (const int32_t*)&v.t->h, (int)(sizeof(DocHdr) / 4));
         wave_copy(lcord, tl.cord, NCH);
         wave_copy(lcst, tl.cst, NCH);
@@ -421,6 +425,8 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         r.zh = &zhs;
         r.tcord = lcord;
         r.tcst = lcst;
+        r.tgst = lgst;
+        r.gdel = lgdel;
         r.tcpos = lcpos;
         r.tccnt = lccnt;
         r.twrid = lwrid;
@@ -445,6 +451,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         wave_copy((int32_t*)&v.t->h, (const int32_t*)&zhs, (int)(sizeof(DocHdr) / 4));
         wave_copy(tl.cord, lcord, NCH);
         wave_copy(tl.cst, lcst, NCH);
+        wave_copy(tl.gst, lgst, NG);
         wave_copy(tl.cpos, lcpos, NCH);
         wave_copy(tl.ccnt, lccnt, NCH);
         wave_copy(tl.wrid, lwrid, WCAP);
