@@ -215,6 +215,8 @@ struct TileState<N, true> {
     int32_t lch[N];         /* leaf node -> chunk id */
     uint8_t lix[N];         /* leaf node -> index in its chunk */
     uint8_t xf[N * 8];      /* slot -> XF_* state of the row it holds */
+    uint16_t ph[N * 8];     /* slot -> a 16-bit hash of its row's property values (RF_PROPS rows; moves with the row):
+                               scour's append test reads the cold values only where the hashes match */
     int32_t cord[NCH];      /* chunk ids in document order */
     int32_t cst[NCH];       /* sum of lst over the chunk at each position */
     static constexpr int NG = NCH / 64; /* chunk groups: positions [64 g, 64 g + 64) */
@@ -1255,7 +1257,10 @@ struct Replica {
     /* copy every column of row a to row b (same doc) */
     /* move row a's slot contents to slot b (hot columns + its cold row id) */
     MT_HD void copy_row(int32_t b, int32_t a) {
-        if constexpr (TILED) z.tl.xf[b] = z.tl.xf[a];
+        if constexpr (TILED) {
+            z.tl.xf[b] = z.tl.xf[a];
+            z.tl.ph[b] = z.tl.ph[a];
+        }
         z.len(b) = z.len(a);
         z.seq(b) = z.seq(a);
         z.rseq(b) = z.rseq(a);
@@ -1275,6 +1280,7 @@ struct Replica {
         IX rid;
         uint8_t cli, rcli, flags, ng;
         uint8_t xf; /* tiled profile: XF_* */
+        uint16_t ph; /* tiled profile: the property hash (TileState::ph) */
     };
     MT_HD HotRow load_row(int32_t a) const {
         HotRow r;
@@ -1288,7 +1294,11 @@ struct Replica {
         r.flags = (uint8_t)(b4 >> 16);
         r.ng = (uint8_t)(b4 >> 24);
         r.xf = 0;
-        if constexpr (TILED) r.xf = z.tl.xf[a];
+        r.ph = 0;
+        if constexpr (TILED) {
+            r.xf = z.tl.xf[a];
+            r.ph = z.tl.ph[a];
+        }
         return r;
     }
     MT_HD void store_row(int32_t b, const HotRow& r) {
@@ -1297,7 +1307,10 @@ struct Replica {
         z.rseq(b) = r.rseq;
         z.rid[b] = r.rid;
         st_bytes4(b, (uint32_t)r.cli | ((uint32_t)r.rcli << 8) | ((uint32_t)r.flags << 16) | ((uint32_t)r.ng << 24));
-        if constexpr (TILED) z.tl.xf[b] = r.xf;
+        if constexpr (TILED) {
+            z.tl.xf[b] = r.xf;
+            z.tl.ph[b] = r.ph;
+        }
     }
     /* shift slab rows [j, c) of leaf n right by one slot (wave-parallel: read all, then write) */
     MT_HD void slab_shift_right(int32_t n, int32_t j, int32_t c) {
@@ -2772,12 +2785,15 @@ struct Replica {
     }
 
     /* ---- segment groups ---------------------------------------------------------------- */
+    /* an index of the pending-group ring in [0, 2 gcap) reduced to [0, gcap): gqHead stays reduced, so no integer
+     * division (tens of instructions on the GPU) */
+    MT_HD int32_t gq_wrap(int32_t x) const { return x >= d.caps.gcap ? x - d.caps.gcap : x; }
     /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39) of a split: the right part (rrid) joins the same
      * pending groups as the left (lrid, in ng of them), in the row's FIFO order = log order, appended at the end
      * of each group's segment list */
     MT_HD void split_groups(int32_t lrid, int32_t rrid, int32_t ng) {
         if (zh->memN + ng > d.caps.mcap) mem_compact();
-        int32_t head = zh->gqN ? d.gq()[zh->gqHead % d.caps.gcap] : 0x7fffffff;
+        int32_t head = zh->gqN ? d.gq()[zh->gqHead] : 0x7fffffff;
         int32_t m0 = zh->memN;
         for (int32_t b = 0; b < m0; b += W::N) {
             int32_t i = b + w.lane();
@@ -2806,7 +2822,7 @@ struct Replica {
     }
     /* drop entries of groups already acked (gid < head gid): wave stream compaction */
     MT_HD void mem_compact() {
-        int32_t head = zh->gqN ? d.gq()[zh->gqHead % d.caps.gcap] : 0x7fffffff;
+        int32_t head = zh->gqN ? d.gq()[zh->gqHead] : 0x7fffffff;
         int32_t n = zh->memN, wpos = 0;
         for (int32_t b = 0; b < n; b += W::N) {
             int32_t i = b + w.lane();
@@ -2847,13 +2863,13 @@ struct Replica {
             group_push(localSeq);
             *created = true;
         }
-        row_enqueue_group(s, d.gq()[(zh->gqHead + zh->gqN - 1) % d.caps.gcap]);
+        row_enqueue_group(s, d.gq()[gq_wrap(zh->gqHead + zh->gqN - 1)]);
     }
     /* pendingSegments.enqueue of a new group (the caller checked the ring's room) */
     MT_HD void group_push(int32_t localSeq) {
         int32_t gid = zh->gidNext;
         zh->gidNext = gid + 1;
-        int32_t q = (zh->gqHead + zh->gqN) % d.caps.gcap;
+        int32_t q = gq_wrap(zh->gqHead + zh->gqN);
         d.gq()[q] = gid;
         d.gql()[q] = localSeq;
         zh->gqN++;
@@ -3226,10 +3242,15 @@ struct Replica {
             }
             zh->nkeys = nk;
         }
+        int32_t hsum = 0;
+        if constexpr (TILED) hsum = w.sum(kl ? prop_mix(kx, pv) : 0); /* TileState::ph */
         w.sync();
         if (kl) {
             c.pv[kx] = (uint16_t)pv;
             c.pk[kx] = (uint8_t)pk;
+        }
+        if constexpr (TILED) {
+            if (l == 0) z.tl.ph[s] = (uint16_t)hsum;
         }
         if (l == 0) c.prw = (uint8_t)prw;
         if (fresh && l == 0) z.flags(s) = (uint8_t)(fl | RF_PROPS);
@@ -3245,14 +3266,30 @@ struct Replica {
         fail(E_UNSUPPORTED);
         return true;
     }
+    /* one key slot's term of the property hash (0 for an absent value): the hash is the sum of the terms */
+    MT_HD static int32_t prop_mix(int32_t k, int32_t v) {
+        return v ? (int32_t)(((uint32_t)v * 0x9E3779B1u + (uint32_t)k * 0x85EBCA77u) >> 16) : 0;
+    }
+    MT_HD void prop_rehash(int32_t s) {
+        if constexpr (TILED) {
+            const typename HT::Cold& c = cold(s);
+            int32_t hsum = 0;
+            for (int32_t k = 0; k < HT::K; k++) hsum += prop_mix(k, c.pv[k]);
+            z.tl.ph[s] = (uint16_t)hsum;
+        }
+    }
     MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collaborating) {
-        const bool rewrite = comb == MT_COMBINE_REWRITE;
         if constexpr (W::N >= 32 && MT_PROPS_PAR) {
             if (nkv <= W::N) {
                 add_props_par(s, kv, nkv, comb, seq, collaborating);
                 return;
             }
         }
+        add_props_serial(s, kv, nkv, comb, seq, collaborating);
+        prop_rehash(s);
+    }
+    MT_HD void add_props_serial(int32_t s, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collaborating) {
+        const bool rewrite = comb == MT_COMBINE_REWRITE;
         typename HT::Cold& c = cold(s); /* the row id is read once, not after every store */
         if (!(z.flags(s) & RF_PROPS)) {
             c.prw = 0;
@@ -3307,6 +3344,7 @@ struct Replica {
         typename HT::Cold& c = cold(s);
         I4 zero = {{0, 0, 0, 0}};
         for (int i = 0; i < HT::K / 8; i++) st4(&c.pv[8 * i], zero);
+        if constexpr (TILED) z.tl.ph[s] = 0;
         for (int i = 0; i < HT::K / 8; i++) {
             uint64_t z8 = 0;
             __builtin_memcpy(__builtin_assume_aligned(&c.pk[8 * i], 8), &z8, 8);
@@ -3547,12 +3585,18 @@ struct Replica {
          * every lane is active */
         int32_t lenP = w.shfl(r.len, q - 1), flP = w.shfl(fl, q - 1);
         int32_t ridP = w.shfl((int32_t)r.rid, q - 1); /* the pair's cold rows by the ids this pass read */
+        int32_t phP = TILED ? w.shfl((int32_t)r.ph, q - 1) : 0;
         if ((pairs >> q) & 1) {
             bool permPair = (flP & fl & RF_PERM) != 0;
             /* localNetLength > 0 on both sides: a zero-length row (the empty right part of a split past a
              * segment's end) is held and leaves no prevSegment (mergeTree.ts:1355-1383) */
             pairOk = lenP > 0 && r.len > 0 && ((flP ^ fl) & RF_PROPS) == 0 &&
                      (permPair || !((flP | fl) & RF_NOTEXT));
+            /* tiled: property hashes that differ decide matchProperties without the cold values */
+            if (TILED && (fl & RF_PROPS) && phP != (int32_t)r.ph) pairOk = false;
+        }
+        if (pairOk) {
+            const bool permPair = (flP & fl & RF_PERM) != 0;
             const typename HT::Cold& ca = d.cold()[ridP];
             const typename HT::Cold& cb = d.cold()[(int32_t)r.rid];
             tofP = (int32_t)ca.toff;
@@ -4913,7 +4957,7 @@ struct Replica {
             fail(E_ASSERT); /* "Segment group not at head of merge tree pending queue" */
             return;
         }
-        int32_t hq = zh->gqHead % d.caps.gcap;
+        int32_t hq = zh->gqHead;
         int32_t g0 = d.gq()[hq], lseq0 = d.gql()[hq];
         int32_t mn = zh->memN, cnt = 0;
         for (int32_t b = 0; b < mn; b += W::N) {
@@ -4927,7 +4971,7 @@ struct Replica {
                 return;
             }
         }
-        zh->gqHead = (zh->gqHead + 1) % d.caps.gcap;
+        zh->gqHead = gq_wrap(zh->gqHead + 1);
         zh->gqN--;
         mn = zh->memN;
         for (int32_t b = 0; b < mn; b += W::N) { /* mark: each member's coordinate (per lane: its leaf's 8 slots) */
@@ -4980,7 +5024,7 @@ struct Replica {
                 break;
             }
             group_push(lseq0); /* { segments: [], localSeq: segmentGroup.localSeq } (client.ts:755-758) */
-            row_enqueue_group(s, d.gq()[(zh->gqHead + zh->gqN - 1) % d.caps.gcap]);
+            row_enqueue_group(s, d.gq()[gq_wrap(zh->gqHead + zh->gqN - 1)]);
             if (dl) {
                 dput(pos);
                 dput(z.len(s));
@@ -5063,8 +5107,8 @@ struct Replica {
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
         if (zh->gqN > 0) {
             MT_PROF_SCOPE(PH_ACK);
-            int32_t gid = d.gq()[zh->gqHead % d.caps.gcap];
-            zh->gqHead = (zh->gqHead + 1) % d.caps.gcap;
+            int32_t gid = d.gq()[zh->gqHead];
+            zh->gqHead = gq_wrap(zh->gqHead + 1);
             zh->gqN--;
             int32_t mn = zh->memN;
             for (int32_t b = 0; b < mn; b += W::N) {
