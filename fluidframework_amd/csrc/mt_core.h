@@ -489,10 +489,6 @@ struct Replica {
     int32_t hmax = INT32_MAX;
     int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
     bool runOnly = false;      /* range_op_tiled: find and split only, leaving the run's first / last slot in */
-    /* tiled GPU insert: the free row ids insert_segments read ahead (raRid), their generations and the found leaf's
-     * nscour (raLeaf / raSc), which insert_row reads with the split's round trip so the row set-up has them */
-    int32_t raRid[2] = {0, 0}, raGen[2] = {-1, -1}, raLeaf = -1, raSc = 0;
-    bool raOn = false;
     int32_t runA = -1, runB = -1; /* runA / runB for remove_run (no visit) */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
@@ -2079,11 +2075,7 @@ struct Replica {
             int32_t j = w.lane();
             int32_t s = n * MAXN + (j & (MAXN - 1));
             RowView r;
-            if (rowsOut) { /* the whole row in the same pass (and the leaf's nscour, for the insert's LRU entry) */
-                if (raOn) {
-                    raLeaf = n;
-                    raSc = nsc[n];
-                }
+            if (rowsOut) { /* the whole row in the same pass */
                 HotRow hr = load_row(s);
                 r = RowView{hr.len, hr.seq, hr.rseq,
                             (uint32_t)hr.cli | ((uint32_t)hr.rcli << 8) | ((uint32_t)hr.flags << 16) | ((uint32_t)hr.ng << 24)};
@@ -4208,13 +4200,8 @@ struct Replica {
             HotRow lr;
             int32_t lc = -1; /* the found leaf's rows and child count (tiled GPU search): the split reuses them */
             constexpr bool PRE = TILED && W::N >= 64;
-            if (PRE && raOn) raLeaf = -1;
             int32_t t = find_reach(pos, refSeq, client, &P, &s, &v, PRE ? &lr : nullptr, PRE ? &lc : nullptr);
             if (t < 0) return -1;
-            if (PRE && raOn) { /* the read-ahead row ids' generations: with the split's reads, for the row set-up */
-                raGen[0] = z.rgen[raRid[0]];
-                raGen[1] = z.rgen[raRid[1]];
-            }
             int32_t fls = PRE && lc >= 0 ? w.bcast((int32_t)lr.flags, s & (MAXN - 1)) : z.flags(s);
             if (P + v > pos && !(fls & RF_MARKER)) {
                 int32_t rs = -1, gap = -1;
@@ -4272,10 +4259,8 @@ struct Replica {
              * SIMD the live registers cost more than the round trips: -2.8 %, r04r) */
             constexpr bool RA = TILED && W::N >= 64;
             const bool text = !marker && !perm;
-            /* the stack's top two: a split of the row at pos takes the top for its right part, the new row the next */
             int32_t nfr = RA ? zh->nfreeRid : 0;
             int32_t frr = RA ? (int32_t)d.frid()[nfr > 0 ? nfr - 1 : 0] : 0;
-            int32_t frr2 = RA ? (int32_t)d.frid()[nfr > 1 ? nfr - 2 : 0] : 0;
             const bool tpreOk = RA && text && L <= W::N;
             int32_t tpre = tpreOk && w.lane() < L ? p.text[op.text_off + w.lane()] : 0;
             int32_t off = 0;
@@ -4285,15 +4270,7 @@ struct Replica {
                 if (off < 0) return;
             }
             /* atT >= 0: right before the row at document coordinate atT (insertAtReferencePosition) */
-            if constexpr (RA) {
-                raRid[0] = frr;
-                raRid[1] = frr2;
-                raGen[0] = raGen[1] = -1;
-                raLeaf = -1;
-                raOn = atT < 0 && pos > 0;
-            }
             int32_t s = atT >= 0 ? leaf_insert_slot(leaf_at(atT >> 3), atT & (MAXN - 1)) : insert_row(pos, refSeq, client, seq);
-            if constexpr (RA) raOn = false;
             if (s < 0) {
                 fail(E_INSERT_FAILED);
                 return;
@@ -4303,23 +4280,13 @@ struct Replica {
             if (RA && zh->nfreeRid == nfr && nfr > 0) { /* alloc_rid, with the stack's top read above */
                 zh->nfreeRid = nfr - 1;
                 rid = frr;
-            } else if (RA && zh->nfreeRid == nfr - 1 && nfr > 1) { /* a split took the top */
-                zh->nfreeRid = nfr - 2;
-                rid = frr2;
             } else {
                 rid = alloc_rid();
             }
             int32_t gen = 0, sc = 0;
-            if (RA) { /* for the window set and the LRU entry: one round trip, unless insert_row read them */
-                bool g0 = rid == frr && raGen[0] >= 0, g1 = rid == frr2 && raGen[1] >= 0;
-                bool scOk = raLeaf >= 0 && raLeaf == s / MAXN;
-                if (g0 || g1) {
-                    gen = g0 ? raGen[0] : raGen[1];
-                    sc = scOk ? raSc : nsc[s / MAXN];
-                } else {
-                    gen = z.rgen[rid];
-                    sc = scOk ? raSc : nsc[s / MAXN];
-                }
+            if (RA) { /* for the window set and the LRU entry: one round trip */
+                gen = z.rgen[rid];
+                sc = nsc[s / MAXN];
             }
             z.rid[s] = (IX)rid;
             typename HT::Cold& c = d.cold()[rid]; /* row id kept in a register, not re-read per field */
