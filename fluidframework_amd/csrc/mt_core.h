@@ -451,6 +451,7 @@ struct Replica {
      * these, so the HBM-resident replay kernel can stage them in LDS with the skeleton (every sequenced
      * message reads l2s and bumps seqOps: no vector-memory round trip for either) */
     DocHdr* zh;
+    uint16_t* keys; /* the document's property key table (z.keys; the tiled replay kernel stages it in LDS) */
     uint8_t* l2s;
     uint16_t* s2l;
     IX* lo;  /* lorder */
@@ -492,7 +493,7 @@ struct Replica {
     int32_t runA = -1, runB = -1; /* runA / runB for remove_run (no visit) */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
-        : d(doc), z(*doc.t), w(wave), zh(&z.h), l2s(z.l2s), s2l(z.s2l), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
+        : d(doc), z(*doc.t), w(wave), zh(&z.h), keys(z.keys), l2s(z.l2s), s2l(z.s2l), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
           nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen), cdel(nullptr), wcp(nullptr), wvs(nullptr),
           wlx(nullptr), tcord(nullptr), tcst(nullptr), tgst(nullptr), gdel(nullptr), tcpos(nullptr), tccnt(nullptr), twrid(nullptr), twgen(nullptr), twslot(nullptr),
           cur(0) {
@@ -1099,7 +1100,7 @@ struct Replica {
         int32_t cv = 0, pd = 0;
         if (has)
             for (int32_t k = 0; k < zh->nkeys; k++)
-                if (z.keys[k] == kid) {
+                if (keys[k] == kid) {
                     cv = cold(s).pv[k];
                     pd = cold(s).pk[k];
                 }
@@ -1131,7 +1132,7 @@ struct Replica {
             for (;;) { /* candidate keys (the doc's key slots and the op's keys) in id order */
                 int32_t best = 0x7fffffff;
                 for (int32_t k = 0; k < zh->nkeys; k++)
-                    if (z.keys[k] > last && z.keys[k] < best) best = z.keys[k];
+                    if (keys[k] > last && keys[k] < best) best = keys[k];
                 for (int32_t j = 0; j < nkv; j++)
                     if (kv[j].key > last && kv[j].key < best) best = kv[j].key;
                 if (best == 0x7fffffff) break;
@@ -3150,12 +3151,12 @@ struct Replica {
     /* ---- properties (segmentPropertiesManager.ts:35-111) ---------------------------- */
     MT_HD int32_t key_slot(uint16_t key) {
         for (int32_t i = 0; i < zh->nkeys; i++)
-            if (z.keys[i] == key) return i;
+            if (keys[i] == key) return i;
         if (zh->nkeys >= HT::K) {
             fail(E_CAPACITY); /* the profile's key slots: a larger profile holds more (capacity promotion) */
             return -1;
         }
-        z.keys[zh->nkeys] = key;
+        keys[zh->nkeys] = key;
         return zh->nkeys++;
     }
 #ifndef MT_PROPS_PAR
@@ -3168,26 +3169,27 @@ struct Replica {
      * the op's j-th key / value; everything is read in one pass, the fold runs on those registers in the
      * reference's order (rewrite deletions, then the op's keys in order, new key slots in first-appearance
      * order), and the row's property state is written back in one pass. Same result as the serial form. */
-    MT_HD void add_props_par(int32_t s, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collaborating) {
+    /* knownFl >= 0: the row's flags as the caller holds them (a row just placed: its cold property state is not read) */
+    MT_HD void add_props_par(int32_t s, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collaborating,
+                             int32_t knownFl = -1) {
         static_assert(HT::K <= W::N, "a lane per key slot");
         const bool rewrite = comb == MT_COMBINE_REWRITE;
         typename HT::Cold& c = cold(s);
         const int32_t l = w.lane();
         const bool kl = l < HT::K;
         const int32_t kx = kl ? l : 0; /* K is 8 or 24: not a mask */
-        uint32_t fl = z.flags(s);
-        int32_t prw = c.prw;
-        int32_t pv = kl ? (int32_t)c.pv[kx] : 0;
-        int32_t pk = kl ? (int32_t)c.pk[kx] : 0;
-        int32_t key = kl ? (int32_t)z.keys[kx] : -1;
+        uint32_t fl = knownFl >= 0 ? (uint32_t)knownFl : (uint32_t)z.flags(s);
+        const bool fresh = !(fl & RF_PROPS);
+        /* propertyManager / properties created: every slot absent, no pending counts */
+        int32_t prw = 0, pv = 0, pk = 0;
+        if (!fresh) {
+            prw = c.prw;
+            pv = kl ? (int32_t)c.pv[kx] : 0;
+            pk = kl ? (int32_t)c.pk[kx] : 0;
+        }
+        int32_t key = kl ? (int32_t)keys[kx] : -1;
         int32_t nk = zh->nkeys;
         int32_t ok = l < nkv ? (int32_t)kv[l].key : -1, ov = l < nkv ? (int32_t)kv[l].value : 0;
-        const bool fresh = !(fl & RF_PROPS);
-        if (fresh) { /* propertyManager / properties created: every slot absent, no pending counts */
-            prw = 0;
-            pv = 0;
-            pk = 0;
-        }
         if (!(prw > 0 && seq != UNASSIGNED_SEQ && collaborating)) {
             if (rewrite) {
                 if (collaborating && seq == UNASSIGNED_SEQ) prw++;
@@ -3212,7 +3214,7 @@ struct Replica {
                     }
                     k = nk++;
                     key = w.writelane(kj, k, key);
-                    if (l == 0) z.keys[k] = (uint16_t)kj;
+                    if (l == 0) keys[k] = (uint16_t)kj;
                 }
                 int32_t pkk = w.bcast(pk, k);
                 if (collaborating) {
@@ -3270,10 +3272,11 @@ struct Replica {
             z.tl.ph[s] = (uint16_t)hsum;
         }
     }
-    MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collaborating) {
+    MT_HD void add_props(int32_t s, const mt_kv* kv, int32_t nkv, int32_t comb, int32_t seq, bool collaborating,
+                         int32_t knownFl = -1) {
         if constexpr (W::N >= 32 && MT_PROPS_PAR) {
             if (nkv <= W::N) {
-                add_props_par(s, kv, nkv, comb, seq, collaborating);
+                add_props_par(s, kv, nkv, comb, seq, collaborating, knownFl);
                 return;
             }
         }
@@ -3295,7 +3298,7 @@ struct Replica {
                 if (c.pv[k] == 0) continue;
                 bool inNew = false;
                 for (int32_t j = 0; j < nkv; j++)
-                    if (kv[j].key == z.keys[k] && kv[j].value != 0 && !(kv[j].value & MT_VALUE_FALSY)) inNew = true;
+                    if (kv[j].key == keys[k] && kv[j].value != 0 && !(kv[j].value & MT_VALUE_FALSY)) inNew = true;
                 bool modify = seq == UNASSIGNED_SEQ || c.pk[k] == 0;
                 if (!inNew && modify) c.pv[k] = 0;
             }
@@ -4261,6 +4264,17 @@ struct Replica {
             const bool text = !marker && !perm;
             int32_t nfr = RA ? zh->nfreeRid : 0;
             int32_t frr = RA ? (int32_t)d.frid()[nfr > 0 ? nfr - 1 : 0] : 0;
+            /* and the entry under it (its line): a split of the row at pos takes the top for its right part */
+            int32_t frr2 = RA ? (int32_t)d.frid()[nfr > 1 ? nfr - 2 : 0] : 0;
+            /* the props record of a segment with properties (the shared pool: a cache hit), for the row set-up */
+            const bool pa = RA && op.props;
+            int32_t prOff = 0, prN = 0, prComb = 0;
+            if (pa) {
+                const mt_props_rec& pr0 = p.props[op.props - 1];
+                prOff = (int32_t)pr0.kv_off;
+                prN = pr0.nkv;
+                prComb = pr0.combining;
+            }
             const bool tpreOk = RA && text && L <= W::N;
             int32_t tpre = tpreOk && w.lane() < L ? p.text[op.text_off + w.lane()] : 0;
             int32_t off = 0;
@@ -4280,6 +4294,9 @@ struct Replica {
             if (RA && zh->nfreeRid == nfr && nfr > 0) { /* alloc_rid, with the stack's top read above */
                 zh->nfreeRid = nfr - 1;
                 rid = frr;
+            } else if (RA && zh->nfreeRid == nfr - 1 && nfr > 1) { /* a split took the top */
+                zh->nfreeRid = nfr - 2;
+                rid = frr2;
             } else {
                 rid = alloc_rid();
             }
@@ -4324,11 +4341,16 @@ struct Replica {
             /* {cli, rcli, flags, ng = 0} in one store */
             st_bytes4(s, (uint32_t)(uint8_t)(client < 0 ? LOCAL_CLIENT : client) |
                              ((uint32_t)(preRseq > 0 ? preRcli : 0) << 8) | ((uint32_t)(uint8_t)fl << 16));
+            if (pa) { /* TextSegment.make(text, props): the new row's flags are known (no RF_PROPS), so nothing of it is
+                         * read; its kv reads go out with the set-up's (one round trip) */
+                add_props(s, p.kv + prOff, prN, prComb == MT_COMBINE_REWRITE ? MT_COMBINE_REWRITE : MT_COMBINE_NONE, 0,
+                          false, fl);
+            }
             if constexpr (RA)
                 row_enter_known(s, rid, gen, seq, preRseq > 0 ? preRseq : NOREM, L);
             else if constexpr (TILED)
                 row_enter(s);
-            if (op.props) { /* TextSegment.make(text, props): addProperties without collab */
+            if (op.props && !pa) { /* TextSegment.make(text, props): addProperties without collab */
                 const mt_props_rec& pr = p.props[op.props - 1];
                 add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE ? MT_COMBINE_REWRITE : MT_COMBINE_NONE,
                           0, false);
@@ -4829,7 +4851,7 @@ struct Replica {
     MT_HD int32_t marker_by_id(int32_t kid, int32_t vid) {
         int32_t slot = -1;
         for (int32_t k = 0; k < zh->nkeys; k++)
-            if (z.keys[k] == kid) slot = k;
+            if (keys[k] == kid) slot = k;
         if (slot < 0 || (vid & ~MT_VALUE_FALSY) == 0) return -1;
         if (zh->mkMask & (1 << slot)) return -2; /* the id key was annotated on a marker: not modelled */
         int32_t found = -1, n = 0;
@@ -5014,7 +5036,7 @@ struct Replica {
         int32_t s = -1;
         /* an annotate's keys: their slots (the doc's key ids, a lane each, read with the rows) */
         const int32_t l = w.lane();
-        int32_t key = kind == MT_OP_ANNOTATE && l < HT::K ? (int32_t)z.keys[l < HT::K ? l : 0] : -1;
+        int32_t key = kind == MT_OP_ANNOTATE && l < HT::K ? (int32_t)keys[l < HT::K ? l : 0] : -1;
 #pragma unroll
         for (int32_t j = 0; j < MAXN; j++) /* the leaf's row ids: one round trip */
             if (mem && j < c && z.rid[leaf * MAXN + j] == (IX)rd) s = leaf * MAXN + j;
@@ -5680,7 +5702,7 @@ struct Replica {
             for (int q = 0; q < np; q++) {
                 int32_t best = -1, bk = 0x7fffffff;
                 for (int k = 0; k < HT::K; k++) {
-                    int32_t key = z.keys[k];
+                    int32_t key = keys[k];
                     if (cold(s).pv[k] && key > last && key < bk) {
                         bk = key;
                         best = k;

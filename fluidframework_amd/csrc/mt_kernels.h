@@ -358,6 +358,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     constexpr int NG = HT::TL::NG;
     __shared__ int32_t lcord[NCH], lcst[NCH], lcpos[NCH], lccnt[NCH], lwrid[WCAP];
     __shared__ int32_t lgst[NG], lgdel[NG]; /* chunk-group sums of lcst and of cdel */
+    __shared__ uint16_t lkeys[HT::K];       /* the property key table */
     __shared__ __attribute__((aligned(16))) uint8_t lwgen[WCAP];
     __shared__ int32_t lwslot[WCAP];
     __shared__ int32_t lhseq[HL]; /* NARROW: the zamboni heap */
@@ -383,6 +384,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         for (int i = threadIdx.x; i < NCH; i += WG) cdel[i] = 0;
         for (int i = threadIdx.x; i < NG; i += WG) lgdel[i] = 0;
         wave_copy(lgst, tl.gst, NG);
+        wave_copy(lkeys, v.t->keys, HT::K);
         wave_copy((int32_t*)&zhs, (const int32_t*)&v.t->h, (int)(sizeof(DocHdr) / 4));
         wave_copy(lcord, tl.cord, NCH);
         wave_copy(lcst, tl.cst, NCH);
@@ -427,6 +429,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         r.tcst = lcst;
         r.tgst = lgst;
         r.gdel = lgdel;
+        r.keys = lkeys;
         r.tcpos = lcpos;
         r.tccnt = lccnt;
         r.twrid = lwrid;
@@ -452,6 +455,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         wave_copy(tl.cord, lcord, NCH);
         wave_copy(tl.cst, lcst, NCH);
         wave_copy(tl.gst, lgst, NG);
+        wave_copy(v.t->keys, lkeys, HT::K);
         wave_copy(tl.cpos, lcpos, NCH);
         wave_copy(tl.ccnt, lccnt, NCH);
         wave_copy(tl.wrid, lwrid, WCAP);
