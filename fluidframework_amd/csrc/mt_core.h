@@ -1599,11 +1599,19 @@ struct Replica {
         }
         w.sync();
     }
+    /* cls[lch[n]][lix[n]] always equals lst[n] (every update writes both): the new sum goes to both, one read */
     MT_HD void lst_add(int32_t n, int32_t d) {
         auto& t = z.tl;
-        int32_t c = t.lch[n];
-        t.lst[n] += d;
-        t.cls[c][t.lix[n]] += d;
+        int32_t c = t.lch[n], v = t.lst[n] + d;
+        t.lst[n] = v;
+        t.cls[c][t.lix[n]] = v;
+        cst_add(tcpos[c], d);
+    }
+    /* lst_add with the leaf's chunk, index and sum read ahead by the caller */
+    MT_HD void lst_add_known(int32_t n, int32_t c, int32_t ix, int32_t old, int32_t d) {
+        auto& t = z.tl;
+        t.lst[n] = old + d;
+        t.cls[c][ix] = old + d;
         cst_add(tcpos[c], d);
     }
     /* recompute leaf n's STABLE length from its rows */
@@ -1802,8 +1810,9 @@ struct Replica {
                     if (w.bcast(rv[q].rseq, l) == NOREM) {
                         t.xf[ss] = XF_STABLE;
                         int32_t dl = w.bcast(rv[q].len, l), lcl = w.bcast(lc[q], l);
-                        t.lst[ss / MAXN] += dl;
-                        t.cls[lcl][w.bcast(lx[q], l)] += dl;
+                        int32_t nv = t.lst[ss / MAXN] + dl; /* cls mirrors lst: one read */
+                        t.lst[ss / MAXN] = nv;
+                        t.cls[lcl][w.bcast(lx[q], l)] = nv;
                         cst_add(tcpos[lcl], dl);
                     } else {
                         t.xf[ss] = 0;
@@ -4652,7 +4661,14 @@ struct Replica {
             int32_t s = n * MAXN + (j & (MAXN - 1));
             RowView r = row_view(s); /* the row, its window flags and id, the leaf's child count: one round trip */
             uint8_t x = 0;
-            if constexpr (TILED) x = t.xf[s];
+            int32_t lch0 = 0, lix0 = 0, lst0 = 0; /* tiled: the leaf's chunk, index and STABLE sum, for its update */
+            if constexpr (TILED) {
+                x = t.xf[s];
+                lch0 = t.lch[n];
+                lix0 = t.lix[n];
+                lst0 = t.lst[n];
+            }
+            int32_t sc0 = nsc[n]; /* the leaf's needsScour, for its LRU entry */
             int32_t rid = z.rid[s];
             int32_t c = nch[n];
             int32_t j0 = k == ka ? (sa & (MAXN - 1)) : 0;
@@ -4694,7 +4710,7 @@ struct Replica {
             if (wadd) x2 = XF_W;
             uint8_t g = wadd ? z.rgen[rid] : 0;
             if (sel) t.xf[s] = x2;
-            if (lsd) lst_add(n, -lsd);
+            if (lsd) lst_add_known(n, lch0, lix0, lst0, -lsd);
             uint64_t wm = w.ballot(wadd);
             if (wm) {
                 int32_t wn = t.wN, cnt = __builtin_popcountll(wm);
@@ -4721,7 +4737,10 @@ struct Replica {
                     pending_add(w.bcast(s, l), localSeq, created);
                 }
                 uint64_t lm = sm & ~w.ballot(pend);
-                if (lm) add_lru(w.bcast(s, W::ffs(lm)), seq); /* the leaf's first: add_lru marks the leaf */
+                if (lm && sc0 != 1 && seq > h.currentSeq) { /* add_lru of the leaf's first such row (it marks the leaf) */
+                    nsc[n] = 1;
+                    heap_add(w.bcast(rid, W::ffs(lm)), seq);
+                }
             }
             if (k == kb || !kvalid(knext(k))) break;
         }
