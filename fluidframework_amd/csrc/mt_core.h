@@ -1199,14 +1199,15 @@ struct Replica {
     }
     MT_HD int32_t vis_of(int32_t s, const RowView& r, int32_t refSeq, int32_t client) const {
         if (is_local(client)) return r.rseq == NOREM ? r.len : 0;
-        uint8_t cq = (uint8_t)r.b4, rcq = (uint8_t)(r.b4 >> 8), fq = (uint8_t)(r.b4 >> 16);
-        int32_t c = cq == LOCAL_CLIENT ? -1 : cq;
-        if (!(c == client || (r.seq != UNASSIGNED_SEQ && r.seq <= refSeq))) return 0;
+        /* the tests of quad_vis_of: short id bytes against the client's byte, one unsigned compare per seq */
+        const uint32_t uc = (uint32_t)(uint8_t)client;
+        const uint32_t ur1 = refSeq >= 0 ? (uint32_t)refSeq + 1u : 0u;
+        uint32_t cq = r.b4 & 0xFFu, rcq = (r.b4 >> 8) & 0xFFu, fq = (r.b4 >> 16) & 0xFFu;
+        if (!(cq == uc || (uint32_t)r.seq < ur1)) return 0;
         if (r.rseq != NOREM) {
-            int32_t rc = rcq == LOCAL_CLIENT ? -1 : rcq;
-            if (rc == client) return 0;
+            if (rcq == uc) return 0;
             if ((fq & RF_OVL) && ovl_has(s, client)) return 0; /* cold read: rare */
-            if (r.rseq != UNASSIGNED_SEQ && r.rseq <= refSeq) return 0;
+            if ((uint32_t)r.rseq < ur1) return 0;
         }
         return r.len;
     }
@@ -2308,8 +2309,10 @@ struct Replica {
     struct QuadRows {
         I4 L, R, Q, BY;
     };
+    /* lanes with s0 < 0 (past the last leaf) and the fields a local perspective does not use are left unset:
+     * quad_vis_of reads neither (zeroing them cost 16 moves per scanned block) */
     MT_HD QuadRows quad_load(int32_t s0, bool local) const {
-        QuadRows x = {};
+        QuadRows x;
         if (s0 >= 0) {
             x.L = ld4(&z.len(s0));
             x.R = ld4(&z.rseq(s0));
@@ -2339,16 +2342,19 @@ struct Replica {
         const I4& Q = x.Q;
         const I4& BY = x.BY; /* {cli, rcli, flags, ng} of the 4 slots */
         int32_t ovq = 0;
+        /* the same tests in fewer instructions: a short id byte equals the client's (LocalClientId -1 is byte 0xFF,
+         * LOCAL_CLIENT), and "s != UNASSIGNED_SEQ && s <= refSeq" is one unsigned compare against refSeq + 1 (0 when
+         * refSeq < 0): UNASSIGNED_SEQ (-1) and NOREM (INT32_MIN) are above every bound as unsigned values */
+        const uint32_t uc = (uint32_t)(uint8_t)client;
+        const uint32_t ur1 = refSeq >= 0 ? (uint32_t)refSeq + 1u : 0u;
         for (int q = 0; q < 4; q++) {
             uint32_t by = (uint32_t)BY.x[q];
-            uint8_t cq = (uint8_t)by, rcq = (uint8_t)(by >> 8), fq = (uint8_t)(by >> 16);
-            int32_t c = cq == LOCAL_CLIENT ? -1 : (int32_t)cq;
+            uint32_t cq = by & 0xFFu, rcq = (by >> 8) & 0xFFu, fq = (by >> 16) & 0xFFu;
             int32_t sq = Q.x[q];
-            bool ok = L.x[q] > 0 && (c == client || (sq != UNASSIGNED_SEQ && sq <= refSeq));
+            bool ok = L.x[q] > 0 && (cq == uc || (uint32_t)sq < ur1);
             int32_t rs = R.x[q];
             if (ok && rs != NOREM) {
-                int32_t rc = rcq == LOCAL_CLIENT ? -1 : (int32_t)rcq;
-                if (rc == client || (rs != UNASSIGNED_SEQ && rs <= refSeq))
+                if (rcq == uc || (uint32_t)rs < ur1)
                     ok = false;
                 else if (fq & RF_OVL)
                     ovq |= 1 << q; /* removedClientOverlap: looked up once below, not in each unrolled slot */
