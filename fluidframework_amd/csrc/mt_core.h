@@ -4305,6 +4305,25 @@ struct Replica {
                 return;
             }
             MT_PROF_SCOPE(PH_PLACE);
+            /* flat GPU profile: the set-up's independent reads issued together once the search is done (no register
+             * lives across it, which at 8 waves per SIMD costs more than it saves, r04r): the free row-id stack's top,
+             * the text (up to a wave's length), the props record; then the row id's generation with the property
+             * reads */
+            constexpr bool FP = !TILED && W::N >= 64;
+            int32_t fnfr = 0, ffrr = 0, ftp = 0, fpOff = 0, fpN = 0, fpComb = 0;
+            const bool ftpOk = FP && text && L <= W::N;
+            const bool fpa = FP && op.props;
+            if constexpr (FP) {
+                fnfr = zh->nfreeRid;
+                ffrr = (int32_t)d.frid()[fnfr > 0 ? fnfr - 1 : 0];
+                ftp = ftpOk && w.lane() < L ? p.text[op.text_off + w.lane()] : 0;
+                if (fpa) {
+                    const mt_props_rec& pr0 = p.props[op.props - 1];
+                    fpOff = (int32_t)pr0.kv_off;
+                    fpN = pr0.nkv;
+                    fpComb = pr0.combining;
+                }
+            }
             int32_t rid;
             if (RA && zh->nfreeRid == nfr && nfr > 0) { /* alloc_rid, with the stack's top read above */
                 zh->nfreeRid = nfr - 1;
@@ -4312,9 +4331,13 @@ struct Replica {
             } else if (RA && zh->nfreeRid == nfr - 1 && nfr > 1) { /* a split took the top */
                 zh->nfreeRid = nfr - 2;
                 rid = frr2;
+            } else if (FP && fnfr > 0) {
+                zh->nfreeRid = fnfr - 1;
+                rid = ffrr;
             } else {
                 rid = alloc_rid();
             }
+            const int32_t fgen = FP ? (int32_t)z.rgen[rid] : 0; /* for the LRU entry */
             int32_t gen = 0, sc = 0;
             if (RA) { /* for the window set and the LRU entry: one round trip */
                 gen = z.rgen[rid];
@@ -4344,9 +4367,10 @@ struct Replica {
             if (text) {
                 MT_PROF_SCOPE(PH_TEXT);
                 int32_t last;
-                if (tpreOk) {
-                    if (w.lane() < L) arena_base(zh->arenaSide)[off + w.lane()] = (uint16_t)tpre;
-                    last = w.bcast(tpre, L - 1);
+                if (tpreOk || ftpOk) {
+                    const int32_t tv = tpreOk ? tpre : ftp;
+                    if (w.lane() < L) arena_base(zh->arenaSide)[off + w.lane()] = (uint16_t)tv;
+                    last = w.bcast(tv, L - 1);
                     w.sync();
                 } else {
                     last = arena_copy(arena_base(zh->arenaSide) + off, p.text + op.text_off, L);
@@ -4356,16 +4380,16 @@ struct Replica {
             /* {cli, rcli, flags, ng = 0} in one store */
             st_bytes4(s, (uint32_t)(uint8_t)(client < 0 ? LOCAL_CLIENT : client) |
                              ((uint32_t)(preRseq > 0 ? preRcli : 0) << 8) | ((uint32_t)(uint8_t)fl << 16));
-            if (pa) { /* TextSegment.make(text, props): the new row's flags are known (no RF_PROPS), so nothing of it is
-                         * read; its kv reads go out with the set-up's (one round trip) */
-                add_props(s, p.kv + prOff, prN, prComb == MT_COMBINE_REWRITE ? MT_COMBINE_REWRITE : MT_COMBINE_NONE, 0,
-                          false, fl);
+            if (pa || fpa) { /* TextSegment.make(text, props): the new row's flags are known (no RF_PROPS), so nothing of
+                              * it is read; its kv reads go out with the set-up's (one round trip) */
+                const int32_t ko = pa ? prOff : fpOff, kn = pa ? prN : fpN, kc = pa ? prComb : fpComb;
+                add_props(s, p.kv + ko, kn, kc == MT_COMBINE_REWRITE ? MT_COMBINE_REWRITE : MT_COMBINE_NONE, 0, false, fl);
             }
             if constexpr (RA)
                 row_enter_known(s, rid, gen, seq, preRseq > 0 ? preRseq : NOREM, L);
             else if constexpr (TILED)
                 row_enter(s);
-            if (op.props && !pa) { /* TextSegment.make(text, props): addProperties without collab */
+            if (op.props && !pa && !fpa) { /* TextSegment.make(text, props): addProperties without collab */
                 const mt_props_rec& pr = p.props[op.props - 1];
                 add_props(s, p.kv + pr.kv_off, pr.nkv, pr.combining == MT_COMBINE_REWRITE ? MT_COMBINE_REWRITE : MT_COMBINE_NONE,
                           0, false);
@@ -4377,6 +4401,8 @@ struct Replica {
                 } else if (seq > h.minSeq) {
                     if (RA)
                         add_lru_known(s / MAXN, rid, gen, sc, seq);
+                    else if (FP)
+                        add_lru_known(s / MAXN, rid, fgen, nsc[s / MAXN], seq);
                     else
                         add_lru(s, seq);
                 }
