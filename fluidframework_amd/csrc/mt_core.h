@@ -3760,27 +3760,31 @@ struct Replica {
                 }
             }
         }
-        uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
-        if ((drop >> q) & 1) {
-            int32_t pos = zh->nfreeRid + __builtin_popcountll(drop & below);
-            z.rgen[r.rid]++;
-            d.frid()[pos] = (IX)r.rid;
+        /* nothing dropped: nothing appended either (an appended row is dropped), so every row keeps its slot, length
+         * and flags and the leaves their child counts; no writes */
+        if (drop) {
+            uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
+            if ((drop >> q) & 1) {
+                int32_t pos = zh->nfreeRid + __builtin_popcountll(drop & below);
+                z.rgen[r.rid]++;
+                d.frid()[pos] = (IX)r.rid;
+            }
+            int32_t ndrop = __builtin_popcountll(drop);
+            zh->nfreeRid += ndrop;
+            h.nrows -= ndrop;
+            /* compaction: kept rows move down within their leaf; vacated slots get length 0 */
+            uint64_t lmask = n >= 0 ? (0xFFull << (8 * li)) : 0ull;
+            int32_t newc = __builtin_popcountll(keep & lmask);
+            w.sync();
+            if ((keep >> q) & 1) {
+                r.len = nlen;
+                r.flags = (uint8_t)fl;
+                store_row(n * MAXN + __builtin_popcountll(keep & lmask & below), r);
+            }
+            if (valid && j >= newc) z.len(n * MAXN + j) = 0; /* disjoint from every kept row's target */
+            if (n >= 0 && j == 0) nch[n] = (int8_t)newc;
+            w.sync();
         }
-        int32_t ndrop = __builtin_popcountll(drop);
-        zh->nfreeRid += ndrop;
-        h.nrows -= ndrop;
-        /* compaction: kept rows move down within their leaf; vacated slots get length 0 */
-        uint64_t lmask = n >= 0 ? (0xFFull << (8 * li)) : 0ull;
-        int32_t newc = __builtin_popcountll(keep & lmask);
-        w.sync();
-        if ((keep >> q) & 1) {
-            r.len = nlen;
-            r.flags = (uint8_t)fl;
-            store_row(n * MAXN + __builtin_popcountll(keep & lmask & below), r);
-        }
-        if (valid && j >= newc) z.len(n * MAXN + j) = 0; /* disjoint from every kept row's target */
-        if (n >= 0 && j == 0) nch[n] = (int8_t)newc;
-        w.sync();
 #pragma unroll
         for (int32_t i = 0; i < MAXN; i++) /* constant indices: the caller's array stays in registers */
             if (i < nl) cnt[i] = __builtin_popcountll(keep & (0xFFull << (8 * i)));
