@@ -4713,6 +4713,7 @@ struct Replica {
             int32_t rs = r.rseq, L = r.len;
             uint32_t b4 = r.b4, fl = (b4 >> 16) & 0xFF;
             bool fresh = sel && rs == NOREM, unas = sel && rs == UNASSIGNED_SEQ;
+            const int32_t rgn = sel ? (int32_t)z.rgen[rid] : 0; /* for the leaf's LRU entry (its read overlaps the updates) */
             int32_t nrs = fresh || unas ? seq : rs; /* rs after the update */
             uint64_t sm = w.ballot(sel);
             zh->sumW += __builtin_popcountll(sm);
@@ -4775,7 +4776,7 @@ struct Replica {
                 uint64_t lm = sm & ~w.ballot(pend);
                 if (lm && sc0 != 1 && seq > h.currentSeq) { /* add_lru of the leaf's first such row (it marks the leaf) */
                     nsc[n] = 1;
-                    heap_add(w.bcast(rid, W::ffs(lm)), seq);
+                    heap_add(w.bcast(rid, W::ffs(lm)), seq, w.bcast(rgn, W::ffs(lm)));
                 }
             }
             if (k == kb || !kvalid(knext(k))) break;
@@ -5087,6 +5088,7 @@ struct Replica {
     MT_HD void ack_rows(int32_t kind, int32_t rd, bool mem, int32_t seq, const mt_kv* kv = nullptr, int32_t nkv = 0,
                         bool rewrite = false) {
         int32_t leaf = mem ? (int32_t)z.rleaf[rd] : 0;
+        int32_t gen = mem ? (int32_t)z.rgen[rd] : 0; /* with the leaf id: the LRU entries need no more reads */
         int32_t c = nch[leaf];
         int32_t s = -1;
         /* an annotate's keys: their slots (the doc's key ids, a lane each, read with the rows) */
@@ -5120,7 +5122,8 @@ struct Replica {
             while (om) {
                 int32_t q = W::ffs(om);
                 om &= om - 1;
-                add_lru(w.bcast(s, q), seq);
+                int32_t sq = w.bcast(s, q);
+                add_lru_known(sq / MAXN, w.bcast(rd, q), w.bcast(gen, q), nsc[sq / MAXN], seq);
             }
             return;
         }
@@ -5145,7 +5148,8 @@ struct Replica {
         while (om) {
             int32_t l = W::ffs(om);
             om &= om - 1;
-            add_lru(w.bcast(s, l), seq);
+            int32_t sl = w.bcast(s, l);
+            add_lru_known(sl / MAXN, w.bcast(rd, l), w.bcast(gen, l), nsc[sl / MAXN], seq);
         }
     }
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
