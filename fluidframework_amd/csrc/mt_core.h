@@ -2637,7 +2637,7 @@ struct Replica {
      * write pass also leaves an empty slot between the halves for the new row (rows after the split move two
      * slots), which *gapOut returns — the shift leaf_insert_slot would make with a second read of the leaf */
     MT_HD int32_t split_row_par(int32_t n, int32_t j, int32_t off, int32_t* rsOut, int32_t* gapOut = nullptr,
-                                const HotRow* pre = nullptr, int32_t preC = -1) {
+                                const HotRow* pre = nullptr, int32_t preC = -1, int32_t* ridOut = nullptr) {
         constexpr int CW = (int)(sizeof(typename HT::Cold) / 4);
         static_assert(W::N >= CW && W::N >= MAXN, "a lane per cold dword and per slot");
         const int32_t l = w.lane();
@@ -2728,18 +2728,20 @@ struct Replica {
         }
         if (ng0) split_groups(rid0, rrid, (int32_t)ng0); /* segmentGroups.copyTo */
         if (rsOut) *rsOut = rs;
+        if (ridOut) *ridOut = rrid;
         return ls;
     }
     /* Split the row at lorder coordinate t at offset off (0 < off < len). Returns the slot of
      * the LEFT part afterwards (the right part is the next row in document order). */
     /* pre / preC (GPU): the leaf's rows (lane l: child l & 7) and child count as a search just read them */
+    /* ridOut: the right part's row id (the caller need not read back what the split wrote) */
     MT_HD int32_t split_row(int32_t t, int32_t off, int32_t* rsOut = nullptr, int32_t* gapOut = nullptr,
-                            const HotRow* pre = nullptr, int32_t preC = -1) {
+                            const HotRow* pre = nullptr, int32_t preC = -1, int32_t* ridOut = nullptr) {
         MT_PROF_SCOPE(PH_SPLIT);
         int32_t n = leaf_at(t >> 3), j = t & 7;
         int32_t s0 = n * MAXN + j;
         if constexpr (W::N >= 64) {
-            if (!dl_on() && !refs_on()) return split_row_par(n, j, off, rsOut, gapOut, pre, preC);
+            if (!dl_on() && !refs_on()) return split_row_par(n, j, off, rsOut, gapOut, pre, preC, ridOut);
         }
         if (z.flags(s0) & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
         bool willSplit = nch[n] + 1 >= MAXN;
@@ -2791,6 +2793,7 @@ struct Replica {
             dtail(2);
         }
         if (rsOut) *rsOut = rs;
+        if (ridOut) *ridOut = rrid;
         return ls;
     }
 
@@ -4557,16 +4560,16 @@ struct Replica {
             int32_t ridFirst = z.rid[sf];
             int32_t sl = sg; /* the last row's slot, while nothing has moved it */
             if (Pf < start) { /* start falls inside the first row: split it; its right part is first */
-                int32_t rs = -1;
-                if (split_row(tf, start - Pf, &rs) < 0 || rs < 0) return;
+                int32_t rs = -1, rr = -1;
+                if (split_row(tf, start - Pf, &rs, nullptr, nullptr, -1, &rr) < 0 || rs < 0) return;
                 sl = -1;
                 if (tf == tg) {
-                    ridLast = z.rid[rs];
+                    ridLast = rr;
                     sl = rs;
                     vg = Pf + vf - start;
                     Pg = start;
                 }
-                ridFirst = z.rid[rs];
+                ridFirst = rr;
             }
             if (Pg + vg > end) { /* end falls inside the last row: split it; its left part keeps the id */
                 if (sl < 0) sl = slot_of(ridLast, -1);
@@ -4676,16 +4679,16 @@ struct Replica {
         int32_t ridFirst = z.rid[sf];
         int32_t sl = sg; /* the last row's slot, while nothing has moved it */
         if (Pf < start) {
-            int32_t rs = -1;
-            if (split_row(tf, start - Pf, &rs, nullptr, fc >= 0 ? &fr : nullptr, fc) < 0 || rs < 0) return;
+            int32_t rs = -1, rr = -1;
+            if (split_row(tf, start - Pf, &rs, nullptr, fc >= 0 ? &fr : nullptr, fc, &rr) < 0 || rs < 0) return;
             sl = -1;
             if (tf == tg) {
-                ridLast = z.rid[rs];
+                ridLast = rr;
                 sl = rs;
                 vg = Pf + vf - start;
                 Pg = start;
             }
-            ridFirst = z.rid[rs];
+            ridFirst = rr;
         }
         if (Pg + vg > end) {
             if (sl < 0) sl = slot_of(ridLast, -1);
