@@ -276,7 +276,6 @@ struct HotT {
     int8_t _pad[(16 - (3 * N) % 16) % 16];
     int32_t hseq[H];
     IX hrid[H];  /* segment (row id) queued for scouring */
-    IX hleaf[H]; /* the leaf it sat in when queued: a hint (rows move), so a pop reads that leaf with the row's own */
     uint8_t hgen[H];  /* its row-id generation when queued: a mismatch means it was unlinked */
     uint16_t s2l[C];  /* short client id -> long id (client.ts:637-661) */
     uint8_t l2s[C];   /* long id (< C) -> short id, 0xFF = not seen yet */
@@ -464,7 +463,6 @@ struct Replica {
     int32_t* hsq;
     IX* hrd;
     uint8_t* hgn;
-    IX* hlf; /* heap entries' leaf hints (z.hleaf, or the kernel's LDS copy) */
     /* tiled profile: scratch of a position search — per-chunk window deltas (all zero between
      * searches) and per window row its chunk position, leaf index and perspective length. The image
      * holds host copies; the GPU kernel points them at LDS. */
@@ -496,7 +494,7 @@ struct Replica {
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
         : d(doc), z(*doc.t), w(wave), zh(&z.h), keys(z.keys), l2s(z.l2s), s2l(z.s2l), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
-          nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen), hlf(z.hleaf), cdel(nullptr), wcp(nullptr), wvs(nullptr),
+          nsc(z.nscour), hsq(z.hseq), hrd(z.hrid), hgn(z.hgen), cdel(nullptr), wcp(nullptr), wvs(nullptr),
           wlx(nullptr), tcord(nullptr), tcst(nullptr), tgst(nullptr), gdel(nullptr), tcpos(nullptr), tccnt(nullptr), twrid(nullptr), twgen(nullptr), twslot(nullptr),
           cur(0) {
         if constexpr (TILED) {
@@ -2890,25 +2888,22 @@ struct Replica {
 
     /* ---- zamboni heap (collections.ts:212-264, LRUSegmentComparer mergeTree.ts:957-960) ---- */
     MT_HD void heap_swap(int32_t i, int32_t j) {
-        IX tr = hrd[i], tl = hlf[i];
+        IX tr = hrd[i];
         int32_t tq = hsq[i];
         uint8_t tg = hgn[i];
         hrd[i] = hrd[j];
         hsq[i] = hsq[j];
         hgn[i] = hgn[j];
-        hlf[i] = hlf[j];
         hrd[j] = tr;
         hsq[j] = tq;
         hgn[j] = tg;
-        hlf[j] = tl;
     }
     /* Heap.add + fixup (collections.ts:221-225, 240-247). On the GPU the sift-up is one step: the
      * ancestors of the new leaf position are read in parallel (lane i: the (i+1)-th ancestor), the
      * ones it passes are exactly the leading run with maxSeq greater than it (ancestors are ordered
      * along a path), and they all move down one level at once. */
     /* gen: the row id's generation if the caller has read it (-1: read here) */
-    /* leaf: where the row sits now (a hint for the pop; -1: unknown) */
-    MT_HD void heap_add(int32_t rid, int32_t seq, int32_t knownGen = -1, int32_t leaf = -1) {
+    MT_HD void heap_add(int32_t rid, int32_t seq, int32_t knownGen = -1) {
         MT_PROF_SCOPE(PH_HEAP);
         int32_t n = h.heapN;
         if (n >= HCAPR) {
@@ -2926,7 +2921,6 @@ struct Replica {
                 hrd[n] = (IX)rid;
                 hsq[n] = seq;
                 hgn[n] = gen;
-                hlf[n] = (IX)leaf;
             }
             w.sync();
             if (n == 0) zh->heapTop = seq;
@@ -2938,12 +2932,11 @@ struct Replica {
             int32_t as = a >= 1 ? hsq[a - 1] : 0;
             uint64_t m = w.ballot(a >= 1 && as - seq > 0);
             int32_t up = __builtin_ctzll(~m); /* length of the leading run */
-            IX ar = 0, al = 0;
+            IX ar = 0;
             uint8_t ag = 0;
             if (l < up) {
                 ar = hrd[a - 1];
                 ag = hgn[a - 1];
-                al = hlf[a - 1];
             }
             w.sync();
             if (l < up) { /* ancestor l+1 moves to ancestor l (ancestor 0 = position k) */
@@ -2951,14 +2944,12 @@ struct Replica {
                 hrd[dst] = ar;
                 hsq[dst] = as;
                 hgn[dst] = ag;
-                hlf[dst] = al;
             }
             int32_t fin = k >> up;
             if (l == 0) {
                 hrd[fin - 1] = (IX)rid;
                 hsq[fin - 1] = seq;
                 hgn[fin - 1] = gen;
-                hlf[fin - 1] = (IX)leaf;
             }
             w.sync();
             if (fin == 1) zh->heapTop = seq;
@@ -2966,7 +2957,6 @@ struct Replica {
             hrd[k - 1] = (IX)rid;
             hsq[k - 1] = seq;
             hgn[k - 1] = gen;
-            hlf[k - 1] = (IX)leaf;
             while (k > 1 && hsq[(k >> 1) - 1] - hsq[k - 1] > 0) {
                 heap_swap((k >> 1) - 1, k - 1);
                 k >>= 1;
@@ -2978,7 +2968,7 @@ struct Replica {
      * entries, every entry is read in one pass (lane = index mod 64, one register per 64 entries and
      * field), the descent is taken on scalars, and the entries on the path move up one level in one
      * parallel pass whose values come from those registers (lane shuffles): one round trip per pop. */
-    MT_HD void heap_pop(int32_t* rid, int32_t* seq, int32_t* gen, int32_t* leaf) {
+    MT_HD void heap_pop(int32_t* rid, int32_t* seq, int32_t* gen) {
         MT_PROF_SCOPE(PH_HEAP);
         MT_PROF_COUNT(PH_C_POP, 1);
         int32_t cnt = h.heapN;
@@ -2998,11 +2988,10 @@ struct Replica {
                 r3 = 192 + l < cnt ? (int32_t)hrd[192 + l] : 0, g3 = 192 + l < cnt ? hgn[192 + l] : 0;
             }
             int32_t last = cnt - 1; /* index of the entry that moves to the root */
-            IX xr = hrd[last], xl = hlf[last];
+            IX xr = hrd[last];
             uint8_t xg = hgn[last];
             *rid = hrd[0];
             *gen = hgn[0];
-            *leaf = hlf[0];
             auto L = [&](int32_t i) -> int32_t { /* maxSeq at 1-based position i (i >= 2) */
                 int32_t x = i - 1, c = x >> 6;
                 int32_t v = c == 0 ? c0 : c == 1 ? c1 : c == 2 ? c2 : c3;
@@ -3040,32 +3029,28 @@ struct Replica {
                 int32_t a0 = w.shfl(v0, sl), a1 = w.shfl(v1, sl), a2 = w.shfl(v2, sl), a3 = w.shfl(v3, sl);
                 return sc == 0 ? a0 : sc == 1 ? a1 : sc == 2 ? a2 : a3;
             };
-            IX mr = 0, ml = 0;
+            IX mr = 0;
             uint8_t mg = 0;
             int32_t ms = 0;
             if (PICK) {
                 mr = (IX)pick(r0, r1, r2, r3);
                 mg = (uint8_t)pick(g0, g1, g2, g3);
                 ms = pick(c0, c1, c2, c3);
-                if (l < d) ml = hlf[src - 1];
             } else if (l < d) {
                 mr = hrd[src - 1];
                 mg = hgn[src - 1];
                 ms = hsq[src - 1];
-                ml = hlf[src - 1];
             }
             w.sync();
             if (l < d) {
                 hrd[dst - 1] = mr;
                 hsq[dst - 1] = ms;
                 hgn[dst - 1] = mg;
-                hlf[dst - 1] = ml;
             }
             if (l == 0) {
                 hrd[k - 1] = xr;
                 hsq[k - 1] = xs;
                 hgn[k - 1] = xg;
-                hlf[k - 1] = xl;
             }
             w.sync();
             zh->heapTop = d > 0 ? w.bcast(ms, 0) : xs;
@@ -3078,9 +3063,8 @@ struct Replica {
             *rid = hrd[0];
             *gen = hgn[0];
             *seq = hsq[0];
-            *leaf = hlf[0];
             int32_t last = cnt - 1;
-            IX xr = hrd[last], xl = hlf[last];
+            IX xr = hrd[last];
             uint8_t xg = hgn[last];
             int32_t xs = hsq[last];
             cnt--;
@@ -3125,27 +3109,24 @@ struct Replica {
                 if (!done) k = lastj;
             }
             int32_t fin = d > 0 ? lastj : 1;
-            IX mr = 0, ml = 0;
+            IX mr = 0;
             uint8_t mg = 0;
             int32_t ms = 0;
             if (l < d) {
                 mr = hrd[src - 1];
                 mg = hgn[src - 1];
                 ms = hsq[src - 1];
-                ml = hlf[src - 1];
             }
             w.sync();
             if (l < d) {
                 hrd[dst - 1] = mr;
                 hsq[dst - 1] = ms;
                 hgn[dst - 1] = mg;
-                hlf[dst - 1] = ml;
             }
             if (l == 0) {
                 hrd[fin - 1] = xr;
                 hsq[fin - 1] = xs;
                 hgn[fin - 1] = xg;
-                hlf[fin - 1] = xl;
             }
             w.sync();
             zh->heapTop = d > 0 ? w.bcast(ms, 0) : xs;
@@ -3153,11 +3134,9 @@ struct Replica {
             *rid = hrd[0];
             *seq = hsq[0];
             *gen = hgn[0];
-            *leaf = hlf[0];
             hrd[0] = hrd[cnt - 1];
             hsq[0] = hsq[cnt - 1];
             hgn[0] = hgn[cnt - 1];
-            hlf[0] = hlf[cnt - 1];
             cnt--;
             h.heapN = cnt;
             int32_t k = 1;
@@ -3176,14 +3155,14 @@ struct Replica {
         int32_t n = s / MAXN;
         if (nsc[n] != 1 && seq > h.currentSeq) {
             nsc[n] = 1;
-            heap_add(z.rid[s], seq, -1, n);
+            heap_add(z.rid[s], seq);
         }
     }
     /* add_lru of a row whose id, generation and leaf's needsScour the caller has read */
     MT_HD void add_lru_known(int32_t n, int32_t rid, int32_t gen, int32_t sc, int32_t seq) {
         if (sc != 1 && seq > h.currentSeq) {
             nsc[n] = 1;
-            heap_add(rid, seq, gen, n);
+            heap_add(rid, seq, gen);
         }
     }
 
@@ -4107,29 +4086,20 @@ struct Replica {
         for (int i = 0; i < 2; i++) {
             if (h.heapN < 1) break;
             if (zh->heapTop > h.minSeq) break; /* peek (mergeTree.ts:1465-1468) */
-            int32_t rid, mseq, gen, hl;
-            heap_pop(&rid, &mseq, &gen, &hl);
+            int32_t rid, mseq, gen;
+            heap_pop(&rid, &mseq, &gen);
             int32_t n, before, after, par;
             if constexpr (W::N >= MAXN * MAXN) {
-                /* slot_of, needsScour and scourNode's row reads in one round trip: the row's leaf and generation with
-                 * everything about the leaf it sat in when queued (a hint, clamped to the node range); a second only
-                 * when the row has moved since */
+                /* slot_of, needsScour and scourNode's row reads in two round trips: the row's leaf, then
+                 * everything about that leaf */
                 int32_t g = z.rgen[rid];
-                int32_t nr = z.rleaf[rid];
-                const int32_t hn = hl < 0 ? 0 : (hl >= HT::N ? HT::N - 1 : hl);
-                int32_t j = w.lane();
-                HotRow r = load_row(hn * MAXN + (j & (MAXN - 1)));
-                before = nch[hn];
-                int32_t sc = nsc[hn];
-                par = npar[hn];
+                n = z.rleaf[rid];
                 if (g != (uint8_t)gen) continue; /* unlinked since it was queued */
-                n = nr;
-                if (nr != hn) { /* moved: the leaf it is in now */
-                    r = load_row(n * MAXN + (j & (MAXN - 1)));
-                    before = nch[n];
-                    sc = nsc[n];
-                    par = npar[n];
-                }
+                int32_t j = w.lane();
+                HotRow r = load_row(n * MAXN + (j & (MAXN - 1)));
+                before = nch[n];
+                int32_t sc = nsc[n];
+                par = npar[n];
                 if (!w.ballot(j < before && r.rid == (IX)rid)) continue; /* merged away since it was queued */
                 if (sc == 0) continue;
                 MT_PROF_COUNT(PH_C_SCOUR, 1);
@@ -4809,7 +4779,7 @@ struct Replica {
                 uint64_t lm = sm & ~w.ballot(pend);
                 if (lm && sc0 != 1 && seq > h.currentSeq) { /* add_lru of the leaf's first such row (it marks the leaf) */
                     nsc[n] = 1;
-                    heap_add(w.bcast(rid, W::ffs(lm)), seq, w.bcast(rgn, W::ffs(lm)), n);
+                    heap_add(w.bcast(rid, W::ffs(lm)), seq, w.bcast(rgn, W::ffs(lm)));
                 }
             }
             if (k == kb || !kvalid(knext(k))) break;

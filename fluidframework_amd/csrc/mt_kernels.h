@@ -70,7 +70,6 @@ struct Skel {
     int8_t nchild[HT::N], nlevel[HT::N], nscour[HT::N];
     int32_t hseq[HT::H];
     int16_t hrid[HT::H];
-    int16_t hleaf[HT::H];
     uint8_t hgen[HT::H];
     uint8_t l2s[HT::C];  /* long -> short client id */
     uint16_t s2l[HT::C]; /* short -> long */
@@ -96,14 +95,12 @@ __device__ inline void skel_move(Skel<HT>& k, HT& z, bool in) {
         wave_copy(k.lorder, z.lorder, N), wave_copy(k.lpos, z.lpos, N), wave_copy(k.nparent, z.nparent, N);
         wave_copy(k.nchild, z.nchild, N), wave_copy(k.nlevel, z.nlevel, N), wave_copy(k.nscour, z.nscour, N);
         wave_copy(k.hseq, z.hseq, H), wave_copy(k.hrid, z.hrid, H), wave_copy(k.hgen, z.hgen, H);
-        wave_copy(k.hleaf, z.hleaf, H);
         wave_copy(k.l2s, z.l2s, C), wave_copy(k.s2l, z.s2l, C);
     } else {
         wave_copy((int32_t*)&z.h, (const int32_t*)&k.zh, NH);
         wave_copy(z.lorder, k.lorder, N), wave_copy(z.lpos, k.lpos, N), wave_copy(z.nparent, k.nparent, N);
         wave_copy(z.nchild, k.nchild, N), wave_copy(z.nlevel, k.nlevel, N), wave_copy(z.nscour, k.nscour, N);
         wave_copy(z.hseq, k.hseq, H), wave_copy(z.hrid, k.hrid, H), wave_copy(z.hgen, k.hgen, H);
-        wave_copy(z.hleaf, k.hleaf, H);
         wave_copy(z.l2s, k.l2s, C), wave_copy(z.s2l, k.s2l, C);
     }
 }
@@ -219,7 +216,7 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
         Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
         MT_PROF_ATTACH(r);
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild, r.nlev = sk.nlevel;
-        r.nsc = sk.nscour, r.hsq = sk.hseq, r.hrd = sk.hrid, r.hgn = sk.hgen, r.hlf = sk.hleaf;
+        r.nsc = sk.nscour, r.hsq = sk.hseq, r.hrd = sk.hrid, r.hgn = sk.hgen;
         r.zh = &sk.zh, r.l2s = sk.l2s, r.s2l = sk.s2l;
         r.replay(p);
         r.commit();
@@ -365,7 +362,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     __shared__ __attribute__((aligned(16))) uint8_t lwgen[WCAP];
     __shared__ int32_t lwslot[WCAP];
     __shared__ int32_t lhseq[HL]; /* NARROW: the zamboni heap */
-    __shared__ typename HT::IX lhrid[HL], lhlf[HL];
+    __shared__ typename HT::IX lhrid[HL];
     __shared__ uint8_t lhgen[HL];
     __shared__ int32_t pfcur, pfdone, pfsink; /* the replaying wave's record, its end, the helpers' sink */
 #ifdef MT_PROF
@@ -399,7 +396,6 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         if constexpr (NARROW) {
             wave_copy(lhseq, v.t->hseq, nheap);
             wave_copy(lhrid, v.t->hrid, nheap);
-            wave_copy(lhlf, v.t->hleaf, nheap);
             wave_copy(lhgen, v.t->hgen, nheap);
         }
         if (threadIdx.x == 0) {
@@ -442,7 +438,6 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         if constexpr (NARROW) {
             r.hsq = lhseq;
             r.hrd = lhrid;
-            r.hlf = lhlf;
             r.hgn = lhgen;
         }
         if (MT_PF_HELPERS > 0) r.pfcur = &pfcur;
@@ -470,7 +465,6 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
             int32_t n = zhs.heapN <= HL ? zhs.heapN : HL;
             wave_copy(v.t->hseq, lhseq, n);
             wave_copy(v.t->hrid, lhrid, n);
-            wave_copy(v.t->hleaf, lhlf, n);
             wave_copy(v.t->hgen, lhgen, n);
         }
     }
