@@ -490,7 +490,6 @@ struct Replica {
     int32_t hmax = INT32_MAX;
     int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
     bool runOnly = false;      /* range_op_tiled: find and split only, leaving the run's first / last slot in */
-    bool lastLeafSplit = false; /* the last split_row split its leaf (rows 4..7 moved to a new leaf) */
     int32_t runA = -1, runB = -1; /* runA / runB for remove_run (no visit) */
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
@@ -2656,7 +2655,6 @@ struct Replica {
          * two slots, slot j + 2 starts as row j and slot j + 1 is the new row's) */
         const int32_t g = gapOut && c + 2 < MAXN ? 1 : 0;
         bool willSplit = c + 1 >= MAXN;
-        lastLeafSplit = willSplit;
         {
             MT_PROF_SCOPE(PH_LEAFINS);
             bool mv = l >= j && l < c && l < MAXN;
@@ -2740,13 +2738,11 @@ struct Replica {
         MT_PROF_SCOPE(PH_SPLIT);
         int32_t n = leaf_at(t >> 3), j = t & 7;
         int32_t s0 = n * MAXN + j;
-        lastLeafSplit = false;
         if constexpr (W::N >= 64) {
             if (!dl_on() && !refs_on()) return split_row_par(n, j, off, rsOut, gapOut, pre, preC, ridOut);
         }
         if (z.flags(s0) & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
         bool willSplit = nch[n] + 1 >= MAXN;
-        lastLeafSplit = willSplit;
         int32_t rs = leaf_insert_slot(n, j + 1, true); /* rs starts as a copy of the row */
         if (rs < 0) return -1;
         /* the left part stays at n*8+j unless the leaf split moved children 4..7 (then it sits just
@@ -4533,11 +4529,9 @@ struct Replica {
             int32_t ridLast = z.rid[sg];
             int32_t ridFirst = z.rid[sf];
             int32_t sl = sg; /* the last row's slot, while nothing has moved it */
-            int32_t sl0 = -1; /* the first split's right part */
             if (Pf < start) { /* start falls inside the first row: split it; its right part is first */
                 int32_t rs = -1, rr = -1;
                 if (split_row(tf, start - Pf, &rs, nullptr, nullptr, -1, &rr) < 0 || rs < 0) return;
-                sl0 = rs;
                 sl = -1;
                 if (tf == tg) {
                     ridLast = rr;
@@ -4547,26 +4541,15 @@ struct Replica {
                 }
                 ridFirst = rr;
             }
-            /* the run's ends without looking them up when nothing can have moved them: the first row's slot is the
-             * first split's right part (or the scan's) unless the second split split a leaf; the last row's is the
-             * second split's left part, or the first split's right part when it was also the last */
-            int32_t ka = Pf < start ? sl0 : sf, kb = sl;
             if (Pg + vg > end) { /* end falls inside the last row: split it; its left part keeps the id */
                 if (sl < 0) sl = slot_of(ridLast, -1);
                 if (sl < 0) {
                     fail(E_ASSERT);
                     return;
                 }
-                kb = split_row(kpos(sl / MAXN) * MAXN + (sl & (MAXN - 1)), end - Pg);
-                if (kb < 0) return;
-                if (lastLeafSplit) ka = -1;
+                if (split_row(kpos(sl / MAXN) * MAXN + (sl & (MAXN - 1)), end - Pg) < 0) return;
             }
-            if (ka >= 0 && kb >= 0) {
-                sa = ka;
-                sb = kb;
-            } else {
-                slot_of2(ridFirst, ridLast, &sa, &sb);
-            }
+            slot_of2(ridFirst, ridLast, &sa, &sb);
             if (sa < 0 || sb < 0) {
                 fail(E_ASSERT);
                 return;
@@ -4665,11 +4648,9 @@ struct Replica {
         int32_t ridLast = z.rid[sg];
         int32_t ridFirst = z.rid[sf];
         int32_t sl = sg; /* the last row's slot, while nothing has moved it */
-        int32_t ka = sf;  /* the first row's slot while known (range_op: the same bookkeeping) */
         if (Pf < start) {
             int32_t rs = -1, rr = -1;
             if (split_row(tf, start - Pf, &rs, nullptr, fc >= 0 ? &fr : nullptr, fc, &rr) < 0 || rs < 0) return;
-            ka = rs;
             sl = -1;
             if (tf == tg) {
                 ridLast = rr;
@@ -4679,24 +4660,16 @@ struct Replica {
             }
             ridFirst = rr;
         }
-        int32_t kb = sl;
         if (Pg + vg > end) {
             if (sl < 0) sl = slot_of(ridLast, -1);
             if (sl < 0) {
                 fail(E_ASSERT);
                 return;
             }
-            kb = split_row(kpos(sl / MAXN) * MAXN + (sl & (MAXN - 1)), end - Pg);
-            if (kb < 0) return;
-            if (lastLeafSplit) ka = -1;
+            if (split_row(kpos(sl / MAXN) * MAXN + (sl & (MAXN - 1)), end - Pg) < 0) return;
         }
         int32_t sa, sb;
-        if (ka >= 0 && kb >= 0) {
-            sa = ka;
-            sb = kb;
-        } else {
-            slot_of2(ridFirst, ridLast, &sa, &sb);
-        }
+        slot_of2(ridFirst, ridLast, &sa, &sb);
         if (sa < 0 || sb < 0) {
             fail(E_ASSERT);
             return;
