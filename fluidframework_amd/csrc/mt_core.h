@@ -3577,9 +3577,6 @@ struct Replica {
         }
         int32_t nlen = r.len;
         uint64_t vmask = w.ballot(valid);
-        /* the generation of every row that may be dropped (unlinked or appended), read now: the frees below then
-         * only store (the read overlaps the walk's) */
-        const int32_t rgn = valid && code >= 2 ? (int32_t)z.rgen[r.rid] : 0;
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
         uint64_t _t1 = __builtin_amdgcn_s_memtime();
         if (prof) prof[PH_S1] += _t1 - _t0;
@@ -3772,7 +3769,7 @@ struct Replica {
             uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
             if ((drop >> q) & 1) {
                 int32_t pos = zh->nfreeRid + __builtin_popcountll(drop & below);
-                z.rgen[r.rid] = (uint8_t)(rgn + 1);
+                z.rgen[r.rid]++;
                 d.frid()[pos] = (IX)r.rid;
             }
             int32_t ndrop = __builtin_popcountll(drop);
