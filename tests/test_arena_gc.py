@@ -54,13 +54,15 @@ def test_gpu_compacting_arena_matches_host_core(config, ops, acap):
 
 def _wide_batch():
     import dataclasses
-    w = dataclasses.replace(gen.config4(12000), max_lag=2200)  # a window set of ~3,000 rows: past the narrow 2,048
-    return gen.generate(w, ids=np.arange(4), threads=4)
+    # refSeq lags up to 18,000 of 36,000 ops: both documents outgrow the narrow 2,048 entries (probed on the GPU,
+    # tools/probe_promote.py: lag 10,000 promotes none, 14,000 one of two, 18,000 and up both)
+    w = dataclasses.replace(gen.config4(36000), max_lag=18000)
+    return gen.generate(w, ids=np.arange(2), threads=2)
 
 
 def _tiled_caps():
     from fluidframework_amd.engine import default_caps
-    c = default_caps(12000, config=4)
+    c = default_caps(36000, config=4)
     return c, tuple(c[k] for k in ("ncap", "hcap", "acap", "mcap", "gcap", "ccap"))
 
 
@@ -85,5 +87,5 @@ def test_gpu_tiled_narrow_to_wide_promotion_matches_host_core():
     eng.replay(b)
     err, _ = eng.errors()
     assert (err == 0).all()
-    assert len(eng.promoted()) > 0, "the window set should outgrow the narrow kernel's"
+    assert len(eng.promoted()) == b.ndocs, "every document's window set should outgrow the narrow kernel's"
     assert np.array_equal(eng.digests(), hd)
