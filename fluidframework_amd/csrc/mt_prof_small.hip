@@ -3,6 +3,7 @@
 #include "mt_kernels.h"
 
 int32_t replay_small_w8(mt_engine* e);
+int32_t replay_small_w4(mt_engine* e);
 int32_t replay_small_dl(mt_engine* e);
 int32_t replay_small_load(mt_engine* e);
 
@@ -11,11 +12,12 @@ int32_t replay_small_load(mt_engine* e);
  * is bound by the latency of its dependent accesses and by issue, and occupancy hides more of it than
  * full LDS residency (4 documents per CU) saves (round-2 sweep of 2-8 waves: profiles/r02_occupancy.txt;
  * the sweep's other builds are no longer compiled; the fully LDS-staged form measured 0.6x on config 2,
- * profiles/r03_c2_4096docs_bench_*.json, and is no longer built). */
+ * profiles/r03_c2_4096docs_bench_*.json, and is no longer built). A batch of at most 4 documents per SIMD
+ * runs the 4-wave build (mt_small_w4.hip: no VGPR spills). */
 static int32_t replay_small(mt_engine* e) {
     if (e->fx) return replay_small_dl(e); /* the delta-event build */
     if (e->loads) return replay_small_load(e); /* snapshot-load records */
-    return replay_small_w8(e);
+    return e->waves <= 4 ? replay_small_w4(e) : replay_small_w8(e); /* mt_engine_create picks the occupancy */
 }
 
 const ProfOps* ops_small() {

@@ -43,13 +43,18 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
     e->promote = !(np && np[0] == '1');
     e->caps0 = *caps;
     e->pro.assign((size_t)ndocs, -1);
-    e->waves = 8; /* occupancy of the HBM-resident small-profile kernel (mt_prof_small.hip) */
     e->profile = prof;
     e->ops = prof == 0 ? ops_small() : prof == 1 ? ops_mid() : prof == 3 ? ops_mat() : prof == 4 ? ops_huge() : ops_big();
     if (hipSetDevice(device) != hipSuccess) {
         delete e;
         return MT_E_HIP;
     }
+    /* occupancy of the HBM-resident small-profile kernel (mt_prof_small.hip): 8 waves per SIMD, or 4 (no VGPR
+     * spills) when the batch's documents, one wave each, fit 4 per SIMD (4 SIMDs per CU); MT_SMALL_WAVES overrides */
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
+    e->waves = ndocs <= (int64_t)ncu * 4 * 4 ? 4 : 8;
+    if (const char* sw = getenv("MT_SMALL_WAVES")) e->waves = atoi(sw) == 4 ? 4 : 8;
     int64_t bytes = prof == 0 ? store_layout(e->s0, k, ndocs)
                   : prof == 1 ? store_layout(e->s1, k, ndocs)
                   : prof == 3 ? store_layout(e->s3, k, ndocs)
