@@ -1731,7 +1731,7 @@ struct Replica {
 #define MT_FIND2 1 /* a tiled range op's two ends found in the same passes (tile_find2 / leaf_find2) */
 #endif
 #ifndef MT_WIN_NB
-#define MT_WIN_NB 2 /* wave passes of the window set issued together: the set is ~80-100 rows, so 2 passes cover it in one round trip without the dead issue of 8 (r04e A/B at 256 x 300k: 8.81 -> 9.66M ops/s) */
+#define MT_WIN_NB 1 /* wave passes of the window set issued together: 2 covered the ~80-100 rows in one round trip (r04e, 8 -> 2: 8.81 -> 9.66M ops/s at 256 x 300k); since the set's entries and the leaf headers sit in LDS (round 5), one pass at a time is faster (r05zd at 256 x 1M: 2 -> 1: 15.73 -> 15.88M, 4: 14.91M) */
 #endif
     MT_HD int32_t win_pass(int32_t refSeq, int32_t client) {
         MT_PROF_SCOPE(PH_WIN);
