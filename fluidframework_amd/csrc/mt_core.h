@@ -1197,10 +1197,16 @@ struct Replica {
         r.b4 = ld_bytes4(s);
         return r;
     }
+    /* the byte a row's client / removedClient must equal to be this client's own: a short id (0..253) as is,
+     * LocalClientId (-1) as LOCAL_CLIENT, and anything else (0x7fff: a client the replica has never seen) as 0xFE,
+     * which no short id takes (get_or_add_short hands out at most 254), so such a client owns no row */
+    MT_HD static uint32_t client_byte(int32_t client) {
+        return (uint32_t)client < 0xFEu ? (uint32_t)client : (client == -1 ? (uint32_t)LOCAL_CLIENT : 0xFEu);
+    }
     MT_HD int32_t vis_of(int32_t s, const RowView& r, int32_t refSeq, int32_t client) const {
         if (is_local(client)) return r.rseq == NOREM ? r.len : 0;
         /* the tests of quad_vis_of: short id bytes against the client's byte, one unsigned compare per seq */
-        const uint32_t uc = (uint32_t)(uint8_t)client;
+        const uint32_t uc = client_byte(client);
         const uint32_t ur1 = refSeq >= 0 ? (uint32_t)refSeq + 1u : 0u;
         uint32_t cq = r.b4 & 0xFFu, rcq = (r.b4 >> 8) & 0xFFu, fq = (r.b4 >> 16) & 0xFFu;
         if (!(cq == uc || (uint32_t)r.seq < ur1)) return 0;
@@ -2345,7 +2351,7 @@ struct Replica {
         /* the same tests in fewer instructions: a short id byte equals the client's (LocalClientId -1 is byte 0xFF,
          * LOCAL_CLIENT), and "s != UNASSIGNED_SEQ && s <= refSeq" is one unsigned compare against refSeq + 1 (0 when
          * refSeq < 0): UNASSIGNED_SEQ (-1) and NOREM (INT32_MIN) are above every bound as unsigned values */
-        const uint32_t uc = (uint32_t)(uint8_t)client;
+        const uint32_t uc = client_byte(client);
         const uint32_t ur1 = refSeq >= 0 ? (uint32_t)refSeq + 1u : 0u;
         for (int q = 0; q < 4; q++) {
             uint32_t by = (uint32_t)BY.x[q];

@@ -129,14 +129,15 @@ struct ReplayAux {
 __device__ inline int64_t aux_doc(const ReplayAux& a) { return a.order ? a.order[blockIdx.x] : (int64_t)blockIdx.x; }
 /* the document's replay start / end on the constant-rate clock (s_memrealtime, 100 MHz), kept in its image header
  * (DocHdr.tStart / tEnd: no register stays live for it through the replay; mt_engine_doc_times) */
-template <class HT>
-__device__ inline void doc_stamp(HT* t, int end) {
+/* Stamped into the header copy the replay writes back (the LDS-staged DocHdr where one is staged): a direct HBM store
+ * by lane 0 beside the other lanes' staging copies of the same header could be overwritten by the stale copy. */
+__device__ inline void doc_stamp(DocHdr& h, int end) {
     if (threadIdx.x == 0) {
         int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
         if (end)
-            t->h.tEnd = now;
+            h.tEnd = now;
         else
-            t->h.tStart = now;
+            h.tStart = now;
     }
 }
 
@@ -175,12 +176,12 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
     p.props = props + props_off[d];
     p.kv = kv + kv_off[d];
     Doc<HT> v = st.doc(d);
-    doc_stamp(v.t, 0);
     if constexpr (LDS) {
         __shared__ __attribute__((aligned(16))) HT hot;
         HT* g = v.t;
         copy_image(&hot, g);
         __syncthreads();
+        doc_stamp(hot.h, 0);
         v.t = &hot;
         Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
         MT_PROF_ATTACH(r);
@@ -190,18 +191,21 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
         if (prof && threadIdx.x == 0)
             for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
 #endif
+        doc_stamp(hot.h, 1);
         __syncthreads();
         copy_image(g, &hot);
     } else if constexpr (SKM == 2) {
         __shared__ __attribute__((aligned(16))) SkelLite<HT> sk;
         skel_lite_move(sk, *v.t, true);
         __syncthreads();
+        doc_stamp(sk.zh, 0);
         Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
         MT_PROF_ATTACH(r);
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild;
         r.zh = &sk.zh;
         r.replay(p);
         r.commit();
+        doc_stamp(sk.zh, 1);
         __syncthreads();
         skel_lite_move(sk, *v.t, false);
 #ifdef MT_PROF
@@ -213,6 +217,7 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
         __shared__ __attribute__((aligned(16))) Skel<HT> sk;
         skel_move(sk, *v.t, true);
         __syncthreads();
+        doc_stamp(sk.zh, 0);
         Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
         MT_PROF_ATTACH(r);
         r.lo = sk.lorder, r.lp = sk.lpos, r.npar = sk.nparent, r.nch = sk.nchild, r.nlev = sk.nlevel;
@@ -220,6 +225,7 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
         r.zh = &sk.zh, r.l2s = sk.l2s, r.s2l = sk.s2l;
         r.replay(p);
         r.commit();
+        doc_stamp(sk.zh, 1);
         __syncthreads();
         skel_move(sk, *v.t, false);
 #ifdef MT_PROF
@@ -227,16 +233,17 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
             for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
 #endif
     } else {
+        doc_stamp(v.t->h, 0);
         Replica<WaveGPU, HT, DL, LOAD> r(v, WaveGPU());
         MT_PROF_ATTACH(r);
         r.replay(p);
         r.commit();
+        doc_stamp(v.t->h, 1);
 #ifdef MT_PROF
         if (prof && threadIdx.x == 0)
             for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
 #endif
     }
-    doc_stamp(v.t, 1);
 }
 
 /* Config 4 (large documents, the tiled profile): one workgroup per document, which has the CU's LDS to
@@ -374,7 +381,6 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     uint64_t* prof = aux.prof;
     (void)prof;
     Doc<HT> v = st.doc(d);
-    if (threadIdx.x < WG) doc_stamp(v.t, 0);
     auto& tl = v.t->tl;
     const bool replayer = threadIdx.x < WG;
     /* what the staged arrays cannot hold: nothing is staged, the replica latches E_CAPACITY */
@@ -398,12 +404,13 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
             wave_copy(lhrid, v.t->hrid, nheap);
             wave_copy(lhgen, v.t->hgen, nheap);
         }
-        if (threadIdx.x == 0) {
-            pfcur = 0;
-            pfdone = 0;
-        }
+    }
+    if (threadIdx.x == 0) { /* every path: helper waves read these after the barrier */
+        pfcur = 0;
+        pfdone = fits ? 0 : 1;
     }
     __syncthreads();
+    if (replayer && fits) doc_stamp(zhs, 0);
     Pools p;
     p.ops = ops + op_off[d];
     p.nops = op_off[d + 1] - op_off[d];
@@ -413,10 +420,11 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     if (!replayer) {
         tiled_prefetch<HT>(v, p.ops, p.nops, &pfcur, &pfdone, lcord, lcst, lccnt, &pfsink);
     } else if (!fits) {
+        doc_stamp(v.t->h, 0);
         R r(v, WaveGPU());
         r.fail(E_CAPACITY);
         r.commit();
-        if (threadIdx.x == 0) *(volatile int32_t*)&pfdone = 1;
+        doc_stamp(v.t->h, 1);
     } else {
         R r(v, WaveGPU());
         MT_PROF_ATTACH(r);
@@ -443,6 +451,7 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
         if (MT_PF_HELPERS > 0) r.pfcur = &pfcur;
         r.replay(p);
         r.commit();
+        doc_stamp(zhs, 1);
         if (threadIdx.x == 0) *(volatile int32_t*)&pfdone = 1;
 #ifdef MT_PROF
         if (prof && threadIdx.x == 0)
@@ -468,7 +477,6 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
             wave_copy(v.t->hgen, lhgen, n);
         }
     }
-    if (replayer) doc_stamp(v.t, 1);
 }
 
 /* K5: per-doc digest of the canonical dump */

@@ -4,7 +4,10 @@
 static int32_t replay_huge(mt_engine* e) {
     constexpr int block = WG * (1 + MT_PF_HELPERS); /* the replaying wave + its prefetch helpers */
     if (e->fx) return launch_replay<HotHuge>(e, k_replay_tiled<HotHuge, true>, block); /* delta events */
-    if (e->wide) return launch_replay<HotHuge>(e, k_replay_tiled<HotHuge, false, false>, block);
+    /* the wide variant: asked for, or a replay that promotion cannot redo from the staged log (an incremental
+     * batch on top of earlier ones, or promotion off), where the narrow kernel's E_CAPACITY would be final */
+    if (e->wide || !e->fresh || !e->promote)
+        return launch_replay<HotHuge>(e, k_replay_tiled<HotHuge, false, false>, block);
     /* the heap in LDS; documents it cannot hold are promoted to the wide variant (mt_replay.hip promote) */
     return launch_replay<HotHuge>(e, k_replay_tiled<HotHuge, false, true>, block);
 }

@@ -505,6 +505,22 @@ int32_t mt_engine_set_order(mt_engine* e, const int32_t* order) {
     return MT_OK;
 }
 
+int32_t mt_engine_set_variant(mt_engine* e, int32_t key, int32_t value) {
+    if (!e) return MT_E_ARG;
+    switch (key) {
+    case MT_VAR_SMALL_WAVES:
+        if (value != 4 && value != 8) return MT_E_ARG;
+        e->waves = value;
+        return MT_OK;
+    case MT_VAR_TILED_WIDE:
+        if (value != 0 && value != 1) return MT_E_ARG;
+        e->wide = value == 1;
+        return MT_OK;
+    default:
+        return MT_E_ARG;
+    }
+}
+
 int32_t mt_engine_work(mt_engine* e, int64_t* out3) {
     if (!e || !out3) return MT_E_ARG;
     int32_t rc = read_hdr(e, nullptr, nullptr, nullptr, out3);

@@ -41,6 +41,7 @@ class _Caps(ctypes.Structure):
 
 
 _LIB = None
+MT_VAR_SMALL_WAVES, MT_VAR_TILED_WIDE = 1, 2  # include/mt_engine.h
 
 
 def lib() -> ctypes.CDLL:
@@ -67,6 +68,7 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_work.argtypes = [vp, vp]
         L.mt_engine_doc_times.argtypes = [vp, vp]
         L.mt_engine_set_order.argtypes = [vp, vp]
+        L.mt_engine_set_variant.argtypes = [vp, i32, i32]
         L.mt_engine_sync.argtypes = [vp]
         L.mt_engine_promoted.argtypes = [vp, vp, i64]
         L.mt_engine_promoted.restype = i64
@@ -130,7 +132,9 @@ class Engine:
     references per document (MT_OP_REF records); caps["pcap"] > 0 gives every document a PermutationVector
     HandleTable of pcap handles (getAllocatedHandle records, MT_OP_NOOP | MT_OPF_LOCAL)."""
 
-    def __init__(self, ndocs: int, device: int = 0, **caps):
+    def __init__(self, ndocs: int, device: int = 0, waves: Optional[int] = None, wide: Optional[bool] = None,
+                 **caps):
+        """`waves` (4 | 8) and `wide` pick a kernel build (mt_engine_set_variant); None keeps the engine's choice."""
         c = default_caps(0)
         c.update(caps)
         self.L = lib()
@@ -141,6 +145,14 @@ class Engine:
             raise EngineError(f"mt_engine_create failed: status {rc}")
         self.h = h.value
         self.ndocs = ndocs
+        if waves is not None:
+            self.set_variant(MT_VAR_SMALL_WAVES, waves)
+        if wide is not None:
+            self.set_variant(MT_VAR_TILED_WIDE, int(bool(wide)))
+
+    def set_variant(self, key: int, value: int):
+        """Kernel build selection (include/mt_engine.h mt_engine_set_variant); results do not depend on it."""
+        self._check(self.L.mt_engine_set_variant(self.h, key, value), "set_variant")
 
     def close(self):
         if getattr(self, "h", None):

@@ -102,6 +102,14 @@ int32_t mt_engine_doc_times(mt_engine* e, int64_t* out2);
  * restores document order). The GPU dispatches workgroups in index order as slots free up, so the documents in
  * decreasing order of expected cost make a longest-first list schedule. No effect on results. */
 int32_t mt_engine_set_order(mt_engine* e, const int32_t* order);
+/* Kernel build selection (no effect on results; no reference counterpart — the reference has one code path):
+ *   MT_VAR_SMALL_WAVES (4 | 8): occupancy build of the config-2/3 replay kernel (default: 4 when the batch's
+ *     documents fit 4 per SIMD, else 8; the MT_SMALL_WAVES environment variable sets it at create);
+ *   MT_VAR_TILED_WIDE (0 | 1): the config-4 (tiled) kernel with the zamboni heap in HBM and the full window set
+ *     (default 0: the narrow LDS-heap build, which promotes documents it cannot hold to the wide one).
+ * Takes effect at the next mt_engine_run. */
+enum { MT_VAR_SMALL_WAVES = 1, MT_VAR_TILED_WIDE = 2 };
+int32_t mt_engine_set_variant(mt_engine* e, int32_t key, int32_t value);
 
 /* Per-doc latched error code (MT_E_*) and index of the event that raised it (-1 if none). */
 int32_t mt_engine_errors(mt_engine* e, int32_t* err, int32_t* err_op);

@@ -89,3 +89,33 @@ def test_gpu_tiled_narrow_to_wide_promotion_matches_host_core():
     assert (err == 0).all()
     assert len(eng.promoted()) == b.ndocs, "every document's window set should outgrow the narrow kernel's"
     assert np.array_equal(eng.digests(), hd)
+
+
+@pytest.mark.gpu
+def test_gpu_tiled_incremental_batch_crossing_narrow_capacity():
+    """A replay on top of earlier batches cannot be redone from the staged log, so promotion cannot rescue it: the
+    engine runs such a batch on the wide tiled kernel (mt_prof_huge.hip). The first batch (600 events per document)
+    fits the narrow kernel; the second takes every document's window set past its 2,048 entries. Both documents
+    must replay to the end, unpromoted, to the host core's digests of the whole log."""
+    from fluidframework_amd import oplog as ol
+    from fluidframework_amd.engine import Engine
+    b = _wide_batch()
+    kw, tup = _tiled_caps()
+    hd, he, _ = core_host.replay_batch(b, tup)
+    assert (he == 0).all()
+    cut = 600
+    head, tail = [], []
+    for d in range(b.ndocs):
+        ops, text, props, kv = b.doc_arrays(d)
+        head.append((ops[:cut], text, props, kv))
+        tail.append((ops[cut:], text, props, kv))
+    eng = Engine(b.ndocs, **kw)
+    eng.start_collab(b.local_long_id)
+    eng.replay(ol.Batch.from_arrays(head, b.local_long_id))
+    err, _ = eng.errors()
+    assert (err == 0).all() and len(eng.promoted()) == 0
+    eng.replay(ol.Batch.from_arrays(tail, b.local_long_id))
+    err, err_op = eng.errors()
+    assert (err == 0).all(), (err, err_op)
+    assert len(eng.promoted()) == 0
+    assert np.array_equal(eng.digests(), hd)

@@ -101,16 +101,40 @@ def test_stored_logs_replay_to_reference_dumps(name):
         assert c.dump() == z["keep_dumps"][off[d]: off[d + 1]].tobytes(), f"doc {d}"
 
 
+def kernel_variants(name):
+    """The replay kernel builds a fixture's profile has (include/mt_engine.h mt_engine_set_variant): every one runs
+    each fixture, whichever the engine would pick for the fixture's batch size. Config-2/3 profile: the 4-wave build
+    (no spills) and the 8-wave build the config-3 bench runs; tiled profile (c4_large): the narrow LDS-heap kernel
+    and the wide one; the other profiles have one build."""
+    _, w = load(name)
+    c = caps_for(w)
+    if c["ncap"] <= 192 and w.mode != gen.MTG_MATRIX:
+        return [dict(waves=4), dict(waves=8)]
+    if c["ncap"] > 16384:
+        return [dict(wide=False), dict(wide=True)]
+    return [dict()]
+
+
+VARIANT_CASES = [(n, v) for n in NAMES for v in kernel_variants(n)]
+
+
+def variant_id(case):
+    n, v = case
+    return n + "".join(f"-{k}{int(x)}" for k, x in v.items())
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", NAMES)
-def test_gpu_engine_matches_reference(name):
+@pytest.mark.parametrize("name,variant", VARIANT_CASES, ids=[variant_id(c) for c in VARIANT_CASES])
+def test_gpu_engine_matches_reference(name, variant):
     from fluidframework_amd.engine import Engine
     z, w, b = regenerate(name)
-    eng = Engine(b.ndocs, **caps_for(w))
+    eng = Engine(b.ndocs, **variant, **caps_for(w))
     eng.start_collab(b.local_long_id)
     eng.replay(b)
     err, err_op = eng.errors()
     assert (err == 0).all(), (err[err != 0][:8], err_op[err != 0][:8])
+    if variant.get("wide"):
+        assert len(eng.promoted()) == 0
     gdig = eng.digests()
     bad = np.nonzero(gdig != z["digests"])[0]
     assert len(bad) == 0, f"HIP engine differs from the reference on docs {bad[:8]}"

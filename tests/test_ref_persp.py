@@ -73,12 +73,13 @@ def test_host_core_answers_match_reference_where_the_engine_answers(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])  # both config-2/3 kernel builds (mt_engine_set_variant)
 @pytest.mark.parametrize("name", list(pl.SETS))
-def test_gpu_answers_match_reference_or_refuse(name):
+def test_gpu_answers_match_reference_or_refuse(name, waves):
     from fluidframework_amd.engine import Engine, EngineError, SegRef
     z, b = load(name)
     c = pl.CAPS[name]
-    eng = Engine(b.ndocs, ncap=c[0], hcap=c[1], acap=c[2], mcap=c[3], gcap=c[4], ccap=c[5])
+    eng = Engine(b.ndocs, waves=waves, ncap=c[0], hcap=c[1], acap=c[2], mcap=c[3], gcap=c[4], ccap=c[5])
     eng.start_collab(b.local_long_id)
     eng.replay(b)
     assert (eng.errors()[0] == 0).all()

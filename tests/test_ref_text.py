@@ -78,11 +78,12 @@ def test_host_core_get_text_matches_reference(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])  # both config-2/3 kernel builds (mt_engine_set_variant)
 @pytest.mark.parametrize("name", NAMES)
-def test_gpu_get_text_matches_reference(name):
+def test_gpu_get_text_matches_reference(name, waves):
     from fluidframework_amd.engine import Engine
     z, w, b = load(name)
-    eng = Engine(b.ndocs, **caps_for(w))
+    eng = Engine(b.ndocs, waves=waves, **caps_for(w))
     eng.start_collab(b.local_long_id)
     eng.replay(b)
     err, _ = eng.errors()

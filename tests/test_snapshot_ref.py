@@ -191,8 +191,9 @@ def test_body_window_set_shape():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])  # the prefix replay on both config-2/3 kernel builds
 @pytest.mark.parametrize("name", [n for n in SETS if n != "c4_large"])
-def test_gpu_snapshot_emit_and_load_match_reference(name):
+def test_gpu_snapshot_emit_and_load_match_reference(name, waves):
     """Both halves on the HIP engine: the prefix replays on the GPU and its dumps are emitted; the
     loaded replicas (load records + tail) replay on the GPU as one batch. (c4_large, two 300k-message
     documents, runs on the CPU tier only: its load records alone are minutes of one wave's work.)"""
@@ -201,7 +202,7 @@ def test_gpu_snapshot_emit_and_load_match_reference(name):
     if not has_snapshots(z):
         pytest.skip("fixture predates snapshots")
     cuts = [int(x) for x in z["snap_cut"]]
-    pre = Engine(b.ndocs, **caps)
+    pre = Engine(b.ndocs, waves=waves, **caps)
     pre.start_collab(b.local_long_id)
     pre.replay(ol.Batch.from_arrays([prefix_arrays(b, d, cuts[d]) for d in range(b.ndocs)], b.local_long_id))
     err, _ = pre.errors()

@@ -134,13 +134,14 @@ def test_unsupported_wire_ops_raise():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])  # both config-2/3 kernel builds (mt_engine_set_variant)
 @pytest.mark.parametrize("name", ["c3_lagged", "c5_perm"])
-def test_gpu_wire_ingestion_matches_reference(name):
+def test_gpu_wire_ingestion_matches_reference(name, waves):
     from fluidframework_amd.engine import Engine
     z, w, b = regenerate(name)
     it = gen.generator_interner()
     per = [_arrays(rebuild(b, d, it)[0]) for d in range(b.ndocs)]
-    eng = Engine(b.ndocs, **caps_for(w))
+    eng = Engine(b.ndocs, waves=waves, **caps_for(w))
     eng.start_collab(b.local_long_id)
     eng.replay(ol.Batch.from_arrays(per, b.local_long_id))
     err, _ = eng.errors()
