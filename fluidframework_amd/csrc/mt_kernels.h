@@ -125,8 +125,12 @@ __device__ inline void skel_lite_move(SkelLite<HT>& k, HT& z, bool in) {
 struct ReplayAux {
     uint64_t* prof;
     const int32_t* order;
+    int64_t doc0; /* a launch over documents [doc0, doc0 + grid): the chunked submit (mt_engine_submit_run) */
 };
-__device__ inline int64_t aux_doc(const ReplayAux& a) { return a.order ? a.order[blockIdx.x] : (int64_t)blockIdx.x; }
+__device__ inline int64_t aux_doc(const ReplayAux& a) {
+    const int64_t b = a.doc0 + (int64_t)blockIdx.x;
+    return a.order ? a.order[b] : b;
+}
 /* the document's replay start / end on the constant-rate clock (s_memrealtime, 100 MHz), kept in its image header
  * (DocHdr.tStart / tEnd: no register stays live for it through the replay; mt_engine_doc_times) */
 /* Stamped into the header copy the replay writes back (the LDS-staged DocHdr where one is staged): a direct HBM store
@@ -806,6 +810,22 @@ struct mt_engine {
         }
     };
     std::vector<Persp> persp_staged, persp_applied;
+    /* the replay launch's document range and stream (mt_engine_run: all documents on `stream`; the chunked
+     * mt_engine_submit_run: one range per chunk, alternating between `stream` and `stream2`) */
+    int64_t run_d0 = 0, run_n = -1;
+    int64_t chunk = 0; /* documents per chunk of mt_engine_submit_run (0: automatic) */
+    hipStream_t run_stream = nullptr;
+    /* mt_engine_submit_run: the copy stream, the second compute stream, and pinned staging buffers for pageable
+     * sources (each with the event of the last copy out of it) */
+    hipStream_t cstream = nullptr, stream2 = nullptr;
+    hipEvent_t evs = nullptr, evc = nullptr, ev2 = nullptr;
+    struct Pin {
+        void* p = nullptr;
+        hipEvent_t ev = nullptr;
+    };
+    static constexpr int NPIN = 3;
+    Pin pin[NPIN];
+    int pin_i = 0;
 };
 
 static inline int32_t hip_fail(mt_engine* e, hipError_t st, const char* what) {
@@ -863,11 +883,13 @@ static inline Store<HT>& store_of(mt_engine* e) {
 /* one replay kernel over the staged batch (a document per workgroup) */
 template <class HT, class K>
 static inline int32_t launch_replay(mt_engine* e, K kern, int block = WG) {
-    hipLaunchKernelGGL(kern, docs_grid(e->ndocs), dim3(block), 0, e->stream, store_of<HT>(e), e->ndocs,
-                       (const mt_op_rec*)e->ops_buf.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
+    const int64_t n = e->run_n < 0 ? e->ndocs : e->run_n;
+    if (n <= 0) return MT_OK;
+    hipLaunchKernelGGL(kern, docs_grid(n), dim3(block), 0, e->run_stream ? e->run_stream : e->stream, store_of<HT>(e),
+                       e->ndocs, (const mt_op_rec*)e->ops_buf.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
                        (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p, (const int64_t*)e->props_off.p,
                        (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p,
-                       ReplayAux{(uint64_t*)e->prof.p, (const int32_t*)e->order.p});
+                       ReplayAux{(uint64_t*)e->prof.p, (const int32_t*)e->order.p, e->run_d0});
     return launch_check(e, "k_replay");
 }
 

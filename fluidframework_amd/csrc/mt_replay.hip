@@ -22,6 +22,193 @@ static int32_t ensure(mt_engine* e, DevBuf& b, size_t bytes) {
 
 static int32_t launch_init(mt_engine* e) { return e->ops->init(e); }
 
+/* ---- staging the op logs ------------------------------------------------------------------------ */
+struct SubmitArgs {
+    const mt_op_rec* ops;
+    const int64_t* op_off;
+    const uint16_t* text;
+    int64_t text_units;
+    const int64_t* text_off;
+    const mt_props_rec* props;
+    int64_t nprops;
+    const int64_t* props_off;
+    const mt_kv* kv;
+    int64_t nkv;
+    const int64_t* kv_off;
+};
+
+/* host-side shape checks before the kernel trusts any offset */
+static bool offsets_ok(const SubmitArgs& a, int64_t nd) {
+    if (!a.op_off || !a.text_off || !a.props_off || !a.kv_off || a.text_units < 0 || a.nprops < 0 || a.nkv < 0)
+        return false;
+    if (a.op_off[0] < 0) return false;
+    for (int64_t d = 0; d < nd; d++) {
+        if (a.op_off[d] > a.op_off[d + 1] || a.text_off[d] < 0 || a.text_off[d] > a.text_units || a.props_off[d] < 0 ||
+            a.props_off[d] > a.nprops || a.kv_off[d] < 0 || a.kv_off[d] > a.nkv)
+            return false;
+    }
+    return !a.op_off[nd] || a.ops;
+}
+
+/* every pool reference of every event of documents [d0, d1) in bounds before the kernel dereferences it (in parallel
+ * on the host: up to 16 threads, one contiguous range each); also each document's perspective floors
+ * (mt_kernels.h persp_refused), whether it holds snapshot-load records, and (text_end) the end of the text the
+ * documents reference */
+static bool check_docs(const SubmitArgs& a, int64_t d0, int64_t d1, mt_engine::Persp* persp, char* loads,
+                       int64_t* text_end) {
+    int64_t te = 0;
+    for (int64_t d = d0; d < d1; d++) {
+        mt_engine::Persp& pp = persp[d];
+        const int64_t to = a.text_off[d];
+        for (int64_t i = a.op_off[d]; i < a.op_off[d + 1]; i++) {
+            const mt_op_rec& o = a.ops[i];
+            int kind = o.kind & MT_OP_KIND_MASK;
+            if (!(o.kind & MT_OPF_LOCAL)) { /* perspective floors (mt_kernels.h persp_refused) */
+                if (kind == MT_OP_RELOAD || kind == MT_OP_COLLAB || kind == MT_OP_APPEND) {
+                    if (!(o.kind & MT_OPF_TREE)) loads[d] = 1; /* a snapshot load: the full build */
+                    if (o.seq > pp.all) pp.all = o.seq;
+                } else if (kind != MT_OP_NOOP && o.client != MT_CLIENT_LOCAL) {
+                    pp.note(o.client, o.ref_seq);
+                }
+            }
+            int64_t end = 0;
+            if (kind == MT_OP_INSERT && (o.seg_kind & 0x7F) == MT_SEG_TEXT) end = to + (int64_t)o.text_off + o.text_len;
+            if (kind == MT_OP_NOOP && (o.kind & MT_OPF_LOCAL) && o.seg_kind == MT_NOOP_HTLOAD)
+                end = to + (int64_t)o.text_off + o.text_len;
+            if (o.seg_kind & MT_SEG_RELPOS) end = std::max(end, to + (int64_t)o.text_off + o.text_len + MT_RELPOS_UNITS);
+            /* snapshot-load records carry the segment length in pos2 (mt_oplog.h) */
+            if ((kind == MT_OP_RELOAD || kind == MT_OP_APPEND) && o.seg_kind == MT_SEG_TEXT) {
+                if (o.pos2 < 0) return false;
+                end = std::max(end, to + (int64_t)o.text_off + o.pos2);
+            }
+            if (end > a.text_units) return false;
+            te = std::max(te, end);
+            if (o.props) {
+                if (a.props_off[d] + (int64_t)o.props > a.nprops) return false;
+                const mt_props_rec& pr = a.props[a.props_off[d] + o.props - 1];
+                if (a.kv_off[d] + (int64_t)pr.kv_off + pr.nkv > a.nkv) return false;
+            }
+        }
+    }
+    if (text_end) *text_end = te;
+    return true;
+}
+
+static int host_threads() {
+    unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::min<unsigned>(16, std::max<unsigned>(1, hc));
+}
+
+static bool check_range(const SubmitArgs& a, int64_t d0, int64_t d1, mt_engine::Persp* persp, char* loads,
+                        int64_t* text_end) {
+    int64_t nops = a.op_off[d1] - a.op_off[d0];
+    int nth = nops > (1 << 20) ? host_threads() : 1;
+    if (nth <= 1 || d1 - d0 < 2) return check_docs(a, d0, d1, persp, loads, text_end);
+    nth = (int)std::min<int64_t>(nth, d1 - d0);
+    std::vector<std::thread> th;
+    std::vector<char> ok((size_t)nth, 1);
+    std::vector<int64_t> te((size_t)nth, 0);
+    for (int t = 0; t < nth; t++)
+        th.emplace_back([&, t] {
+            ok[(size_t)t] = check_docs(a, d0 + (d1 - d0) * t / nth, d0 + (d1 - d0) * (t + 1) / nth, persp, loads,
+                                       &te[(size_t)t]);
+        });
+    for (auto& x : th) x.join();
+    for (char c : ok)
+        if (!c) return false;
+    if (text_end) *text_end = *std::max_element(te.begin(), te.end());
+    return true;
+}
+
+static int32_t ensure_staging(mt_engine* e, const SubmitArgs& a) {
+    int64_t nd = e->ndocs, nops = a.op_off[nd];
+    int32_t rc;
+    if ((rc = ensure(e, e->ops_buf, sizeof(mt_op_rec) * nops))) return rc;
+    if ((rc = ensure(e, e->op_off, sizeof(int64_t) * (nd + 1)))) return rc;
+    if ((rc = ensure(e, e->text, 2 * a.text_units))) return rc;
+    if ((rc = ensure(e, e->text_off, sizeof(int64_t) * (nd + 1)))) return rc;
+    if ((rc = ensure(e, e->props, sizeof(mt_props_rec) * a.nprops))) return rc;
+    if ((rc = ensure(e, e->props_off, sizeof(int64_t) * (nd + 1)))) return rc;
+    if ((rc = ensure(e, e->kv, sizeof(mt_kv) * a.nkv))) return rc;
+    return ensure(e, e->kv_off, sizeof(int64_t) * (nd + 1));
+}
+
+/* the offsets and the property pools (small next to the records and the text) */
+static int32_t copy_small(mt_engine* e, const SubmitArgs& a, hipStream_t s) {
+    int64_t nd = e->ndocs;
+    HIPCHK(e, hipMemcpyAsync(e->op_off.p, a.op_off, sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice, s));
+    HIPCHK(e, hipMemcpyAsync(e->text_off.p, a.text_off, sizeof(int64_t) * nd, hipMemcpyHostToDevice, s));
+    if (a.nprops) HIPCHK(e, hipMemcpyAsync(e->props.p, a.props, sizeof(mt_props_rec) * a.nprops, hipMemcpyHostToDevice, s));
+    HIPCHK(e, hipMemcpyAsync(e->props_off.p, a.props_off, sizeof(int64_t) * nd, hipMemcpyHostToDevice, s));
+    if (a.nkv) HIPCHK(e, hipMemcpyAsync(e->kv.p, a.kv, sizeof(mt_kv) * a.nkv, hipMemcpyHostToDevice, s));
+    HIPCHK(e, hipMemcpyAsync(e->kv_off.p, a.kv_off, sizeof(int64_t) * nd, hipMemcpyHostToDevice, s));
+    return MT_OK;
+}
+
+/* the host copies of a staged batch's offsets, floors and load flag */
+static void keep_staged(mt_engine* e, const SubmitArgs& a, std::vector<mt_engine::Persp>& persp,
+                        const std::vector<char>& loads) {
+    int64_t nd = e->ndocs;
+    e->h_op_off.assign(a.op_off, a.op_off + nd + 1);
+    e->h_text_off.assign(a.text_off, a.text_off + nd);
+    e->h_props_off.assign(a.props_off, a.props_off + nd);
+    e->h_kv_off.assign(a.kv_off, a.kv_off + nd);
+    e->persp_staged.swap(persp);
+    e->loads = std::find(loads.begin(), loads.end(), 1) != loads.end();
+    e->staged = true;
+}
+
+static bool host_pinned(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    hipError_t st = hipPointerGetAttributes(&at, p);
+    if (st != hipSuccess) {
+        (void)hipGetLastError(); /* pageable memory is an error here, not a sticky one */
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+/* n bytes from host `src` to device `dst` on the copy stream: straight from pinned memory, or through the engine's
+ * pinned staging buffers (host threads fill one while the DMA engine drains the others) */
+static constexpr size_t PIN_BYTES = (size_t)128 << 20;
+static int32_t stage_h2d(mt_engine* e, void* dst, const void* src, size_t n, bool pinned) {
+    if (!n) return MT_OK;
+    if (pinned) {
+        HIPCHK(e, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, e->cstream));
+        return MT_OK;
+    }
+    uint8_t* d = (uint8_t*)dst;
+    const uint8_t* s = (const uint8_t*)src;
+    while (n) {
+        mt_engine::Pin& b = e->pin[e->pin_i];
+        e->pin_i = (e->pin_i + 1) % mt_engine::NPIN;
+        if (!b.p) {
+            HIPCHK(e, hipHostMalloc(&b.p, PIN_BYTES, hipHostMallocDefault));
+            HIPCHK(e, hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+        } else {
+            HIPCHK(e, hipEventSynchronize(b.ev)); /* its previous copy has left it */
+        }
+        size_t m = std::min(n, PIN_BYTES);
+        int nth = m >= ((size_t)8 << 20) ? std::min(8, host_threads()) : 1;
+        if (nth <= 1) {
+            memcpy(b.p, s, m);
+        } else {
+            std::vector<std::thread> th;
+            for (int t = 0; t < nth; t++)
+                th.emplace_back([&, t] {
+                    size_t lo = (m * t / nth) & ~(size_t)63, hi = t + 1 == nth ? m : (m * (t + 1) / nth) & ~(size_t)63;
+                    memcpy((uint8_t*)b.p + lo, s + lo, hi - lo);
+                });
+            for (auto& x : th) x.join();
+        }
+        HIPCHK(e, hipMemcpyAsync(d, b.p, m, hipMemcpyHostToDevice, e->cstream));
+        HIPCHK(e, hipEventRecord(b.ev, e->cstream));
+        d += m, s += m, n -= m;
+    }
+    return MT_OK;
+}
+
 extern "C" {
 
 int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_engine** out) {
@@ -100,6 +287,19 @@ void mt_engine_destroy(mt_engine* e) {
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->cstream) {
+        (void)hipStreamSynchronize(e->cstream);
+        (void)hipStreamSynchronize(e->stream2);
+        (void)hipStreamDestroy(e->cstream);
+        (void)hipStreamDestroy(e->stream2);
+        (void)hipEventDestroy(e->evs);
+        (void)hipEventDestroy(e->evc);
+        (void)hipEventDestroy(e->ev2);
+    }
+    for (auto& b : e->pin) {
+        if (b.p) (void)hipHostFree(b.p);
+        if (b.ev) (void)hipEventDestroy(b.ev);
+    }
     delete e;
 }
 
@@ -147,95 +347,36 @@ int32_t mt_engine_start_collab_docs(mt_engine* e, const int32_t* local_long_ids,
 int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_off, const uint16_t* text,
                          int64_t text_units, const int64_t* text_off, const mt_props_rec* props, int64_t nprops,
                          const int64_t* props_off, const mt_kv* kv, int64_t nkv, const int64_t* kv_off) {
-    if (!e || !op_off || !text_off || !props_off || !kv_off) return MT_E_ARG;
+    if (!e) return MT_E_ARG;
+    const SubmitArgs a{ops, op_off, text, text_units, text_off, props, nprops, props_off, kv, nkv, kv_off};
+    if (!offsets_ok(a, e->ndocs)) return MT_E_ARG;
     int64_t nd = e->ndocs;
     int64_t nops = op_off[nd];
-    for (int64_t d = 0; d < nd; d++) {
-        /* host-side shape checks before the kernel trusts any offset */
-        if (op_off[d] < 0 || op_off[d] > op_off[d + 1] || text_off[d] < 0 || text_off[d] > text_units ||
-            props_off[d] < 0 || props_off[d] > nprops || kv_off[d] < 0 || kv_off[d] > nkv)
-            return MT_E_ARG;
-    }
-    /* every pool reference of every event must be in bounds before the kernel dereferences it: the
-     * documents are checked in parallel on the host (up to 16 threads, one contiguous range each) */
     std::vector<mt_engine::Persp> persp((size_t)nd);
     std::vector<char> loads((size_t)nd, 0);
-    auto check = [&](int64_t d0, int64_t d1) -> bool {
-        for (int64_t d = d0; d < d1; d++) {
-            mt_engine::Persp& pp = persp[(size_t)d];
-            for (int64_t i = op_off[d]; i < op_off[d + 1]; i++) {
-                const mt_op_rec& o = ops[i];
-                int kind = o.kind & MT_OP_KIND_MASK;
-                if (!(o.kind & MT_OPF_LOCAL)) { /* perspective floors (mt_kernels.h persp_refused) */
-                    if (kind == MT_OP_RELOAD || kind == MT_OP_COLLAB || kind == MT_OP_APPEND) {
-                        if (!(o.kind & MT_OPF_TREE)) loads[(size_t)d] = 1; /* a snapshot load: the full build */
-                        if (o.seq > pp.all) pp.all = o.seq;
-                    } else if (kind != MT_OP_NOOP && o.client != MT_CLIENT_LOCAL) {
-                        pp.note(o.client, o.ref_seq);
-                    }
-                }
-                if (kind == MT_OP_INSERT && (o.seg_kind & 0x7F) == MT_SEG_TEXT &&
-                    text_off[d] + (int64_t)o.text_off + o.text_len > text_units)
-                    return false;
-                if (kind == MT_OP_NOOP && (o.kind & MT_OPF_LOCAL) && o.seg_kind == MT_NOOP_HTLOAD &&
-                    text_off[d] + (int64_t)o.text_off + o.text_len > text_units)
-                    return false;
-                if ((o.seg_kind & MT_SEG_RELPOS) &&
-                    text_off[d] + (int64_t)o.text_off + o.text_len + MT_RELPOS_UNITS > text_units)
-                    return false;
-                /* snapshot-load records carry the segment length in pos2 (mt_oplog.h) */
-                if ((kind == MT_OP_RELOAD || kind == MT_OP_APPEND) && o.seg_kind == MT_SEG_TEXT &&
-                    (o.pos2 < 0 || text_off[d] + (int64_t)o.text_off + o.pos2 > text_units))
-                    return false;
-                if (o.props) {
-                    if (props_off[d] + (int64_t)o.props > nprops) return false;
-                    const mt_props_rec& pr = props[props_off[d] + o.props - 1];
-                    if (kv_off[d] + (int64_t)pr.kv_off + pr.nkv > nkv) return false;
-                }
-            }
-        }
-        return true;
-    };
-    int nth = nops > (1 << 20) ? (int)std::min<int64_t>(16, std::max<unsigned>(1, std::thread::hardware_concurrency())) : 1;
-    if (nth <= 1) {
-        if (!check(0, nd)) return MT_E_ARG;
-    } else {
-        std::vector<std::thread> th;
-        std::vector<char> ok((size_t)nth, 1);
-        for (int t = 0; t < nth; t++)
-            th.emplace_back([&, t] { ok[(size_t)t] = check(nd * t / nth, nd * (t + 1) / nth); });
-        for (auto& x : th) x.join();
-        for (char c : ok)
-            if (!c) return MT_E_ARG;
-    }
+    if (!check_range(a, 0, nd, persp.data(), loads.data(), nullptr)) return MT_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc;
-    if ((rc = ensure(e, e->ops_buf, sizeof(mt_op_rec) * nops))) return rc;
-    if ((rc = ensure(e, e->op_off, sizeof(int64_t) * (nd + 1)))) return rc;
-    if ((rc = ensure(e, e->text, 2 * text_units))) return rc;
-    if ((rc = ensure(e, e->text_off, sizeof(int64_t) * (nd + 1)))) return rc;
-    if ((rc = ensure(e, e->props, sizeof(mt_props_rec) * nprops))) return rc;
-    if ((rc = ensure(e, e->props_off, sizeof(int64_t) * (nd + 1)))) return rc;
-    if ((rc = ensure(e, e->kv, sizeof(mt_kv) * nkv))) return rc;
-    if ((rc = ensure(e, e->kv_off, sizeof(int64_t) * (nd + 1)))) return rc;
+    if ((rc = ensure_staging(e, a))) return rc;
     if (nops) HIPCHK(e, hipMemcpyAsync(e->ops_buf.p, ops, sizeof(mt_op_rec) * nops, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->op_off.p, op_off, sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice, e->stream));
     if (text_units) HIPCHK(e, hipMemcpyAsync(e->text.p, text, 2 * text_units, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->text_off.p, text_off, sizeof(int64_t) * nd, hipMemcpyHostToDevice, e->stream));
-    if (nprops)
-        HIPCHK(e, hipMemcpyAsync(e->props.p, props, sizeof(mt_props_rec) * nprops, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->props_off.p, props_off, sizeof(int64_t) * nd, hipMemcpyHostToDevice, e->stream));
-    if (nkv) HIPCHK(e, hipMemcpyAsync(e->kv.p, kv, sizeof(mt_kv) * nkv, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->kv_off.p, kv_off, sizeof(int64_t) * nd, hipMemcpyHostToDevice, e->stream));
+    if ((rc = copy_small(e, a, e->stream))) return rc;
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    e->h_op_off.assign(op_off, op_off + nd + 1);
-    e->h_text_off.assign(text_off, text_off + nd);
-    e->h_props_off.assign(props_off, props_off + nd);
-    e->h_kv_off.assign(kv_off, kv_off + nd);
-    e->persp_staged.swap(persp);
-    e->loads = std::find(loads.begin(), loads.end(), 1) != loads.end();
-    e->staged = true;
+    keep_staged(e, a, persp, loads);
     return MT_OK;
+}
+
+int32_t mt_host_alloc(int64_t bytes, void** out) {
+    if (!out || bytes < 0) return MT_E_ARG;
+    *out = nullptr;
+    if (hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 16), hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return MT_E_NOMEM;
+    }
+    return MT_OK;
+}
+void mt_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int32_t mt_engine_reset(mt_engine* e) {
@@ -249,6 +390,8 @@ int32_t mt_engine_reset(mt_engine* e) {
 
 static int32_t stage_subset(mt_engine* e, mt_engine* o);
 
+static int32_t after_launch(mt_engine* e);
+
 int32_t mt_engine_run(mt_engine* e) {
     if (!e || !e->staged) return MT_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
@@ -259,6 +402,94 @@ int32_t mt_engine_run(mt_engine* e) {
     int32_t rc = e->ops->replay(e);
     if (rc) return rc;
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+    return after_launch(e);
+}
+
+/* documents per chunk of mt_engine_submit_run: an eighth of the batch, but never fewer than the documents the GPU
+ * holds at once (a chunk's launch must fill the machine by itself; config 4's 256 documents stay one launch) */
+static int64_t chunk_docs(const mt_engine* e) {
+    if (e->chunk > 0) return e->chunk;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || ncu < 1) ncu = 256;
+    int64_t resident = e->profile == 4 ? ncu : (int64_t)ncu * 4 * (e->profile == 0 ? e->waves : 7);
+    return std::max<int64_t>(resident, (e->ndocs + 7) / 8);
+}
+
+int32_t mt_engine_submit_run(mt_engine* e, const mt_op_rec* ops, const int64_t* op_off, const uint16_t* text,
+                             int64_t text_units, const int64_t* text_off, const mt_props_rec* props, int64_t nprops,
+                             const int64_t* props_off, const mt_kv* kv, int64_t nkv, const int64_t* kv_off) {
+    if (!e) return MT_E_ARG;
+    const SubmitArgs a{ops, op_off, text, text_units, text_off, props, nprops, props_off, kv, nkv, kv_off};
+    if (!offsets_ok(a, e->ndocs)) return MT_E_ARG;
+    const int64_t nd = e->ndocs;
+    HIPCHK(e, hipSetDevice(e->device));
+    int32_t rc;
+    if ((rc = ensure_staging(e, a))) return rc;
+#ifdef MT_PROF
+    if (ensure(e, e->prof, sizeof(uint64_t) * PH_N * e->ndocs)) return MT_E_NOMEM;
+#endif
+    if (!e->cstream) {
+        HIPCHK(e, hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking));
+        HIPCHK(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+        HIPCHK(e, hipEventCreateWithFlags(&e->evs, hipEventDisableTiming));
+        HIPCHK(e, hipEventCreateWithFlags(&e->evc, hipEventDisableTiming));
+        HIPCHK(e, hipEventCreateWithFlags(&e->ev2, hipEventDisableTiming));
+    }
+    e->staged = false;
+    /* everything queued on the engine stream so far (a reset, the last replay reading the buffers about to be
+     * overwritten) comes first, for the copies and both compute streams */
+    HIPCHK(e, hipEventRecord(e->evs, e->stream));
+    HIPCHK(e, hipStreamWaitEvent(e->cstream, e->evs, 0));
+    HIPCHK(e, hipStreamWaitEvent(e->stream2, e->evs, 0));
+    HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+    if ((rc = copy_small(e, a, e->cstream))) return rc;
+    const bool pin_ops = host_pinned(ops), pin_text = host_pinned(text);
+    const int64_t step = e->order.p ? nd : chunk_docs(e); /* a dispatch order permutes across chunks: one launch */
+    std::vector<mt_engine::Persp> persp((size_t)nd);
+    std::vector<char> loads((size_t)nd, 0);
+    int64_t text_hi = 0; /* the text staged so far: a prefix of the pool */
+    int k = 0;
+    rc = MT_OK;
+    for (int64_t d0 = 0; d0 < nd; d0 += step, k++) {
+        const int64_t d1 = std::min(nd, d0 + step);
+        int64_t te = 0;
+        if (!check_range(a, d0, d1, persp.data(), loads.data(), &te)) {
+            rc = MT_E_ARG;
+            break;
+        }
+        if (te > text_hi) {
+            if ((rc = stage_h2d(e, (uint16_t*)e->text.p + text_hi, text + text_hi, 2 * (size_t)(te - text_hi), pin_text)))
+                break;
+            text_hi = te;
+        }
+        if ((rc = stage_h2d(e, (mt_op_rec*)e->ops_buf.p + op_off[d0], ops + op_off[d0],
+                            sizeof(mt_op_rec) * (size_t)(op_off[d1] - op_off[d0]), pin_ops)))
+            break;
+        HIPCHK(e, hipEventRecord(e->evc, e->cstream));
+        hipStream_t s = (k & 1) ? e->stream2 : e->stream;
+        HIPCHK(e, hipStreamWaitEvent(s, e->evc, 0));
+        e->loads = std::find(loads.begin() + d0, loads.begin() + d1, 1) != loads.begin() + d1;
+        e->run_d0 = d0, e->run_n = d1 - d0, e->run_stream = s;
+        rc = e->ops->replay(e);
+        e->run_d0 = 0, e->run_n = -1, e->run_stream = nullptr;
+        if (rc) break;
+    }
+    /* the second compute stream joins the engine stream; the caller's buffers are free once the copies are done */
+    HIPCHK(e, hipEventRecord(e->ev2, e->stream2));
+    HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev2, 0));
+    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->cstream));
+    if (rc) {
+        (void)hipStreamSynchronize(e->stream); /* the chunks launched before the failure have replayed */
+        return rc;
+    }
+    keep_staged(e, a, persp, loads);
+    return after_launch(e);
+}
+
+/* the bookkeeping after a replay launch (mt_engine_run, mt_engine_submit_run) */
+static int32_t after_launch(mt_engine* e) {
+    int32_t rc;
     e->ran = true;
     e->ran_fresh = e->fresh;
     if (e->fresh) e->persp_applied.assign((size_t)e->ndocs, mt_engine::Persp());
@@ -515,6 +746,10 @@ int32_t mt_engine_set_variant(mt_engine* e, int32_t key, int32_t value) {
     case MT_VAR_TILED_WIDE:
         if (value != 0 && value != 1) return MT_E_ARG;
         e->wide = value == 1;
+        return MT_OK;
+    case MT_VAR_CHUNK_DOCS:
+        if (value < 0) return MT_E_ARG;
+        e->chunk = value;
         return MT_OK;
     default:
         return MT_E_ARG;

@@ -41,7 +41,7 @@ class _Caps(ctypes.Structure):
 
 
 _LIB = None
-MT_VAR_SMALL_WAVES, MT_VAR_TILED_WIDE = 1, 2  # include/mt_engine.h
+MT_VAR_SMALL_WAVES, MT_VAR_TILED_WIDE, MT_VAR_CHUNK_DOCS = 1, 2, 3  # include/mt_engine.h
 
 
 def lib() -> ctypes.CDLL:
@@ -64,6 +64,9 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_get_handle.argtypes = [vp, i64, i32, vp]
         L.mt_engine_submit.argtypes = [vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, i64, vp]
         L.mt_engine_run.argtypes = [vp]
+        L.mt_engine_submit_run.argtypes = [vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, i64, vp]
+        L.mt_host_alloc.argtypes = [i64, ctypes.POINTER(vp)]
+        L.mt_host_free.argtypes = [vp]
         L.mt_engine_reset.argtypes = [vp]
         L.mt_engine_work.argtypes = [vp, vp]
         L.mt_engine_doc_times.argtypes = [vp, vp]
@@ -182,6 +185,17 @@ class Engine:
         self._check(self.L.mt_engine_submit(self.h, _p(ops), _p(b.op_off), _p(b.text), len(b.text), _p(b.text_off),
                                              _p(b.props), len(b.props), _p(b.props_off), _p(b.kv), len(b.kv),
                                              _p(b.kv_off)), "submit")
+
+    def submit_run(self, b: ol.Batch):
+        """submit + run with the hand-off overlapped (mt_engine_submit_run): chunk k of the documents replays while
+        chunk k+1 is checked and copied. Returns with the replay running; sync() waits."""
+        if b.ndocs != self.ndocs:
+            raise EngineError("batch doc count != engine doc count")
+        ops = b.ops if len(b.ops) else np.zeros(1, ol.OP_DTYPE)
+        self._keep = (ops, b)
+        self._check(self.L.mt_engine_submit_run(self.h, _p(ops), _p(b.op_off), _p(b.text), len(b.text),
+                                                 _p(b.text_off), _p(b.props), len(b.props), _p(b.props_off),
+                                                 _p(b.kv), len(b.kv), _p(b.kv_off)), "submit_run")
 
     def reset(self):
         self._check(self.L.mt_engine_reset(self.h), "reset")
@@ -384,3 +398,36 @@ class Engine:
         out = np.zeros((self.ndocs, 4), np.int32)
         self._check(self.L.mt_engine_stats(self.h, _p(out)), "stats")
         return out
+
+
+class PinnedArray:
+    """A numpy array over pinned host memory (mt_host_alloc): op logs built or kept there hand off by DMA alone."""
+
+    def __init__(self, shape, dtype):
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape)) * dt.itemsize
+        p = ctypes.c_void_p()
+        rc = lib().mt_host_alloc(n, ctypes.byref(p))
+        if rc != 0:
+            raise EngineError(f"mt_host_alloc({n}) failed: status {rc}")
+        self._p = p.value
+        buf = (ctypes.c_uint8 * max(n, 1)).from_address(self._p)
+        self.array = np.frombuffer(buf, dtype=dt, count=int(np.prod(shape))).reshape(shape)
+
+    def close(self):
+        if getattr(self, "_p", None):
+            self.array = None
+            lib().mt_host_free(self._p)
+            self._p = None
+
+    __del__ = close
+
+
+def pinned_batch(b: ol.Batch):
+    """A copy of the batch with its records and text in pinned host memory; returns (batch, keep-alive handles)."""
+    import dataclasses
+    ops = PinnedArray(b.ops.shape, b.ops.dtype)
+    ops.array[...] = b.ops
+    text = PinnedArray(b.text.shape, b.text.dtype)
+    text.array[...] = b.text
+    return dataclasses.replace(b, ops=ops.array, text=text.array), (ops, text)

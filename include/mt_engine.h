@@ -71,6 +71,19 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
                          int64_t text_units, const int64_t* text_off, const mt_props_rec* props, int64_t nprops,
                          const int64_t* props_off, const mt_kv* kv, int64_t nkv, const int64_t* kv_off);
 
+/* mt_engine_submit + mt_engine_run with the hand-off overlapped: the documents go in chunks (an eighth of the batch, at
+ * least the documents the GPU holds at once), and chunk k's records replay while chunk k+1's are checked on the host
+ * and copied (from pinned memory directly, from pageable memory through the engine's pinned staging buffers). The
+ * same results as submit + run; returns once every record has been copied (the caller's buffers are free again), with
+ * the replay running (mt_engine_sync waits). On MT_E_ARG (a record out of bounds) the chunks before the bad one have
+ * been replayed and nothing stays staged. */
+int32_t mt_engine_submit_run(mt_engine* e, const mt_op_rec* ops, const int64_t* op_off, const uint16_t* text,
+                             int64_t text_units, const int64_t* text_off, const mt_props_rec* props, int64_t nprops,
+                             const int64_t* props_off, const mt_kv* kv, int64_t nkv, const int64_t* kv_off);
+/* Pinned (page-locked) host memory for op logs a caller builds in place: the hand-off then copies by DMA alone. */
+int32_t mt_host_alloc(int64_t bytes, void** out);
+void mt_host_free(void* p);
+
 /* Apply every staged event to its doc: Client.applyMsg for sequenced messages (client.ts:797),
  * insertSegmentLocal / removeRangeLocal / annotateRangeLocal for local edits (202/189/164).
  * Asynchronous on the engine's HIP stream; mt_engine_sync waits. */
@@ -107,8 +120,9 @@ int32_t mt_engine_set_order(mt_engine* e, const int32_t* order);
  *     documents fit 4 per SIMD, else 8; the MT_SMALL_WAVES environment variable sets it at create);
  *   MT_VAR_TILED_WIDE (0 | 1): the config-4 (tiled) kernel with the zamboni heap in HBM and the full window set
  *     (default 0: the narrow LDS-heap build, which promotes documents it cannot hold to the wide one).
- * Takes effect at the next mt_engine_run. */
-enum { MT_VAR_SMALL_WAVES = 1, MT_VAR_TILED_WIDE = 2 };
+ *   MT_VAR_CHUNK_DOCS (>= 0): documents per chunk of mt_engine_submit_run (0: automatic).
+ * Takes effect at the next mt_engine_run / mt_engine_submit_run. */
+enum { MT_VAR_SMALL_WAVES = 1, MT_VAR_TILED_WIDE = 2, MT_VAR_CHUNK_DOCS = 3 };
 int32_t mt_engine_set_variant(mt_engine* e, int32_t key, int32_t value);
 
 /* Per-doc latched error code (MT_E_*) and index of the event that raised it (-1 if none). */

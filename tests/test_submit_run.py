@@ -1,0 +1,119 @@
+"""The overlapped hand-off (mt_engine_submit_run): the documents are checked, copied and replayed chunk by chunk, the
+chunks alternating between two compute streams while the next chunk copies. It must leave exactly what
+mt_engine_submit + mt_engine_run leaves: the same replicas (digests, errors), the same perspective floors for the
+reads, the same staged batch for later resets and runs — from pageable memory (pinned staging buffers) and from
+pinned memory (mt_host_alloc). Reference parity: the c3_lagged reference fixture replays to the reference's digests
+through the chunked path. A record out of bounds in a later chunk fails the call with MT_E_ARG."""
+import numpy as np
+import pytest
+
+from fluidframework_amd import gen
+from fluidframework_amd import oplog as ol
+
+
+def _batch(n=64, ops=512):
+    return gen.generate(gen.config3(ops), ids=np.arange(n), threads=8)
+
+
+def _engine(b, chunk=0, **kw):
+    from fluidframework_amd.engine import MT_VAR_CHUNK_DOCS, Engine, default_caps
+    eng = Engine(b.ndocs, **kw, **default_caps(512))
+    if chunk:
+        eng.set_variant(MT_VAR_CHUNK_DOCS, chunk)
+    eng.start_collab(b.local_long_id)
+    return eng
+
+
+def _length(eng, d, ref_seq, client):
+    from fluidframework_amd.engine import EngineError
+    try:
+        return eng.get_length(d, ref_seq, client)
+    except EngineError as e:  # a perspective the engine refuses (MT_E_UNSUPPORTED): refused alike
+        return ("refused", e.code)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])
+def test_gpu_submit_run_equals_submit_then_run(waves):
+    from fluidframework_amd.engine import pinned_batch
+    b = _batch()
+    ref = _engine(b, waves=waves)
+    ref.replay(b)
+    rerr, _ = ref.errors()
+    assert (rerr == 0).all()
+    rdig = ref.digests()
+    pb, keep = pinned_batch(b)
+    for chunk, batch in ((8, b), (5, b), (8, pb), (0, b)):
+        eng = _engine(b, chunk=chunk, waves=waves)
+        eng.submit_run(batch)
+        eng.sync()
+        err, _ = eng.errors()
+        assert (err == 0).all()
+        assert np.array_equal(eng.digests(), rdig), f"chunk {chunk}"
+        # the perspective floors the reads use came from every chunk
+        for d in (0, 17, 63):
+            for c in (1, 2, 3):
+                assert _length(eng, d, 300, c) == _length(ref, d, 300, c)
+        # the staged batch stays for reset + run (the bench's steps)
+        eng.reset()
+        eng.run()
+        eng.sync()
+        assert np.array_equal(eng.digests(), rdig)
+        eng.close()
+    del keep
+
+
+@pytest.mark.gpu
+def test_gpu_submit_run_incremental_batches():
+    """A second chunked batch on top of the first (no reset) = the whole log in one batch."""
+    b = _batch(40, 800)
+    ref = _engine(b)
+    ref.replay(b)
+    head, tail = [], []
+    for d in range(b.ndocs):
+        ops, text, props, kv = b.doc_arrays(d)
+        head.append((ops[:300], text, props, kv))
+        tail.append((ops[300:], text, props, kv))
+    eng = _engine(b, chunk=6)
+    eng.submit_run(ol.Batch.from_arrays(head, b.local_long_id))
+    eng.sync()
+    eng.submit_run(ol.Batch.from_arrays(tail, b.local_long_id))
+    eng.sync()
+    err, _ = eng.errors()
+    assert (err == 0).all()
+    assert np.array_equal(eng.digests(), ref.digests())
+
+
+@pytest.mark.gpu
+def test_gpu_submit_run_rejects_a_bad_record_in_a_later_chunk():
+    from fluidframework_amd.engine import EngineError
+    b = _batch(32, 256)
+    ops = b.ops.copy()
+    d = 27
+    lo, hi = int(b.op_off[d]), int(b.op_off[d + 1])
+    text_ins = ((ops["kind"][lo:hi] & 7) == ol.OP_INSERT) & ((ops["seg_kind"][lo:hi] & 0x7F) == ol.SEG_TEXT)
+    ins = lo + int(np.nonzero(text_ins)[0][0])
+    ops["text_off"][ins] = len(b.text) + 10  # past the text pool
+    import dataclasses
+    bad = dataclasses.replace(b, ops=ops)
+    eng = _engine(b, chunk=8)
+    with pytest.raises(EngineError) as ex:
+        eng.submit_run(bad)
+    assert ex.value.code == 16
+    with pytest.raises(EngineError):
+        eng.run()  # nothing stays staged
+
+
+@pytest.mark.gpu
+def test_gpu_submit_run_matches_reference_fixture():
+    from test_ref_goldens import caps_for, regenerate
+    from fluidframework_amd.engine import MT_VAR_CHUNK_DOCS, Engine
+    z, w, b = regenerate("c3_lagged")
+    eng = Engine(b.ndocs, **caps_for(w))
+    eng.set_variant(MT_VAR_CHUNK_DOCS, max(1, b.ndocs // 5))
+    eng.start_collab(b.local_long_id)
+    eng.submit_run(b)
+    eng.sync()
+    err, _ = eng.errors()
+    assert (err == 0).all()
+    assert np.array_equal(eng.digests(), z["digests"])

@@ -52,25 +52,25 @@ for S in "$@"; do
       cat "$OUT/bench_c$A.json" ;;
     trace)
       timeout -k 10 $(prof_lim "$A") rocprofv3 --kernel-trace --stats -d "$OUT/trace_c$A" -o run --output-format csv \
-        -- python3 bench.py $(bargs "$A") --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/trace_c$A.json" \
+        -- python3 bench.py $(bargs "$A") --steps 2 --warmup 1 --no-cpu-baseline --no-e2e > "$OUT/trace_c$A.json" \
         2> "$OUT/trace_c$A.err" || fail "$S" $? "$OUT/trace_c$A.err"
       f=$(find "$OUT/trace_c$A" -name '*kernel_stats.csv' | head -1)
       cp "$f" "$OUT/trace_c${A}_kernel_stats.csv"; head -3 "$f" ;;
     traffic)
       for C in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL $(prof_lim "$A") rocprofv3 --pmc $C -d "$OUT/pmc_${C}_c$A" -o run --output-format csv \
-          -- python3 bench.py $(bargs "$A") --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc_${C}_c$A.json" \
+          -- python3 bench.py $(bargs "$A") --steps 1 --warmup 0 --no-cpu-baseline --no-e2e > "$OUT/pmc_${C}_c$A.json" \
           2> "$OUT/pmc_${C}_c$A.err" || fail "$S/$C" $? "$OUT/pmc_${C}_c$A.err"
       done ;;
     inst)
       timeout -s KILL $(prof_lim "$A") rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM \
         SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH -d "$OUT/pmc_inst_c$A" -o run --output-format csv \
-        -- python3 bench.py $(bargs "$A") --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc_inst_c$A.json" \
+        -- python3 bench.py $(bargs "$A") --steps 1 --warmup 0 --no-cpu-baseline --no-e2e > "$OUT/pmc_inst_c$A.json" \
         2> "$OUT/pmc_inst_c$A.err" || fail "$S" $? "$OUT/pmc_inst_c$A.err" ;;
     wait)
       timeout -s KILL $(prof_lim "$A") rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
         SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT -d "$OUT/pmc_wait_c$A" -o run \
-        --output-format csv -- python3 bench.py $(bargs "$A") --steps 1 --warmup 0 --no-cpu-baseline \
+        --output-format csv -- python3 bench.py $(bargs "$A") --steps 1 --warmup 0 --no-cpu-baseline --no-e2e \
         > "$OUT/pmc_wait_c$A.json" 2> "$OUT/pmc_wait_c$A.err" || fail "$S" $? "$OUT/pmc_wait_c$A.err" ;;
     phase)
       v="PHASE_$A"
@@ -83,7 +83,7 @@ for S in "$@"; do
       for L in ${LIBS//,/ }; do
         n=$(basename "$L" .so)
         MT_REPLAY_LIB=$PWD/fluidframework_amd/build/$L timeout -k 10 $(prof_lim "$C") python -u bench.py $(bargs "$C") \
-          --no-cpu-baseline --digests-out "$OUT/dig_c${C}_$n.npy" > "$OUT/ab_c${C}_$n.json" 2> "$OUT/ab_c${C}_$n.err" \
+          --no-cpu-baseline --no-e2e --digests-out "$OUT/dig_c${C}_$n.npy" > "$OUT/ab_c${C}_$n.json" 2> "$OUT/ab_c${C}_$n.err" \
           || fail "$S/$n" $? "$OUT/ab_c${C}_$n.err"
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['value']/1e6,3), 'Mops/s', round(d['roofline']['kernel_ms'],1), 'ms')" "$OUT/ab_c${C}_$n.json" "$n"
         if [ -z "$first" ]; then first=$n; else
