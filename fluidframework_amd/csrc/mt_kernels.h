@@ -126,10 +126,16 @@ struct ReplayAux {
     uint64_t* prof;
     const int32_t* order;
     int64_t doc0; /* a launch over documents [doc0, doc0 + grid): the chunked submit (mt_engine_submit_run) */
+    int32_t compact; /* the staged pools are indexed by launch position, not by document (mt_engine_submit_docs:
+                        `order` lists the documents with records) */
 };
 __device__ inline int64_t aux_doc(const ReplayAux& a) {
     const int64_t b = a.doc0 + (int64_t)blockIdx.x;
     return a.order ? a.order[b] : b;
+}
+/* the entry of the staged offset arrays that holds document d's pools */
+__device__ inline int64_t aux_pool(const ReplayAux& a, int64_t d) {
+    return a.compact ? a.doc0 + (int64_t)blockIdx.x : d;
 }
 /* the document's replay start / end on the constant-rate clock (s_memrealtime, 100 MHz), kept in its image header
  * (DocHdr.tStart / tEnd: no register stays live for it through the replay; mt_engine_doc_times) */
@@ -174,11 +180,12 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
 #define MT_PROF_ATTACH(r) (void)0
 #endif
     Pools p;
-    p.ops = ops + op_off[d];
-    p.nops = op_off[d + 1] - op_off[d];
-    p.text = text + text_off[d];
-    p.props = props + props_off[d];
-    p.kv = kv + kv_off[d];
+    const int64_t pi = aux_pool(aux, d);
+    p.ops = ops + op_off[pi];
+    p.nops = op_off[pi + 1] - op_off[pi];
+    p.text = text + text_off[pi];
+    p.props = props + props_off[pi];
+    p.kv = kv + kv_off[pi];
     Doc<HT> v = st.doc(d);
     if constexpr (LDS) {
         __shared__ __attribute__((aligned(16))) HT hot;
@@ -416,11 +423,12 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     __syncthreads();
     if (replayer && fits) doc_stamp(zhs, 0);
     Pools p;
-    p.ops = ops + op_off[d];
-    p.nops = op_off[d + 1] - op_off[d];
-    p.text = text + text_off[d];
-    p.props = props + props_off[d];
-    p.kv = kv + kv_off[d];
+    const int64_t pi = aux_pool(aux, d);
+    p.ops = ops + op_off[pi];
+    p.nops = op_off[pi + 1] - op_off[pi];
+    p.text = text + text_off[pi];
+    p.props = props + props_off[pi];
+    p.kv = kv + kv_off[pi];
     if (!replayer) {
         tiled_prefetch<HT>(v, p.ops, p.nops, &pfcur, &pfdone, lcord, lcst, lccnt, &pfsink);
     } else if (!fits) {
@@ -814,6 +822,11 @@ struct mt_engine {
      * mt_engine_submit_run: one range per chunk, alternating between `stream` and `stream2`) */
     int64_t run_d0 = 0, run_n = -1;
     int64_t chunk = 0; /* documents per chunk of mt_engine_submit_run (0: automatic) */
+    /* a staged batch of some documents only (mt_engine_submit_docs): their ids (`sub`, increasing; nsub = -1: every
+     * document); the staged offsets then hold one entry per listed document */
+    int64_t nsub = -1;
+    DevBuf sub;
+    std::vector<int64_t> h_sub;
     hipStream_t run_stream = nullptr;
     /* mt_engine_submit_run: the copy stream, the second compute stream, and pinned staging buffers for pageable
      * sources (each with the event of the last copy out of it) */
@@ -883,13 +896,14 @@ static inline Store<HT>& store_of(mt_engine* e) {
 /* one replay kernel over the staged batch (a document per workgroup) */
 template <class HT, class K>
 static inline int32_t launch_replay(mt_engine* e, K kern, int block = WG) {
-    const int64_t n = e->run_n < 0 ? e->ndocs : e->run_n;
+    const int64_t n = e->run_n >= 0 ? e->run_n : e->nsub >= 0 ? e->nsub : e->ndocs;
     if (n <= 0) return MT_OK;
+    const int32_t* order = e->nsub >= 0 ? (const int32_t*)e->sub.p : (const int32_t*)e->order.p;
     hipLaunchKernelGGL(kern, docs_grid(n), dim3(block), 0, e->run_stream ? e->run_stream : e->stream, store_of<HT>(e),
                        e->ndocs, (const mt_op_rec*)e->ops_buf.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
                        (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p, (const int64_t*)e->props_off.p,
                        (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p,
-                       ReplayAux{(uint64_t*)e->prof.p, (const int32_t*)e->order.p, e->run_d0});
+                       ReplayAux{(uint64_t*)e->prof.p, order, e->run_d0, e->nsub >= 0 ? 1 : 0});
     return launch_check(e, "k_replay");
 }
 

@@ -120,8 +120,9 @@ static bool check_range(const SubmitArgs& a, int64_t d0, int64_t d1, mt_engine::
     return true;
 }
 
-static int32_t ensure_staging(mt_engine* e, const SubmitArgs& a) {
-    int64_t nd = e->ndocs, nops = a.op_off[nd];
+static int32_t ensure_staging(mt_engine* e, const SubmitArgs& a, int64_t nd = -1) {
+    if (nd < 0) nd = e->ndocs; /* staged entries */
+    int64_t nops = a.op_off[nd];
     int32_t rc;
     if ((rc = ensure(e, e->ops_buf, sizeof(mt_op_rec) * nops))) return rc;
     if ((rc = ensure(e, e->op_off, sizeof(int64_t) * (nd + 1)))) return rc;
@@ -134,8 +135,8 @@ static int32_t ensure_staging(mt_engine* e, const SubmitArgs& a) {
 }
 
 /* the offsets and the property pools (small next to the records and the text) */
-static int32_t copy_small(mt_engine* e, const SubmitArgs& a, hipStream_t s) {
-    int64_t nd = e->ndocs;
+static int32_t copy_small(mt_engine* e, const SubmitArgs& a, hipStream_t s, int64_t nd = -1) {
+    if (nd < 0) nd = e->ndocs; /* staged entries */
     HIPCHK(e, hipMemcpyAsync(e->op_off.p, a.op_off, sizeof(int64_t) * (nd + 1), hipMemcpyHostToDevice, s));
     HIPCHK(e, hipMemcpyAsync(e->text_off.p, a.text_off, sizeof(int64_t) * nd, hipMemcpyHostToDevice, s));
     if (a.nprops) HIPCHK(e, hipMemcpyAsync(e->props.p, a.props, sizeof(mt_props_rec) * a.nprops, hipMemcpyHostToDevice, s));
@@ -148,7 +149,7 @@ static int32_t copy_small(mt_engine* e, const SubmitArgs& a, hipStream_t s) {
 /* the host copies of a staged batch's offsets, floors and load flag */
 static void keep_staged(mt_engine* e, const SubmitArgs& a, std::vector<mt_engine::Persp>& persp,
                         const std::vector<char>& loads) {
-    int64_t nd = e->ndocs;
+    int64_t nd = (int64_t)persp.size(); /* staged entries: every document, or the listed ones (mt_engine_submit_docs) */
     e->h_op_off.assign(a.op_off, a.op_off + nd + 1);
     e->h_text_off.assign(a.text_off, a.text_off + nd);
     e->h_props_off.assign(a.props_off, a.props_off + nd);
@@ -280,7 +281,7 @@ void mt_engine_destroy(mt_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->borrowed) e->text.p = e->props.p = e->kv.p = nullptr; /* the parent's */
     DevBuf* bufs[] = {&e->ops_buf, &e->op_off, &e->text, &e->text_off, &e->props,     &e->props_off,
-                      &e->kv,     &e->kv_off, &e->tmp,  &e->local_ids, &e->prof, &e->order};
+                      &e->kv,     &e->kv_off, &e->tmp,  &e->local_ids, &e->prof, &e->order, &e->sub};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (e->mem) (void)hipFree(e->mem);
@@ -358,10 +359,41 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc;
     if ((rc = ensure_staging(e, a))) return rc;
+    e->nsub = -1;
+    e->h_sub.clear();
     if (nops) HIPCHK(e, hipMemcpyAsync(e->ops_buf.p, ops, sizeof(mt_op_rec) * nops, hipMemcpyHostToDevice, e->stream));
     if (text_units) HIPCHK(e, hipMemcpyAsync(e->text.p, text, 2 * text_units, hipMemcpyHostToDevice, e->stream));
     if ((rc = copy_small(e, a, e->stream))) return rc;
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    keep_staged(e, a, persp, loads);
+    return MT_OK;
+}
+
+int32_t mt_engine_submit_docs(mt_engine* e, int64_t m, const int64_t* docs, const mt_op_rec* ops, const int64_t* op_off,
+                              const uint16_t* text, int64_t text_units, const int64_t* text_off,
+                              const mt_props_rec* props, int64_t nprops, const int64_t* props_off, const mt_kv* kv,
+                              int64_t nkv, const int64_t* kv_off) {
+    if (!e || m < 0 || m > e->ndocs || (m && !docs)) return MT_E_ARG;
+    for (int64_t k = 0; k < m; k++)
+        if (docs[k] < 0 || docs[k] >= e->ndocs || (k && docs[k] <= docs[k - 1])) return MT_E_ARG; /* increasing ids */
+    const SubmitArgs a{ops, op_off, text, text_units, text_off, props, nprops, props_off, kv, nkv, kv_off};
+    if (!offsets_ok(a, m)) return MT_E_ARG;
+    std::vector<mt_engine::Persp> persp((size_t)m);
+    std::vector<char> loads((size_t)m, 0);
+    if (!check_range(a, 0, m, persp.data(), loads.data(), nullptr)) return MT_E_ARG;
+    HIPCHK(e, hipSetDevice(e->device));
+    int32_t rc;
+    if ((rc = ensure_staging(e, a, m))) return rc;
+    if ((rc = ensure(e, e->sub, sizeof(int32_t) * (size_t)std::max<int64_t>(m, 1)))) return rc;
+    e->h_sub.assign(docs, docs + m);
+    std::vector<int32_t> ids(docs, docs + m);
+    int64_t nops = op_off[m];
+    if (nops) HIPCHK(e, hipMemcpyAsync(e->ops_buf.p, ops, sizeof(mt_op_rec) * nops, hipMemcpyHostToDevice, e->stream));
+    if (text_units) HIPCHK(e, hipMemcpyAsync(e->text.p, text, 2 * text_units, hipMemcpyHostToDevice, e->stream));
+    if (m) HIPCHK(e, hipMemcpyAsync(e->sub.p, ids.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, e->stream));
+    if ((rc = copy_small(e, a, e->stream, m))) return rc;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->nsub = m;
     keep_staged(e, a, persp, loads);
     return MT_OK;
 }
@@ -436,6 +468,8 @@ int32_t mt_engine_submit_run(mt_engine* e, const mt_op_rec* ops, const int64_t* 
         HIPCHK(e, hipEventCreateWithFlags(&e->ev2, hipEventDisableTiming));
     }
     e->staged = false;
+    e->nsub = -1;
+    e->h_sub.clear();
     /* everything queued on the engine stream so far (a reset, the last replay reading the buffers about to be
      * overwritten) comes first, for the copies and both compute streams */
     HIPCHK(e, hipEventRecord(e->evs, e->stream));
@@ -493,8 +527,10 @@ static int32_t after_launch(mt_engine* e) {
     e->ran = true;
     e->ran_fresh = e->fresh;
     if (e->fresh) e->persp_applied.assign((size_t)e->ndocs, mt_engine::Persp());
-    for (size_t d = 0; d < e->persp_staged.size() && d < e->persp_applied.size(); d++)
-        e->persp_applied[d].merge(e->persp_staged[d]);
+    for (size_t k = 0; k < e->persp_staged.size(); k++) {
+        size_t d = e->nsub >= 0 ? (size_t)e->h_sub[k] : k;
+        if (d < e->persp_applied.size()) e->persp_applied[d].merge(e->persp_staged[k]);
+    }
     e->fresh = false;
     e->forwarded = false;
     /* documents promoted by an earlier replay of this replica history live on in `over`: their parent
@@ -579,6 +615,12 @@ static void scatter(T* dst, const std::vector<T>& src, const std::vector<int64_t
 }
 /* stage, in `o`, the records `e` has staged for its promoted documents (e->pro_docs, in order), gathered
  * device to device; their text / props / kv pools stay the parent's */
+/* the staged entry holding document d's records (-1: none staged for it) */
+static int64_t staged_entry(const mt_engine* e, int64_t d) {
+    if (e->nsub < 0) return d;
+    auto it = std::lower_bound(e->h_sub.begin(), e->h_sub.end(), d);
+    return it != e->h_sub.end() && *it == d ? (int64_t)(it - e->h_sub.begin()) : -1;
+}
 static int32_t stage_subset(mt_engine* e, mt_engine* o) {
     int64_t m = (int64_t)e->pro_docs.size();
     int32_t rc;
@@ -586,12 +628,16 @@ static int32_t stage_subset(mt_engine* e, mt_engine* o) {
     o->h_text_off.resize((size_t)m);
     o->h_props_off.resize((size_t)m);
     o->h_kv_off.resize((size_t)m);
+    o->nsub = -1;
+    std::vector<int64_t> src((size_t)m);
     for (int64_t i = 0; i < m; i++) {
-        int64_t d = e->pro_docs[(size_t)i];
-        o->h_op_off[(size_t)i + 1] = o->h_op_off[(size_t)i] + e->h_op_off[(size_t)d + 1] - e->h_op_off[(size_t)d];
-        o->h_text_off[(size_t)i] = e->h_text_off[(size_t)d];
-        o->h_props_off[(size_t)i] = e->h_props_off[(size_t)d];
-        o->h_kv_off[(size_t)i] = e->h_kv_off[(size_t)d];
+        int64_t k = staged_entry(e, e->pro_docs[(size_t)i]);
+        src[(size_t)i] = k;
+        int64_t n = k < 0 ? 0 : e->h_op_off[(size_t)k + 1] - e->h_op_off[(size_t)k];
+        o->h_op_off[(size_t)i + 1] = o->h_op_off[(size_t)i] + n;
+        o->h_text_off[(size_t)i] = k < 0 ? 0 : e->h_text_off[(size_t)k];
+        o->h_props_off[(size_t)i] = k < 0 ? 0 : e->h_props_off[(size_t)k];
+        o->h_kv_off[(size_t)i] = k < 0 ? 0 : e->h_kv_off[(size_t)k];
     }
     if ((rc = ensure(o, o->ops_buf, sizeof(mt_op_rec) * o->h_op_off[(size_t)m]))) return rc;
     if ((rc = ensure(o, o->op_off, sizeof(int64_t) * (m + 1)))) return rc;
@@ -599,10 +645,10 @@ static int32_t stage_subset(mt_engine* e, mt_engine* o) {
     if ((rc = ensure(o, o->props_off, sizeof(int64_t) * m))) return rc;
     if ((rc = ensure(o, o->kv_off, sizeof(int64_t) * m))) return rc;
     for (int64_t i = 0; i < m; i++) {
-        int64_t d = e->pro_docs[(size_t)i], n = e->h_op_off[(size_t)d + 1] - e->h_op_off[(size_t)d];
+        int64_t k = src[(size_t)i], n = o->h_op_off[(size_t)i + 1] - o->h_op_off[(size_t)i];
         if (n)
             HIPCHK(o, hipMemcpyAsync((mt_op_rec*)o->ops_buf.p + o->h_op_off[(size_t)i],
-                                     (const mt_op_rec*)e->ops_buf.p + e->h_op_off[(size_t)d], sizeof(mt_op_rec) * n,
+                                     (const mt_op_rec*)e->ops_buf.p + e->h_op_off[(size_t)k], sizeof(mt_op_rec) * n,
                                      hipMemcpyDeviceToDevice, o->stream));
     }
     HIPCHK(o, hipMemcpyAsync(o->op_off.p, o->h_op_off.data(), sizeof(int64_t) * (m + 1), hipMemcpyHostToDevice, o->stream));
@@ -1045,6 +1091,22 @@ int64_t mt_engine_deltas(mt_engine* e, int64_t doc, int32_t* out, int64_t cap) {
         if (hipStreamSynchronize(e->stream) != hipSuccess) return -MT_E_HIP;
     }
     return logged;
+}
+
+int32_t mt_engine_doc_error(mt_engine* e, int64_t doc, int32_t* err, int32_t* err_op) {
+    if (!e || doc < 0 || doc >= e->ndocs) return MT_E_ARG;
+    e = route(e, &doc);
+    HIPCHK(e, hipSetDevice(e->device));
+    int64_t stride = 0, off = 0;
+    delta_geometry(e, &off, &stride); /* the block stride; the header is at the block's start */
+    int32_t v[2];
+    const uint8_t* h = (const uint8_t*)e->mem + doc * stride + offsetof(DocHdr, err);
+    static_assert(offsetof(DocHdr, errOp) == offsetof(DocHdr, err) + 4, "err, errOp adjacent");
+    HIPCHK(e, hipMemcpyAsync(v, h, sizeof v, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (err) *err = v[0];
+    if (err_op) *err_op = v[1];
+    return MT_OK;
 }
 
 int32_t mt_engine_ref_capacity(const mt_engine* e) { return e ? e->rcap : 0; }

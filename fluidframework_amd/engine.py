@@ -65,6 +65,8 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_submit.argtypes = [vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, i64, vp]
         L.mt_engine_run.argtypes = [vp]
         L.mt_engine_submit_run.argtypes = [vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, i64, vp]
+        L.mt_engine_submit_docs.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, i64, vp]
+        L.mt_engine_doc_error.argtypes = [vp, i64, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.mt_host_alloc.argtypes = [i64, ctypes.POINTER(vp)]
         L.mt_host_free.argtypes = [vp]
         L.mt_engine_reset.argtypes = [vp]
@@ -196,6 +198,24 @@ class Engine:
         self._check(self.L.mt_engine_submit_run(self.h, _p(ops), _p(b.op_off), _p(b.text), len(b.text),
                                                  _p(b.text_off), _p(b.props), len(b.props), _p(b.props_off),
                                                  _p(b.kv), len(b.kv), _p(b.kv_off)), "submit_run")
+
+    def submit_docs(self, docs, b: ol.Batch):
+        """Stage records for some documents only (mt_engine_submit_docs): `b` holds one log per entry of `docs`
+        (increasing document ids); the next run() replays those documents alone."""
+        d = np.ascontiguousarray(docs, np.int64)
+        if b.ndocs != len(d):
+            raise EngineError("one log per listed document")
+        ops = b.ops if len(b.ops) else np.zeros(1, ol.OP_DTYPE)
+        self._keep = (ops, b, d)
+        self._check(self.L.mt_engine_submit_docs(self.h, len(d), _p(d), _p(ops), _p(b.op_off), _p(b.text), len(b.text),
+                                                  _p(b.text_off), _p(b.props), len(b.props), _p(b.props_off),
+                                                  _p(b.kv), len(b.kv), _p(b.kv_off)), "submit_docs")
+
+    def doc_error(self, doc: int):
+        """(err, err_op) of one document (mt_engine_doc_error)."""
+        e, o = ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.L.mt_engine_doc_error(self.h, doc, ctypes.byref(e), ctypes.byref(o)), "doc_error")
+        return e.value, o.value
 
     def reset(self):
         self._check(self.L.mt_engine_reset(self.h), "reset")

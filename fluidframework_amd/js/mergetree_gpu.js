@@ -193,6 +193,7 @@ class ReplayEngine {
         this.nrefs = new Array(ndocs).fill(0);   // local references created per document
         this.pending = Array.from({ length: ndocs }, () => []); // op types in flight, per pending group
         this.version = 0; // bumped by every enqueued record and every collaboration start: cached reads expire
+        this.dirty = new Set(); // documents with queued records
     }
 
     longIndex(name) {
@@ -222,6 +223,7 @@ class ReplayEngine {
 
     enqueue(doc, kind, fields, segOrProps) {
         this.version++;
+        this.dirty.add(doc);
         const q = this.queues[doc];
         const r = { kind, seg_kind: 0, client: 0, seq: 0, ref_seq: 0, min_seq: 0, pos1: 0, pos2: 0, text_off: 0,
             text_len: 0, props: 0, ...fields };
@@ -269,28 +271,41 @@ class ReplayEngine {
         const keys = Object.keys(props);
         for (const k of keys) q.kv.push([this.interner.key(k), this.interner.value(props[k])]);
         // ICombiningOp -> mt_oplog.h MT_COMBINE_*: rewrite 1, incr 2, consensus 3 (without defaultValue / minValue)
-        const COMB = { rewrite: 1, incr: 2, consensus: 3 };
-        if (combiningOp && (COMB[combiningOp.name] === undefined ||
-            (combiningOp.name !== "rewrite" && (combiningOp.defaultValue !== undefined || combiningOp.minValue !== undefined)))) {
+        const COMB = new Map([["rewrite", 1], ["incr", 2], ["consensus", 3]]);
+        // combine() starts from any defaultValue that is not undefined (null included) and clamps only to a truthy
+        // minValue (properties.ts:26-38); wire.py refuses the same ones
+        if (combiningOp && (!COMB.has(combiningOp.name) ||
+            (combiningOp.name !== "rewrite" && (combiningOp.defaultValue !== undefined || combiningOp.minValue)))) {
             throw new Error(`combiningOp ${combiningOp.name} unsupported`);
         }
-        q.props.push([off, keys.length, combiningOp ? COMB[combiningOp.name] : 0]);
+        q.props.push([off, keys.length, combiningOp ? COMB.get(combiningOp.name) : 0]);
         return q.props.length;
     }
 
-    /* submit every queued event of every document, replay on the GPU, wait */
+    /* submit the queued events of the documents that have any (mt_engine_submit_docs: the others are not staged and
+     * their workgroups are not launched), replay them on the GPU, wait */
     flush() {
+        const dirty = [];
+        for (const d of this.dirty) if (this.queues[d].recs.length) dirty.push(d);
+        this.dirty.clear();
+        if (dirty.length === 0) return;
+        dirty.sort((a, b) => a - b);
         let nrec = 0, ntext = 0, nprops = 0, nkv = 0;
-        for (const q of this.queues) { nrec += q.recs.length; ntext += q.text.length; nprops += q.props.length; nkv += q.kv.length; }
-        if (nrec === 0) return;
+        for (const d of dirty) {
+            const q = this.queues[d];
+            nrec += q.recs.length; ntext += q.text.length; nprops += q.props.length; nkv += q.kv.length;
+        }
+        const m = dirty.length;
+        const docs = BigInt64Array.from(dirty, (d) => BigInt(d));
         const ops = new Uint8Array(32 * nrec), dv = new DataView(ops.buffer);
         const text = new Uint16Array(Math.max(ntext, 1));
         const props = new Uint8Array(8 * Math.max(nprops, 1)), pv = new DataView(props.buffer);
         const kv = new Uint8Array(4 * Math.max(nkv, 1)), kvv = new DataView(kv.buffer);
-        const opOff = new BigInt64Array(this.ndocs + 1), textOff = new BigInt64Array(this.ndocs + 1);
-        const propsOff = new BigInt64Array(this.ndocs + 1), kvOff = new BigInt64Array(this.ndocs + 1);
+        const opOff = new BigInt64Array(m + 1), textOff = new BigInt64Array(m + 1);
+        const propsOff = new BigInt64Array(m + 1), kvOff = new BigInt64Array(m + 1);
         let ro = 0, to = 0, po = 0, ko = 0;
-        this.queues.forEach((q, d) => {
+        dirty.forEach((doc, d) => {
+            const q = this.queues[doc];
             opOff[d] = BigInt(ro); textOff[d] = BigInt(to); propsOff[d] = BigInt(po); kvOff[d] = BigInt(ko);
             for (const r of q.recs) {
                 const b = 32 * ro++;
@@ -306,16 +321,17 @@ class ReplayEngine {
             for (const [k, v] of q.kv) { kvv.setUint16(4 * ko, k, true); kvv.setUint16(4 * ko + 2, v, true); ko++; }
             q.recs = []; q.text = []; q.props = []; q.kv = [];
         });
-        opOff[this.ndocs] = BigInt(ro); textOff[this.ndocs] = BigInt(to);
-        propsOff[this.ndocs] = BigInt(po); kvOff[this.ndocs] = BigInt(ko);
-        addon.submit(this.h, ops, opOff, text, textOff, props, propsOff, kv, kvOff);
+        opOff[m] = BigInt(ro); textOff[m] = BigInt(to);
+        propsOff[m] = BigInt(po); kvOff[m] = BigInt(ko);
+        addon.submitDocs(this.h, docs, ops, opOff, text, textOff, props, propsOff, kv, kvOff);
         addon.run(this.h);
         addon.sync(this.h);
     }
 
+    /* the document's latched error, read alone (8 bytes) */
     checkDoc(doc) {
-        const [err, errOp] = addon.errors(this.h);
-        if (err[doc] !== 0) throw new Error(`document ${doc}: ${ERRORS[err[doc]] || err[doc]} at event ${errOp[doc]}`);
+        const [err, errOp] = addon.docError(this.h, doc);
+        if (err !== 0) throw new Error(`document ${doc}: ${ERRORS[err] || err} at event ${errOp}`);
     }
 
     digests() { this.flush(); return addon.digests(this.h); }

@@ -194,6 +194,55 @@ static napi_value js_submit(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+/* submitDocs(h, BigInt64Array docs, Uint8Array ops, BigInt64Array opOff, Uint16Array text, BigInt64Array textOff,
+ *            Uint8Array props, BigInt64Array propsOff, Uint8Array kv, BigInt64Array kvOff): records for the listed
+ * documents only, one offset entry per listed document (mt_engine_submit_docs) */
+static napi_value js_submit_docs(napi_env env, napi_callback_info info) {
+    napi_value argv[10];
+    if (!get_args(env, info, 10, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    void *docs, *ops, *op_off, *text, *text_off, *props, *props_off, *kv, *kv_off;
+    size_t m, nops_b, noo, ntext, nto, nprops_b, npo, nkv_b, nko;
+    if (!view_of(env, argv[1], &docs, &m, napi_bigint64_array) ||
+        !view_of(env, argv[2], &ops, &nops_b, napi_uint8_array) ||
+        !view_of(env, argv[3], &op_off, &noo, napi_bigint64_array) ||
+        !view_of(env, argv[4], &text, &ntext, napi_uint16_array) ||
+        !view_of(env, argv[5], &text_off, &nto, napi_bigint64_array) ||
+        !view_of(env, argv[6], &props, &nprops_b, napi_uint8_array) ||
+        !view_of(env, argv[7], &props_off, &npo, napi_bigint64_array) ||
+        !view_of(env, argv[8], &kv, &nkv_b, napi_uint8_array) ||
+        !view_of(env, argv[9], &kv_off, &nko, napi_bigint64_array))
+        return nullptr;
+    if (noo != m + 1 || nto < m || npo < m || nko < m || nops_b % sizeof(mt_op_rec) || nprops_b % sizeof(mt_props_rec) ||
+        nkv_b % sizeof(mt_kv) || ((const int64_t*)op_off)[m] * (int64_t)sizeof(mt_op_rec) > (int64_t)nops_b)
+        return throw_status(env, e, MT_E_ARG, "submitDocs (array shapes)");
+    int32_t rc = mt_engine_submit_docs(e, (int64_t)m, (const int64_t*)docs, (const mt_op_rec*)ops, (const int64_t*)op_off,
+                                       (const uint16_t*)text, (int64_t)ntext, (const int64_t*)text_off,
+                                       (const mt_props_rec*)props, (int64_t)(nprops_b / sizeof(mt_props_rec)),
+                                       (const int64_t*)props_off, (const mt_kv*)kv, (int64_t)(nkv_b / sizeof(mt_kv)),
+                                       (const int64_t*)kv_off);
+    if (rc) return throw_status(env, e, rc, "mt_engine_submit_docs");
+    return nullptr;
+}
+
+/* docError(h, doc) -> [err, errOp] of one document (mt_engine_doc_error) */
+static napi_value js_doc_error(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    if (!e || !i64_of(env, argv[1], &doc)) return nullptr;
+    int32_t err = 0, op = 0;
+    int32_t rc = mt_engine_doc_error(e, doc, &err, &op);
+    if (rc) return throw_status(env, e, rc, "mt_engine_doc_error");
+    napi_value out;
+    NAPI_OK(napi_create_array_with_length(env, 2, &out));
+    NAPI_OK(napi_set_element(env, out, 0, num(env, err)));
+    NAPI_OK(napi_set_element(env, out, 1, num(env, op)));
+    return out;
+}
+
 #define SIMPLE(name, call)                                            \
     static napi_value name(napi_env env, napi_callback_info info) {   \
         napi_value argv[1];                                           \
@@ -573,7 +622,8 @@ static napi_value init(napi_env env, napi_value exports) {
                {"deltas", js_deltas},       {"refPositions", js_ref_positions},
                {"resolveRemoteClientPosition", js_resolve_remote}, {"adjustPosition", js_adjust_position},
                {"handleToPosition", js_handle_to_position}, {"getMarkerFromId", js_marker_from_id},
-               {"dump", js_dump},           {"segmentIds", js_segment_ids}};
+               {"dump", js_dump},           {"segmentIds", js_segment_ids},
+               {"submitDocs", js_submit_docs}, {"docError", js_doc_error}};
     for (auto& f : fns) {
         napi_value fn;
         NAPI_OK(napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn));

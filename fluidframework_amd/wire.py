@@ -75,7 +75,9 @@ def combining_kind(comb) -> int:
     if name == "rewrite":
         return ol.COMBINE_REWRITE
     if name in ("incr", "consensus"):
-        if comb.get("defaultValue") is not None or comb.get("minValue") is not None:
+        # combine() starts from defaultValue whenever the key is present (a JSON null included: null + undefined and
+        # null.seq are not undefined's results) and clamps only to a truthy minValue (properties.ts:26-38)
+        if "defaultValue" in comb or comb.get("minValue"):
             raise ValueError(f"combining op {name!r} with a defaultValue / minValue is not supported")
         return ol.COMBINE_INCR if name == "incr" else ol.COMBINE_CONSENSUS
     raise ValueError(f"combining op {name!r} is not supported")

@@ -80,6 +80,14 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
 int32_t mt_engine_submit_run(mt_engine* e, const mt_op_rec* ops, const int64_t* op_off, const uint16_t* text,
                              int64_t text_units, const int64_t* text_off, const mt_props_rec* props, int64_t nprops,
                              const int64_t* props_off, const mt_kv* kv, int64_t nkv, const int64_t* kv_off);
+/* Stage records for some documents only: docs[0..m) (increasing ids) and, for docs[k], the records
+ * ops[op_off[k] .. op_off[k+1]) with pools at text+text_off[k], props+props_off[k], kv+kv_off[k]. The next
+ * mt_engine_run replays those documents alone (one small launch); the others keep their state. What an interactive
+ * host (the JS facade's reads) stages after a few edits; the reference applies each op as it arrives. */
+int32_t mt_engine_submit_docs(mt_engine* e, int64_t m, const int64_t* docs, const mt_op_rec* ops, const int64_t* op_off,
+                              const uint16_t* text, int64_t text_units, const int64_t* text_off,
+                              const mt_props_rec* props, int64_t nprops, const int64_t* props_off, const mt_kv* kv,
+                              int64_t nkv, const int64_t* kv_off);
 /* Pinned (page-locked) host memory for op logs a caller builds in place: the hand-off then copies by DMA alone. */
 int32_t mt_host_alloc(int64_t bytes, void** out);
 void mt_host_free(void* p);
@@ -127,6 +135,8 @@ int32_t mt_engine_set_variant(mt_engine* e, int32_t key, int32_t value);
 
 /* Per-doc latched error code (MT_E_*) and index of the event that raised it (-1 if none). */
 int32_t mt_engine_errors(mt_engine* e, int32_t* err, int32_t* err_op);
+/* The same for one document (an 8-byte read). */
+int32_t mt_engine_doc_error(mt_engine* e, int64_t doc, int32_t* err, int32_t* err_op);
 /* Per-doc FNV-1a-64 digest of the canonical segment dump (mt_oplog.h), computed on device. */
 int32_t mt_engine_digests(mt_engine* e, uint64_t* out);
 /* Canonical dump of one doc; returns bytes needed (writes if cap suffices), <0 on error. */

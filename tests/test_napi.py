@@ -21,7 +21,8 @@ NODE = shutil.which("node")
 pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
 EXPORTS = ["create", "startCollab", "submit", "run", "sync", "reset", "errors", "digests", "getLength", "getText",
-           "getContainingSegment", "getPosition", "ndocs", "lastRunMs", "deltas", "refPositions"]
+           "getContainingSegment", "getPosition", "ndocs", "lastRunMs", "deltas", "refPositions", "submitDocs",
+           "docError"]
 
 
 def _node(script: str) -> str:
@@ -159,3 +160,16 @@ def test_typings_declare_every_export_and_method():
         internal = {"enqueue", "propsRecord", "checkDoc", "fields", "sent", "read"}
         for m in methods - internal:
             assert re.search(rf"\b{m}\b", dbody), f"{cls}.{m} is not declared in the typings"
+
+
+@pytest.mark.gpu
+def test_interactive_reads_flush_only_dirty_documents():
+    """tools/facade_latency.js on a 4,096-document engine: local edits, remote sequenced inserts and reads, each read
+    flushing only the documents with queued records (mt_engine_submit_docs) and reading one document's error
+    (mt_engine_doc_error); every answer is checked by the script against the text it expects."""
+    native.build_napi()
+    r = subprocess.run([NODE, os.path.join(ROOT, "tools", "facade_latency.js"), "4096", "40"], capture_output=True,
+                       text=True, cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["answers_checked"] and out["docs_touched"] > 40

@@ -117,3 +117,36 @@ def test_gpu_submit_run_matches_reference_fixture():
     err, _ = eng.errors()
     assert (err == 0).all()
     assert np.array_equal(eng.digests(), z["digests"])
+
+
+@pytest.mark.gpu
+def test_gpu_submit_docs_replays_listed_documents_only():
+    """mt_engine_submit_docs: records for some documents, in batches of a few documents each (what the JS facade
+    flushes before a read), replay to the same replicas as the whole log in one batch; documents with no records in
+    a batch keep their state; one document's error reads alone (mt_engine_doc_error)."""
+    b = _batch(48, 600)
+    ref = _engine(b)
+    ref.replay(b)
+    rdig = ref.digests()
+    eng = _engine(b)
+    rng = np.random.default_rng(7)
+    pos = np.zeros(b.ndocs, np.int64)  # records of each document applied so far
+    per = [b.doc_arrays(d) for d in range(b.ndocs)]
+    while (pos < np.diff(b.op_off)).any():
+        left = np.nonzero(pos < np.diff(b.op_off))[0]
+        docs = np.sort(rng.choice(left, size=min(len(left), int(rng.integers(1, 6))), replace=False))
+        arrays = []
+        for d in docs:
+            ops, text, props, kv = per[d]
+            n = int(rng.integers(1, 200))
+            arrays.append((ops[pos[d]: pos[d] + n], text, props, kv))
+            pos[d] = min(pos[d] + n, len(ops))
+        eng.submit_docs(docs, ol.Batch.from_arrays(arrays, b.local_long_id[docs]))
+        eng.run()
+        eng.sync()
+        for d in docs:
+            assert eng.doc_error(int(d))[0] == 0
+    assert np.array_equal(eng.digests(), rdig)
+    err, err_op = eng.errors()
+    assert (err == 0).all()
+    assert all(eng.doc_error(d) == (int(err[d]), int(err_op[d])) for d in range(b.ndocs))

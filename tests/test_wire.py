@@ -121,13 +121,19 @@ def test_unsupported_wire_ops_raise():
         wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
                                                    "combiningOp": {"name": "incr", "defaultValue": 3}}),
                          wire.ClientNames())
+    with pytest.raises(ValueError):  # a null defaultValue is a start value too (properties.ts:26-28)
+        wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
+                                                   "combiningOp": {"name": "consensus", "defaultValue": None}}),
+                         wire.ClientNames())
     with pytest.raises(ValueError):  # an unknown combining op
         wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
                                                    "combiningOp": {"name": "max"}}), wire.ClientNames())
     for name, kind in (("incr", ol.COMBINE_INCR), ("consensus", ol.COMBINE_CONSENSUS)):
-        wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
-                                                   "combiningOp": {"name": name}}), wire.ClientNames())
-        assert log.props[log.ops[-1][10] - 1][2] == kind
+        # a falsy minValue clamps nothing (`if (combiningInfo.minValue)`, properties.ts:33): as absent
+        for extra in ({}, {"minValue": 0}, {"minValue": None}):
+            wire.add_message(log, dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
+                                                       "combiningOp": dict(name=name, **extra)}), wire.ClientNames())
+            assert log.props[log.ops[-1][10] - 1][2] == kind
     names = wire.ClientNames(["x"])
     wire.add_message(log, dict(base, clientId="y", type="noop"), names)
     assert names.name(1) == "y" and log.ops[-1][0] == ol.OP_NOOP
