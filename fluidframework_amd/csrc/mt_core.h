@@ -142,6 +142,9 @@ struct DocHdr {
     int32_t ovTop, ovFree; /* overlap overflow pool: next never-used block, free-list head (0 = none) */
     int32_t gidNext;       /* id of the next pending segment group (ids increase along the queue) */
     int32_t mkMask;        /* property key slots an annotate changed on a marker (marker_keys_annotated) */
+    int32_t ndv; /* derived property values (mt_oplog.h MT_VALUE_DERIVED): bits 0-7 the STRCAT entries, 8-15 the
+                    consensus-object entries, bit 16 a NaN was made; nonzero bits 8-16: some row may hold a value
+                    matchProperties never matches */
     int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
     int64_t tStart, tEnd; /* the last replay kernel's start / end for this document (s_memrealtime ticks) */
@@ -283,6 +286,10 @@ struct HotT {
     uint16_t ovn[OVB];  /* overlap overflow pool: next block of a chain (0 = end) / of the free list */
     int8_t _pad2[(16 - (2 * K_ + 2 * OVB) % 16) % 16];
     uint64_t ovp[OVB];  /* 8 more removedClientOverlap entries (short id + 1) per block */
+    /* derived property values (incr / consensus, mt_oplog.h MT_VALUE_DERIVED): STRCAT entries {base id | k << 16}
+     * (String(base) + "undefined" x k) and consensus objects' seqs, interned by content per document */
+    int32_t dvs[128];
+    int32_t dvc[128];
     TileState<N_, TILED_> tl;
 };
 
@@ -378,6 +385,8 @@ struct Pools {
     const uint16_t* text;
     const mt_props_rec* props;
     const mt_kv* kv;
+    const uint8_t* vkind = nullptr; /* per value id its MT_VKIND_* (mt_engine_set_value_kinds), nvk entries */
+    int32_t nvk = 0;
 };
 
 /* Phase clock for the profiling build only (-DMT_PROF, tools/phase_profile.py): shader-clock
@@ -491,6 +500,8 @@ struct Replica {
     int32_t zq = 0, zms = 0; /* zamboniSegments calls queued by the record being applied, the first's minSeq */
     bool runOnly = false;      /* range_op_tiled: find and split only, leaving the run's first / last slot in */
     int32_t runA = -1, runB = -1; /* runA / runB for remove_run (no visit) */
+    const uint8_t* vk = nullptr; /* the value kinds of the replay's Pools (combine_value) */
+    int32_t nvk = 0;
 
     MT_HD Replica(const Doc<HT>& doc, const W& wave)
         : d(doc), z(*doc.t), w(wave), zh(&z.h), keys(z.keys), l2s(z.l2s), s2l(z.s2l), lo(z.lorder), lp(z.lpos), npar(z.nparent), nch(z.nchild), nlev(z.nlevel),
@@ -3252,9 +3263,9 @@ struct Replica {
                         continue;
                     }
                 }
-                if (comb >= MT_COMBINE_INCR) { /* combine_unsupported: latched, or the value stays */
-                    if (combine_unsupported(comb, w.bcast(pv, k))) break;
-                    continue;
+                if (comb >= MT_COMBINE_INCR) { /* Properties.combine (combine_value) */
+                    vj = combine_value(comb, w.bcast(pv, k), seq);
+                    if (vj < 0) break;
                 }
                 pv = w.writelane(vj, k, pv);
             }
@@ -3275,14 +3286,63 @@ struct Replica {
         w.sync();
     }
     /* Properties.combine (properties.ts:26-59) as addProperties calls it (segmentPropertiesManager.ts:96-97): with
-     * newValue still undefined. "incr" makes the key's value NaN (current + undefined; a string
-     * gets "undefined" appended); "consensus" over an absent value (no defaultValue: wire.py refuses one) makes an
-     * {value: undefined, seq} object, over a present one returns it unchanged. Values the engine cannot hold latch
-     * E_UNSUPPORTED (true); an unchanged value is kept (false). */
-    MT_HD bool combine_unsupported(int32_t comb, int32_t cur) {
-        if (comb == MT_COMBINE_CONSENSUS && cur != 0) return false;
+     * newValue still undefined, and no defaultValue / minValue (wire.py and the facade refuse
+     * them). "incr": current + undefined — NaN from nothing, NaN, a number or a boolean; the string + "undefined"
+     * from a string or a consensus object ("[object Object]undefined"; an interned object or array: refused, its
+     * String() has no canonical base). "consensus":
+     * a present value unchanged (cv.seq === -1 only for an object a local consensus made, which the engine refuses);
+     * over nothing a {value: undefined, seq} object. Returns the key's new value id, or -1 (latched: an incr over a
+     * value of undeclared kind, E_UNSUPPORTED; a full table of derived values, E_CAPACITY). */
+    MT_HD int32_t combine_value(int32_t comb, int32_t cur, int32_t seq) {
+        if (comb == MT_COMBINE_CONSENSUS) return cur != 0 ? cur : dv_intern(1, seq);
+        if (cur == 0 || cur == MT_VALUE_NAN) return dv_nan();
+        if (cur >= MT_VALUE_CONS0 && cur < MT_VALUE_NAN) return dv_intern(0, 1 << 16); /* "[object Object]undefined" */
+        if (cur >= MT_VALUE_STRCAT0 && cur < MT_VALUE_CONS0) {
+            int32_t x = z.dvs[cur - MT_VALUE_STRCAT0];
+            if ((uint32_t)x >= 0x7FFF0000u) {
+                fail(E_CAPACITY);
+                return -1;
+            }
+            return dv_intern(0, x + (1 << 16));
+        }
+        const int32_t id = cur & ~MT_VALUE_FALSY;
+        const int32_t kind = id < nvk ? (int32_t)vk[id] : MT_VKIND_UNKNOWN;
+        if (kind == MT_VKIND_NUMERIC) return dv_nan();
+        if (kind == MT_VKIND_STRING) return dv_intern(0, cur | (1 << 16));
         fail(E_UNSUPPORTED);
-        return true;
+        return -1;
+    }
+    MT_HD int32_t dv_nan() {
+        zh->ndv |= 1 << 16;
+        return MT_VALUE_NAN;
+    }
+    /* the per-document entry holding a derived value (cons = 0: STRCAT x; 1: a consensus object of seq x), added if
+     * new; its value id */
+    MT_HD int32_t dv_intern(int32_t cons, int32_t x) {
+        int32_t nd = zh->ndv;
+        const int32_t n = cons ? (nd >> 8) & 0xFF : nd & 0xFF, cap = cons ? 127 : 128;
+        int32_t* tab = cons ? z.dvc : z.dvs;
+#pragma clang loop unroll(disable)
+        for (int32_t i = 0; i < n; i++)
+            if (tab[i] == x) return (cons ? MT_VALUE_CONS0 : MT_VALUE_STRCAT0) + i;
+        if (n >= cap) {
+            fail(E_CAPACITY);
+            return -1;
+        }
+        w.sync();
+        if (w.lane() == 0) tab[n] = x;
+        w.sync();
+        zh->ndv = nd + (cons ? 1 << 8 : 1);
+        return (cons ? MT_VALUE_CONS0 : MT_VALUE_STRCAT0) + n;
+    }
+    /* some key value of 8 slots (4 dwords) is NaN or a consensus object: matchProperties never matches it */
+    MT_HD static bool pv_unmatchable(const I4& v) {
+        bool u = false;
+        for (int q = 0; q < 4; q++) {
+            uint32_t x = (uint32_t)v.x[q];
+            u |= ((x >> 7) & 0x1FFu) == 0xFFu || ((x >> 23) & 0x1FFu) == 0xFFu;
+        }
+        return u;
     }
     /* one key slot's term of the property hash (0 for an absent value): the hash is the sum of the terms */
     MT_HD static int32_t prop_mix(int32_t k, int32_t v) {
@@ -3341,8 +3401,10 @@ struct Replica {
                     continue;
                 }
             }
-            if (comb >= MT_COMBINE_INCR) {
-                if (combine_unsupported(comb, c.pv[k])) return;
+            if (comb >= MT_COMBINE_INCR) { /* Properties.combine (combine_value) */
+                int32_t v = combine_value(comb, c.pv[k], seq);
+                if (v < 0) return;
+                c.pv[k] = (uint16_t)v;
                 continue;
             }
             c.pv[k] = kv[j].value;
@@ -3376,8 +3438,11 @@ struct Replica {
         if (!pa) return true;
         const typename HT::Cold& ca = cold(a);
         const typename HT::Cold& cb = cold(b);
-        for (int i = 0; i < HT::K / 8; i++) /* 8 key slots per 16-byte compare */
-            if (!eq4(ld4((const int32_t*)&ca.pv[8 * i]), ld4((const int32_t*)&cb.pv[8 * i]))) return false;
+        const bool um = (zh->ndv >> 8) != 0; /* NaN or consensus objects exist: never matched (pv_unmatchable) */
+        for (int i = 0; i < HT::K / 8; i++) { /* 8 key slots per 16-byte compare */
+            I4 va = ld4((const int32_t*)&ca.pv[8 * i]);
+            if (!eq4(va, ld4((const int32_t*)&cb.pv[8 * i])) || (um && pv_unmatchable(va))) return false;
+        }
         return true;
     }
 
@@ -3623,6 +3688,9 @@ struct Replica {
             if (pairOk && (fl & RF_PROPS)) { /* matchProperties (properties.ts:61-92) */
                 for (int i = 0; i < HT::K / 8; i++)
                     if (!eq4(ld4((const int32_t*)&ca.pv[8 * i]), ld4((const int32_t*)&cb.pv[8 * i]))) pairOk = false;
+                if (pairOk && (zh->ndv >> 8)) /* NaN and consensus objects never match (pv_unmatchable) */
+                    for (int i = 0; i < HT::K / 8; i++)
+                        if (pv_unmatchable(ld4((const int32_t*)&ca.pv[8 * i]))) pairOk = false;
             }
             if (pairOk && permPair) { /* PermutationSegment.canAppend: handles follow, or both unallocated */
                 uint32_t sa = (uint32_t)tofP, sb = (uint32_t)tofK;
@@ -5776,9 +5844,35 @@ struct Replica {
                         best = k;
                     }
                 }
-                uint16_t kv2[2] = {(uint16_t)bk, cold(s).pv[best]};
+                uint16_t v = cold(s).pv[best];
+                if (v >= MT_VALUE_DERIVED && v < MT_VALUE_NAN) v = v < MT_VALUE_CONS0 ? MT_VALUE_STRCAT0 : MT_VALUE_CONS0;
+                uint16_t kv2[2] = {(uint16_t)bk, v};
                 put_bytes(o, kv2, 4);
                 last = bk;
+            }
+            if (zh->ndv & 0xFFFF) { /* derived values' contents, in pair order (mt_oplog.h) */
+                last = -1;
+                for (int q = 0; q < np; q++) {
+                    int32_t best = -1, bk = 0x7fffffff;
+                    for (int k = 0; k < HT::K; k++) {
+                        int32_t key = keys[k];
+                        if (cold(s).pv[k] && key > last && key < bk) {
+                            bk = key;
+                            best = k;
+                        }
+                    }
+                    last = bk;
+                    int32_t v = cold(s).pv[best];
+                    if (v < MT_VALUE_DERIVED || v >= MT_VALUE_NAN) continue;
+                    int32_t ab[2];
+                    if (v < MT_VALUE_CONS0) {
+                        int32_t x = z.dvs[v - MT_VALUE_STRCAT0];
+                        ab[0] = x & 0xFFFF, ab[1] = (int32_t)((uint32_t)x >> 16);
+                    } else {
+                        ab[0] = z.dvc[v - MT_VALUE_CONS0], ab[1] = 0;
+                    }
+                    put_bytes(o, ab, 8);
+                }
             }
             if (hnd) {
                 int32_t st = (int32_t)cold(s).toff;
@@ -5800,6 +5894,8 @@ struct Replica {
     /* Apply a whole event stream, one record at a time. */
     MT_HD void replay(const Pools& p) {
         static_assert(sizeof(mt_op_rec) == 32, "op record is 8 dwords");
+        vk = p.vkind;
+        nvk = p.nvk;
         hmax = INT32_MIN; /* the heap's largest maxSeq */
         for (int32_t b = 0; b < h.heapN; b += W::N) {
             int32_t i = b + w.lane();

@@ -26,6 +26,8 @@ struct mth_store {
     Store<HotMat> s3;
     Store<HotHuge> s4;
     uint8_t* mem;
+    uint8_t* vkind; /* value kinds (mth_set_value_kinds; mt_engine_set_value_kinds) */
+    int32_t nvk;
 };
 
 /* call F with a Replica<WaveHost, HT, true> (delta events on) for doc d of the store's profile */
@@ -98,6 +100,7 @@ mth_store* mth_create_fx2(int64_t ndocs, const int32_t* caps6, int32_t dcap, int
 
 void mth_destroy(mth_store* s) {
     if (!s) return;
+    free(s->vkind);
     free(s->mem);
     free(s);
 }
@@ -109,7 +112,9 @@ void mth_start_collab(mth_store* s, int64_t doc, int32_t long_id, int32_t min_se
 int32_t mth_apply(mth_store* s, int64_t doc, const mt_op_rec* op, const uint16_t* text, const mt_props_rec* props,
                   const mt_kv* kv) {
     return with_replica(s, doc, [&](auto& r) {
-        Pools p = {op, 1, text, props, kv};
+        Pools p = {op, 1, text, props, kv, s->vkind, s->nvk};
+        r.vk = s->vkind;
+        r.nvk = s->nvk;
         r.apply(*op, p);
         return r.h.err;
     });
@@ -118,10 +123,17 @@ int32_t mth_apply(mth_store* s, int64_t doc, const mt_op_rec* op, const uint16_t
 int32_t mth_replay(mth_store* s, int64_t doc, const mt_op_rec* ops, int64_t n, const uint16_t* text,
                    const mt_props_rec* props, const mt_kv* kv) {
     return with_replica(s, doc, [&](auto& r) {
-        Pools p = {ops, n, text, props, kv};
+        Pools p = {ops, n, text, props, kv, s->vkind, s->nvk};
         r.replay(p);
         return r.h.err;
     });
+}
+
+void mth_set_value_kinds(mth_store* s, const uint8_t* kinds, int32_t n) {
+    free(s->vkind);
+    s->vkind = n > 0 ? (uint8_t*)malloc((size_t)n) : nullptr;
+    if (n > 0) memcpy(s->vkind, kinds, (size_t)n);
+    s->nvk = n > 0 ? n : 0;
 }
 
 int32_t mth_error(mth_store* s, int64_t doc) {

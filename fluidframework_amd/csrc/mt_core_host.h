@@ -21,6 +21,7 @@ int32_t mth_apply(mth_store* s, int64_t doc, const mt_op_rec* op, const uint16_t
                   const mt_kv* kv);
 int32_t mth_replay(mth_store* s, int64_t doc, const mt_op_rec* ops, int64_t n, const uint16_t* text,
                    const mt_props_rec* props, const mt_kv* kv);
+void mth_set_value_kinds(mth_store* s, const uint8_t* kinds, int32_t n);
 int32_t mth_error(mth_store* s, int64_t doc);
 int32_t mth_error_op(mth_store* s, int64_t doc);
 int32_t mth_length(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client);

@@ -128,6 +128,8 @@ struct ReplayAux {
     int64_t doc0; /* a launch over documents [doc0, doc0 + grid): the chunked submit (mt_engine_submit_run) */
     int32_t compact; /* the staged pools are indexed by launch position, not by document (mt_engine_submit_docs:
                         `order` lists the documents with records) */
+    const uint8_t* vkind; /* value kinds (mt_engine_set_value_kinds), nvk entries */
+    int32_t nvk;
 };
 __device__ inline int64_t aux_doc(const ReplayAux& a) {
     const int64_t b = a.doc0 + (int64_t)blockIdx.x;
@@ -186,6 +188,8 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
     p.text = text + text_off[pi];
     p.props = props + props_off[pi];
     p.kv = kv + kv_off[pi];
+    p.vkind = aux.vkind;
+    p.nvk = aux.nvk;
     Doc<HT> v = st.doc(d);
     if constexpr (LDS) {
         __shared__ __attribute__((aligned(16))) HT hot;
@@ -429,6 +433,8 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     p.text = text + text_off[pi];
     p.props = props + props_off[pi];
     p.kv = kv + kv_off[pi];
+    p.vkind = aux.vkind;
+    p.nvk = aux.nvk;
     if (!replayer) {
         tiled_prefetch<HT>(v, p.ops, p.nops, &pfcur, &pfdone, lcord, lcst, lccnt, &pfsink);
     } else if (!fits) {
@@ -827,6 +833,10 @@ struct mt_engine {
     int64_t nsub = -1;
     DevBuf sub;
     std::vector<int64_t> h_sub;
+    /* the host's value kinds (mt_engine_set_value_kinds) */
+    DevBuf vkind;
+    int32_t nvk = 0;
+    std::vector<uint8_t> h_vkind;
     hipStream_t run_stream = nullptr;
     /* mt_engine_submit_run: the copy stream, the second compute stream, and pinned staging buffers for pageable
      * sources (each with the event of the last copy out of it) */
@@ -903,7 +913,8 @@ static inline int32_t launch_replay(mt_engine* e, K kern, int block = WG) {
                        e->ndocs, (const mt_op_rec*)e->ops_buf.p, (const int64_t*)e->op_off.p, (const uint16_t*)e->text.p,
                        (const int64_t*)e->text_off.p, (const mt_props_rec*)e->props.p, (const int64_t*)e->props_off.p,
                        (const mt_kv*)e->kv.p, (const int64_t*)e->kv_off.p,
-                       ReplayAux{(uint64_t*)e->prof.p, order, e->run_d0, e->nsub >= 0 ? 1 : 0});
+                       ReplayAux{(uint64_t*)e->prof.p, order, e->run_d0, e->nsub >= 0 ? 1 : 0,
+                                 (const uint8_t*)e->vkind.p, e->nvk});
     return launch_check(e, "k_replay");
 }
 

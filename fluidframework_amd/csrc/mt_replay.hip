@@ -281,7 +281,7 @@ void mt_engine_destroy(mt_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->borrowed) e->text.p = e->props.p = e->kv.p = nullptr; /* the parent's */
     DevBuf* bufs[] = {&e->ops_buf, &e->op_off, &e->text, &e->text_off, &e->props,     &e->props_off,
-                      &e->kv,     &e->kv_off, &e->tmp,  &e->local_ids, &e->prof, &e->order, &e->sub};
+                      &e->kv,     &e->kv_off, &e->tmp,  &e->local_ids, &e->prof, &e->order, &e->sub, &e->vkind};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (e->mem) (void)hipFree(e->mem);
@@ -698,6 +698,7 @@ static int32_t promote(mt_engine* e) {
     }
     o->promote = e->promote;
     o->wide = e->profile == 4; /* HotHuge -> HotHuge: the same layout, the wide kernel */
+    if (e->nvk && (rc = mt_engine_set_value_kinds(o, e->h_vkind.data(), e->nvk))) return rc;
     if (e->collab) {
         std::vector<int32_t> loc((size_t)(3 * m)); /* the promoted documents' ids, minSeqs, currentSeqs */
         for (int64_t i = 0; i < m; i++)
@@ -779,6 +780,19 @@ int32_t mt_engine_set_order(mt_engine* e, const int32_t* order) {
     if (ensure(e, e->order, sizeof(int32_t) * e->ndocs)) return MT_E_NOMEM;
     HIPCHK(e, hipMemcpyAsync(e->order.p, order, sizeof(int32_t) * e->ndocs, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return MT_OK;
+}
+
+int32_t mt_engine_set_value_kinds(mt_engine* e, const uint8_t* kinds, int32_t n) {
+    if (!e || n < 0 || (n && !kinds) || n > MT_VALUE_DERIVED) return MT_E_ARG;
+    HIPCHK(e, hipSetDevice(e->device));
+    int32_t rc = ensure(e, e->vkind, (size_t)std::max(n, 1));
+    if (rc) return rc;
+    e->h_vkind.assign(kinds, kinds + n);
+    if (n) HIPCHK(e, hipMemcpyAsync(e->vkind.p, kinds, (size_t)n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->nvk = n;
+    if (e->over) return mt_engine_set_value_kinds(e->over, kinds, n); /* promoted documents replay there */
     return MT_OK;
 }
 

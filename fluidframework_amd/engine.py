@@ -74,6 +74,7 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_doc_times.argtypes = [vp, vp]
         L.mt_engine_set_order.argtypes = [vp, vp]
         L.mt_engine_set_variant.argtypes = [vp, i32, i32]
+        L.mt_engine_set_value_kinds.argtypes = [vp, vp, i32]
         L.mt_engine_sync.argtypes = [vp]
         L.mt_engine_promoted.argtypes = [vp, vp, i64]
         L.mt_engine_promoted.restype = i64
@@ -154,6 +155,11 @@ class Engine:
             self.set_variant(MT_VAR_SMALL_WAVES, waves)
         if wide is not None:
             self.set_variant(MT_VAR_TILED_WIDE, int(bool(wide)))
+
+    def set_value_kinds(self, kinds):
+        """What an incr annotate makes of each value id (oplog.value_kinds(interner); mt_engine_set_value_kinds)."""
+        k = np.ascontiguousarray(kinds, np.uint8)
+        self._check(self.L.mt_engine_set_value_kinds(self.h, _p(k), len(k)), "set_value_kinds")
 
     def set_variant(self, key: int, value: int):
         """Kernel build selection (include/mt_engine.h mt_engine_set_variant); results do not depend on it."""

@@ -37,6 +37,8 @@ const SEG = { TEXT: 0, MARKER: 1, PERM: 2 };
 const SEG_RELPOS = 0x80; // positions relative to markers (mt_oplog.h MT_SEG_RELPOS)
 const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
 const VALUE_FALSY = 0x8000;
+/* values the engine derives from incr / consensus (include/mt_oplog.h MT_VALUE_DERIVED ..) */
+const VALUE_DERIVED = 0x7F00, VALUE_STRCAT0 = 0x7F00, VALUE_CONS0 = 0x7F80, VALUE_NAN = 0x7FFF;
 const ERRORS = { 1: "MergeTree insert failed", 2: "assertion", 3: "invalid op range", 4: "unsupported",
     5: "capacity exceeded" };
 
@@ -60,9 +62,22 @@ class Interner {
         if (v === null || v === undefined) return 0;
         const s = canonical(v);
         let i = this.values.get(s);
-        if (i === undefined) { i = this.nv++; this.values.set(s, i); }
+        if (i === undefined) {
+            if (this.nv >= VALUE_DERIVED) throw new Error("too many distinct property values");
+            i = this.nv++;
+            this.values.set(s, i);
+        }
         const falsy = typeof v !== "object" && !v;
         return i | (falsy ? VALUE_FALSY : 0);
+    }
+    /* include/mt_oplog.h MT_VKIND_* per value id (mt_engine_set_value_kinds): what an incr annotate makes of it */
+    kinds() {
+        const k = new Uint8Array(this.nv);
+        for (const [sv, i] of this.values) {
+            const v = JSON.parse(sv);
+            k[i] = typeof v === "number" || typeof v === "boolean" ? 1 : typeof v === "string" ? 2 : 0;
+        }
+        return k;
     }
 }
 
@@ -136,14 +151,27 @@ function decodeDump(bytes, interner, nameOf) {
         const np = dv.getUint16(o, true), refType = dv.getUint16(o + 2, true);
         o += 4;
         let properties;
+        const pairs = [];
+        for (let k = 0; k < np; k++) pairs.push([dv.getUint16(o + 4 * k, true), dv.getUint16(o + 4 * k + 2, true)]);
+        o += 4 * np;
         if (flags & 1) {
             properties = {};
-            for (let k = 0; k < np; k++) {
-                const v = dv.getUint16(o + 4 * k + 2, true) & ~VALUE_FALSY;
-                properties[keyName.get(dv.getUint16(o + 4 * k, true))] = v === 0 ? null : valueOf.get(v);
+            for (const [key, raw] of pairs) {
+                let val;
+                if (raw === VALUE_NAN) {
+                    val = NaN;
+                } else if (raw === VALUE_STRCAT0 || raw === VALUE_CONS0) { // contents follow the pairs (mt_oplog.h)
+                    const a = dv.getInt32(o, true), b = dv.getInt32(o + 4, true);
+                    o += 8;
+                    val = raw === VALUE_CONS0 ? { value: undefined, seq: a }
+                        : (a === 0 ? "[object Object]" : String(valueOf.get(a & ~VALUE_FALSY))) + "undefined".repeat(b);
+                } else {
+                    const v = raw & ~VALUE_FALSY;
+                    val = v === 0 ? null : valueOf.get(v);
+                }
+                properties[keyName.get(key)] = val;
             }
         }
-        o += 4 * np;
         let start = HANDLE_UNALLOCATED;
         if (flags & 16) { start = dv.getInt32(o, true); o += 4; }
         const seg = {
@@ -194,6 +222,7 @@ class ReplayEngine {
         this.pending = Array.from({ length: ndocs }, () => []); // op types in flight, per pending group
         this.version = 0; // bumped by every enqueued record and every collaboration start: cached reads expire
         this.dirty = new Set(); // documents with queued records
+        this.kindsSent = 0; // interner values whose kinds the engine has
     }
 
     longIndex(name) {
@@ -323,6 +352,10 @@ class ReplayEngine {
         });
         opOff[m] = BigInt(ro); textOff[m] = BigInt(to);
         propsOff[m] = BigInt(po); kvOff[m] = BigInt(ko);
+        if (this.interner.nv !== this.kindsSent) { // the value kinds an incr annotate needs (mt_engine_set_value_kinds)
+            addon.setValueKinds(this.h, this.interner.kinds());
+            this.kindsSent = this.interner.nv;
+        }
         addon.submitDocs(this.h, docs, ops, opOff, text, textOff, props, propsOff, kv, kvOff);
         addon.run(this.h);
         addon.sync(this.h);

@@ -226,6 +226,19 @@ static napi_value js_submit_docs(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+/* setValueKinds(h, Uint8Array kinds): MT_VKIND_* per value id (mt_engine_set_value_kinds) */
+static napi_value js_set_value_kinds(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mt_engine* e = engine_of(env, argv[0]);
+    void* k;
+    size_t n;
+    if (!e || !view_of(env, argv[1], &k, &n, napi_uint8_array)) return nullptr;
+    int32_t rc = mt_engine_set_value_kinds(e, (const uint8_t*)k, (int32_t)n);
+    if (rc) return throw_status(env, e, rc, "mt_engine_set_value_kinds");
+    return nullptr;
+}
+
 /* docError(h, doc) -> [err, errOp] of one document (mt_engine_doc_error) */
 static napi_value js_doc_error(napi_env env, napi_callback_info info) {
     napi_value argv[2];
@@ -623,7 +636,7 @@ static napi_value init(napi_env env, napi_value exports) {
                {"resolveRemoteClientPosition", js_resolve_remote}, {"adjustPosition", js_adjust_position},
                {"handleToPosition", js_handle_to_position}, {"getMarkerFromId", js_marker_from_id},
                {"dump", js_dump},           {"segmentIds", js_segment_ids},
-               {"submitDocs", js_submit_docs}, {"docError", js_doc_error}};
+               {"submitDocs", js_submit_docs}, {"docError", js_doc_error}, {"setValueKinds", js_set_value_kinds}};
     for (auto& f : fns) {
         napi_value fn;
         NAPI_OK(napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn));

@@ -11,7 +11,7 @@ from __future__ import annotations
 import json
 import struct
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, NamedTuple, Optional, Sequence
 
 import numpy as np
 
@@ -88,7 +88,7 @@ class Interner:
         i = self.value_ids.get(s)
         if i is None:
             i = len(self.values)
-            if i >= VALUE_FALSY:
+            if i >= VALUE_DERIVED:  # the ids above are the engine's derived values (mt_oplog.h)
                 raise ValueError("too many distinct property values")
             self.values.append(s)
             self.value_ids[s] = i
@@ -159,6 +159,44 @@ def decode_deltas(words):
     return out
 
 
+# values the engine derives from incr / consensus annotates (include/mt_oplog.h MT_VALUE_DERIVED ..): host interners
+# stay below VALUE_DERIVED; a dump writes each by its kind, its contents after the segment's pairs
+VALUE_DERIVED, VALUE_STRCAT0, VALUE_CONS0, VALUE_NAN = 0x7F00, 0x7F00, 0x7F80, 0x7FFF
+VKIND_UNKNOWN, VKIND_NUMERIC, VKIND_STRING = 0, 1, 2
+
+
+class Derived(NamedTuple):
+    """A property value Properties.combine made (properties.ts:26-59, newValue undefined): "nan"; "strcat": String(
+    value a) + "undefined" x b (a = 0: a consensus object's "[object Object]"); "cons": {value: undefined, seq: a}."""
+    kind: str
+    a: int
+    b: int
+
+
+def derived_json(d: "Derived", interner: "Interner") -> Any:
+    """The value JSON.stringify gives a derived value (SnapshotV1 serializes properties as JSON): NaN -> null, a
+    consensus object -> {"seq": seq} (`value` undefined is dropped), a string as itself."""
+    if d.kind == "nan":
+        return None
+    if d.kind == "cons":
+        return {"seq": d.a}
+    base = "[object Object]" if d.a == 0 else interner.value_obj(d.a)
+    return base + "undefined" * d.b
+
+
+def value_kinds(interner: "Interner") -> np.ndarray:
+    """MT_VKIND_* per value id of an interner (mt_engine_set_value_kinds): numbers and booleans NUMERIC (incr makes
+    NaN), strings STRING (incr appends "undefined"); objects and arrays stay UNKNOWN (an incr over one latches
+    MT_E_UNSUPPORTED: String() of one can equal a string's, so the derived value would have no canonical base)."""
+    k = np.zeros(len(interner.values), np.uint8)
+    for i, sv in enumerate(interner.values):
+        if i == 0:
+            continue
+        v = json.loads(sv)
+        k[i] = VKIND_NUMERIC if isinstance(v, (bool, int, float)) else VKIND_STRING if isinstance(v, str) else 0
+    return k
+
+
 # canonical-dump segment flag bits (include/mt_oplog.h MT_DF_*)
 DF_HAS_PROPS, DF_REMOVED, DF_LSEQ, DF_LRSEQ, DF_HANDLE = 1, 2, 4, 8, 16
 HANDLE_UNALLOCATED = -0x80000000  # Handle.unallocated (matrix handletable.ts:11)
@@ -180,6 +218,13 @@ def parse_dump(b: bytes):
         off += 4
         props = [struct.unpack_from("<2H", b, off + 4 * k) for k in range(nprops)]
         off += 4 * nprops
+        for k, (key, v) in enumerate(props):  # derived values' contents follow the pairs (mt_oplog.h)
+            if v in (VALUE_STRCAT0, VALUE_CONS0):
+                a, c = struct.unpack_from("<2i", b, off)
+                off += 8
+                props[k] = (key, Derived("strcat", a, c) if v == VALUE_STRCAT0 else Derived("cons", a, 0))
+            elif v == VALUE_NAN:
+                props[k] = (key, Derived("nan", 0, 0))
         start = HANDLE_UNALLOCATED
         if flags & DF_HANDLE:  # an allocated PermutationSegment start (mt_oplog.h MT_DF_HANDLE)
             (start,) = struct.unpack_from("<i", b, off)

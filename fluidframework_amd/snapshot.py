@@ -38,7 +38,8 @@ def _js(v: Any) -> str:
 def _props(seg, interner: ol.Interner) -> Optional[Dict[str, Any]]:
     if not seg["flags"] & 1:  # MT_DF_HAS_PROPS: properties !== undefined
         return None
-    return {interner.key_str(k): interner.value_obj(v) for k, v in seg["props"]}
+    return {interner.key_str(k): ol.derived_json(v, interner) if isinstance(v, ol.Derived) else interner.value_obj(v)
+            for k, v in seg["props"]}
 
 
 def _json_spec(seg, props):

@@ -88,6 +88,10 @@ int32_t mt_engine_submit_docs(mt_engine* e, int64_t m, const int64_t* docs, cons
                               const uint16_t* text, int64_t text_units, const int64_t* text_off,
                               const mt_props_rec* props, int64_t nprops, const int64_t* props_off, const mt_kv* kv,
                               int64_t nkv, const int64_t* kv_off);
+/* The kind of each property value id (MT_VKIND_*, kinds[id & ~MT_VALUE_FALSY], n entries): what an "incr" combining
+ * annotate makes of a key holding it (properties.ts:26-59: current + undefined). Without it an incr over a present
+ * interned value latches MT_E_UNSUPPORTED. Takes effect at the next run. */
+int32_t mt_engine_set_value_kinds(mt_engine* e, const uint8_t* kinds, int32_t n);
 /* Pinned (page-locked) host memory for op logs a caller builds in place: the hand-off then copies by DMA alone. */
 int32_t mt_host_alloc(int64_t bytes, void** out);
 void mt_host_free(void* p);

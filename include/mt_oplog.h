@@ -135,8 +135,13 @@ enum {
     MT_COMBINE_REWRITE = 1,
     /* "incr" / "consensus" (properties.ts:26-59) as addProperties applies them (segmentPropertiesManager.ts:92-106:
      * every key is modified, pending local updates notwithstanding, and combine gets newValue undefined, SURVEY
-     * Appendix A2): incr makes the value NaN, consensus over an absent value a {value: undefined, seq} object —
-     * both latch MT_E_UNSUPPORTED where the reference computes them; consensus over a present value keeps it. */
+     * Appendix A2): incr makes the value `current + undefined` — NaN from a number, a boolean or nothing, the string
+     * with "undefined" appended from a string or a consensus object ("[object Object]") — and consensus over an absent
+     * value a {value: undefined, seq} object; consensus over a present value keeps it. The values the engine derives
+     * this way are per-document (MT_VALUE_NAN, MT_VALUE_STRCAT0.., MT_VALUE_CONS0..); telling numbers from strings
+     * takes the host's value kinds (mt_engine_set_value_kinds): an incr over a value of undeclared kind latches
+     * MT_E_UNSUPPORTED, as does a local consensus annotate (its ack needs annotateMarkerNotifyConsensus's pending
+     * consensus, client.ts:982-989). */
     MT_COMBINE_INCR = 2,
     MT_COMBINE_CONSENSUS = 3,
 };
@@ -168,6 +173,18 @@ typedef struct mt_props_rec {
 /* value ids carrying this bit are falsy JSON values (0, "", false); relevant to `rewrite`
  * (segmentPropertiesManager.ts:72: `!newProps[key]`) */
 #define MT_VALUE_FALSY 0x8000
+/* Values the engine derives from incr / consensus (never in op records; host interners stay below
+ * MT_VALUE_DERIVED): NaN; a string String(base) + "undefined" x k (per-document table entries MT_VALUE_STRCAT0 + i);
+ * a {value: undefined, seq} consensus object (entries MT_VALUE_CONS0 + i). matchProperties (properties.ts:61-92)
+ * never matches NaN (NaN !== NaN) or a consensus object (its `value` is undefined), so a row holding either never
+ * takes an append in zamboni. */
+#define MT_VALUE_DERIVED 0x7F00
+#define MT_VALUE_STRCAT0 0x7F00 /* 128 entries */
+#define MT_VALUE_CONS0 0x7F80   /* 127 entries */
+#define MT_VALUE_NAN 0x7FFF
+/* value kinds the host declares per value id (mt_engine_set_value_kinds): what `value + undefined` makes */
+/* (an object or array stays UNKNOWN: String() of one can equal a string's, so `it + undefined` has no canonical base) */
+enum { MT_VKIND_UNKNOWN = 0, MT_VKIND_NUMERIC = 1 /* number, boolean: NaN */, MT_VKIND_STRING = 2 /* a string */ };
 
 typedef struct mt_kv {
     uint16_t key;
@@ -182,7 +199,11 @@ typedef struct mt_kv {
  * record: uint8 kind; uint8 flags; uint8 noverlap; uint8 ngroups;
  *         int32 len, seq, client, removedSeq, removedClient, localSeq, localRemovedSeq, leaf;
  *         int32 overlap[noverlap];
- *         uint16 nprops; uint16 refType; (key,value) x nprops sorted by key id;
+ *         uint16 nprops; uint16 refType; (key,value) x nprops sorted by key id, a derived value (MT_VALUE_DERIVED..)
+ *         written by its kind — MT_VALUE_STRCAT0, MT_VALUE_CONS0 or MT_VALUE_NAN — not its per-document entry;
+ *         then, for each pair whose value is MT_VALUE_STRCAT0 or MT_VALUE_CONS0, in pair order: int32 a, int32 b
+ *         (STRCAT: the base value id, 0 = a consensus object's "[object Object]", and the count of "undefined"s;
+ *         CONS: the object's seq, 0) — a dump with no derived value is unchanged;
  *         int32 start (MT_DF_HANDLE only: a PermutationSegment's allocated handle, permutationvector.ts:38);
  *         text: len x uint16 (text segments only)
  * client fields are LONG client indices; -1 = the reference's "original" (LocalClientId).

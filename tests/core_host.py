@@ -40,6 +40,7 @@ def lib():
         L.mth_apply.argtypes = [vp, i64, vp, vp, vp, vp]
         L.mth_replay.argtypes = [vp, i64, vp, i64, vp, vp, vp]
         L.mth_error.argtypes = [vp, i64]
+        L.mth_set_value_kinds.argtypes = [vp, vp, i32]
         L.mth_error_op.argtypes = [vp, i64]
         L.mth_length.argtypes = [vp, i64, i32, i32]
         L.mth_length_local.argtypes = [vp, i64]
@@ -79,6 +80,10 @@ class HostStore:
         if getattr(self, "h", None):
             self.L.mth_destroy(self.h)
             self.h = None
+
+    def set_value_kinds(self, kinds):
+        self._vk = np.ascontiguousarray(kinds, np.uint8)
+        self.L.mth_set_value_kinds(self.h, _p(self._vk), len(self._vk))
 
     def start_collab(self, doc, long_id, min_seq=0, cur_seq=0):
         self.L.mth_start_collab(self.h, doc, long_id, min_seq, cur_seq)
@@ -172,9 +177,12 @@ class HostStore:
         return dict(zip(("nleaf", "hw_slots", "hw_heap", "heap", "mem", "arena_top", "nodes", "ops"), out.tolist()))
 
 
-def replay_batch(batch: ol.Batch, caps=DEFAULT_CAPS, dcap: int = 0, rcap: int = 0, pcap: int = 0):
-    """Replay every document of a batch on the host core; returns (digests, errors, store)."""
+def replay_batch(batch: ol.Batch, caps=DEFAULT_CAPS, dcap: int = 0, rcap: int = 0, pcap: int = 0, kinds=None):
+    """Replay every document of a batch on the host core; returns (digests, errors, store). `kinds`: the value
+    kinds (oplog.value_kinds) incr annotates need."""
     st = HostStore(batch.ndocs, caps, dcap, rcap, pcap)
+    if kinds is not None:
+        st.set_value_kinds(kinds)
     dig = np.zeros(batch.ndocs, np.uint64)
     err = np.zeros(batch.ndocs, np.int32)
     for d in range(batch.ndocs):

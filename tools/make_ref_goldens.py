@@ -304,7 +304,9 @@ def make_combine(node: str) -> None:
     """tests/golden/refcombine.npz: annotates with combining ops incr / consensus (tests/combine_inject.py) in
     config-3 and config-5 logs, replayed by the reference with tools/ref_replay.mjs --combine-watch: per document the
     first record after which a segment holds a value only Properties.combine makes (NaN, a {value, seq} object;
-    -1: none) and, for the documents with none, the digest of the final replica."""
+    -1: none) and, for the documents with none, the digest of the final replica; the replicas right before that record
+    (prefix digests); and every document's final replica replayed past it, with the derived values dumped by content
+    (final digests, two documents' dumps)."""
     import combine_inject
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     out = {}
@@ -325,6 +327,22 @@ def make_combine(node: str) -> None:
         off = np.fromfile(os.path.join(d, "ref_dump_off.bin"), "<i8")
         dig = np.asarray([fnv1a64(blob[off[i]: off[i + 1]].tobytes()) if first[i] < 0 else 0 for i in range(n)],
                          np.uint64)
+        # the whole logs, every replica dumped with its derived values by content (include/mt_oplog.h
+        # MT_VALUE_DERIVED; tools/ref_replay.mjs derivedOf): the final replicas past the combined values
+        df = os.path.join(SCRATCH, f"combine_{name}_full")
+        write_batch(b, gen.generator_interner(), df)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay.mjs"), ERASED, df], capture_output=True,
+                           text=True)
+        if r.returncode != 0 or json.load(open(os.path.join(df, "ref_err.json")))["errors"]:
+            raise RuntimeError(f"reference full replay failed: {r.stderr[-2000:]}")
+        fb = np.fromfile(os.path.join(df, "ref_dumps.bin"), np.uint8)
+        fo = np.fromfile(os.path.join(df, "ref_dump_off.bin"), "<i8")
+        out[f"{name}_final_digests"] = np.asarray([fnv1a64(fb[fo[i]: fo[i + 1]].tobytes()) for i in range(n)],
+                                                  np.uint64)
+        keep = [i for i in range(n) if first[i] >= 0][:2]  # two documents' full dumps (self-contained vectors)
+        out[f"{name}_keep_docs"] = np.asarray(keep, np.int64)
+        out[f"{name}_keep_dumps"] = np.concatenate([fb[fo[i]: fo[i + 1]] for i in keep])
+        out[f"{name}_keep_dump_off"] = np.cumsum([0] + [int(fo[i + 1] - fo[i]) for i in keep]).astype(np.int64)
         # the replicas right before that record (the prefix [0, first)): pins what the kept values did until then
         pre = ol.Batch.from_arrays([tuple(x if k else x[: (first[i] if first[i] >= 0 else len(x))]
                                           for k, x in enumerate(b.doc_arrays(i))) for i in range(n)], b.local_long_id)
@@ -348,7 +366,7 @@ def make_combine(node: str) -> None:
               f"combined value", flush=True)
     np.savez_compressed(os.path.join(GOLDEN, "refcombine.npz"), **out,
                         source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node "
-                                "by tools/ref_replay.mjs --combine-watch"))
+                                "by tools/ref_replay.mjs (--combine-watch for first / prefix)"))
 
 
 def make_refentry(node: str) -> None:

@@ -489,6 +489,33 @@ async function snapshotDoc(doc, cut, loadLong) {
     return { tree, loaded: dump(b) };
 }
 
+// ---- derived values (include/mt_oplog.h MT_VALUE_DERIVED): what Properties.combine makes with newValue undefined
+// (properties.ts:26-59): NaN; a {value: undefined, seq} consensus object; base + "undefined" x k, base an interned
+// string or a consensus object ("[object Object]", base 0; the engine refuses an incr over an interned object or array,
+// whose String() could equal a string's). [kind marker, a, b] as the canonical dump writes them.
+const VALUE_STRCAT0 = 0x7F00, VALUE_CONS0 = 0x7F80, VALUE_NAN = 0x7FFF;
+const jsStringOf = new Map(); // each interned string -> its id (with the falsy bit)
+values.forEach((sv, i) => {
+    if (i === 0) return;
+    const v = JSON.parse(sv);
+    if (typeof v === "string") jsStringOf.set(v, i | (v === "" ? FALSY : 0));
+});
+function derivedOf(v) {
+    if (typeof v === "number" && Number.isNaN(v)) return [VALUE_NAN];
+    if (v !== null && typeof v === "object" && !Array.isArray(v) && v.value === undefined && typeof v.seq === "number" &&
+        Object.keys(v).every((k) => k === "value" || k === "seq")) return [VALUE_CONS0, v.seq, 0];
+    if (typeof v === "string") {
+        let s = v, k = 0;
+        while (s.endsWith("undefined")) {
+            s = s.slice(0, -9);
+            k++;
+            if (jsStringOf.has(s)) return [VALUE_STRCAT0, jsStringOf.get(s), k];
+            if (s === "[object Object]") return [VALUE_STRCAT0, 0, k];
+        }
+    }
+    return null;
+}
+
 // ---- canonical dump (include/mt_oplog.h; the order and fields of oracle/mt_oracle.c mto_dump) ----
 class Out {
     constructor() { this.parts = []; }
@@ -536,12 +563,22 @@ function dump(client) {
             const pk = hasProps ? Object.keys(s.properties).map((k) => [keyId.get(k), s.properties[k]]).sort((a, b) => a[0] - b[0]) : [];
             o.u16(pk.length);
             o.u16(isMarker ? s.refType : 0);
+            const extra = [];
             for (const [k, v] of pk) {
-                const id = valueId.get(canonical(v));
-                if (k === undefined || id === undefined) throw new Error(`property not in the interner: ${k} ${canonical(v)}`);
+                // NaN first: canonical(NaN) is JSON's "null", the interner's id 0
+                const id = typeof v === "number" && Number.isNaN(v) ? undefined : valueId.get(canonical(v));
+                if (k === undefined) throw new Error(`property key not in the interner: ${k}`);
+                if (id === undefined) { // a value Properties.combine made (include/mt_oplog.h MT_VALUE_DERIVED)
+                    const dv = derivedOf(v);
+                    if (!dv) throw new Error(`property not in the interner: ${k} ${canonical(v)}`);
+                    o.u16(k); o.u16(dv[0]);
+                    if (dv.length > 1) extra.push(dv[1], dv[2]);
+                    continue;
+                }
                 const falsy = v !== null && typeof v !== "object" && !v;
                 o.u16(k); o.u16(id | (falsy ? FALSY : 0));
             }
+            for (const x of extra) o.i32(x);
             if (hnd) o.i32(s.start); // MT_DF_HANDLE
             if (isText) for (let j = 0; j < s.text.length; j++) o.u16(s.text.charCodeAt(j));
         }
