@@ -23,6 +23,11 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#ifndef MT_A32 /* element addressing by 32-bit offsets from the block base (HotT::at32), per array group: 1 leaf lines,
+                  2 row ids / leaves / generations / kids, 4 cold rows, 8 the free-id stack and the membership logs */
+#define MT_A32 0
+#endif
+
 #include <type_traits>
 
 #include "../../include/mt_oplog.h"
@@ -262,6 +267,24 @@ struct HotT {
         uint8_t b[8][4]; /* per slot {cli, rcli, flags, ng}: a quad's byte columns in one 16-byte read */
     };
     Leaf lf[N];
+    /* Per-lane element addresses as the image base + a 32-bit byte offset (the offset in 32-bit arithmetic, then
+     * zero-extended): the GPU compiler keeps the one base pointer (an SGPR pair) and issues each load / store with a
+     * 32-bit per-lane offset (global_load ... v_off, s_base), where a member array indexed directly becomes a
+     * 64-bit address per lane from a base of its own (a hoisted SGPR pair per array, which the 8-waves-per-SIMD
+     * kernel spills). A small negative index stays inside the document's block, as before. */
+    template <class T>
+    MT_HD T& at32(int32_t off) { return *(T*)((uint8_t*)this + (uint64_t)(uint32_t)off); }
+    MT_HD static int32_t lfo(int s, int f) { return (int32_t)offsetof(HotT, lf) + (s >> 3) * 128 + f + (s & 7) * 4; }
+#if MT_A32 & 1
+    MT_HD int32_t& len(int s) { return at32<int32_t>(lfo(s, 0)); }
+    MT_HD int32_t& seq(int s) { return at32<int32_t>(lfo(s, 32)); }
+    MT_HD int32_t& rseq(int s) { return at32<int32_t>(lfo(s, 64)); }
+    MT_HD uint8_t& cli(int s) { return at32<uint8_t>(lfo(s, 96)); }
+    MT_HD uint8_t& rcli(int s) { return at32<uint8_t>(lfo(s, 97)); }
+    MT_HD uint8_t& flags(int s) { return at32<uint8_t>(lfo(s, 98)); }
+    MT_HD uint8_t& ng(int s) { return at32<uint8_t>(lfo(s, 99)); }
+    MT_HD const int32_t* bytes4(int s) { return &at32<const int32_t>(lfo(s, 96)); }
+#else
     MT_HD int32_t& len(int s) { return lf[s >> 3].len[s & 7]; }
     MT_HD int32_t& seq(int s) { return lf[s >> 3].seq[s & 7]; }
     MT_HD int32_t& rseq(int s) { return lf[s >> 3].rseq[s & 7]; }
@@ -270,9 +293,21 @@ struct HotT {
     MT_HD uint8_t& flags(int s) { return lf[s >> 3].b[s & 7][2]; }
     MT_HD uint8_t& ng(int s) { return lf[s >> 3].b[s & 7][3]; }
     MT_HD const int32_t* bytes4(int s) { return (const int32_t*)&lf[s >> 3].b[s & 7][0]; }
+#endif
     IX rid[S];   /* slot -> row id (stable identity of a segment; cold data index) */
     IX rleaf[S]; /* row id -> leaf node currently holding it */
     uint8_t rgen[S]; /* row id -> generation, bumped when the id is freed */
+#if MT_A32 & 2
+    MT_HD IX& RID(int s) { return at32<IX>((int32_t)offsetof(HotT, rid) + s * (int32_t)sizeof(IX)); }
+    MT_HD IX& RLEAF(int r) { return at32<IX>((int32_t)offsetof(HotT, rleaf) + r * (int32_t)sizeof(IX)); }
+    MT_HD uint8_t& RGEN(int r) { return at32<uint8_t>((int32_t)offsetof(HotT, rgen) + r); }
+    MT_HD IX& KIDS(int i) { return at32<IX>((int32_t)offsetof(HotT, kids) + i * (int32_t)sizeof(IX)); }
+#else
+    MT_HD IX& RID(int s) { return rid[s]; }
+    MT_HD IX& RLEAF(int r) { return rleaf[r]; }
+    MT_HD uint8_t& RGEN(int r) { return rgen[r]; }
+    MT_HD IX& KIDS(int i) { return kids[i]; }
+#endif
     IX nparent[N], lorder[N], lpos[N]; /* lorder / lpos: dense leaf order (not used when TILED) */
     IX kids[N * 8];
     int8_t nchild[N], nlevel[N], nscour[N];
@@ -337,6 +372,7 @@ MT_HD constexpr int64_t align256c(int64_t x) { return (x + 255) & ~(int64_t)255;
  * instead of one pointer per region. */
 template <class HT>
 struct Doc {
+    typedef typename HT::IX IX_;
     HT* t;      /* hot image: the block itself, or its LDS copy */
     uint8_t* b; /* the document's global block */
     Caps caps;
@@ -370,6 +406,29 @@ struct Doc {
     MT_HD LColl* colls() const { return (LColl*)(b + off_coll(caps)); }
     MT_HD int32_t* ht() const { return (int32_t*)(b + off_ht(caps)); }
     MT_HD typename HT::Cold* cold() const { return (typename HT::Cold*)(b + OFF_COLD); } /* HT::S records */
+    /* elements by 32-bit offsets from the block base (HotT::at32) */
+    template <class T>
+    MT_HD T& at32(int32_t off) const { return *(T*)(b + (uint64_t)(uint32_t)off); }
+#if MT_A32 & 4
+    MT_HD typename HT::Cold& COLD(int32_t r) const {
+        return at32<typename HT::Cold>((int32_t)OFF_COLD + r * (int32_t)sizeof(typename HT::Cold));
+    }
+#else
+    MT_HD typename HT::Cold& COLD(int32_t r) const { return cold()[r]; }
+#endif
+#if MT_A32 & 8
+    MT_HD IX_& FRID(int32_t i) const { return at32<IX_>((int32_t)OFF_FRID + i * (int32_t)sizeof(IX_)); }
+    MT_HD int32_t& MGID(int32_t i) const { return at32<int32_t>((int32_t)off_mgid(caps) + 4 * i); }
+    MT_HD int32_t& MRID(int32_t i) const { return at32<int32_t>((int32_t)off_mrid(caps) + 4 * i); }
+    MT_HD int32_t& GQ(int32_t i) const { return at32<int32_t>((int32_t)off_gq(caps) + 4 * i); }
+    MT_HD int32_t& GQL(int32_t i) const { return at32<int32_t>((int32_t)off_gql(caps) + 4 * i); }
+#else
+    MT_HD IX_& FRID(int32_t i) const { return frid()[i]; }
+    MT_HD int32_t& MGID(int32_t i) const { return mgid()[i]; }
+    MT_HD int32_t& MRID(int32_t i) const { return mrid()[i]; }
+    MT_HD int32_t& GQ(int32_t i) const { return gq()[i]; }
+    MT_HD int32_t& GQL(int32_t i) const { return gql()[i]; }
+#endif
     MT_HD typename HT::IX* frid() const { return (typename HT::IX*)(b + OFF_FRID); } /* free row-id stack */
     MT_HD uint16_t* arena() const { return (uint16_t*)(b + OFF_ARENA); } /* 2 * acap */
     MT_HD int32_t* mgid() const { return (int32_t*)(b + off_mgid(caps)); }
@@ -541,7 +600,7 @@ struct Replica {
         w.sync();
     }
 
-    MT_HD typename HT::Cold& cold(int32_t s) const { return d.cold()[z.rid[s]]; }
+    MT_HD typename HT::Cold& cold(int32_t s) const { return d.COLD(z.RID(s)); }
     /* cold row of slot a into slot b's row, 16 bytes per load / store */
     MT_HD void copy_cold(int32_t b, int32_t a) {
         const int32_t* src = (const int32_t*)&cold(a);
@@ -606,8 +665,8 @@ struct Replica {
         for (int32_t b = 0; b < HT::S; b += W::N) {
             int32_t i = b + w.lane();
             if (i < HT::S) {
-                d.frid()[i] = (IX)(HT::S - 1 - i);
-                z.rgen[i] = 0;
+                d.FRID(i) = (IX)(HT::S - 1 - i);
+                z.RGEN(i) = 0;
                 z.len(i) = 0;
                 z.seq(i) = 0;
                 z.rseq(i) = 0;
@@ -615,7 +674,7 @@ struct Replica {
                 z.rcli(i) = 0;
                 z.flags(i) = 0;
                 z.ng(i) = 0;
-                z.rid[i] = 0;
+                z.RID(i) = 0;
                 if constexpr (TILED) z.tl.xf[i] = 0;
             }
         }
@@ -749,7 +808,7 @@ struct Replica {
     }
     /* the handles of a row zamboni unlinks */
     MT_HD void ht_unlinked(int32_t rid, int32_t len) {
-        if ((int32_t)d.cold()[rid].toff != 0) ht_free_range((int32_t)d.cold()[rid].toff, len);
+        if ((int32_t)d.COLD(rid).toff != 0) ht_free_range((int32_t)d.COLD(rid).toff, len);
     }
     /* PermutationVector.getAllocatedHandle(pos) (157-183) in the local view: the handle of the row at pos
      * (getMaybeHandle: start + offset when allocated), else walkSegments(pos, pos + 1, splitRange) splits a
@@ -949,7 +1008,7 @@ struct Replica {
         }
         int32_t off = 0;
         int32_t s = containing(pos, h.currentSeq, h.localShort, &off);
-        LRef r = {s >= 0 ? (int32_t)z.rid[s] : REF_DETACHED, s >= 0 ? off : 0, type, 0, -1, 0, 0, 0};
+        LRef r = {s >= 0 ? (int32_t)z.RID(s) : REF_DETACHED, s >= 0 ? off : 0, type, 0, -1, 0, 0, 0};
         if (s >= 0 && entry_kind(r.rid, off) == 1) { /* the reference's addLocalRef throws here: the tree */
             r.rid = REF_GHOST;                            /* is untouched and the reference is not kept */
             d.refs()[n] = r;
@@ -979,7 +1038,7 @@ struct Replica {
         if (r.rid < 0) return;
         if (w.lane() == 0) {
             d.refs()[i].rid = REF_FROZEN - r.rid;
-            d.refs()[i].ek = z.rgen[r.rid];
+            d.refs()[i].ek = z.RGEN(r.rid);
             d.refs()[i].erid = r.rid; /* the entry it leaves stays (localReference.ts:225-264) */
             d.refs()[i].eoff = r.off;
             d.refs()[i].ekd = r.ek;
@@ -1002,14 +1061,14 @@ struct Replica {
         if (start < L) {
             int32_t s = containing(start, refSeq, client, &off);
             if (s >= 0) {
-                tgt = z.rid[s];
+                tgt = z.RID(s);
                 ci = coll_get(tgt, z.len(s));
                 need = 1; /* refsByOffset[0] */
             }
         } else if (L > 0) {
             int32_t s = containing(L - 1, refSeq, client, &off);
             if (s >= 0) {
-                tgt = z.rid[s];
+                tgt = z.RID(s);
                 toff = z.len(s) - 1;
                 ci = coll_get(tgt, z.len(s));
                 need = z.len(s); /* refsByOffset[cachedLength - 1] */
@@ -1279,7 +1338,7 @@ struct Replica {
         z.len(b) = z.len(a);
         z.seq(b) = z.seq(a);
         z.rseq(b) = z.rseq(a);
-        z.rid[b] = z.rid[a];
+        z.RID(b) = z.RID(a);
         st_bytes4(b, ld_bytes4(a));
     }
     /* a slot's {cli, rcli, flags, ng} bytes as one dword (one memory access instead of four) */
@@ -1302,7 +1361,7 @@ struct Replica {
         r.len = z.len(a);
         r.seq = z.seq(a);
         r.rseq = z.rseq(a);
-        r.rid = z.rid[a];
+        r.rid = z.RID(a);
         uint32_t b4 = ld_bytes4(a);
         r.cli = (uint8_t)b4;
         r.rcli = (uint8_t)(b4 >> 8);
@@ -1320,7 +1379,7 @@ struct Replica {
         z.len(b) = r.len;
         z.seq(b) = r.seq;
         z.rseq(b) = r.rseq;
-        z.rid[b] = r.rid;
+        z.RID(b) = r.rid;
         st_bytes4(b, (uint32_t)r.cli | ((uint32_t)r.rcli << 8) | ((uint32_t)r.flags << 16) | ((uint32_t)r.ng << 24));
         if constexpr (TILED) {
             z.tl.xf[b] = r.xf;
@@ -1376,33 +1435,33 @@ struct Replica {
             return 0;
         }
         zh->nfreeRid = n - 1;
-        return d.frid()[n - 1]; /* (a read-ahead of the next entry measured slower: r04l, r04m) */
+        return d.FRID(n - 1); /* (a read-ahead of the next entry measured slower: r04l, r04m) */
     }
     MT_HD void free_rid(int32_t r) {
-        z.rgen[r]++;
-        d.frid()[zh->nfreeRid++] = (IX)r;
+        z.RGEN(r)++;
+        d.FRID(zh->nfreeRid++) = (IX)r;
     }
     /* record leaf n as the holder of its first `cnt` rows */
     MT_HD void set_leaf_of_rows(int32_t n, int32_t cnt) {
         for (int32_t b = 0; b < cnt; b += W::N) {
             int32_t j = b + w.lane();
-            int32_t r = j < cnt ? z.rid[n * MAXN + j] : -1;
-            if (r >= 0) z.rleaf[r] = (IX)n;
+            int32_t r = j < cnt ? z.RID(n * MAXN + j) : -1;
+            if (r >= 0) z.RLEAF(r) = (IX)n;
         }
         w.sync();
     }
     /* slot of a live row id (its leaf is rleaf[rid]); -1 if the id was freed since `gen` */
     MT_HD int32_t slot_of(int32_t rid, int32_t gen) {
-        int32_t g = z.rgen[rid], leaf = z.rleaf[rid]; /* both reads in one round trip */
+        int32_t g = z.RGEN(rid), leaf = z.RLEAF(rid); /* both reads in one round trip */
         if (gen >= 0 && g != (uint8_t)gen) return -1;
         int32_t c = nch[leaf];
         if (W::N == 1) {
             for (int32_t j = 0; j < c; j++)
-                if (z.rid[leaf * MAXN + j] == rid) return leaf * MAXN + j;
+                if (z.RID(leaf * MAXN + j) == rid) return leaf * MAXN + j;
             return -1;
         }
         int32_t j = w.lane();
-        int32_t r = z.rid[leaf * MAXN + (j & (MAXN - 1))]; /* with the child count: one round trip */
+        int32_t r = z.RID(leaf * MAXN + (j & (MAXN - 1))); /* with the child count: one round trip */
         uint64_t m = w.ballot(j < c && r == rid);
         return m ? leaf * MAXN + W::ffs(m) : -1;
     }
@@ -1410,12 +1469,12 @@ struct Replica {
     /* slot_of(ra, -1) and slot_of(rb, -1) with both lookups' reads issued together (two round trips, not four) */
     MT_HD void slot_of2(int32_t ra, int32_t rb, int32_t* sa, int32_t* sb) {
         if constexpr (W::N >= 2 * MAXN) {
-            int32_t la = z.rleaf[ra], lb = z.rleaf[rb];
+            int32_t la = z.RLEAF(ra), lb = z.RLEAF(rb);
             int32_t ca = nch[la], cb = nch[lb];
             const int32_t j = w.lane();
             const bool first = j < MAXN;
             int32_t lf = first ? la : lb;
-            int32_t r = j < 2 * MAXN ? (int32_t)z.rid[lf * MAXN + (j & (MAXN - 1))] : -1;
+            int32_t r = j < 2 * MAXN ? (int32_t)z.RID(lf * MAXN + (j & (MAXN - 1))) : -1;
             uint64_t m = w.ballot(j < 2 * MAXN && (j & (MAXN - 1)) < (first ? ca : cb) && r == (first ? ra : rb));
             uint64_t ma = m & 0xFFull, mb = (m >> MAXN) & 0xFFull;
             *sa = ma ? la * MAXN + W::ffs(ma) : -1;
@@ -1694,7 +1753,7 @@ struct Replica {
             return;
         }
         twrid[t.wN] = rid;
-        twgen[t.wN] = z.rgen[rid];
+        twgen[t.wN] = z.RGEN(rid);
         twslot[t.wN] = s;
         t.wN++;
     }
@@ -1724,7 +1783,7 @@ struct Replica {
             if (z.rseq(s) == NOREM) lst_add(s / MAXN, z.len(s));
         } else {
             z.tl.xf[s] = XF_W;
-            win_add(z.rid[s], s);
+            win_add(z.RID(s), s);
         }
     }
     /* a row just marked removed: leaves the STABLE summaries; W unless the removal is settled */
@@ -1736,7 +1795,7 @@ struct Replica {
         }
         if (!(x & XF_W) && !settled(s)) {
             x = XF_W;
-            win_add(z.rid[s], s);
+            win_add(z.RID(s), s);
         }
         z.tl.xf[s] = x;
     }
@@ -1778,8 +1837,8 @@ struct Replica {
 #pragma unroll
             for (int q = 0; q < NB; q++) {
                 int32_t c = s[q], l = c / MAXN;
-                uint8_t gg = z.rgen[rd[q]]; /* every load of the pass unconditional: they issue together */
-                IX lr = z.rleaf[rd[q]], cr = z.rid[c];
+                uint8_t gg = z.RGEN(rd[q]); /* every load of the pass unconditional: they issue together */
+                IX lr = z.RLEAF(rd[q]), cr = z.RID(c);
                 int32_t cn = nch[l];
                 bool gok = g[q] >= 0 && gg == (uint8_t)g[q];
                 bool hit = gok & (lr == (IX)l) & ((c & (MAXN - 1)) < cn) & (cr == (IX)rd[q]);
@@ -1796,11 +1855,11 @@ struct Replica {
 #pragma unroll
             for (int q = 0; q < NB; q++) { /* the rows that moved: leaf, slot, row */
                 if (s[q] == -2) {
-                    int32_t lf = z.rleaf[rd[q]];
+                    int32_t lf = z.RLEAF(rd[q]);
                     int32_t c = nch[lf];
                     s[q] = -1;
                     for (int32_t j = 0; j < MAXN; j++)
-                        if (j < c && z.rid[lf * MAXN + j] == (IX)rd[q]) s[q] = lf * MAXN + j;
+                        if (j < c && z.RID(lf * MAXN + j) == (IX)rd[q]) s[q] = lf * MAXN + j;
                     if (s[q] >= 0) {
                         rv[q] = row_view(s[q]);
                         lc[q] = t.lch[lf];
@@ -2457,14 +2516,14 @@ struct Replica {
     MT_HD void node_insert_child(int32_t p, int32_t idx, int32_t child) {
         /* interior node p: insert `child` at idx (insertChildNode, mergeTree.ts:2162-2172) */
         int32_t n = nch[p];
-        for (int32_t i = n; i > idx; i--) z.kids[p * MAXN + i] = z.kids[p * MAXN + i - 1];
-        z.kids[p * MAXN + idx] = (IX)child;
+        for (int32_t i = n; i > idx; i--) z.KIDS(p * MAXN + i) = z.KIDS(p * MAXN + i - 1);
+        z.KIDS(p * MAXN + idx) = (IX)child;
         nch[p] = (int8_t)(n + 1);
         npar[child] = (IX)p;
     }
     MT_HD int32_t child_index(int32_t p, int32_t child) const {
         for (int32_t i = 0; i < nch[p]; i++)
-            if (z.kids[p * MAXN + i] == child) return i;
+            if (z.KIDS(p * MAXN + i) == child) return i;
         return -1;
     }
     /* insert leaf `nl` into lorder right after leaf `after` */
@@ -2505,14 +2564,14 @@ struct Replica {
                     w.sync();
                     if (mv) {
                         store_row(nn * MAXN + l, r);
-                        if ((int32_t)r.rid >= 0) z.rleaf[r.rid] = (IX)nn; /* a slot awaiting its row holds -1 */
+                        if ((int32_t)r.rid >= 0) z.RLEAF(r.rid) = (IX)nn; /* a slot awaiting its row holds -1 */
                         z.len(n * MAXN + 4 + l) = 0;
                     }
                 } else {
-                    int32_t c = mv ? (int32_t)z.kids[n * MAXN + 4 + l] : 0;
+                    int32_t c = mv ? (int32_t)z.KIDS(n * MAXN + 4 + l) : 0;
                     w.sync();
                     if (mv) {
-                        z.kids[nn * MAXN + l] = (IX)c;
+                        z.KIDS(nn * MAXN + l) = (IX)c;
                         npar[c] = (IX)nn;
                     }
                 }
@@ -2523,8 +2582,8 @@ struct Replica {
                 clear_slots(n * MAXN + 4, 4);
             } else {
                 for (int32_t i = 0; i < 4; i++) {
-                    int32_t c = z.kids[n * MAXN + 4 + i];
-                    z.kids[nn * MAXN + i] = (IX)c;
+                    int32_t c = z.KIDS(n * MAXN + 4 + i);
+                    z.KIDS(nn * MAXN + i) = (IX)c;
                     npar[c] = (IX)nn;
                 }
             }
@@ -2541,8 +2600,8 @@ struct Replica {
             if (p < 0) {
                 int32_t r = alloc_node((int8_t)(lvl + 1));
                 if (r < 0) return -1;
-                z.kids[r * MAXN + 0] = (IX)n;
-                z.kids[r * MAXN + 1] = (IX)nn;
+                z.KIDS(r * MAXN + 0) = (IX)n;
+                z.KIDS(r * MAXN + 1) = (IX)nn;
                 nch[r] = 2;
                 npar[n] = (IX)r;
                 npar[nn] = (IX)r;
@@ -2554,12 +2613,12 @@ struct Replica {
                  * move right one place from registers */
                 const int32_t l = w.lane();
                 int32_t cnt = nch[p];
-                int32_t kid = l < MAXN ? (int32_t)z.kids[p * MAXN + (l & (MAXN - 1))] : -1;
+                int32_t kid = l < MAXN ? (int32_t)z.KIDS(p * MAXN + (l & (MAXN - 1))) : -1;
                 uint64_t m = w.ballot(l < cnt && kid == n);
                 int32_t idx = (m ? W::ffs(m) : -1) + 1;
                 w.sync();
-                if (l >= idx && l < cnt) z.kids[p * MAXN + l + 1] = (IX)kid;
-                if (l == 0) z.kids[p * MAXN + idx] = (IX)nn;
+                if (l >= idx && l < cnt) z.KIDS(p * MAXN + l + 1) = (IX)kid;
+                if (l == 0) z.KIDS(p * MAXN + idx) = (IX)nn;
                 w.sync();
                 nch[p] = (int8_t)(cnt + 1);
                 npar[nn] = (IX)p;
@@ -2577,7 +2636,7 @@ struct Replica {
         MT_PROF_SCOPE(PH_LEAFINS);
         int32_t c = nch[n];
         slab_shift_right(n, dup ? j - 1 : j, c);
-        z.rid[n * MAXN + j] = -1; /* not a row yet (a leaf split must not re-home it): the caller assigns one */
+        z.RID(n * MAXN + j) = -1; /* not a row yet (a leaf split must not re-home it): the caller assigns one */
         if constexpr (TILED)
             if (!dup) z.tl.xf[n * MAXN + j] = 0;
         nch[n] = (int8_t)(c + 1);
@@ -2660,7 +2719,7 @@ struct Replica {
         HotRow rr = pre ? *pre : load_row(n * MAXN + (l & (MAXN - 1)));
         int32_t c = pre ? preC : nch[n];
         int32_t nfr = zh->nfreeRid;
-        int32_t frr = d.frid()[nfr > 0 ? nfr - 1 : 0];
+        int32_t frr = d.FRID(nfr > 0 ? nfr - 1 : 0);
         uint32_t fl0 = (uint32_t)w.bcast((int32_t)rr.flags, j);
         if (fl0 & RF_MARKER) return s0; /* Marker.createSplitSegmentAt -> undefined */
         int32_t rid0 = w.bcast((int32_t)rr.rid, j), len0 = w.bcast(rr.len, j);
@@ -2678,7 +2737,7 @@ struct Replica {
             w.sync();
             if (mv) store_row(n * MAXN + l + 1 + g, rr);
             w.sync();
-            z.rid[n * MAXN + j + 1] = -1; /* not a row yet (a leaf split must not re-home it) */
+            z.RID(n * MAXN + j + 1) = -1; /* not a row yet (a leaf split must not re-home it) */
             if (g) {
                 if constexpr (TILED) z.tl.xf[n * MAXN + j + 1] = 0;
                 *gapOut = n * MAXN + j + 1;
@@ -2708,8 +2767,8 @@ struct Replica {
         } else {
             rrid = alloc_rid();
         }
-        z.rid[rs] = (IX)rrid;
-        z.rleaf[rrid] = (IX)(rs / MAXN);
+        z.RID(rs) = (IX)rrid;
+        z.RLEAF(rrid) = (IX)(rs / MAXN);
         /* splitAt copies every field (mergeTree.ts:523-567); the right part's text offset (or a PermutationSegment's
          * start + pos, unallocated staying 0) and its length differ */
         uint32_t toff0 = (uint32_t)w.bcast(cv, 2);
@@ -2767,13 +2826,13 @@ struct Replica {
         int32_t ls = n * MAXN + j;
         if (willSplit && j >= 4) ls = rs - 1;
         int32_t rrid = alloc_rid();
-        z.rid[rs] = (IX)rrid;
-        z.rleaf[rrid] = (IX)(rs / MAXN);
+        z.RID(rs) = (IX)rrid;
+        z.RLEAF(rrid) = (IX)(rs / MAXN);
         typename HT::Cold& cl = cold(ls);
-        typename HT::Cold& cr = d.cold()[rrid];
+        typename HT::Cold& cr = d.COLD(rrid);
         copy_cold(rs, ls); /* splitAt copies every field (mergeTree.ts:523-567) */
         if (cl.ovx) ovl_clone(rs, ls);
-        if (refs_on()) refs_split(z.rid[ls], rrid, off);
+        if (refs_on()) refs_split(z.RID(ls), rrid, off);
         int32_t lenL = z.len(ls);
         if (off < lenL) {
             z.len(rs) = lenL - off;
@@ -2791,7 +2850,7 @@ struct Replica {
         h.nrows++;
         zh->sumW += 2;
         if constexpr (TILED) {
-            if (z.tl.xf[rs] & XF_W) win_add(z.rid[rs], rs);
+            if (z.tl.xf[rs] & XF_W) win_add(z.RID(rs), rs);
             if (z.tl.xf[rs] & XF_STABLE) { /* the halves may sit in two leaves after a leaf split */
                 int32_t two[2] = {ls / MAXN, rs / MAXN};
                 leaves_restat(two, rs / MAXN != ls / MAXN ? 2 : 1);
@@ -2800,7 +2859,7 @@ struct Replica {
         /* segmentGroups.copyTo (segmentGroupCollection.ts:37-39): the new segment joins the
          * same pending groups (in the row's FIFO order = log order), appended at the end of each
          * group's segment list */
-        if (z.ng(ls)) split_groups(z.rid[ls], z.rid[rs], z.ng(ls));
+        if (z.ng(ls)) split_groups(z.RID(ls), z.RID(rs), z.ng(ls));
         if (dl_on()) { /* MergeTreeMaintenanceType.SPLIT (mergeTree.ts:2264-2269): [segment, next] */
             dhead(MT_DELTA_SPLIT);
             dseg(-1, z.len(ls));
@@ -2821,12 +2880,12 @@ struct Replica {
      * of each group's segment list */
     MT_HD void split_groups(int32_t lrid, int32_t rrid, int32_t ng) {
         if (zh->memN + ng > d.caps.mcap) mem_compact();
-        int32_t head = zh->gqN ? d.gq()[zh->gqHead] : 0x7fffffff;
+        int32_t head = zh->gqN ? d.GQ(zh->gqHead) : 0x7fffffff;
         int32_t m0 = zh->memN;
         for (int32_t b = 0; b < m0; b += W::N) {
             int32_t i = b + w.lane();
-            int32_t g = i < m0 ? d.mgid()[i] : -1;
-            uint64_t m = w.ballot(i < m0 && d.mrid()[i] == lrid && g >= head);
+            int32_t g = i < m0 ? d.MGID(i) : -1;
+            uint64_t m = w.ballot(i < m0 && d.MRID(i) == lrid && g >= head);
             while (m) {
                 int32_t l = W::ffs(m);
                 m &= m - 1;
@@ -2844,25 +2903,25 @@ struct Replica {
                 return;
             }
         }
-        d.mgid()[m] = gid;
-        d.mrid()[m] = rid;
+        d.MGID(m) = gid;
+        d.MRID(m) = rid;
         zh->memN = m + 1;
     }
     /* drop entries of groups already acked (gid < head gid): wave stream compaction */
     MT_HD void mem_compact() {
-        int32_t head = zh->gqN ? d.gq()[zh->gqHead] : 0x7fffffff;
+        int32_t head = zh->gqN ? d.GQ(zh->gqHead) : 0x7fffffff;
         int32_t n = zh->memN, wpos = 0;
         for (int32_t b = 0; b < n; b += W::N) {
             int32_t i = b + w.lane();
-            int32_t g = i < n ? d.mgid()[i] : -1;
-            int32_t sd = i < n ? d.mrid()[i] : 0;
+            int32_t g = i < n ? d.MGID(i) : -1;
+            int32_t sd = i < n ? d.MRID(i) : 0;
             bool keep = i < n && g >= head;
             int32_t tot;
             int32_t off = w.excl_scan(keep ? 1 : 0, &tot);
             w.sync();
             if (keep) {
-                d.mgid()[wpos + off] = g;
-                d.mrid()[wpos + off] = sd;
+                d.MGID(wpos + off) = g;
+                d.MRID(wpos + off) = sd;
             }
             w.sync();
             wpos += tot;
@@ -2877,7 +2936,7 @@ struct Replica {
             return;
         }
         z.ng(s) = (uint8_t)(ng + 1);
-        mem_append(gid, z.rid[s]);
+        mem_append(gid, z.RID(s));
     }
     /* addToPendingList (mergeTree.ts:1955-1962). Group ids come from a per-document counter, so they
      * increase along the pending queue (acks and compaction compare them with the head's); the ring
@@ -2891,15 +2950,15 @@ struct Replica {
             group_push(localSeq);
             *created = true;
         }
-        row_enqueue_group(s, d.gq()[gq_wrap(zh->gqHead + zh->gqN - 1)]);
+        row_enqueue_group(s, d.GQ(gq_wrap(zh->gqHead + zh->gqN - 1)));
     }
     /* pendingSegments.enqueue of a new group (the caller checked the ring's room) */
     MT_HD void group_push(int32_t localSeq) {
         int32_t gid = zh->gidNext;
         zh->gidNext = gid + 1;
         int32_t q = gq_wrap(zh->gqHead + zh->gqN);
-        d.gq()[q] = gid;
-        d.gql()[q] = localSeq;
+        d.GQ(q) = gid;
+        d.GQL(q) = localSeq;
         zh->gqN++;
     }
 
@@ -2931,7 +2990,7 @@ struct Replica {
         int32_t k = n + 1; /* L[k] (1-based) lives at index k-1 */
         h.heapN = n + 1;
         if (n + 1 > zh->hwHeap) zh->hwHeap = n + 1;
-        uint8_t gen = knownGen >= 0 ? (uint8_t)knownGen : z.rgen[rid];
+        uint8_t gen = knownGen >= 0 ? (uint8_t)knownGen : z.RGEN(rid);
         if (seq >= hmax) { /* every ancestor's maxSeq <= hmax <= seq: the fixup moves nothing (collections.ts:240-247) */
             hmax = seq;
             if (w.lane() == 0) {
@@ -3172,7 +3231,7 @@ struct Replica {
         int32_t n = s / MAXN;
         if (nsc[n] != 1 && seq > h.currentSeq) {
             nsc[n] = 1;
-            heap_add(z.rid[s], seq);
+            heap_add(z.RID(s), seq);
         }
     }
     /* add_lru of a row whose id, generation and leaf's needsScour the caller has read */
@@ -3479,7 +3538,7 @@ struct Replica {
             xa = z.tl.xf[a];
             xb = z.tl.xf[b];
         }
-        append_rows(a, b, z.rid[a], z.rid[b], z.len(a), z.len(b), z.flags(a), z.flags(b), xa, xb);
+        append_rows(a, b, z.RID(a), z.RID(b), z.len(a), z.len(b), z.flags(a), z.flags(b), xa, xb);
     }
     /* append_text with the two rows' ids, lengths, flags and window flags as the caller read them (scour) */
     MT_HD void append_stat(int32_t a, int32_t Lb, uint32_t xa, uint32_t xb) {
@@ -3561,12 +3620,12 @@ struct Replica {
                             dseg(-1, z.len(s));
                             dtail(1);
                         }
-                        if (ht_on() && (z.flags(s) & RF_PERM)) ht_unlinked(z.rid[s], z.len(s));
+                        if (ht_on() && (z.flags(s) & RF_PERM)) ht_unlinked(z.RID(s), z.len(s));
                         if (refs_on()) { /* the segment loses its parent: its references detach */
-                            refs_move(z.rid[s], INT32_MIN, REF_DETACHED, 0);
-                            coll_drop(z.rid[s]);
+                            refs_move(z.RID(s), INT32_MIN, REF_DETACHED, 0);
+                            coll_drop(z.RID(s));
                         }
-                        free_rid(z.rid[s]); /* unlinked */
+                        free_rid(z.RID(s)); /* unlinked */
                     }
                     prev = -1;
                 } else {
@@ -3580,7 +3639,7 @@ struct Replica {
                                   ((z.flags(prev) ^ z.flags(s)) & RF_PROPS) == 0 && match_props(prev, s) &&
                                   can_append(prev, s);
                         if (ok) {
-                            if (refs_on()) refs_append(z.rid[prev], z.rid[s], z.len(prev));
+                            if (refs_on()) refs_append(z.RID(prev), z.RID(s), z.len(prev));
                             append_text(prev, s);
                             if (dl_on()) { /* APPEND (mergeTree.ts:1368-1373): [prevSegment, segment] */
                                 dhead(MT_DELTA_APPEND);
@@ -3588,7 +3647,7 @@ struct Replica {
                                 dseg(-1, z.len(s));
                                 dtail(2);
                             }
-                            free_rid(z.rid[s]);
+                            free_rid(z.RID(s));
                         } else {
                             int32_t dst = n * MAXN + wpos;
                             if (wpos != k) copy_row(dst, s);
@@ -3681,8 +3740,8 @@ struct Replica {
         }
         if (pairOk) {
             const bool permPair = (flP & fl & RF_PERM) != 0;
-            const typename HT::Cold& ca = d.cold()[ridP];
-            const typename HT::Cold& cb = d.cold()[(int32_t)r.rid];
+            const typename HT::Cold& ca = d.COLD(ridP);
+            const typename HT::Cold& cb = d.COLD((int32_t)r.rid);
             tofP = (int32_t)ca.toff;
             tofK = (int32_t)cb.toff;
             if (pairOk && (fl & RF_PROPS)) { /* matchProperties (properties.ts:61-92) */
@@ -3770,7 +3829,7 @@ struct Replica {
                         copy_jobs(jd, js, jn, nj);
                         nj = 0;
                         if (valid && nlen != r.len) z.len(n * MAXN + j) = nlen;
-                        if ((moved >> q) & 1) d.cold()[r.rid].toff = (uint32_t)ntof;
+                        if ((moved >> q) & 1) d.COLD(r.rid).toff = (uint32_t)ntof;
                         moved = 0;
                         w.sync();
                         serial = true;
@@ -3796,7 +3855,7 @@ struct Replica {
         }
 #if MT_APPEND_BATCH
         if (nj) copy_jobs(jd, js, jn, nj);
-        if ((moved >> q) & 1) d.cold()[r.rid].toff = (uint32_t)ntof;
+        if ((moved >> q) & 1) d.COLD(r.rid).toff = (uint32_t)ntof;
 #endif
 #if defined(MT_PROF) && defined(__HIP_DEVICE_COMPILE__)
         uint64_t _t2 = __builtin_amdgcn_s_memtime();
@@ -3843,8 +3902,8 @@ struct Replica {
             uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
             if ((drop >> q) & 1) {
                 int32_t pos = zh->nfreeRid + __builtin_popcountll(drop & below);
-                z.rgen[r.rid]++;
-                d.frid()[pos] = (IX)r.rid;
+                z.RGEN(r.rid)++;
+                d.FRID(pos) = (IX)r.rid;
             }
             int32_t ndrop = __builtin_popcountll(drop);
             zh->nfreeRid += ndrop;
@@ -3888,11 +3947,11 @@ struct Replica {
         {
             int32_t sib[MAXN], cnt[MAXN];
 #pragma unroll
-            for (int32_t i = 0; i < MAXN; i++) sib[i] = i < pc ? z.kids[parent * MAXN + i] : -1;
+            for (int32_t i = 0; i < MAXN; i++) sib[i] = i < pc ? z.KIDS(parent * MAXN + i) : -1;
             scour_par(sib, pc, cnt);
         }
         MT_PROF_SCOPE(PH_P1);
-        int32_t okv = q < pc ? (int32_t)z.kids[parent * MAXN + (q & (MAXN - 1))] : 0; /* lane i: old leaf i */
+        int32_t okv = q < pc ? (int32_t)z.KIDS(parent * MAXN + (q & (MAXN - 1))) : 0; /* lane i: old leaf i */
         int32_t ocv = q < pc ? (int32_t)nch[okv] : 0;                                 /* its rows after scour */
         int32_t total;
         int32_t oex = w.excl_scan(ocv, &total); /* lane i: leaf i's first row in the run of all rows */
@@ -3926,7 +3985,7 @@ struct Replica {
         w.sync();
         if (has) {
             store_row(dst, r);
-            z.rleaf[r.rid] = (IX)(dst / MAXN);
+            z.RLEAF(r.rid) = (IX)(dst / MAXN);
         }
         w.sync();
         if (q < cc) { /* the new leaves' headers, a lane each */
@@ -3962,7 +4021,7 @@ struct Replica {
         }
         h.nleaf = nl + delta;
         if (delta > 0) note_leaves();
-        if (q < cc) z.kids[parent * MAXN + q] = (IX)nkv;
+        if (q < cc) z.KIDS(parent * MAXN + q) = (IX)nkv;
         w.sync();
         nch[parent] = (int8_t)cc;
         return true;
@@ -3983,11 +4042,11 @@ struct Replica {
             int32_t total = 0;
             if constexpr (W::N >= MAXN * MAXN) {
                 int32_t sib[MAXN], cnt[MAXN];
-                for (int32_t i = 0; i < MAXN; i++) sib[i] = i < pc ? z.kids[parent * MAXN + i] : -1;
+                for (int32_t i = 0; i < MAXN; i++) sib[i] = i < pc ? z.KIDS(parent * MAXN + i) : -1;
                 scour_par(sib, pc, cnt);
                 for (int32_t i = 0; i < pc; i++) total += cnt[i];
             } else {
-                for (int32_t i = 0; i < pc; i++) total += scour_leaf(z.kids[parent * MAXN + i]);
+                for (int32_t i = 0; i < pc; i++) total += scour_leaf(z.KIDS(parent * MAXN + i));
             }
             MT_PROF_SCOPE(PH_P1);
             int32_t cc = total / (MAXN / 2);
@@ -3999,7 +4058,7 @@ struct Replica {
             int32_t oldk[MAXN];
             int32_t ocnt[MAXN];
             for (int32_t i = 0; i < pc; i++) {
-                oldk[i] = z.kids[parent * MAXN + i];
+                oldk[i] = z.KIDS(parent * MAXN + i);
                 ocnt[i] = nch[oldk[i]];
             }
             int32_t firstPos = TILED ? 0 : lp[oldk[0]];
@@ -4027,7 +4086,7 @@ struct Replica {
                 w.sync();
                 if (has) {
                     store_row(dst, r);
-                    z.rleaf[r.rid] = (IX)(dst / MAXN);
+                    z.RLEAF(r.rid) = (IX)(dst / MAXN);
                 }
                 w.sync();
             } else {
@@ -4039,7 +4098,7 @@ struct Replica {
                 for (int32_t i = 0; i < cc; i++)
                     for (int32_t j = 0; j < ncnt[i]; j++) {
                         store_row(newk[i] * MAXN + j, tmp[q]);
-                        z.rleaf[tmp[q++].rid] = (IX)newk[i];
+                        z.RLEAF(tmp[q++].rid) = (IX)newk[i];
                     }
             }
             for (int32_t ni = 0; ni < cc; ni++) {
@@ -4068,7 +4127,7 @@ struct Replica {
             }
             h.nleaf = nl + delta;
             if (delta > 0) note_leaves();
-            for (int32_t i = 0; i < cc; i++) z.kids[parent * MAXN + i] = (IX)newk[i];
+            for (int32_t i = 0; i < cc; i++) z.KIDS(parent * MAXN + i) = (IX)newk[i];
             nch[parent] = (int8_t)cc;
           }
         } else {
@@ -4078,10 +4137,10 @@ struct Replica {
                  * its rank among all grandchildren places it in the regrouped nodes */
                 int32_t q = w.lane();
                 int32_t i = q >> 3, j = q & (MAXN - 1);
-                int32_t cb = i < pc ? z.kids[parent * MAXN + i] : -1;
+                int32_t cb = i < pc ? z.KIDS(parent * MAXN + i) : -1;
                 int32_t cn = cb >= 0 ? nch[cb] : 0;
                 bool has = j < cn;
-                int32_t ch = has ? z.kids[cb * MAXN + j] : -1;
+                int32_t ch = has ? z.KIDS(cb * MAXN + j) : -1;
                 uint64_t vm = w.ballot(has);
                 int32_t total = __builtin_popcountll(vm);
                 uint64_t below = q ? (~0ull >> (64 - q)) : 0ull;
@@ -4106,14 +4165,14 @@ struct Replica {
                 int32_t nb = w.shfl(nbv, ni >= 0 && ni < cc ? ni : 0); /* every lane active: a shuffle */
                 w.sync();
                 if (has) {
-                    z.kids[nb * MAXN + slot] = (IX)ch;
+                    z.KIDS(nb * MAXN + slot) = (IX)ch;
                     npar[ch] = (IX)nb;
                 }
                 w.sync();
                 if (q < cc) {
                     nch[nbv] = (int8_t)(base + (q < extra ? 1 : 0));
                     npar[nbv] = (IX)parent;
-                    z.kids[parent * MAXN + q] = (IX)nbv;
+                    z.KIDS(parent * MAXN + q) = (IX)nbv;
                 }
                 w.sync();
                 nch[parent] = (int8_t)cc;
@@ -4122,9 +4181,9 @@ struct Replica {
                 int32_t total = 0;
                 int32_t oldk[MAXN];
                 for (int32_t i = 0; i < pc; i++) {
-                    int32_t cb = z.kids[parent * MAXN + i];
+                    int32_t cb = z.KIDS(parent * MAXN + i);
                     oldk[i] = cb;
-                    for (int32_t q = 0; q < nch[cb]; q++) hold[total++] = z.kids[cb * MAXN + q];
+                    for (int32_t q = 0; q < nch[cb]; q++) hold[total++] = z.KIDS(cb * MAXN + q);
                 }
                 int32_t cc = total / (MAXN / 2);
                 if (cc > MAXN - 1) cc = MAXN - 1;
@@ -4139,12 +4198,12 @@ struct Replica {
                     if (nb < 0) return;
                     for (int32_t q = 0; q < cnt; q++) {
                         int32_t ch = hold[read++];
-                        z.kids[nb * MAXN + q] = (IX)ch;
+                        z.KIDS(nb * MAXN + q) = (IX)ch;
                         npar[ch] = (IX)nb;
                     }
                     nch[nb] = (int8_t)cnt;
                     npar[nb] = (IX)parent;
-                    z.kids[parent * MAXN + ni] = (IX)nb;
+                    z.KIDS(parent * MAXN + ni) = (IX)nb;
                 }
                 nch[parent] = (int8_t)cc;
             }
@@ -4166,8 +4225,8 @@ struct Replica {
             if constexpr (W::N >= MAXN * MAXN) {
                 /* slot_of, needsScour and scourNode's row reads in two round trips: the row's leaf, then
                  * everything about that leaf */
-                int32_t g = z.rgen[rid];
-                n = z.rleaf[rid];
+                int32_t g = z.RGEN(rid);
+                n = z.RLEAF(rid);
                 if (g != (uint8_t)gen) continue; /* unlinked since it was queued */
                 int32_t j = w.lane();
                 HotRow r = load_row(n * MAXN + (j & (MAXN - 1)));
@@ -4359,9 +4418,9 @@ struct Replica {
             constexpr bool RA = TILED && W::N >= 64;
             const bool text = !marker && !perm;
             int32_t nfr = RA ? zh->nfreeRid : 0;
-            int32_t frr = RA ? (int32_t)d.frid()[nfr > 0 ? nfr - 1 : 0] : 0;
+            int32_t frr = RA ? (int32_t)d.FRID(nfr > 0 ? nfr - 1 : 0) : 0;
             /* and the entry under it (its line): a split of the row at pos takes the top for its right part */
-            int32_t frr2 = RA ? (int32_t)d.frid()[nfr > 1 ? nfr - 2 : 0] : 0;
+            int32_t frr2 = RA ? (int32_t)d.FRID(nfr > 1 ? nfr - 2 : 0) : 0;
             /* the props record of a segment with properties (the shared pool: a cache hit), for the row set-up */
             const bool pa = RA && op.props;
             int32_t prOff = 0, prN = 0, prComb = 0;
@@ -4396,7 +4455,7 @@ struct Replica {
             const bool fpa = FP && op.props;
             if constexpr (FP) {
                 fnfr = zh->nfreeRid;
-                ffrr = (int32_t)d.frid()[fnfr > 0 ? fnfr - 1 : 0];
+                ffrr = (int32_t)d.FRID(fnfr > 0 ? fnfr - 1 : 0);
                 ftp = ftpOk && w.lane() < L ? p.text[op.text_off + w.lane()] : 0;
                 if (fpa) {
                     const mt_props_rec& pr0 = p.props[op.props - 1];
@@ -4418,14 +4477,14 @@ struct Replica {
             } else {
                 rid = alloc_rid();
             }
-            const int32_t fgen = FP ? (int32_t)z.rgen[rid] : 0; /* for the LRU entry */
+            const int32_t fgen = FP ? (int32_t)z.RGEN(rid) : 0; /* for the LRU entry */
             int32_t gen = 0, sc = 0;
             if (RA) { /* for the window set and the LRU entry: one round trip */
-                gen = z.rgen[rid];
+                gen = z.RGEN(rid);
                 sc = nsc[s / MAXN];
             }
-            z.rid[s] = (IX)rid;
-            typename HT::Cold& c = d.cold()[rid]; /* row id kept in a register, not re-read per field */
+            z.RID(s) = (IX)rid;
+            typename HT::Cold& c = d.COLD(rid); /* row id kept in a register, not re-read per field */
             z.len(s) = L;
             z.seq(s) = seq;
             z.rseq(s) = preRseq > 0 ? preRseq : NOREM;
@@ -4441,7 +4500,7 @@ struct Replica {
             c0.x[3] = 0;
             st4(&c, c0);
             c.ovl = 0;
-            z.rleaf[rid] = (IX)(s / MAXN);
+            z.RLEAF(rid) = (IX)(s / MAXN);
             h.nrows++;
             zh->sumW++;
             if (preRseq <= 0) h.localLen += L;
@@ -4600,8 +4659,8 @@ struct Replica {
         if (tf < 0) return;
         int32_t sa = sf, sb = sg; /* no split: the rows stay where the scan found them */
         if (Pf < start || Pg + vg > end) {
-            int32_t ridLast = z.rid[sg];
-            int32_t ridFirst = z.rid[sf];
+            int32_t ridLast = z.RID(sg);
+            int32_t ridFirst = z.RID(sf);
             int32_t sl = sg; /* the last row's slot, while nothing has moved it */
             if (Pf < start) { /* start falls inside the first row: split it; its right part is first */
                 int32_t rs = -1, rr = -1;
@@ -4719,8 +4778,8 @@ struct Replica {
             visit_run(sf, sg, refSeq, client, leaf, dl);
             return;
         }
-        int32_t ridLast = z.rid[sg];
-        int32_t ridFirst = z.rid[sf];
+        int32_t ridLast = z.RID(sg);
+        int32_t ridFirst = z.RID(sf);
         int32_t sl = sg; /* the last row's slot, while nothing has moved it */
         if (Pf < start) {
             int32_t rs = -1, rr = -1;
@@ -4782,7 +4841,7 @@ struct Replica {
                 lst0 = t.lst[n];
             }
             int32_t sc0 = nsc[n]; /* the leaf's needsScour, for its LRU entry */
-            int32_t rid = z.rid[s];
+            int32_t rid = z.RID(s);
             int32_t c = nch[n];
             int32_t j0 = k == ka ? (sa & (MAXN - 1)) : 0;
             int32_t j1 = k == kb ? (sb & (MAXN - 1)) : c - 1;
@@ -4790,14 +4849,14 @@ struct Replica {
             int32_t rs = r.rseq, L = r.len;
             uint32_t b4 = r.b4, fl = (b4 >> 16) & 0xFF;
             bool fresh = sel && rs == NOREM, unas = sel && rs == UNASSIGNED_SEQ;
-            const int32_t rgn = sel ? (int32_t)z.rgen[rid] : 0; /* for the leaf's LRU entry (its read overlaps the updates) */
+            const int32_t rgn = sel ? (int32_t)z.RGEN(rid) : 0; /* for the leaf's LRU entry (its read overlaps the updates) */
             int32_t nrs = fresh || unas ? seq : rs; /* rs after the update */
             uint64_t sm = w.ballot(sel);
             zh->sumW += __builtin_popcountll(sm);
             h.localLen -= w.sum(fresh ? L : 0); /* the rows leave the local view */
             if (fresh) {
                 z.rseq(s) = seq;
-                d.cold()[rid].lrseq = localSeq;
+                d.COLD(rid).lrseq = localSeq;
                 uint32_t f2 = hasL ? (fl | RF_LRSEQ) : (fl & ~(uint32_t)RF_LRSEQ);
                 st_bytes4(s, (b4 & 0xFF0000FFu) | (rcl << 8) | (f2 << 16));
             } else if (unas) {
@@ -4822,7 +4881,7 @@ struct Replica {
                       (nrs == NOREM || (nrs != UNASSIGNED_SEQ && nrs <= h.minSeq));
             bool wadd = sel && !(x2 & XF_W) && !st;
             if (wadd) x2 = XF_W;
-            uint8_t g = wadd ? z.rgen[rid] : 0;
+            uint8_t g = wadd ? z.RGEN(rid) : 0;
             if (sel) t.xf[s] = x2;
             if (lsd) lst_add_known(n, lch0, lix0, lst0, -lsd);
             uint64_t wm = w.ballot(wadd);
@@ -4939,8 +4998,8 @@ struct Replica {
                     dn++;
                 }
                 if (rf) { /* savedLocalRefs; segment.localRefs = undefined (mergeTree.ts:2673-2676) */
-                    if (refs_move(z.rid[s], INT32_MIN, REF_SAVED, 0)) saved = true;
-                    coll_drop(z.rid[s]);
+                    if (refs_move(z.RID(s), INT32_MIN, REF_SAVED, 0)) saved = true;
+                    coll_drop(z.RID(s));
                 }
             }
             if constexpr (TILED) row_removed(s);
@@ -5080,11 +5139,11 @@ struct Replica {
             return;
         }
         int32_t hq = zh->gqHead;
-        int32_t g0 = d.gq()[hq], lseq0 = d.gql()[hq];
+        int32_t g0 = d.GQ(hq), lseq0 = d.GQL(hq);
         int32_t mn = zh->memN, cnt = 0;
         for (int32_t b = 0; b < mn; b += W::N) {
             int32_t i = b + w.lane();
-            cnt += w.sum(i < mn && d.mgid()[i] == g0 ? 1 : 0);
+            cnt += w.sum(i < mn && d.MGID(i) == g0 ? 1 : 0);
         }
         if (zh->memN + cnt > d.caps.mcap) {
             mem_compact();
@@ -5098,11 +5157,11 @@ struct Replica {
         mn = zh->memN;
         for (int32_t b = 0; b < mn; b += W::N) { /* mark: each member's coordinate (per lane: its leaf's 8 slots) */
             int32_t i = b + w.lane();
-            if (i < mn && d.mgid()[i] == g0) {
-                int32_t rd = d.mrid()[i], lf = z.rleaf[rd], t = -1;
+            if (i < mn && d.MGID(i) == g0) {
+                int32_t rd = d.MRID(i), lf = z.RLEAF(rd), t = -1;
                 for (int32_t j = 0; j < MAXN; j++)
-                    if (j < nch[lf] && z.rid[lf * MAXN + j] == rd) t = kpos(lf) * MAXN + j;
-                d.mgid()[i] = t >= 0 ? -(t + 2) : -1;
+                    if (j < nch[lf] && z.RID(lf * MAXN + j) == rd) t = kpos(lf) * MAXN + j;
+                d.MGID(i) = t >= 0 ? -(t + 2) : -1;
                 if (t < 0) fail(E_ASSERT);
             }
         }
@@ -5114,7 +5173,7 @@ struct Replica {
             int32_t best = -1, bi = -1; /* the marked entry with the smallest coordinate (largest mark) */
             for (int32_t b = 0; b < mn; b += W::N) {
                 int32_t i = b + w.lane();
-                int32_t v = i < mn ? d.mgid()[i] : 0;
+                int32_t v = i < mn ? d.MGID(i) : 0;
                 int32_t m = w.max(v <= -2 ? v : INT32_MIN);
                 if (m != INT32_MIN && (bi < 0 || m > best)) {
                     best = m;
@@ -5125,7 +5184,7 @@ struct Replica {
                 fail(E_ASSERT);
                 break;
             }
-            d.mgid()[bi] = -1;
+            d.MGID(bi) = -1;
             w.sync();
             int32_t s = slot_at(-(best + 2));
             if (s < 0) {
@@ -5146,7 +5205,7 @@ struct Replica {
                 break;
             }
             group_push(lseq0); /* { segments: [], localSeq: segmentGroup.localSeq } (client.ts:755-758) */
-            row_enqueue_group(s, d.gq()[gq_wrap(zh->gqHead + zh->gqN - 1)]);
+            row_enqueue_group(s, d.GQ(gq_wrap(zh->gqHead + zh->gqN - 1)));
             if (dl) {
                 dput(pos);
                 dput(z.len(s));
@@ -5164,8 +5223,8 @@ struct Replica {
      * in parallel, the LRU entries (addToLRUSet) in member order. Same result as the serial loop in ack(). */
     MT_HD void ack_rows(int32_t kind, int32_t rd, bool mem, int32_t seq, const mt_kv* kv = nullptr, int32_t nkv = 0,
                         bool rewrite = false) {
-        int32_t leaf = mem ? (int32_t)z.rleaf[rd] : 0;
-        int32_t gen = mem ? (int32_t)z.rgen[rd] : 0; /* with the leaf id: the LRU entries need no more reads */
+        int32_t leaf = mem ? (int32_t)z.RLEAF(rd) : 0;
+        int32_t gen = mem ? (int32_t)z.RGEN(rd) : 0; /* with the leaf id: the LRU entries need no more reads */
         int32_t c = nch[leaf];
         int32_t s = -1;
         /* an annotate's keys: their slots (the doc's key ids, a lane each, read with the rows) */
@@ -5173,12 +5232,12 @@ struct Replica {
         int32_t key = kind == MT_OP_ANNOTATE && l < HT::K ? (int32_t)keys[l < HT::K ? l : 0] : -1;
 #pragma unroll
         for (int32_t j = 0; j < MAXN; j++) /* the leaf's row ids: one round trip */
-            if (mem && j < c && z.rid[leaf * MAXN + j] == (IX)rd) s = leaf * MAXN + j;
+            if (mem && j < c && z.RID(leaf * MAXN + j) == (IX)rd) s = leaf * MAXN + j;
         bool bad = mem && s < 0;
         bool ok = mem && s >= 0;
         if (kind == MT_OP_ANNOTATE) { /* ackPendingProperties (segmentPropertiesManager.ts:19-33), a lane per row */
             if (ok && !(z.flags(s) & RF_PROPS)) bad = true;
-            typename HT::Cold& cr = d.cold()[ok ? rd : 0];
+            typename HT::Cold& cr = d.COLD(ok ? rd : 0);
             if (ok) {
                 int32_t ng = z.ng(s);
                 if (ng < 1) bad = true;
@@ -5232,14 +5291,14 @@ struct Replica {
     MT_HD void ack(int32_t kind, const mt_kv* kv, int32_t nkv, bool rewrite, int32_t seq) {
         if (zh->gqN > 0) {
             MT_PROF_SCOPE(PH_ACK);
-            int32_t gid = d.gq()[zh->gqHead];
+            int32_t gid = d.GQ(zh->gqHead);
             zh->gqHead = gq_wrap(zh->gqHead + 1);
             zh->gqN--;
             int32_t mn = zh->memN;
             for (int32_t b = 0; b < mn; b += W::N) {
                 int32_t i = b + w.lane();
-                int32_t rd = i < mn ? d.mrid()[i] : 0;
-                uint64_t msk = w.ballot(i < mn && d.mgid()[i] == gid);
+                int32_t rd = i < mn ? d.MRID(i) : 0;
+                uint64_t msk = w.ballot(i < mn && d.MGID(i) == gid);
                 if constexpr (W::N >= 64) {
                     if (kind == MT_OP_INSERT || kind == MT_OP_REMOVE || (MT_ACKANN_PAR && kind == MT_OP_ANNOTATE)) {
                         /* a lane per member row; LRU entries in member order */
@@ -5494,7 +5553,7 @@ struct Replica {
                 int32_t c = 0;
                 for (int32_t i = bi * K; i < cnt && c < K; i++, c++) {
                     int32_t ch = hrd[i];
-                    z.kids[nb * MAXN + c] = (IX)ch;
+                    z.KIDS(nb * MAXN + c) = (IX)ch;
                     npar[ch] = (IX)nb;
                 }
                 nch[nb] = (int8_t)c;
@@ -5519,7 +5578,7 @@ struct Replica {
             off = arena_alloc(L);
             if (off < 0) return false;
         }
-        z.rid[s] = (IX)alloc_rid();
+        z.RID(s) = (IX)alloc_rid();
         cold(s).gc = 0;
         z.len(s) = L;
         z.seq(s) = op.seq;
@@ -5537,7 +5596,7 @@ struct Replica {
         cold(s).lrseq = 0;
         cold(s).ovl = 0;
         cold(s).ovx = 0;
-        z.rleaf[z.rid[s]] = (IX)(s / MAXN);
+        z.RLEAF(z.RID(s)) = (IX)(s / MAXN);
         int32_t fl = (marker ? RF_MARKER : 0) | (perm ? RF_PERM : 0);
         if (marker) {
             cold(s).toff = (uint32_t)op.pos2;
