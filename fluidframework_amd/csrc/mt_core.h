@@ -553,6 +553,14 @@ struct Replica {
     int32_t* twslot;
     int64_t cur; /* index of the record being applied in the current Pools (snapshot reload reads ahead) */
     int32_t* pfcur = nullptr; /* tiled kernel: where the prefetch helper waves read `cur` (LDS) */
+    /* tiled kernel built with MT_WIN_HELPER: the LDS mailbox of the second wave that evaluates the window set's second
+     * block of entries while this wave does the first (win_pass, win_helper) */
+    struct WinMail {
+        int32_t req, done, n, refSeq, client, minSeq, local, quit;
+        int32_t s[64], lc[64], lx[64], len[64], rseq[64], v[64], cp[64], st[64];
+    };
+    WinMail* wm = nullptr;
+    int32_t wmseq = 0;
     /* an upper bound of every maxSeq in the zamboni heap (INT32_MAX: unknown), set when a replay starts: an
      * entry at or above it cannot move up, so heap_add appends it without reading its ancestors */
     int32_t hmax = INT32_MAX;
@@ -1274,7 +1282,11 @@ struct Replica {
         return (uint32_t)client < 0xFEu ? (uint32_t)client : (client == -1 ? (uint32_t)LOCAL_CLIENT : 0xFEu);
     }
     MT_HD int32_t vis_of(int32_t s, const RowView& r, int32_t refSeq, int32_t client) const {
-        if (is_local(client)) return r.rseq == NOREM ? r.len : 0;
+        return vis_of_l(s, r, refSeq, client, is_local(client));
+    }
+    /* vis_of with the local-perspective test decided by the caller (the window helper wave, win_block) */
+    MT_HD int32_t vis_of_l(int32_t s, const RowView& r, int32_t refSeq, int32_t client, bool local) const {
+        if (local) return r.rseq == NOREM ? r.len : 0;
         /* the tests of quad_vis_of: short id bytes against the client's byte, one unsigned compare per seq */
         const uint32_t uc = client_byte(client);
         const uint32_t ur1 = refSeq >= 0 ? (uint32_t)refSeq + 1u : 0u;
@@ -1809,9 +1821,103 @@ struct Replica {
 #ifndef MT_WIN_NB
 #define MT_WIN_NB 1 /* wave passes of the window set issued together: 2 covered the ~80-100 rows in one round trip (r04e, 8 -> 2: 8.81 -> 9.66M ops/s at 256 x 300k); since the set's entries and the leaf headers sit in LDS (round 5), one pass at a time is faster (r05zd at 256 x 1M: 2 -> 1: 15.73 -> 15.88M, 4: 14.91M) */
 #endif
+#ifndef MT_WIN_HELPER
+#define MT_WIN_HELPER 0 /* tiled kernel: a second wave evaluates the window set's second block (win_helper) */
+#endif
+    /* stages 1-3 of win_pass for one block of window entries (lane i = b0 + lane < n) under (refSeq, client) with the
+     * given minSeq and local-perspective test: the entry (rd, g), its row's slot s (-1: gone), the row, its leaf's
+     * chunk (lc) and index (lx), settle / keep, the perspective length v and the chunk position cp */
+    struct WinRow {
+        int32_t rd, g, s, lc, lx, v, cp;
+        bool settle, keep;
+        RowView rv;
+    };
+    MT_HD WinRow win_block(int32_t b0, int32_t n, int32_t refSeq, int32_t client, int32_t minSeq, bool local) {
+        auto& t = z.tl;
+        WinRow x;
+        int32_t i = b0 + w.lane();
+        bool ok = i < n;
+        x.rd = ok ? twrid[i] : 0;
+        x.g = ok ? twgen[i] : -1;
+        x.s = ok ? twslot[i] : 0;
+        int32_t c = x.s, l = c / MAXN;
+        uint8_t gg = z.RGEN(x.rd);
+        IX lr = z.RLEAF(x.rd), cr = z.RID(c);
+        int32_t cn = nch[l];
+        bool gok = x.g >= 0 && gg == (uint8_t)x.g;
+        bool hit = gok & (lr == (IX)l) & ((c & (MAXN - 1)) < cn) & (cr == (IX)x.rd);
+        x.rv = row_view(c);
+        x.lc = t.lch[l];
+        x.lx = t.lix[l];
+        if (!hit) x.s = gok ? -2 : -1;
+        if (x.s == -2) {
+            int32_t lf = z.RLEAF(x.rd);
+            int32_t cc = nch[lf];
+            x.s = -1;
+            for (int32_t j = 0; j < MAXN; j++)
+                if (j < cc && z.RID(lf * MAXN + j) == (IX)x.rd) x.s = lf * MAXN + j;
+            if (x.s >= 0) {
+                x.rv = row_view(x.s);
+                x.lc = t.lch[lf];
+                x.lx = t.lix[lf];
+            }
+        }
+        const RowView& r = x.rv;
+        x.settle = x.s >= 0 && r.seq != UNASSIGNED_SEQ && r.seq <= minSeq &&
+                   (r.rseq == NOREM || (r.rseq != UNASSIGNED_SEQ && r.rseq <= minSeq));
+        x.keep = x.s >= 0 && !x.settle;
+        x.v = x.cp = 0;
+        if (x.keep) {
+            x.v = vis_of_l(x.s, x.rv, refSeq, client, local);
+            x.cp = tcpos[x.lc];
+        }
+        return x;
+    }
+    /* the helper wave's loop (k_replay_tiled with MT_WIN_HELPER): each request of the replaying wave (a window pass
+     * with more than W::N entries) evaluated on the second block, the results left in the mailbox. Exits when the
+     * replaying wave is done (`*quit`). Every wait is bounded. */
+    MT_HD void win_helper(const volatile int32_t* quit) {
+#ifdef __HIP_DEVICE_COMPILE__
+        if constexpr (TILED && W::N == 64) {
+            volatile WinMail* m = wm;
+#if MT_WIN_HELPER == 2
+            for (;;) { /* barrier handoff: every request is two workgroup barriers, matched by win_pass2 */
+                __syncthreads(); /* a request (or the end) is posted */
+                if (m->quit) return;
+                WinRow x = win_block(W::N, m->n, m->refSeq, m->client, m->minSeq, m->local != 0);
+                int32_t l = w.lane();
+                m->s[l] = x.s, m->lc[l] = x.lc, m->lx[l] = x.lx, m->len[l] = x.rv.len, m->rseq[l] = x.rv.rseq;
+                m->v[l] = x.v, m->cp[l] = x.cp, m->st[l] = (x.settle ? 1 : 0) | (x.keep ? 2 : 0);
+                __syncthreads(); /* the results are in */
+            }
+#endif
+            int32_t last = 0;
+            for (;;) {
+                int32_t spins = 0;
+                while (m->req == last && !*quit && ++spins < (1 << 26)) __builtin_amdgcn_s_sleep(1);
+                if (m->req == last) return; /* done (or a replaying wave gone quiet: stop waiting) */
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                last = m->req;
+                WinRow x = win_block(W::N, m->n, m->refSeq, m->client, m->minSeq, m->local != 0);
+                int32_t l = w.lane();
+                m->s[l] = x.s, m->lc[l] = x.lc, m->lx[l] = x.lx, m->len[l] = x.rv.len, m->rseq[l] = x.rv.rseq;
+                m->v[l] = x.v, m->cp[l] = x.cp, m->st[l] = (x.settle ? 1 : 0) | (x.keep ? 2 : 0);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (l == 0) m->done = last;
+            }
+        }
+#else
+        (void)quit;
+#endif
+    }
     MT_HD int32_t win_pass(int32_t refSeq, int32_t client) {
         MT_PROF_SCOPE(PH_WIN);
         auto& t = z.tl;
+#if MT_WIN_HELPER
+        if constexpr (TILED && W::N == 64) {
+            if (wm) return win_pass2(refSeq, client);
+        }
+#endif
         /* NB passes of the wave at a time, stage by stage: every entry's loads of one stage are issued
          * together (one round trip per stage, not one per stage per pass); the settling and the
          * compaction then run pass by pass, in entry order. Every read of a block precedes its writes,
@@ -1919,6 +2025,92 @@ struct Replica {
         t.wN = wpos;
         return total;
     }
+#if MT_WIN_HELPER
+    /* win_pass with the helper wave: the second block's entries evaluated by the helper while this wave evaluates the
+     * first; then both blocks settled and compacted in entry order, as win_pass does, and the rest of the set (more
+     * than 2 W::N entries) here. The compaction writes only positions below the entries still to be read. */
+    MT_HD int32_t win_pass2(int32_t refSeq, int32_t client) {
+        auto& t = z.tl;
+        int32_t n = t.wN, wpos = 0, total = 0;
+        const bool local = is_local(client);
+        volatile WinMail* m = wm;
+        const bool split = n > W::N;
+        if (split) { /* post the request: the second block, this perspective */
+            if (w.lane() == 0) {
+                m->n = n, m->refSeq = refSeq, m->client = client, m->minSeq = h.minSeq, m->local = local ? 1 : 0;
+            }
+#if MT_WIN_HELPER == 2
+            __syncthreads(); /* the helper's first barrier of the request */
+#else
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            wmseq++;
+            if (w.lane() == 0) m->req = wmseq;
+#endif
+        }
+        for (int32_t b0 = 0; b0 < n; b0 += W::N) {
+            WinRow x;
+            if (b0 == W::N && split) { /* the helper's results */
+#if MT_WIN_HELPER == 2
+                __syncthreads(); /* the helper's second barrier */
+#else
+                int32_t spins = 0;
+                while (m->done != wmseq && ++spins < (1 << 26)) __builtin_amdgcn_s_sleep(1);
+                if (m->done != wmseq) { /* the helper never answered: stop here, the document latched */
+                    fail(E_ASSERT);
+                    return total;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
+                int32_t l = w.lane(), i = b0 + l;
+                x.rd = i < n ? twrid[i] : 0;
+                x.g = i < n ? twgen[i] : -1;
+                x.s = m->s[l], x.lc = m->lc[l], x.lx = m->lx[l], x.rv.len = m->len[l], x.rv.rseq = m->rseq[l];
+                x.v = m->v[l], x.cp = m->cp[l];
+                int32_t st = m->st[l];
+                x.settle = (st & 1) != 0, x.keep = (st & 2) != 0;
+            } else {
+                x = win_block(b0, n, refSeq, client, h.minSeq, local);
+            }
+            uint64_t msk = w.ballot(x.settle);
+            while (msk) { /* serial, on the values the block read */
+                int32_t l = W::ffs(msk);
+                msk &= msk - 1;
+                int32_t ss = w.bcast(x.s, l);
+                if (w.bcast(x.rv.rseq, l) == NOREM) {
+                    t.xf[ss] = XF_STABLE;
+                    int32_t dl = w.bcast(x.rv.len, l), lcl = w.bcast(x.lc, l);
+                    int32_t nv = t.lst[ss / MAXN] + dl;
+                    t.lst[ss / MAXN] = nv;
+                    t.cls[lcl][w.bcast(x.lx, l)] = nv;
+                    cst_add(tcpos[lcl], dl);
+                } else {
+                    t.xf[ss] = 0;
+                }
+            }
+            int32_t tot;
+            int32_t off = w.excl_scan(x.keep ? 1 : 0, &tot);
+            w.sync();
+            if (x.keep) {
+                int32_t o = wpos + off;
+                twrid[o] = x.rd;
+                twgen[o] = (uint8_t)x.g;
+                twslot[o] = x.s;
+                wcp[o] = x.cp;
+                wlx[o] = (uint8_t)x.lx;
+                wvs[o] = x.v;
+                if (x.v) {
+                    W::atomic_add(&cdel[x.cp], x.v);
+                    W::atomic_add(&gdel[x.cp >> 6], x.v);
+                }
+            }
+            w.sync();
+            wpos += tot;
+            total += w.sum(x.v);
+        }
+        t.wN = wpos;
+        return total;
+    }
+#endif
     /* zero the chunk deltas of the last win_pass */
     MT_HD void win_clear() {
         int32_t n = z.tl.wN;

@@ -272,6 +272,12 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
 #define MT_PF_HELPERS 0 /* prefetch helper waves per config-4 document (0: one wave per document; 1 and 2
                            * measured 2.4 % and 3.2 % slower at 256 x 300k, profiles/r04f_ab) */
 #endif
+/* waves besides the replaying one in a config-4 workgroup: the prefetch helpers, or the window helper (MT_WIN_HELPER,
+ * mt_core.h win_helper) */
+#ifndef MT_WIN_HELPER
+#define MT_WIN_HELPER 0
+#endif
+#define MT_TILED_HELPERS (MT_WIN_HELPER ? 1 : MT_PF_HELPERS)
 #ifndef MT_PF_AHEAD
 #define MT_PF_AHEAD 2 /* records ahead of the replaying wave each helper looks */
 #endif
@@ -364,7 +370,7 @@ __device__ void tiled_prefetch(Doc<HT> v, const mt_op_rec* ops, int64_t nops, co
  * heap or window set would outgrow them latches E_CAPACITY and the engine replays it in the wide variant
  * (NARROW = false: the heap in HBM, the full window set) — capacity promotion (mt_replay.hip). */
 template <class HT, bool DL = false, bool NARROW = false>
-__global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
+__global__ __launch_bounds__(WG * (1 + MT_TILED_HELPERS)) void k_replay_tiled(Store<HT> st, int64_t ndocs, const mt_op_rec* ops,
                                                      const int64_t* op_off, const uint16_t* text,
                                                      const int64_t* text_off, const mt_props_rec* props,
                                                      const int64_t* props_off, const mt_kv* kv, const int64_t* kv_off,
@@ -387,6 +393,9 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     __shared__ typename HT::IX lhrid[HL];
     __shared__ uint8_t lhgen[HL];
     __shared__ int32_t pfcur, pfdone, pfsink; /* the replaying wave's record, its end, the helpers' sink */
+#if MT_WIN_HELPER
+    __shared__ typename R::WinMail wmail; /* the window helper's mailbox */
+#endif
 #ifdef MT_PROF
     __shared__ uint64_t sprof[PH_N];
     for (int i = threadIdx.x; i < PH_N; i += blockDim.x) sprof[i] = 0;
@@ -423,6 +432,9 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     if (threadIdx.x == 0) { /* every path: helper waves read these after the barrier */
         pfcur = 0;
         pfdone = fits ? 0 : 1;
+#if MT_WIN_HELPER
+        wmail.req = wmail.done = wmail.quit = 0;
+#endif
     }
     __syncthreads();
     if (replayer && fits) doc_stamp(zhs, 0);
@@ -436,7 +448,19 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
     p.vkind = aux.vkind;
     p.nvk = aux.nvk;
     if (!replayer) {
+#if MT_WIN_HELPER
+        if (threadIdx.x < 2 * WG) { /* the window helper: the replaying wave's LDS views of the set and the rope */
+            R hr(v, WaveGPU());
+            hr.tcpos = lcpos;
+            hr.twrid = lwrid;
+            hr.twgen = lwgen;
+            hr.twslot = lwslot;
+            hr.wm = &wmail;
+            hr.win_helper(&pfdone);
+        }
+#else
         tiled_prefetch<HT>(v, p.ops, p.nops, &pfcur, &pfdone, lcord, lcst, lccnt, &pfsink);
+#endif
     } else if (!fits) {
         doc_stamp(v.t->h, 0);
         R r(v, WaveGPU());
@@ -467,6 +491,9 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
             r.hgn = lhgen;
         }
         if (MT_PF_HELPERS > 0) r.pfcur = &pfcur;
+#if MT_WIN_HELPER
+        r.wm = &wmail;
+#endif
         r.replay(p);
         r.commit();
         doc_stamp(zhs, 1);
@@ -476,6 +503,12 @@ __global__ __launch_bounds__(WG * (1 + MT_PF_HELPERS)) void k_replay_tiled(Store
             for (int i = 0; i < PH_N; i++) prof[d * PH_N + i] = r.prof[i];
 #endif
     }
+#if MT_WIN_HELPER == 2
+    if (replayer) { /* the end: the helper's last barrier (win_helper) */
+        if (threadIdx.x == 0) wmail.quit = 1;
+        __syncthreads();
+    }
+#endif
     __syncthreads();
     if (replayer && fits) {
         wave_copy((int32_t*)&v.t->h, (const int32_t*)&zhs, (int)(sizeof(DocHdr) / 4));

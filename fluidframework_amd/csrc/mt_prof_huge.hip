@@ -2,7 +2,7 @@
 #include "mt_kernels.h"
 
 static int32_t replay_huge(mt_engine* e) {
-    constexpr int block = WG * (1 + MT_PF_HELPERS); /* the replaying wave + its prefetch helpers */
+    constexpr int block = WG * (1 + MT_TILED_HELPERS); /* the replaying wave + its helper waves */
     if (e->fx) return launch_replay<HotHuge>(e, k_replay_tiled<HotHuge, true>, block); /* delta events */
     /* the wide variant: asked for, or a replay that promotion cannot redo from the staged log (an incremental
      * batch on top of earlier ones, or promotion off), where the narrow kernel's E_CAPACITY would be final */
