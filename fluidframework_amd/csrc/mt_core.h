@@ -1821,8 +1821,11 @@ struct Replica {
 #ifndef MT_WIN_NB
 #define MT_WIN_NB 1 /* wave passes of the window set issued together: 2 covered the ~80-100 rows in one round trip (r04e, 8 -> 2: 8.81 -> 9.66M ops/s at 256 x 300k); since the set's entries and the leaf headers sit in LDS (round 5), one pass at a time is faster (r05zd at 256 x 1M: 2 -> 1: 15.73 -> 15.88M, 4: 14.91M) */
 #endif
-#ifndef MT_WIN_HELPER
-#define MT_WIN_HELPER 0 /* tiled kernel: a second wave evaluates the window set's second block (win_helper) */
+#ifndef MT_WIN_HELPER /* tiled kernel: a second wave of the document's workgroup evaluates the window set's second block
+                          (win_helper) — 2: handed over by two workgroup barriers (r06h at 256 x 300k: 16.21 -> 16.36M
+                          ops/s); 1: by polled LDS flags (r06g: 16.23 -> 15.46M, the s_sleep wake-up costs more than the
+                          global round trip it hides, tools/wave_sync_probe.hip); 0: one wave */
+#define MT_WIN_HELPER 2
 #endif
     /* stages 1-3 of win_pass for one block of window entries (lane i = b0 + lane < n) under (refSeq, client) with the
      * given minSeq and local-perspective test: the entry (rd, g), its row's slot s (-1: gone), the row, its leaf's
@@ -1913,7 +1916,7 @@ struct Replica {
     MT_HD int32_t win_pass(int32_t refSeq, int32_t client) {
         MT_PROF_SCOPE(PH_WIN);
         auto& t = z.tl;
-#if MT_WIN_HELPER
+#if MT_WIN_HELPER && defined(__HIPCC__)
         if constexpr (TILED && W::N == 64) {
             if (wm) return win_pass2(refSeq, client);
         }
@@ -2025,7 +2028,7 @@ struct Replica {
         t.wN = wpos;
         return total;
     }
-#if MT_WIN_HELPER
+#if MT_WIN_HELPER && defined(__HIPCC__)
     /* win_pass with the helper wave: the second block's entries evaluated by the helper while this wave evaluates the
      * first; then both blocks settled and compacted in entry order, as win_pass does, and the rest of the set (more
      * than 2 W::N entries) here. The compaction writes only positions below the entries still to be read. */

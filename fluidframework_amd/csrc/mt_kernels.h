@@ -275,7 +275,7 @@ __global__ __launch_bounds__(WG, MINW) MT_SGPR_ATTR void k_replay(Store<HT> st, 
 /* waves besides the replaying one in a config-4 workgroup: the prefetch helpers, or the window helper (MT_WIN_HELPER,
  * mt_core.h win_helper) */
 #ifndef MT_WIN_HELPER
-#define MT_WIN_HELPER 0
+#define MT_WIN_HELPER 2 /* mt_core.h */
 #endif
 #define MT_TILED_HELPERS (MT_WIN_HELPER ? 1 : MT_PF_HELPERS)
 #ifndef MT_PF_AHEAD

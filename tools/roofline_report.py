@@ -12,8 +12,8 @@ states:
     /opt/skills/guides/MI355X_MICROARCH.md HBM section) + WRITE_SIZE, KB x 1024, and the raw (x1)
     figure; traffic / alg for both;
   - instructions per event (SQ_INSTS_* / events) and the wave-cycle wait fraction.
-The PMC runs are bench.py --steps 1 --warmup 0: two replay dispatches (timed step + end-to-end
-step), reported per dispatch.
+The PMC runs are bench.py --steps 1 --warmup 0 --no-e2e (tools/gpu.sh): one replay dispatch per run (two in
+rounds before 6, with the end-to-end step), reported per dispatch.
 """
 import csv
 import glob
