@@ -170,7 +170,7 @@ static bool host_pinned(const void* p) {
     return at.type == hipMemoryTypeHost;
 }
 
-/* n bytes from host `src` to device `dst` on the copy stream: straight from pinned memory, or through the engine's
+/* n bytes from host `src` to device `dst` on the copy stream: directly (pinned memory, or a single chunk), or through the engine's
  * pinned staging buffers (host threads fill one while the DMA engine drains the others) */
 static constexpr size_t PIN_BYTES = (size_t)128 << 20;
 static int32_t stage_h2d(mt_engine* e, void* dst, const void* src, size_t n, bool pinned) {
@@ -477,8 +477,11 @@ int32_t mt_engine_submit_run(mt_engine* e, const mt_op_rec* ops, const int64_t* 
     HIPCHK(e, hipStreamWaitEvent(e->stream2, e->evs, 0));
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     if ((rc = copy_small(e, a, e->cstream))) return rc;
-    const bool pin_ops = host_pinned(ops), pin_text = host_pinned(text);
     const int64_t step = e->order.p ? nd : chunk_docs(e); /* a dispatch order permutes across chunks: one launch */
+    /* one chunk leaves nothing to overlap: the runtime's own pageable copy then beats the staging buffers (8,192
+     * documents: 66 vs 105 ms, profiles/r06z_c3_share0of8_8192docs_bench.json) */
+    const bool single = step >= nd;
+    const bool pin_ops = single || host_pinned(ops), pin_text = single || host_pinned(text);
     std::vector<mt_engine::Persp> persp((size_t)nd);
     std::vector<char> loads((size_t)nd, 0);
     int64_t text_hi = 0; /* the text staged so far: a prefix of the pool */
