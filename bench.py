@@ -355,8 +355,8 @@ def main() -> None:
                                          "(tools/gpu.sh traffic:C, tools/roofline_report.py)",
                          "kernel": "k_replay_tiled" if args.config == 4 else "k_replay", "kernel_ms": avg_kernel_ms,
                          "alg_bytes_per_launch": alg_bytes, "alg_bytes_node": total_alg,
-                         "alg_formula": ("tile summaries (BASELINE.md): A(op) = 4 B x chunks + 64 B x window rows "
-                                         "+ 640 B + 32 B x rows written" if args.config == 4 else
+                         "alg_formula": ("tile summaries, HBM-resident bytes (BASELINE.md, round 6): A(op) = 32 B x "
+                                         "window rows + 640 B + 32 B x rows written" if args.config == 4 else
                                          "flat scan (BASELINE.md): A(op) = 16 B x rows + 32 B x rows written")},
             "cpu_baseline": cpu,
             "doc_time_ms": doc_ms,

@@ -5656,9 +5656,10 @@ struct Replica {
             grouped = (op.kind & MT_OPF_GROUPED) != 0; /* a group member before the last (mt_oplog.h) */
             if (!grouped) zh->seqOps++; /* one sequenced message per group */
             if (grouped) {
-            } else if constexpr (TILED) /* BASELINE.md tile formula, in 16-byte units: 4 B per chunk summary,
-                                    64 B per window row, 640 B for the target chunk's leaves + leaf line */
-                zh->sumR += (4 * z.tl.nchunk + 64 * z.tl.wN + 640) / 16;
+            } else if constexpr (TILED) /* BASELINE.md tile formula (round 6: HBM-resident bytes only), in 16-byte
+                                    units: 32 B per window row, 640 B for the target chunk's leaves + leaf line; the
+                                    chunk summaries and the window set's entries are LDS-resident during a replay */
+                zh->sumR += (32 * z.tl.wN + 640) / 16;
             else
                 zh->sumR += h.nrows;
             if (kind != MT_OP_NOOP) {
