@@ -150,6 +150,10 @@ def main() -> None:
     ap.add_argument("--share", default="",
                     help="R/N: on one GPU, replay the share rank R of an N-rank strong-scaling run would get (the "
                          "per-GPU load of the multi-GPU bench, measured without the other ranks; value = that share)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="under torch.distributed.run on a one-GPU box: every rank on device 0, collectives over gloo "
+                         "(the multi-rank path of this script end to end on real hardware; not a scaling measurement: "
+                         "the ranks share one GPU)")
     ap.add_argument("--gen-cache", default=os.environ.get("MT_GEN_CACHE", ""),
                     help="directory caching generated workloads between runs (profiler passes)")
     args = ap.parse_args()
@@ -169,12 +173,16 @@ def main() -> None:
                              f"torch.distributed.run --nproc-per-node {args.gpus}")
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
     dist = None
+    device = 0 if args.rehearse else local_rank
+    coll_dev = "cpu" if args.rehearse else f"cuda:{device}"  # where the collectives' tensors live
     if world > 1 or "LOCAL_WORLD_SIZE" in os.environ:  # under torch.distributed.run: RCCL even for one rank
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = local_rank
+        torch.cuda.set_device(device)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     ndef, odef, desc = CONFIGS[args.config]
     docs = args.docs or ndef
@@ -308,7 +316,7 @@ def main() -> None:
         np.save(args.digests_out, digests)
 
     if dist:
-        dev = f"cuda:{device}"
+        dev = coll_dev
         elapsed = shard.max_over_ranks(elapsed, dist, dev)
         total_seq_ops = shard.sum_over_ranks(seq_ops, dist, dev)
         total_alg = shard.sum_over_ranks(alg_bytes, dist, dev)
@@ -346,6 +354,8 @@ def main() -> None:
                        "local_edits_rank0": local_events,
                        "parallelism": (f"share {a_rank}/{a_world} of the docs bin-packed x{a_world} ({args.assign} "
                                        f"costs), one GPU: value is that share's rate" if args.share else
+                                       f"REHEARSAL: {world} ranks on one GPU over gloo, docs bin-packed x{world} "
+                                       f"(not a scaling measurement)" if args.rehearse else
                                        f"docs bin-packed x{world} ({args.assign} costs)"),
                        "docs_promoted_rank0": promoted, "docs_in_error_rank0": int(len(bad))},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
