@@ -149,11 +149,13 @@ struct DocHdr {
     int32_t mkMask;        /* property key slots an annotate changed on a marker (marker_keys_annotated) */
     int32_t ndv; /* derived property values (mt_oplog.h MT_VALUE_DERIVED): bits 0-7 the STRCAT entries, 8-15 the
                     consensus-object entries, bit 16 a NaN was made; nonzero bits 8-16: some row may hold a value
-                    matchProperties never matches */
+                    matchProperties never matches. Bit 24 (DV_RUN): a SubSequence document (mt_oplog.h MT_SEG_RUN: its
+                    text-bearing rows are SubSequence rows, whose canAppend has MaxRun 128 and no newline rule) */
     int64_t sumR, sumW; /* roofline counters: sum over sequenced msgs of rows before the op and
                            rows written by it (BASELINE.md A(op) = 16 R + 32 W) */
     int64_t tStart, tEnd; /* the last replay kernel's start / end for this document (s_memrealtime ticks) */
 };
+enum : int32_t { DV_RUN = 1 << 24 };
 /* the int32 fields of DocHdr the replica keeps in registers while it runs; the rarely used ones
  * (nclients, nextSid, errOp, nkeys, hwSlots, gcEpoch, loadPos, ovTop, ovFree, and since round 2 root,
  * nfree, freeHead, nfreeRid, hwHeap, seqOps) stay in the image and are read and written there (z.h),
@@ -726,6 +728,7 @@ struct Replica {
         zh->loadPos = 0;
         zh->gidNext = 0;
         zh->mkMask = 0;
+        zh->ndv = 0;
         zh->ovTop = 1; /* block 0 is the null link */
         zh->ovFree = 0;
         for (int32_t b = 0; b < HT::C; b += W::N) {
@@ -3692,7 +3695,7 @@ struct Replica {
         if (!pa) return true;
         const typename HT::Cold& ca = cold(a);
         const typename HT::Cold& cb = cold(b);
-        const bool um = (zh->ndv >> 8) != 0; /* NaN or consensus objects exist: never matched (pv_unmatchable) */
+        const bool um = ((zh->ndv >> 8) & 0x1FF) != 0; /* NaN or consensus objects exist: never matched (pv_unmatchable) */
         for (int i = 0; i < HT::K / 8; i++) { /* 8 key slots per 16-byte compare */
             I4 va = ld4((const int32_t*)&ca.pv[8 * i]);
             if (!eq4(va, ld4((const int32_t*)&cb.pv[8 * i])) || (um && pv_unmatchable(va))) return false;
@@ -3701,7 +3704,15 @@ struct Replica {
     }
 
     /* ---- zamboni: scourNode / pack / zamboniSegments (mergeTree.ts:1322-1511) ---------- */
-    /* canAppend (textSegment.ts:63-68) */
+    /* a SubSequence document (DV_RUN): read from the image header, only where a length test needs it */
+    MT_HD bool run_doc() const { return (zh->ndv & DV_RUN) != 0; }
+    /* the length half of canAppend for rows of lengths La, Lb: TextSegment's granularity (textSegment.ts:66-67,
+     * TextSegmentGranularity 256), or in a SubSequence document MaxRun (sequence sharedSequence.ts:12, 57-60) */
+    MT_HD bool gran_ok(int32_t La, int32_t Lb) const {
+        const int32_t m = La < Lb ? La : Lb;
+        return m <= MT_RUN_MAXRUN || (m <= GRANULARITY && !run_doc());
+    }
+    /* canAppend (textSegment.ts:63-68; SubSequence: sharedSequence.ts:57-60, no newline rule) */
     MT_HD bool can_append(int32_t a, int32_t b) {
         MT_PROF_SCOPE(PH_CAND);
         /* PermutationSegment.canAppend (permutationvector.ts:87-93): both unallocated, or b's handles follow a's */
@@ -3710,7 +3721,7 @@ struct Replica {
         if (z.flags(a) & RF_MARKER) return false;
         if (ends_nl(a, z.len(a))) return false;
         if (z.flags(b) & RF_MARKER) return false;
-        return z.len(a) <= GRANULARITY || z.len(b) <= GRANULARITY;
+        return gran_ok(z.len(a), z.len(b));
     }
     /* PermutationSegment.canAppend's handle rule for rows a (current length La) and b */
     MT_HD bool perm_follows(int32_t a, int32_t b, int32_t La) {
@@ -3722,7 +3733,7 @@ struct Replica {
         int32_t f = z.flags(a);
         if (f & RF_NLK) return (f & RF_NL) != 0;
         MT_PROF_SCOPE(PH_CAND);
-        bool nl = La > 0 && arena_base(zh->arenaSide)[cold(a).toff + La - 1] == '\n';
+        bool nl = La > 0 && !run_doc() && arena_base(zh->arenaSide)[cold(a).toff + La - 1] == '\n';
         z.flags(a) = (uint8_t)(f | RF_NLK | (nl ? RF_NL : 0));
         return nl;
     }
@@ -3829,8 +3840,7 @@ struct Replica {
                          * only read for a candidate pair. Same conjunction as mergeTree.ts:1355-1360. */
                         bool ok = prev >= 0 && local_len(s) > 0 &&
                                   ((z.flags(prev) & z.flags(s) & RF_PERM) ||
-                                   (!((z.flags(prev) | z.flags(s)) & RF_NOTEXT) &&
-                                    (z.len(prev) <= GRANULARITY || z.len(s) <= GRANULARITY))) &&
+                                   (!((z.flags(prev) | z.flags(s)) & RF_NOTEXT) && gran_ok(z.len(prev), z.len(s)))) &&
                                   ((z.flags(prev) ^ z.flags(s)) & RF_PROPS) == 0 && match_props(prev, s) &&
                                   can_append(prev, s);
                         if (ok) {
@@ -3942,7 +3952,7 @@ struct Replica {
             if (pairOk && (fl & RF_PROPS)) { /* matchProperties (properties.ts:61-92) */
                 for (int i = 0; i < HT::K / 8; i++)
                     if (!eq4(ld4((const int32_t*)&ca.pv[8 * i]), ld4((const int32_t*)&cb.pv[8 * i]))) pairOk = false;
-                if (pairOk && (zh->ndv >> 8)) /* NaN and consensus objects never match (pv_unmatchable) */
+                if (pairOk && ((zh->ndv >> 8) & 0x1FF)) /* NaN and consensus objects never match (pv_unmatchable) */
                     for (int i = 0; i < HT::K / 8; i++)
                         if (pv_unmatchable(ld4((const int32_t*)&ca.pv[8 * i]))) pairOk = false;
             }
@@ -3951,7 +3961,7 @@ struct Replica {
                 pairOk = sa == 0 ? sb == 0 : sb == sa + (uint32_t)lenP;
             } else if (pairOk) { /* TextSegment.canAppend: the run does not end with "\n" (textSegment.ts:64) */
                 bool nl = (flP & RF_NLK) ? (flP & RF_NL) != 0
-                                         : arena_base(zh->arenaSide)[tofP + lenP - 1] == '\n';
+                                         : !run_doc() && arena_base(zh->arenaSide)[tofP + lenP - 1] == '\n';
                 pairOk = !nl;
             }
         }
@@ -3987,7 +3997,7 @@ struct Replica {
             int32_t fk = w.bcast(fl, k);
             bool ok = true;
             /* the serial part: a text append needs either side <= TextSegment granularity (the run grows) */
-            if (!(prevFl & fk & RF_PERM)) ok = prevLen <= GRANULARITY || lk <= GRANULARITY;
+            if (!(prevFl & fk & RF_PERM)) ok = gran_ok(prevLen, lk);
             if (ok) {
                 int32_t sp = w.bcast(n, prev) * MAXN + (prev & (MAXN - 1));
                 int32_t sk = w.bcast(n, k) * MAXN + (k & (MAXN - 1));
@@ -4604,6 +4614,10 @@ struct Replica {
         int32_t localSeq = hasL ? ++zh->localSeq : 0;
         bool marker = op.seg_kind == MT_SEG_MARKER;
         bool perm = op.seg_kind == MT_SEG_PERM; /* PermutationSegment(length) (permutationvector.ts:47-51) */
+        /* new SubSequence(items) (sharedSequence.ts:116-125): its items are the record's units (item ids); the document
+         * becomes a SubSequence document (the host keeps TextSegment inserts out of it, mt_engine_submit) */
+        const bool run = op.seg_kind == MT_SEG_RUN;
+        if (run) zh->ndv |= DV_RUN;
         int32_t L = seg_len(op);
         if (L <= 0) ensure_boundary(pos, refSeq, client); /* the split still happens (2004) */
         if (L > 0) {
@@ -4710,7 +4724,7 @@ struct Replica {
                 } else {
                     last = arena_copy(arena_base(zh->arenaSide) + off, p.text + op.text_off, L);
                 }
-                fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
+                fl |= RF_NLK | (last == '\n' && !run ? RF_NL : 0);
             }
             /* {cli, rcli, flags, ng = 0} in one store */
             st_bytes4(s, (uint32_t)(uint8_t)(client < 0 ? LOCAL_CLIENT : client) |
@@ -5764,6 +5778,8 @@ struct Replica {
     /* one loaded segment into slot s (a fresh row): text / marker / permutation, props, merge info */
     MT_HD bool place_loaded(const mt_op_rec& op, const Pools& p, int32_t s) {
         bool marker = op.seg_kind == MT_SEG_MARKER, perm = op.seg_kind == MT_SEG_PERM;
+        const bool run = op.seg_kind == MT_SEG_RUN; /* a loaded SubSequence ({items} spec) */
+        if (run) zh->ndv |= DV_RUN;
         int32_t L = seg_len(op);
         if (L <= 0) {
             fail(E_UNSUPPORTED); /* a snapshot holds no empty segments */
@@ -5801,7 +5817,7 @@ struct Replica {
         } else {
             cold(s).toff = (uint32_t)off;
             int32_t last = arena_copy(arena_base(zh->arenaSide) + off, p.text + op.text_off, L);
-            fl |= RF_NLK | (last == '\n' ? RF_NL : 0);
+            fl |= RF_NLK | (last == '\n' && !run ? RF_NL : 0);
         }
         z.flags(s) = (uint8_t)fl;
         if (op.props) {
@@ -5876,6 +5892,7 @@ struct Replica {
         int64_t n = 0;
         int32_t P = 0; /* position of the pass's first row */
         const uint16_t* base = arena_base(zh->arenaSide);
+        const bool runD = run_doc(); /* SubSequence rows are not TextSegments: gatherText gives their placeholders */
         if constexpr (W::N >= MAXN * MAXN) {
             /* 8 leaves x 8 slots per pass of the wave: each lane's row length under the perspective, one
              * scan for the positions and one for the output offsets, and every lane copies its own piece */
@@ -5897,7 +5914,7 @@ struct Replica {
                 int32_t vtot;
                 int32_t p = P + w.excl_scan(v, &vtot);
                 bool hit = v > 0 && start < p + v && end > p;
-                bool text = s >= 0 && !(z.flags(s) & RF_NOTEXT);
+                bool text = s >= 0 && !(z.flags(s) & RF_NOTEXT) && !runD;
                 int32_t a = 0, b = 0;
                 if (hit && text) text_piece(v, start - p, end - p, &a, &b);
                 /* a placeholder run longer than 2^24 units (a merged PermutationSegment of millions of rows
@@ -5928,7 +5945,7 @@ struct Replica {
                 int32_t v = vis(s, refSeq, client), p = P;
                 P += v;
                 if (v <= 0 || !(start < p + v && end > p)) continue;
-                if (z.flags(s) & RF_NOTEXT) {
+                if ((z.flags(s) & RF_NOTEXT) || runD) {
                     if ((int64_t)pl * v > PH_RUN_MAX) return -E_UNSUPPORTED;
                     for (int32_t u = 0; u < pl * v; u++, n++)
                         if (out && n < cap) out[n] = ph[u % pl];
@@ -5944,6 +5961,44 @@ struct Replica {
                 n += b - a;
             }
         }
+        return n;
+    }
+
+    /* SharedSequence.getItems(start, end) (sequence sharedSequence.ts:150-183) in the local view: walkSegments(start,
+     * end) visits the rows of positive length intersecting [start, end) and pushes every item of each SubSequence row
+     * (markers and permutation rows push none); then the items before `start` in the first such row are spliced off
+     * (start - getPosition(first)) and the array cut to end - start (end = MT_TEXT_DEFAULT: undefined, no cut; end <=
+     * start: none). So a marker inside the range shifts the cut as it does in the reference. Item ids (the units) into
+     * out (cap), the count returned. */
+    MT_HD int64_t get_items(int32_t start, int32_t end, uint16_t* out, int64_t cap) {
+        const bool noEnd = end == TEXT_RANGE_DEFAULT;
+        if (!noEnd && end <= start) return 0;
+        const int32_t refSeq = h.currentSeq, client = h.localShort;
+        const int32_t e = noEnd ? INT32_MAX : end;
+        const uint16_t* base = arena_base(zh->arenaSide);
+        int64_t lo = -1, hi = INT64_MAX, n = 0; /* the kept window of the pushed items, once the first row is known */
+        int64_t I = 0;                          /* items pushed before the pass's first row */
+        int32_t P = 0;
+        for (int32_t k = 0; kvalid(k); k = knext(k)) { /* rolled: a read, not a replay path */
+            int32_t lf = leaf_at(k), c = nch[lf];
+            for (int32_t j = 0; j < c; j++) {
+                int32_t s = lf * MAXN + j;
+                int32_t v = vis(s, refSeq, client), p = P;
+                P += v;
+                if (v <= 0 || !(start < p + v && e > p) || (z.flags(s) & RF_NOTEXT)) continue;
+                if (lo < 0) { /* the first SubSequence row: splice(0, start - getPosition(it)) */
+                    lo = start - p > 0 ? start - p : 0;
+                    if (!noEnd) hi = lo + (int64_t)(end - start);
+                }
+                const uint16_t* src = base + cold(s).toff;
+                for (int32_t u = 0; u < v; u++, I++)
+                    if (I >= lo && I < hi) {
+                        if (out && n < cap) out[n] = src[u];
+                        n++;
+                    }
+            }
+        }
+        w.sync();
         return n;
     }
 
@@ -6053,6 +6108,7 @@ struct Replica {
         int32_t hdr[6] = {h.currentSeq, h.minSeq, zh->localSeq, length_local(), nsegs, h.nleaf};
         put_bytes(o, hdr, sizeof(hdr));
         const uint16_t* base = arena_base(zh->arenaSide);
+        const bool runD = run_doc(); /* text-bearing rows are SubSequence rows (kind MT_SEG_RUN) */
         int32_t ordinal = -1;
         for (int32_t k = 0; kvalid(k); k = knext(k)) {
           ordinal++;
@@ -6067,7 +6123,7 @@ struct Replica {
                 for (int k = 0; k < HT::K; k++)
                     if (cold(s).pv[k]) np++;
             bool hnd = (fl & RF_PERM) && cold(s).toff != 0; /* an allocated PermutationSegment start */
-            uint8_t b4[4] = {(uint8_t)((fl & RF_MARKER) ? MT_SEG_MARKER : (fl & RF_PERM) ? MT_SEG_PERM : MT_SEG_TEXT),
+            uint8_t b4[4] = {(uint8_t)((fl & RF_MARKER) ? MT_SEG_MARKER : (fl & RF_PERM) ? MT_SEG_PERM : runD ? MT_SEG_RUN : MT_SEG_TEXT),
                              (uint8_t)(((fl & RF_PROPS) ? MT_DF_HAS_PROPS : 0) | (rem ? MT_DF_REMOVED : 0) |
                                        ((fl & RF_LSEQ) ? MT_DF_LSEQ : 0) | ((fl & RF_LRSEQ) ? MT_DF_LRSEQ : 0) |
                                        (hnd ? MT_DF_HANDLE : 0)),

@@ -175,6 +175,11 @@ int64_t mth_text_range(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_
     });
 }
 
+/* SharedSequence.getItems(start, end) in the local view (Replica::get_items; end = INT32_MIN: undefined) */
+int64_t mth_items(mth_store* s, int64_t doc, int32_t start, int32_t end, uint16_t* out, int64_t cap) {
+    return with_replica(s, doc, [&](auto& r) { return r.get_items(start, end, out, cap); });
+}
+
 /* getContainingSegment + getPosition of the found row: out6 = {found, offset, length, seq, long client,
  * position} (the layout of the oracle's mto_get_containing) */
 int32_t mth_containing(mth_store* s, int64_t doc, int32_t pos, int32_t ref_seq, int32_t long_client, int32_t* out6) {

@@ -31,6 +31,7 @@ int32_t mth_pos_from_relpos(mth_store* s, int64_t doc, int32_t kid, int32_t vid,
                             int32_t off, int32_t ref_seq, int32_t long_client, int32_t* out);
 int64_t mth_text_range(mth_store* s, int64_t doc, int32_t ref_seq, int32_t long_client, const uint16_t* ph,
                        int32_t pl, int32_t start, int32_t end, uint16_t* out, int64_t cap);
+int64_t mth_items(mth_store* s, int64_t doc, int32_t start, int32_t end, uint16_t* out, int64_t cap);
 int64_t mth_dump(mth_store* s, int64_t doc, uint8_t* out, int64_t cap);
 uint64_t mth_digest(mth_store* s, int64_t doc);
 void mth_stats(mth_store* s, int64_t doc, int32_t* out8);

@@ -602,7 +602,8 @@ __global__ __launch_bounds__(WG) void k_text(Store<HT> st, int64_t doc, int32_t 
         sh = r.short_of(long_client);
         if (sh < 0) sh = 0x7fff;
     }
-    int64_t m = r.get_text_range(ref_seq, sh, start, end, ph, pl, out, cap);
+    /* pl < 0: SharedSequence.getItems(start, end) in the local view (the C ABI's mt_engine_get_items) */
+    int64_t m = pl < 0 ? r.get_items(start, end, out, cap) : r.get_text_range(ref_seq, sh, start, end, ph, pl, out, cap);
     if (threadIdx.x == 0) *n = m;
 }
 
@@ -836,6 +837,7 @@ struct mt_engine {
      * records, `applied` covers every record replayed since create / reset. */
     struct Persp {
         int32_t all = INT32_MIN;
+        int32_t segk = 0; /* segment kinds the document's records inserted: 1 TextSegment, 2 SubSequence (never both) */
         std::vector<std::pair<int32_t, int32_t>> ref;
         void note(int32_t c, int32_t r) {
             for (auto& x : ref)
@@ -847,6 +849,7 @@ struct mt_engine {
         }
         void merge(const Persp& o) {
             if (o.all > all) all = o.all;
+            segk |= o.segk;
             for (auto& x : o.ref) note(x.first, x.second);
         }
         int32_t floor(int32_t c) const {

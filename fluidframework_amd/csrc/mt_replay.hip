@@ -72,12 +72,23 @@ static bool check_docs(const SubmitArgs& a, int64_t d0, int64_t d1, mt_engine::P
                 }
             }
             int64_t end = 0;
-            if (kind == MT_OP_INSERT && (o.seg_kind & 0x7F) == MT_SEG_TEXT) end = to + (int64_t)o.text_off + o.text_len;
+            if (kind == MT_OP_INSERT || kind == MT_OP_RELOAD || kind == MT_OP_APPEND) {
+                /* a segment-bearing record: a known kind, and a document of TextSegments or of SubSequences, not both
+                 * (mt_oplog.h MT_SEG_RUN; the kinds its earlier batches inserted are seeded by seed_segk) */
+                const int sk = o.seg_kind & 0x7F;
+                if (sk > MT_SEG_RUN) return false;
+                const bool regen = (o.kind & (MT_OPF_LOCAL | MT_OPF_REGEN)) == (MT_OPF_LOCAL | MT_OPF_REGEN);
+                const int32_t len = kind == MT_OP_INSERT ? o.text_len : o.pos2;
+                if ((sk == MT_SEG_TEXT || sk == MT_SEG_RUN) && !regen && len > 0) pp.segk |= sk == MT_SEG_TEXT ? 1 : 2;
+                if (pp.segk == 3) return false;
+            }
+            const bool units = (o.seg_kind & 0x7F) == MT_SEG_TEXT || (o.seg_kind & 0x7F) == MT_SEG_RUN;
+            if (kind == MT_OP_INSERT && units) end = to + (int64_t)o.text_off + o.text_len;
             if (kind == MT_OP_NOOP && (o.kind & MT_OPF_LOCAL) && o.seg_kind == MT_NOOP_HTLOAD)
                 end = to + (int64_t)o.text_off + o.text_len;
             if (o.seg_kind & MT_SEG_RELPOS) end = std::max(end, to + (int64_t)o.text_off + o.text_len + MT_RELPOS_UNITS);
             /* snapshot-load records carry the segment length in pos2 (mt_oplog.h) */
-            if ((kind == MT_OP_RELOAD || kind == MT_OP_APPEND) && o.seg_kind == MT_SEG_TEXT) {
+            if ((kind == MT_OP_RELOAD || kind == MT_OP_APPEND) && units) {
                 if (o.pos2 < 0) return false;
                 end = std::max(end, to + (int64_t)o.text_off + o.pos2);
             }
@@ -97,6 +108,14 @@ static bool check_docs(const SubmitArgs& a, int64_t d0, int64_t d1, mt_engine::P
 static int host_threads() {
     unsigned hc = std::thread::hardware_concurrency();
     return (int)std::min<unsigned>(16, std::max<unsigned>(1, hc));
+}
+
+/* the segment kinds the staged documents' replicas already hold (an incremental batch; a reset clears them) */
+static void seed_segk(const mt_engine* e, std::vector<mt_engine::Persp>& persp, const int64_t* docs) {
+    for (size_t k = 0; k < persp.size(); k++) {
+        size_t d = docs ? (size_t)docs[k] : k;
+        persp[k].segk = !e->fresh && d < e->persp_applied.size() ? e->persp_applied[d].segk : 0;
+    }
 }
 
 static bool check_range(const SubmitArgs& a, int64_t d0, int64_t d1, mt_engine::Persp* persp, char* loads,
@@ -355,6 +374,7 @@ int32_t mt_engine_submit(mt_engine* e, const mt_op_rec* ops, const int64_t* op_o
     int64_t nops = op_off[nd];
     std::vector<mt_engine::Persp> persp((size_t)nd);
     std::vector<char> loads((size_t)nd, 0);
+    seed_segk(e, persp, nullptr);
     if (!check_range(a, 0, nd, persp.data(), loads.data(), nullptr)) return MT_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc;
@@ -380,6 +400,7 @@ int32_t mt_engine_submit_docs(mt_engine* e, int64_t m, const int64_t* docs, cons
     if (!offsets_ok(a, m)) return MT_E_ARG;
     std::vector<mt_engine::Persp> persp((size_t)m);
     std::vector<char> loads((size_t)m, 0);
+    seed_segk(e, persp, docs);
     if (!check_range(a, 0, m, persp.data(), loads.data(), nullptr)) return MT_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
     int32_t rc;
@@ -484,6 +505,7 @@ int32_t mt_engine_submit_run(mt_engine* e, const mt_op_rec* ops, const int64_t* 
     const bool pin_ops = single || host_pinned(ops), pin_text = single || host_pinned(text);
     std::vector<mt_engine::Persp> persp((size_t)nd);
     std::vector<char> loads((size_t)nd, 0);
+    seed_segk(e, persp, nullptr);
     int64_t text_hi = 0; /* the text staged so far: a prefix of the pool */
     int k = 0;
     rc = MT_OK;
@@ -895,6 +917,9 @@ int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t l
                                     cap);
 }
 
+static int64_t text_read(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, const uint16_t* placeholder,
+                         int32_t placeholder_len, int32_t start, int32_t end, uint16_t* out, int64_t cap);
+
 int64_t mt_engine_get_text_range(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client,
                                  const uint16_t* placeholder, int32_t placeholder_len, int32_t start, int32_t end,
                                  uint16_t* out, int64_t cap) {
@@ -902,10 +927,20 @@ int64_t mt_engine_get_text_range(mt_engine* e, int64_t doc, int32_t ref_seq, int
         (placeholder_len > 0 && !placeholder))
         return -MT_E_ARG;
     if (placeholder_len == 1 && placeholder[0] == '*') return -MT_E_UNSUPPORTED; /* Marker.toString() */
+    return text_read(e, doc, ref_seq, long_client, placeholder, placeholder_len, start, end, out, cap);
+}
+
+int64_t mt_engine_get_items(mt_engine* e, int64_t doc, int32_t start, int32_t end, uint16_t* out, int64_t cap) {
+    if (!e || doc < 0 || doc >= e->ndocs || cap < 0 || start == MT_TEXT_DEFAULT) return -MT_E_ARG;
+    return text_read(e, doc, 0, -1, nullptr, -1, start, end, out, cap); /* placeholder length -1: k_text's items mode */
+}
+
+static int64_t text_read(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client, const uint16_t* placeholder,
+                         int32_t placeholder_len, int32_t start, int32_t end, uint16_t* out, int64_t cap) {
     int32_t floor = persp_floor(e, doc, long_client);
     e = route(e, &doc);
     if (hipSetDevice(e->device) != hipSuccess) return -MT_E_HIP;
-    size_t phb = (2 * (size_t)placeholder_len + 15) & ~(size_t)15;
+    size_t phb = (2 * (size_t)(placeholder_len > 0 ? placeholder_len : 0) + 15) & ~(size_t)15;
     if (ensure(e, e->tmp, 16 + phb + 2 * (size_t)(out ? cap : 0) + 16)) return -MT_E_HIP;
     int64_t* dn = (int64_t*)e->tmp.p;
     uint16_t* dph = (uint16_t*)((uint8_t*)e->tmp.p + 16);

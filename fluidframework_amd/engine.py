@@ -91,6 +91,8 @@ def lib() -> ctypes.CDLL:
         L.mt_engine_get_text.restype = i64
         L.mt_engine_get_text_range.argtypes = [vp, i64, i32, i32, vp, i32, i32, i32, vp, i64]
         L.mt_engine_get_text_range.restype = i64
+        L.mt_engine_get_items.argtypes = [vp, i64, i32, i32, vp, i64]
+        L.mt_engine_get_items.restype = i64
         L.mt_engine_stats.argtypes = [vp, vp]
         L.mt_engine_get_containing_segment.argtypes = [vp, i64, i32, i32, i32, ctypes.POINTER(SegRef)]
         L.mt_engine_get_position.argtypes = [vp, i64, i32, i32, i32, i32, ctypes.POINTER(i32)]
@@ -309,6 +311,17 @@ class Engine:
         buf = np.zeros(max(n, 1), "<u2")
         self.L.mt_engine_get_text_range(self.h, doc, ref_seq, long_client, pp, pl, a, b, _p(buf), n)
         return buf[:n].tobytes().decode("utf-16-le")
+
+    def get_items(self, doc: int, start: int, end: Optional[int] = None) -> list:
+        """SharedSequence.getItems(start, end) (sequence sharedSequence.ts:150-183) of a SubSequence document in the
+        local view: item ids (oplog.Interner.item_obj maps them back; end None = undefined)."""
+        b = TEXT_DEFAULT if end is None else end
+        n = self.L.mt_engine_get_items(self.h, doc, start, b, None, 0)
+        if n < 0:
+            raise EngineError(f"get_items failed {n}", -n)
+        buf = np.zeros(max(n, 1), "<u2")
+        self.L.mt_engine_get_items(self.h, doc, start, b, _p(buf), n)
+        return buf[:n].tolist()
 
     def pos_from_relative_pos(self, doc: int, key_id: int, value_id: int, before: bool = False,
                               offset: Optional[int] = None, ref_seq: int = 0, long_client: int = -1) -> int:

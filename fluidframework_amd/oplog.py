@@ -23,7 +23,7 @@ OPF_GROUPED = 0x40
 OPF_TREE = 0x20  # MergeTree-level call (mt_oplog.h MT_OPF_TREE)
 OPF_REGEN = 0x10  # regeneratePendingOp (MT_OPF_REGEN)
 OPF_ATREF = 0x08  # insertAtReferencePositionLocal (MT_OPF_ATREF)
-SEG_TEXT, SEG_MARKER, SEG_PERM = 0, 1, 2
+SEG_TEXT, SEG_MARKER, SEG_PERM, SEG_RUN = 0, 1, 2, 3  # SEG_RUN: SubSequence items (mt_oplog.h MT_SEG_RUN)
 SEG_RELPOS = 0x80  # seg_kind flag: positions relative to markers (mt_oplog.h MT_SEG_RELPOS)
 RELPOS_UNITS = 10  # MT_RELPOS_UNITS
 MARKER_ID_KEY = "markerId"  # reservedMarkerIdKey (merge-tree properties / mergeTree.ts getId)
@@ -63,13 +63,30 @@ def _falsy(v: Any) -> bool:
 
 
 class Interner:
-    """Batch-global key / value string tables. Value id 0 is JSON null (= delete)."""
+    """Batch-global key / value string tables. Value id 0 is JSON null (= delete). `items`: SubSequence items
+    (mt_oplog.h MT_SEG_RUN) by canonical JSON, ids 0..65535: what a SubSequence row's units hold."""
 
     def __init__(self) -> None:
         self.keys: List[str] = [""]
         self.key_ids: Dict[str, int] = {}
         self.values: List[str] = ["null"]
         self.value_ids: Dict[str, int] = {}
+        self.items: List[str] = []
+        self.item_ids: Dict[str, int] = {}
+
+    def item(self, v: Any) -> int:
+        s = canonical_json(v)
+        i = self.item_ids.get(s)
+        if i is None:
+            i = len(self.items)
+            if i > 0xFFFF:
+                raise ValueError("too many distinct SubSequence items")
+            self.items.append(s)
+            self.item_ids[s] = i
+        return i
+
+    def item_obj(self, i: int) -> Any:
+        return json.loads(self.items[i])
 
     def key(self, k: str) -> int:
         i = self.key_ids.get(k)
@@ -229,14 +246,17 @@ def parse_dump(b: bytes):
         if flags & DF_HANDLE:  # an allocated PermutationSegment start (mt_oplog.h MT_DF_HANDLE)
             (start,) = struct.unpack_from("<i", b, off)
             off += 4
-        text = ""
+        text, items = "", None
         if kind == SEG_TEXT:
             text = b[off: off + 2 * f[0]].decode("utf-16-le")
+            off += 2 * f[0]
+        elif kind == SEG_RUN:  # a SubSequence's item ids
+            items = list(struct.unpack_from(f"<{f[0]}H", b, off))
             off += 2 * f[0]
         segs.append(dict(kind=kind, flags=flags, ngroups=ngroups, len=f[0], seq=f[1], client=f[2],
                          removedSeq=f[3] if flags & 2 else None, removedClient=f[4], localSeq=f[5],
                          localRemovedSeq=f[6], leaf=f[7], overlap=ov, props=props, refType=ref_type, text=text,
-                         start=start))
+                         start=start, items=items))
     if off != len(b):
         raise ValueError("trailing bytes after the canonical dump")
     return dict(currentSeq=hdr[0], minSeq=hdr[1], localSeq=hdr[2], length=hdr[3], nsegs=hdr[4],
@@ -282,14 +302,20 @@ class DocLog:
     def add(self, kind: int, *, client: int = 0, seq: int = 0, ref_seq: int = 0, min_seq: int = 0,
             pos1: int = 0, pos2: int = 0, text: Optional[str] = None, marker: Optional[int] = None,
             props: Optional[Dict[str, Any]] = None, combining: int = COMBINE_NONE,
-            perm: Optional[int] = None) -> None:
-        """One record; `perm` = the row count of a PermutationSegment insert / loaded segment."""
+            perm: Optional[int] = None, items: Optional[list] = None) -> None:
+        """One record; `perm` = the row count of a PermutationSegment insert / loaded segment; `items` = a SubSequence
+        insert / loaded segment's items (interned: the row's units are their item ids)."""
         seg_kind = SEG_TEXT
         toff = tlen = 0
         if kind & 7 in _SEGMENT_KINDS:
             if perm is not None:
                 seg_kind = SEG_PERM
                 tlen = perm
+            elif items is not None:
+                seg_kind = SEG_RUN
+                toff = len(self.text)
+                self.text.extend(self.interner.item(v) for v in items)
+                tlen = len(items)
             elif marker is not None:
                 seg_kind = SEG_MARKER
                 pos2 = marker
@@ -306,7 +332,7 @@ class DocLog:
         pool (mt_oplog.h MT_SEG_RELPOS)."""
         self.add(kind, **kw)
         r = list(self.ops[-1])
-        if kind & 7 == OP_INSERT and r[1] == SEG_TEXT:
+        if kind & 7 == OP_INSERT and r[1] in (SEG_TEXT, SEG_RUN):
             assert r[8] + r[9] == len(self.text)
         else:
             r[8], r[9] = len(self.text), 0

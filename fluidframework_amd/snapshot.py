@@ -26,6 +26,7 @@ HEADER = "header"           # SnapshotLegacy.header (snapshotlegacy.ts:55)
 BODY = "body"               # SnapshotLegacy.body
 CHUNK_SIZE = 10000          # SnapshotV1.chunkSize (snapshotV1.ts:40)
 TEXT_GRANULARITY = 256      # TextSegmentGranularity (mergeTree.ts:1093)
+MAX_RUN = 128               # SubSequence MaxRun (sequence sharedSequence.ts:12)
 UNALLOCATED = -0x80000000   # Handle.unallocated (matrix handletable.ts:11)
 
 
@@ -42,11 +43,17 @@ def _props(seg, interner: ol.Interner) -> Optional[Dict[str, Any]]:
             for k, v in seg["props"]}
 
 
-def _json_spec(seg, props):
+def _json_spec(seg, props, interner: Optional[ol.Interner] = None):
     """ISegment.toJSONObject: TextSegment (textSegment.ts:48-54), Marker (mergeTree.ts:690-694),
-    PermutationSegment (permutationvector.ts:77-79)."""
+    PermutationSegment (permutationvector.ts:77-79), SubSequence (sequence sharedSequence.ts:43-47: {items} and
+    addSerializedProps' props; the item ids map back through the interner's items)."""
     if seg["kind"] == ol.SEG_TEXT:
         return {"text": seg["text"], "props": props} if props is not None else seg["text"]
+    if seg["kind"] == ol.SEG_RUN:
+        j = {"items": [interner.item_obj(u) for u in seg["items"]]}
+        if props is not None:
+            j["props"] = props
+        return j
     if seg["kind"] == ol.SEG_MARKER:
         j = {"marker": {"refType": seg["refType"]}}
         if props is not None:
@@ -61,9 +68,18 @@ def _can_append(a, b) -> bool:
             return False
         sa, sb = a.get("start", UNALLOCATED), b.get("start", UNALLOCATED)
         return sb == UNALLOCATED if sa == UNALLOCATED else sb == sa + a["len"]
+    if a["kind"] == ol.SEG_RUN:  # SubSequence.canAppend (sharedSequence.ts:57-60): no newline rule
+        return b["kind"] == ol.SEG_RUN and (a["len"] <= MAX_RUN or b["len"] <= MAX_RUN)
     if a["kind"] != ol.SEG_TEXT or b["kind"] != ol.SEG_TEXT:  # Marker.canAppend is false
         return False
     return not a["text"].endswith("\n") and (a["len"] <= TEXT_GRANULARITY or b["len"] <= TEXT_GRANULARITY)
+
+
+def _appended(prev, cur):
+    """prev.append(cur) (TextSegment / SubSequence / PermutationSegment): the merged segment"""
+    return dict(prev, len=prev["len"] + cur["len"],
+                text=(prev["text"] + cur["text"]) if prev["kind"] == ol.SEG_TEXT else None,
+                items=(prev["items"] + cur["items"]) if prev["kind"] == ol.SEG_RUN else None)
 
 
 def extract_segments(hdr, segs, interner: ol.Interner, long_name) -> List[tuple]:
@@ -75,7 +91,7 @@ def extract_segments(hdr, segs, interner: ol.Interner, long_name) -> List[tuple]
 
     def push(p):
         if p is not None:
-            out.append((_json_spec(p, p["_props"]), p["len"]))
+            out.append((_json_spec(p, p["_props"], interner), p["len"]))
 
     for s in segs:
         removed = s["removedSeq"] is not None
@@ -87,15 +103,14 @@ def extract_segments(hdr, segs, interner: ol.Interner, long_name) -> List[tuple]
             if prev is None:
                 prev = cur
             elif _can_append(prev, cur) and prev["_props"] == cur["_props"]:
-                prev = dict(prev, len=prev["len"] + cur["len"],
-                            text=(prev["text"] + cur["text"]) if prev["kind"] == ol.SEG_TEXT else None)
+                prev = _appended(prev, cur)
             else:
                 push(prev)
                 prev = cur
         else:
             push(prev)
             prev = None
-            raw: Dict[str, Any] = {"json": _json_spec(s, props)}
+            raw: Dict[str, Any] = {"json": _json_spec(s, props, interner)}
             if s["seq"] > min_seq:
                 raw["seq"] = s["seq"]
                 raw["client"] = long_name(s["client"])
@@ -161,14 +176,13 @@ def extract_segments_legacy(hdr, segs, interner: ol.Interner) -> List[tuple]:
             continue
         cur = dict(s, _props=_props(s, interner))
         if prev is not None and _can_append(prev, cur) and prev["_props"] == cur["_props"]:
-            prev = dict(prev, len=prev["len"] + cur["len"],
-                        text=(prev["text"] + cur["text"]) if prev["kind"] == ol.SEG_TEXT else None)
+            prev = _appended(prev, cur)
         else:
             if prev is not None:
-                out.append((_json_spec(prev, prev["_props"]), prev["len"]))
+                out.append((_json_spec(prev, prev["_props"], interner), prev["len"]))
             prev = cur
     if prev is not None:
-        out.append((_json_spec(prev, prev["_props"]), prev["len"]))
+        out.append((_json_spec(prev, prev["_props"], interner), prev["len"]))
     return out
 
 
@@ -442,6 +456,8 @@ def load_records(tree: dict, log: ol.DocLog, client_index, local_client: Optiona
                 log.ops[-1] = tuple(r)
         elif "marker" in spec:
             log.add(kind, marker=spec["marker"]["refType"], props=spec.get("props"), **common)
+        elif "items" in spec:  # SubSequence.fromJSONObject (sharedSequence.ts:23-32)
+            log.add(kind, items=spec["items"], props=spec.get("props"), **common)
         else:
             log.add(kind, text=spec["text"], props=spec.get("props"), **common)
 

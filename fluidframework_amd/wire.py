@@ -8,8 +8,9 @@ group's members but the last flagged MT_OPF_GROUPED), with the message's client 
 minSeq. The records then go to the engine like any other batch (mt_engine_submit).
 
 Supported segment specs: a string, `{text, props}`, `{marker: {refType}, props}` (textSegment.ts,
-mergeTree.ts:690-708) and `[length, start]` PermutationSegment rows (matrix permutationvector.ts:
-75-77). `relativePos1/2` (IRelativePosition {id, before, offset}, ops.ts:56-61) become MT_SEG_RELPOS records that the
+mergeTree.ts:690-708), `[length, start]` PermutationSegment rows (matrix permutationvector.ts:
+75-77) and `{items, props}` SubSequence runs (SharedObjectSequence / SharedNumberSequence, sequence
+sharedSequence.ts:18-47: the items are interned, oplog.Interner.item). `relativePos1/2` (IRelativePosition {id, before, offset}, ops.ts:56-61) become MT_SEG_RELPOS records that the
 engine resolves as Client.getValidOpRange does (posFromRelativePos under the op's refSeq and client); they
 need an engine with the client-feature build (caps.dcap or caps.rcap > 0). Combining ops other than
 `rewrite` raise ValueError.
@@ -52,6 +53,8 @@ def _op_record(log: ol.DocLog, kind: int, op: Dict[str, Any], common: Dict[str, 
             add(kind, pos1=p1, perm=int(seg[0]), **common)
         elif "marker" in seg:
             add(kind, pos1=p1, marker=seg["marker"]["refType"], props=seg.get("props"), **common)
+        elif "items" in seg:  # SubSequence.fromJSONObject (sharedSequence.ts:23-32)
+            add(kind, pos1=p1, items=seg["items"], props=seg.get("props"), **common)
         elif "text" in seg:
             add(kind, pos1=p1, text=seg["text"], props=seg.get("props"), **common)
         else:
@@ -153,7 +156,7 @@ def record_op(rec, text, props, kv, interner: ol.Interner) -> Dict[str, Any]:
     ps, comb = _props_of(props, kv, int(rec["props"]), interner)
     sk = int(rec["seg_kind"])
     rel = _relpos_of(rec, text, interner) if sk & ol.SEG_RELPOS else (None, None)
-    op = _record_op(rec, kind, sk & 0x7F, ps, comb, text)
+    op = _record_op(rec, kind, sk & 0x7F, ps, comb, text, interner)
     for i, r in enumerate(rel):
         if r is not None:
             op.pop(f"pos{i + 1}", None)
@@ -161,10 +164,15 @@ def record_op(rec, text, props, kv, interner: ol.Interner) -> Dict[str, Any]:
     return op
 
 
-def _record_op(rec, kind, sk, ps, comb, text) -> Dict[str, Any]:
+def _record_op(rec, kind, sk, ps, comb, text, interner: ol.Interner) -> Dict[str, Any]:
     if kind == ol.OP_INSERT:
         if sk == ol.SEG_PERM:
             seg = [int(rec["text_len"]), UNALLOCATED]
+        elif sk == ol.SEG_RUN:  # SubSequence.toJSONObject (sharedSequence.ts:43-47)
+            ids = text[int(rec["text_off"]): int(rec["text_off"]) + int(rec["text_len"])]
+            seg = {"items": [interner.item_obj(int(u)) for u in ids]}
+            if ps is not None:
+                seg["props"] = ps
         elif sk == ol.SEG_MARKER:
             seg = {"marker": {"refType": int(rec["pos2"])}}
             if ps is not None:

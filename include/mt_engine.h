@@ -162,6 +162,13 @@ int64_t mt_engine_get_text(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t l
 int64_t mt_engine_get_text_range(mt_engine* e, int64_t doc, int32_t ref_seq, int32_t long_client,
                                  const uint16_t* placeholder, int32_t placeholder_len, int32_t start, int32_t end,
                                  uint16_t* out, int64_t cap);
+/* SharedSequence.getItems(start, end) (sequence sharedSequence.ts:150-183; SharedObjectSequence /
+ * SharedNumberSequence.getRange) of a SubSequence document (mt_oplog.h MT_SEG_RUN) in the local view: the item ids
+ * (the host's item interner) of every visited SubSequence segment of [start, end), the ones before `start` in the
+ * first of them spliced off and the result cut to end - start (end = MT_TEXT_DEFAULT: undefined, no cut; end <= start:
+ * none). Returns the item count (writes at most cap), <0 on error. In such a document getText sees no TextSegment:
+ * every visited segment gives the placeholder. */
+int64_t mt_engine_get_items(mt_engine* e, int64_t doc, int32_t start, int32_t end, uint16_t* out, int64_t cap);
 /* A segment handle (the reference returns live ISegment objects, mergeTree.ts:87-117): the row's
  * stable id and its generation. A handle stops resolving once zamboni merges the row into its
  * neighbour or unlinks it (mergeTree.ts:1322-1398), as a detached reference segment would. */

@@ -115,7 +115,14 @@ enum {
     MT_SEG_MARKER = 1, /* Marker, length 1 (mergeTree.ts:668-832)          */
     MT_SEG_PERM = 2,   /* PermutationSegment (matrix permutationvector.ts:36-122): length =
                           text_len, no text, handle unallocated; any two such rows can append */
+    MT_SEG_RUN = 3,    /* SubSequence<T> (sequence sharedSequence.ts:18-101: SharedObjectSequence /
+                          SharedNumberSequence items): the text units are item ids (the host's item interner);
+                          canAppend = both SubSequence and either length <= MaxRun (128), no newline rule. A document
+                          holds SubSequence rows or TextSegment rows, never both (SharedSequence's specToSegment
+                          makes only SubSequence; mt_engine_submit refuses a document mixing the two kinds);
+                          markers and PermutationSegments may sit beside either */
 };
+#define MT_RUN_MAXRUN 128 /* MaxRun (sharedSequence.ts:12) */
 
 /* seg_kind bit: the record's positions are relative to markers (IRelativePosition, ops.ts:56-61;
  * Client.getValidOpRange client.ts:486-503 resolves them with MergeTree.posFromRelativePos, mergeTree.ts:
@@ -196,7 +203,8 @@ typedef struct mt_kv {
  * (mergeTree.ts:3002-3016). The per-document digest is FNV-1a-64 over these bytes.
  *
  * header: int32 currentSeq, minSeq, localSeq, localLength, nsegs, nleaf
- * record: uint8 kind; uint8 flags; uint8 noverlap; uint8 ngroups;
+ * record: uint8 kind (MT_SEG_*: 0 TextSegment, 1 Marker, 2 PermutationSegment, 3 SubSequence);
+ *         uint8 flags; uint8 noverlap; uint8 ngroups;
  *         int32 len, seq, client, removedSeq, removedClient, localSeq, localRemovedSeq, leaf;
  *         int32 overlap[noverlap];
  *         uint16 nprops; uint16 refType; (key,value) x nprops sorted by key id, a derived value (MT_VALUE_DERIVED..)
@@ -205,7 +213,7 @@ typedef struct mt_kv {
  *         (STRCAT: the base value id, 0 = a consensus object's "[object Object]", and the count of "undefined"s;
  *         CONS: the object's seq, 0) — a dump with no derived value is unchanged;
  *         int32 start (MT_DF_HANDLE only: a PermutationSegment's allocated handle, permutationvector.ts:38);
- *         text: len x uint16 (text segments only)
+ *         text: len x uint16 (text segments: UTF-16 units; SubSequence segments: item ids)
  * client fields are LONG client indices; -1 = the reference's "original" (LocalClientId).
  */
 enum {

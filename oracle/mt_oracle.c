@@ -59,7 +59,7 @@ typedef struct GroupQ {
 
 struct Seg { /* BaseSegment (mergeTree.ts:428-572) + TextSegment/Marker */
     Node hdr;
-    int kind;    /* MT_SEG_TEXT / MT_SEG_MARKER */
+    int kind;    /* MT_SEG_TEXT / MT_SEG_MARKER / MT_SEG_PERM / MT_SEG_RUN (SubSequence: text = item ids) */
     int refType; /* Marker.refType */
     uint16_t* text;
     int tcap;
@@ -281,7 +281,7 @@ static Seg* newSeg(mto_client* c, int kind, const uint16_t* text, int len, int r
     /* BaseSegment field initialisers (mergeTree.ts:432-433) */
     s->clientId = LocalClientId;
     s->seq = UniversalSequenceNumber;
-    if (kind == MT_SEG_TEXT) {
+    if (kind == MT_SEG_TEXT || kind == MT_SEG_RUN) { /* SubSequence(items): cachedLength = items.length */
         s->tcap = len > 0 ? len : 1;
         s->text = xmalloc(sizeof(uint16_t) * s->tcap);
         if (len) memcpy(s->text, text, sizeof(uint16_t) * len);
@@ -903,13 +903,17 @@ static int matchProperties(const Seg* a, const Seg* b) {
  * append; a non-permutation segment has start === undefined and never matches. */
 static int canAppend(const Seg* a, const Seg* b) {
     if (a->kind == MT_SEG_PERM) return b->kind == MT_SEG_PERM;
+    /* SubSequence.canAppend (sequence sharedSequence.ts:57-60): SubSequence.is(segment) && (this.cachedLength <= MaxRun
+     * || segment.cachedLength <= MaxRun); no newline rule */
+    if (a->kind == MT_SEG_RUN)
+        return b->kind == MT_SEG_RUN && (a->hdr.cachedLength <= MT_RUN_MAXRUN || b->hdr.cachedLength <= MT_RUN_MAXRUN);
     if (a->kind != MT_SEG_TEXT) return 0;
     int len = a->hdr.cachedLength;
     if (len > 0 && a->text[len - 1] == '\n') return 0;
     if (b->kind != MT_SEG_TEXT) return 0;
     return a->hdr.cachedLength <= TextSegmentGranularity || b->hdr.cachedLength <= TextSegmentGranularity;
 }
-/* TextSegment.append (textSegment.ts:74-85) */
+/* TextSegment.append (textSegment.ts:74-85); SubSequence.append (sharedSequence.ts:66-76): items.concat */
 static void segAppend(Seg* a, const Seg* b) {
     int n = a->hdr.cachedLength + b->hdr.cachedLength;
     if (a->kind == MT_SEG_PERM) { /* PermutationSegment.append (permutationvector.ts:95-101) */
@@ -950,9 +954,10 @@ static Seg* splitAt(mto_client* c, Seg* s, int pos) {
     if (s->kind == MT_SEG_PERM) { /* new PermutationSegment(cachedLength - pos); cachedLength = pos */
         r = newSeg(c, MT_SEG_PERM, NULL, len - pos, 0);
         s->hdr.cachedLength = pos;
-    } else { /* text.substring(pos) / substring(0, pos): past the end, an empty right part */
+    } else { /* text.substring(pos) / substring(0, pos): past the end, an empty right part; SubSequence's
+                items.slice(pos) / slice(0, pos) the same (sharedSequence.ts:93-101) */
         int cut = pos < len ? pos : len;
-        r = newSeg(c, MT_SEG_TEXT, s->text + cut, len - cut, 0);
+        r = newSeg(c, s->kind, s->text + cut, len - cut, 0);
         s->hdr.cachedLength = cut;
     }
     /* propertyManager.copyTo (segmentPropertiesManager.ts:113-128) */
@@ -1655,6 +1660,8 @@ static Seg* specToSegment(mto_client* c, const mt_op_rec* op) { /* textSegment.t
         s = newSeg(c, MT_SEG_MARKER, NULL, 0, op->pos2);
     else if (op->seg_kind == MT_SEG_PERM) /* PermutationVector.insert (permutationvector.ts:147-151) */
         s = newSeg(c, MT_SEG_PERM, NULL, len, 0);
+    else if (op->seg_kind == MT_SEG_RUN) /* new SubSequence(items) (SharedSequence.insert, sharedSequence.ts:116-125) */
+        s = newSeg(c, MT_SEG_RUN, c->textPool + op->text_off, len, 0);
     else
         s = newSeg(c, MT_SEG_TEXT, c->textPool + op->text_off, len, 0);
     if (op->props) { /* TextSegment.make(text, props) -> addProperties(props) (no collab window) */
@@ -1924,7 +1931,7 @@ static void dumpWalk(mto_client* c, Block* b, Out* o, int* leafIdx, int* nsegs) 
                     put16(o, (uint16_t)s->props.a[k].key);
                     put16(o, (uint16_t)s->props.a[k].val);
                 }
-            if (s->kind == MT_SEG_TEXT) put(o, s->text, 2 * (int64_t)s->hdr.cachedLength);
+            if (s->kind == MT_SEG_TEXT || s->kind == MT_SEG_RUN) put(o, s->text, 2 * (int64_t)s->hdr.cachedLength);
         }
         return;
     }

@@ -49,6 +49,8 @@ def lib():
         L.mth_text_range.argtypes = [vp, i64, i32, i32, vp, i32, i32, i32, vp, i64]
         L.mth_text_range.restype = i64
         L.mth_pos_from_relpos.argtypes = [vp, i64, i32, i32, i32, i32, i32, i32, i32, vp]
+        L.mth_items.argtypes = [vp, i64, i32, i32, vp, i64]
+        L.mth_items.restype = i64
         L.mth_dump.argtypes = [vp, i64, vp, i64]
         L.mth_dump.restype = i64
         L.mth_digest.argtypes = [vp, i64]
@@ -125,6 +127,17 @@ class HostStore:
         buf = np.zeros(max(n, 1), "<u2")
         self.L.mth_text_range(self.h, doc, ref_seq, long_client, _p(ph), pl, a, b, _p(buf), n)
         return buf[:n].tobytes().decode("utf-16-le")
+
+    def length_local(self, doc) -> int:
+        return int(self.L.mth_length_local(self.h, doc))
+
+    def items(self, doc, start, end=None) -> list:
+        """SharedSequence.getItems(start, end) of a SubSequence document: item ids (Replica::get_items)"""
+        b = -(1 << 31) if end is None else end
+        n = self.L.mth_items(self.h, doc, start, b, None, 0)
+        buf = np.zeros(max(n, 1), "<u2")
+        self.L.mth_items(self.h, doc, start, b, _p(buf), n)
+        return buf[:n].tolist()
 
     def pos_from_relative_pos(self, doc, key_id, value_id, before=False, offset=None, ref_seq=0, long_client=-1):
         out = np.zeros(1, np.int32)

@@ -1,0 +1,317 @@
+"""SubSequence documents (SharedObjectSequence / SharedNumberSequence: sequence sharedSequence.ts:18-101) against the
+REFERENCE (tests/golden/refsubseq_*.npz, tools/make_ref_goldens.py --subseq).
+
+The fixtures take three generated sets (config-2 observers, config-3 lagged editors with local-pending ops and
+group messages, config-4-shaped long documents whose texts end in newlines) and make every TextSegment insert a
+SubSequence insert of the same units (tests/subseq_logs.py: the items are numbers, an item id is the number). The
+reference replays them with the sequence package's own SubSequence class (type-erased beside merge-tree) and records
+its per-document digests (SubSequence rows dump as kind 3 with their item ids), SnapshotV1 summaries at a cut with
+the digests of fresh replicas that load them and replay the rest, and the first documents' dumps. What differs from
+the TextSegment logs is zamboni's canAppend (MaxRun 128, no newline rule), so every digest differs from the
+TextSegment set's.
+
+CPU tier: the logs regenerate bit-identically; the oracle and the host build of the engine core reproduce every
+digest; the stored logs replay to the stored dumps byte for byte. GPU tier: the HIP engine (each kernel build of the
+profile) reproduces every digest; a document mixing TextSegment and SubSequence inserts is refused at submit.
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import gen
+from fluidframework_amd import oplog as ol
+from fluidframework_amd import snapshot as sn
+import core_host
+import oracle_client as oc
+import subseq_logs
+from test_ref_goldens import _sha, caps_for
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "refsubseq_*.npz")))
+NAMES = [os.path.basename(f)[len("refsubseq_"):-4] for f in FIXTURES]
+
+
+def load(name):
+    z = np.load(os.path.join(GOLDEN, f"refsubseq_{name}.npz"), allow_pickle=False)
+    w = gen.Workload(**json.loads(str(z["workload"])))
+    return z, w
+
+
+def regenerate(name):
+    z, w = load(name)
+    return z, w, subseq_logs.to_run(gen.generate(w, ids=z["doc_ids"], threads=8))
+
+
+def test_fixture_set_complete():
+    assert set(NAMES) == {"c2_observer", "c3_lagged", "c4_scaled"}
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_subseq_digests_differ_from_text_sets(name):
+    """The conversion matters: MaxRun and the missing newline rule change every document's tree."""
+    z, _ = load(name)
+    t = np.load(os.path.join(GOLDEN, f"ref_{name}.npz"), allow_pickle=False)
+    assert np.array_equal(z["doc_ids"], t["doc_ids"])
+    assert (z["digests"] != t["digests"]).all()
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_and_host_core_match_reference(name):
+    z, w, b = regenerate(name)
+    assert _sha(b) == str(z["log_sha256"]), "generator or conversion no longer produces the fixture's op logs"
+    want = z["digests"]
+    _, odig, oerr = oc.replay_batch(b, threads=8)
+    assert (oerr == 0).all()
+    bad = np.nonzero(odig != want)[0]
+    assert len(bad) == 0, f"oracle differs from the reference on docs {bad[:8]}"
+    c = caps_for(w)
+    hdig, herr, _ = core_host.replay_batch(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
+    assert (herr == 0).all()
+    bad = np.nonzero(hdig != want)[0]
+    assert len(bad) == 0, f"engine core (host build) differs from the reference on docs {bad[:8]}"
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_stored_logs_replay_to_reference_dumps(name):
+    z, w = load(name)
+    props, kv = gen.props_table()
+    off = z["keep_dump_off"]
+    for d in range(len(z["keep_local"])):
+        ops = z["keep_ops"][z["keep_op_off"][d]: z["keep_op_off"][d + 1]]
+        text = z["keep_text"][z["keep_text_off"][d]:]
+        c = oc.OracleClient()
+        c.start_collab(int(z["keep_local"][d]))
+        c.replay_arrays(np.ascontiguousarray(ops), np.ascontiguousarray(text), props, kv)
+        ref = z["keep_dumps"][off[d]: off[d + 1]].tobytes()
+        assert c.dump() == ref, f"doc {d}"
+        _, segs = ol.parse_dump(ref)
+        assert segs and all(s["kind"] in (ol.SEG_RUN, ol.SEG_MARKER) for s in segs)
+        assert any(s["kind"] == ol.SEG_RUN and s["items"] for s in segs)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_host_core_text_and_items(name):
+    """getText sees no TextSegment in a SubSequence document (every visible segment adds its placeholder), and
+    getItems of the whole local view is the visible SubSequence rows' items in order (the dump's)."""
+    z, w, b = regenerate(name)
+    b = b.subset(range(4))
+    c = caps_for(w)
+    _, herr, st = core_host.replay_batch(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
+    assert (herr == 0).all()
+    for d in range(b.ndocs):
+        n = st.length_local(d)
+        assert st.text(d) == ""
+        assert st.text_range(d, placeholder="#") == "#" * n
+        hdr, segs = ol.parse_dump(st.dump(d))
+        # the local view: every row not removed (pending local inserts included, pending local removes excluded)
+        want = [u for s in segs if s["kind"] == ol.SEG_RUN and s["removedSeq"] is None for u in s["items"]]
+        items = st.items(d, 0)
+        assert len(items) == n and items == want
+
+
+def _fnv(bs: bytes) -> int:
+    h = 0xcbf29ce484222325
+    for x in bs:
+        h = ((h ^ x) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def items_batch():
+    import text_markers
+    z = np.load(os.path.join(GOLDEN, "refitems_c3_markers.npz"), allow_pickle=False)
+    w = gen.Workload(**json.loads(str(z["workload"])))
+    b = subseq_logs.to_run(text_markers.with_markers(gen.generate(w, ids=z["doc_ids"], threads=8)))
+    return z, w, b
+
+
+def check_items(z, get):
+    """every getItems answer: length and FNV-1a-64 of its item ids; document 0's in full"""
+    blob = z["doc0_units"].tobytes()
+    at = 0
+    for (d, a, e), n, f in zip(z["queries"], z["lengths"], z["fnv"]):
+        got = get(int(d), int(a), None if e == -(1 << 31) else int(e))
+        u = np.asarray(got, "<u2").tobytes()
+        assert len(got) == n and _fnv(u) == int(f), (int(d), int(a), int(e), len(got), int(n))
+        if d == 0:
+            assert u == blob[at: at + len(u)]
+            at += len(u)
+
+
+def test_items_with_markers_host_core():
+    """SharedSequence.getItems over SubSequence documents holding markers: the reference's answers (its splice cut
+    counts a marker's position but pushes none of its items), and the documents' digests."""
+    z, w, b = items_batch()
+    assert _sha(b) == str(z["log_sha256"])
+    c = caps_for(w)
+    hdig, herr, st = core_host.replay_batch(b, (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"]))
+    assert (herr == 0).all() and (hdig == z["digests"]).all()
+    _, odig, _ = oc.replay_batch(b, threads=8)
+    assert (odig == z["digests"]).all()
+    check_items(z, st.items)
+
+
+def _variants(name):
+    from test_ref_goldens import kernel_variants  # noqa: F401  (the same builds as the TextSegment set of the name)
+    _, w = load(name)
+    c = caps_for(w)
+    return [dict(waves=4), dict(waves=8)] if c["ncap"] <= 192 else [dict()]
+
+
+GPU_CASES = [(n, v) for n in NAMES for v in _variants(n)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,variant", GPU_CASES,
+                         ids=[n + "".join(f"-{k}{int(x)}" for k, x in v.items()) for n, v in GPU_CASES])
+def test_gpu_engine_matches_reference(name, variant):
+    from fluidframework_amd.engine import Engine
+    z, w, b = regenerate(name)
+    eng = Engine(b.ndocs, **variant, **caps_for(w))
+    try:
+        eng.start_collab(b.local_long_id)
+        eng.replay(b)
+        err, err_op = eng.errors()
+        assert (err == 0).all(), (err[err != 0][:8], err_op[err != 0][:8])
+        bad = np.nonzero(eng.digests() != z["digests"])[0]
+        assert len(bad) == 0, f"HIP engine differs from the reference on docs {bad[:8]}"
+        for d in range(2):  # getText: no TextSegment; getItems of the whole local view: the dump's visible items
+            n = eng.get_length(d)
+            assert eng.get_text(d) == "" and eng.get_text(d, placeholder="#") == "#" * n
+            _, segs = ol.parse_dump(eng.dump(d))
+            assert eng.get_items(d, 0) == [u for s in segs if s["kind"] == ol.SEG_RUN and s["removedSeq"] is None
+                                           for u in s["items"]]
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])
+def test_gpu_items_with_markers(waves):
+    from fluidframework_amd.engine import Engine
+    z, w, b = items_batch()
+    eng = Engine(b.ndocs, waves=waves, **caps_for(w))
+    try:
+        eng.start_collab(b.local_long_id)
+        eng.replay(b)
+        err, _ = eng.errors()
+        assert (err == 0).all() and (eng.digests() == z["digests"]).all()
+        check_items(z, eng.get_items)
+    finally:
+        eng.close()
+
+
+def _mixed(b, d, first_run: bool):
+    """document d's log with its first text-bearing insert of one kind and every later one of the other"""
+    ops = b.ops.copy()
+    lo, hi = int(b.op_off[d]), int(b.op_off[d + 1])
+    o = ops[lo:hi]
+    ins = np.nonzero(((o["kind"] & 7) == ol.OP_INSERT) & ((o["seg_kind"] & 0x7F) == ol.SEG_TEXT) & (o["text_len"] > 0))[0]
+    o["seg_kind"][ins[1:]] = ol.SEG_TEXT if first_run else ol.SEG_RUN
+    o["seg_kind"][ins[0]] = ol.SEG_RUN if first_run else ol.SEG_TEXT
+    ops[lo:hi] = o
+    import dataclasses
+    return dataclasses.replace(b, ops=ops)
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_segment_kinds_refused():
+    """A document of TextSegments never takes a SubSequence insert, nor the reverse (mt_oplog.h MT_SEG_RUN): the submit
+    is refused with MT_E_ARG, within one batch and across incremental batches; a reset forgets the kinds."""
+    from fluidframework_amd.engine import Engine, EngineError
+    z, w, b = regenerate("c2_observer")
+    b = b.subset(range(2))
+    text_b = gen.generate(w, ids=z["doc_ids"][:2], threads=2)
+    eng = Engine(2, **caps_for(w))
+    try:
+        eng.start_collab(b.local_long_id)
+        for first_run in (True, False):
+            with pytest.raises(EngineError):
+                eng.submit(_mixed(text_b, 1, first_run))
+        eng.replay(b)  # SubSequence documents
+        assert (eng.digests() == z["digests"][:2]).all()
+        with pytest.raises(EngineError):  # a TextSegment batch for them later
+            eng.submit(text_b)
+        eng.reset()
+        eng.start_collab(b.local_long_id)
+        eng.replay(text_b)  # after a reset the same documents take TextSegments
+        t = np.load(os.path.join(GOLDEN, "ref_c2_observer.npz"), allow_pickle=False)
+        assert (eng.digests() == t["digests"][:2]).all()
+    finally:
+        eng.close()
+
+
+def item_interner():
+    """the generator's interner with items 0..127 interned as themselves: a fixture item is the number its id is"""
+    it = gen.generator_interner()
+    for i in range(128):
+        assert it.item(i) == i
+    return it
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_snapshot_emit_and_load_match_reference(name):
+    """SnapshotV1 of SubSequence replicas ({items} specs, MaxRun coalescing) from the host core's dump must hash equal
+    to the reference's tree; our tree loaded (SubSequence.fromJSONObject records) plus the tail must reach the
+    reference's loaded digests, or fail where it fails; the oracle does the same from the reference's own trees."""
+    from test_snapshot_ref import check_loaded, load_arrays, long_name, oracle_dump, oracle_error_index, prefix_arrays, sha
+    z, w, b = regenerate(name)
+    it = item_interner()
+    c = caps_for(w)
+    caps = (c["ncap"], c["hcap"], c["acap"], c["mcap"], c["gcap"], c["ccap"])
+    st = core_host.HostStore(b.ndocs, caps)
+    ld = core_host.HostStore(b.ndocs, caps)
+    for d in range(b.ndocs):
+        cut = int(z["snap_cut"][d])
+        st.start_collab(d, int(b.local_long_id[d]))
+        assert st.replay(d, *prefix_arrays(b, d, cut)) == 0
+        tree = sn.emit_from_dump(st.dump(d), it, long_name)
+        assert sha(tree) == str(z["snap_sha256"][d]), f"doc {d}: emitted snapshot differs from the reference's"
+        arrays, nload = load_arrays(tree, b, d, cut, it)
+        err = ld.replay(d, *arrays)
+        check_loaded(z, d, err, ld.error_op(d) if err else -1, ld.digest(d) if err == 0 else 0, nload, arrays[0])
+    trees = json.loads(str(z["keep_snap_trees"]))
+    assert any("items" in json.dumps(x) for t in trees for x in sn.segment_specs(t))
+    for d, tree in enumerate(trees):  # the reference's own trees
+        arrays, nload = load_arrays(tree, b, d, int(z["snap_cut"][d]), it)
+        err, oc_ = oracle_dump(arrays, -1, it)
+        at = oracle_error_index(arrays, it) if err else -1
+        check_loaded(z, d, err, at, oc_.digest() if err == 0 else 0, nload, arrays[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_snapshot_emit_and_load_match_reference(name, waves):
+    """Both halves on the HIP engine: the prefixes replay on the GPU and their dumps are emitted as SubSequence
+    summaries; the loaded replicas (load records + tail) replay on the GPU as one batch."""
+    from fluidframework_amd.engine import Engine
+    from test_snapshot_ref import check_loaded, load_arrays, long_name, prefix_arrays, sha
+    z, w, b = regenerate(name)
+    it = item_interner()
+    caps = caps_for(w)
+    cuts = [int(x) for x in z["snap_cut"]]
+    pre = Engine(b.ndocs, waves=waves, **caps)
+    pre.start_collab(b.local_long_id)
+    pre.replay(ol.Batch.from_arrays([prefix_arrays(b, d, cuts[d]) for d in range(b.ndocs)], b.local_long_id))
+    err, _ = pre.errors()
+    assert (err == 0).all()
+    loads, nloads = [], []
+    for d in range(b.ndocs):
+        tree = sn.emit_from_dump(pre.dump(d), it, long_name)
+        assert sha(tree) == str(z["snap_sha256"][d]), f"doc {d}: emitted snapshot differs from the reference's"
+        a, n = load_arrays(tree, b, d, cuts[d], it)
+        loads.append(a)
+        nloads.append(n)
+    pre.close()
+    eng = Engine(b.ndocs, **caps)
+    try:
+        eng.replay(ol.Batch.from_arrays(loads, np.full(b.ndocs, -1, np.int32)))
+        err, err_op = eng.errors()
+        dig = eng.digests()
+        for d in range(b.ndocs):
+            check_loaded(z, d, int(err[d]), int(err_op[d]), int(dig[d]), nloads[d], loads[d][0])
+    finally:
+        eng.close()

@@ -22,6 +22,11 @@ def _seg(rec, text, it, props):
     ps = _props(rec, it, props)
     if rec["seg_kind"] == ol.SEG_PERM:
         return [int(rec["text_len"]), -0x80000000]
+    if rec["seg_kind"] == ol.SEG_RUN:  # SubSequence.toJSONObject: {items, props}
+        s = {"items": [it.item_obj(int(u)) for u in text[rec["text_off"]: rec["text_off"] + rec["text_len"]]]}
+        if ps is not None:
+            s["props"] = ps[0]
+        return s
     if rec["seg_kind"] == ol.SEG_MARKER:
         s = {"marker": {"refType": int(rec["pos2"])}}
         if ps is not None:
@@ -108,6 +113,26 @@ def test_wire_ingestion_replays_to_reference_digests(name):
         c.start_collab(int(b.local_long_id[d]))
         assert c.replay_arrays(*_arrays(r)) == 0
         assert c.digest() == int(z["digests"][d]), f"doc {d}"
+
+
+@pytest.mark.parametrize("name", ["c2_observer", "c3_lagged"])
+def test_wire_subsequence_ingestion_replays_to_reference_digests(name):
+    """SubSequence inserts on the wire ({items, props} specs, interned items) rebuild the refsubseq logs: the oracle
+    reaches the reference's SubSequence digests."""
+    import test_ref_subseq as ts
+    z, w, b = ts.regenerate(name)
+    it = ts.item_interner()
+    for d in range(0, b.ndocs, 4):
+        r, nmsg = rebuild(b, d, it)
+        c = oc.OracleClient(it)
+        c.start_collab(int(b.local_long_id[d]))
+        assert c.replay_arrays(*_arrays(r)) == 0
+        assert c.digest() == int(z["digests"][d]), f"doc {d}"
+    # and the product's inverse (wire.record_messages) writes {items} specs back
+    ops, text, props, kv = b.doc_arrays(0)
+    msgs = wire.record_messages(ops, text, props, kv, it, lambda i: f"c{i}")
+    ins = [m["contents"] for m, _ in msgs if m["type"] == "op" and m["contents"].get("type") == 0]
+    assert ins and all("items" in op["seg"] for op in ins)
 
 
 def test_unsupported_wire_ops_raise():

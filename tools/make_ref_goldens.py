@@ -66,8 +66,11 @@ def write_batch(b: ol.Batch, interner: ol.Interner, d: str) -> None:
     b.kv.tofile(os.path.join(d, "kv.bin"))
     b.kv_off.astype("<i8").tofile(os.path.join(d, "kv_off.bin"))
     b.local_long_id.astype("<i4").tofile(os.path.join(d, "local.bin"))
+    meta = {"keys": interner.keys, "values": interner.values}
+    if getattr(interner, "items", None):  # SubSequence items by id (ref_replay.mjs; none: an item is its id)
+        meta["items"] = interner.items
     with open(os.path.join(d, "meta.json"), "w") as f:
-        json.dump({"keys": interner.keys, "values": interner.values}, f)
+        json.dump(meta, f)
 
 
 def log_sha(b: ol.Batch) -> str:
@@ -853,6 +856,106 @@ def make_replaytool(node: str) -> None:
                 "tools/ref_replay_tool.mjs: clientReplayTool.ts's reconstruction over the reference Client"))
 
 
+SUBSEQ_SETS = ("c2_observer", "c3_lagged", "c4_scaled")
+
+
+def make_subseq(node: str) -> None:
+    """tests/golden/refsubseq_<set>.npz: the sets' logs with every TextSegment insert made a SubSequence insert of the
+    same units as numbers (tests/subseq_logs.py: a SharedNumberSequence replica's log; sequence sharedSequence.ts:18-101)
+    replayed by the reference Client with the sequence package's own SubSequence class (type-erased beside merge-tree):
+    per-document digests (SubSequence rows dump as kind 3 with their items), SnapshotV1 summaries at a cut loaded by a
+    fresh reference Client and replayed to the end (tree hashes, loaded digests), and the first documents' logs and
+    dumps. The oracle must agree on every digest."""
+    import oracle_client as oc
+    import subseq_logs
+    for name in SUBSEQ_SETS:
+        w, ids = SETS[name]
+        b = subseq_logs.to_run(gen.generate(w, ids=ids, threads=8))
+        cuts = [snapshot_cut(b.doc(i)[0], int(b.local_long_id[i])) for i in range(b.ndocs)]
+        dumps, info, secs, (trees, loaded, tail_err, tail_msgs, load_err, load_msgs) = run_reference(
+            b, os.path.join(SCRATCH, name + "_subseq"), node, cuts)
+        digests = np.asarray([fnv1a64(x) for x in dumps], np.uint64)
+        orig = np.load(os.path.join(GOLDEN, f"ref_{name}.npz"))["digests"]
+        _, odig, oerr = oc.replay_batch(b, threads=8)
+        agree = int((odig == digests).sum())
+        nrun = int(sum(x.count(bytes([3])) > 0 for x in dumps))
+        print(f"refsubseq_{name}: {b.ndocs} docs, {b.nops} events, reference {info['seconds']:.2f}s; oracle agrees on "
+              f"{agree}/{b.ndocs}; {int((digests != orig).sum())} digests differ from the TextSegment logs'; "
+              f"{len(tail_msgs)} loaded replicas throw, {len(load_msgs)} snapshots do not load", flush=True)
+        keep = b.subset(range(min(KEEP.get(name, KEEP_LOGS), b.ndocs)))
+        np.savez_compressed(
+            os.path.join(GOLDEN, f"refsubseq_{name}.npz"),
+            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(b),
+            digests=digests, nevents=np.diff(b.op_off),
+            keep_ops=keep.ops, keep_op_off=keep.op_off, keep_text=keep.text, keep_text_off=keep.text_off,
+            keep_local=keep.local_long_id,
+            keep_dumps=np.frombuffer(b"".join(dumps[: keep.ndocs]), np.uint8),
+            keep_dump_off=np.concatenate([[0], np.cumsum([len(x) for x in dumps[: keep.ndocs]])]).astype(np.int64),
+            snap_cut=np.asarray(cuts, np.int64),
+            snap_sha256=np.asarray([hashlib.sha256(canonical_tree(t).encode()).hexdigest() for t in trees]),
+            snap_loaded_digests=np.asarray([fnv1a64(x) for x in loaded], np.uint64),
+            snap_tail_error=tail_err,
+            snap_load_error=load_err,
+            keep_snap_trees=json.dumps(trees[: keep.ndocs]),
+            source=("packages/dds/merge-tree/src + packages/dds/sequence/src/sharedSequence.ts SubSequence (reference, "
+                    "type-erased by tools/ts_erase.py) under node by tools/ref_replay.mjs; logs: tests/subseq_logs.py"),
+        )
+        del nrun
+
+
+def item_queries(b, seed: int):
+    """getItems(start, end) queries per document in the local view: the whole sequence (end undefined), ranges inside,
+    a range starting at 0, an empty and a reversed range (none), a negative start, ends past the length; lengths are
+    not known here, so ranges are drawn up to 1,500 and the reference clips them."""
+    q = []
+    rng = np.random.default_rng(seed)
+    for d in range(b.ndocs):
+        q.append([d, 0, None])
+        for _ in range(6):
+            a, e = sorted(int(x) for x in rng.integers(0, 1500, 2))
+            q.append([d, a, e])
+            q.append([d, a, None])
+        a = int(rng.integers(0, 1500))
+        q += [[d, 0, a], [d, a, a], [d, a + 9, a], [d, -3, int(rng.integers(1, 1500))], [d, a, 4000]]
+    return q
+
+
+def make_items(node: str) -> None:
+    """tests/golden/refitems_c3_markers.npz: config-3 logs with markers (tests/text_markers.py) whose TextSegment
+    inserts are SubSequence inserts (tests/subseq_logs.py), replayed by the reference: per-document digests and
+    SharedSequence.getItems(start, end) answers (sharedSequence.ts:150-183 over the reference Client; its splice-based
+    cut makes a marker inside the range shift the answer) as lengths, FNV-1a-64 over the item ids (uint16 LE), and
+    document 0's answers in full."""
+    import oracle_client as oc
+    import subseq_logs
+    import text_markers
+    w, ids = TEXT_SETS["c3_markers"]
+    b = subseq_logs.to_run(text_markers.with_markers(gen.generate(w, ids=ids, threads=8)))
+    q = item_queries(b, 777)
+    d = os.path.join(SCRATCH, "c3_markers_items")
+    write_batch(b, gen.generator_interner(), d)
+    with open(os.path.join(d, "itemqueries.json"), "w") as f:
+        json.dump(q, f)
+    dumps, info, secs, _ = run_reference(b, d, node)
+    items = json.load(open(os.path.join(d, "ref_items.json")))
+    assert len(items) == len(q)
+    digests = np.asarray([fnv1a64(x) for x in dumps], np.uint64)
+    _, odig, _ = oc.replay_batch(b, threads=8)
+    units = [np.asarray(x, "<u2").tobytes() for x in items]
+    qa = np.asarray([[x[0], x[1], -(1 << 31) if x[2] is None else x[2]] for x in q], np.int32)
+    blob = np.frombuffer(b"".join(u for (x, u) in zip(q, units) if x[0] == 0), np.uint8)
+    np.savez_compressed(
+        os.path.join(GOLDEN, "refitems_c3_markers.npz"),
+        workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(b),
+        digests=digests, queries=qa, lengths=np.asarray([len(x) for x in items], np.int64),
+        fnv=np.asarray([fnv1a64(u) for u in units], np.uint64), doc0_units=blob,
+        source=("packages/dds/merge-tree/src + sequence sharedSequence.ts SubSequence (reference, type-erased by "
+                "tools/ts_erase.py) under node by tools/ref_replay.mjs: SharedSequence.getItems after each replay"),
+    )
+    print(f"refitems_c3_markers: {b.ndocs} docs, {len(q)} queries, {sum(len(x) for x in items)} items; oracle agrees "
+          f"on {int((odig == digests).sum())}/{b.ndocs} digests", flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default=",".join(SETS))
@@ -871,8 +974,13 @@ def main() -> None:
     ap.add_argument("--unref", action="store_true", help="write the removeLocalReference fixtures (refunref_*.npz) only")
     ap.add_argument("--persp", action="store_true", help="write the past-perspective read fixtures (refpersp_*.npz) only")
     ap.add_argument("--replaytool", action="store_true", help="write the client replay tool fixture only")
+    ap.add_argument("--subseq", action="store_true", help="write the SubSequence fixtures (refsubseq_*.npz) only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
+    if args.subseq:
+        make_subseq(args.node)
+        make_items(args.node)
+        return
     if args.replaytool:
         make_replaytool(args.node)
         return

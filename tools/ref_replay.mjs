@@ -24,7 +24,7 @@ const withDeltas = process.argv.includes("--deltas");
 // segments reset their start; dumps carry allocated starts (MT_DF_HANDLE) -> batch-dir/ref_handles.json
 const withHandles = process.argv.includes("--handles");
 const traceDoc = process.argv.includes("--trace-refs") ? Number(process.argv[process.argv.indexOf("--trace-refs") + 1]) : -1;
-let Client, TextSegment, Marker, PermutationSegment, SnapshotV1, SnapshotLegacy, LocalReference; // bound in main() (Node 12 has no top-level await)
+let Client, TextSegment, Marker, PermutationSegment, SubSequence, SnapshotV1, SnapshotLegacy, LocalReference; // bound in main() (Node 12 has no top-level await)
 let HandleTable, isHandleValid;
 let curHandles = null; // the HandleTable of the replica being replayed (--handles)
 const handleTables = {};
@@ -69,6 +69,35 @@ function textOf(doc, rec) {
     return s;
 }
 
+// SubSequence items (mt_oplog.h MT_SEG_RUN: the text units are item ids): meta.items, when present, is the host's item
+// interner (id -> canonical JSON); without it an item is the number its id is (a SharedNumberSequence)
+const items = meta.items || null;
+const itemId = items ? new Map(items.map((v, i) => [v, i])) : null;
+function itemsOf(doc, rec) {
+    const off = textOff[doc] + rec.text_off, out = [];
+    for (let j = 0; j < rec.text_len; j++) {
+        const u = text.readUInt16LE(2 * (off + j));
+        out.push(items ? JSON.parse(items[u]) : u);
+    }
+    return out;
+}
+function itemUnit(v) {
+    if (!items) return v;
+    const id = itemId.get(canonical(v));
+    if (id === undefined) throw new Error(`item not in the interner: ${canonical(v)}`);
+    return id;
+}
+// a record's inserted segment (insertSegmentLocal / MergeTree.insertSegments): TextSegment.make, Marker.make, a
+// PermutationSegment or a SubSequence, with the record's properties
+function segOf(doc, rec, ps) {
+    if (rec.seg_kind === 2 || rec.seg_kind === 3) {
+        const seg = rec.seg_kind === 2 ? new PermutationSegment(rec.text_len) : new SubSequence(itemsOf(doc, rec));
+        if (ps) seg.addProperties(ps.set);
+        return seg;
+    }
+    return rec.seg_kind === 1 ? Marker.make(rec.pos2, ps && ps.set) : TextSegment.make(textOf(doc, rec), ps && ps.set);
+}
+
 function record(i) {
     const b = 32 * i;
     return {
@@ -104,6 +133,7 @@ function wireOpAbs(doc, rec) {
         let seg;
         if (rec.seg_kind === 2) return { type: 0, pos1: rec.pos1, seg: new PermutationSegment(rec.text_len).toJSONObject() };
         if (rec.seg_kind === 1) seg = { marker: { refType: rec.pos2 } };
+        else if (rec.seg_kind === 3) seg = { items: itemsOf(doc, rec) }; // SubSequence.toJSONObject
         else seg = ps ? { text: textOf(doc, rec) } : textOf(doc, rec);
         if (ps) seg.props = ps.set;
         return { type: 0, pos1: rec.pos1, seg };
@@ -114,9 +144,11 @@ function wireOpAbs(doc, rec) {
     return op;
 }
 
-// SharedString's specToSegment; PermutationVector's (PermutationSegment.fromJSONObject) for array specs
+// SharedString's specToSegment; PermutationVector's (PermutationSegment.fromJSONObject) for array specs; SharedSequence's
+// (SubSequence.fromJSONObject, sequenceFactory.ts) for {items} specs
 const specToSegment = (spec) => (Array.isArray(spec) ? PermutationSegment.fromJSONObject(spec)
-    : TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec));
+    : (spec && typeof spec === "object" && "items" in spec) ? SubSequence.fromJSONObject(spec)
+        : TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec));
 const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
 
 // apply records [from, to) of `doc` to `client` (applyMsg / the local-edit entry points)
@@ -159,7 +191,8 @@ function applyRange(client, doc, from, to) {
             const w = [3, -1]; // MT_DELTA_REGEN
             for (const o of ops) {
                 const len = o.type === 0 ? (typeof o.seg === "string" ? o.seg.length : o.seg.text !== undefined
-                    ? o.seg.text.length : Array.isArray(o.seg) ? o.seg[0] : 1) : o.pos2 - o.pos1;
+                    ? o.seg.text.length : o.seg.items !== undefined ? o.seg.items.length : Array.isArray(o.seg) ? o.seg[0] : 1)
+                    : o.pos2 - o.pos1;
                 w.push(o.pos1, len, o.type);
             }
             w.push(END, ops.length);
@@ -178,9 +211,7 @@ function applyRange(client, doc, from, to) {
             const opArgs = { op: wireOp(doc, rec) };
             const ps = propSet(doc, rec.props);
             if (kind === 0) {
-                const seg = rec.seg_kind === 2 ? new PermutationSegment(rec.text_len)
-                    : rec.seg_kind === 1 ? Marker.make(rec.pos2, ps && ps.set) : TextSegment.make(textOf(doc, rec), ps && ps.set);
-                if (rec.seg_kind === 2 && ps) seg.addProperties(ps.set);
+                const seg = segOf(doc, rec, ps);
                 mt.insertSegments(rec.pos1, [seg], rec.ref_seq, cid, rec.seq, opArgs);
             } else if (kind === 1) {
                 mt.markRangeRemoved(rec.pos1, rec.pos2, rec.ref_seq, cid, rec.seq, false, opArgs);
@@ -197,9 +228,7 @@ function applyRange(client, doc, from, to) {
             }
             if (kind === 0) {
                 const ps = propSet(doc, rec.props);
-                const seg = rec.seg_kind === 2 ? new PermutationSegment(rec.text_len)
-                    : rec.seg_kind === 1 ? Marker.make(rec.pos2, ps && ps.set) : TextSegment.make(textOf(doc, rec), ps && ps.set);
-                if (rec.seg_kind === 2 && ps) seg.addProperties(ps.set);
+                const seg = segOf(doc, rec, ps);
                 let sent;
                 if (rec.kind & 0x08) { // MT_OPF_ATREF: insertAtReferencePositionLocal at reference pos1
                     const r = curRefs[rec.pos1];
@@ -543,8 +572,8 @@ function dump(client) {
     leaves.forEach((b, li) => {
         for (let i = 0; i < b.childCount; i++) {
             const s = b.children[i];
-            const isText = s.type === "TextSegment", isMarker = s.type === "Marker";
-            const kind = isText ? 0 : isMarker ? 1 : 2;
+            const isText = s.type === "TextSegment", isMarker = s.type === "Marker", isRun = s.type === "SubSequence";
+            const kind = isText ? 0 : isMarker ? 1 : isRun ? 3 : 2;
             const hasProps = s.properties !== undefined;
             const hnd = s.type === "PermutationSegment" && s.start >= 1; // an allocated start
             const removed = s.removedSeq !== undefined;
@@ -581,6 +610,7 @@ function dump(client) {
             for (const x of extra) o.i32(x);
             if (hnd) o.i32(s.start); // MT_DF_HANDLE
             if (isText) for (let j = 0; j < s.text.length; j++) o.u16(s.text.charCodeAt(j));
+            if (isRun) for (const v of s.items) o.u16(itemUnit(v));
         }
     });
     return o.buf();
@@ -590,6 +620,7 @@ async function main() {
 MT = await import(path.join(erased, "index.mjs"));
 ({ Client, TextSegment, Marker, LocalReference } = MT);
 ({ PermutationSegment } = await import(path.join(erased, "permutationSegment.mjs")));
+({ SubSequence } = await import(path.join(erased, "subSequence.mjs")));
 ({ HandleTable, isHandleValid } = await import(path.join(erased, "handletable.mjs")));
 ({ SnapshotV1 } = await import(path.join(erased, "snapshotV1.mjs")));
 ({ SnapshotLegacy } = await import(path.join(erased, "snapshotlegacy.mjs")));
@@ -615,6 +646,27 @@ const relAnswers = [];
 const lqpath = path.join(dir, "lenqueries.json");
 const lenQueries = fs.existsSync(lqpath) ? JSON.parse(fs.readFileSync(lqpath)) : [];
 const lengths = [];
+// optional getItems queries (itemqueries.json: [[doc, start, end | null], ...]): SharedSequence.getItems (sequence
+// sharedSequence.ts:150-183, restated below over the reference Client, as SharedSegmentSequence's walkSegments and
+// getPosition forward to it) after the doc's replay -> ref_items.json (item ids, itemUnit)
+const iqpath = path.join(dir, "itemqueries.json");
+const itemQueries = fs.existsSync(iqpath) ? JSON.parse(fs.readFileSync(iqpath)) : [];
+const itemAnswers = [];
+function getItems(client, start, end) {
+    const out = [];
+    let firstSegment;
+    if (end !== undefined && end <= start) return out;
+    client.walkSegments((segment) => {
+        if (SubSequence.is(segment)) {
+            if (firstSegment === undefined) firstSegment = segment;
+            out.push(...segment.items);
+        }
+        return true;
+    }, start, end);
+    if (firstSegment !== undefined) out.splice(0, start - client.getPosition(firstSegment));
+    if (end !== undefined) out.splice(end - start);
+    return out;
+}
 const t0 = process.hrtime.bigint();
 const dumps = [], errs = {};
 for (let d = 0; d < ndocs; d++) {
@@ -658,6 +710,10 @@ for (let d = 0; d < ndocs; d++) {
             const refSeq = local ? mt.collabWindow.currentSeq : ref;
             const cid = local ? mt.collabWindow.clientId : c.getOrAddShortClientId(name(cl));
             lengths.push(mt.getLength(refSeq, cid));
+        }
+        for (const [qd, st, en] of itemQueries) {
+            if (qd !== d) continue;
+            itemAnswers.push(getItems(c, st, en === null ? undefined : en).map(itemUnit));
         }
         for (const [qd, id, before, offset] of relQueries) {
             if (qd !== d) continue;
@@ -757,6 +813,7 @@ if (Object.keys(refPositions).length) {
 fs.writeFileSync(path.join(dir, "ref_err.json"), JSON.stringify({ errors: errs, seconds: secs }));
 if (queries.length) fs.writeFileSync(path.join(dir, "ref_answers.json"), JSON.stringify(answers));
 if (textQueries.length) fs.writeFileSync(path.join(dir, "ref_texts.json"), JSON.stringify(texts));
+if (itemQueries.length) fs.writeFileSync(path.join(dir, "ref_items.json"), JSON.stringify(itemAnswers));
 if (lenQueries.length) fs.writeFileSync(path.join(dir, "ref_lengths.json"), JSON.stringify(lengths));
 if (withHandles) {
     const snap = {};

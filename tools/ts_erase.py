@@ -1118,16 +1118,41 @@ def matrix_sources(matrix_dir: str) -> Dict[str, str]:
     return {"handletable": handletable, "permutationSegment": head + cls + "\n"}
 
 
+SEQUENCE_SRC = "/root/reference/packages/dds/sequence/src"
+
+
+def sequence_sources(seq_dir: str) -> Dict[str, str]:
+    """The sequence package's SubSequence segment (sharedSequence.ts:12-101: SharedObjectSequence / SharedNumberSequence
+    items) and its MaxRun constant, as one extra module over the erased merge-tree. Only the segment class is taken:
+    SharedSequence itself needs the container runtime, while the fixtures replay raw Client ops on SubSequence rows."""
+    with open(os.path.join(seq_dir, "sharedSequence.ts")) as f:
+        src = f.read()
+    m = Module("sharedSequence", src)
+    k = next(i for i, t in enumerate(m.toks) if t.text == "class" and m.t(i + 1) == "SubSequence")
+    j = k
+    while m.t(j) != "{":
+        j += 1
+    cls = src[m.toks[k - 1].start:m.toks[m.match[j]].end]
+    c = next(i for i, t in enumerate(m.toks) if t.text == "const" and m.t(i + 1) == "MaxRun")
+    e = c
+    while m.t(e) != ";":
+        e += 1
+    maxrun = src[m.toks[c].start:m.toks[e].end]
+    head = 'import { BaseSegment, LocalReferenceCollection } from "./index";\n'
+    return {"subSequence": head + maxrun + "\n" + cls + "\n"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--src", default="/root/reference/packages/dds/merge-tree/src")
     ap.add_argument("--out", default="/tmp/mt-oracle")
     ap.add_argument("--matrix", default=MATRIX_SRC)
+    ap.add_argument("--sequence", default=SEQUENCE_SRC)
     args = ap.parse_args()
     if os.path.abspath(args.out).startswith(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))):
         raise SystemExit("the erased reference must not be written inside the repository")
-    erase_project(args.src, args.out, MT_FILES, matrix_sources(args.matrix))
-    print(f"erased {len(MT_FILES)} merge-tree modules + PermutationSegment into {args.out}")
+    erase_project(args.src, args.out, MT_FILES, {**matrix_sources(args.matrix), **sequence_sources(args.sequence)})
+    print(f"erased {len(MT_FILES)} merge-tree modules + PermutationSegment + SubSequence into {args.out}")
 
 
 if __name__ == "__main__":
