@@ -90,6 +90,9 @@ export interface DeltaEvent {
 export declare class Interner {
     key(k: string): number;
     value(v: unknown): number;
+    /** a SubSequence item's id (the units of a SubSequence row) and back */
+    item(v: unknown): number;
+    itemObj(i: number): unknown;
 }
 
 export declare function decodeDeltas(words: Int32Array, interner: Interner): DeltaEvent[];
@@ -132,6 +135,11 @@ export declare class GpuClient {
     /** Client.applyMsg (client.ts:797-819), group ops included */
     applyMsg(msg: SequencedMessage): void;
     insertTextLocal(pos: number, text: string, props?: PropertySet): MergeTreeOp | undefined;
+    /** SharedSequence.insert (sequence sharedSequence.ts:116-125): a SubSequence of `items` */
+    insertItemsLocal(pos: number, items: unknown[], props?: PropertySet): MergeTreeOp | undefined;
+    /** SharedSequence.getItems (sharedSequence.ts:150-183) / getItemCount of a SubSequence document */
+    getItems(start: number, end?: number): unknown[];
+    getItemCount(): number;
     insertMarkerLocal(pos: number, refType: number, props?: PropertySet): MergeTreeOp;
     removeRangeLocal(start: number, end: number): MergeTreeOp;
     annotateRangeLocal(start: number, end: number, props: PropertySet, combiningOp?: ICombiningOp): MergeTreeOp;

@@ -33,7 +33,7 @@ const ReferenceType = { Simple: 0x0, Tile: 0x1, NestBegin: 0x2, NestEnd: 0x4, Sl
 const NOOP_SPLIT = 1; // seg_kind of a local NOOP record: walkSegments' splitRange (mt_oplog.h MT_NOOP_SPLIT)
 const TILE_LABELS_KEY = "referenceTileLabels"; // reservedTileLabelsKey (mergeTree.ts:615)
 const HANDLE_UNALLOCATED = -0x80000000; // Handle.unallocated (matrix handletable.ts:11)
-const SEG = { TEXT: 0, MARKER: 1, PERM: 2 };
+const SEG = { TEXT: 0, MARKER: 1, PERM: 2, RUN: 3 }; // RUN: SubSequence items (mt_oplog.h MT_SEG_RUN)
 const SEG_RELPOS = 0x80; // positions relative to markers (mt_oplog.h MT_SEG_RELPOS)
 const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
 const VALUE_FALSY = 0x8000;
@@ -52,7 +52,20 @@ function canonical(v) {
 
 /* batch-global property key / value tables (value id 0 = null = delete, segmentPropertiesManager.ts:102-106) */
 class Interner {
-    constructor() { this.keys = new Map(); this.values = new Map(); this.nk = 1; this.nv = 1; }
+    constructor() { this.keys = new Map(); this.values = new Map(); this.nk = 1; this.nv = 1; this.items = new Map(); this.itemList = []; }
+    /* SubSequence items (SharedObjectSequence / SharedNumberSequence) by canonical JSON: a SubSequence row's units */
+    item(v) {
+        const s = canonical(v);
+        let i = this.items.get(s);
+        if (i === undefined) {
+            if (this.itemList.length > 0xffff) throw new Error("too many distinct SubSequence items");
+            i = this.itemList.length;
+            this.items.set(s, i);
+            this.itemList.push(v);
+        }
+        return i;
+    }
+    itemObj(i) { return this.itemList[i]; }
     key(k) {
         let i = this.keys.get(k);
         if (i === undefined) { i = this.nk++; this.keys.set(k, i); }
@@ -137,6 +150,7 @@ function decodeDeltas(words, interner) {
  * (undefined when not removed), localSeq / localRemovedSeq, properties, text / refType / start, the leaf block
  * ordinal and its index (ordinal) in walkAllSegments order. */
 function decodeDump(bytes, interner, nameOf) {
+    const TYPES = ["TextSegment", "Marker", "PermutationSegment", "SubSequence"];
     const dv = new DataView(bytes.buffer, bytes.byteOffset, bytes.byteLength);
     const keyName = new Map([...interner.keys].map(([k, i]) => [i, k]));
     const valueOf = new Map([...interner.values].map(([v, i]) => [i, JSON.parse(v)]));
@@ -175,7 +189,7 @@ function decodeDump(bytes, interner, nameOf) {
         let start = HANDLE_UNALLOCATED;
         if (flags & 16) { start = dv.getInt32(o, true); o += 4; }
         const seg = {
-            type: kind === SEG.TEXT ? "TextSegment" : kind === SEG.MARKER ? "Marker" : "PermutationSegment",
+            type: TYPES[kind],
             cachedLength: f[0], seq: f[1], clientId: nameOf(f[2]),
             removedSeq: flags & 2 ? f[3] : undefined, removedClientId: flags & 2 ? nameOf(f[4]) : undefined,
             localSeq: flags & 4 ? f[5] : undefined, localRemovedSeq: flags & 8 ? f[6] : undefined,
@@ -186,6 +200,10 @@ function decodeDump(bytes, interner, nameOf) {
             for (let j = 0; j < f[0]; j++) t += String.fromCharCode(dv.getUint16(o + 2 * j, true));
             o += 2 * f[0];
             seg.text = t;
+        } else if (kind === SEG.RUN) { // SubSequence.items
+            seg.items = [];
+            for (let j = 0; j < f[0]; j++) seg.items.push(interner.itemObj(dv.getUint16(o + 2 * j, true)));
+            o += 2 * f[0];
         } else if (kind === SEG.MARKER) {
             seg.refType = refType;
         } else {
@@ -272,6 +290,9 @@ class ReplayEngine {
             } else if (seg && typeof seg.text === "string") {
                 r.text_off = q.text.length; r.text_len = seg.text.length; props = seg.props;
                 for (let i = 0; i < seg.text.length; i++) q.text.push(seg.text.charCodeAt(i));
+            } else if (seg && Array.isArray(seg.items)) { // SubSequence {items, props} (sharedSequence.ts:23-47)
+                r.seg_kind = SEG.RUN; r.text_off = q.text.length; r.text_len = seg.items.length; props = seg.props;
+                for (const v of seg.items) q.text.push(this.interner.item(v));
             } else {
                 throw new Error("unsupported segment spec");
             }
@@ -281,7 +302,7 @@ class ReplayEngine {
         }
         if (fields.rel1 || fields.rel2) { // IRelativePosition(s): the spec follows the record's text (mt_oplog.h MT_SEG_RELPOS)
             delete r.rel1; delete r.rel2;
-            if (!(k === OP.INSERT && r.seg_kind === SEG.TEXT)) { r.text_off = q.text.length; r.text_len = 0; }
+            if (!(k === OP.INSERT && (r.seg_kind === SEG.TEXT || r.seg_kind === SEG.RUN))) { r.text_off = q.text.length; r.text_len = 0; }
             q.text.push(this.interner.key(MARKER_ID_KEY), (fields.rel1 ? 1 : 0) | (fields.rel2 ? 2 : 0));
             for (const rp of [fields.rel1, fields.rel2]) {
                 if (!rp) { q.text.push(0, 0, 0, 0); continue; }
@@ -671,14 +692,32 @@ class GpuClient {
         }
     }
 
+    /* SharedSequence.insert(pos, items, props) (sequence sharedSequence.ts:116-125): a SubSequence of the items
+     * (interned; a SharedObjectSequence / SharedNumberSequence document holds no TextSegment) */
+    insertItemsLocal(pos, items, props) {
+        if (items.length === 0) return undefined;
+        const seg = props ? { items, props } : { items };
+        this.engine.enqueue(this.doc, OP.INSERT | OPF_LOCAL, { pos1: pos }, seg);
+        this.sent(OP.INSERT);
+        return { type: OP.INSERT, pos1: pos, seg };
+    }
+
+    /* SharedSequence.getItems(start, end) (sharedSequence.ts:150-183) / getItemCount(): the local view's items of
+     * [start, end) (mt_engine_get_items: the reference's splice-based cut, a marker inside the range included) */
+    getItems(start, end) {
+        return addon.getItems(this.read(), this.doc, start, end).map((i) => this.engine.interner.itemObj(i));
+    }
+    getItemCount() { return this.getLength(); }
+
     /* Client.insertSegmentLocal(pos, segment) (client.ts:202-211) for a segment spec: a string, {text, props},
-     * {marker: {refType}, props} or a PermutationSegment [length, start] */
+     * {marker: {refType}, props}, {items, props} (SubSequence) or a PermutationSegment [length, start] */
     insertSegmentLocal(pos, spec) {
         if (typeof spec === "string" || (spec && typeof spec.text === "string")) {
             const text = typeof spec === "string" ? spec : spec.text;
             return this.insertTextLocal(pos, text, typeof spec === "string" ? undefined : spec.props);
         }
         if (spec && spec.marker) return this.insertMarkerLocal(pos, spec.marker.refType, spec.props);
+        if (spec && Array.isArray(spec.items)) return this.insertItemsLocal(pos, spec.items, spec.props);
         if (Array.isArray(spec)) {
             this.engine.enqueue(this.doc, OP.INSERT | OPF_LOCAL, { pos1: pos }, spec);
             this.sent(OP.INSERT);

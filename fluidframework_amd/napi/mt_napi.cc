@@ -416,6 +416,31 @@ static napi_value js_get_text(napi_env env, napi_callback_info info) {
     return s;
 }
 
+/* getItems(h, doc, start[, end]) -> item ids: SharedSequence.getItems (sequence sharedSequence.ts:150-183) of a
+ * SubSequence document in the local view (mt_engine_get_items; an undefined end is the reference's undefined) */
+static napi_value js_get_items(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    size_t argc = 4;
+    if (napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr) != napi_ok || argc < 3) {
+        napi_throw_type_error(env, nullptr, "missing arguments");
+        return nullptr;
+    }
+    mt_engine* e = engine_of(env, argv[0]);
+    int64_t doc;
+    int32_t start, end = MT_TEXT_DEFAULT;
+    if (!e || !i64_of(env, argv[1], &doc) || !i32_of(env, argv[2], &start)) return nullptr;
+    if (argc > 3 && !opt_undefined(env, argv[3]) && !i32_of(env, argv[3], &end)) return nullptr;
+    int64_t n = mt_engine_get_items(e, doc, start, end, nullptr, 0);
+    if (n < 0) return throw_status(env, e, (int32_t)-n, "mt_engine_get_items");
+    std::vector<uint16_t> buf((size_t)n + 1);
+    int64_t m = mt_engine_get_items(e, doc, start, end, buf.data(), n);
+    if (m < 0) return throw_status(env, e, (int32_t)-m, "mt_engine_get_items");
+    napi_value arr;
+    NAPI_OK(napi_create_array_with_length(env, (size_t)n, &arr));
+    for (int64_t i = 0; i < n; i++) NAPI_OK(napi_set_element(env, arr, (uint32_t)i, num(env, buf[(size_t)i])));
+    return arr;
+}
+
 /* an mt_seg_ref as {rid, gen, offset, length, seq, client, removedSeq, removedClient, ordinal}; undefined for none
  * (removedSeq: undefined when not removed, as the reference's ISegment.removedSeq) */
 static napi_value seg_ref_value(napi_env env, const mt_seg_ref& r) {
@@ -629,7 +654,7 @@ static napi_value init(napi_env env, napi_value exports) {
     } fns[] = {{"create", js_create},       {"startCollab", js_start_collab}, {"submit", js_submit},
                {"run", js_run},             {"sync", js_sync},                {"reset", js_reset},
                {"errors", js_errors},       {"digests", js_digests},          {"getLength", js_get_length},
-               {"getText", js_get_text}, {"posFromRelativePos", js_pos_from_relpos},
+               {"getText", js_get_text}, {"getItems", js_get_items}, {"posFromRelativePos", js_pos_from_relpos},
                {"handleTable", js_handle_table},     {"getHandle", js_get_handle},    {"getContainingSegment", js_get_containing},
                {"getPosition", js_get_position}, {"ndocs", js_ndocs},        {"lastRunMs", js_last_run_ms},
                {"deltas", js_deltas},       {"refPositions", js_ref_positions},

@@ -29,8 +29,10 @@ The tool as written tests `message.clientId !== clientId` (clientReplayTool.ts:2
 OTHER clients' ops as local transactions and then again as remote messages, never the client's own, and
 could not pass its own final equality asserts; this module follows the evident intent (own messages are local
 transactions, every message is applied once, in order), and tools/ref_replay_tool.mjs restates the same loop
-over the reference merge-tree to pin it. Sequence types other than SharedString (object / number sequences,
-sparse matrix: segment types the engine does not model) raise.
+over the reference merge-tree to pin it. SharedObjectSequence / SharedNumberSequence trees (the tool's other
+mergeTreeTypes, SubSequence.fromJSONObject specs: sequence sharedSequence.ts:18-101) replay as SubSequence documents
+(mt_oplog.h MT_SEG_RUN) whose replicas also report their items (SharedSequence.getItems); a sparse matrix
+(RunSegment / PaddingSegment, sequence sparsematrix.ts) raises.
 """
 from __future__ import annotations
 
@@ -46,9 +48,10 @@ CHUNKED_OP = "chunkedOp"  # ContainerMessageType.ChunkedOp (containerRuntime.ts:
 ATTACH = "attach"  # ContainerMessageType.Attach (134)
 OPERATION = "op"  # MessageType.Operation (protocol.ts:16)
 SHARED_STRING = "https://graph.microsoft.com/types/mergeTree"  # SharedStringFactory.Type (sequenceFactory.ts:23)
-OTHER_SEQUENCES = ("https://graph.microsoft.com/types/mergeTree/object-sequence",
-                   "https://graph.microsoft.com/types/mergeTree/number-sequence",
-                   "https://graph.microsoft.com/types/mergeTree/sparse-matrix")
+OBJECT_SEQUENCE = "https://graph.microsoft.com/types/mergeTree/object-sequence"  # SharedObjectSequenceFactory.Type
+NUMBER_SEQUENCE = "https://graph.microsoft.com/types/mergeTree/number-sequence"  # SharedNumberSequenceFactory.Type
+SPARSE_MATRIX = "https://graph.microsoft.com/types/mergeTree/sparse-matrix"      # SparseMatrixFactory.Type
+SEQUENCE_TYPES = (OBJECT_SEQUENCE, NUMBER_SEQUENCE)
 READONLY = "readonly"
 
 
@@ -100,14 +103,14 @@ def dds_trees(attach: Dict[str, Any]) -> Dict[str, List[tuple]]:
     return out
 
 
-def merge_trees_of(attach: Dict[str, Any]) -> Dict[str, dict]:
-    """processAttachMessage (264-320): full path -> the `content` subtree of each SharedString in the snapshot."""
+def merge_trees_of(attach: Dict[str, Any], types: Optional[Dict[str, str]] = None) -> Dict[str, dict]:
+    """processAttachMessage (264-320): full path -> the `content` subtree of each merge tree in the snapshot, in the
+    tool's mergeTreeTypes order (SharedString, then the object and number sequences); `types` gets each path's type."""
     found = {}
     trees = dds_trees(attach)
-    for t in OTHER_SEQUENCES:
-        if t in trees:
-            raise ValueError(f"{t}: its segment types are not modelled by the engine")
-    for path, tree in trees.get(SHARED_STRING, []):
+    if SPARSE_MATRIX in trees:
+        raise ValueError(f"{SPARSE_MATRIX}: its RunSegment / PaddingSegment types are not modelled by the engine")
+    for typ, path, tree in [(t, p, x) for t in (SHARED_STRING,) + SEQUENCE_TYPES for p, x in trees.get(t, [])]:
         entries = list(tree.get("entries") or [])
         content = None
         while entries:
@@ -117,6 +120,8 @@ def merge_trees_of(attach: Dict[str, Any]) -> Dict[str, dict]:
         if content is None or content["path"] != "content":
             raise ValueError(f"{path}: no content tree")
         found[path] = content["value"]
+        if types is not None:
+            types[path] = typ
     return found
 
 
@@ -124,6 +129,7 @@ def merge_trees_of(attach: Dict[str, Any]) -> Dict[str, dict]:
 class Log:
     """The merge-tree messages of a recorded document and the attach snapshots of its merge trees."""
     trees: Dict[str, dict] = field(default_factory=dict)  # full path -> merge-tree snapshot
+    types: Dict[str, str] = field(default_factory=dict)  # full path -> its channel type
     messages: List[Dict[str, Any]] = field(default_factory=list)  # sequenced messages, contents = the op
     paths: List[str] = field(default_factory=list)  # each message's merge tree
     clients: List[str] = field(default_factory=list)  # clients that sent an op to a merge tree, first-seen order
@@ -152,7 +158,7 @@ def parse(messages: Iterable[Dict[str, Any]]) -> Log:
             if c.get("type") == ATTACH:  # a legacy attach inside the envelopes
                 a = dict(c["content"])
                 a["id"] = "/".join(str(p) for p in parts + [a["id"]])
-                log.trees.update(merge_trees_of(a))
+                log.trees.update(merge_trees_of(a, log.types))
                 continue
             content = c.get("content")
             if not isinstance(content, dict):
@@ -165,7 +171,7 @@ def parse(messages: Iterable[Dict[str, Any]]) -> Log:
                     log.messages.append(dict(m, contents=_parse(content["contents"])))
                     log.paths.append(path)
         elif t == ATTACH:
-            log.trees.update(merge_trees_of(_parse(m["contents"])))
+            log.trees.update(merge_trees_of(_parse(m["contents"]), log.types))
     return log
 
 
@@ -232,7 +238,8 @@ def streams(log: Log, interner: Optional[ol.Interner] = None) -> Streams:
 
 def replay(log: Log, device: int = 0, **caps):
     """Replay every (merge tree, client) replica of a recorded log in one engine launch on `device`; returns
-    [(path, client, text, length)] in clientReplayTool's order (clients, then merge trees)."""
+    [(path, client, text, length, items)] in clientReplayTool's order (clients, then merge trees); items: a sequence
+    tree's SharedSequence.getItems(0) values, None for a SharedString."""
     from .engine import Engine, default_caps
     st = streams(log)
     c = default_caps(0)
@@ -246,7 +253,9 @@ def replay(log: Log, device: int = 0, **caps):
         if bad:
             i = bad[0]
             raise RuntimeError(f"replica {st.docs[i]} failed at record {err_op[i]}: error {err[i]}")
-        return [(p, c_, eng.get_text(i), eng.get_length(i)) for i, (p, c_) in enumerate(st.docs)]
+        return [(p, c_, eng.get_text(i), eng.get_length(i),
+                 [st.interner.item_obj(u) for u in eng.get_items(i, 0)] if log.types.get(p) in SEQUENCE_TYPES else None)
+                for i, (p, c_) in enumerate(st.docs)]
     finally:
         eng.close()
 
@@ -269,15 +278,15 @@ def main(argv=None) -> int:
         msgs = json.load(f)[: a.to]
     log = parse(msgs)
     for path in log.trees:
-        print(f"MergeTree Found:\n {json.dumps({'fullPath': path, 'type': SHARED_STRING})}")
+        print(f"MergeTree Found:\n {json.dumps({'fullPath': path, 'type': log.types.get(path, SHARED_STRING)})}")
     if a.verbose:
         for p, m in zip(log.paths, log.messages):
             print(f"MergeTree op {p}:\n {json.dumps(m['contents'])}")
     reps = replay(log)
-    obs = {p: (t, n) for p, c, t, n in reps if c == READONLY}
+    obs = {p: (t, n, it) for p, c, t, n, it in reps if c == READONLY}
     errors = 0
-    for p, c, t, n in reps:
-        if (t, n) != obs[p]:
+    for p, c, t, n, it in reps:  # the tool compares getLength and getText; a sequence's items are compared too
+        if (t, n, it) != obs[p]:
             errors += 1
             if errors <= 5:
                 print(f"{c} {p}: length {n} text differs from the readonly client's (length {obs[p][1]})",

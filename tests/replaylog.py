@@ -37,18 +37,59 @@ def _attach_snapshot(fixture: str) -> dict:
                          "value": {"entries": [attrs] + summary["entries"]}}]}
 
 
+def _sequence_snapshot(kind: str, seed: int) -> dict:
+    """a data store's snapshot holding one SharedObjectSequence / SharedNumberSequence: `.attributes` naming its type
+    + a `content` tree, the v1 summary (snapshot.emit_v1) of a few SubSequence segments of items"""
+    from fluidframework_amd import snapshot as sn
+    it = ol.Interner()
+    rng = np.random.default_rng(1000 + seed)
+    segs = []
+    for k in range(6):
+        items = [_item(kind, int(x)) for x in rng.integers(48, 123, int(rng.integers(1, 40)))]
+        segs.append(dict(kind=ol.SEG_RUN, flags=0, ngroups=0, len=len(items), seq=0, client=-1, removedSeq=None,
+                         removedClient=0, localSeq=0, localRemovedSeq=0, leaf=0, overlap=[], props=[], refType=0,
+                         text="", start=None, items=[it.item(v) for v in items]))
+    tree = sn.emit_v1({"minSeq": 0, "currentSeq": 0}, segs, it, lambda i: f"c{i}")
+    typ = rt.OBJECT_SEQUENCE if kind == "objects" else rt.NUMBER_SEQUENCE
+    attrs = {"mode": "100644", "path": ".attributes", "type": "Blob",
+             "value": {"contents": json.dumps({"type": typ, "snapshotFormatVersion": "0.1"}), "encoding": "utf-8"}}
+    return {"entries": [{"mode": "040000", "path": STR, "type": "Tree", "value": {"entries": [
+        attrs, {"mode": "040000", "path": "content", "type": "Tree", "value": tree}]}}]}
+
+
+def _item(kind: str, unit: int):
+    """the item a generated text unit stands for: a number (SharedNumberSequence) or an object (SharedObjectSequence)"""
+    return unit if kind == "numbers" else {"c": chr(unit), "n": unit % 7}
+
+
+def _as_items(op, kind: str):
+    """a SharedString insert op's text spec as a SharedSequence.insert's {items, props} spec (sharedSequence.ts:116-125)"""
+    if op.get("type") == 3:
+        return dict(op, ops=[_as_items(m, kind) for m in op["ops"]])
+    if op.get("type") != 0:
+        return op
+    seg = op["seg"]
+    text, props = (seg, None) if isinstance(seg, str) else (seg["text"], seg.get("props"))
+    spec = {"items": [_item(kind, ord(ch)) for ch in text]}
+    if props is not None:
+        spec["props"] = props
+    return dict(op, seg=spec)
+
+
 def _envelope(op, rng):
     c = {"address": DS, "contents": {"content": {"address": STR, "contents": op}, "type": "component"}}
     return json.dumps(c) if rng.random() < 0.1 else c
 
 
-def build(seed: int, nops: int = 2000, legacy_attach: bool = False, fixture: str = "headerAndBody"):
-    """(messages, farm batch): one recorded document."""
+def build(seed: int, nops: int = 2000, legacy_attach: bool = False, fixture: str = "headerAndBody",
+          kind: str = "string"):
+    """(messages, farm batch): one recorded document. kind "objects" / "numbers": the channel is a SharedObjectSequence
+    / SharedNumberSequence whose inserts carry the farm's texts as items."""
     farm = gen.generate(gen.config1(nops), ids=list(range(8 * seed, 8 * seed + 8)), threads=8)
     ops, text, props, kv = farm.doc(0)  # the observer: every sequenced message in order
     it = gen.generator_interner()
     rng = np.random.default_rng(seed)
-    snap = _attach_snapshot(fixture)
+    snap = _attach_snapshot(fixture) if kind == "string" else _sequence_snapshot(kind, seed)
     out = []
     if legacy_attach:  # an attach inside an operation's envelopes (clientReplayTool.ts:153-157)
         out.append({"clientId": "c1", "sequenceNumber": 0, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
@@ -62,7 +103,7 @@ def build(seed: int, nops: int = 2000, legacy_attach: bool = False, fixture: str
         if msg["type"] != "op":
             out.append(dict(base, type="noop", contents=None))
             continue
-        env = _envelope(msg["contents"], rng)
+        env = _envelope(msg["contents"] if kind == "string" else _as_items(msg["contents"], kind), rng)
         if legacy_attach:
             env = {"address": "root", "contents": env if isinstance(env, dict) else json.loads(env)}
         r = rng.random()
@@ -88,3 +129,9 @@ def documents():
     """the two recorded documents of the fixture"""
     return [build(0, legacy_attach=False, fixture="headerAndBody")[0],
             build(1, legacy_attach=True, fixture="withMarkers")[0]]
+
+
+def sequence_documents():
+    """two recorded documents of SubSequence channels (refreplaytool_seq.npz): a SharedObjectSequence attached by a
+    container Attach message, a SharedNumberSequence by a legacy attach"""
+    return [build(2, legacy_attach=False, kind="objects")[0], build(3, legacy_attach=True, kind="numbers")[0]]

@@ -141,6 +141,22 @@ def test_client_surface_through_node():
     assert out["refused"]  # a perspective the reference's partial lengths answer differently is refused
 
 
+@pytest.mark.gpu
+def test_subsequence_through_node():
+    """tests/napi_subseq.js: a SharedObjectSequence replica through node -> addon -> GPU (insertItemsLocal, {items}
+    messages, an ack, getItems / getItemCount, getText with and without placeholder, segments either side of MaxRun);
+    the answers are the type-erased reference's for the same steps (tools/make_napi_subseq.mjs)"""
+    native.build_napi()
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "napi_subseq.js")], capture_output=True, text=True,
+                       cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "napi_subseq_expected.json")))
+    assert len(out["answers"]) == len(want)
+    for i, (g, w) in enumerate(zip(out["answers"], want)):
+        assert g == w, (i, g, w)
+
+
 def test_typings_declare_every_export_and_method():
     """fluidframework_amd/js/mergetree_gpu.d.ts declares every name the facade exports and every public method
     of its classes (no TypeScript compiler in this image: a textual check)"""

@@ -115,3 +115,63 @@ def test_replay_tool_cli_on_gpu(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out == {"merge_trees": 1, "messages": 2000, "replicas": 8, "errors": 0}
+
+
+def load_seq():
+    z = np.load(os.path.join(GOLDEN, "refreplaytool_seq.npz"), allow_pickle=False)
+    docs = replaylog.sequence_documents()
+    for k, msgs in enumerate(docs):
+        assert hashlib.sha256(json.dumps(msgs).encode()).hexdigest() == str(z["log_sha256"][k]), "logs changed"
+    return z, docs
+
+
+def _items_fnv(values) -> tuple:
+    j = json.dumps(values, separators=(",", ":")).encode()
+    h = 0xcbf29ce484222325
+    for x in j:
+        h = ((h ^ x) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return len(values), h
+
+
+def test_sequence_trees_parse():
+    """the tool's other mergeTreeTypes: an object sequence (container attach) and a number sequence (legacy attach)"""
+    z, docs = load_seq()
+    types = [rt.OBJECT_SEQUENCE, rt.NUMBER_SEQUENCE]
+    for k, msgs in enumerate(docs):
+        log = rt.parse(msgs)
+        assert list(log.types.values()) == [types[k]] and len(log.messages) == 2000
+        m = z["doc"] == k
+        assert [(p, c) for p, c in zip(z["path"][m], z["client"][m])] == \
+            [(p, c) for c in rt.clients_of(log) for p in log.trees]
+    with pytest.raises(ValueError):  # a sparse matrix's RunSegment / PaddingSegment trees are not modelled
+        rt.merge_trees_of({"id": "x", "type": rt.SPARSE_MATRIX, "snapshot": {"entries": []}})
+
+
+def test_host_core_sequence_replicas_match_reference_tool():
+    """SubSequence replicas rebuilt by the tool's steps: getLength, getText (no TextSegment: empty) and getItems equal
+    the reference tool's for every client, and every replica converges to the observer's items."""
+    z, docs = load_seq()
+    for k, msgs in enumerate(docs):
+        st = rt.streams(rt.parse(msgs))
+        caps = (CAPS["ncap"], CAPS["hcap"], CAPS["acap"], CAPS["mcap"], CAPS["gcap"], CAPS["ccap"])
+        hs = core_host.HostStore(st.batch.ndocs, caps)
+        err = np.asarray([hs.replay(d, *st.batch.doc(d)) for d in range(st.batch.ndocs)])
+        assert (err == 0).all(), err
+        m = z["doc"] == k
+        for i, (tl, n, ni, f) in enumerate(zip(z["text_len"][m], z["length"][m], z["nitems"][m], z["items_fnv"][m])):
+            items = [st.interner.item_obj(u) for u in hs.items(i, 0)]
+            assert (len(hs.text(i)), hs.length_local(i)) == (tl, n) and _items_fnv(items) == (ni, int(f)), (k, i)
+        obs = json.loads(str(z["observer_items"][k]))
+        assert [st.interner.item_obj(u) for u in hs.items(st.batch.ndocs - 1, 0)] == obs
+
+
+@pytest.mark.gpu
+def test_gpu_sequence_replicas_match_reference_tool():
+    z, docs = load_seq()
+    for k, msgs in enumerate(docs):
+        reps = rt.replay(rt.parse(msgs), **CAPS)
+        m = z["doc"] == k
+        assert len(reps) == int(m.sum())
+        for (p, c, t, n, items), tl, ln, ni, f in zip(reps, z["text_len"][m], z["length"][m], z["nitems"][m],
+                                                       z["items_fnv"][m]):
+            assert (len(t), n) == (tl, ln) and _items_fnv(items) == (ni, int(f)), (k, p, c)

@@ -812,6 +812,43 @@ def make_persp(node: str) -> None:
               f"answers", flush=True)
 
 
+def make_replaytool_seq(node: str) -> None:
+    """tests/golden/refreplaytool_seq.npz: the reference tool's replicas (tools/ref_replay_tool.mjs) for recorded
+    documents of a SharedObjectSequence and a SharedNumberSequence (tests/replaylog.py sequence_documents): per replica
+    its getLength, getText (empty: no TextSegment) and its items (SharedSequence.getItems(0) over the reference Client)
+    as the length and FNV-1a-64 of their JSON; the observers' items JSON in full."""
+    import replaylog
+    rows, obs, shas = [], [], []
+    for k, msgs in enumerate(replaylog.sequence_documents()):
+        d = os.path.join(SCRATCH, f"replaytool_seq_{k}")
+        os.makedirs(d, exist_ok=True)
+        blob = json.dumps(msgs)
+        shas.append(hashlib.sha256(blob.encode()).hexdigest())
+        with open(os.path.join(d, "messages.json"), "w") as f:
+            f.write(blob)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "ref_replay_tool.mjs"), ERASED,
+                            os.path.join(d, "messages.json"), os.path.join(d, "out.json")], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference replay tool failed: {r.stderr[-2000:]}")
+        reps = json.load(open(os.path.join(d, "out.json")))["replicas"]
+        for path, client, text, length, items in reps:
+            ij = json.dumps(items, separators=(",", ":"))
+            rows.append([k, path, client, len(text), length, len(items), fnv1a64(ij.encode())])
+            if client == "readonly":
+                obs.append(ij)
+        print(f"replaytool seq doc {k}: {len(reps)} replicas, lengths {sorted(set(x[3] for x in reps))}", flush=True)
+    np.savez_compressed(
+        os.path.join(GOLDEN, "refreplaytool_seq.npz"),
+        doc=np.asarray([x[0] for x in rows], np.int32), path=np.asarray([x[1] for x in rows]),
+        client=np.asarray([x[2] for x in rows]), text_len=np.asarray([x[3] for x in rows], np.int64),
+        length=np.asarray([x[4] for x in rows], np.int64), nitems=np.asarray([x[5] for x in rows], np.int64),
+        items_fnv=np.asarray([x[6] for x in rows], np.uint64), observer_items=np.asarray(obs),
+        log_sha256=np.asarray(shas),
+        source=("packages/dds/merge-tree/src + sequence sharedSequence.ts SubSequence (reference, type-erased by "
+                "tools/ts_erase.py) under node by tools/ref_replay_tool.mjs: clientReplayTool.ts's reconstruction of "
+                "object / number sequence trees over the reference Client"))
+
+
 def make_replaytool(node: str) -> None:
     """tests/golden/refreplaytool.npz: the reference merge-tree client replay tool's per-client replicas
     (clientReplayTool.ts:113-258, restated over the reference Client by tools/ref_replay_tool.mjs) for the
@@ -833,7 +870,7 @@ def make_replaytool(node: str) -> None:
         if r.returncode != 0:
             raise RuntimeError(f"reference replay tool failed: {r.stderr[-2000:]}")
         reps = json.load(open(os.path.join(d, "out.json")))["replicas"]
-        for path, client, text, length in reps:
+        for path, client, text, length in (r[:4] for r in reps):
             rows.append([k, path, client, len(text), fnv1a64(text.encode("utf-16-le")), length])
             if client == "readonly":
                 texts.append(text)
@@ -983,6 +1020,7 @@ def main() -> None:
         return
     if args.replaytool:
         make_replaytool(args.node)
+        make_replaytool_seq(args.node)
         return
     if args.persp:
         make_persp(args.node)

@@ -15,12 +15,18 @@
 //
 // usage: node ref_replay_tool.mjs <erased-dir> <messages.json> <out.json> [--literal]
 //   --literal: run the tool's loop exactly as written instead (line 211's `!==`) and report its outcome
-//   out.json: {"replicas": [[path, client, text, length], ...]} in (client, path) order
+//   out.json: {"replicas": [[path, client, text, length(, items)], ...]} in (client, path) order; items (the
+//   replica's SharedSequence.getItems(0), restated over the reference Client) for SharedObjectSequence /
+//   SharedNumberSequence trees only
 import fs from "fs";
 import path from "path";
 
 const [erased, msgPath, outPath] = process.argv.slice(2);
 const SHARED_STRING = "https://graph.microsoft.com/types/mergeTree";
+const SPARSE_MATRIX = "https://graph.microsoft.com/types/mergeTree/sparse-matrix";
+const OBJECT_SEQUENCE = "https://graph.microsoft.com/types/mergeTree/object-sequence";
+const NUMBER_SEQUENCE = "https://graph.microsoft.com/types/mergeTree/number-sequence";
+let SubSequence; // the sequence package's segment (type-erased beside merge-tree), bound in main()
 const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
 
 const storageOf = (tree) => {
@@ -58,17 +64,39 @@ function ddsTrees(attach) { // getDssTreesFromAttach (322-356)
     }
     return out;
 }
-function processAttach(attach, attachTrees) { // processAttachMessage (264-320), SharedString only
+// processAttachMessage (264-320): the tool's mergeTreeTypes in its order, each tree with its factory's segmentFromSpec
+// (SharedStringFactory: TextSegment / Marker; the object and number sequences: SubSequence.fromJSONObject). The sparse
+// matrix's RunSegment / PaddingSegment are not restated here: a log holding one is refused.
+function processAttach(attach, attachTrees) {
     const trees = ddsTrees(attach);
-    for (const t of trees.get(SHARED_STRING) || []) {
-        const entries = [...t.value.entries];
-        let content;
-        while (entries.length > 0) {
-            content = entries.shift();
-            if (content.path === "content") break;
+    if (trees.has(SPARSE_MATRIX)) throw new Error("sparse matrix trees are not restated");
+    for (const type of [SHARED_STRING, OBJECT_SEQUENCE, NUMBER_SEQUENCE]) {
+        for (const t of trees.get(type) || []) {
+            const entries = [...t.value.entries];
+            let content;
+            while (entries.length > 0) {
+                content = entries.shift();
+                if (content.path === "content") break;
+            }
+            attachTrees.set(t.fullPath, { tree: content.value, seq: type !== SHARED_STRING });
         }
-        attachTrees.set(t.fullPath, content.value);
     }
+}
+// SharedSequence.getItems (sequence sharedSequence.ts:150-183) over the reference Client (walkSegments + getPosition)
+function getItems(client, start, end) {
+    const out = [];
+    let firstSegment;
+    if (end !== undefined && end <= start) return out;
+    client.walkSegments((segment) => {
+        if (SubSequence.is(segment)) {
+            if (firstSegment === undefined) firstSegment = segment;
+            out.push(...segment.items);
+        }
+        return true;
+    }, start, end);
+    if (firstSegment !== undefined) out.splice(0, start - client.getPosition(firstSegment));
+    if (end !== undefined) out.splice(end - start);
+    return out;
 }
 
 const literal = process.argv.includes("--literal");
@@ -76,15 +104,15 @@ const literal = process.argv.includes("--literal");
 // pushed to the pending queue, applied as this client's local transaction, and pushed again; the client's own
 // ops are skipped. The first exception ends the tool (it rethrows); otherwise its final asserts compare every
 // replica's length and text with the readonly replica's. Returns what happened.
-async function literalRun(MT, clients, attachTrees, mtMessages, specToSegment) {
+async function literalRun(MT, clients, attachTrees, mtMessages, specOf) {
     const { Client, createGroupOp, MergeTreeDeltaType } = MT;
     clients = new Map(clients);
     clients.set("readonly", new Map());
     for (const clientId of clients.keys()) {
         const client = clients.get(clientId);
         for (const id of attachTrees.keys()) {
-            const c = new Client(specToSegment, logger);
-            const { catchupOpsP } = await c.load(runtimeOf(clientId), storageOf(attachTrees.get(id)));
+            const c = new Client(specOf(id), logger);
+            const { catchupOpsP } = await c.load(runtimeOf(clientId), storageOf(attachTrees.get(id).tree));
             await catchupOpsP;
             client.set(id, c);
         }
@@ -128,7 +156,10 @@ async function literalRun(MT, clients, attachTrees, mtMessages, specToSegment) {
 async function main() {
     const MT = await import(path.join(erased, "index.mjs"));
     const { Client, TextSegment, Marker, createGroupOp, MergeTreeDeltaType } = MT;
-    const specToSegment = (spec) => TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec);
+    ({ SubSequence } = await import(path.join(erased, "subSequence.mjs")));
+    const stringSpec = (spec) => TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec);
+    const seqSpec = (spec) => SubSequence.fromJSONObject(spec);
+    const specOf = (id) => (attachTrees.get(id).seq ? seqSpec : stringSpec);
     const messages = JSON.parse(fs.readFileSync(msgPath));
     const attachTrees = new Map();
     const mtMessages = [];
@@ -180,7 +211,7 @@ async function main() {
     }
     const out = [];
     if (literal && attachTrees.size > 0) { // the loop as written (190-256), to record what it does
-        fs.writeFileSync(outPath, JSON.stringify({ literal: await literalRun(MT, clients, attachTrees, mtMessages, specToSegment) }));
+        fs.writeFileSync(outPath, JSON.stringify({ literal: await literalRun(MT, clients, attachTrees, mtMessages, specOf) }));
         console.log(JSON.stringify({ literal: true, messages: mtMessages.length }));
         return;
     }
@@ -189,8 +220,8 @@ async function main() {
         for (const clientId of clients.keys()) {
             const client = clients.get(clientId);
             for (const id of attachTrees.keys()) {
-                const c = new Client(specToSegment, logger);
-                const { catchupOpsP } = await c.load(runtimeOf(clientId), storageOf(attachTrees.get(id)));
+                const c = new Client(specOf(id), logger);
+                const { catchupOpsP } = await c.load(runtimeOf(clientId), storageOf(attachTrees.get(id).tree));
                 await catchupOpsP;
                 client.set(id, c);
             }
@@ -206,8 +237,12 @@ async function main() {
                 pending.push(message);
             }
             for (const m of pending) client.get(m.fullPath).applyMsg(m);
-            for (const [id, c] of client) out.push([id, clientId, new MT.MergeTreeTextHelper(c.mergeTree).getText(
-                c.getCurrentSeq(), c.getClientId()), c.getLength()]);
+            for (const [id, c] of client) {
+                const row = [id, clientId, new MT.MergeTreeTextHelper(c.mergeTree).getText(c.getCurrentSeq(), c.getClientId()),
+                    c.getLength()];
+                if (attachTrees.get(id).seq) row.push(getItems(c, 0));
+                out.push(row);
+            }
         }
     }
     fs.writeFileSync(outPath, JSON.stringify({ replicas: out }));
