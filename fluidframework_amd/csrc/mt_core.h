@@ -5972,7 +5972,7 @@ struct Replica {
      * out (cap), the count returned. */
     MT_HD int64_t get_items(int32_t start, int32_t end, uint16_t* out, int64_t cap) {
         const bool noEnd = end == TEXT_RANGE_DEFAULT;
-        if (!noEnd && end <= start) return 0;
+        if ((!noEnd && end <= start) || !run_doc()) return 0; /* TextSegments are no SubSequence: none pushed */
         const int32_t refSeq = h.currentSeq, client = h.localShort;
         const int32_t e = noEnd ? INT32_MAX : end;
         const uint16_t* base = arena_base(zh->arenaSide);

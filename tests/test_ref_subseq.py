@@ -112,6 +112,14 @@ def test_host_core_text_and_items(name):
         assert len(items) == n and items == want
 
 
+def test_items_of_a_text_document_are_none():
+    """SharedSequence.getItems pushes only SubSequence segments: a TextSegment document has no items"""
+    z, w, b = regenerate("c2_observer")
+    text_b = gen.generate(w, ids=z["doc_ids"][:1], threads=1)
+    _, herr, st = core_host.replay_batch(text_b)
+    assert (herr == 0).all() and st.length_local(0) > 0 and st.items(0, 0) == []
+
+
 def _fnv(bs: bytes) -> int:
     h = 0xcbf29ce484222325
     for x in bs:
