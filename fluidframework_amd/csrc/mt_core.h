@@ -57,6 +57,11 @@ enum : int32_t {
     OVB = 64,          /* overflow blocks per document (8 overlap entries each) */
 };
 enum : uint8_t { LOCAL_CLIENT = 0xFF }; /* short id of LocalClientId (-1) */
+/* A short id is a byte of the leaf lines: slots 0..252 name clients (s2l: their long ids), RETIRED_CLIENT marks a
+ * row whose client's slot was recycled (its long id then lives in the document's retired-client table, by row id),
+ * 0xFE is a client the replica has not seen. See Replica::reclaim_shorts. */
+enum : uint8_t { RETIRED_CLIENT = 0xFD, MAX_SLOTS = 0xFD };
+enum : uint16_t { FREE_SLOT = 0xFFFF }; /* s2l of a recycled slot (no long id takes 0xFFFF: NonCollabClient) */
 
 /* error codes (mt_engine.h MT_E_*) */
 enum : int32_t {
@@ -380,7 +385,11 @@ struct Doc {
     Caps caps;
     static constexpr int64_t OFF_COLD = align256c((int64_t)sizeof(HT));
     static constexpr int64_t OFF_FRID = align256c(OFF_COLD + (int64_t)sizeof(typename HT::Cold) * HT::S);
-    static constexpr int64_t OFF_ARENA = align256c(OFF_FRID + (int64_t)sizeof(typename HT::IX) * HT::S);
+    /* retired clients by row id: {client long id, removedClient long id} of a row whose short-id byte is
+     * RETIRED_CLIENT (written by reclaim_shorts, copied by splits, read by the dump and the segment queries) */
+    static constexpr int64_t OFF_RCL = align256c(OFF_FRID + (int64_t)sizeof(typename HT::IX) * HT::S);
+    static constexpr bool HAS_RCL = HT::N > 640; /* the profiles that recycle short ids (Replica::RECLAIM) */
+    static constexpr int64_t OFF_ARENA = align256c(OFF_RCL + (HAS_RCL ? 4 * (int64_t)HT::S : 0));
     MT_HD static int64_t off_mgid(const Caps& c) { return OFF_ARENA + align256c(4 * (int64_t)c.acap); }
     MT_HD static int64_t off_mrid(const Caps& c) { return off_mgid(c) + align256c(4 * (int64_t)c.mcap); }
     MT_HD static int64_t off_gq(const Caps& c) { return off_mrid(c) + align256c(4 * (int64_t)c.mcap); }
@@ -433,6 +442,7 @@ struct Doc {
 #endif
     MT_HD typename HT::IX* frid() const { return (typename HT::IX*)(b + OFF_FRID); } /* free row-id stack */
     MT_HD uint16_t* arena() const { return (uint16_t*)(b + OFF_ARENA); } /* 2 * acap */
+    MT_HD uint32_t& RCL(int32_t r) const { return ((uint32_t*)(b + OFF_RCL))[r]; } /* lo: client, hi: removedClient */
     MT_HD int32_t* mgid() const { return (int32_t*)(b + off_mgid(caps)); }
     MT_HD int32_t* mrid() const { return (int32_t*)(b + off_mrid(caps)); } /* row id of each membership entry */
     MT_HD int32_t* gq() const { return (int32_t*)(b + off_gq(caps)); }
@@ -505,6 +515,10 @@ struct Replica {
     static constexpr bool TILED = HT::TILED;
     static constexpr int WCAPR = NARROW ? MT_NARROW_W : HT::TL::WCAP; /* window-set entries */
     static constexpr int HCAPR = NARROW ? MT_NARROW_H : HT::H;        /* zamboni heap entries */
+    /* short-id recycling (reclaim_shorts) is built into the larger profiles only: a config-2/3/5 document that meets
+     * its 254th client latches E_CAPACITY and replays again in HotMid (capacity promotion, mt_replay.hip), so the
+     * small kernels carry none of it */
+    static constexpr bool RECLAIM = Doc<HT>::HAS_RCL;
     Doc<HT> d;
     HT& z; /* the hot image */
     W w;
@@ -1233,22 +1247,145 @@ struct Replica {
             int32_t s = l2s[longId];
             return s == 0xFF ? -1 : s;
         }
-        for (int32_t i = 0; i < zh->nclients; i++)
-            if (s2l[i] == longId) return i;
+        const int32_t n = zh->nclients;
+        if constexpr (!RECLAIM) {
+            for (int32_t i = 0; i < n; i++)
+                if (s2l[i] == longId) return i;
+            return -1;
+        }
+        for (int32_t b = 0; b < n; b += W::N) { /* a wave pass per 64 slots (long ids past the l2s table) */
+            int32_t i = b + w.lane();
+            uint64_t m = w.ballot(i < n && (int32_t)s2l[i] == longId);
+            if (m) return b + W::ffs(m);
+        }
         return -1;
     }
+    /* client.ts:637-661 getOrAddShortClientId. The reference numbers clients without bound; here a client takes a
+     * slot (0..252), and when every slot is taken the slots no row of the collaboration window needs are recycled
+     * (reclaim_shorts) — so a document may see any number of clients, at most 253 of them with rows in the window
+     * at once (E_CAPACITY past that). */
     MT_HD int32_t get_or_add_short(int32_t longId) {
         int32_t s = short_of(longId);
         if (s >= 0) return s;
         int32_t n = zh->nclients;
-        if (n >= HT::C || n >= 0xFE) {
-            fail(E_CAPACITY);
-            return 0;
+        int32_t slot = -1;
+        if (n < MAX_SLOTS && n < HT::C) {
+            slot = n;
+            zh->nclients = n + 1;
+        } else {
+            if constexpr (RECLAIM) {
+                slot = free_slot();
+                if (slot < 0 && reclaim_shorts()) slot = free_slot();
+            }
+            if (slot < 0) {
+                fail(E_CAPACITY);
+                return 0;
+            }
         }
-        s2l[n] = (uint16_t)longId;
-        if ((uint32_t)longId < (uint32_t)HT::C) l2s[longId] = (uint8_t)n;
-        zh->nclients = n + 1;
-        return n;
+        s2l[slot] = (uint16_t)longId;
+        if ((uint32_t)longId < (uint32_t)HT::C) l2s[longId] = (uint8_t)slot;
+        return slot;
+    }
+    MT_HD int32_t free_slot() {
+        const int32_t n = zh->nclients;
+        for (int32_t b = 0; b < n; b += W::N) {
+            int32_t i = b + w.lane();
+            uint64_t m = w.ballot(i < n && s2l[i] == FREE_SLOT);
+            if (m) return b + W::ffs(m);
+        }
+        return -1;
+    }
+    /* Recycle the short ids no row of the collaboration window needs. A short id is only ever compared for
+     * equality, and only where a row's seq or removedSeq lies in the window (above minSeq, or local-pending): a
+     * settled row is visible, or removed, under every perspective the protocol admits (refSeq >= minSeq), whatever
+     * its client (the visibility predicate, mergeTree.ts:1692-1732; breakTie compares seqs). So the slots of clients
+     * with no window row, no removedClientOverlap entry and not the local client are freed; a settled row holding
+     * one keeps its long ids in the retired-client table (Doc::RCL, by row id) and the byte RETIRED_CLIENT, which
+     * no client's byte equals. Returns whether a slot was freed. Rare (a document's 254th client), rolled. */
+    MT_HD bool reclaim_shorts() {
+        uint64_t act[4] = {0, 0, 0, 0};
+        auto mark = [&](uint32_t b) {
+            if (b < MAX_SLOTS) act[b >> 6] |= 1ull << (b & 63);
+        };
+        if (h.localShort >= 0) mark((uint32_t)h.localShort);
+        const int32_t minSeq = h.minSeq;
+        /* the values lanes hold, each distinct one marked once (a ballot loop, no atomics) */
+        auto mark_lanes = [&](bool has, uint32_t v) {
+            uint64_t m = w.ballot(has);
+            while (m) {
+                uint32_t x = (uint32_t)w.bcast((int32_t)v, W::ffs(m));
+                mark(x);
+                has = has && v != x;
+                m = w.ballot(has);
+            }
+        };
+#pragma clang loop unroll(disable)
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+            const int32_t n = leaf_at(k), c = nch[n];
+            for (int32_t j0 = 0; j0 < c; j0 += W::N) { /* a lane per row of the leaf */
+                const int32_t j = j0 + w.lane();
+                const bool row = j < c;
+                const int32_t s = n * MAXN + (row ? j : 0);
+                int32_t sq = 0, rs = NOREM;
+                uint32_t b4 = 0;
+                if (row) {
+                    sq = z.seq(s);
+                    rs = z.rseq(s);
+                    b4 = ld_bytes4(s);
+                }
+                const bool rem = rs != NOREM;
+                const bool win = row && (sq == UNASSIGNED_SEQ || sq > minSeq ||
+                                         (rem && (rs == UNASSIGNED_SEQ || rs > minSeq)) || (((b4 >> 16) & 0xFF) & RF_OVL));
+                mark_lanes(win, b4 & 0xFF);
+                mark_lanes(win && rem, (b4 >> 8) & 0xFF);
+                uint64_t ov = w.ballot(win && (((b4 >> 16) & 0xFF) & RF_OVL));
+                while (ov) { /* removedClientOverlap lists: every entry stays */
+                    int32_t l = W::ffs(ov);
+                    ov &= ov - 1;
+                    int32_t so = n * MAXN + j0 + l;
+#pragma clang loop unroll(disable)
+                    for (int32_t q = 0, e; (e = ovl_at(so, q)) >= 0; q++) mark((uint32_t)e);
+                }
+            }
+        }
+        bool freed = false;
+        for (int32_t sl = 0; sl < zh->nclients; sl++)
+            if (!((act[sl >> 6] >> (sl & 63)) & 1) && s2l[sl] != FREE_SLOT) freed = true;
+        if (!freed) return false;
+        /* retire the settled rows' bytes of the slots about to be freed */
+#pragma clang loop unroll(disable)
+        for (int32_t k = 0; kvalid(k); k = knext(k)) {
+            const int32_t n = leaf_at(k), c = nch[n];
+            for (int32_t j0 = 0; j0 < c; j0 += W::N) {
+                const int32_t j = j0 + w.lane();
+                const bool row = j < c;
+                const int32_t s = n * MAXN + (row ? j : 0);
+                const uint32_t b4 = row ? ld_bytes4(s) : 0;
+                const uint32_t cb = b4 & 0xFF, rb = (b4 >> 8) & 0xFF;
+                const bool rem = row && z.rseq(s) != NOREM;
+                const bool rc = row && cb < MAX_SLOTS && !((act[cb >> 6] >> (cb & 63)) & 1);
+                const bool rr = rem && rb < MAX_SLOTS && !((act[rb >> 6] >> (rb & 63)) & 1);
+                w.sync();
+                if (rc || rr) {
+                    int32_t r = (int32_t)z.RID(s);
+                    uint32_t e = d.RCL(r);
+                    if (rc) e = (e & 0xFFFF0000u) | (uint32_t)s2l[cb];
+                    if (rr) e = (e & 0xFFFFu) | ((uint32_t)s2l[rb] << 16);
+                    d.RCL(r) = e;
+                    st_bytes4(s, (b4 & 0xFFFF0000u) | (rc ? (uint32_t)RETIRED_CLIENT : cb) |
+                                     ((rr ? (uint32_t)RETIRED_CLIENT : rb) << 8));
+                }
+                w.sync();
+            }
+        }
+        for (int32_t sl = 0; sl < zh->nclients; sl++) {
+            if (((act[sl >> 6] >> (sl & 63)) & 1) || s2l[sl] == FREE_SLOT) continue;
+            int32_t lo = s2l[sl];
+            if ((uint32_t)lo < (uint32_t)HT::C) l2s[lo] = 0xFF;
+            s2l[sl] = FREE_SLOT;
+        }
+        w.sync();
+        return true;
     }
     /* startOrUpdateCollaboration (client.ts:1053-1073) + startCollaboration (mergeTree.ts:1287) */
     MT_HD void start_collab(int32_t longId, int32_t minSeq, int32_t curSeq) {
@@ -1282,7 +1419,7 @@ struct Replica {
      * LocalClientId (-1) as LOCAL_CLIENT, and anything else (0x7fff: a client the replica has never seen) as 0xFE,
      * which no short id takes (get_or_add_short hands out at most 254), so such a client owns no row */
     MT_HD static uint32_t client_byte(int32_t client) {
-        return (uint32_t)client < 0xFEu ? (uint32_t)client : (client == -1 ? (uint32_t)LOCAL_CLIENT : 0xFEu);
+        return (uint32_t)client < (uint32_t)MAX_SLOTS ? (uint32_t)client : (client == -1 ? (uint32_t)LOCAL_CLIENT : 0xFEu);
     }
     MT_HD int32_t vis_of(int32_t s, const RowView& r, int32_t refSeq, int32_t client) const {
         return vis_of_l(s, r, refSeq, client, is_local(client));
@@ -2982,6 +3119,11 @@ struct Replica {
         }
         int32_t* cdst = (int32_t*)&cd[rrid];
         if (l < CW) cdst[l] = l == 2 ? (int32_t)rtoff : cv;
+        /* a retired client byte: the right part's long ids (the retired-client table is by row id) */
+        if constexpr (RECLAIM) {
+            const uint32_t cb0 = (uint32_t)w.bcast((int32_t)rr.cli | ((int32_t)rr.rcli << 8), j);
+            if ((cb0 & 0xFF) == RETIRED_CLIENT || (cb0 >> 8) == RETIRED_CLIENT) d.RCL(rrid) = d.RCL(rid0);
+        }
         w.sync();
         if (ovx0) ovl_clone(rs, ls);
         z.len(rs) = lenR;
@@ -3029,6 +3171,7 @@ struct Replica {
         typename HT::Cold& cl = cold(ls);
         typename HT::Cold& cr = d.COLD(rrid);
         copy_cold(rs, ls); /* splitAt copies every field (mergeTree.ts:523-567) */
+        if (RECLAIM && (z.cli(ls) == RETIRED_CLIENT || z.rcli(ls) == RETIRED_CLIENT)) d.RCL(rrid) = d.RCL(z.RID(ls));
         if (cl.ovx) ovl_clone(rs, ls);
         if (refs_on()) refs_split(z.RID(ls), rrid, off);
         int32_t lenL = z.len(ls);
@@ -5599,6 +5742,13 @@ struct Replica {
             h.opsDone++;
             return;
         }
+        /* the sender's short id of a sequenced or MergeTree-level record: in the recycling profiles registered at
+         * one call site (its slot allocation and recycling, get_or_add_short, is inlined once); the small profiles
+         * keep the call at each use, which their register allocation prefers (A/B) */
+        const bool tree = (op.kind & MT_OPF_TREE) != 0;
+        const bool seqd = !(op.kind & MT_OPF_LOCAL) && (tree || kind < MT_OP_RELOAD);
+        const int32_t sc =
+            RECLAIM && seqd && !(tree && op.client == MT_CLIENT_LOCAL) ? get_or_add_short(op.client) : -1;
         /* the edit the record makes, if any */
         mt_op_rec o = op;
         bool edit = false, remote = false, grouped = false;
@@ -5612,7 +5762,7 @@ struct Replica {
             eref = UNIVERSAL_SEQ;
             eseq = op.seq;
         } else if (op.kind & MT_OPF_TREE) { /* MergeTree-level call with explicit (refSeq, clientId, seq) */
-            ecli = op.client == MT_CLIENT_LOCAL ? -1 : get_or_add_short(op.client);
+            ecli = RECLAIM ? sc : op.client == MT_CLIENT_LOCAL ? -1 : get_or_add_short(op.client);
             if (op.client == MT_CLIENT_NONCOLLAB || (op.kind & MT_OPF_LOCAL) || kind > MT_OP_ANNOTATE ||
                 (kind == MT_OP_INSERT && op.seg_kind != MT_SEG_MARKER && op.text_len == 0)) {
                 fail(E_UNSUPPORTED);
@@ -5666,7 +5816,7 @@ struct Replica {
             }
         } else {
             remote = true;
-            get_or_add_short(op.client);
+            if constexpr (!RECLAIM) get_or_add_short(op.client);
             grouped = (op.kind & MT_OPF_GROUPED) != 0; /* a group member before the last (mt_oplog.h) */
             if (!grouped) zh->seqOps++; /* one sequenced message per group */
             if (grouped) {
@@ -5680,7 +5830,7 @@ struct Replica {
                 if ((int32_t)op.client == h.localLong) {
                     ack(kind, kv, nkv, rw, op.seq);
                 } else {
-                    ecli = get_or_add_short(op.client);
+                    ecli = RECLAIM ? sc : get_or_add_short(op.client);
                     eref = op.ref_seq;
                     eseq = op.seq;
                     edit = true;
@@ -6091,6 +6241,15 @@ struct Replica {
         k->n += len;
     }
     MT_HD int32_t long_of(uint8_t sh) const { return sh == LOCAL_CLIENT ? -1 : (int32_t)s2l[sh]; }
+    /* the long ids of the client / removedClient of the row in slot s (a retired byte: the retired-client table) */
+    MT_HD int32_t long_of_cli(int32_t s) const {
+        uint8_t b = z.cli(s);
+        return b == RETIRED_CLIENT ? (int32_t)(d.RCL(z.RID(s)) & 0xFFFF) : long_of(b);
+    }
+    MT_HD int32_t long_of_rcli(int32_t s) const {
+        uint8_t b = z.rcli(s);
+        return b == RETIRED_CLIENT ? (int32_t)(d.RCL(z.RID(s)) >> 16) : long_of(b);
+    }
     /* Serial dump (only lane 0 writes the buffer); returns the byte count. */
     MT_HD int64_t dump(uint8_t* out, int64_t cap) {
         Sink k = {w.lane() == 0 ? out : 0, cap, 0, MT_FNV_OFFSET, false};
@@ -6131,9 +6290,9 @@ struct Replica {
             put_bytes(o, b4, 4);
             int32_t f[8] = {z.len(s),
                             z.seq(s),
-                            long_of(z.cli(s)),
+                            long_of_cli(s),
                             rem ? z.rseq(s) : 0,
-                            rem ? long_of(z.rcli(s)) : 0,
+                            rem ? long_of_rcli(s) : 0,
                             (fl & RF_LSEQ) ? cold(s).lseq : 0,
                             (fl & RF_LRSEQ) ? cold(s).lrseq : 0,
                             ordinal};

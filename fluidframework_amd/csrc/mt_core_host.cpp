@@ -195,7 +195,7 @@ int32_t mth_containing(mth_store* s, int64_t doc, int32_t pos, int32_t ref_seq, 
         out6[1] = off;
         out6[2] = r.z.len(slot);
         out6[3] = r.z.seq(slot);
-        out6[4] = r.long_of(r.z.cli(slot));
+        out6[4] = r.long_of_cli(slot);
         out6[5] = r.position_of(slot, rs, sh);
         return 1;
     });

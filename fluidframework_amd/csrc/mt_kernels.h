@@ -630,9 +630,9 @@ __device__ inline void seg_fields(R& r, int32_t s, int32_t off, int32_t* res) {
     res[3] = off;
     res[4] = r.z.len(s);
     res[5] = r.z.seq(s);
-    res[6] = r.long_of(r.z.cli(s));
+    res[6] = r.long_of_cli(s);
     res[7] = rs;
-    res[8] = rs == NOREM ? 0 : r.long_of(r.z.rcli(s));
+    res[8] = rs == NOREM ? 0 : r.long_of_rcli(s);
     res[9] = r.ordinal_of(s);
 }
 #define MT_SEGQ_N 10

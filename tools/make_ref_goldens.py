@@ -993,6 +993,40 @@ def make_items(node: str) -> None:
           f"on {int((odig == digests).sum())}/{b.ndocs} digests", flush=True)
 
 
+SESSION_SETS = {  # name -> (workload, document ids): remote clients renamed per message (tests/session_logs.py, p = 1)
+    "c3_sessions": (gen.config3(4096), list(range(16))),
+    "c2_sessions": (gen.config2(2000), list(range(16))),
+    "c4_sessions": (gen.config4(20000), list(range(2))),
+    "c5_sessions": (gen.config5(1500), list(range(16))),
+}
+
+
+def make_sessions(node: str) -> None:
+    """tests/golden/refsess_<set>.npz: documents whose remote clients reconnect under new long ids at every message
+    that covers their previous one (hundreds to thousands of distinct clients per document: more than the engine's
+    253 short-id slots), replayed by the reference: per-document digests (the dump's client fields are long ids, so
+    every retired row's client must come back exactly), the distinct client counts, and the first documents' dumps."""
+    import oracle_client as oc
+    import session_logs
+    for name, (w, ids) in SESSION_SETS.items():
+        b = session_logs.with_sessions(gen.generate(w, ids=ids, threads=8), p=1.0)
+        dumps, info, secs, _ = run_reference(b, os.path.join(SCRATCH, name), node)
+        digests = np.asarray([fnv1a64(x) for x in dumps], np.uint64)
+        _, odig, oerr = oc.replay_batch(b, threads=8)
+        print(f"refsess_{name}: {b.ndocs} docs, {b.nops} events, clients per doc {min(b.nclients)}-{max(b.nclients)}; "
+              f"reference {info['seconds']:.2f}s; oracle agrees on {int((odig == digests).sum())}/{b.ndocs}", flush=True)
+        keep = min(2, b.ndocs)
+        np.savez_compressed(
+            os.path.join(GOLDEN, f"refsess_{name}.npz"),
+            workload=json.dumps(dataclasses.asdict(w)), doc_ids=np.asarray(ids, np.int64), log_sha256=log_sha(b),
+            digests=digests, nclients=np.asarray(b.nclients, np.int64), session_p=1.0,
+            keep_dumps=np.frombuffer(b"".join(dumps[:keep]), np.uint8),
+            keep_dump_off=np.concatenate([[0], np.cumsum([len(x) for x in dumps[:keep]])]).astype(np.int64),
+            source=("packages/dds/merge-tree/src (reference, type-erased by tools/ts_erase.py) under node by "
+                    "tools/ref_replay.mjs; logs: tests/session_logs.py over the in-repo generator"),
+        )
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default=",".join(SETS))
@@ -1012,8 +1046,12 @@ def main() -> None:
     ap.add_argument("--persp", action="store_true", help="write the past-perspective read fixtures (refpersp_*.npz) only")
     ap.add_argument("--replaytool", action="store_true", help="write the client replay tool fixture only")
     ap.add_argument("--subseq", action="store_true", help="write the SubSequence fixtures (refsubseq_*.npz) only")
+    ap.add_argument("--sessions", action="store_true", help="write the many-client fixtures (refsess_*.npz) only")
     args = ap.parse_args()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ts_erase.py"), "--out", ERASED], check=True)
+    if args.sessions:
+        make_sessions(args.node)
+        return
     if args.subseq:
         make_subseq(args.node)
         make_items(args.node)
