@@ -256,12 +256,14 @@ int32_t mt_engine_create(int32_t device, int64_t ndocs, const mt_caps* caps, mt_
         delete e;
         return MT_E_HIP;
     }
-    /* occupancy of the HBM-resident small-profile kernel (mt_prof_small.hip): 8 waves per SIMD, or 4 (no VGPR
-     * spills) when the batch's documents, one wave each, fit 4 per SIMD (4 SIMDs per CU); MT_SMALL_WAVES overrides */
+    /* the small-profile kernel build (mt_prof_small.hip): the hot image in LDS when the batch's documents fit three
+     * per CU (1: config 1 0.667 -> 0.691M ops/s, config 3 at 256 / 768 documents +3.0 / +1.5 %, profiles/r06l_ab/);
+     * else HBM-resident, 4 waves per SIMD (no VGPR spills) when the documents, one wave each, fit 4 per SIMD (4 SIMDs
+     * per CU), 8 otherwise; MT_SMALL_WAVES overrides */
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
-    e->waves = ndocs <= (int64_t)ncu * 4 * 4 ? 4 : 8;
-    if (const char* sw = getenv("MT_SMALL_WAVES")) e->waves = atoi(sw) == 4 ? 4 : 8;
+    e->waves = ndocs <= (int64_t)ncu * 3 ? 1 : ndocs <= (int64_t)ncu * 4 * 4 ? 4 : 8;
+    if (const char* sw = getenv("MT_SMALL_WAVES")) e->waves = atoi(sw) == 1 ? 1 : atoi(sw) == 4 ? 4 : 8;
     int64_t bytes = prof == 0 ? store_layout(e->s0, k, ndocs)
                   : prof == 1 ? store_layout(e->s1, k, ndocs)
                   : prof == 3 ? store_layout(e->s3, k, ndocs)
@@ -464,7 +466,9 @@ static int64_t chunk_docs(const mt_engine* e) {
     if (e->chunk > 0) return e->chunk;
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || ncu < 1) ncu = 256;
-    int64_t resident = e->profile == 4 ? ncu : (int64_t)ncu * 4 * (e->profile == 0 ? e->waves : 7);
+    int64_t resident = e->profile == 4                      ? ncu
+                       : e->profile == 0 && e->waves == 1 ? (int64_t)ncu * 3 /* the LDS-image build */
+                                                          : (int64_t)ncu * 4 * (e->profile == 0 ? e->waves : 7);
     return std::max<int64_t>(resident, (e->ndocs + 7) / 8);
 }
 
@@ -825,7 +829,7 @@ int32_t mt_engine_set_variant(mt_engine* e, int32_t key, int32_t value) {
     if (!e) return MT_E_ARG;
     switch (key) {
     case MT_VAR_SMALL_WAVES:
-        if (value != 4 && value != 8) return MT_E_ARG;
+        if (value != 1 && value != 4 && value != 8) return MT_E_ARG;
         e->waves = value;
         return MT_OK;
     case MT_VAR_TILED_WIDE:

@@ -142,7 +142,7 @@ class Engine:
 
     def __init__(self, ndocs: int, device: int = 0, waves: Optional[int] = None, wide: Optional[bool] = None,
                  **caps):
-        """`waves` (4 | 8) and `wide` pick a kernel build (mt_engine_set_variant); None keeps the engine's choice."""
+        """`waves` (1 = the LDS-image build | 4 | 8) and `wide` pick a kernel build (mt_engine_set_variant); None keeps the engine's choice."""
         c = default_caps(0)
         c.update(caps)
         self.L = lib()

@@ -128,8 +128,9 @@ int32_t mt_engine_doc_times(mt_engine* e, int64_t* out2);
  * decreasing order of expected cost make a longest-first list schedule. No effect on results. */
 int32_t mt_engine_set_order(mt_engine* e, const int32_t* order);
 /* Kernel build selection (no effect on results; no reference counterpart — the reference has one code path):
- *   MT_VAR_SMALL_WAVES (4 | 8): occupancy build of the config-2/3 replay kernel (default: 4 when the batch's
- *     documents fit 4 per SIMD, else 8; the MT_SMALL_WAVES environment variable sets it at create);
+ *   MT_VAR_SMALL_WAVES (1 | 4 | 8): build of the config-2/3 replay kernel: 1 = the hot image in LDS (three documents
+ *     per CU), 4 or 8 = HBM-resident at 4 or 8 waves per SIMD (default: 1 when the batch's documents fit three per
+ *     CU, 4 when they fit 4 per SIMD, else 8; the MT_SMALL_WAVES environment variable sets it at create);
  *   MT_VAR_TILED_WIDE (0 | 1): the config-4 (tiled) kernel with the zamboni heap in HBM and the full window set
  *     (default 0: the narrow LDS-heap build, which promotes documents it cannot hold to the wide one).
  *   MT_VAR_CHUNK_DOCS (>= 0): documents per chunk of mt_engine_submit_run (0: automatic).

@@ -1,7 +1,7 @@
-"""The config-2/3 profile's two k_replay builds (mt_prof_small.hip): 8 waves per SIMD (mt_small_w8.hip) and 4 waves
-per SIMD without VGPR spills (mt_small_w4.hip), which mt_engine_create picks when the batch's documents fit 4 per SIMD.
-Both replay the same batches to the host core's digests (MT_SMALL_WAVES forces one build; the engine reads it at
-creation)."""
+"""The config-2/3 profile's three k_replay builds (mt_prof_small.hip): 8 waves per SIMD (mt_small_w8.hip), 4 waves
+per SIMD without VGPR spills (mt_small_w4.hip), which mt_engine_create picks when the batch's documents fit 4 per SIMD,
+and the LDS-image build (mt_small_lds.hip, MT_SMALL_WAVES=1: three documents per CU). All replay the same batches to
+the host core's digests (MT_SMALL_WAVES forces one build; the engine reads it at creation)."""
 import numpy as np
 import pytest
 
@@ -12,7 +12,7 @@ from test_ref_goldens import caps_for
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("config,ops", [(2, 3000), (3, 2048)])
-@pytest.mark.parametrize("waves", ["4", "8"])
+@pytest.mark.parametrize("waves", ["1", "4", "8"])
 def test_gpu_small_profile_builds_match_host_core(monkeypatch, config, ops, waves):
     from fluidframework_amd.engine import Engine
     w = {2: gen.config2, 3: gen.config3}[config](ops)

@@ -114,7 +114,7 @@ def test_gpu_combining_ops_match_reference(name):
     err, _ = eng.errors()
     assert (err == 0).all()
     assert np.array_equal(eng.digests(), z[f"{name}_prefix_digests"])
-    for waves in ((4, 8) if c["ncap"] <= 192 else (None,)):
+    for waves in ((1, 4, 8) if c["ncap"] <= 192 else (None,)):
         eng2 = Engine(b.ndocs, waves=waves, **c)
         eng2.set_value_kinds(KINDS)
         eng2.start_collab(b.local_long_id)

@@ -108,7 +108,7 @@ def test_gpu_delta_stream_matches_reference(name):
         got = eng.deltas(d)
         assert np.array_equal(got, want), f"doc {d}: first difference at word {first_diff(got, want)}"
     # the same engine with the stream off replays to the same trees (deltas observe, never steer)
-    for waves in (4, 8):  # both config-2/3 kernel builds (mt_engine_set_variant)
+    for waves in (1, 4, 8):  # every config-2/3 kernel build (mt_engine_set_variant)
         eng2 = Engine(b.ndocs, waves=waves, **caps_for(w))
         eng2.start_collab(b.local_long_id)
         eng2.replay(b)

@@ -103,13 +103,13 @@ def test_stored_logs_replay_to_reference_dumps(name):
 
 def kernel_variants(name):
     """The replay kernel builds a fixture's profile has (include/mt_engine.h mt_engine_set_variant): every one runs
-    each fixture, whichever the engine would pick for the fixture's batch size. Config-2/3 profile: the 4-wave build
-    (no spills) and the 8-wave build the config-3 bench runs; tiled profile (c4_large): the narrow LDS-heap kernel
+    each fixture, whichever the engine would pick for the fixture's batch size. Config-2/3 profile: the LDS-image build
+    (waves=1, mt_small_lds.hip), the 4-wave build (no spills) and the 8-wave build the config-3 bench runs; tiled profile (c4_large): the narrow LDS-heap kernel
     and the wide one; the other profiles have one build."""
     _, w = load(name)
     c = caps_for(w)
     if c["ncap"] <= 192 and w.mode != gen.MTG_MATRIX:
-        return [dict(waves=4), dict(waves=8)]
+        return [dict(waves=1), dict(waves=4), dict(waves=8)]
     if c["ncap"] > 16384:
         return [dict(wide=False), dict(wide=True)]
     return [dict()]

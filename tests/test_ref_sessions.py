@@ -75,7 +75,7 @@ def test_oracle_and_host_core_match_reference(name):
 def _variants(name):
     _, w, _ = regenerate(name)
     c = caps_for(w)
-    return [dict(waves=4), dict(waves=8)] if c["ncap"] <= 192 and w.mode != gen.MTG_MATRIX else [dict()]
+    return [dict(waves=1), dict(waves=4), dict(waves=8)] if c["ncap"] <= 192 and w.mode != gen.MTG_MATRIX else [dict()]
 
 
 GPU_CASES = [(n, v) for n in NAMES for v in _variants(n)]

@@ -165,7 +165,7 @@ def _variants(name):
     from test_ref_goldens import kernel_variants  # noqa: F401  (the same builds as the TextSegment set of the name)
     _, w = load(name)
     c = caps_for(w)
-    return [dict(waves=4), dict(waves=8)] if c["ncap"] <= 192 else [dict()]
+    return [dict(waves=1), dict(waves=4), dict(waves=8)] if c["ncap"] <= 192 else [dict()]
 
 
 GPU_CASES = [(n, v) for n in NAMES for v in _variants(n)]

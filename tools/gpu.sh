@@ -11,6 +11,7 @@
 #   traffic:C        FETCH_SIZE pass + WRITE_SIZE pass              -> OUT/pmc_fetch_cC, OUT/pmc_write_cC
 #   inst:C           SQ instruction-count pass                      -> OUT/pmc_inst_cC
 #   wait:C           SQ wait / busy / LDS bank-conflict pass        -> OUT/pmc_wait_cC
+#   icache:C         instruction-cache pass (SQC_ICACHE_*, SQ_IFETCH) -> OUT/pmc_icache_cC
 #   phase:C          per-phase cycle clocks (profiling build)       -> OUT/phase_cC.txt
 #   py:SCRIPT        python -u SCRIPT (a helper under tools/)       -> OUT/py_<name>.txt
 #   ab:C:L1,L2,...   bench.py --config C per library build/Lk (MT_REPLAY_LIB), digests compared with L1
@@ -72,6 +73,11 @@ for S in "$@"; do
         SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT -d "$OUT/pmc_wait_c$A" -o run \
         --output-format csv -- python3 bench.py $(bargs "$A") --steps 1 --warmup 0 --no-cpu-baseline --no-e2e \
         > "$OUT/pmc_wait_c$A.json" 2> "$OUT/pmc_wait_c$A.err" || fail "$S" $? "$OUT/pmc_wait_c$A.err" ;;
+    icache)
+      timeout -s KILL $(prof_lim "$A") rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_IFETCH SQC_ICACHE_REQ \
+        SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE -d "$OUT/pmc_icache_c$A" -o run \
+        --output-format csv -- python3 bench.py $(bargs "$A") --steps 1 --warmup 0 --no-cpu-baseline --no-e2e \
+        > "$OUT/pmc_icache_c$A.json" 2> "$OUT/pmc_icache_c$A.err" || fail "$S" $? "$OUT/pmc_icache_c$A.err" ;;
     phase)
       v="PHASE_$A"
       timeout -k 10 $(prof_lim "$A") python -u tools/phase_profile.py --config "$A" ${!v} > "$OUT/phase_c$A.txt" 2>&1 \
