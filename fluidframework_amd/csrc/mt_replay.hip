@@ -513,8 +513,14 @@ int32_t mt_engine_submit_run(mt_engine* e, const mt_op_rec* ops, const int64_t* 
     int64_t text_hi = 0; /* the text staged so far: a prefix of the pool */
     int k = 0;
     rc = MT_OK;
-    for (int64_t d0 = 0; d0 < nd; d0 += step, k++) {
-        const int64_t d1 = std::min(nd, d0 + step);
+    /* the first chunks ramp up (a quarter, then half a chunk): the replay starts once a quarter of the first chunk is
+     * copied instead of all of it, and the later, full chunks overlap the copies as before */
+    static const int ramp_env = getenv("MT_SUBMIT_RAMP") ? atoi(getenv("MT_SUBMIT_RAMP")) : 1;
+    const bool ramp = ramp_env != 0 && !single && e->chunk <= 0;
+    int64_t len = step;
+    for (int64_t d0 = 0; d0 < nd; d0 += len, k++) {
+        len = ramp && k < 2 ? std::max<int64_t>(1, step >> (2 - k)) : step;
+        const int64_t d1 = std::min(nd, d0 + len);
         int64_t te = 0;
         if (!check_range(a, d0, d1, persp.data(), loads.data(), &te)) {
             rc = MT_E_ARG;
